@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""Headline benchmark: spans/sec into DependencyLinks (+ % of HBM roofline), BASELINE.json.
+
+One step = one pass of the zipkin-aggregate dependency path over one batch already resident in
+HBM: reset the exact accumulator, accumulate the batch (K1 span_join + spill), [N>1: RCCL SUM
+all-reduce of the accumulator across traceId-hash shards], finalize into device-resident
+(parent, child) -> Moments arrays (K5), including the status check the reference's fail-fast
+semantics need.
+
+Workload (BASELINE.json configs[1], "C2"): 1e8 span records per GPU, zipkin-tracegen shape
+(maxDepth 6, ~24 records / ~12 logical spans per trace, ~4.15e6 traces), 500 services, generated
+on device (synthetic). N > 1: every rank owns its own traceId-hash shard of the same size
+(weak scaling; at N = 8 that is 8e8 records, the scale of configs[2]).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.3 TB/s is the measured copy rate
+BYTES_PER_RECORD = 48
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--records", type=int, default=100_000_000, help="span records per GPU")
+    ap.add_argument("--services", type=int, default=500)
+    ap.add_argument("--max-depth", type=int, default=6)
+    ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--cpu-sample", type=int, default=20_000_000, help="records for the CPU baseline leg (0: skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local)
+
+    from zipkin_amd import DepsContext, DeviceColumns, tracegen_params
+
+    S = a.services
+    cells = S * S
+    stream = torch.cuda.current_stream(dev)
+    table = torch.zeros(cells * 16, dtype=torch.int64, device=dev)
+    ctx = DepsContext(S, device=local, stream=stream.cuda_stream, timing=True,
+                      table_ptr=table.data_ptr(), table_bytes=table.numel() * 8)
+    traces_cap = int(a.records / 15) + 1000
+    p = tracegen_params(a.seed, traces_cap, target_records=a.records, max_depth=a.max_depth, num_services=S,
+                        rank=rank, world=world)
+    cols = DeviceColumns(a.records, device=f"cuda:{local}")
+    n, ntr = ctx.tracegen_device(p, cols)
+    out = {
+        "m0": torch.empty(cells, dtype=torch.int64, device=dev),
+        "m1": torch.empty(cells, dtype=torch.float64, device=dev),
+        "m2": torch.empty(cells, dtype=torch.float64, device=dev),
+        "m3": torch.empty(cells, dtype=torch.float64, device=dev),
+        "m4": torch.empty(cells, dtype=torch.float64, device=dev),
+        "present": torch.empty(cells, dtype=torch.uint8, device=dev),
+    }
+
+    def step():
+        ctx.reset()
+        ctx.accumulate(cols)
+        if dist is not None:
+            dist.all_reduce(table)  # exact u64-limb SUM over xGMI (RCCL): shards are disjoint traces
+            ctx.note_merged(n * world)
+        ctx.finalize(out_device=out)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    tm0 = ctx.timing()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(a.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    tm1 = ctx.timing()
+    ev_ms = ev0.elapsed_time(ev1)
+    elapsed = wall
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_records = n * world
+    value = total_records * a.steps / elapsed
+    join_calls = tm1["join_calls"] - tm0["join_calls"]
+    join_avg_ms = (tm1["join_ms_total"] - tm0["join_ms_total"]) / max(1, join_calls)
+    achieved = n * BYTES_PER_RECORD / (join_avg_ms * 1e-3) / 1e9
+    st = ctx.stats()
+
+    cpu = None
+    if rank == 0 and world == 1 and a.cpu_sample > 0:
+        cpu = cpu_baseline(cols, min(a.cpu_sample, n), S, a.cpu_threads)
+
+    traffic = None
+    pmc = ROOT / "profiles" / "pmc_latest.json"
+    if pmc.exists():
+        try:
+            j = json.loads(pmc.read_text())
+            if j.get("records") == n:
+                traffic = j.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        line = {
+            "metric": "spans/sec into DependencyLinks (1/2/4/8 GPU) + % of HBM roofline",
+            "value": value,
+            "unit": "spans/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed * 1e3 / a.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (zipkin-tracegen-shaped, generated on device)",
+            "config": {
+                "workload": "C2: 1e8 span records/GPU, 500 services, dependency link table + Moments",
+                "records_per_gpu": n,
+                "traces_per_gpu": ntr,
+                "services": S,
+                "max_depth": a.max_depth,
+                "parallelism": f"traceId-hash shards x{world}" + (", RCCL all-reduce of the link table" if world > 1 else ""),
+                "step": "reset + span_join + spill + [all-reduce] + finalize(m0..m4) + status check",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_span_join_tile",
+                "achieved": achieved,
+                "peak": PEAK_HBM_GBS,
+                "unit": "GB/s",
+                "frac": achieved / PEAK_HBM_GBS,
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": n * BYTES_PER_RECORD,
+                "avg_launch_ms": join_avg_ms,
+            },
+            "cpu_baseline": cpu,
+            "detail": {
+                "event_ms_per_step": ev_ms / a.steps,
+                "finalize_ms_last": tm1["finalize_ms"],
+                "spill_ms_last": tm1["spill_ms"],
+                "links": int(st["joined_links"]) // max(1, a.steps + a.warmup),
+            },
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(cols, sample, S, threads):
+    """The oracle's multithreaded C restatement (kind "port") on the first `sample` records of the
+    same batch, on this box's host cores. A reported baseline only."""
+    from oracle import oracle
+
+    host = cols.to_host()
+    # cut at a trace boundary so the sample is trace-complete
+    tid = host.trace_id
+    cut = sample
+    while cut < len(tid) and cut > 0 and tid[cut] == tid[cut - 1]:
+        cut -= 1
+    part = host.take(slice(0, cut))
+    oracle.aggregate(part.take(slice(0, min(cut, 100_000))), S, threads=threads)  # warm the library
+    r = oracle.aggregate(part, S, threads=threads)
+    return {
+        "value": cut / r.seconds,
+        "unit": "spans/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"first {cut} records (whole traces) of the benchmark batch; oracle/zk_oracle.c, "
+        f"{threads} threads, {r.seconds:.2f} s",
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,60 @@
+"""The C-ABI library loads and exports every entry point include/zkagg.h declares (no GPU calls)."""
+import ctypes as C
+import re
+from pathlib import Path
+
+import pytest
+
+from tests.conftest import gpu_available
+from zipkin_amd import _abi
+
+HEADER = Path(__file__).resolve().parent.parent / "include" / "zkagg.h"
+
+
+def declared_functions():
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    return sorted(set(re.findall(r"\b(zk_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_what_the_binding_binds():
+    assert declared_functions() == sorted(_abi.SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    L = _abi.lib()
+    raw = C.CDLL(str(_abi.LIB_PATH))
+    for name in declared_functions():
+        assert hasattr(raw, name), name
+    assert L.zk_abi_version() == 1
+
+
+def test_status_strings():
+    for s in range(0, 11):
+        assert _abi.status_str(s) and _abi.status_str(s) != "unknown status"
+
+
+def test_ctx_create_rejects_bad_config_without_touching_a_device():
+    L = _abi.lib()
+    cfg = _abi.zk_config()
+    h = C.c_void_p()
+    cfg.num_services = 0
+    assert L.zk_ctx_create(C.byref(cfg), C.byref(h)) == _abi.ZK_ERR_INVALID_ARG
+    cfg.num_services = 70000
+    assert L.zk_ctx_create(C.byref(cfg), C.byref(h)) == _abi.ZK_ERR_INVALID_ARG
+    assert L.zk_ctx_create(None, C.byref(h)) == _abi.ZK_ERR_INVALID_ARG
+
+
+@pytest.mark.skipif(gpu_available(), reason="checks the no-device path")
+def test_no_device_fails_loudly_instead_of_falling_back():
+    from zipkin_amd import DepsContext, ZkError
+
+    with pytest.raises(ZkError) as e:
+        DepsContext(10)
+    assert e.value.status == _abi.ZK_ERR_NO_DEVICE
+
+
+def test_null_ctx_calls_are_errors():
+    L = _abi.lib()
+    assert L.zk_deps_reset(None) == _abi.ZK_ERR_INVALID_ARG
+    assert L.zk_ctx_destroy(None) == _abi.ZK_ERR_INVALID_ARG
+    assert L.zk_deps_accumulate(None, None, 0) == _abi.ZK_ERR_INVALID_ARG

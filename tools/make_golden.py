@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Regenerate tests/golden/*.json (run in the build container, where /root/reference exists).
+
+Fixtures are DATA only — inputs and expected outputs — never reference source text:
+
+* reference_kats.json   values and expectations transcribed from the reference's own unit tests
+                        (SpanTest.scala, DependenciesTest.scala, AnormAggregatesTest.scala,
+                        ThriftConversionsTest.scala)
+* aggregates_sql.json   the 150 stored DependencyLinks of zipkin-tracegen/src/testdata/aggregates.sql
+                        (a data file the reference ships for its tests), parsed to JSON
+* moment_accessors.json the outputs of the reference's own Moments accessor port
+                        (zipkin-web/.../component_data/momentAnnotations.js) executed by node on
+                        the aggregates.sql moments
+* moments_kats.json     exact and Algebird-fold Moments of small duration sets (oracle/moments.py)
+* job_kats.json         hand-built span sets through the span-level oracle (oracle/spans.py)
+
+Usage: python tools/make_golden.py
+"""
+from __future__ import annotations
+
+import json
+import re
+import subprocess
+import sys
+import tempfile
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+REF = Path("/root/reference")
+OUT = ROOT / "tests" / "golden"
+
+from oracle.moments import algebird_fold, exact_moments  # noqa: E402
+from oracle.spans import Annotation, Endpoint, Span, aggregate_job  # noqa: E402
+
+
+def reference_kats() -> dict:
+    # SpanTest.scala:30-44, 59-113 ; DependenciesTest.scala:28-81 ; AnormAggregatesTest.scala:30-58
+    # ThriftConversionsTest.scala:55-81
+    return {
+        "source": "transcribed from the reference unit tests (file:line per case)",
+        "span_merge": {
+            "ref": "zipkin-common/src/test/scala/com/twitter/zipkin/common/SpanTest.scala:59-68",
+            "span1": {"trace_id": 12345, "name": "", "id": 666, "parent_id": None, "debug": True,
+                      "annotations": [[1, "value1", [1, 2, "service"]]]},
+            "span2": {"trace_id": 12345, "name": "methodcall", "id": 666, "parent_id": None, "debug": False,
+                      "annotations": [[2, "value2", [3, 4, "service"]]]},
+            "expected": {"trace_id": 12345, "name": "methodcall", "id": 666, "parent_id": None, "debug": True,
+                         "annotations": [[1, "value1", [1, 2, "service"]], [2, "value2", [3, 4, "service"]]]},
+        },
+        "span_merge_unknown": {
+            "ref": "SpanTest.scala:70-76",
+            "names": ["Unknown", "get"],
+            "expected": "get",
+        },
+        "first_last_duration": {
+            "ref": "SpanTest.scala:34-36,78-93",
+            "annotations": [[1, "value1", [1, 2, "service"]], [2, "value2", [3, 4, "Service"]],
+                            [3, "value3", [5, 6, "service"]]],
+            "first": 0, "last": 2, "duration": 2, "service_names": ["service"],
+        },
+        "no_annotations_duration": {"ref": "SpanTest.scala:95-98", "duration": None},
+        "validate": {
+            "ref": "SpanTest.scala:100-113",
+            "valid": [[1, "cs"], [2, "sr"], [3, "ss"], [4, "cr"]],
+            "invalid": [[1, "cs"], [2, "sr"], [3, "ss"], [4, "cr"], [5, "cs"]],
+        },
+        "not_client_side": {"ref": "SpanTest.scala:86-89", "annotations": [[1, "sr"]], "client_side": False},
+        "services_case_sensitive": {
+            "ref": "DependenciesTest.scala:28-40",
+            "equal": [["foo", "foo"]], "different": [["foo", "bar"], ["foo", "Foo"], ["foo", "FOO"]],
+        },
+        "dependency_link_plus": {
+            "ref": "DependenciesTest.scala:42-54",
+            "links": [["tfe", "mobileweb", 2], ["tfe", "mobileweb", 4], ["Gizmoduck", "tflock", 4]],
+            "combine": [0, 1], "incompatible": [0, 2],
+        },
+        "dependencies_monoid": {
+            "ref": "DependenciesTest.scala:57-81",
+            "deps1": {"start_s": 0, "end_s": 3600, "links": [["tfe", "mobileweb", 2], ["Gizmoduck", "tflock", 4]]},
+            "deps2": {"start_s": 3600, "end_s": 7200, "links": [["tfe", "mobileweb", 4], ["mobileweb", "Gizmoduck", 4]]},
+            "expected_start_s": 0, "expected_end_s": 7200,
+            "expected_links": [["mobileweb", "Gizmoduck", [4]], ["tfe", "mobileweb", [2, 4]], ["Gizmoduck", "tflock", [4]]],
+        },
+        "anorm_window": {
+            "ref": "zipkin-anormdb/src/test/scala/com/twitter/zipkin/storage/anormdb/AnormAggregatesTest.scala:30-58",
+            "stored": {"start_us": 1_000_000, "end_us": 2_000_000,
+                       "links": [["parent1", "child1", 18], ["parent2", "child2", 42]]},
+            "queries": [
+                {"start_us": 1_000_000, "end_us": 2_000_000, "hit": True, "what": "inclusive, start to end"},
+                {"start_us": 0, "end_us": "now", "hit": True, "what": "all time"},
+                {"start_us": 0, "end_us": None, "hit": True, "what": "end defaults to now"},
+                {"start_us": 0, "end_us": 1_001_000, "hit": False, "what": "end inside the dependency"},
+                {"start_us": 1_001_000, "end_us": 1_999_000, "hit": False, "what": "start and end inside"},
+                {"start_us": 1_001_000, "end_us": 3_000_000, "hit": False, "what": "start inside"},
+            ],
+        },
+        "thrift_unknown_service": {
+            "ref": "zipkin-scrooge/src/test/scala/com/twitter/zipkin/adapter/ThriftConversionsTest.scala:55-63",
+            "input": [None, ""], "expected": "Unknown service name",
+        },
+    }
+
+
+def aggregates_sql() -> dict:
+    path = REF / "zipkin-tracegen/src/testdata/aggregates.sql"
+    deps, links = [], []
+    for line in path.read_text().splitlines():
+        m = re.match(r"INSERT INTO zipkin_dependencies \(dlid, start_ts, end_ts\) VALUES \((\d+), (\d+), (\d+)\);", line)
+        if m:
+            deps.append({"dlid": int(m[1]), "start_ts": int(m[2]), "end_ts": int(m[3])})
+            continue
+        m = re.match(
+            r"INSERT INTO zipkin_dependency_links \(dlid, parent, child, m0, m1, m2, m3, m4\) VALUES "
+            r"\((\d+), '([^']*)', '([^']*)', ([^,]+),([^,]+),([^,]+),([^,]+),([^)]+)\);",
+            line,
+        )
+        if m:
+            links.append({"dlid": int(m[1]), "parent": m[2], "child": m[3], "m0": int(m[4]),
+                          "m1": float(m[5]), "m2": float(m[6]), "m3": float(m[7]), "m4": float(m[8])})
+    return {"source": "zipkin-tracegen/src/testdata/aggregates.sql", "dependencies": deps, "links": links}
+
+
+def moment_accessors(sql: dict) -> dict:
+    """Execute the reference's momentAnnotations.js (AMD module) under node on the stored moments."""
+    js = REF / "zipkin-web/src/main/resources/app/js/component_data/momentAnnotations.js"
+    inputs = [{k: l[k] for k in ("m0", "m1", "m2", "m3", "m4")} for l in sql["links"]]
+    runner = (
+        "var f; global.define = function(deps, factory){ f = factory(); };\n"
+        f"require({json.dumps(str(js))});\n"
+        f"var xs = {json.dumps(inputs)};\n"
+        "console.log(JSON.stringify(xs.map(function(m){ return f(m); })));\n"
+    )
+    with tempfile.NamedTemporaryFile("w", suffix=".js", delete=False) as fh:
+        fh.write(runner)
+        name = fh.name
+    out = subprocess.run(["node", name], check=True, capture_output=True, text=True).stdout
+    res = json.loads(out)
+    return {"source": "node execution of zipkin-web/.../component_data/momentAnnotations.js",
+            "inputs": inputs, "outputs": res}
+
+
+def moments_kats() -> dict:
+    sets = [[2, 4], [1, 2, 3, 4, 10], [18], [1000, 1000, 1000], [0, 5000],
+            [3000, 1000, 2000, 7000, 9000, 1000], [7, 7, 7, 8], list(range(1, 101)),
+            [1, 10**6, 10**9], [123456789, 987654321, 555555555, 42]]
+    out = []
+    for vs in sets:
+        out.append({"values": vs, "exact": list(exact_moments(vs)), "algebird_fold": list(algebird_fold(float(v) for v in vs))})
+    return {"source": "oracle/moments.py (exact rational, and algebird-core 0.8.1 MomentsGroup.plus left fold)",
+            "cases": out}
+
+
+def _ep(svc):
+    return Endpoint(1, 2, svc)
+
+
+def _rpc(tid, sid, pid, caller_svc_unused, callee, cs, sr, ss, cr):
+    """client + server fragments of one RPC, both carrying the callee endpoint (TraceGen.scala:127-140)."""
+    e = _ep(callee)
+    client = Span(tid, "rpc", sid, pid, (Annotation(cs, "cs", e), Annotation(cr, "cr", e)))
+    server = Span(tid, "rpc", sid, pid, (Annotation(sr, "sr", e), Annotation(ss, "ss", e)))
+    return [client, server]
+
+
+def job_kats() -> dict:
+    cases = {}
+
+    def add(name, spans, note):
+        r = aggregate_job(spans, strict=False)
+        cases[name] = {
+            "note": note,
+            "spans": [
+                {"trace_id": s.trace_id, "name": s.name, "id": s.id, "parent_id": s.parent_id,
+                 "annotations": [[a.timestamp, a.value, None if a.host is None else a.host.service_name]
+                                 for a in s.annotations]}
+                for s in spans
+            ],
+            "links": [{"parent": k[0], "child": k[1], "durations": v, "exact": list(exact_moments(v))}
+                      for k, v in sorted(r.durations.items())],
+            "no_service": r.no_service,
+        }
+
+    root = Span(1, "root", 10, None, (Annotation(100, "sr", _ep("web")), Annotation(900, "ss", _ep("web"))))
+    add("client_server_fragments", [root] + _rpc(1, 11, 10, "web", "db", 200, 210, 400, 410),
+        "one RPC split into client and server fragments; duration = cr - cs")
+    add("missing_parent", [Span(2, "x", 21, 999, (Annotation(5, "sr", _ep("a")), Annotation(9, "ss", _ep("a"))))],
+        "child whose parent span is absent is dropped by the inner join")
+    bad_parent = Span(3, "p", 30, None, (Annotation(1, "sr", _ep("p")), Annotation(2, "sr", _ep("p")), Annotation(3, "ss", _ep("p"))))
+    add("invalid_parent_drops_children", [bad_parent] + _rpc(3, 31, 30, "p", "c", 10, 11, 20, 21),
+        "parent with two sr annotations is invalid, so its child has no join partner")
+    add("self_parent", [Span(4, "s", 40, 40, (Annotation(1, "sr", _ep("me")), Annotation(5, "ss", _ep("me"))))],
+        "parentId == id joins the span with itself: a self link")
+    add("client_side_service_only", [root.__class__(5, "r", 50, None, (Annotation(1, "sr", _ep("front")), Annotation(99, "ss", _ep("front")))),
+                                     Span(5, "c", 51, 50, (Annotation(10, "cs", _ep("back")), Annotation(30, "cr", _ep("back"))))],
+        "child span with only cs/cr annotations takes its service from the client side")
+    dup = _rpc(6, 61, 60, "r", "d", 10, 11, 20, 21)
+    add("duplicate_fragment_invalid", [Span(6, "r", 60, None, (Annotation(1, "sr", _ep("r")), Annotation(50, "ss", _ep("r"))))] + dup + [dup[1]],
+        "the same server fragment stored twice doubles sr/ss: the merged child is invalid")
+    add("empty_input", [], "no spans: no links, no Dependencies record")
+    add("no_service_host", [Span(7, "r", 70, None, (Annotation(1, "sr", _ep("r")), Annotation(9, "ss", _ep("r")))),
+                            Span(7, "c", 71, 70, (Annotation(2, "sr", None), Annotation(4, "ss", None)))],
+        "joined child without any core-annotation host: the reference throws None.get")
+    add("custom_annotations_extend_duration",
+        [Span(8, "r", 80, None, (Annotation(1, "sr", _ep("r")), Annotation(99, "ss", _ep("r")))),
+         Span(8, "c", 81, 80, (Annotation(10, "sr", _ep("c")), Annotation(5, "custom", _ep("c")), Annotation(40, "ss", _ep("c")), Annotation(55, "other", None)))],
+        "duration = max - min over ALL annotations, not just core ones")
+    add("case_sensitive_services",
+        [Span(9, "r", 90, None, (Annotation(1, "sr", _ep("Svc")), Annotation(99, "ss", _ep("Svc")))),
+         Span(9, "c", 91, 90, (Annotation(10, "sr", _ep("svc")), Annotation(20, "ss", _ep("svc"))))],
+        "Service equality is case-sensitive (DependenciesTest.scala:28-40)")
+    return {"source": "oracle/spans.py aggregate_job (ZipkinAggregateJob.scala:20-43)", "cases": cases}
+
+
+def main() -> None:
+    OUT.mkdir(parents=True, exist_ok=True)
+    sql = aggregates_sql()
+    files = {
+        "reference_kats.json": reference_kats(),
+        "aggregates_sql.json": sql,
+        "moment_accessors.json": moment_accessors(sql),
+        "moments_kats.json": moments_kats(),
+        "job_kats.json": job_kats(),
+    }
+    for name, obj in files.items():
+        (OUT / name).write_text(json.dumps(obj, indent=1, sort_keys=False) + "\n")
+        print("wrote", OUT / name)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,203 @@
+"""ctypes binding of the zkagg C ABI (include/zkagg.h).
+
+This is the same surface a JVM host binds through JNI/JNA; Python uses it for
+the tests and the bench. Loading never falls back to anything: a missing or unloadable
+libzkagg.so raises ZkLibraryError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("ZKAGG_LIB", _PKG / "libzkagg.so"))
+
+# status codes (zk_status)
+ZK_OK = 0
+ZK_ERR_INVALID_ARG = 1
+ZK_ERR_HIP = 2
+ZK_ERR_NO_SERVICE = 3
+ZK_ERR_DURATION_RANGE = 4
+ZK_ERR_TRACE_TOO_LARGE = 5
+ZK_ERR_CAPACITY = 6
+ZK_ERR_NOT_CLUSTERED = 7
+ZK_ERR_NO_DEVICE = 8
+ZK_ERR_SERVICE_RANGE = 9
+ZK_ERR_UNSUPPORTED = 10
+
+# record flags
+ZK_F_HAS_PARENT = 1 << 0
+ZK_F_HAS_ANNOTATIONS = 1 << 1
+ZK_F_SVC_CLIENT = 1 << 2
+ZK_F_SVC_SERVER = 1 << 3
+ZK_F_CS_SHIFT = 8
+ZK_F_CR_SHIFT = 10
+ZK_F_SR_SHIFT = 12
+ZK_F_SS_SHIFT = 14
+
+ZK_BATCH_DEVICE_PTRS = 1 << 0
+ZK_BATCH_TRACE_CLUSTERED = 1 << 1
+
+LIMBS_PER_CELL = 16
+
+
+class ZkLibraryError(RuntimeError):
+    pass
+
+
+class ZkError(RuntimeError):
+    def __init__(self, status: int, message: str):
+        super().__init__(f"zk status {status}: {message}")
+        self.status = status
+        self.message = message
+
+
+class zk_span_cols(C.Structure):
+    _fields_ = [
+        ("trace_id", C.c_void_p),
+        ("span_id", C.c_void_p),
+        ("parent_id", C.c_void_p),
+        ("first_ts", C.c_void_p),
+        ("last_ts", C.c_void_p),
+        ("service_id", C.c_void_p),
+        ("flags", C.c_void_p),
+        ("n", C.c_uint64),
+    ]
+
+
+class zk_config(C.Structure):
+    _fields_ = [
+        ("num_services", C.c_uint32),
+        ("device", C.c_int32),
+        ("stream", C.c_void_p),
+        ("strict", C.c_uint32),
+        ("max_trace_records", C.c_uint32),
+        ("timing", C.c_uint32),
+        ("table", C.c_void_p),
+        ("table_bytes", C.c_uint64),
+        ("reserved", C.c_uint32 * 8),
+    ]
+
+
+class zk_stats(C.Structure):
+    _fields_ = [
+        (name, C.c_uint64)
+        for name in (
+            "records",
+            "merged_spans",
+            "valid_spans",
+            "invalid_spans",
+            "child_spans",
+            "joined_links",
+            "missing_parent",
+            "no_service",
+            "ambiguous",
+            "spilled_traces",
+            "duration_range",
+            "service_range",
+            "trace_too_large",
+        )
+    ] + [("reserved", C.c_uint64 * 3)]
+
+    def as_dict(self) -> dict:
+        return {k: int(getattr(self, k)) for k, _ in self._fields_ if k != "reserved"}
+
+
+class zk_timing(C.Structure):
+    _fields_ = [
+        ("join_ms", C.c_double),
+        ("reduce_ms", C.c_double),
+        ("spill_ms", C.c_double),
+        ("finalize_ms", C.c_double),
+        ("join_calls", C.c_uint64),
+        ("join_ms_total", C.c_double),
+        ("reduce_ms_total", C.c_double),
+        ("reserved", C.c_double * 4),
+    ]
+
+
+class zk_link_table(C.Structure):
+    _fields_ = [
+        ("m0", C.c_void_p),
+        ("m1", C.c_void_p),
+        ("m2", C.c_void_p),
+        ("m3", C.c_void_p),
+        ("m4", C.c_void_p),
+        ("present", C.c_void_p),
+        ("device_ptrs", C.c_uint32),
+    ]
+
+
+class zk_tracegen_params(C.Structure):
+    _fields_ = [
+        ("seed", C.c_uint64),
+        ("num_traces", C.c_uint64),
+        ("target_records", C.c_uint64),
+        ("max_depth", C.c_uint32),
+        ("num_services", C.c_uint32),
+        ("base_ts", C.c_int64),
+        ("rank", C.c_uint32),
+        ("world", C.c_uint32),
+        ("reserved", C.c_uint32 * 4),
+    ]
+
+
+# every symbol include/zkagg.h declares: (name, restype, argtypes)
+_P = C.c_void_p
+_SIGNATURES = [
+    ("zk_abi_version", C.c_uint32, []),
+    ("zk_ctx_create", C.c_int, [C.POINTER(zk_config), C.POINTER(_P)]),
+    ("zk_ctx_destroy", C.c_int, [_P]),
+    ("zk_last_error", C.c_char_p, [_P]),
+    ("zk_status_str", C.c_char_p, [C.c_int]),
+    ("zk_ctx_sync", C.c_int, [_P]),
+    ("zk_ctx_stats", C.c_int, [_P, C.POINTER(zk_stats)]),
+    ("zk_ctx_timing", C.c_int, [_P, C.POINTER(zk_timing)]),
+    ("zk_deps_reset", C.c_int, [_P]),
+    ("zk_deps_accumulate", C.c_int, [_P, C.POINTER(zk_span_cols), C.c_uint32]),
+    ("zk_deps_finalize", C.c_int, [_P, C.POINTER(zk_link_table)]),
+    ("zk_deps_partial", C.c_int, [_P, C.POINTER(_P), C.POINTER(C.c_uint64)]),
+    ("zk_deps_note_merged", C.c_int, [_P, C.c_uint64]),
+    ("zk_trace_shard", C.c_uint32, [C.c_uint64, C.c_uint32]),
+    (
+        "zk_tracegen_host",
+        C.c_int,
+        [C.POINTER(zk_tracegen_params), C.POINTER(zk_span_cols), C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)],
+    ),
+    (
+        "zk_tracegen_device",
+        C.c_int,
+        [_P, C.POINTER(zk_tracegen_params), C.POINTER(zk_span_cols), C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)],
+    ),
+]
+
+SYMBOLS = [s[0] for s in _SIGNATURES]
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libzkagg.so (once). Raises ZkLibraryError if it is missing or lacks a symbol."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise ZkLibraryError(f"{LIB_PATH} not built: run __graft_entry__.build() (no fallback exists)")
+    try:
+        L = C.CDLL(str(LIB_PATH))
+    except OSError as e:  # pragma: no cover
+        raise ZkLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+    for name, res, args in _SIGNATURES:
+        try:
+            f = getattr(L, name)
+        except AttributeError as e:
+            raise ZkLibraryError(f"{LIB_PATH} does not export {name}") from e
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def status_str(s: int) -> str:
+    return lib().zk_status_str(s).decode()

@@ -1,0 +1,58 @@
+"""Build libzkagg.so in-tree with hipcc for gfx950 (no JIT cache, so the .so travels with the repo)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+SOURCES = ["zk_join.hip", "zk_finalize.hip", "zk_tracegen.hip", "zk_api.cpp"]
+HEADERS = ["zk_internal.h", "zk_tracegen.h"]
+LIB = PKG / "libzkagg.so"
+ARCH = os.environ.get("ZK_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (Path(c).exists() or c == "hipcc"):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def needs_build() -> bool:
+    if not LIB.exists():
+        return True
+    t = LIB.stat().st_mtime
+    deps = [CSRC / s for s in SOURCES + HEADERS] + [ROOT / "include" / "zkagg.h"]
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    if not force and not needs_build():
+        return LIB
+    cmd = [
+        _hipcc(),
+        f"--offload-arch={ARCH}",
+        "-O3",
+        "-fPIC",
+        "-shared",
+        "-std=c++17",
+        "-Wno-unused-result",
+        "-Wno-unused-value",
+        f"-I{ROOT / 'include'}",
+        *[str(CSRC / s) for s in SOURCES],
+        "-o",
+        str(LIB) + ".tmp",
+    ]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(str(LIB) + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

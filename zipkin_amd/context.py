@@ -1,0 +1,169 @@
+"""DepsContext: one device-resident zipkin-aggregate accumulator (a zk_ctx).
+
+Mirrors the compute half of ZipkinAggregateJob.scala:20-43: `accumulate` takes trace-clustered
+span fragment batches, `finalize` produces the dense (parent, child) -> Moments table that the
+job would turn into one Dependencies record.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _abi
+from .columns import DeviceColumns, SpanColumns
+
+
+@dataclass
+class LinkTable:
+    """Dense S x S table: cell p*S + c is DependencyLink(parent=p, child=c)."""
+
+    num_services: int
+    m0: np.ndarray
+    m1: np.ndarray
+    m2: np.ndarray
+    m3: np.ndarray
+    m4: np.ndarray
+    present: np.ndarray
+
+    def links(self):
+        """Yield (parent_id, child_id, (m0, m1, m2, m3, m4)) for every present cell."""
+        S = self.num_services
+        for c in np.flatnonzero(self.present):
+            yield int(c // S), int(c % S), (
+                int(self.m0[c]),
+                float(self.m1[c]),
+                float(self.m2[c]),
+                float(self.m3[c]),
+                float(self.m4[c]),
+            )
+
+    def as_dict(self) -> dict:
+        return {(p, c): m for p, c, m in self.links()}
+
+
+class DepsContext:
+    def __init__(
+        self,
+        num_services: int,
+        *,
+        device: int = 0,
+        stream: int | None = None,
+        strict: bool = True,
+        max_trace_records: int = 0,
+        timing: bool = False,
+        table_ptr: int = 0,
+        table_bytes: int = 0,
+    ):
+        self._L = _abi.lib()
+        cfg = _abi.zk_config()
+        cfg.num_services = num_services
+        cfg.device = device
+        cfg.stream = stream
+        cfg.strict = 1 if strict else 0
+        cfg.max_trace_records = max_trace_records
+        cfg.timing = 1 if timing else 0
+        cfg.table = table_ptr or None
+        cfg.table_bytes = table_bytes
+        h = C.c_void_p()
+        st = self._L.zk_ctx_create(C.byref(cfg), C.byref(h))
+        if st != _abi.ZK_OK:
+            raise _abi.ZkError(st, _abi.status_str(st))
+        self._h = h
+        self.num_services = num_services
+
+    # -- plumbing ---------------------------------------------------------------------------
+    def _check(self, st: int) -> None:
+        if st != _abi.ZK_OK:
+            raise _abi.ZkError(st, self._L.zk_last_error(self._h).decode() or _abi.status_str(st))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.zk_ctx_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    # -- dependency path --------------------------------------------------------------------
+    def reset(self) -> None:
+        self._check(self._L.zk_deps_reset(self._h))
+
+    def accumulate(self, cols, *, clustered: bool = True, n: int | None = None) -> None:
+        flags = _abi.ZK_BATCH_TRACE_CLUSTERED if clustered else 0
+        if isinstance(cols, DeviceColumns):
+            ab = cols.abi(n)
+            flags |= _abi.ZK_BATCH_DEVICE_PTRS
+        elif isinstance(cols, SpanColumns):
+            ab = cols.abi()
+        else:
+            ab = cols  # a prepared zk_span_cols + caller sets flags through `clustered`
+        self._check(self._L.zk_deps_accumulate(self._h, C.byref(ab), flags))
+
+    def finalize(self, out_device=None) -> LinkTable | None:
+        """Finalize into host numpy arrays (default) or into caller device buffers.
+
+        out_device: optional dict of torch tensors m0 (int64), m1..m4 (float64), present (uint8).
+        """
+        S = self.num_services
+        cells = S * S
+        t = _abi.zk_link_table()
+        if out_device is not None:
+            for k in ("m0", "m1", "m2", "m3", "m4", "present"):
+                setattr(t, k, out_device[k].data_ptr())
+            t.device_ptrs = 1
+            self._check(self._L.zk_deps_finalize(self._h, C.byref(t)))
+            return None
+        m0 = np.zeros(cells, np.uint64)
+        ms = [np.zeros(cells, np.float64) for _ in range(4)]
+        pr = np.zeros(cells, np.uint8)
+        t.m0 = m0.ctypes.data
+        t.m1, t.m2, t.m3, t.m4 = (a.ctypes.data for a in ms)
+        t.present = pr.ctypes.data
+        t.device_ptrs = 0
+        self._check(self._L.zk_deps_finalize(self._h, C.byref(t)))
+        return LinkTable(S, m0, *ms, pr)
+
+    def stats(self) -> dict:
+        s = _abi.zk_stats()
+        self._check(self._L.zk_ctx_stats(self._h, C.byref(s)))
+        return s.as_dict()
+
+    def timing(self) -> dict:
+        t = _abi.zk_timing()
+        self._check(self._L.zk_ctx_timing(self._h, C.byref(t)))
+        return {k: getattr(t, k) for k, _ in t._fields_ if k != "reserved"}
+
+    def sync(self) -> None:
+        self._check(self._L.zk_ctx_sync(self._h))
+
+    def partial(self) -> tuple[int, int]:
+        p, b = C.c_void_p(), C.c_uint64()
+        self._check(self._L.zk_deps_partial(self._h, C.byref(p), C.byref(b)))
+        return int(p.value or 0), int(b.value)
+
+    def note_merged(self, total_records: int) -> None:
+        self._check(self._L.zk_deps_note_merged(self._h, total_records))
+
+    def tracegen_device(self, params: _abi.zk_tracegen_params, out: DeviceColumns) -> tuple[int, int]:
+        nrec, ntr = C.c_uint64(), C.c_uint64()
+        ab = out.abi(out.capacity)
+        self._check(
+            self._L.zk_tracegen_device(self._h, C.byref(params), C.byref(ab), out.capacity, C.byref(nrec), C.byref(ntr))
+        )
+        out.n = int(nrec.value)
+        return int(nrec.value), int(ntr.value)

@@ -1,0 +1,401 @@
+// zk_api.cpp — the C ABI of libzkagg (include/zkagg.h): context, memory, launches, status.
+//
+// Host-side counterpart of the reference's Scalding driver (ZipkinAggregateJob.scala:10-46):
+// instead of four Hadoop shuffles it owns one device-resident exact accumulator per context and
+// orders every kernel on one HIP stream. There is deliberately no host compute path.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "zk_internal.h"
+
+using namespace zk;
+
+struct EventPair {
+    hipEvent_t a = nullptr, b = nullptr;
+};
+
+struct zk_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    uint32_t S = 0;
+    bool strict = true;
+    uint32_t max_trace = 131072;
+    bool timing = false;
+    uint64_t* table = nullptr;            // S*S*kLimbs
+    bool own_table = true;
+    unsigned long long* stats = nullptr;  // kStatShards*ST_N
+    unsigned int* spill_count = nullptr;
+    uint64_t* spill_list = nullptr;
+    uint64_t spill_cap = 0;
+    uint8_t* spill_scratch = nullptr;
+    uint64_t spill_stride = 0;
+    uint32_t spill_wgs = 16;
+    // host-pointer input staging
+    void* stage = nullptr;
+    uint64_t stage_cap = 0;
+    // finalize staging for host outputs
+    void* fin_stage = nullptr;
+    uint64_t records_since_reset = 0;
+    std::string err;
+    // timing
+    std::vector<EventPair> ev_free, ev_join, ev_spill, ev_fin;
+    zk_timing tm{};
+};
+
+namespace {
+
+zk_status fail(zk_ctx* c, zk_status s, const std::string& msg) {
+    if (c) c->err = msg;
+    return s;
+}
+
+zk_status hip_fail(zk_ctx* c, hipError_t e, const char* where) {
+    return fail(c, ZK_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+#define ZK_HIP(ctx, call)                                   \
+    do {                                                    \
+        hipError_t _e = (call);                             \
+        if (_e != hipSuccess) return hip_fail(ctx, _e, #call); \
+    } while (0)
+
+EventPair take_pair(zk_ctx* c) {
+    EventPair p;
+    if (!c->ev_free.empty()) {
+        p = c->ev_free.back();
+        c->ev_free.pop_back();
+    } else {
+        hipEventCreate(&p.a);
+        hipEventCreate(&p.b);
+    }
+    return p;
+}
+
+uint64_t tiles_for(uint64_t n) { return (n + 1023) / 1024; }
+
+zk_status ensure_spill(zk_ctx* c, uint64_t n) {
+    const uint64_t need = tiles_for(n) + 1;
+    if (need > c->spill_cap) {
+        if (c->spill_list) ZK_HIP(c, hipFree(c->spill_list));
+        uint64_t cap = need < (1ull << 16) ? (1ull << 16) : need;
+        ZK_HIP(c, hipMalloc(&c->spill_list, cap * sizeof(uint64_t)));
+        c->spill_cap = cap;
+    }
+    if (!c->spill_scratch) {
+        c->spill_stride = spill_scratch_bytes_per_wg(c->max_trace);
+        ZK_HIP(c, hipMalloc(&c->spill_scratch, c->spill_stride * c->spill_wgs));
+    }
+    return ZK_OK;
+}
+
+zk_status stats_sum(zk_ctx* c, uint64_t out[ST_N]) {
+    std::vector<unsigned long long> h((size_t)kStatShards * ST_N);
+    ZK_HIP(c, hipMemcpyAsync(h.data(), c->stats, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    ZK_HIP(c, hipStreamSynchronize(c->stream));
+    for (int s = 0; s < ST_N; ++s) out[s] = 0;
+    for (int sh = 0; sh < kStatShards; ++sh)
+        for (int s = 0; s < ST_N; ++s) out[s] += h[(size_t)sh * ST_N + s];
+    return ZK_OK;
+}
+
+bool cols_ok(const zk_span_cols* c) {
+    return c && c->trace_id && c->span_id && c->parent_id && c->first_ts && c->last_ts && c->service_id && c->flags;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t zk_abi_version(void) { return ZK_ABI_VERSION; }
+
+const char* zk_status_str(zk_status s) {
+    switch (s) {
+        case ZK_OK: return "ok";
+        case ZK_ERR_INVALID_ARG: return "invalid argument";
+        case ZK_ERR_HIP: return "HIP runtime error";
+        case ZK_ERR_NO_SERVICE: return "joined span without service name (reference: None.get)";
+        case ZK_ERR_DURATION_RANGE: return "span duration >= 2^40 us";
+        case ZK_ERR_TRACE_TOO_LARGE: return "trace longer than max_trace_records";
+        case ZK_ERR_CAPACITY: return "exact accumulator headroom exhausted";
+        case ZK_ERR_NOT_CLUSTERED: return "batch is not trace-clustered";
+        case ZK_ERR_NO_DEVICE: return "no gfx950 HIP device";
+        case ZK_ERR_SERVICE_RANGE: return "service_id >= num_services";
+        case ZK_ERR_UNSUPPORTED: return "unsupported";
+    }
+    return "unknown status";
+}
+
+const char* zk_last_error(const zk_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+zk_status zk_ctx_create(const zk_config* cfg, zk_ctx** out) {
+    if (!cfg || !out) return ZK_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (cfg->num_services == 0 || cfg->num_services > 65535) return ZK_ERR_INVALID_ARG;
+    if (cfg->max_trace_records > (1u << 20)) return ZK_ERR_INVALID_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return ZK_ERR_NO_DEVICE;
+    if (cfg->device < 0 || cfg->device >= ndev) return ZK_ERR_NO_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, cfg->device) != hipSuccess) return ZK_ERR_NO_DEVICE;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return ZK_ERR_NO_DEVICE;
+    zk_ctx* c = new zk_ctx();
+    c->device = cfg->device;
+    c->S = cfg->num_services;
+    c->strict = cfg->strict != 0;
+    c->timing = cfg->timing != 0;
+    if (cfg->max_trace_records) c->max_trace = cfg->max_trace_records;
+    zk_status st = ZK_OK;
+    hipError_t e = hipSetDevice(c->device);
+    if (e == hipSuccess) {
+        if (cfg->stream) {
+            c->stream = (hipStream_t)cfg->stream;
+        } else {
+            e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+            c->own_stream = true;
+        }
+    }
+    const uint64_t cells = (uint64_t)c->S * c->S;
+    if (cfg->table) {
+        if (cfg->table_bytes < cells * kLimbs * 8) {
+            delete c;
+            return ZK_ERR_INVALID_ARG;
+        }
+        c->table = (uint64_t*)cfg->table;
+        c->own_table = false;
+    } else if (e == hipSuccess) {
+        e = hipMalloc(&c->table, cells * kLimbs * 8);
+    }
+    if (e == hipSuccess) e = hipMalloc(&c->stats, (size_t)kStatShards * ST_N * 8);
+    if (e == hipSuccess) e = hipMalloc(&c->spill_count, 256);
+    if (e != hipSuccess) st = ZK_ERR_HIP;
+    if (st == ZK_OK) st = zk_deps_reset(c);
+    if (st == ZK_OK) st = ensure_spill(c, 1);
+    if (st != ZK_OK) {
+        zk_ctx_destroy(c);
+        return st;
+    }
+    *out = c;
+    return ZK_OK;
+}
+
+zk_status zk_ctx_destroy(zk_ctx* c) {
+    if (!c) return ZK_ERR_INVALID_ARG;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->own_table) hipFree(c->table);
+    hipFree(c->stats);
+    hipFree(c->spill_count);
+    hipFree(c->spill_list);
+    hipFree(c->spill_scratch);
+    hipFree(c->stage);
+    hipFree(c->fin_stage);
+    for (auto* v : {&c->ev_free, &c->ev_join, &c->ev_spill, &c->ev_fin})
+        for (auto& p : *v) {
+            hipEventDestroy(p.a);
+            hipEventDestroy(p.b);
+        }
+    if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+    delete c;
+    return ZK_OK;
+}
+
+zk_status zk_ctx_sync(zk_ctx* c) {
+    if (!c) return ZK_ERR_INVALID_ARG;
+    ZK_HIP(c, hipSetDevice(c->device));
+    ZK_HIP(c, hipStreamSynchronize(c->stream));
+    return ZK_OK;
+}
+
+zk_status zk_deps_reset(zk_ctx* c) {
+    if (!c) return ZK_ERR_INVALID_ARG;
+    ZK_HIP(c, hipSetDevice(c->device));
+    ZK_HIP(c, hipMemsetAsync(c->table, 0, (size_t)c->S * c->S * kLimbs * 8, c->stream));
+    ZK_HIP(c, hipMemsetAsync(c->stats, 0, (size_t)kStatShards * ST_N * 8, c->stream));
+    c->records_since_reset = 0;
+    return ZK_OK;
+}
+
+zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags) {
+    if (!c) return ZK_ERR_INVALID_ARG;
+    if (!cols) return fail(c, ZK_ERR_INVALID_ARG, "null columns");
+    if (!(flags & ZK_BATCH_TRACE_CLUSTERED))
+        return fail(c, ZK_ERR_NOT_CLUSTERED, "accumulate requires ZK_BATCH_TRACE_CLUSTERED batches");
+    const uint64_t n = cols->n;
+    if (n == 0) return ZK_OK;
+    if (!cols_ok(cols)) return fail(c, ZK_ERR_INVALID_ARG, "null column pointer");
+    if (c->records_since_reset + n > kMaxRecordsSinceReset)
+        return fail(c, ZK_ERR_CAPACITY, "more than 2^32-1 records since reset");
+    ZK_HIP(c, hipSetDevice(c->device));
+    SpanColsDev d{cols->trace_id, cols->span_id, cols->parent_id, cols->first_ts,
+                  cols->last_ts,  cols->service_id, cols->flags,   n};
+    if (!(flags & ZK_BATCH_DEVICE_PTRS)) {
+        // PCIe path: stage the host columns in HBM (reported separately, never the bench value)
+        if (n > c->stage_cap) {
+            if (c->stage) ZK_HIP(c, hipFree(c->stage));
+            ZK_HIP(c, hipMalloc(&c->stage, n * 48));
+            c->stage_cap = n;
+        }
+        uint8_t* p = (uint8_t*)c->stage;
+        uint64_t* tid = (uint64_t*)p;
+        uint64_t* sid = tid + n;
+        uint64_t* pid = sid + n;
+        int64_t* fts = (int64_t*)(pid + n);
+        int64_t* lts = fts + n;
+        uint32_t* svc = (uint32_t*)(lts + n);
+        uint32_t* flg = svc + n;
+        ZK_HIP(c, hipMemcpyAsync(tid, cols->trace_id, n * 8, hipMemcpyHostToDevice, c->stream));
+        ZK_HIP(c, hipMemcpyAsync(sid, cols->span_id, n * 8, hipMemcpyHostToDevice, c->stream));
+        ZK_HIP(c, hipMemcpyAsync(pid, cols->parent_id, n * 8, hipMemcpyHostToDevice, c->stream));
+        ZK_HIP(c, hipMemcpyAsync(fts, cols->first_ts, n * 8, hipMemcpyHostToDevice, c->stream));
+        ZK_HIP(c, hipMemcpyAsync(lts, cols->last_ts, n * 8, hipMemcpyHostToDevice, c->stream));
+        ZK_HIP(c, hipMemcpyAsync(svc, cols->service_id, n * 4, hipMemcpyHostToDevice, c->stream));
+        ZK_HIP(c, hipMemcpyAsync(flg, cols->flags, n * 4, hipMemcpyHostToDevice, c->stream));
+        d = SpanColsDev{tid, sid, pid, fts, lts, svc, flg, n};
+    }
+    zk_status st = ensure_spill(c, n);
+    if (st != ZK_OK) return st;
+    ZK_HIP(c, hipMemsetAsync(c->spill_count, 0, 4, c->stream));
+    JoinArgs a{};
+    a.c = d;
+    a.table = c->table;
+    a.stats = c->stats;
+    a.S = c->S;
+    a.spill_count = c->spill_count;
+    a.spill_list = c->spill_list;
+    a.spill_cap = c->spill_cap;
+    a.spill_scratch = c->spill_scratch;
+    a.spill_scratch_stride = c->spill_stride;
+    a.max_trace = c->max_trace;
+    EventPair ej, es;
+    if (c->timing) {
+        ej = take_pair(c);
+        ZK_HIP(c, hipEventRecord(ej.a, c->stream));
+    }
+    ZK_HIP(c, launch_join(a, c->stream));
+    if (c->timing) {
+        ZK_HIP(c, hipEventRecord(ej.b, c->stream));
+        c->ev_join.push_back(ej);
+        es = take_pair(c);
+        ZK_HIP(c, hipEventRecord(es.a, c->stream));
+    }
+    ZK_HIP(c, launch_spill(a, c->spill_wgs, c->stream));
+    if (c->timing) {
+        ZK_HIP(c, hipEventRecord(es.b, c->stream));
+        c->ev_spill.push_back(es);
+    }
+    c->records_since_reset += n;
+    return ZK_OK;
+}
+
+zk_status zk_deps_finalize(zk_ctx* c, const zk_link_table* out) {
+    if (!c) return ZK_ERR_INVALID_ARG;
+    if (!out || !out->m0 || !out->m1 || !out->m2 || !out->m3 || !out->m4 || !out->present)
+        return fail(c, ZK_ERR_INVALID_ARG, "null output array");
+    ZK_HIP(c, hipSetDevice(c->device));
+    const uint64_t cells = (uint64_t)c->S * c->S;
+    zk_link_table dev = *out;
+    if (!out->device_ptrs) {
+        if (!c->fin_stage) ZK_HIP(c, hipMalloc(&c->fin_stage, cells * 41 + 64));
+        uint8_t* p = (uint8_t*)c->fin_stage;
+        dev.m0 = (uint64_t*)p;
+        dev.m1 = (double*)(p + cells * 8);
+        dev.m2 = (double*)(p + cells * 16);
+        dev.m3 = (double*)(p + cells * 24);
+        dev.m4 = (double*)(p + cells * 32);
+        dev.present = p + cells * 40;
+    }
+    EventPair ef;
+    if (c->timing) {
+        ef = take_pair(c);
+        ZK_HIP(c, hipEventRecord(ef.a, c->stream));
+    }
+    ZK_HIP(c, launch_finalize(c->table, c->S, &dev, c->stream));
+    if (c->timing) {
+        ZK_HIP(c, hipEventRecord(ef.b, c->stream));
+        c->ev_fin.push_back(ef);
+    }
+    if (!out->device_ptrs) {
+        ZK_HIP(c, hipMemcpyAsync(out->m0, dev.m0, cells * 8, hipMemcpyDeviceToHost, c->stream));
+        ZK_HIP(c, hipMemcpyAsync(out->m1, dev.m1, cells * 8, hipMemcpyDeviceToHost, c->stream));
+        ZK_HIP(c, hipMemcpyAsync(out->m2, dev.m2, cells * 8, hipMemcpyDeviceToHost, c->stream));
+        ZK_HIP(c, hipMemcpyAsync(out->m3, dev.m3, cells * 8, hipMemcpyDeviceToHost, c->stream));
+        ZK_HIP(c, hipMemcpyAsync(out->m4, dev.m4, cells * 8, hipMemcpyDeviceToHost, c->stream));
+        ZK_HIP(c, hipMemcpyAsync(out->present, dev.present, cells, hipMemcpyDeviceToHost, c->stream));
+    }
+    uint64_t s[ST_N];
+    zk_status st = stats_sum(c, s);
+    if (st != ZK_OK) return st;
+    if (s[ST_TOO_LARGE]) return fail(c, ZK_ERR_TRACE_TOO_LARGE, "trace longer than max_trace_records skipped");
+    if (s[ST_SVC_RANGE]) return fail(c, ZK_ERR_SERVICE_RANGE, "record with service_id >= num_services");
+    if (s[ST_DUR_RANGE]) return fail(c, ZK_ERR_DURATION_RANGE, "link with duration >= 2^40 us dropped");
+    if (c->strict && s[ST_NO_SERVICE])
+        return fail(c, ZK_ERR_NO_SERVICE, "joined span without a service name (reference: None.get)");
+    return ZK_OK;
+}
+
+zk_status zk_ctx_stats(zk_ctx* c, zk_stats* out) {
+    if (!c || !out) return ZK_ERR_INVALID_ARG;
+    ZK_HIP(c, hipSetDevice(c->device));
+    uint64_t s[ST_N];
+    zk_status st = stats_sum(c, s);
+    if (st != ZK_OK) return st;
+    memset(out, 0, sizeof(*out));
+    uint64_t* o = &out->records;
+    for (int i = 0; i < ST_TOO_LARGE + 1; ++i) o[i] = s[i];
+    return ZK_OK;
+}
+
+zk_status zk_ctx_timing(zk_ctx* c, zk_timing* out) {
+    if (!c || !out) return ZK_ERR_INVALID_ARG;
+    ZK_HIP(c, hipSetDevice(c->device));
+    ZK_HIP(c, hipStreamSynchronize(c->stream));
+    auto drain = [&](std::vector<EventPair>& v, double* last, double* total, uint64_t* calls) {
+        for (auto& p : v) {
+            float ms = 0;
+            hipEventElapsedTime(&ms, p.a, p.b);
+            *last = ms;
+            if (total) *total += ms;
+            if (calls) ++*calls;
+            c->ev_free.push_back(p);
+        }
+        v.clear();
+    };
+    drain(c->ev_join, &c->tm.join_ms, &c->tm.join_ms_total, &c->tm.join_calls);
+    drain(c->ev_spill, &c->tm.spill_ms, nullptr, nullptr);
+    drain(c->ev_fin, &c->tm.finalize_ms, nullptr, nullptr);
+    *out = c->tm;
+    return ZK_OK;
+}
+
+zk_status zk_deps_partial(zk_ctx* c, void** dev_ptr, uint64_t* bytes) {
+    if (!c || !dev_ptr || !bytes) return ZK_ERR_INVALID_ARG;
+    *dev_ptr = c->table;
+    *bytes = (uint64_t)c->S * c->S * kLimbs * 8;
+    return ZK_OK;
+}
+
+zk_status zk_deps_note_merged(zk_ctx* c, uint64_t total_records) {
+    if (!c) return ZK_ERR_INVALID_ARG;
+    if (total_records > kMaxRecordsSinceReset)
+        return fail(c, ZK_ERR_CAPACITY, "merged table exceeds 2^32-1 records");
+    c->records_since_reset = total_records;
+    return ZK_OK;
+}
+
+zk_status zk_tracegen_device(zk_ctx* c, const zk_tracegen_params* p, const zk_span_cols* out, uint64_t cap,
+                             uint64_t* n_records, uint64_t* n_traces) {
+    if (!c) return ZK_ERR_INVALID_ARG;
+    if (!p || !cols_ok(out) || !n_records || !n_traces || p->max_depth == 0 || p->max_depth > 16 ||
+        p->num_services == 0 || (p->world && p->rank >= p->world))
+        return fail(c, ZK_ERR_INVALID_ARG, "bad tracegen arguments");
+    ZK_HIP(c, hipSetDevice(c->device));
+    ZK_HIP(c, launch_tracegen(p, out, cap, n_records, n_traces, c->stream));
+    return ZK_OK;
+}
+
+}  // extern "C"

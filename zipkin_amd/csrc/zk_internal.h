@@ -1,0 +1,87 @@
+// zk_internal.h — shared definitions of the zkagg HIP library (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/zkagg.h"
+
+namespace zk {
+
+// ---- exact accumulator layout ----------------------------------------------------------------
+// One S x S cell = 16 u64 limbs (128 B). Each limb is a sum of 32-bit chunks, so it absorbs
+// 2^32 additions without carrying; the cross-chunk carries are resolved only in finalize.
+// With d < 2^40 us:  d: 2 chunks, d^2 (<2^80): 3, d^3 (<2^120): 4, d^4 (<2^160): 5.
+constexpr int kLimbs = 16;
+constexpr int kLimbM0 = 0;
+constexpr int kLimbS1 = 1;   // 2 limbs
+constexpr int kLimbS2 = 3;   // 3 limbs
+constexpr int kLimbS3 = 6;   // 4 limbs
+constexpr int kLimbS4 = 10;  // 5 limbs
+constexpr uint64_t kMaxDuration = 1ull << 40;
+constexpr uint64_t kMaxRecordsSinceReset = 0xFFFFFFFFull;
+
+// service key: (kind << 30) | id, kind 0 = server side, 1 = client side, 2 = none.
+// atomicMin over fragments picks Span.serviceName's preference (server before client,
+// Span.scala:125-131); the lowest id breaks ties between disagreeing fragments (ambiguous).
+constexpr uint32_t kSvcKindShift = 30;
+constexpr uint32_t kSvcIdMask = (1u << 30) - 1;
+constexpr uint32_t kSvcNone = 0xFFFFFFFFu;
+
+// device stats slots (mirror zk_stats field order)
+enum Stat : int {
+    ST_RECORDS = 0,
+    ST_MERGED,
+    ST_VALID,
+    ST_INVALID,
+    ST_CHILD,
+    ST_JOINED,
+    ST_MISSING_PARENT,
+    ST_NO_SERVICE,
+    ST_AMBIGUOUS,
+    ST_SPILLED,
+    ST_DUR_RANGE,
+    ST_SVC_RANGE,
+    ST_TOO_LARGE,
+    ST_N = 16
+};
+constexpr int kStatShards = 256;  // stats buffer = kStatShards x ST_N u64
+
+struct SpanColsDev {
+    const uint64_t* trace_id;
+    const uint64_t* span_id;
+    const uint64_t* parent_id;
+    const int64_t* first_ts;
+    const int64_t* last_ts;
+    const uint32_t* service_id;
+    const uint32_t* flags;
+    uint64_t n;
+};
+
+// Everything the join kernels need for one accumulate call.
+struct JoinArgs {
+    SpanColsDev c;
+    uint64_t* table;          // S*S*kLimbs
+    unsigned long long* stats;  // kStatShards x ST_N
+    uint32_t S;
+    // spill (giant traces)
+    unsigned int* spill_count;
+    uint64_t* spill_list;
+    uint64_t spill_cap;
+    // per-spill-WG global scratch
+    uint8_t* spill_scratch;
+    uint64_t spill_scratch_stride;  // bytes per WG
+    uint32_t max_trace;             // records
+};
+
+// host-side launchers (implemented in the .hip files)
+hipError_t launch_join(const JoinArgs& a, hipStream_t s);
+hipError_t launch_spill(const JoinArgs& a, uint32_t spill_wgs, hipStream_t s);
+uint64_t spill_scratch_bytes_per_wg(uint32_t max_trace);
+hipError_t launch_finalize(const uint64_t* table, uint32_t S, const zk_link_table* out,
+                           hipStream_t s);
+hipError_t launch_tracegen(const zk_tracegen_params* p, const zk_span_cols* out, uint64_t cap,
+                           uint64_t* n_records, uint64_t* n_traces, hipStream_t s);
+
+}  // namespace zk
