@@ -13,16 +13,16 @@ STEPS="${STEPS:-tests smoke bench prof}"
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1
+      timeout -k 10 500 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1
       ok_or_stop $? tests; tail -5 gpurun_out/gpu_tests.log ;;
     smoke)
-      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+      timeout -k 10 150 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
       ok_or_stop $? smoke; tail -3 gpurun_out/smoke.log ;;
     bench)
-      timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
+      timeout -k 10 250 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
       ok_or_stop $? bench; tail -2 gpurun_out/bench.log ;;
     prof)
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --cpu-sample 0 ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
+      timeout -k 10 250 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --cpu-sample 0 ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
       ok_or_stop $? prof; find gpurun_out/prof -name '*stats*' | head ;;
   esac
 done
