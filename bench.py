@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--cpu-sample", type=int, default=20_000_000, help="records for the CPU baseline leg (0: skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--ablate", type=int, default=0, help="diagnostic: 1 = K1 without link emission (not a valid result)")
     return ap.parse_args()
 
 
@@ -69,7 +70,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     table = torch.zeros(cells * 16, dtype=torch.int64, device=dev)
     ctx = DepsContext(S, device=local, stream=stream.cuda_stream, timing=True,
-                      table_ptr=table.data_ptr(), table_bytes=table.numel() * 8)
+                      table_ptr=table.data_ptr(), table_bytes=table.numel() * 8, ablate=a.ablate)
     traces_cap = int(a.records / 15) + 1000
     p = tracegen_params(a.seed, traces_cap, target_records=a.records, max_depth=a.max_depth, num_services=S,
                         rank=rank, world=world)

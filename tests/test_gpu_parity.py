@@ -36,6 +36,8 @@ def assert_parity(got, st, ref):
         assert bad.size == 0, f"{name} differs in {bad.size} cells, first {bad[:3]}: {a[bad[:3]]} vs {b[bad[:3]]}"
     assert np.array_equal(got.present, (m0 > 0).astype(np.uint8))
     for k, v in ref.stats.items():
+        if k == "spilled_traces":  # a GPU scheduling detail (tile overflow), not a job quantity
+            continue
         assert st[k] == v, f"stat {k}: gpu {st[k]} != oracle {v}"
 
 

@@ -26,6 +26,7 @@ struct zk_ctx {
     bool strict = true;
     uint32_t max_trace = 131072;
     bool timing = false;
+    uint32_t ablate = 0;
     uint64_t* table = nullptr;            // S*S*kLimbs
     bool own_table = true;
     unsigned long long* stats = nullptr;  // kStatShards*ST_N
@@ -148,6 +149,7 @@ zk_status zk_ctx_create(const zk_config* cfg, zk_ctx** out) {
     c->S = cfg->num_services;
     c->strict = cfg->strict != 0;
     c->timing = cfg->timing != 0;
+    c->ablate = cfg->reserved[0];  // diagnostic ablation switch, never set by the product
     if (cfg->max_trace_records) c->max_trace = cfg->max_trace_records;
     zk_status st = ZK_OK;
     hipError_t e = hipSetDevice(c->device);
@@ -271,6 +273,7 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
     a.spill_scratch = c->spill_scratch;
     a.spill_scratch_stride = c->spill_stride;
     a.max_trace = c->max_trace;
+    a.ablate = c->ablate;
     EventPair ej, es;
     if (c->timing) {
         ej = take_pair(c);

@@ -73,6 +73,7 @@ struct JoinArgs {
     uint8_t* spill_scratch;
     uint64_t spill_scratch_stride;  // bytes per WG
     uint32_t max_trace;             // records
+    uint32_t ablate;                // diagnostic builds only: 1 = join but do not emit links
 };
 
 // host-side launchers (implemented in the .hip files)

@@ -363,7 +363,7 @@ __global__ __launch_bounds__(WG) void k_span_join_tile(JoinArgs a) {
                             if (d >= kMaxDuration) {
                                 st.inc(ST_DUR_RANGE);
                             } else {
-                                emit_link(a.table, (sp & kSvcIdMask) * a.S + (sL & kSvcIdMask), d);
+                                if (!a.ablate) emit_link(a.table, (sp & kSvcIdMask) * a.S + (sL & kSvcIdMask), d);
                             }
                         }
                     } else {
