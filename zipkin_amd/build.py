@@ -9,7 +9,7 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = PKG / "csrc"
-SOURCES = ["zk_join.hip", "zk_finalize.hip", "zk_tracegen.hip", "zk_api.cpp"]
+SOURCES = ["zk_join.hip", "zk_reduce.hip", "zk_finalize.hip", "zk_tracegen.hip", "zk_api.cpp"]
 HEADERS = ["zk_internal.h", "zk_tracegen.h"]
 LIB = PKG / "libzkagg.so"
 ARCH = os.environ.get("ZK_OFFLOAD_ARCH", "gfx950")

@@ -36,6 +36,10 @@ struct zk_ctx {
     uint8_t* spill_scratch = nullptr;
     uint64_t spill_stride = 0;
     uint32_t spill_wgs = 16;
+    // per-tile link lists (K1 -> K3)
+    uint64_t* links = nullptr;
+    uint32_t* link_count = nullptr;
+    uint64_t link_tiles = 0;
     // host-pointer input staging
     void* stage = nullptr;
     uint64_t stage_cap = 0;
@@ -44,7 +48,7 @@ struct zk_ctx {
     uint64_t records_since_reset = 0;
     std::string err;
     // timing
-    std::vector<EventPair> ev_free, ev_join, ev_spill, ev_fin;
+    std::vector<EventPair> ev_free, ev_join, ev_reduce, ev_spill, ev_fin;
     zk_timing tm{};
 };
 
@@ -77,7 +81,23 @@ EventPair take_pair(zk_ctx* c) {
     return p;
 }
 
-uint64_t tiles_for(uint64_t n) { return (n + 1023) / 1024; }
+uint64_t tiles_for(uint64_t n) { return (n + join_tile_records() - 1) / join_tile_records(); }
+
+zk_status ensure_links(zk_ctx* c, uint64_t n) {
+    const uint64_t tiles = tiles_for(n);
+    if (tiles <= c->link_tiles) return ZK_OK;
+    if (c->links) ZK_HIP(c, hipFree(c->links));
+    if (c->link_count) ZK_HIP(c, hipFree(c->link_count));
+    c->links = nullptr;
+    c->link_count = nullptr;
+    c->link_tiles = 0;
+    ZK_HIP(c, hipMalloc(&c->links, tiles * join_tile_capacity() * sizeof(uint64_t)));
+    ZK_HIP(c, hipMalloc(&c->link_count, tiles * sizeof(uint32_t)));
+    c->link_tiles = tiles;
+    return ZK_OK;
+}
+
+bool aligned(const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; }
 
 zk_status ensure_spill(zk_ctx* c, uint64_t n) {
     const uint64_t need = tiles_for(n) + 1;
@@ -194,9 +214,11 @@ zk_status zk_ctx_destroy(zk_ctx* c) {
     hipFree(c->spill_count);
     hipFree(c->spill_list);
     hipFree(c->spill_scratch);
+    hipFree(c->links);
+    hipFree(c->link_count);
     hipFree(c->stage);
     hipFree(c->fin_stage);
-    for (auto* v : {&c->ev_free, &c->ev_join, &c->ev_spill, &c->ev_fin})
+    for (auto* v : {&c->ev_free, &c->ev_join, &c->ev_reduce, &c->ev_spill, &c->ev_fin})
         for (auto& p : *v) {
             hipEventDestroy(p.a);
             hipEventDestroy(p.b);
@@ -239,17 +261,23 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
         // PCIe path: stage the host columns in HBM (reported separately, never the bench value)
         if (n > c->stage_cap) {
             if (c->stage) ZK_HIP(c, hipFree(c->stage));
-            ZK_HIP(c, hipMalloc(&c->stage, n * 48));
+            ZK_HIP(c, hipMalloc(&c->stage, n * 48 + 7 * 256));
             c->stage_cap = n;
         }
         uint8_t* p = (uint8_t*)c->stage;
-        uint64_t* tid = (uint64_t*)p;
-        uint64_t* sid = tid + n;
-        uint64_t* pid = sid + n;
-        int64_t* fts = (int64_t*)(pid + n);
-        int64_t* lts = fts + n;
-        uint32_t* svc = (uint32_t*)(lts + n);
-        uint32_t* flg = svc + n;
+        // every staged column starts on a 256-byte boundary (K1 uses 16-byte pair loads)
+        auto carve = [&](uint64_t bytes) {
+            uint8_t* q = p;
+            p += (bytes + 255) & ~255ull;
+            return q;
+        };
+        uint64_t* tid = (uint64_t*)carve(n * 8);
+        uint64_t* sid = (uint64_t*)carve(n * 8);
+        uint64_t* pid = (uint64_t*)carve(n * 8);
+        int64_t* fts = (int64_t*)carve(n * 8);
+        int64_t* lts = (int64_t*)carve(n * 8);
+        uint32_t* svc = (uint32_t*)carve(n * 4);
+        uint32_t* flg = (uint32_t*)carve(n * 4);
         ZK_HIP(c, hipMemcpyAsync(tid, cols->trace_id, n * 8, hipMemcpyHostToDevice, c->stream));
         ZK_HIP(c, hipMemcpyAsync(sid, cols->span_id, n * 8, hipMemcpyHostToDevice, c->stream));
         ZK_HIP(c, hipMemcpyAsync(pid, cols->parent_id, n * 8, hipMemcpyHostToDevice, c->stream));
@@ -259,7 +287,15 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
         ZK_HIP(c, hipMemcpyAsync(flg, cols->flags, n * 4, hipMemcpyHostToDevice, c->stream));
         d = SpanColsDev{tid, sid, pid, fts, lts, svc, flg, n};
     }
+    if (flags & ZK_BATCH_DEVICE_PTRS) {
+        // K1 reads two records per lane with one 16-byte (u64 columns) / 8-byte (u32) load
+        if (!aligned(d.trace_id, 16) || !aligned(d.span_id, 16) || !aligned(d.parent_id, 16) ||
+            !aligned(d.first_ts, 16) || !aligned(d.last_ts, 16) || !aligned(d.service_id, 8) ||
+            !aligned(d.flags, 8))
+            return fail(c, ZK_ERR_INVALID_ARG, "device columns must be 16-byte (u64) / 8-byte (u32) aligned");
+    }
     zk_status st = ensure_spill(c, n);
+    if (st == ZK_OK) st = ensure_links(c, n);
     if (st != ZK_OK) return st;
     ZK_HIP(c, hipMemsetAsync(c->spill_count, 0, 4, c->stream));
     JoinArgs a{};
@@ -274,7 +310,10 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
     a.spill_scratch_stride = c->spill_stride;
     a.max_trace = c->max_trace;
     a.ablate = c->ablate;
-    EventPair ej, es;
+    a.links = c->links;
+    a.link_count = c->link_count;
+    a.link_stride = join_tile_capacity();
+    EventPair ej, er, es;
     if (c->timing) {
         ej = take_pair(c);
         ZK_HIP(c, hipEventRecord(ej.a, c->stream));
@@ -283,6 +322,13 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
     if (c->timing) {
         ZK_HIP(c, hipEventRecord(ej.b, c->stream));
         c->ev_join.push_back(ej);
+        er = take_pair(c);
+        ZK_HIP(c, hipEventRecord(er.a, c->stream));
+    }
+    ZK_HIP(c, launch_link_reduce(c->links, c->link_count, join_tile_capacity(), tiles_for(n), c->table, c->stream));
+    if (c->timing) {
+        ZK_HIP(c, hipEventRecord(er.b, c->stream));
+        c->ev_reduce.push_back(er);
         es = take_pair(c);
         ZK_HIP(c, hipEventRecord(es.a, c->stream));
     }
@@ -369,6 +415,7 @@ zk_status zk_ctx_timing(zk_ctx* c, zk_timing* out) {
         v.clear();
     };
     drain(c->ev_join, &c->tm.join_ms, &c->tm.join_ms_total, &c->tm.join_calls);
+    drain(c->ev_reduce, &c->tm.reduce_ms, &c->tm.reduce_ms_total, nullptr);
     drain(c->ev_spill, &c->tm.spill_ms, nullptr, nullptr);
     drain(c->ev_fin, &c->tm.finalize_ms, nullptr, nullptr);
     *out = c->tm;

@@ -74,10 +74,18 @@ struct JoinArgs {
     uint64_t spill_scratch_stride;  // bytes per WG
     uint32_t max_trace;             // records
     uint32_t ablate;                // diagnostic builds only: 1 = join but do not emit links
+    // per-tile link lists written by K1: tile t's links at links[t*link_stride ...], link_count[t]
+    uint64_t* links;                // (cell << 40) | duration
+    uint32_t* link_count;
+    uint64_t link_stride;
 };
 
 // host-side launchers (implemented in the .hip files)
 hipError_t launch_join(const JoinArgs& a, hipStream_t s);
+uint64_t join_tile_records();   // TILE (records owned per K1 workgroup)
+uint64_t join_tile_capacity();  // CAP (max links per tile)
+hipError_t launch_link_reduce(const uint64_t* links, const uint32_t* counts, uint64_t stride, uint64_t tiles,
+                              uint64_t* table, hipStream_t s);
 hipError_t launch_spill(const JoinArgs& a, uint32_t spill_wgs, hipStream_t s);
 uint64_t spill_scratch_bytes_per_wg(uint32_t max_trace);
 hipError_t launch_finalize(const uint64_t* table, uint32_t S, const zk_link_table* out,

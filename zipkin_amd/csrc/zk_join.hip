@@ -124,257 +124,391 @@ __device__ __forceinline__ void flush_stats(StatPack& sp, uint32_t* s_stat, unsi
 
 // =============================================================================================
 // K1: tile kernel
+//
+// Workgroup = 256 threads owning the traces that START in records [lo, lo + TILE); a trace may
+// overhang the tile by up to TILE records (CAP = 2 TILE), longer ones are spilled. Thread t holds
+// records 2t, 2t+1 (+TILE for the overhang), so every u64 column is read with one 16-byte load
+// per lane. LDS is 46 KB, i.e. three workgroups per CU: one loads while the others merge/join.
+//
+// Hash slot word (u32): bits 0..10 leader index + 1; bits 12..15 "seen >= 1" and 16..19
+// "seen >= 2" for cs, cr, sr, ss (Span.isValid = no ">= 2" bit); bit 20 some fragment has a
+// parentId, bit 21 some fragment has none. Fragments OR their bits into the slot, so validity and
+// parent presence need no per-span counters.
 // =============================================================================================
-template <int TILE, int CAP, int WG>
-__global__ __launch_bounds__(WG) void k_span_join_tile(JoinArgs a) {
-    static_assert(CAP % WG == 0 && CAP >= TILE && (CAP & (CAP - 1)) == 0 && CAP <= 4096, "tile");
-    constexpr int PT = CAP / WG;
+constexpr uint32_t kSlotIdx = 0x7FFu;
+constexpr int kSlotA = 12;
+constexpr int kSlotB = 16;
+constexpr uint32_t kSlotP1 = 1u << 20;
+constexpr uint32_t kSlotP0 = 1u << 21;
+
+// own bits of a fragment and the "seen exactly once" core annotations it may promote to ">= 2"
+__device__ __forceinline__ uint32_t frag_bits(uint32_t f, uint32_t* once) {
+    uint32_t A = 0, B = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint32_t k = (f >> (ZK_F_CS_SHIFT + 2 * c)) & 3u;
+        A |= (k >= 1 ? 1u : 0u) << c;
+        B |= (k >= 2 ? 1u : 0u) << c;
+    }
+    *once = A & ~B;
+    return (A << kSlotA) | (B << kSlotB) | ((f & ZK_F_HAS_PARENT) ? kSlotP1 : kSlotP0);
+}
+__device__ __forceinline__ bool slot_valid(uint32_t w) { return ((w >> kSlotB) & 0xFu) == 0u; }
+
+__device__ __forceinline__ uint64_t spread32(uint32_t x) {
+    uint64_t v = x;
+    v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+    v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+    v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    v = (v | (v << 2)) & 0x3333333333333333ull;
+    v = (v | (v << 1)) & 0x5555555555555555ull;
+    return v;
+}
+
+// two consecutive elements starting at i (i even, columns 16-byte aligned); zeros past `lim`
+__device__ __forceinline__ void ld2_u64(const uint64_t* __restrict__ p, uint64_t i, uint64_t lim, uint64_t v[2]) {
+    if (i + 1 < lim) {
+        const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(p + i);
+        v[0] = x.x;
+        v[1] = x.y;
+    } else {
+        v[0] = i < lim ? p[i] : 0;
+        v[1] = 0;
+    }
+}
+__device__ __forceinline__ void ld2_u32(const uint32_t* __restrict__ p, uint64_t i, uint64_t lim, uint32_t v[2]) {
+    if (i + 1 < lim) {
+        const uint2 x = *reinterpret_cast<const uint2*>(p + i);
+        v[0] = x.x;
+        v[1] = x.y;
+    } else {
+        v[0] = i < lim ? p[i] : 0;
+        v[1] = 0;
+    }
+}
+
+template <int TILE, int WG>
+__global__ __launch_bounds__(WG, 3) void k_span_join_tile(JoinArgs a) {
+    constexpr int CAP = 2 * TILE;
     constexpr int H = 2 * CAP;
-    constexpr int NC = CAP / 64;
+    constexpr int NWORD = CAP / 64;
+    static_assert(TILE == 2 * WG && CAP <= 2047, "two records per thread per half");
     __shared__ uint64_t s_sid[CAP];
     __shared__ long long s_first[CAP];
     __shared__ long long s_last[CAP];
-    __shared__ uint64_t s_cnt[CAP];
     __shared__ uint64_t s_pid[CAP];
     __shared__ uint32_t s_svck[CAP];
     __shared__ uint16_t s_seg[CAP];
     __shared__ uint32_t s_ht[H];
-    __shared__ int s_chunk_last[NC];
-    __shared__ int s_chunk_pref[NC];
+    __shared__ uint64_t s_mask[NWORD];
+    __shared__ int s_wprev[NWORD];
     __shared__ uint32_t s_stat[ST_N];
-    __shared__ uint64_t s_start, s_end;
-    __shared__ int s_tail, s_cut;
+    __shared__ uint32_t s_wsum[WG / 64];
+    __shared__ int s_end, s_tail;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t n = a.c.n;
     const uint64_t lo = (uint64_t)blockIdx.x * TILE;
     const uint64_t hi = (lo + TILE < n) ? lo + TILE : n;
+    const int tile_n = (int)(hi - lo);
     const uint64_t* __restrict__ tr = a.c.trace_id;
 
-    // ---- 1. which traces does this tile own: those starting in [lo, hi) -------------------
+    // ---- 1. loads of the tile half (all columns) + trace-boundary bitmask ------------------
+    // r[h][e]: half h (0 = tile, 1 = overhang), element e -> local record j = h*TILE + 2 tid + e
+    uint64_t r_tid[2][2], r_sid[2][2], r_pid[2][2];
+    uint64_t r_first[2][2], r_last[2][2];
+    uint32_t r_svc[2][2], r_flags[2][2];
+    {
+        const uint64_t i = lo + 2 * tid;
+        ld2_u64(tr, i, hi, r_tid[0]);
+        ld2_u64(a.c.span_id, i, hi, r_sid[0]);
+        ld2_u64(a.c.parent_id, i, hi, r_pid[0]);
+        ld2_u64((const uint64_t*)a.c.first_ts, i, hi, r_first[0]);
+        ld2_u64((const uint64_t*)a.c.last_ts, i, hi, r_last[0]);
+        ld2_u32(a.c.service_id, i, hi, r_svc[0]);
+        ld2_u32(a.c.flags, i, hi, r_flags[0]);
+    }
     if (tid < ST_N) s_stat[tid] = 0u;
-    if (wave == 0) {
-        uint64_t start = hi;
-        for (uint64_t base = lo; base < hi; base += 64) {
-            const uint64_t i = base + lane;
-            bool b = false;
-            if (i < hi) b = (i == 0) || (tr[i] != tr[i - 1]);
-            const uint64_t m = __ballot(b);
-            if (m) {
-                start = base + (uint64_t)(__ffsll((unsigned long long)m) - 1);
-                break;
-            }
+    // overhang scan by wave 0: traceIds of the next 64 records, issued with the tile loads
+    uint64_t ov[2] = {0, 0};
+    const bool full_tile = tile_n == TILE;
+    if (wave == 0 && full_tile) ld2_u64(tr, hi + 2 * (lane & 31), n, ov);
+    {
+        uint64_t prev = __shfl_up(r_tid[0][1], 1);
+        if (lane == 0) prev = (lo + 2 * tid > 0) ? tr[lo + 2 * tid - 1] : ~r_tid[0][0];
+        const bool b0 = (2 * tid < tile_n) && r_tid[0][0] != prev;
+        const bool b1 = (2 * tid + 1 < tile_n) && r_tid[0][1] != r_tid[0][0];
+        const uint64_t m0 = __ballot(b0), m1 = __ballot(b1);
+        if (lane == 0) {
+            s_mask[2 * wave] = spread32((uint32_t)m0) | (spread32((uint32_t)m1) << 1);
+            s_mask[2 * wave + 1] = spread32((uint32_t)(m0 >> 32)) | (spread32((uint32_t)(m1 >> 32)) << 1);
         }
-        int tail = 0;
-        uint64_t end = start;
-        if (start < hi) {
-            const uint64_t limit = start + CAP;  // records [start, limit) fit the tile
-            end = ~0ull;
-            for (uint64_t base = hi; base <= limit; base += 64) {
-                const uint64_t i = base + lane;
-                bool b = false;
-                if (i <= limit) b = (i >= n) || (tr[i] != tr[i - 1]);
-                const uint64_t m = __ballot(b);
-                if (m) {
-                    end = base + (uint64_t)(__ffsll((unsigned long long)m) - 1);
+    }
+    if (wave == 0) {
+        // end of the last owned trace: first boundary at local index >= tile_n
+        int end = tile_n, tail = 0;
+        if (full_tile) {
+            end = -1;
+            for (int base = TILE; base < CAP; base += 64) {
+                const uint64_t g = lo + base + 2 * (lane & 31);
+                uint64_t v[2];
+                if (base == TILE) {
+                    v[0] = ov[0];
+                    v[1] = ov[1];
+                } else {
+                    ld2_u64(tr, g, n, v);
+                }
+                uint64_t prev = __shfl_up(v[1], 1);
+                if (lane == 0) prev = tr[g - 1];
+                const bool b0 = lane < 32 && (g >= n || v[0] != prev);
+                const bool b1 = lane < 32 && (g + 1 >= n || v[1] != v[0]);
+                const uint64_t w = spread32((uint32_t)__ballot(b0)) | (spread32((uint32_t)__ballot(b1)) << 1);
+                if (lane == 0) s_mask[base / 64] = w;
+                if (w) {
+                    end = base + (int)__ffsll((unsigned long long)w) - 1;
                     break;
                 }
             }
-            if (end == ~0ull) {  // the last owned trace does not fit: spill it
+            if (end < 0) {
                 tail = 1;
-                end = hi;
+                end = TILE;
             }
         }
         if (lane == 0) {
-            s_start = start;
             s_end = end;
             s_tail = tail;
         }
     }
     __syncthreads();
-    const uint64_t start = s_start;
-    if (start >= hi) return;
+    // start = first boundary in the tile half; cut = start of the trace that overhangs CAP
+    int start = -1, last_b = -1;
+#pragma unroll
+    for (int w = 0; w < TILE / 64; ++w) {
+        const uint64_t x = s_mask[w];
+        if (x && start < 0) start = 64 * w + (int)__ffsll((unsigned long long)x) - 1;
+        if (x) last_b = 64 * w + 63 - (int)__clzll((long long)x);
+    }
+    if (start < 0) {  // every record here belongs to a trace started by an earlier tile
+        if (tid == 0) a.link_count[blockIdx.x] = 0u;
+        return;
+    }
     const int tail = s_tail;
-    const int m_load = (int)(s_end - start);
+    const int end = s_end;
+    const int m = tail ? last_b : end;  // records [start, m) are ours
+    if (tid == 0) {
+        int p = -1;
+        const int used = (end + 63) / 64;
+        for (int w = 0; w < NWORD; ++w) {
+            s_wprev[w] = p;
+            const uint64_t x = w < used ? s_mask[w] : 0;
+            if (x) p = 64 * w + 63 - (int)__clzll((long long)x);
+        }
+        if (tail) {
+            const unsigned int idx = atomicAdd(a.spill_count, 1u);
+            if (idx < a.spill_cap) a.spill_list[idx] = lo + (uint64_t)last_b;
+            atomicAdd(&a.stats[ST_SPILLED], 1ull);
+        }
+    }
+    // ---- 2. overhang columns -------------------------------------------------------------------
+    if (end > TILE) {
+        const uint64_t i = lo + TILE + 2 * tid;
+        const uint64_t lim = lo + (uint64_t)end;
+        ld2_u64(tr, i, lim, r_tid[1]);
+        ld2_u64(a.c.span_id, i, lim, r_sid[1]);
+        ld2_u64(a.c.parent_id, i, lim, r_pid[1]);
+        ld2_u64((const uint64_t*)a.c.first_ts, i, lim, r_first[1]);
+        ld2_u64((const uint64_t*)a.c.last_ts, i, lim, r_last[1]);
+        ld2_u32(a.c.service_id, i, lim, r_svc[1]);
+        ld2_u32(a.c.flags, i, lim, r_flags[1]);
+    } else {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            r_sid[1][e] = r_pid[1][e] = r_first[1][e] = r_last[1][e] = 0;
+            r_svc[1][e] = r_flags[1][e] = 0;
+        }
+    }
+    __syncthreads();  // s_wprev
 
-    // ---- 2. coalesced column loads + trace segmentation (ballot of traceId changes) -------
-    uint64_t r_sid[PT], r_pid[PT];
-    long long r_first[PT], r_last[PT];
-    uint32_t r_flags[PT], r_svck[PT];
-    int r_seg[PT], r_leader[PT];
-    bool r_rerr[PT];
+    // ---- 3. segment ids, LDS staging -------------------------------------------------------------
+    int r_seg[2][2];
+    uint32_t r_svck[2][2];
+    bool r_rerr[2][2];
+    StatPack st;
 #pragma unroll
-    for (int k = 0; k < PT; ++k) {
-        const int j = tid + k * WG;
-        const bool in = j < m_load;
-        const uint64_t gi = start + (uint64_t)j;
-        uint64_t t = 0;
-        r_sid[k] = 0;
-        r_pid[k] = 0;
-        r_first[k] = 0;
-        r_last[k] = 0;
-        r_flags[k] = 0;
-        r_rerr[k] = false;
-        uint32_t svc = 0;
-        if (in) {
-            t = tr[gi];
-            r_sid[k] = a.c.span_id[gi];
-            r_pid[k] = a.c.parent_id[gi];
-            r_first[k] = a.c.first_ts[gi];
-            r_last[k] = a.c.last_ts[gi];
-            svc = a.c.service_id[gi];
-            r_flags[k] = a.c.flags[gi];
-        }
-        r_svck[k] = svc_key(r_flags[k], svc, a.S, &r_rerr[k]);
-        uint64_t tprev = __shfl_up(t, 1);
-        if (lane == 0 && in && j > 0) tprev = tr[gi - 1];
-        const bool b = in && (j == 0 || t != tprev);
-        const uint64_t mask = __ballot(b);
-        const int c = (k * WG + wave * 64) >> 6;
-        if (lane == 0) s_chunk_last[c] = mask ? (c * 64 + 63 - __clzll((long long)mask)) : -1;
-        const uint64_t pm = mask & ((2ull << lane) - 1ull);
-        r_seg[k] = pm ? (c * 64 + 63 - __clzll((long long)pm)) : -1;
-    }
-    __syncthreads();
-    if (wave == 0) {
-        int v = lane < NC ? s_chunk_last[lane] : -1;
+    for (int h = 0; h < 2; ++h) {
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int o = __shfl_up(v, off);
-            if (lane >= off) v = v > o ? v : o;
-        }
-        int ex = __shfl_up(v, 1);
-        if (lane == 0) ex = -1;
-        if (lane < NC) s_chunk_pref[lane] = ex;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < PT; ++k) {
-        const int j = tid + k * WG;
-        if (r_seg[k] < 0) r_seg[k] = s_chunk_pref[j >> 6];
-        if (j < m_load) {
-            const uint32_t f = r_flags[k];
-            const bool ha = (f & ZK_F_HAS_ANNOTATIONS) != 0;
-            s_sid[j] = r_sid[k];
-            s_seg[j] = (uint16_t)r_seg[k];
-            s_first[j] = ha ? r_first[k] : LLONG_MAX;
-            s_last[j] = ha ? r_last[k] : LLONG_MIN;
-            s_cnt[j] = pack_counts(f);
-            s_pid[j] = (f & ZK_F_HAS_PARENT) ? r_pid[k] : ~0ull;
-            s_svck[j] = r_svck[k];
-            if (tail && j == m_load - 1) s_cut = r_seg[k];
+        for (int e = 0; e < 2; ++e) {
+            const int j = h * TILE + 2 * tid + e;
+            r_rerr[h][e] = false;
+            r_svck[h][e] = svc_key(r_flags[h][e], r_svc[h][e], a.S, &r_rerr[h][e]);
+            r_seg[h][e] = -1;
+            if (j >= start && j < m) {
+                const int w = j >> 6;
+                const uint64_t bits = s_mask[w] & ((2ull << (j & 63)) - 1ull);
+                const int seg = bits ? 64 * w + 63 - (int)__clzll((long long)bits) : s_wprev[w];
+                r_seg[h][e] = seg;
+                const uint32_t f = r_flags[h][e];
+                const bool ha = (f & ZK_F_HAS_ANNOTATIONS) != 0;
+                s_sid[j] = r_sid[h][e];
+                s_seg[j] = (uint16_t)seg;
+                s_first[j] = ha ? (long long)r_first[h][e] : LLONG_MAX;
+                s_last[j] = ha ? (long long)r_last[h][e] : LLONG_MIN;
+                s_pid[j] = (f & ZK_F_HAS_PARENT) ? r_pid[h][e] : ~0ull;
+                s_svck[j] = r_svck[h][e];
+            }
         }
     }
     for (int x = tid; x < H; x += WG) s_ht[x] = 0u;
     __syncthreads();
-    const int m = tail ? s_cut : m_load;
-    if (tail && tid == 0) {
-        const unsigned int idx = atomicAdd(a.spill_count, 1u);
-        if (idx < a.spill_cap) a.spill_list[idx] = start + (uint64_t)m;
-        atomicAdd(&a.stats[ST_SPILLED], 1ull);
-    }
 
-    // ---- 3. groupBy((id, traceId)): insert into the LDS hash, first fragment leads --------
+    // ---- 4. groupBy((id, traceId)): the first fragment to claim a slot leads ------------------
+    int r_leader[2][2];
+    uint32_t r_slot[2][2];
 #pragma unroll
-    for (int k = 0; k < PT; ++k) {
-        const int j = tid + k * WG;
-        r_leader[k] = -1;
-        if (j < m) {
-            const uint64_t sid = r_sid[k];
-            const uint16_t seg = (uint16_t)r_seg[k];
-            uint32_t slot = slot_hash(sid, seg) & (H - 1);
-            for (;;) {
-                const uint32_t old = atomicCAS(&s_ht[slot], 0u, (uint32_t)(j + 1));
-                if (old == 0u) {
-                    r_leader[k] = j;
-                    break;
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            r_leader[h][e] = -1;
+            r_slot[h][e] = 0;
+            const int j = h * TILE + 2 * tid + e;
+            if (r_seg[h][e] >= 0) {
+                const uint64_t sid = r_sid[h][e];
+                const uint16_t seg = (uint16_t)r_seg[h][e];
+                uint32_t once;
+                const uint32_t bits = frag_bits(r_flags[h][e], &once);
+                uint32_t slot = slot_hash(sid, seg) & (H - 1);
+                for (;;) {
+                    const uint32_t old = atomicCAS(&s_ht[slot], 0u, (uint32_t)(j + 1) | bits);
+                    if (old == 0u) {
+                        r_leader[h][e] = j;
+                        break;
+                    }
+                    const int o = (int)(old & kSlotIdx) - 1;
+                    if (s_sid[o] == sid && s_seg[o] == seg) {
+                        r_leader[h][e] = o;
+                        break;
+                    }
+                    slot = (slot + 1) & (H - 1);
                 }
-                const int o = (int)old - 1;
-                if (s_sid[o] == sid && s_seg[o] == seg) {
-                    r_leader[k] = o;
+                r_slot[h][e] = slot;
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- 5. reduce(mergeSpan) -------------------------------------------------------------------
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int j = h * TILE + 2 * tid + e;
+            const int L = r_leader[h][e];
+            if (L >= 0 && L != j) {
+                const uint32_t f = r_flags[h][e];
+                if (f & ZK_F_HAS_ANNOTATIONS) {
+                    atomicMin(&s_first[L], (long long)r_first[h][e]);
+                    atomicMax(&s_last[L], (long long)r_last[h][e]);
+                }
+                if (r_svck[h][e] != kSvcNone) atomicMin(&s_svck[L], r_svck[h][e]);
+                if (f & ZK_F_HAS_PARENT) atomicMin((unsigned long long*)&s_pid[L], (unsigned long long)r_pid[h][e]);
+                uint32_t once;
+                const uint32_t bits = frag_bits(f, &once);
+                const uint32_t old = atomicOr(&s_ht[r_slot[h][e]], bits);
+                const uint32_t promote = once & (old >> kSlotA) & 0xFu;  // second occurrence
+                if (promote) atomicOr(&s_ht[r_slot[h][e]], promote << kSlotB);
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- 6. filter(isValid), join on (parentId, traceId), emit (cell, duration) links ---------
+    uint64_t r_link[2][2];
+    uint32_t nlinks = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            r_link[h][e] = ~0ull;
+            const int L = r_leader[h][e];
+            if (L < 0) continue;
+            const int j = h * TILE + 2 * tid + e;
+            const uint32_t f = r_flags[h][e];
+            const uint32_t w = s_ht[r_slot[h][e]];
+            const uint32_t sL = s_svck[L];
+            const uint64_t pL = s_pid[L];
+            bool amb = (f & ZK_F_HAS_PARENT) ? (r_pid[h][e] != pL) : ((w & kSlotP1) != 0u);
+            const uint32_t sk = r_svck[h][e];
+            if (sk != kSvcNone && (sk >> kSvcKindShift) == (sL >> kSvcKindShift) && sk != sL) amb = true;
+            if (amb) st.inc(ST_AMBIGUOUS);
+            if (r_rerr[h][e]) st.inc(ST_SVC_RANGE);
+            if (L != j) continue;
+            st.inc(ST_MERGED);
+            const bool valid = slot_valid(w);
+            st.inc(valid ? ST_VALID : ST_INVALID);
+            if (!(valid && (w & kSlotP1))) continue;
+            st.inc(ST_CHILD);
+            const uint16_t seg = (uint16_t)r_seg[h][e];
+            uint32_t slot = slot_hash(pL, seg) & (H - 1);
+            uint32_t pw = 0;
+            for (;;) {
+                const uint32_t o = s_ht[slot];
+                if (o == 0u) break;
+                const int oi = (int)(o & kSlotIdx) - 1;
+                if (s_sid[oi] == pL && s_seg[oi] == seg) {
+                    pw = o;
                     break;
                 }
                 slot = (slot + 1) & (H - 1);
             }
-        }
-    }
-    __syncthreads();
-
-    // ---- 4. reduce(mergeSpan): fold every other fragment into its leader -------------------
-#pragma unroll
-    for (int k = 0; k < PT; ++k) {
-        const int j = tid + k * WG;
-        const int L = r_leader[k];
-        if (j < m && L != j) {
-            const uint32_t f = r_flags[k];
-            if (f & ZK_F_HAS_ANNOTATIONS) {
-                atomicMin(&s_first[L], r_first[k]);
-                atomicMax(&s_last[L], r_last[k]);
+            if (pw == 0u || !slot_valid(pw)) {
+                st.inc(ST_MISSING_PARENT);
+                continue;
             }
-            atomicAdd((unsigned long long*)&s_cnt[L], (unsigned long long)pack_counts(f));
-            if (r_svck[k] != kSvcNone) atomicMin(&s_svck[L], r_svck[k]);
-            if (f & ZK_F_HAS_PARENT) atomicMin((unsigned long long*)&s_pid[L], (unsigned long long)r_pid[k]);
+            st.inc(ST_JOINED);
+            const uint32_t sp = s_svck[(pw & kSlotIdx) - 1];
+            if (sp == kSvcNone || sL == kSvcNone) {
+                st.inc(ST_NO_SERVICE);
+                continue;
+            }
+            const uint64_t d = (uint64_t)(s_last[j] - s_first[j]);
+            if (d >= kMaxDuration) {
+                st.inc(ST_DUR_RANGE);
+                continue;
+            }
+            const uint64_t cell = (uint64_t)(sp & kSvcIdMask) * a.S + (sL & kSvcIdMask);
+            r_link[h][e] = (cell << 40) | d;
+            ++nlinks;
         }
     }
-    __syncthreads();
-
-    // ---- 5. filter(isValid), join on (parentId, traceId), emit DependencyLink moments ------
-    StatPack st;
+    // block exclusive scan of per-thread link counts -> compact per-tile link list
+    uint32_t incl = nlinks;
 #pragma unroll
-    for (int k = 0; k < PT; ++k) {
-        const int j = tid + k * WG;
-        if (j < m) {
-            const int L = r_leader[k];
-            const uint32_t f = r_flags[k];
-            const uint64_t cL = s_cnt[L];
-            const uint32_t npar = counts_npar(cL);
-            const uint32_t sL = s_svck[L];
-            bool amb = (f & ZK_F_HAS_PARENT) ? (r_pid[k] != s_pid[L]) : (npar > 0);
-            const uint32_t sk = r_svck[k];
-            if (sk != kSvcNone && (sk >> kSvcKindShift) == (sL >> kSvcKindShift) && sk != sL) amb = true;
-            if (amb) st.inc(ST_AMBIGUOUS);
-            if (r_rerr[k]) st.inc(ST_SVC_RANGE);
-            if (L == j) {
-                st.inc(ST_MERGED);
-                const bool valid = counts_valid(cL);
-                st.inc(valid ? ST_VALID : ST_INVALID);
-                if (valid && npar > 0) {
-                    st.inc(ST_CHILD);
-                    const uint64_t p = s_pid[j];
-                    const uint16_t seg = (uint16_t)r_seg[k];
-                    uint32_t slot = slot_hash(p, seg) & (H - 1);
-                    int P = -1;
-                    for (;;) {
-                        const uint32_t o = s_ht[slot];
-                        if (o == 0u) break;
-                        if (s_sid[o - 1] == p && s_seg[o - 1] == seg) {
-                            P = (int)o - 1;
-                            break;
-                        }
-                        slot = (slot + 1) & (H - 1);
-                    }
-                    if (P >= 0 && counts_valid(s_cnt[P])) {
-                        st.inc(ST_JOINED);
-                        const uint32_t sp = s_svck[P];
-                        if (sp == kSvcNone || sL == kSvcNone) {
-                            st.inc(ST_NO_SERVICE);
-                        } else {
-                            const uint64_t d = (uint64_t)(s_last[j] - s_first[j]);
-                            if (d >= kMaxDuration) {
-                                st.inc(ST_DUR_RANGE);
-                            } else {
-                                if (!a.ablate) emit_link(a.table, (sp & kSvcIdMask) * a.S + (sL & kSvcIdMask), d);
-                            }
-                        }
-                    } else {
-                        st.inc(ST_MISSING_PARENT);
-                    }
-                }
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    if (lane == 63) s_wsum[wave] = incl;
+    if (tid == 0) st.inc(ST_RECORDS, (uint32_t)(m - start));
+    flush_stats(st, s_stat, a.stats);  // contains a barrier, publishes s_wsum
+    uint32_t base = 0, total = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < WG / 64; ++w2) {
+        const uint32_t v = s_wsum[w2];
+        if (w2 < wave) base += v;
+        total += v;
+    }
+    uint32_t pos = base + incl - nlinks;
+    uint64_t* __restrict__ out = a.links + (uint64_t)blockIdx.x * a.link_stride;
+    if (!a.ablate) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                if (r_link[h][e] != ~0ull) out[pos++] = r_link[h][e];
             }
         }
     }
-    if (tid == 0) st.inc(ST_RECORDS, (uint32_t)m);
-    flush_stats(st, s_stat, a.stats);
+    if (tid == 0) a.link_count[blockIdx.x] = a.ablate ? 0u : total;
 }
 
 // =============================================================================================
@@ -602,9 +736,8 @@ __global__ __launch_bounds__(kSpillWG) void k_span_join_spill(JoinArgs a) {
 }
 
 // tile geometry of the shipped K1
-constexpr int kTile = 1024;
-constexpr int kCap = 2048;
 constexpr int kTileWG = 256;
+constexpr int kTile = 2 * kTileWG;
 
 }  // namespace
 
@@ -617,7 +750,7 @@ uint64_t spill_scratch_bytes_per_wg(uint32_t max_trace) {
 hipError_t launch_join(const JoinArgs& a, hipStream_t s) {
     if (a.c.n == 0) return hipSuccess;
     const uint64_t tiles = (a.c.n + kTile - 1) / kTile;
-    hipLaunchKernelGGL((k_span_join_tile<kTile, kCap, kTileWG>), dim3((unsigned)tiles), dim3(kTileWG), 0, s, a);
+    hipLaunchKernelGGL((k_span_join_tile<kTile, kTileWG>), dim3((unsigned)tiles), dim3(kTileWG), 0, s, a);
     return hipGetLastError();
 }
 
@@ -628,5 +761,6 @@ hipError_t launch_spill(const JoinArgs& a, uint32_t spill_wgs, hipStream_t s) {
 }
 
 uint64_t join_tile_records() { return kTile; }
+uint64_t join_tile_capacity() { return 2 * kTile; }
 
 }  // namespace zk
