@@ -39,7 +39,9 @@ struct zk_ctx {
     // per-tile link lists (K1 -> K3)
     uint64_t* links = nullptr;
     uint32_t* link_count = nullptr;
-    uint64_t link_tiles = 0;
+    uint64_t link_slots = 0;  // capacity of `links` in u64
+    uint32_t link_lists = 0;  // capacity of `link_count`
+    uint32_t cus = 256;
     // host-pointer input staging
     void* stage = nullptr;
     uint64_t stage_cap = 0;
@@ -83,17 +85,19 @@ EventPair take_pair(zk_ctx* c) {
 
 uint64_t tiles_for(uint64_t n) { return (n + join_tile_records() - 1) / join_tile_records(); }
 
-zk_status ensure_links(zk_ctx* c, uint64_t n) {
-    const uint64_t tiles = tiles_for(n);
-    if (tiles <= c->link_tiles) return ZK_OK;
+zk_status ensure_links(zk_ctx* c, uint32_t grid, uint64_t stride) {
+    const uint64_t slots = (uint64_t)grid * stride;
+    if (slots <= c->link_slots && grid <= c->link_lists) return ZK_OK;
     if (c->links) ZK_HIP(c, hipFree(c->links));
     if (c->link_count) ZK_HIP(c, hipFree(c->link_count));
     c->links = nullptr;
     c->link_count = nullptr;
-    c->link_tiles = 0;
-    ZK_HIP(c, hipMalloc(&c->links, tiles * join_tile_capacity() * sizeof(uint64_t)));
-    ZK_HIP(c, hipMalloc(&c->link_count, tiles * sizeof(uint32_t)));
-    c->link_tiles = tiles;
+    c->link_slots = 0;
+    c->link_lists = 0;
+    ZK_HIP(c, hipMalloc(&c->links, slots * sizeof(uint64_t)));
+    ZK_HIP(c, hipMalloc(&c->link_count, (uint64_t)grid * sizeof(uint32_t)));
+    c->link_slots = slots;
+    c->link_lists = grid;
     return ZK_OK;
 }
 
@@ -169,6 +173,7 @@ zk_status zk_ctx_create(const zk_config* cfg, zk_ctx** out) {
     c->S = cfg->num_services;
     c->strict = cfg->strict != 0;
     c->timing = cfg->timing != 0;
+    c->cus = prop.multiProcessorCount > 0 ? (uint32_t)prop.multiProcessorCount : 256;
     c->ablate = cfg->reserved[0];  // diagnostic ablation switch, never set by the product
     if (cfg->max_trace_records) c->max_trace = cfg->max_trace_records;
     zk_status st = ZK_OK;
@@ -294,8 +299,11 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
             !aligned(d.flags, 8))
             return fail(c, ZK_ERR_INVALID_ARG, "device columns must be 16-byte (u64) / 8-byte (u32) aligned");
     }
+    uint32_t grid = 0;
+    uint64_t per_wg = 0, stride = 0;
+    join_geometry(n, c->cus, &grid, &per_wg, &stride);
     zk_status st = ensure_spill(c, n);
-    if (st == ZK_OK) st = ensure_links(c, n);
+    if (st == ZK_OK) st = ensure_links(c, grid, stride);
     if (st != ZK_OK) return st;
     ZK_HIP(c, hipMemsetAsync(c->spill_count, 0, 4, c->stream));
     JoinArgs a{};
@@ -312,7 +320,9 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
     a.ablate = c->ablate;
     a.links = c->links;
     a.link_count = c->link_count;
-    a.link_stride = join_tile_capacity();
+    a.link_stride = stride;
+    a.per_wg = per_wg;
+    a.grid = grid;
     EventPair ej, er, es;
     if (c->timing) {
         ej = take_pair(c);
@@ -325,7 +335,7 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
         er = take_pair(c);
         ZK_HIP(c, hipEventRecord(er.a, c->stream));
     }
-    ZK_HIP(c, launch_link_reduce(c->links, c->link_count, join_tile_capacity(), tiles_for(n), c->table, c->stream));
+    ZK_HIP(c, launch_link_reduce(c->links, c->link_count, stride, grid, c->table, c->stream));
     if (c->timing) {
         ZK_HIP(c, hipEventRecord(er.b, c->stream));
         c->ev_reduce.push_back(er);

@@ -78,12 +78,16 @@ struct JoinArgs {
     uint64_t* links;                // (cell << 40) | duration
     uint32_t* link_count;
     uint64_t link_stride;
+    // persistent K1 geometry: workgroup w owns traces starting in [w*per_wg, (w+1)*per_wg)
+    uint64_t per_wg;
+    uint32_t grid;
 };
 
 // host-side launchers (implemented in the .hip files)
 hipError_t launch_join(const JoinArgs& a, hipStream_t s);
-uint64_t join_tile_records();   // TILE (records owned per K1 workgroup)
-uint64_t join_tile_capacity();  // CAP (max links per tile)
+uint64_t join_tile_records();   // TILE (records per K1 window)
+// K1 launch geometry for n records on a device with `cus` compute units
+void join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, uint64_t* link_stride);
 hipError_t launch_link_reduce(const uint64_t* links, const uint32_t* counts, uint64_t stride, uint64_t tiles,
                               uint64_t* table, hipStream_t s);
 hipError_t launch_spill(const JoinArgs& a, uint32_t spill_wgs, hipStream_t s);

@@ -187,267 +187,278 @@ __device__ __forceinline__ void ld2_u32(const uint32_t* __restrict__ p, uint64_t
     }
 }
 
+// per-thread stat counters: 16 x 32-bit fields (flushed once per workgroup)
+struct StatPack32 {
+    uint64_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    __device__ __forceinline__ void inc(int s) { w[s >> 1] += 1ull << (32 * (s & 1)); }
+};
+
+__device__ __forceinline__ void flush_stats32(StatPack32& sp, uint32_t* s_stat, unsigned long long* g_stats) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint64_t v = wave_sum_u64(sp.w[i]);
+        if (lane == 0 && v) {
+            if ((uint32_t)v) atomicAdd(&s_stat[2 * i], (uint32_t)v);
+            if ((uint32_t)(v >> 32)) atomicAdd(&s_stat[2 * i + 1], (uint32_t)(v >> 32));
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < ST_N) {
+        const uint32_t v = s_stat[threadIdx.x];
+        unsigned long long* slot = g_stats + (uint64_t)(blockIdx.x % kStatShards) * ST_N;
+        if (v) atomicAdd(&slot[threadIdx.x], (unsigned long long)v);
+    }
+}
+
+struct Window {  // two consecutive records per thread
+    uint64_t tid[2], sid[2], pid[2], first[2], last[2];
+    uint32_t svc[2], flags[2];
+    uint64_t prev;  // traceId of the record before this wave's first record
+};
+
+__device__ __forceinline__ void load_window(const JoinArgs& a, uint64_t ws, Window& w) {
+    const uint64_t n = a.c.n;
+    const uint64_t i = ws + 2 * threadIdx.x;
+    ld2_u64(a.c.trace_id, i, n, w.tid);
+    ld2_u64(a.c.span_id, i, n, w.sid);
+    ld2_u64(a.c.parent_id, i, n, w.pid);
+    ld2_u64((const uint64_t*)a.c.first_ts, i, n, w.first);
+    ld2_u64((const uint64_t*)a.c.last_ts, i, n, w.last);
+    ld2_u32(a.c.service_id, i, n, w.svc);
+    ld2_u32(a.c.flags, i, n, w.flags);
+    w.prev = 0;
+    if ((threadIdx.x & 63) == 0 && i > 0 && i - 1 < n) w.prev = a.c.trace_id[i - 1];
+}
+
+// =============================================================================================
+// K1: persistent streaming span_join
+//
+// Workgroup w owns the traces that START in records [R0, R1) = [w, w+1) * per_wg. It streams
+// through them in windows of TILE records (two per thread, 16-byte column loads): the trace
+// boundaries of the window come from a ballot bitmask; the complete traces of the window are
+// merged, validated and joined in LDS; the incomplete last trace starts the next window (its
+// records are re-read, mostly from L2). The next window's columns are prefetched into registers
+// right after its start is known, so HBM streams while the LDS phases run. A trace longer than a
+// window goes to the spill kernel. Three workgroups per CU (23 KB LDS, <= 168 VGPRs).
+//
+// Hash slot word (u32): bits 0..10 leader index + 1; bits 12..15 "seen >= 1" and 16..19
+// "seen >= 2" for cs, cr, sr, ss (Span.isValid = no ">= 2" bit); bit 20 some fragment has a
+// parentId, bit 21 some fragment has none.
+// =============================================================================================
 template <int TILE, int WG>
-__global__ __launch_bounds__(WG, 3) void k_span_join_tile(JoinArgs a) {
-    constexpr int CAP = 2 * TILE;
-    constexpr int H = 2 * CAP;
-    constexpr int NWORD = CAP / 64;
-    static_assert(TILE == 2 * WG && CAP <= 2047, "two records per thread per half");
-    __shared__ uint64_t s_sid[CAP];
-    __shared__ long long s_first[CAP];
-    __shared__ long long s_last[CAP];
-    __shared__ uint64_t s_pid[CAP];
-    __shared__ uint32_t s_svck[CAP];
-    __shared__ uint16_t s_seg[CAP];
+__global__ __launch_bounds__(WG, 3) void k_span_join_stream(JoinArgs a) {
+    constexpr int H = 2 * TILE;
+    constexpr int NWORD = TILE / 64;
+    static_assert(TILE == 2 * WG && TILE <= 2047, "two records per thread");
+    __shared__ uint64_t s_sid[TILE];
+    __shared__ long long s_first[TILE];
+    __shared__ long long s_last[TILE];
+    __shared__ uint64_t s_pid[TILE];
+    __shared__ uint32_t s_svck[TILE];
+    __shared__ uint16_t s_seg[TILE];
     __shared__ uint32_t s_ht[H];
     __shared__ uint64_t s_mask[NWORD];
-    __shared__ int s_wprev[NWORD];
     __shared__ uint32_t s_stat[ST_N];
     __shared__ uint32_t s_wsum[WG / 64];
-    __shared__ int s_end, s_tail;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t n = a.c.n;
-    const uint64_t lo = (uint64_t)blockIdx.x * TILE;
-    const uint64_t hi = (lo + TILE < n) ? lo + TILE : n;
-    const int tile_n = (int)(hi - lo);
-    const uint64_t* __restrict__ tr = a.c.trace_id;
-
-    // ---- 1. loads of the tile half (all columns) + trace-boundary bitmask ------------------
-    // r[h][e]: half h (0 = tile, 1 = overhang), element e -> local record j = h*TILE + 2 tid + e
-    uint64_t r_tid[2][2], r_sid[2][2], r_pid[2][2];
-    uint64_t r_first[2][2], r_last[2][2];
-    uint32_t r_svc[2][2], r_flags[2][2];
-    {
-        const uint64_t i = lo + 2 * tid;
-        ld2_u64(tr, i, hi, r_tid[0]);
-        ld2_u64(a.c.span_id, i, hi, r_sid[0]);
-        ld2_u64(a.c.parent_id, i, hi, r_pid[0]);
-        ld2_u64((const uint64_t*)a.c.first_ts, i, hi, r_first[0]);
-        ld2_u64((const uint64_t*)a.c.last_ts, i, hi, r_last[0]);
-        ld2_u32(a.c.service_id, i, hi, r_svc[0]);
-        ld2_u32(a.c.flags, i, hi, r_flags[0]);
-    }
-    if (tid < ST_N) s_stat[tid] = 0u;
-    // overhang scan by wave 0: traceIds of the next 64 records, issued with the tile loads
-    uint64_t ov[2] = {0, 0};
-    const bool full_tile = tile_n == TILE;
-    if (wave == 0 && full_tile) ld2_u64(tr, hi + 2 * (lane & 31), n, ov);
-    {
-        uint64_t prev = __shfl_up(r_tid[0][1], 1);
-        if (lane == 0) prev = (lo + 2 * tid > 0) ? tr[lo + 2 * tid - 1] : ~r_tid[0][0];
-        const bool b0 = (2 * tid < tile_n) && r_tid[0][0] != prev;
-        const bool b1 = (2 * tid + 1 < tile_n) && r_tid[0][1] != r_tid[0][0];
-        const uint64_t m0 = __ballot(b0), m1 = __ballot(b1);
-        if (lane == 0) {
-            s_mask[2 * wave] = spread32((uint32_t)m0) | (spread32((uint32_t)m1) << 1);
-            s_mask[2 * wave + 1] = spread32((uint32_t)(m0 >> 32)) | (spread32((uint32_t)(m1 >> 32)) << 1);
-        }
-    }
-    if (wave == 0) {
-        // end of the last owned trace: first boundary at local index >= tile_n
-        int end = tile_n, tail = 0;
-        if (full_tile) {
-            end = -1;
-            for (int base = TILE; base < CAP; base += 64) {
-                const uint64_t g = lo + base + 2 * (lane & 31);
-                uint64_t v[2];
-                if (base == TILE) {
-                    v[0] = ov[0];
-                    v[1] = ov[1];
-                } else {
-                    ld2_u64(tr, g, n, v);
-                }
-                uint64_t prev = __shfl_up(v[1], 1);
-                if (lane == 0) prev = tr[g - 1];
-                const bool b0 = lane < 32 && (g >= n || v[0] != prev);
-                const bool b1 = lane < 32 && (g + 1 >= n || v[1] != v[0]);
-                const uint64_t w = spread32((uint32_t)__ballot(b0)) | (spread32((uint32_t)__ballot(b1)) << 1);
-                if (lane == 0) s_mask[base / 64] = w;
-                if (w) {
-                    end = base + (int)__ffsll((unsigned long long)w) - 1;
-                    break;
-                }
-            }
-            if (end < 0) {
-                tail = 1;
-                end = TILE;
-            }
-        }
-        if (lane == 0) {
-            s_end = end;
-            s_tail = tail;
-        }
-    }
-    __syncthreads();
-    // start = first boundary in the tile half; cut = start of the trace that overhangs CAP
-    int start = -1, last_b = -1;
-#pragma unroll
-    for (int w = 0; w < TILE / 64; ++w) {
-        const uint64_t x = s_mask[w];
-        if (x && start < 0) start = 64 * w + (int)__ffsll((unsigned long long)x) - 1;
-        if (x) last_b = 64 * w + 63 - (int)__clzll((long long)x);
-    }
-    if (start < 0) {  // every record here belongs to a trace started by an earlier tile
+    const uint64_t R0 = (uint64_t)blockIdx.x * a.per_wg;
+    if (R0 >= n) {
         if (tid == 0) a.link_count[blockIdx.x] = 0u;
         return;
     }
-    const int tail = s_tail;
-    const int end = s_end;
-    const int m = tail ? last_b : end;  // records [start, m) are ours
-    if (tid == 0) {
-        int p = -1;
-        const int used = (end + 63) / 64;
-        for (int w = 0; w < NWORD; ++w) {
-            s_wprev[w] = p;
-            const uint64_t x = w < used ? s_mask[w] : 0;
-            if (x) p = 64 * w + 63 - (int)__clzll((long long)x);
-        }
-        if (tail) {
-            const unsigned int idx = atomicAdd(a.spill_count, 1u);
-            if (idx < a.spill_cap) a.spill_list[idx] = lo + (uint64_t)last_b;
-            atomicAdd(&a.stats[ST_SPILLED], 1ull);
-        }
-    }
-    // ---- 2. overhang columns -------------------------------------------------------------------
-    if (end > TILE) {
-        const uint64_t i = lo + TILE + 2 * tid;
-        const uint64_t lim = lo + (uint64_t)end;
-        ld2_u64(tr, i, lim, r_tid[1]);
-        ld2_u64(a.c.span_id, i, lim, r_sid[1]);
-        ld2_u64(a.c.parent_id, i, lim, r_pid[1]);
-        ld2_u64((const uint64_t*)a.c.first_ts, i, lim, r_first[1]);
-        ld2_u64((const uint64_t*)a.c.last_ts, i, lim, r_last[1]);
-        ld2_u32(a.c.service_id, i, lim, r_svc[1]);
-        ld2_u32(a.c.flags, i, lim, r_flags[1]);
-    } else {
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            r_sid[1][e] = r_pid[1][e] = r_first[1][e] = r_last[1][e] = 0;
-            r_svc[1][e] = r_flags[1][e] = 0;
-        }
-    }
-    __syncthreads();  // s_wprev
+    const uint64_t R1 = (R0 + a.per_wg < n) ? R0 + a.per_wg : n;
+    uint64_t* __restrict__ out = a.links + (uint64_t)blockIdx.x * a.link_stride;
+    uint32_t nout = 0;        // links written by this workgroup (uniform)
+    uint64_t nrec = 0;        // records aggregated (uniform)
+    StatPack32 st;
+    if (tid < ST_N) s_stat[tid] = 0u;
 
-    // ---- 3. segment ids, LDS staging -------------------------------------------------------------
-    int r_seg[2][2];
-    uint32_t r_svck[2][2];
-    bool r_rerr[2][2];
-    StatPack st;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const int j = h * TILE + 2 * tid + e;
-            r_rerr[h][e] = false;
-            r_svck[h][e] = svc_key(r_flags[h][e], r_svc[h][e], a.S, &r_rerr[h][e]);
-            r_seg[h][e] = -1;
-            if (j >= start && j < m) {
-                const int w = j >> 6;
-                const uint64_t bits = s_mask[w] & ((2ull << (j & 63)) - 1ull);
-                const int seg = bits ? 64 * w + 63 - (int)__clzll((long long)bits) : s_wprev[w];
-                r_seg[h][e] = seg;
-                const uint32_t f = r_flags[h][e];
-                const bool ha = (f & ZK_F_HAS_ANNOTATIONS) != 0;
-                s_sid[j] = r_sid[h][e];
-                s_seg[j] = (uint16_t)seg;
-                s_first[j] = ha ? (long long)r_first[h][e] : LLONG_MAX;
-                s_last[j] = ha ? (long long)r_last[h][e] : LLONG_MIN;
-                s_pid[j] = (f & ZK_F_HAS_PARENT) ? r_pid[h][e] : ~0ull;
-                s_svck[j] = r_svck[h][e];
+    uint64_t ws = R0;         // window start (even)
+    uint64_t seek = R0;       // first record that may start one of our traces
+    Window cur, nxt;
+    load_window(a, ws, cur);
+    for (;;) {
+        const int wn = (int)((n - ws) < (uint64_t)TILE ? (n - ws) : (uint64_t)TILE);
+        // ---- 1. trace boundaries of the window -------------------------------------------------
+        {
+            uint64_t prev = __shfl_up(cur.tid[1], 1);
+            if (lane == 0) prev = (ws + 2 * tid > 0) ? cur.prev : ~cur.tid[0];
+            const bool b0 = (2 * tid < wn) && cur.tid[0] != prev;
+            const bool b1 = (2 * tid + 1 < wn) && cur.tid[1] != cur.tid[0];
+            const uint64_t m0 = __ballot(b0), m1 = __ballot(b1);
+            if (lane == 0) {
+                s_mask[2 * wave] = spread32((uint32_t)m0) | (spread32((uint32_t)m1) << 1);
+                s_mask[2 * wave + 1] = spread32((uint32_t)(m0 >> 32)) | (spread32((uint32_t)(m1 >> 32)) << 1);
             }
         }
-    }
-    for (int x = tid; x < H; x += WG) s_ht[x] = 0u;
-    __syncthreads();
-
-    // ---- 4. groupBy((id, traceId)): the first fragment to claim a slot leads ------------------
-    int r_leader[2][2];
-    uint32_t r_slot[2][2];
+        __syncthreads();
+        // ---- 2. which records are ours, where the next window starts (uniform) ----------------
+        const int lo_j = (int)(seek - ws);
+        const int r1_j = (R1 - ws < (uint64_t)wn) ? (int)(R1 - ws) : wn;
+        int start = -1, stop = -1, last_b = -1;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+        for (int w = 0; w < NWORD; ++w) {
+            const uint64_t x = s_mask[w];
+            if (!x) continue;
+            last_b = 64 * w + 63 - (int)__clzll((long long)x);
+            // first boundary >= lo_j and first boundary >= r1_j
+            const int base = 64 * w;
+            if (start < 0 && base + 63 >= lo_j) {
+                const uint64_t y = lo_j > base ? (x & (~0ull << (lo_j - base))) : x;
+                if (y) start = base + (int)__ffsll((unsigned long long)y) - 1;
+            }
+            if (stop < 0 && base + 63 >= r1_j) {
+                const uint64_t y = r1_j > base ? (x & (~0ull << (r1_j - base))) : x;
+                if (y) stop = base + (int)__ffsll((unsigned long long)y) - 1;
+            }
+        }
+        const bool at_end = ws + (uint64_t)wn >= n;
+        int m;                  // records [start, m) are processed in this window
+        bool done = false;
+        uint64_t next_seek = 0;
+        if (start < 0 || (stop >= 0 && stop <= start)) {
+            // no trace of ours starts in the rest of this window
+            done = (start >= 0) || at_end || ws + (uint64_t)TILE >= R1;
+            next_seek = ws + (uint64_t)TILE;
+            start = m = 0;
+        } else if (stop >= 0) {
+            m = stop;  // traces starting at/after R1 belong to the next workgroup
+            done = true;
+        } else if (at_end) {
+            m = wn;
+            done = true;
+        } else if (last_b > start) {
+            m = last_b;  // the last trace may continue past the window: it starts the next one
+            next_seek = ws + (uint64_t)last_b;
+        } else if (start > 1) {
+            m = start;  // a single long trace starts mid-window: give it a window of its own
+            next_seek = ws + (uint64_t)start;
+        } else {
+            // the trace at `start` is longer than a window: spill it, then seek past it
+            if (tid == 0) {
+                const unsigned int idx = atomicAdd(a.spill_count, 1u);
+                if (idx < a.spill_cap) a.spill_list[idx] = ws + (uint64_t)start;
+                atomicAdd(&a.stats[ST_SPILLED], 1ull);
+            }
+            m = start;
+            next_seek = ws + (uint64_t)TILE;
+        }
+        if (!done && next_seek >= R1) done = true;
+        const uint64_t next_ws = next_seek & ~1ull;
+        if (!done) load_window(a, next_ws, nxt);  // in flight during the LDS phases below
+        nrec += (uint64_t)(m - start);
+
+        // ---- 3. segment ids and LDS staging ----------------------------------------------------
+        int r_seg[2];
+        uint32_t r_svck[2];
+        bool r_rerr[2];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-            r_leader[h][e] = -1;
-            r_slot[h][e] = 0;
-            const int j = h * TILE + 2 * tid + e;
-            if (r_seg[h][e] >= 0) {
-                const uint64_t sid = r_sid[h][e];
-                const uint16_t seg = (uint16_t)r_seg[h][e];
+            const int j = 2 * tid + e;
+            r_rerr[e] = false;
+            r_svck[e] = svc_key(cur.flags[e], cur.svc[e], a.S, &r_rerr[e]);
+            r_seg[e] = -1;
+            if (j >= start && j < m) {
+                int w = j >> 6;
+                uint64_t bits = s_mask[w] & ((2ull << (j & 63)) - 1ull);
+                while (!bits) bits = s_mask[--w];  // start is a boundary, so this terminates
+                const int seg = 64 * w + 63 - (int)__clzll((long long)bits);
+                r_seg[e] = seg;
+                const uint32_t f = cur.flags[e];
+                const bool ha = (f & ZK_F_HAS_ANNOTATIONS) != 0;
+                s_sid[j] = cur.sid[e];
+                s_seg[j] = (uint16_t)seg;
+                s_first[j] = ha ? (long long)cur.first[e] : LLONG_MAX;
+                s_last[j] = ha ? (long long)cur.last[e] : LLONG_MIN;
+                s_pid[j] = (f & ZK_F_HAS_PARENT) ? cur.pid[e] : ~0ull;
+                s_svck[j] = r_svck[e];
+            }
+        }
+        for (int x = tid; x < H; x += WG) s_ht[x] = 0u;
+        __syncthreads();
+
+        // ---- 4. groupBy((id, traceId)): the first fragment to claim a slot leads --------------
+        int r_leader[2];
+        uint32_t r_slot[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            r_leader[e] = -1;
+            r_slot[e] = 0;
+            if (r_seg[e] >= 0) {
+                const int j = 2 * tid + e;
+                const uint64_t sid = cur.sid[e];
+                const uint16_t seg = (uint16_t)r_seg[e];
                 uint32_t once;
-                const uint32_t bits = frag_bits(r_flags[h][e], &once);
+                const uint32_t bits = frag_bits(cur.flags[e], &once);
                 uint32_t slot = slot_hash(sid, seg) & (H - 1);
                 for (;;) {
                     const uint32_t old = atomicCAS(&s_ht[slot], 0u, (uint32_t)(j + 1) | bits);
                     if (old == 0u) {
-                        r_leader[h][e] = j;
+                        r_leader[e] = j;
                         break;
                     }
                     const int o = (int)(old & kSlotIdx) - 1;
                     if (s_sid[o] == sid && s_seg[o] == seg) {
-                        r_leader[h][e] = o;
+                        r_leader[e] = o;
                         break;
                     }
                     slot = (slot + 1) & (H - 1);
                 }
-                r_slot[h][e] = slot;
+                r_slot[e] = slot;
             }
         }
-    }
-    __syncthreads();
+        __syncthreads();
 
-    // ---- 5. reduce(mergeSpan) -------------------------------------------------------------------
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
+        // ---- 5. reduce(mergeSpan) ------------------------------------------------------------------
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-            const int j = h * TILE + 2 * tid + e;
-            const int L = r_leader[h][e];
+            const int j = 2 * tid + e;
+            const int L = r_leader[e];
             if (L >= 0 && L != j) {
-                const uint32_t f = r_flags[h][e];
+                const uint32_t f = cur.flags[e];
                 if (f & ZK_F_HAS_ANNOTATIONS) {
-                    atomicMin(&s_first[L], (long long)r_first[h][e]);
-                    atomicMax(&s_last[L], (long long)r_last[h][e]);
+                    atomicMin(&s_first[L], (long long)cur.first[e]);
+                    atomicMax(&s_last[L], (long long)cur.last[e]);
                 }
-                if (r_svck[h][e] != kSvcNone) atomicMin(&s_svck[L], r_svck[h][e]);
-                if (f & ZK_F_HAS_PARENT) atomicMin((unsigned long long*)&s_pid[L], (unsigned long long)r_pid[h][e]);
+                if (r_svck[e] != kSvcNone) atomicMin(&s_svck[L], r_svck[e]);
+                if (f & ZK_F_HAS_PARENT) atomicMin((unsigned long long*)&s_pid[L], (unsigned long long)cur.pid[e]);
                 uint32_t once;
                 const uint32_t bits = frag_bits(f, &once);
-                const uint32_t old = atomicOr(&s_ht[r_slot[h][e]], bits);
+                const uint32_t old = atomicOr(&s_ht[r_slot[e]], bits);
                 const uint32_t promote = once & (old >> kSlotA) & 0xFu;  // second occurrence
-                if (promote) atomicOr(&s_ht[r_slot[h][e]], promote << kSlotB);
+                if (promote) atomicOr(&s_ht[r_slot[e]], promote << kSlotB);
             }
         }
-    }
-    __syncthreads();
+        __syncthreads();
 
-    // ---- 6. filter(isValid), join on (parentId, traceId), emit (cell, duration) links ---------
-    uint64_t r_link[2][2];
-    uint32_t nlinks = 0;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
+        // ---- 6. filter(isValid), join on (parentId, traceId), (cell, duration) links ----------
+        uint64_t r_link[2];
+        uint32_t nl = 0;
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-            r_link[h][e] = ~0ull;
-            const int L = r_leader[h][e];
+            r_link[e] = ~0ull;
+            const int L = r_leader[e];
             if (L < 0) continue;
-            const int j = h * TILE + 2 * tid + e;
-            const uint32_t f = r_flags[h][e];
-            const uint32_t w = s_ht[r_slot[h][e]];
+            const int j = 2 * tid + e;
+            const uint32_t f = cur.flags[e];
+            const uint32_t w = s_ht[r_slot[e]];
             const uint32_t sL = s_svck[L];
             const uint64_t pL = s_pid[L];
-            bool amb = (f & ZK_F_HAS_PARENT) ? (r_pid[h][e] != pL) : ((w & kSlotP1) != 0u);
-            const uint32_t sk = r_svck[h][e];
+            bool amb = (f & ZK_F_HAS_PARENT) ? (cur.pid[e] != pL) : ((w & kSlotP1) != 0u);
+            const uint32_t sk = r_svck[e];
             if (sk != kSvcNone && (sk >> kSvcKindShift) == (sL >> kSvcKindShift) && sk != sL) amb = true;
             if (amb) st.inc(ST_AMBIGUOUS);
-            if (r_rerr[h][e]) st.inc(ST_SVC_RANGE);
+            if (r_rerr[e]) st.inc(ST_SVC_RANGE);
             if (L != j) continue;
             st.inc(ST_MERGED);
             const bool valid = slot_valid(w);
             st.inc(valid ? ST_VALID : ST_INVALID);
             if (!(valid && (w & kSlotP1))) continue;
             st.inc(ST_CHILD);
-            const uint16_t seg = (uint16_t)r_seg[h][e];
+            const uint16_t seg = (uint16_t)r_seg[e];
             uint32_t slot = slot_hash(pL, seg) & (H - 1);
             uint32_t pw = 0;
             for (;;) {
@@ -476,39 +487,43 @@ __global__ __launch_bounds__(WG, 3) void k_span_join_tile(JoinArgs a) {
                 continue;
             }
             const uint64_t cell = (uint64_t)(sp & kSvcIdMask) * a.S + (sL & kSvcIdMask);
-            r_link[h][e] = (cell << 40) | d;
-            ++nlinks;
+            r_link[e] = (cell << 40) | d;
+            ++nl;
         }
-    }
-    // block exclusive scan of per-thread link counts -> compact per-tile link list
-    uint32_t incl = nlinks;
+        // ---- 7. append the window's links to this workgroup's list -----------------------------
+        uint32_t incl = nl;
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t o = __shfl_up(incl, off);
-        if (lane >= off) incl += o;
-    }
-    if (lane == 63) s_wsum[wave] = incl;
-    if (tid == 0) st.inc(ST_RECORDS, (uint32_t)(m - start));
-    flush_stats(st, s_stat, a.stats);  // contains a barrier, publishes s_wsum
-    uint32_t base = 0, total = 0;
-#pragma unroll
-    for (int w2 = 0; w2 < WG / 64; ++w2) {
-        const uint32_t v = s_wsum[w2];
-        if (w2 < wave) base += v;
-        total += v;
-    }
-    uint32_t pos = base + incl - nlinks;
-    uint64_t* __restrict__ out = a.links + (uint64_t)blockIdx.x * a.link_stride;
-    if (!a.ablate) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                if (r_link[h][e] != ~0ull) out[pos++] = r_link[h][e];
-            }
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t o = __shfl_up(incl, off);
+            if (lane >= off) incl += o;
         }
+        if (lane == 63) s_wsum[wave] = incl;
+        __syncthreads();
+        uint32_t base = 0, total = 0;
+#pragma unroll
+        for (int w2 = 0; w2 < WG / 64; ++w2) {
+            const uint32_t v = s_wsum[w2];
+            if (w2 < wave) base += v;
+            total += v;
+        }
+        if (!a.ablate) {
+            uint32_t pos = nout + base + incl - nl;
+#pragma unroll
+            for (int e = 0; e < 2; ++e)
+                if (r_link[e] != ~0ull) out[pos++] = r_link[e];
+            nout += total;
+        }
+        if (done) break;
+        ws = next_ws;
+        seek = next_seek;
+        cur = nxt;
+        __syncthreads();  // s_wsum / s_mask reuse
     }
-    if (tid == 0) a.link_count[blockIdx.x] = a.ablate ? 0u : total;
+    if (tid == 0) {
+        a.link_count[blockIdx.x] = nout;
+        atomicAdd(&a.stats[(uint64_t)(blockIdx.x % kStatShards) * ST_N + ST_RECORDS], (unsigned long long)nrec);
+    }
+    flush_stats32(st, s_stat, a.stats);
 }
 
 // =============================================================================================
@@ -749,8 +764,7 @@ uint64_t spill_scratch_bytes_per_wg(uint32_t max_trace) {
 
 hipError_t launch_join(const JoinArgs& a, hipStream_t s) {
     if (a.c.n == 0) return hipSuccess;
-    const uint64_t tiles = (a.c.n + kTile - 1) / kTile;
-    hipLaunchKernelGGL((k_span_join_tile<kTile, kTileWG>), dim3((unsigned)tiles), dim3(kTileWG), 0, s, a);
+    hipLaunchKernelGGL((k_span_join_stream<kTile, kTileWG>), dim3((unsigned)a.grid), dim3(kTileWG), 0, s, a);
     return hipGetLastError();
 }
 
@@ -761,6 +775,15 @@ hipError_t launch_spill(const JoinArgs& a, uint32_t spill_wgs, hipStream_t s) {
 }
 
 uint64_t join_tile_records() { return kTile; }
-uint64_t join_tile_capacity() { return 2 * kTile; }
+
+void join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, uint64_t* link_stride) {
+    const uint64_t windows = (n + kTile - 1) / kTile;
+    uint64_t g = (uint64_t)cus * 3;  // three resident workgroups per CU
+    if (g > windows) g = windows ? windows : 1;
+    const uint64_t per = ((n + g - 1) / g + kTile - 1) / kTile * kTile;
+    *grid = (uint32_t)g;
+    *per_wg = per ? per : kTile;
+    *link_stride = *per_wg + kTile;  // a workgroup's last trace may overhang its range by < TILE
+}
 
 }  // namespace zk
