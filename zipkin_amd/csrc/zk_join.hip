@@ -350,6 +350,7 @@ __global__ __launch_bounds__(WG, 3) void k_span_join_stream(JoinArgs a) {
         const uint64_t next_ws = next_seek & ~1ull;
         if (!done) load_window(a, next_ws, nxt);  // in flight during the LDS phases below
         nrec += (uint64_t)(m - start);
+        if (a.ablate != 2) {  // diagnostic: 2 = stream windows only
 
         // ---- 3. segment ids and LDS staging ----------------------------------------------------
         int r_seg[2];
@@ -513,6 +514,7 @@ __global__ __launch_bounds__(WG, 3) void k_span_join_stream(JoinArgs a) {
                 if (r_link[e] != ~0ull) out[pos++] = r_link[e];
             nout += total;
         }
+        }  // ablate != 2
         if (done) break;
         ws = next_ws;
         seek = next_seek;
