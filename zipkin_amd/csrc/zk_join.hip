@@ -247,7 +247,7 @@ __device__ __forceinline__ void load_window(const JoinArgs& a, uint64_t ws, Wind
 // parentId, bit 21 some fragment has none.
 // =============================================================================================
 template <int TILE, int WG>
-__global__ __launch_bounds__(WG, 3) void k_span_join_stream(JoinArgs a) {
+__global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
     constexpr int H = 2 * TILE;
     constexpr int NWORD = TILE / 64;
     static_assert(TILE == 2 * WG && TILE <= 2047, "two records per thread");
@@ -780,7 +780,7 @@ uint64_t join_tile_records() { return kTile; }
 
 void join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, uint64_t* link_stride) {
     const uint64_t windows = (n + kTile - 1) / kTile;
-    uint64_t g = (uint64_t)cus * 3;  // three resident workgroups per CU
+    uint64_t g = (uint64_t)cus * 4;  // four resident workgroups per CU (<= 128 VGPRs, 23 KB LDS)
     if (g > windows) g = windows ? windows : 1;
     const uint64_t per = ((n + g - 1) / g + kTile - 1) / kTile * kTile;
     *grid = (uint32_t)g;
