@@ -93,7 +93,7 @@ typedef struct zk_span_cols {
                                               row-per-trace reads, StorageRecordReader.scala:49-54) */
 
 typedef struct zk_config {
-    uint32_t num_services;       /* S: service ids are 0..S-1, link table is S x S */
+    uint32_t num_services;       /* S <= 4096: service ids are 0..S-1, link table is S x S */
     int32_t  device;             /* HIP device ordinal */
     void*    stream;             /* hipStream_t to run on, or NULL for a private stream */
     uint32_t strict;             /* 1: finalize returns ZK_ERR_NO_SERVICE like the reference's

@@ -42,6 +42,12 @@ struct zk_ctx {
     uint64_t link_slots = 0;  // capacity of `links` in u64
     uint32_t link_lists = 0;  // capacity of `link_count`
     uint32_t cus = 256;
+    // partitioned reduce state (nb = 0: atomic reduce)
+    uint32_t nb = 0, cb_shift = 0;
+    uint32_t* hist = nullptr;
+    uint32_t* col_off = nullptr;
+    uint64_t* bucket_base = nullptr;
+    uint64_t* sorted = nullptr;
     // host-pointer input staging
     void* stage = nullptr;
     uint64_t stage_cap = 0;
@@ -96,6 +102,18 @@ zk_status ensure_links(zk_ctx* c, uint32_t grid, uint64_t stride) {
     c->link_lists = 0;
     ZK_HIP(c, hipMalloc(&c->links, slots * sizeof(uint64_t)));
     ZK_HIP(c, hipMalloc(&c->link_count, (uint64_t)grid * sizeof(uint32_t)));
+    if (c->nb) {
+        hipFree(c->hist);
+        hipFree(c->col_off);
+        hipFree(c->sorted);
+        c->hist = nullptr;
+        c->col_off = nullptr;
+        c->sorted = nullptr;
+        ZK_HIP(c, hipMalloc(&c->hist, (uint64_t)grid * c->nb * sizeof(uint32_t)));
+        ZK_HIP(c, hipMalloc(&c->col_off, (uint64_t)grid * c->nb * sizeof(uint32_t)));
+        ZK_HIP(c, hipMalloc(&c->sorted, slots * sizeof(uint64_t)));
+        if (!c->bucket_base) ZK_HIP(c, hipMalloc(&c->bucket_base, (c->nb + 1) * sizeof(uint64_t)));
+    }
     c->link_slots = slots;
     c->link_lists = grid;
     return ZK_OK;
@@ -160,7 +178,7 @@ const char* zk_last_error(const zk_ctx* ctx) { return ctx ? ctx->err.c_str() : "
 zk_status zk_ctx_create(const zk_config* cfg, zk_ctx** out) {
     if (!cfg || !out) return ZK_ERR_INVALID_ARG;
     *out = nullptr;
-    if (cfg->num_services == 0 || cfg->num_services > 65535) return ZK_ERR_INVALID_ARG;
+    if (cfg->num_services == 0 || cfg->num_services > kMaxServices) return ZK_ERR_INVALID_ARG;
     if (cfg->max_trace_records > (1u << 20)) return ZK_ERR_INVALID_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return ZK_ERR_NO_DEVICE;
@@ -174,6 +192,7 @@ zk_status zk_ctx_create(const zk_config* cfg, zk_ctx** out) {
     c->strict = cfg->strict != 0;
     c->timing = cfg->timing != 0;
     c->cus = prop.multiProcessorCount > 0 ? (uint32_t)prop.multiProcessorCount : 256;
+    bucket_geometry(c->S, &c->nb, &c->cb_shift);
     c->ablate = cfg->reserved[0];  // diagnostic ablation switch, never set by the product
     if (cfg->max_trace_records) c->max_trace = cfg->max_trace_records;
     zk_status st = ZK_OK;
@@ -221,6 +240,10 @@ zk_status zk_ctx_destroy(zk_ctx* c) {
     hipFree(c->spill_scratch);
     hipFree(c->links);
     hipFree(c->link_count);
+    hipFree(c->hist);
+    hipFree(c->col_off);
+    hipFree(c->bucket_base);
+    hipFree(c->sorted);
     hipFree(c->stage);
     hipFree(c->fin_stage);
     for (auto* v : {&c->ev_free, &c->ev_join, &c->ev_reduce, &c->ev_spill, &c->ev_fin})
@@ -323,6 +346,9 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
     a.link_stride = stride;
     a.per_wg = per_wg;
     a.grid = grid;
+    a.hist = c->hist;
+    a.nb = c->nb;
+    a.cb_shift = c->cb_shift;
     EventPair ej, er, es;
     if (c->timing) {
         ej = take_pair(c);
@@ -335,7 +361,24 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
         er = take_pair(c);
         ZK_HIP(c, hipEventRecord(er.a, c->stream));
     }
-    ZK_HIP(c, launch_link_reduce(c->links, c->link_count, stride, grid, c->table, c->stream));
+    if (c->nb) {
+        ReduceArgs r{};
+        r.links = c->links;
+        r.counts = c->link_count;
+        r.stride = stride;
+        r.lists = grid;
+        r.hist = c->hist;
+        r.nb = c->nb;
+        r.cb_shift = c->cb_shift;
+        r.col_off = c->col_off;
+        r.bucket_base = c->bucket_base;
+        r.sorted = c->sorted;
+        r.table = c->table;
+        r.cells = (uint64_t)c->S * c->S;
+        ZK_HIP(c, launch_partitioned_reduce(r, c->stream));
+    } else {
+        ZK_HIP(c, launch_link_reduce(c->links, c->link_count, stride, grid, c->table, c->stream));
+    }
     if (c->timing) {
         ZK_HIP(c, hipEventRecord(er.b, c->stream));
         c->ev_reduce.push_back(er);

@@ -21,6 +21,8 @@ constexpr int kLimbS3 = 6;   // 4 limbs
 constexpr int kLimbS4 = 10;  // 5 limbs
 constexpr uint64_t kMaxDuration = 1ull << 40;
 constexpr uint64_t kMaxRecordsSinceReset = 0xFFFFFFFFull;
+constexpr uint32_t kMaxServices = 4096;    // a link packs the cell in 24 bits: (cell << 40) | d
+constexpr uint32_t kMaxBuckets = 1024;     // partitioned reduce: <= 1024 buckets of <= 1024 cells
 
 // service key: (kind << 30) | id, kind 0 = server side, 1 = client side, 2 = none.
 // atomicMin over fragments picks Span.serviceName's preference (server before client,
@@ -81,6 +83,10 @@ struct JoinArgs {
     // persistent K1 geometry: workgroup w owns traces starting in [w*per_wg, (w+1)*per_wg)
     uint64_t per_wg;
     uint32_t grid;
+    // cell-bucket histogram per K1 workgroup, bucket-major (hist[b * grid + w]); nb = 0 disables it
+    uint32_t* hist;
+    uint32_t nb;
+    uint32_t cb_shift;  // bucket = cell >> cb_shift
 };
 
 // host-side launchers (implemented in the .hip files)
@@ -90,6 +96,23 @@ uint64_t join_tile_records();   // TILE (records per K1 window)
 void join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, uint64_t* link_stride);
 hipError_t launch_link_reduce(const uint64_t* links, const uint32_t* counts, uint64_t stride, uint64_t tiles,
                               uint64_t* table, hipStream_t s);
+// partitioned reduce (no global atomics): hist -> offsets -> bucket-sorted links -> LDS reduce
+struct ReduceArgs {
+    const uint64_t* links;   // per-workgroup lists from K1
+    const uint32_t* counts;
+    uint64_t stride;
+    uint32_t lists;          // K1 grid
+    const uint32_t* hist;    // [nb][lists]
+    uint32_t nb, cb_shift;
+    uint32_t* col_off;       // [nb][lists] exclusive offsets within each bucket
+    uint64_t* bucket_base;   // [nb + 1]
+    uint64_t* sorted;        // links grouped by bucket
+    uint64_t* table;
+    uint64_t cells;
+};
+hipError_t launch_partitioned_reduce(const ReduceArgs& r, hipStream_t s);
+// bucket geometry for S services (nb = 0: use the atomic reduce)
+void bucket_geometry(uint32_t S, uint32_t* nb, uint32_t* cb_shift);
 hipError_t launch_spill(const JoinArgs& a, uint32_t spill_wgs, hipStream_t s);
 uint64_t spill_scratch_bytes_per_wg(uint32_t max_trace);
 hipError_t launch_finalize(const uint64_t* table, uint32_t S, const zk_link_table* out,

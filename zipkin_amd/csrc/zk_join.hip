@@ -261,12 +261,14 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
     __shared__ uint64_t s_mask[NWORD];
     __shared__ uint32_t s_stat[ST_N];
     __shared__ uint32_t s_wsum[WG / 64];
+    __shared__ uint32_t s_hist[kMaxBuckets];  // links per cell bucket (K2's scatter offsets)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t n = a.c.n;
     const uint64_t R0 = (uint64_t)blockIdx.x * a.per_wg;
     if (R0 >= n) {
         if (tid == 0) a.link_count[blockIdx.x] = 0u;
+        for (uint32_t x = tid; x < a.nb; x += WG) a.hist[(uint64_t)x * a.grid + blockIdx.x] = 0u;
         return;
     }
     const uint64_t R1 = (R0 + a.per_wg < n) ? R0 + a.per_wg : n;
@@ -275,6 +277,7 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
     uint64_t nrec = 0;        // records aggregated (uniform)
     StatPack32 st;
     if (tid < ST_N) s_stat[tid] = 0u;
+    for (uint32_t x = tid; x < a.nb; x += WG) s_hist[x] = 0u;
 
     uint64_t ws = R0;         // window start (even)
     uint64_t seek = R0;       // first record that may start one of our traces
@@ -489,6 +492,7 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
             }
             const uint64_t cell = (uint64_t)(sp & kSvcIdMask) * a.S + (sL & kSvcIdMask);
             r_link[e] = (cell << 40) | d;
+            if (a.nb && !a.ablate) atomicAdd(&s_hist[cell >> a.cb_shift], 1u);
             ++nl;
         }
         // ---- 7. append the window's links to this workgroup's list -----------------------------
@@ -525,7 +529,8 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
         a.link_count[blockIdx.x] = nout;
         atomicAdd(&a.stats[(uint64_t)(blockIdx.x % kStatShards) * ST_N + ST_RECORDS], (unsigned long long)nrec);
     }
-    flush_stats32(st, s_stat, a.stats);
+    flush_stats32(st, s_stat, a.stats);  // its barrier also publishes s_hist
+    for (uint32_t x = tid; x < a.nb; x += WG) a.hist[(uint64_t)x * a.grid + blockIdx.x] = s_hist[x];
 }
 
 // =============================================================================================
