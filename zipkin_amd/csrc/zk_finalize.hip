@@ -10,14 +10,14 @@
 //   m2 = (n S2 - S1^2)/n
 //   m3 = (n^2 S3 - 3 n S1 S2 + 2 S1^3)/n^2
 //   m4 = (n^3 S4 - 4 n^2 S1 S3 + 6 n S1^2 S2 - 3 S1^4)/n^3
-// are evaluated in 512-bit integers and divided with one round-to-nearest-even: the result is the
+// are evaluated in 384-bit integers and divided with one round-to-nearest-even: the result is the
 // correctly rounded value of the exact moments, independent of order, GPU count and batching.
 #include "zk_internal.h"
 
 namespace zk {
 namespace {
 
-constexpr int W = 8;  // 512-bit
+constexpr int W = 6;  // 384-bit: every numerator is < 2^300 (n < 2^32, d < 2^40)
 struct U512 {
     uint64_t w[W];
 };
@@ -73,11 +73,12 @@ __device__ __forceinline__ bool u_is_zero(const U512& a) {
 }
 
 // truncated product (inputs are small enough that nothing is lost)
-__device__ U512 u_mul(const U512& a, const U512& b) {
+__device__ __forceinline__ U512 u_mul(const U512& a, const U512& b) {
     U512 r = u_zero();
+#pragma unroll
     for (int i = 0; i < W; ++i) {
-        if (a.w[i] == 0) continue;
         uint64_t carry = 0;
+#pragma unroll
         for (int j = 0; i + j < W; ++j) {
             const unsigned __int128 p =
                 (unsigned __int128)a.w[i] * b.w[j] + r.w[i + j] + carry;
@@ -101,20 +102,29 @@ __device__ __forceinline__ U512 u_mul_small(const U512& a, uint64_t m) {
 }
 
 __device__ __forceinline__ int u_bitlen(const U512& a) {
-    for (int i = W - 1; i >= 0; --i) {
-        if (a.w[i]) return 64 * i + 64 - __clzll((long long)a.w[i]);
-    }
-    return 0;
+    int L = 0;
+#pragma unroll
+    for (int i = 0; i < W; ++i)
+        if (a.w[i]) L = 64 * i + 64 - __clzll((long long)a.w[i]);
+    return L;
 }
 
-__device__ U512 u_shl(const U512& a, int s) {
-    U512 r = u_zero();
+// word shifts select among compile-time variants so the words stay in registers (a runtime
+// word index would put the number in scratch)
+__device__ __forceinline__ U512 u_shl(const U512& a, int s) {
     const int ws = s >> 6, bs = s & 63;
-    for (int i = W - 1; i >= ws; --i) {
-        uint64_t v = a.w[i - ws] << bs;
-        if (bs && i - ws - 1 >= 0) v |= a.w[i - ws - 1] >> (64 - bs);
-        r.w[i] = v;
+    U512 t = u_zero();
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        if (k == ws) {
+#pragma unroll
+            for (int i = 0; i < W; ++i) t.w[i] = i >= k ? a.w[i - k] : 0;
+        }
     }
+    if (!bs) return t;
+    U512 r;
+#pragma unroll
+    for (int i = W - 1; i >= 0; --i) r.w[i] = (t.w[i] << bs) | (i ? t.w[i - 1] >> (64 - bs) : 0);
     return r;
 }
 
@@ -125,35 +135,89 @@ __device__ __forceinline__ void u_shr1(U512& a) {
 }
 
 // sum_k limb[k] * 2^(32k)
-__device__ __forceinline__ U512 from_chunks(const uint64_t* limb, int nchunks) {
+template <int NCHUNKS>
+__device__ __forceinline__ U512 from_chunks(const uint64_t* limb) {
     U512 r = u_zero();
-    for (int k = 0; k < nchunks; ++k) {
+#pragma unroll
+    for (int k = 0; k < NCHUNKS; ++k) {
+        // limb[k] * 2^(32k): word k/2, shifted by 32 if k is odd
         U512 t = u_zero();
-        t.w[0] = limb[k];
-        r = u_add(r, u_shl(t, 32 * k));
+        if (k & 1) {
+            t.w[k / 2] = limb[k] << 32;
+            if (k / 2 + 1 < W) t.w[k / 2 + 1] = limb[k] >> 32;
+        } else {
+            t.w[k / 2] = limb[k];
+        }
+        r = u_add(r, t);
     }
     return r;
 }
 
-// correctly rounded (RNE) value of A / D for A, D > 0
-__device__ double div_round(U512 A, U512 D) {
+__device__ __forceinline__ U512 u_shr(const U512& a, int s) {
+    const int ws = s >> 6, bs = s & 63;
+    U512 t = u_zero();
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        if (k == ws) {
+#pragma unroll
+            for (int i = 0; i < W; ++i) t.w[i] = i + k < W ? a.w[i + k] : 0;
+        }
+    }
+    if (!bs) return t;
+    U512 r;
+#pragma unroll
+    for (int i = 0; i < W; ++i) r.w[i] = (t.w[i] >> bs) | (i + 1 < W ? t.w[i + 1] << (64 - bs) : 0);
+    return r;
+}
+
+// low `s` bits of a are all zero?
+__device__ __forceinline__ bool u_low_zero(const U512& a, int s) {
+    uint64_t o = 0;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        const int rem = s - 64 * i;
+        const uint64_t m = rem >= 64 ? ~0ull : (rem <= 0 ? 0ull : ((1ull << rem) - 1ull));
+        o |= a.w[i] & m;
+    }
+    return o == 0;
+}
+
+__device__ __forceinline__ double u_to_double(const U512& a) {
+    double x = 0.0;
+    for (int i = W - 1; i >= 0; --i) x = x * 18446744073709551616.0 + (double)a.w[i];
+    return x;
+}
+
+// correctly rounded (RNE) value of A / D for A, D > 0.
+// Scale so that Q = floor(A 2^s / D) has 58..59 bits; when s < 0 the low -s bits of A are
+// shifted out and kept as a sticky flag (floor(floor(A/2^k)/D) = floor(A/(2^k D))), so every
+// operand stays below ~2^160. Q is found by double-precision estimates that never overshoot,
+// each followed by an exact remainder update, then the 59-bit Q is rounded to 53 bits.
+__device__ __forceinline__ double div_round(U512 A, const U512& D) {
     if (u_is_zero(A)) return 0.0;
     const int a = u_bitlen(A), b = u_bitlen(D);
-    const int s = 58 - a + b;  // scale so that floor(A 2^s / D) is in [2^57, 2^59)
-    if (s >= 0)
+    const int s = 58 - a + b;  // floor(A 2^s / D) in [2^57, 2^59)
+    bool sticky = false;
+    if (s >= 0) {
         A = u_shl(A, s);
-    else
-        D = u_shl(D, -s);
-    U512 Dsh = u_shl(D, 58);
-    uint64_t q = 0;
-    for (int i = 58; i >= 0; --i) {
-        if (u_cmp(A, Dsh) >= 0) {
-            A = u_sub(A, Dsh);
-            q |= 1ull << i;
-        }
-        u_shr1(Dsh);
+    } else {
+        sticky = !u_low_zero(A, -s);
+        A = u_shr(A, -s);
     }
-    const bool sticky = !u_is_zero(A);
+    const double dd = u_to_double(D);
+    uint64_t q = 0;
+    for (int it = 0; it < 4; ++it) {
+        if (u_cmp(A, D) < 0) break;
+        double t = u_to_double(A) / dd * (1.0 - 0x1p-48);
+        uint64_t ti = t < 1.0 ? 1ull : (uint64_t)t;  // underestimate (>= 1: A >= D)
+        A = u_sub(A, u_mul_small(D, ti));
+        q += ti;
+    }
+    while (u_cmp(A, D) >= 0) {  // at most a couple of steps after the estimates
+        A = u_sub(A, D);
+        ++q;
+    }
+    sticky = sticky || !u_is_zero(A);
     const int L = 64 - __clzll((long long)q);  // 58 or 59
     int r = L - 53;
     uint64_t mant = q >> r;
@@ -167,7 +231,7 @@ __device__ double div_round(U512 A, U512 D) {
     return ldexp((double)mant, r - s);
 }
 
-__device__ double signed_ratio(const U512& P, const U512& Q, const U512& D) {
+__device__ __forceinline__ double signed_ratio(const U512& P, const U512& Q, const U512& D) {
     const int c = u_cmp(P, Q);
     if (c == 0) return 0.0;
     if (c > 0) return div_round(u_sub(P, Q), D);
@@ -190,10 +254,10 @@ __global__ __launch_bounds__(256) void k_finalize(const uint64_t* __restrict__ t
     const uint64_t n = L[kLimbM0];
     double m1 = 0, m2 = 0, m3 = 0, m4 = 0;
     if (n) {
-        const U512 S1 = from_chunks(L + kLimbS1, 2);
-        const U512 S2 = from_chunks(L + kLimbS2, 3);
-        const U512 S3 = from_chunks(L + kLimbS3, 4);
-        const U512 S4 = from_chunks(L + kLimbS4, 5);
+        const U512 S1 = from_chunks<2>(L + kLimbS1);
+        const U512 S2 = from_chunks<3>(L + kLimbS2);
+        const U512 S3 = from_chunks<4>(L + kLimbS3);
+        const U512 S4 = from_chunks<5>(L + kLimbS4);
         U512 N1 = u_zero();
         N1.w[0] = n;
         const U512 N2 = u_mul_small(N1, n);

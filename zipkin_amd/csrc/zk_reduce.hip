@@ -145,41 +145,148 @@ __global__ __launch_bounds__(256) void k_link_scatter(ReduceArgs r) {
     }
 }
 
-template <int CB_SHIFT>
+// Exact sums of one run of durations (<= 4096 links of one cell), kept in registers.
+struct RunSums {
+    uint64_t n, s1;          // s1 < 2^52
+    unsigned __int128 s2;    // < 2^92
+    unsigned __int128 s3;    // low 128 bits of s3 (< 2^132)
+    uint64_t s3h;
+    uint64_t s4[3];          // < 2^172
+    __device__ __forceinline__ void clear() {
+        n = s1 = s3h = 0;
+        s2 = s3 = 0;
+        s4[0] = s4[1] = s4[2] = 0;
+    }
+    __device__ __forceinline__ void add(uint64_t d) {
+        const unsigned __int128 d2 = (unsigned __int128)d * d;  // < 2^80
+        const unsigned __int128 d3 = d2 * d;                    // < 2^120
+        const unsigned __int128 p0 = (unsigned __int128)(uint64_t)d3 * d;
+        const unsigned __int128 p1 = (unsigned __int128)(uint64_t)(d3 >> 64) * d + (uint64_t)(p0 >> 64);
+        ++n;
+        s1 += d;
+        s2 += d2;
+        const unsigned __int128 t3 = s3 + d3;
+        s3h += (t3 < s3);
+        s3 = t3;
+        // s4 += d^4 = p1:lo64(p0)
+        const uint64_t w0 = (uint64_t)p0, w1 = (uint64_t)p1, w2 = (uint64_t)(p1 >> 64);
+        const unsigned __int128 a0 = (unsigned __int128)s4[0] + w0;
+        const unsigned __int128 a1 = (unsigned __int128)s4[1] + w1 + (uint64_t)(a0 >> 64);
+        s4[0] = (uint64_t)a0;
+        s4[1] = (uint64_t)a1;
+        s4[2] += w2 + (uint64_t)(a1 >> 64);
+    }
+    // add the run as 32-bit chunks into the 15 limbs of an LDS cell (the topmost limb of each sum
+    // may receive more than 32 bits: the table only needs value = sum of limb_k * 2^(32k))
+    __device__ __forceinline__ void flush(uint64_t* cell) const {
+        constexpr uint64_t M = 0xFFFFFFFFull;
+        uint64_t v[15];
+        v[0] = n;
+        v[1] = s1 & M;
+        v[2] = s1 >> 32;
+        const uint64_t s2lo = (uint64_t)s2, s2hi = (uint64_t)(s2 >> 64);
+        v[3] = s2lo & M;
+        v[4] = s2lo >> 32;
+        v[5] = s2hi;
+        const uint64_t s3lo = (uint64_t)s3, s3mid = (uint64_t)(s3 >> 64);
+        v[6] = s3lo & M;
+        v[7] = s3lo >> 32;
+        v[8] = s3mid & M;
+        v[9] = (s3mid >> 32) | (s3h << 32);
+        v[10] = s4[0] & M;
+        v[11] = s4[0] >> 32;
+        v[12] = s4[1] & M;
+        v[13] = s4[1] >> 32;
+        v[14] = s4[2];
+#pragma unroll
+        for (int q = 0; q < 15; ++q)
+            if (v[q]) atomicAdd((unsigned long long*)&cell[q], (unsigned long long)v[q]);
+    }
+};
+
+// One cell bucket (<= 1024 cells) per workgroup. Links are processed in chunks of C: counting-sort
+// the chunk by cell in LDS, then every thread sums the runs of its P = C/1024 consecutive sorted
+// links exactly in registers and adds each run once (15 chunk limbs) into the LDS cell. Finally the
+// workgroup adds its cells to the table: plain read-modify-write, it is the cells' only owner.
+template <int CB_SHIFT, int C>
 __global__ __launch_bounds__(1024) void k_bucket_reduce(ReduceArgs r, uint32_t splits) {
     constexpr int CB = 1 << CB_SHIFT;
-    extern __shared__ __attribute__((aligned(16))) uint64_t s_acc[];  // [CB][15]
+    constexpr int P = C / 1024;
+    __shared__ uint32_t s_tmp[32];
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    uint64_t* s_acc = smem;                          // [CB][15]
+    uint64_t* s_sorted = smem + CB * 15;             // [C] (local cell << 40) | d
+    uint32_t* s_hist = (uint32_t*)(s_sorted + C);    // [CB]
+    uint32_t* s_cur = s_hist + CB;                   // [CB]
+    const int tid = threadIdx.x;
     const uint32_t b = blockIdx.x / splits, part = blockIdx.x % splits;
-    for (uint32_t x = threadIdx.x; x < (uint32_t)CB * 15; x += blockDim.x) s_acc[x] = 0;
-    __syncthreads();
+    for (int x = tid; x < CB * 15; x += 1024) s_acc[x] = 0;
+    for (int x = tid; x < CB; x += 1024) s_hist[x] = 0;
     const uint64_t lo = r.bucket_base[b], hi = r.bucket_base[b + 1];
     const uint64_t per = (hi - lo + splits - 1) / splits;
     const uint64_t s0 = lo + per * part;
     const uint64_t s1 = (s0 + per < hi) ? s0 + per : hi;
     const uint64_t cell0 = (uint64_t)b << CB_SHIFT;
-    const int q = threadIdx.x & 15;
-    const uint32_t groups = blockDim.x >> 4;
-    for (uint64_t i = s0 + (threadIdx.x >> 4); i < s1; i += groups) {
-        const uint64_t v = r.sorted[i];
-        const uint32_t cl = (uint32_t)((v >> 40) - cell0);
-        const uint64_t d = v & (kMaxDuration - 1);
-        if (q < 15) {
-            const uint64_t x = limb_value(q, d);
-            if (x) atomicAdd((unsigned long long*)&s_acc[cl * 15 + q], (unsigned long long)x);
-        }
-    }
     __syncthreads();
+    for (uint64_t base = s0; base < s1; base += C) {
+        const int cnt = (int)((s1 - base) < (uint64_t)C ? (s1 - base) : (uint64_t)C);
+        uint64_t v[P];
+        uint32_t cl[P];
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            const int i = tid + k * 1024;
+            v[k] = i < cnt ? r.sorted[base + i] : 0;
+            cl[k] = (uint32_t)((v[k] >> 40) - cell0);
+            if (i < cnt) atomicAdd(&s_hist[cl[k]], 1u);
+        }
+        __syncthreads();
+        {
+            uint32_t tot;
+            const uint32_t h = tid < CB ? s_hist[tid] : 0u;
+            const uint32_t ex = block_excl_scan_1024(h, s_tmp, &tot);
+            if (tid < CB) s_cur[tid] = ex;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            if (tid + k * 1024 < cnt) {
+                const uint32_t pos = atomicAdd(&s_cur[cl[k]], 1u);
+                s_sorted[pos] = ((uint64_t)cl[k] << 40) | (v[k] & (kMaxDuration - 1));
+            }
+        }
+        __syncthreads();
+        RunSums run;
+        run.clear();
+        int cur = -1;
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            const int p = tid * P + k;
+            if (p < cnt) {
+                const uint64_t x = s_sorted[p];
+                const int c = (int)(x >> 40);
+                if (c != cur) {
+                    if (cur >= 0) run.flush(s_acc + cur * 15);
+                    run.clear();
+                    cur = c;
+                }
+                run.add(x & (kMaxDuration - 1));
+            }
+        }
+        if (cur >= 0) run.flush(s_acc + cur * 15);
+        for (int x = tid; x < CB; x += 1024) s_hist[x] = 0;
+        __syncthreads();
+    }
     const uint64_t ncell = (cell0 + CB <= r.cells) ? CB : r.cells - cell0;
-    for (uint32_t x = threadIdx.x; x < ncell * 16; x += blockDim.x) {
-        const uint32_t cl = x >> 4, l = x & 15;
+    for (uint32_t x = tid; x < ncell * 16; x += 1024) {
+        const uint32_t c = x >> 4, l = x & 15;
         if (l == 15) continue;
-        const uint64_t v = s_acc[cl * 15 + l];
-        if (!v) continue;
-        uint64_t* dst = r.table + (cell0 + cl) * kLimbs + l;
+        const uint64_t val = s_acc[c * 15 + l];
+        if (!val) continue;
+        uint64_t* dst = r.table + (cell0 + c) * kLimbs + l;
         if (splits == 1)
-            *dst += v;  // this workgroup owns the cell
+            *dst += val;  // this workgroup owns the cell
         else
-            atomicAdd((unsigned long long*)dst, (unsigned long long)v);
+            atomicAdd((unsigned long long*)dst, (unsigned long long)val);
     }
 }
 
@@ -205,19 +312,18 @@ hipError_t launch_partitioned_reduce(const ReduceArgs& r, hipStream_t s) {
     hipLaunchKernelGGL(k_bucket_base, dim3(1), dim3(1024), 0, s, r.bucket_base, r.nb);
     hipLaunchKernelGGL(k_link_scatter, dim3(r.lists), dim3(256), 0, s, r);
     const uint32_t splits = r.nb >= 256 ? 1u : (512u + r.nb - 1) / r.nb;
-    const size_t lds = (size_t)(1u << r.cb_shift) * 15 * sizeof(uint64_t);
+    constexpr int C9 = 4096, C10 = 2048;
+    const size_t lds9 = (512 * 15 + C9) * 8 + 512 * 8, lds10 = (1024 * 15 + C10) * 8 + 1024 * 8;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_bucket_reduce<9>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)((1u << 9) * 15 * sizeof(uint64_t)));
-        (void)hipFuncSetAttribute((const void*)k_bucket_reduce<10>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)((1u << 10) * 15 * sizeof(uint64_t)));
+        (void)hipFuncSetAttribute((const void*)k_bucket_reduce<9, C9>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds9);
+        (void)hipFuncSetAttribute((const void*)k_bucket_reduce<10, C10>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds10);
         attr_set = true;
     }
     if (r.cb_shift == 9)
-        hipLaunchKernelGGL(k_bucket_reduce<9>, dim3(r.nb * splits), dim3(1024), lds, s, r, splits);
+        hipLaunchKernelGGL((k_bucket_reduce<9, C9>), dim3(r.nb * splits), dim3(1024), lds9, s, r, splits);
     else
-        hipLaunchKernelGGL(k_bucket_reduce<10>, dim3(r.nb * splits), dim3(1024), lds, s, r, splits);
+        hipLaunchKernelGGL((k_bucket_reduce<10, C10>), dim3(r.nb * splits), dim3(1024), lds10, s, r, splits);
     return hipGetLastError();
 }
 
