@@ -166,25 +166,21 @@ __device__ __forceinline__ uint64_t spread32(uint32_t x) {
 }
 
 // two consecutive elements starting at i (i even, columns 16-byte aligned); zeros past `lim`
+// Two consecutive elements starting at i (i even), RAW: elements at or past `lim` are garbage and
+// every consumer masks by record index. Branch-free and unmasked on purpose: a conditional tail
+// load, or a select right after the load, makes the compiler wait (vmcnt) for the load at once,
+// which serialises the column loads and defeats the prefetch. Index i < lim reads the aligned pair
+// at i (columns are 16-B / 8-B aligned, so the pair never crosses a page even when i + 1 == lim);
+// i >= lim reads pair 0.
 __device__ __forceinline__ void ld2_u64(const uint64_t* __restrict__ p, uint64_t i, uint64_t lim, uint64_t v[2]) {
-    if (i + 1 < lim) {
-        const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(p + i);
-        v[0] = x.x;
-        v[1] = x.y;
-    } else {
-        v[0] = i < lim ? p[i] : 0;
-        v[1] = 0;
-    }
+    const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(p + (i < lim ? i : 0));
+    v[0] = x.x;
+    v[1] = x.y;
 }
 __device__ __forceinline__ void ld2_u32(const uint32_t* __restrict__ p, uint64_t i, uint64_t lim, uint32_t v[2]) {
-    if (i + 1 < lim) {
-        const uint2 x = *reinterpret_cast<const uint2*>(p + i);
-        v[0] = x.x;
-        v[1] = x.y;
-    } else {
-        v[0] = i < lim ? p[i] : 0;
-        v[1] = 0;
-    }
+    const uint2 x = *reinterpret_cast<const uint2*>(p + (i < lim ? i : 0));
+    v[0] = x.x;
+    v[1] = x.y;
 }
 
 // per-thread stat counters: 16 x 32-bit fields (flushed once per workgroup)
@@ -227,8 +223,8 @@ __device__ __forceinline__ void load_window(const JoinArgs& a, uint64_t ws, Wind
     ld2_u64((const uint64_t*)a.c.last_ts, i, n, w.last);
     ld2_u32(a.c.service_id, i, n, w.svc);
     ld2_u32(a.c.flags, i, n, w.flags);
-    w.prev = 0;
-    if ((threadIdx.x & 63) == 0 && i > 0 && i - 1 < n) w.prev = a.c.trace_id[i - 1];
+    // traceId before the pair (only lane 0's is used); unconditional for the same reason as ld2
+    w.prev = a.c.trace_id[(i > 0 && i - 1 < n) ? i - 1 : 0];
 }
 
 // =============================================================================================
@@ -351,7 +347,7 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
         }
         if (!done && next_seek >= R1) done = true;
         const uint64_t next_ws = next_seek & ~1ull;
-        if (!done) load_window(a, next_ws, nxt);  // in flight during the LDS phases below
+        load_window(a, done ? ws : next_ws, nxt);  // in flight during the LDS phases below (unconditional: see ld2)
         nrec += (uint64_t)(m - start);
         if (a.ablate != 2) {  // diagnostic: 2 = stream windows only
 
