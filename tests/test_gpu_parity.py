@@ -82,7 +82,8 @@ def test_tracegen_device_equals_host(gpu):
 
 @pytest.mark.parametrize(
     "seed,traces,depth,S",
-    [(1, 10000, 7, 57), (2, 3000, 7, 20), (3, 20000, 6, 500), (4, 200000, 6, 500), (5, 50000, 3, 1)],
+    [(1, 10000, 7, 57), (2, 3000, 7, 20), (3, 20000, 6, 500), (4, 200000, 6, 500), (5, 50000, 3, 1),
+     (6, 30000, 6, 1000), (7, 20000, 6, 1500)],
 )
 def test_parity_tracegen(gpu, seed, traces, depth, S):
     cols = tracegen_host(seed, traces, max_depth=depth, num_services=S)

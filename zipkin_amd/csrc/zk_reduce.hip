@@ -55,8 +55,8 @@ __global__ __launch_bounds__(256) void k_link_reduce_atomic(const uint64_t* __re
 // one owner, so no global atomic is issued (when a bucket is split over several workgroups for
 // parallelism, the few flush adds are atomic).
 
-__device__ __forceinline__ uint32_t block_excl_scan_1024(uint32_t v, uint32_t* s_tmp, uint32_t* total) {
-    // blockDim.x == 1024 (16 waves)
+template <int NW>  // waves per block (blockDim.x == 64 * NW, NW <= 16)
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_tmp, uint32_t* total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t incl = v;
 #pragma unroll
@@ -67,16 +67,16 @@ __device__ __forceinline__ uint32_t block_excl_scan_1024(uint32_t v, uint32_t* s
     if (lane == 63) s_tmp[wave] = incl;
     __syncthreads();
     if (wave == 0) {
-        uint32_t w = lane < 16 ? s_tmp[lane] : 0u;
+        uint32_t w = lane < NW ? s_tmp[lane] : 0u;
 #pragma unroll
-        for (int off = 1; off < 16; off <<= 1) {
+        for (int off = 1; off < NW; off <<= 1) {
             const uint32_t o = __shfl_up(w, off);
             if (lane >= off) w += o;
         }
-        if (lane < 16) s_tmp[16 + lane] = w;  // inclusive wave totals
+        if (lane < NW) s_tmp[16 + lane] = w;  // inclusive wave totals
     }
     __syncthreads();
-    *total = s_tmp[16 + 15];
+    *total = s_tmp[16 + NW - 1];
     return (wave ? s_tmp[16 + wave - 1] : 0u) + incl - v;
 }
 
@@ -89,7 +89,7 @@ __global__ __launch_bounds__(1024) void k_bucket_colscan(const uint32_t* __restr
         const uint32_t w = base + threadIdx.x;
         const uint32_t v = w < lists ? hist[(uint64_t)b * lists + w] : 0u;
         uint32_t tot;
-        const uint32_t ex = block_excl_scan_1024(v, s_tmp, &tot);
+        const uint32_t ex = block_excl_scan<16>(v, s_tmp, &tot);
         if (w < lists) col_off[(uint64_t)b * lists + w] = (uint32_t)carry + ex;
         carry += tot;
         __syncthreads();
@@ -103,13 +103,14 @@ __global__ __launch_bounds__(1024) void k_bucket_base(uint64_t* __restrict__ bas
     const uint32_t b = threadIdx.x;
     const uint32_t v = b < nb ? (uint32_t)base[b] : 0u;
     uint32_t tot;
-    const uint32_t ex = block_excl_scan_1024(v, s_tmp, &tot);
+    const uint32_t ex = block_excl_scan<16>(v, s_tmp, &tot);
     __syncthreads();
     if (b < nb) base[b] = ex;
     if (b == 0) base[nb] = tot;
 }
 
 __global__ __launch_bounds__(256) void k_link_scatter(ReduceArgs r) {
+    constexpr int U = 8;  // links per thread in flight
     __shared__ uint32_t s_cur[kMaxBuckets];
     const uint32_t w = blockIdx.x;
     for (uint32_t b = threadIdx.x; b < r.nb; b += 256)
@@ -118,29 +119,44 @@ __global__ __launch_bounds__(256) void k_link_scatter(ReduceArgs r) {
     const uint32_t c = r.counts[w];
     const uint64_t* __restrict__ L = r.links + (uint64_t)w * r.stride;
     const int lane = threadIdx.x & 63;
-    for (uint32_t base = 0; base < c; base += 256) {
-        const uint32_t i = base + threadIdx.x;
-        const bool in = i < c;
-        const uint64_t v = in ? L[i] : 0;
-        const uint32_t b = (uint32_t)((v >> 40) >> r.cb_shift);
+    for (uint32_t base = 0; base < c; base += 256 * U) {
+        uint64_t v[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const uint32_t i = base + threadIdx.x + 256 * k;
+            v[k] = L[i < c ? i : 0];  // branch-free: all U loads in flight together
+        }
         if (r.nb <= 32) {
-            // few buckets: aggregate the wave's lanes per bucket before touching the LDS cursor
-            uint64_t todo = __ballot(in);
-            while (todo) {
-                const int l0 = __ffsll((unsigned long long)todo) - 1;
-                const uint32_t b0 = __shfl(b, l0);
-                const uint64_t same = __ballot(in && b == b0) & todo;
-                uint32_t basepos = 0;
-                if (lane == l0) basepos = atomicAdd(&s_cur[b0], (uint32_t)__popcll(same));
-                basepos = __shfl(basepos, l0);
-                if ((same >> lane) & 1ull) {
-                    const uint32_t rank = (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
-                    r.sorted[basepos + rank] = v;
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const bool in = base + threadIdx.x + 256 * k < c;
+                const uint32_t b = (uint32_t)((v[k] >> 40) >> r.cb_shift);
+                // few buckets: aggregate the wave's lanes per bucket before touching the LDS cursor
+                uint64_t todo = __ballot(in);
+                while (todo) {
+                    const int l0 = __ffsll((unsigned long long)todo) - 1;
+                    const uint32_t b0 = __shfl(b, l0);
+                    const uint64_t same = __ballot(in && b == b0) & todo;
+                    uint32_t basepos = 0;
+                    if (lane == l0) basepos = atomicAdd(&s_cur[b0], (uint32_t)__popcll(same));
+                    basepos = __shfl(basepos, l0);
+                    if ((same >> lane) & 1ull) {
+                        const uint32_t rank = (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+                        r.sorted[basepos + rank] = v[k];
+                    }
+                    todo &= ~same;
                 }
-                todo &= ~same;
             }
-        } else if (in) {
-            r.sorted[atomicAdd(&s_cur[b], 1u)] = v;
+        } else {
+            uint32_t pos[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const bool in = base + threadIdx.x + 256 * k < c;
+                pos[k] = in ? atomicAdd(&s_cur[(uint32_t)((v[k] >> 40) >> r.cb_shift)], 1u) : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+                if (base + threadIdx.x + 256 * k < c) r.sorted[pos[k]] = v[k];
         }
     }
 }
@@ -208,10 +224,11 @@ struct RunSums {
 // the chunk by cell in LDS, then every thread sums the runs of its P = C/1024 consecutive sorted
 // links exactly in registers and adds each run once (15 chunk limbs) into the LDS cell. Finally the
 // workgroup adds its cells to the table: plain read-modify-write, it is the cells' only owner.
-template <int CB_SHIFT, int C>
-__global__ __launch_bounds__(1024) void k_bucket_reduce(ReduceArgs r, uint32_t splits) {
+template <int CB_SHIFT, int C, int WG>
+__global__ __launch_bounds__(WG) void k_bucket_reduce(ReduceArgs r, uint32_t splits) {
     constexpr int CB = 1 << CB_SHIFT;
-    constexpr int P = C / 1024;
+    constexpr int P = C / WG;
+    static_assert(P * WG == C && CB <= 2 * WG, "geometry");
     __shared__ uint32_t s_tmp[32];
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     uint64_t* s_acc = smem;                          // [CB][15]
@@ -220,8 +237,8 @@ __global__ __launch_bounds__(1024) void k_bucket_reduce(ReduceArgs r, uint32_t s
     uint32_t* s_cur = s_hist + CB;                   // [CB]
     const int tid = threadIdx.x;
     const uint32_t b = blockIdx.x / splits, part = blockIdx.x % splits;
-    for (int x = tid; x < CB * 15; x += 1024) s_acc[x] = 0;
-    for (int x = tid; x < CB; x += 1024) s_hist[x] = 0;
+    for (int x = tid; x < CB * 15; x += WG) s_acc[x] = 0;
+    for (int x = tid; x < CB; x += WG) s_hist[x] = 0;
     const uint64_t lo = r.bucket_base[b], hi = r.bucket_base[b + 1];
     const uint64_t per = (hi - lo + splits - 1) / splits;
     const uint64_t s0 = lo + per * part;
@@ -234,22 +251,38 @@ __global__ __launch_bounds__(1024) void k_bucket_reduce(ReduceArgs r, uint32_t s
         uint32_t cl[P];
 #pragma unroll
         for (int k = 0; k < P; ++k) {
-            const int i = tid + k * 1024;
-            v[k] = i < cnt ? r.sorted[base + i] : 0;
+            const int i = tid + k * WG;
+            v[k] = r.sorted[base + (i < cnt ? i : 0)];  // branch-free: P loads in flight
+        }
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
             cl[k] = (uint32_t)((v[k] >> 40) - cell0);
-            if (i < cnt) atomicAdd(&s_hist[cl[k]], 1u);
+            if (tid + k * WG < cnt) atomicAdd(&s_hist[cl[k]], 1u);
         }
         __syncthreads();
         {
+            // CB <= 2 WG bins: thread t owns the BPT consecutive bins [t*BPT, t*BPT + BPT)
+            constexpr int BPT = (CB + WG - 1) / WG;
+            uint32_t h[BPT], sum = 0;
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) {
+                const int bin = tid * BPT + q;
+                h[q] = bin < CB ? s_hist[bin] : 0u;
+                sum += h[q];
+            }
             uint32_t tot;
-            const uint32_t h = tid < CB ? s_hist[tid] : 0u;
-            const uint32_t ex = block_excl_scan_1024(h, s_tmp, &tot);
-            if (tid < CB) s_cur[tid] = ex;
+            uint32_t ex = block_excl_scan<WG / 64>(sum, s_tmp, &tot);
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) {
+                const int bin = tid * BPT + q;
+                if (bin < CB) s_cur[bin] = ex;
+                ex += h[q];
+            }
         }
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < P; ++k) {
-            if (tid + k * 1024 < cnt) {
+            if (tid + k * WG < cnt) {
                 const uint32_t pos = atomicAdd(&s_cur[cl[k]], 1u);
                 s_sorted[pos] = ((uint64_t)cl[k] << 40) | (v[k] & (kMaxDuration - 1));
             }
@@ -273,11 +306,11 @@ __global__ __launch_bounds__(1024) void k_bucket_reduce(ReduceArgs r, uint32_t s
             }
         }
         if (cur >= 0) run.flush(s_acc + cur * 15);
-        for (int x = tid; x < CB; x += 1024) s_hist[x] = 0;
+        for (int x = tid; x < CB; x += WG) s_hist[x] = 0;
         __syncthreads();
     }
     const uint64_t ncell = (cell0 + CB <= r.cells) ? CB : r.cells - cell0;
-    for (uint32_t x = tid; x < ncell * 16; x += 1024) {
+    for (uint32_t x = tid; x < ncell * 16; x += WG) {
         const uint32_t c = x >> 4, l = x & 15;
         if (l == 15) continue;
         const uint64_t val = s_acc[c * 15 + l];
@@ -312,18 +345,22 @@ hipError_t launch_partitioned_reduce(const ReduceArgs& r, hipStream_t s) {
     hipLaunchKernelGGL(k_bucket_base, dim3(1), dim3(1024), 0, s, r.bucket_base, r.nb);
     hipLaunchKernelGGL(k_link_scatter, dim3(r.lists), dim3(256), 0, s, r);
     const uint32_t splits = r.nb >= 256 ? 1u : (512u + r.nb - 1) / r.nb;
-    constexpr int C9 = 4096, C10 = 2048;
+    // CB = 512: 512 threads, 1536-link chunks -> 77.8 KB LDS, two workgroups per CU
+    // CB = 1024: 1024 threads, 2048-link chunks -> 147 KB LDS, one workgroup per CU
+    constexpr int C9 = 1536, C10 = 2048;
     const size_t lds9 = (512 * 15 + C9) * 8 + 512 * 8, lds10 = (1024 * 15 + C10) * 8 + 1024 * 8;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_bucket_reduce<9, C9>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds9);
-        (void)hipFuncSetAttribute((const void*)k_bucket_reduce<10, C10>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds10);
+        (void)hipFuncSetAttribute((const void*)k_bucket_reduce<9, C9, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds9);
+        (void)hipFuncSetAttribute((const void*)k_bucket_reduce<10, C10, 1024>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds10);
         attr_set = true;
     }
     if (r.cb_shift == 9)
-        hipLaunchKernelGGL((k_bucket_reduce<9, C9>), dim3(r.nb * splits), dim3(1024), lds9, s, r, splits);
+        hipLaunchKernelGGL((k_bucket_reduce<9, C9, 512>), dim3(r.nb * splits), dim3(512), lds9, s, r, splits);
     else
-        hipLaunchKernelGGL((k_bucket_reduce<10, C10>), dim3(r.nb * splits), dim3(1024), lds10, s, r, splits);
+        hipLaunchKernelGGL((k_bucket_reduce<10, C10, 1024>), dim3(r.nb * splits), dim3(1024), lds10, s, r, splits);
     return hipGetLastError();
 }
 
