@@ -119,12 +119,21 @@ __global__ __launch_bounds__(256) void k_link_scatter(ReduceArgs r) {
     const uint32_t c = r.counts[w];
     const uint64_t* __restrict__ L = r.links + (uint64_t)w * r.stride;
     const int lane = threadIdx.x & 63;
+    // loads run one iteration ahead of the stores: a wave's vmcnt counts loads and stores in
+    // issue order, so waiting for loads issued after the stores would also wait for the stores
+    uint64_t nxt[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        const uint32_t i = threadIdx.x + 256 * k;
+        nxt[k] = L[i < c ? i : 0];
+    }
     for (uint32_t base = 0; base < c; base += 256 * U) {
         uint64_t v[U];
 #pragma unroll
         for (int k = 0; k < U; ++k) {
-            const uint32_t i = base + threadIdx.x + 256 * k;
-            v[k] = L[i < c ? i : 0];  // branch-free: all U loads in flight together
+            v[k] = nxt[k];
+            const uint32_t i = base + 256 * U + threadIdx.x + 256 * k;
+            nxt[k] = L[i < c ? i : 0];  // branch-free: all U loads in flight together
         }
         if (r.nb <= 32) {
 #pragma unroll
@@ -245,14 +254,21 @@ __global__ __launch_bounds__(WG) void k_bucket_reduce(ReduceArgs r, uint32_t spl
     const uint64_t s1 = (s0 + per < hi) ? s0 + per : hi;
     const uint64_t cell0 = (uint64_t)b << CB_SHIFT;
     __syncthreads();
+    uint64_t nxt[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        const uint64_t i = s0 + tid + k * WG;
+        nxt[k] = r.sorted[i < s1 ? i : 0];
+    }
     for (uint64_t base = s0; base < s1; base += C) {
         const int cnt = (int)((s1 - base) < (uint64_t)C ? (s1 - base) : (uint64_t)C);
         uint64_t v[P];
         uint32_t cl[P];
 #pragma unroll
         for (int k = 0; k < P; ++k) {
-            const int i = tid + k * WG;
-            v[k] = r.sorted[base + (i < cnt ? i : 0)];  // branch-free: P loads in flight
+            v[k] = nxt[k];
+            const uint64_t i = base + C + tid + k * WG;
+            nxt[k] = r.sorted[i < s1 ? i : 0];  // next chunk in flight during this one
         }
 #pragma unroll
         for (int k = 0; k < P; ++k) {
