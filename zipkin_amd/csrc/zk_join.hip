@@ -453,7 +453,8 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
             atomicMin(&s_svck[tgt], nl ? svck[e] : kSvcNone);
             atomicMin((unsigned long long*)&s_pid[tgt],
                       (unsigned long long)((nl && (f & ZK_F_HAS_PARENT)) ? cur.pid[e] : ~0ull));
-            const uint32_t hs = nl ? slot_of[e] : DUMMY;
+            // lanes with nothing to fold OR zero into a slot of their own (no same-address pile-up)
+            const uint32_t hs = nl ? slot_of[e] : (in[e] ? slot_of[e] : (uint32_t)((jj + e) & (H - 1)));
             const uint32_t old = atomicOr(&s_ht[hs], nl ? bits[e] : 0u);
             const uint32_t promote = nl ? (once[e] & (old >> kSlotA) & 0xFu) : 0u;  // second occurrence
             atomicOr(&s_ht[hs], promote << kSlotB);
@@ -532,7 +533,9 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
             st.add(ST_JOINED, pok);
             st.add(ST_NO_SERVICE, nosvc);
             st.add(ST_DUR_RANGE, dbad);
-            atomicAdd(&s_hist[(has && a.nb) ? (uint32_t)(cell >> a.cb_shift) : kMaxBuckets], 1u);
+            // lanes without a link add 0 to a bin of their own (no same-address pile-up)
+            atomicAdd(&s_hist[(has && a.nb) ? (uint32_t)(cell >> a.cb_shift) : (uint32_t)(j & (kMaxBuckets - 1))],
+                      has ? 1u : 0u);
         }
         // ---- 7. append the window's links to this workgroup's list -----------------------------
         uint32_t incl = nl;
