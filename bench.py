@@ -164,7 +164,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_span_join_tile",
+                "kernel": "k_span_join_stream",
                 "achieved": achieved,
                 "peak": PEAK_HBM_GBS,
                 "unit": "GB/s",

@@ -183,27 +183,20 @@ __device__ __forceinline__ void ld2_u32(const uint32_t* __restrict__ p, uint64_t
     v[1] = x.y;
 }
 
-// per-thread stat counters: 16-bit fields, two per u32 (a lane adds at most 2 per window, and a
-// workgroup streams < 2^32 / 1024 records, so a field stays below 2^15)
-struct StatPack16 {
-    uint32_t w[7] = {0, 0, 0, 0, 0, 0, 0};
-    __device__ __forceinline__ void add(int s, bool c) { w[s >> 1] += (c ? 1u : 0u) << (16 * (s & 1)); }
+// per-thread stat counters: 16 x 32-bit fields (flushed once per workgroup)
+struct StatPack32 {
+    uint64_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    __device__ __forceinline__ void inc(int s) { w[s >> 1] += 1ull << (32 * (s & 1)); }
 };
 
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    return v;
-}
-
-__device__ __forceinline__ void flush_stats16(const StatPack16& sp, uint32_t* s_stat, unsigned long long* g_stats) {
+__device__ __forceinline__ void flush_stats32(StatPack32& sp, uint32_t* s_stat, unsigned long long* g_stats) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int i = 0; i < 7; ++i) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t v = wave_sum_u32((sp.w[i] >> (16 * h)) & 0xFFFFu);
-            if (lane == 0 && v) atomicAdd(&s_stat[2 * i + h], v);
+    for (int i = 0; i < 8; ++i) {
+        const uint64_t v = wave_sum_u64(sp.w[i]);
+        if (lane == 0 && v) {
+            if ((uint32_t)v) atomicAdd(&s_stat[2 * i], (uint32_t)v);
+            if ((uint32_t)(v >> 32)) atomicAdd(&s_stat[2 * i + 1], (uint32_t)(v >> 32));
         }
     }
     __syncthreads();
@@ -243,12 +236,7 @@ __device__ __forceinline__ void load_window(const JoinArgs& a, uint64_t ws, Wind
 // merged, validated and joined in LDS; the incomplete last trace starts the next window (its
 // records are re-read, mostly from L2). The next window's columns are prefetched into registers
 // right after its start is known, so HBM streams while the LDS phases run. A trace longer than a
-// window goes to the spill kernel. Four workgroups per CU (24 KB LDS, <= 128 VGPRs).
-//
-// The per-record code is written branch-free wherever possible (pair stores into LDS, merges as
-// unconditional atomics with neutral values, one insert loop and one probe loop covering both of
-// a thread's records): divergent ifs cost exec-mask bookkeeping that dominated the instruction
-// stream (profiles/pmc_r01_v5).
+// window goes to the spill kernel. Three workgroups per CU (23 KB LDS, <= 168 VGPRs).
 //
 // Hash slot word (u32): bits 0..10 leader index + 1; bits 12..15 "seen >= 1" and 16..19
 // "seen >= 2" for cs, cr, sr, ss (Span.isValid = no ">= 2" bit); bit 20 some fragment has a
@@ -258,23 +246,20 @@ template <int TILE, int WG>
 __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
     constexpr int H = 2 * TILE;
     constexpr int NWORD = TILE / 64;
-    constexpr uint32_t DUMMY = H;  // hash slot written by lanes with nothing to merge
-    static_assert(TILE == 2 * WG && TILE <= 2047 && H == 4 * WG, "two records per thread");
-    __shared__ __attribute__((aligned(16))) uint64_t s_sid[TILE];
-    __shared__ __attribute__((aligned(16))) long long s_first[TILE];
-    __shared__ __attribute__((aligned(16))) long long s_last[TILE];
-    __shared__ __attribute__((aligned(16))) uint64_t s_pid[TILE];
-    __shared__ __attribute__((aligned(16))) uint32_t s_ht[H + 4];
-    __shared__ __attribute__((aligned(16))) uint32_t s_svck[TILE];
-    __shared__ __attribute__((aligned(16))) uint32_t s_seg2[WG];  // seg of records 2t | 2t+1 << 16
+    static_assert(TILE == 2 * WG && TILE <= 2047, "two records per thread");
+    __shared__ uint64_t s_sid[TILE];
+    __shared__ long long s_first[TILE];
+    __shared__ long long s_last[TILE];
+    __shared__ uint64_t s_pid[TILE];
+    __shared__ uint32_t s_svck[TILE];
+    __shared__ uint16_t s_seg[TILE];
+    __shared__ uint32_t s_ht[H];
     __shared__ uint64_t s_mask[NWORD];
     __shared__ uint32_t s_stat[ST_N];
     __shared__ uint32_t s_wsum[WG / 64];
-    __shared__ uint32_t s_hist[kMaxBuckets + 1];  // + a dummy bin for lanes without a link
-    const uint16_t* s_seg = reinterpret_cast<const uint16_t*>(s_seg2);
+    __shared__ uint32_t s_hist[kMaxBuckets];  // links per cell bucket (K2's scatter offsets)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int jj = 2 * tid;  // local index of this thread's first record
     const uint64_t n = a.c.n;
     const uint64_t R0 = (uint64_t)blockIdx.x * a.per_wg;
     if (R0 >= n) {
@@ -284,46 +269,42 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
     }
     const uint64_t R1 = (R0 + a.per_wg < n) ? R0 + a.per_wg : n;
     uint64_t* __restrict__ out = a.links + (uint64_t)blockIdx.x * a.link_stride;
-    uint32_t nout = 0;  // links written by this workgroup (uniform)
-    uint64_t nrec = 0;  // records aggregated (uniform)
-    StatPack16 st;
+    uint32_t nout = 0;        // links written by this workgroup (uniform)
+    uint64_t nrec = 0;        // records aggregated (uniform)
+    StatPack32 st;
     if (tid < ST_N) s_stat[tid] = 0u;
-    if (tid < 4) s_ht[H + tid] = 0u;  // dummy slots (never cleared per window, only OR-ed with 0)
-    for (uint32_t x = tid; x <= kMaxBuckets; x += WG) s_hist[x] = 0u;
+    for (uint32_t x = tid; x < a.nb; x += WG) s_hist[x] = 0u;
 
-    uint64_t ws = R0;    // window start (even)
-    uint64_t seek = R0;  // first record that may start one of our traces
+    uint64_t ws = R0;         // window start (even)
+    uint64_t seek = R0;       // first record that may start one of our traces
     Window cur, nxt;
     load_window(a, ws, cur);
     for (;;) {
         const int wn = (int)((n - ws) < (uint64_t)TILE ? (n - ws) : (uint64_t)TILE);
         // ---- 1. trace boundaries of the window -------------------------------------------------
-        uint64_t wlo, whi;  // this wave's two mask words (uniform)
         {
             uint64_t prev = __shfl_up(cur.tid[1], 1);
-            if (lane == 0) prev = (ws + jj > 0) ? cur.prev : ~cur.tid[0];
-            const bool b0 = (jj < wn) && cur.tid[0] != prev;
-            const bool b1 = (jj + 1 < wn) && cur.tid[1] != cur.tid[0];
+            if (lane == 0) prev = (ws + 2 * tid > 0) ? cur.prev : ~cur.tid[0];
+            const bool b0 = (2 * tid < wn) && cur.tid[0] != prev;
+            const bool b1 = (2 * tid + 1 < wn) && cur.tid[1] != cur.tid[0];
             const uint64_t m0 = __ballot(b0), m1 = __ballot(b1);
-            wlo = spread32((uint32_t)m0) | (spread32((uint32_t)m1) << 1);
-            whi = spread32((uint32_t)(m0 >> 32)) | (spread32((uint32_t)(m1 >> 32)) << 1);
             if (lane == 0) {
-                s_mask[2 * wave] = wlo;
-                s_mask[2 * wave + 1] = whi;
+                s_mask[2 * wave] = spread32((uint32_t)m0) | (spread32((uint32_t)m1) << 1);
+                s_mask[2 * wave + 1] = spread32((uint32_t)(m0 >> 32)) | (spread32((uint32_t)(m1 >> 32)) << 1);
             }
         }
         __syncthreads();
         // ---- 2. which records are ours, where the next window starts (uniform) ----------------
         const int lo_j = (int)(seek - ws);
         const int r1_j = (R1 - ws < (uint64_t)wn) ? (int)(R1 - ws) : wn;
-        int start = -1, stop = -1, last_b = -1, cin = -1;  // cin: last boundary before this wave
+        int start = -1, stop = -1, last_b = -1;
 #pragma unroll
         for (int w = 0; w < NWORD; ++w) {
             const uint64_t x = s_mask[w];
             if (!x) continue;
+            last_b = 64 * w + 63 - (int)__clzll((long long)x);
+            // first boundary >= lo_j and first boundary >= r1_j
             const int base = 64 * w;
-            last_b = base + 63 - (int)__clzll((long long)x);
-            if (w < 2 * wave) cin = last_b;
             if (start < 0 && base + 63 >= lo_j) {
                 const uint64_t y = lo_j > base ? (x & (~0ull << (lo_j - base))) : x;
                 if (y) start = base + (int)__ffsll((unsigned long long)y) - 1;
@@ -334,11 +315,12 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
             }
         }
         const bool at_end = ws + (uint64_t)wn >= n;
-        int m;  // records [start, m) are processed in this window
+        int m;                  // records [start, m) are processed in this window
         bool done = false;
         uint64_t next_seek = 0;
         if (start < 0 || (stop >= 0 && stop <= start)) {
-            done = (start >= 0) || at_end || ws + (uint64_t)TILE >= R1;  // nothing of ours here
+            // no trace of ours starts in the rest of this window
+            done = (start >= 0) || at_end || ws + (uint64_t)TILE >= R1;
             next_seek = ws + (uint64_t)TILE;
             start = m = 0;
         } else if (stop >= 0) {
@@ -365,177 +347,149 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
         }
         if (!done && next_seek >= R1) done = true;
         const uint64_t next_ws = next_seek & ~1ull;
-        load_window(a, done ? ws : next_ws, nxt);  // in flight during the LDS phases (unconditional: see ld2)
+        load_window(a, done ? ws : next_ws, nxt);  // in flight during the LDS phases below (unconditional: see ld2)
         nrec += (uint64_t)(m - start);
+        if (a.ablate != 2) {  // diagnostic: 2 = stream windows only
 
-        // ---- 3. segment ids (from this wave's mask words) and LDS staging ---------------------
-        bool in[2], rerr[2];
-        int seg[2];
-        uint32_t svck[2], bits[2], once[2];
-        {
-            const uint64_t myword = lane < 32 ? wlo : whi;
-            int pre = cin;
-            if (lane >= 32 && wlo) pre = 64 * (2 * wave) + 63 - (int)__clzll((long long)wlo);
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const int j = jj + e;
-                const uint64_t b = myword & ((2ull << (j & 63)) - 1ull);
-                seg[e] = b ? (j & ~63) + 63 - (int)__clzll((long long)b) : pre;
-                in[e] = j >= start && j < m;
-                rerr[e] = false;
-                svck[e] = svc_key(cur.flags[e], cur.svc[e], a.S, &rerr[e]);
-                bits[e] = frag_bits(cur.flags[e], &once[e]);
-            }
-            // pair stores (records outside [start, m) are written too: nothing ever reads them)
-            const bool ha0 = (cur.flags[0] & ZK_F_HAS_ANNOTATIONS) != 0;
-            const bool ha1 = (cur.flags[1] & ZK_F_HAS_ANNOTATIONS) != 0;
-            *reinterpret_cast<ulonglong2*>(&s_sid[jj]) = make_ulonglong2(cur.sid[0], cur.sid[1]);
-            *reinterpret_cast<longlong2*>(&s_first[jj]) =
-                make_longlong2(ha0 ? (long long)cur.first[0] : LLONG_MAX, ha1 ? (long long)cur.first[1] : LLONG_MAX);
-            *reinterpret_cast<longlong2*>(&s_last[jj]) =
-                make_longlong2(ha0 ? (long long)cur.last[0] : LLONG_MIN, ha1 ? (long long)cur.last[1] : LLONG_MIN);
-            *reinterpret_cast<ulonglong2*>(&s_pid[jj]) =
-                make_ulonglong2((cur.flags[0] & ZK_F_HAS_PARENT) ? cur.pid[0] : ~0ull,
-                                (cur.flags[1] & ZK_F_HAS_PARENT) ? cur.pid[1] : ~0ull);
-            *reinterpret_cast<uint2*>(&s_svck[jj]) = make_uint2(svck[0], svck[1]);
-            s_seg2[tid] = (uint32_t)(seg[0] & 0xFFFF) | ((uint32_t)(seg[1] & 0xFFFF) << 16);
-            *reinterpret_cast<uint4*>(&s_ht[4 * tid]) = make_uint4(0u, 0u, 0u, 0u);
-        }
-        __syncthreads();
-
-        // ---- 4. groupBy((id, traceId)): one insert loop for both records ------------------------
-        int lead[2] = {-1, -1};
-        uint32_t slot_of[2] = {DUMMY, DUMMY};
-        {
-            int e = in[0] ? 0 : (in[1] ? 1 : 2);
-            uint64_t key = e == 0 ? cur.sid[0] : cur.sid[1];
-            uint32_t sg = (uint32_t)(e == 0 ? seg[0] : seg[1]);
-            uint32_t mine = (uint32_t)(jj + (e == 0 ? 0 : 1) + 1) | (e == 0 ? bits[0] : bits[1]);
-            uint32_t slot = slot_hash(key, sg) & (H - 1);
-            while (e < 2) {
-                const uint32_t old = atomicCAS(&s_ht[slot], 0u, mine);
-                int found = -1;
-                if (old == 0u) {
-                    found = jj + e;
-                } else {
-                    const int o = (int)(old & kSlotIdx) - 1;
-                    if (s_sid[o] == key && s_seg[o] == sg) found = o;
-                }
-                if (found >= 0) {
-                    if (e == 0) {
-                        lead[0] = found;
-                        slot_of[0] = slot;
-                    } else {
-                        lead[1] = found;
-                        slot_of[1] = slot;
-                    }
-                    e = (e == 0 && in[1]) ? 1 : 2;
-                    key = cur.sid[1];
-                    sg = (uint32_t)seg[1];
-                    mine = (uint32_t)(jj + 2) | bits[1];
-                    slot = slot_hash(key, sg) & (H - 1);
-                } else {
-                    slot = (slot + 1) & (H - 1);
-                }
-            }
-        }
-        __syncthreads();
-
-        // ---- 5. reduce(mergeSpan): unconditional atomics, neutral for leaders / other records --
+        // ---- 3. segment ids and LDS staging ----------------------------------------------------
+        int r_seg[2];
+        uint32_t r_svck[2];
+        bool r_rerr[2];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-            const bool nl = lead[e] >= 0 && lead[e] != jj + e;  // fragment to fold into its leader
-            const int tgt = nl ? lead[e] : jj + e;
-            const uint32_t f = cur.flags[e];
-            const bool ha = nl && (f & ZK_F_HAS_ANNOTATIONS);
-            atomicMin(&s_first[tgt], ha ? (long long)cur.first[e] : LLONG_MAX);
-            atomicMax(&s_last[tgt], ha ? (long long)cur.last[e] : LLONG_MIN);
-            atomicMin(&s_svck[tgt], nl ? svck[e] : kSvcNone);
-            atomicMin((unsigned long long*)&s_pid[tgt],
-                      (unsigned long long)((nl && (f & ZK_F_HAS_PARENT)) ? cur.pid[e] : ~0ull));
-            // lanes with nothing to fold OR zero into a slot of their own (no same-address pile-up)
-            const uint32_t hs = nl ? slot_of[e] : (in[e] ? slot_of[e] : (uint32_t)((jj + e) & (H - 1)));
-            const uint32_t old = atomicOr(&s_ht[hs], nl ? bits[e] : 0u);
-            const uint32_t promote = nl ? (once[e] & (old >> kSlotA) & 0xFu) : 0u;  // second occurrence
-            atomicOr(&s_ht[hs], promote << kSlotB);
+            const int j = 2 * tid + e;
+            r_rerr[e] = false;
+            r_svck[e] = svc_key(cur.flags[e], cur.svc[e], a.S, &r_rerr[e]);
+            r_seg[e] = -1;
+            if (j >= start && j < m) {
+                int w = j >> 6;
+                uint64_t bits = s_mask[w] & ((2ull << (j & 63)) - 1ull);
+                while (!bits) bits = s_mask[--w];  // start is a boundary, so this terminates
+                const int seg = 64 * w + 63 - (int)__clzll((long long)bits);
+                r_seg[e] = seg;
+                const uint32_t f = cur.flags[e];
+                const bool ha = (f & ZK_F_HAS_ANNOTATIONS) != 0;
+                s_sid[j] = cur.sid[e];
+                s_seg[j] = (uint16_t)seg;
+                s_first[j] = ha ? (long long)cur.first[e] : LLONG_MAX;
+                s_last[j] = ha ? (long long)cur.last[e] : LLONG_MIN;
+                s_pid[j] = (f & ZK_F_HAS_PARENT) ? cur.pid[e] : ~0ull;
+                s_svck[j] = r_svck[e];
+            }
+        }
+        for (int x = tid; x < H; x += WG) s_ht[x] = 0u;
+        __syncthreads();
+
+        // ---- 4. groupBy((id, traceId)): the first fragment to claim a slot leads --------------
+        int r_leader[2];
+        uint32_t r_slot[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            r_leader[e] = -1;
+            r_slot[e] = 0;
+            if (r_seg[e] >= 0) {
+                const int j = 2 * tid + e;
+                const uint64_t sid = cur.sid[e];
+                const uint16_t seg = (uint16_t)r_seg[e];
+                uint32_t once;
+                const uint32_t bits = frag_bits(cur.flags[e], &once);
+                uint32_t slot = slot_hash(sid, seg) & (H - 1);
+                for (;;) {
+                    const uint32_t old = atomicCAS(&s_ht[slot], 0u, (uint32_t)(j + 1) | bits);
+                    if (old == 0u) {
+                        r_leader[e] = j;
+                        break;
+                    }
+                    const int o = (int)(old & kSlotIdx) - 1;
+                    if (s_sid[o] == sid && s_seg[o] == seg) {
+                        r_leader[e] = o;
+                        break;
+                    }
+                    slot = (slot + 1) & (H - 1);
+                }
+                r_slot[e] = slot;
+            }
+        }
+        __syncthreads();
+
+        // ---- 5. reduce(mergeSpan) ------------------------------------------------------------------
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int j = 2 * tid + e;
+            const int L = r_leader[e];
+            if (L >= 0 && L != j) {
+                const uint32_t f = cur.flags[e];
+                if (f & ZK_F_HAS_ANNOTATIONS) {
+                    atomicMin(&s_first[L], (long long)cur.first[e]);
+                    atomicMax(&s_last[L], (long long)cur.last[e]);
+                }
+                if (r_svck[e] != kSvcNone) atomicMin(&s_svck[L], r_svck[e]);
+                if (f & ZK_F_HAS_PARENT) atomicMin((unsigned long long*)&s_pid[L], (unsigned long long)cur.pid[e]);
+                uint32_t once;
+                const uint32_t bits = frag_bits(f, &once);
+                const uint32_t old = atomicOr(&s_ht[r_slot[e]], bits);
+                const uint32_t promote = once & (old >> kSlotA) & 0xFu;  // second occurrence
+                if (promote) atomicOr(&s_ht[r_slot[e]], promote << kSlotB);
+            }
         }
         __syncthreads();
 
         // ---- 6. filter(isValid), join on (parentId, traceId), (cell, duration) links ----------
-        uint32_t w[2], sL[2];
-        uint64_t pL[2];
-        bool leader[2], child[2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const int L = in[e] ? lead[e] : jj + e;
-            w[e] = s_ht[slot_of[e]];
-            sL[e] = s_svck[L];
-            pL[e] = s_pid[L];
-            const uint32_t f = cur.flags[e];
-            bool amb = (f & ZK_F_HAS_PARENT) ? (cur.pid[e] != pL[e]) : ((w[e] & kSlotP1) != 0u);
-            const uint32_t sk = svck[e];
-            amb = amb || (sk != kSvcNone && (sk >> kSvcKindShift) == (sL[e] >> kSvcKindShift) && sk != sL[e]);
-            leader[e] = in[e] && lead[e] == jj + e;
-            const bool valid = slot_valid(w[e]);
-            child[e] = leader[e] && valid && (w[e] & kSlotP1);
-            st.add(ST_AMBIGUOUS, in[e] && amb);
-            st.add(ST_SVC_RANGE, in[e] && rerr[e]);
-            st.add(ST_MERGED, leader[e]);
-            st.add(ST_VALID, leader[e] && valid);
-            st.add(ST_INVALID, leader[e] && !valid);
-            st.add(ST_CHILD, child[e]);
-        }
-        // parent probes: one loop for both records
-        uint32_t pw[2] = {0u, 0u};
-        {
-            int e = child[0] ? 0 : (child[1] ? 1 : 2);
-            uint64_t key = e == 0 ? pL[0] : pL[1];
-            uint32_t sg = (uint32_t)(e == 0 ? seg[0] : seg[1]);
-            uint32_t slot = slot_hash(key, sg) & (H - 1);
-            while (e < 2) {
-                const uint32_t o = s_ht[slot];
-                bool stop_e = o == 0u;
-                if (!stop_e) {
-                    const int oi = (int)(o & kSlotIdx) - 1;
-                    if (s_sid[oi] == key && s_seg[oi] == sg) {
-                        stop_e = true;
-                        if (e == 0)
-                            pw[0] = o;
-                        else
-                            pw[1] = o;
-                    }
-                }
-                if (stop_e) {
-                    e = (e == 0 && child[1]) ? 1 : 2;
-                    key = pL[1];
-                    sg = (uint32_t)seg[1];
-                    slot = slot_hash(key, sg) & (H - 1);
-                } else {
-                    slot = (slot + 1) & (H - 1);
-                }
-            }
-        }
-        uint64_t link[2];
+        uint64_t r_link[2];
         uint32_t nl = 0;
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-            const int j = jj + e;
-            const bool pok = child[e] && pw[e] != 0u && slot_valid(pw[e]);
-            const uint32_t sp = s_svck[pok ? (int)(pw[e] & kSlotIdx) - 1 : j];
-            const bool nosvc = pok && (sp == kSvcNone || sL[e] == kSvcNone);
-            const uint64_t d = (uint64_t)s_last[j] - (uint64_t)s_first[j];
-            const bool dbad = pok && !nosvc && d >= kMaxDuration;
-            const bool has = pok && !nosvc && !dbad;
-            const uint64_t cell = (uint64_t)(sp & kSvcIdMask) * a.S + (sL[e] & kSvcIdMask);
-            link[e] = has ? ((cell << 40) | d) : ~0ull;
-            nl += has ? 1u : 0u;
-            st.add(ST_MISSING_PARENT, child[e] && !pok);
-            st.add(ST_JOINED, pok);
-            st.add(ST_NO_SERVICE, nosvc);
-            st.add(ST_DUR_RANGE, dbad);
-            // lanes without a link add 0 to a bin of their own (no same-address pile-up)
-            atomicAdd(&s_hist[(has && a.nb) ? (uint32_t)(cell >> a.cb_shift) : (uint32_t)(j & (kMaxBuckets - 1))],
-                      has ? 1u : 0u);
+            r_link[e] = ~0ull;
+            const int L = r_leader[e];
+            if (L < 0) continue;
+            const int j = 2 * tid + e;
+            const uint32_t f = cur.flags[e];
+            const uint32_t w = s_ht[r_slot[e]];
+            const uint32_t sL = s_svck[L];
+            const uint64_t pL = s_pid[L];
+            bool amb = (f & ZK_F_HAS_PARENT) ? (cur.pid[e] != pL) : ((w & kSlotP1) != 0u);
+            const uint32_t sk = r_svck[e];
+            if (sk != kSvcNone && (sk >> kSvcKindShift) == (sL >> kSvcKindShift) && sk != sL) amb = true;
+            if (amb) st.inc(ST_AMBIGUOUS);
+            if (r_rerr[e]) st.inc(ST_SVC_RANGE);
+            if (L != j) continue;
+            st.inc(ST_MERGED);
+            const bool valid = slot_valid(w);
+            st.inc(valid ? ST_VALID : ST_INVALID);
+            if (!(valid && (w & kSlotP1))) continue;
+            st.inc(ST_CHILD);
+            const uint16_t seg = (uint16_t)r_seg[e];
+            uint32_t slot = slot_hash(pL, seg) & (H - 1);
+            uint32_t pw = 0;
+            for (;;) {
+                const uint32_t o = s_ht[slot];
+                if (o == 0u) break;
+                const int oi = (int)(o & kSlotIdx) - 1;
+                if (s_sid[oi] == pL && s_seg[oi] == seg) {
+                    pw = o;
+                    break;
+                }
+                slot = (slot + 1) & (H - 1);
+            }
+            if (pw == 0u || !slot_valid(pw)) {
+                st.inc(ST_MISSING_PARENT);
+                continue;
+            }
+            st.inc(ST_JOINED);
+            const uint32_t sp = s_svck[(pw & kSlotIdx) - 1];
+            if (sp == kSvcNone || sL == kSvcNone) {
+                st.inc(ST_NO_SERVICE);
+                continue;
+            }
+            const uint64_t d = (uint64_t)(s_last[j] - s_first[j]);
+            if (d >= kMaxDuration) {
+                st.inc(ST_DUR_RANGE);
+                continue;
+            }
+            const uint64_t cell = (uint64_t)(sp & kSvcIdMask) * a.S + (sL & kSvcIdMask);
+            r_link[e] = (cell << 40) | d;
+            if (a.nb && !a.ablate) atomicAdd(&s_hist[cell >> a.cb_shift], 1u);
+            ++nl;
         }
         // ---- 7. append the window's links to this workgroup's list -----------------------------
         uint32_t incl = nl;
@@ -555,10 +509,12 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
         }
         if (!a.ablate) {
             uint32_t pos = nout + base + incl - nl;
-            if (link[0] != ~0ull) out[pos++] = link[0];
-            if (link[1] != ~0ull) out[pos] = link[1];
+#pragma unroll
+            for (int e = 0; e < 2; ++e)
+                if (r_link[e] != ~0ull) out[pos++] = r_link[e];
             nout += total;
         }
+        }  // ablate != 2
         if (done) break;
         ws = next_ws;
         seek = next_seek;
@@ -569,9 +525,8 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
         a.link_count[blockIdx.x] = nout;
         atomicAdd(&a.stats[(uint64_t)(blockIdx.x % kStatShards) * ST_N + ST_RECORDS], (unsigned long long)nrec);
     }
-    flush_stats16(st, s_stat, a.stats);  // its barrier also publishes s_hist
-    for (uint32_t x = tid; x < a.nb; x += WG)
-        a.hist[(uint64_t)x * a.grid + blockIdx.x] = a.ablate ? 0u : s_hist[x];
+    flush_stats32(st, s_stat, a.stats);  // its barrier also publishes s_hist
+    for (uint32_t x = tid; x < a.nb; x += WG) a.hist[(uint64_t)x * a.grid + blockIdx.x] = s_hist[x];
 }
 
 // =============================================================================================
