@@ -64,6 +64,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from zipkin_amd import DepsContext, DeviceColumns, tracegen_params
+    from zipkin_amd.shards import allreduce_table
 
     S = a.services
     cells = S * S
@@ -89,7 +90,7 @@ def main():
         ctx.reset()
         ctx.accumulate(cols)
         if dist is not None:
-            dist.all_reduce(table)  # exact u64-limb SUM over xGMI (RCCL): shards are disjoint traces
+            allreduce_table(table)  # exact u64-limb SUM over xGMI (RCCL): shards are disjoint traces
             ctx.note_merged(n * world)
         ctx.finalize(out_device=out)
 

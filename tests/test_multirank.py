@@ -1,0 +1,103 @@
+"""The N > 1 path on CPU: world_size-2 gloo processes, traceId-hash shards, exact SUM all-reduce.
+
+What the multi-GPU step relies on (zipkin_amd/shards.py):
+  * shard = mix64(traceId) % world puts every fragment of a trace on one rank, so merges
+    (ZipkinAggregateJob.scala:21) and joins (:30) are rank-local;
+  * the carry-free limb table of disjoint shards adds limb-wise to the table of the union, so one
+    SUM all-reduce (RCCL on the GPU box, gloo here) gives the exact job-wide power sums.
+Each rank aggregates its shard with the oracle (the GPU accumulator is covered by the gpu tests),
+encodes the exact sums in the device limb layout, all-reduces through zipkin_amd.shards and checks
+the decoded result against the oracle run over the union of all shards.
+"""
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from oracle.oracle import aggregate
+from zipkin_amd import SpanColumns, table, tracegen_host
+from zipkin_amd.shards import shard_of, split
+
+S = 57
+WORLD = 2
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _oracle_sums(cols):
+    r = aggregate(cols, S, threads=2)
+    return {(int(c) // S, int(c) % S): r.power_sums(int(c)) for c in r.present_cells()}, r.stats
+
+
+def _worker(rank, world, port, mode):
+    import torch
+    import torch.distributed as dist
+
+    from zipkin_amd.shards import allreduce_stats, allreduce_table
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        if mode == "tracegen":
+            # weak scaling as in bench.py: every rank generates its own shard
+            shards = [tracegen_host(seed=5, num_traces=300, max_depth=6, num_services=S, rank=r, world=world)
+                      for r in range(world)]
+        else:
+            # one global batch, partitioned by the ingest-side hash
+            full = tracegen_host(seed=6, num_traces=600, max_depth=6, num_services=S)
+            shards = split(full, world)
+        mine = shards[rank]
+        assert len(mine) > 0
+        assert (shard_of(np.unique(mine.trace_id), world) == rank).all()
+
+        sums, stats = _oracle_sums(mine)
+        t = torch.from_numpy(table.encode(sums, S))
+        allreduce_table(t)
+        got = table.decode(t.numpy(), S)
+        gstats = allreduce_stats(stats)
+
+        want, wstats = _oracle_sums(SpanColumns.concat(shards))
+        assert got == want, "all-reduced limb table differs from the oracle over the union"
+        for k in ("records", "merged_spans", "valid_spans", "child_spans", "joined_links", "missing_parent"):
+            assert gstats[k] == wstats[k], k
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["tracegen", "split"])
+def test_two_rank_allreduce_is_exact(mode):
+    mp.spawn(_worker, args=(WORLD, _free_port(), mode), nprocs=WORLD, join=True)
+
+
+def test_limb_encoding_roundtrip_and_linearity():
+    rng = np.random.default_rng(0)
+    d = rng.integers(0, 1 << 40, size=1000, dtype=np.uint64)
+    a, b = d[:400], d[400:]
+
+    def sums(x):
+        v = [int(t) for t in x]
+        return (len(v), sum(v), sum(t * t for t in v), sum(t ** 3 for t in v), sum(t ** 4 for t in v))
+
+    ta = table.encode({(0, 1): sums(a)}, 2).view(np.uint64)
+    tb = table.encode({(0, 1): sums(b)}, 2).view(np.uint64)
+    tot = (ta + tb).view(np.int64)  # limb-wise u64 addition = the all-reduce
+    assert table.decode(tot, 2) == {(0, 1): sums(d)}
+    assert table.decode(table.encode({(1, 0): sums(d)}, 2), 2) == {(1, 0): sums(d)}
+
+
+def test_split_partitions_whole_traces():
+    full = tracegen_host(seed=7, num_traces=400, max_depth=5, num_services=S)
+    parts = split(full, 4)
+    assert sum(len(p) for p in parts) == len(full)
+    seen = set()
+    for r, p in enumerate(parts):
+        u = set(np.unique(p.trace_id).tolist())
+        assert not (u & seen)
+        seen |= u
+        # trace-clustered order survives the split
+        change = np.flatnonzero(np.diff(p.trace_id.view(np.int64)) != 0)
+        assert len(change) + 1 == len(u)

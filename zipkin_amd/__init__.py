@@ -6,6 +6,7 @@ binds it (ctypes) and mirrors the reference's Aggregates store surface for the h
 from ._abi import ZkError, ZkLibraryError  # noqa: F401
 from .columns import BYTES_PER_RECORD, DeviceColumns, SpanColumns, tracegen_host, tracegen_params  # noqa: F401
 from .context import DepsContext, LinkTable  # noqa: F401
+from . import table  # noqa: F401
 
 __all__ = [
     "ZkError",

@@ -1,0 +1,82 @@
+"""Multi-GPU step of the dependency path: traceId-hash shards and one exact SUM all-reduce.
+
+Both shuffle keys of the reference job contain traceId -- the merge key (id, traceId) at
+ZipkinAggregateJob.scala:21 and the join key (parentId, traceId) at :30 -- so with
+shard = mix64(traceId) % world (zk_trace_shard) every merge and every join is rank-local. The only
+exchange is the reduce of the per-(parent, child) link table (`.group.sum`, :40): one SUM
+all-reduce of the carry-free u64-limb accumulator (zipkin_amd/table.py), which is exact and
+order-independent, so any world size gives bit-identical Moments. One process per GPU;
+backend "nccl" (RCCL over xGMI) on the GPU box, "gloo" for the CPU tests.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _abi
+from .columns import SpanColumns
+
+
+def shard_of(trace_ids: np.ndarray, world: int) -> np.ndarray:
+    """Shard index of every traceId (the same hash the device tracegen and ingest use)."""
+    L = _abi.lib()
+    tids = np.asarray(trace_ids, dtype=np.uint64)
+    return np.fromiter((L.zk_trace_shard(int(t), world) for t in tids), dtype=np.uint32, count=len(tids))
+
+
+def split(cols: SpanColumns, world: int) -> list[SpanColumns]:
+    """Partition a trace-clustered batch into per-rank batches (order inside a shard is kept)."""
+    s = shard_of(cols.trace_id, world)
+    return [cols.take(np.flatnonzero(s == r)) for r in range(world)]
+
+
+def allreduce_table(table, group=None) -> None:
+    """In-place SUM of the exact accumulator (int64 tensor, device or host) across ranks.
+
+    int64 two's-complement addition is bit-identical to the u64 limb addition the layout needs.
+    """
+    import torch.distributed as dist
+
+    dist.all_reduce(table, op=dist.ReduceOp.SUM, group=group)
+
+
+def allreduce_stats(stats: dict, device="cpu", group=None) -> dict:
+    """Job-wide zk_stats: every counter is a sum over ranks."""
+    import torch
+    import torch.distributed as dist
+
+    keys = sorted(stats)
+    t = torch.tensor([int(stats[k]) for k in keys], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return {k: int(v) for k, v in zip(keys, t.tolist())}
+
+
+class ShardedDeps:
+    """One rank of the sharded job: a DepsContext over a caller-owned (all-reducible) table.
+
+    step(cols): reset -> accumulate this rank's shard -> SUM all-reduce -> finalize. With
+    world == 1 the all-reduce is skipped. Every rank ends with the same finalized table.
+    """
+
+    def __init__(self, num_services: int, *, device: int = 0, stream=None, timing: bool = False,
+                 group=None, ablate: int = 0):
+        import torch
+        import torch.distributed as dist
+
+        from .context import DepsContext
+
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.group = group
+        self.num_services = num_services
+        dev = torch.device("cuda", device)
+        self.table = torch.zeros(num_services * num_services * 16, dtype=torch.int64, device=dev)
+        self.ctx = DepsContext(num_services, device=device, stream=stream, timing=timing,
+                               table_ptr=self.table.data_ptr(), table_bytes=self.table.numel() * 8, ablate=ablate)
+
+    def step(self, cols, total_records: int | None = None, out_device=None):
+        self.ctx.reset()
+        self.ctx.accumulate(cols)
+        if self.world > 1:
+            allreduce_table(self.table, self.group)
+            if total_records is not None:
+                self.ctx.note_merged(total_records)
+        return self.ctx.finalize(out_device=out_device)
