@@ -8,12 +8,15 @@ import pytest
 from tests.conftest import gpu_available
 from zipkin_amd import _abi
 
-HEADER = Path(__file__).resolve().parent.parent / "include" / "zkagg.h"
+INCLUDE = Path(__file__).resolve().parent.parent / "include"
 
 
 def declared_functions():
-    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
-    return sorted(set(re.findall(r"\b(zk_[a-z0-9_]+)\s*\(", text)))
+    names = set()
+    for h in sorted(INCLUDE.glob("*.h")):
+        text = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
+        names |= set(re.findall(r"\b(zk_[a-z0-9_]+)\s*\(", text))
+    return sorted(names)
 
 
 def test_header_declares_what_the_binding_binds():

@@ -143,8 +143,23 @@ class zk_tracegen_params(C.Structure):
     ]
 
 
-# every symbol include/zkagg.h declares: (name, restype, argtypes)
+class zk_kv_config(C.Structure):
+    _fields_ = [
+        ("num_services", C.c_uint32),
+        ("device", C.c_int32),
+        ("stream", C.c_void_p),
+        ("width", C.c_uint32),
+        ("depth", C.c_uint32),
+        ("candidates", C.c_uint32),
+        ("seed", C.c_uint64),
+        ("reserved", C.c_uint32 * 8),
+    ]
+
+
+# every symbol include/*.h declares: (name, restype, argtypes)
 _P = C.c_void_p
+_U64P = C.POINTER(C.c_uint64)
+_U32P = C.POINTER(C.c_uint32)
 _SIGNATURES = [
     ("zk_abi_version", C.c_uint32, []),
     ("zk_ctx_create", C.c_int, [C.POINTER(zk_config), C.POINTER(_P)]),
@@ -170,6 +185,20 @@ _SIGNATURES = [
         C.c_int,
         [_P, C.POINTER(zk_tracegen_params), C.POINTER(zk_span_cols), C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)],
     ),
+    # include/zksketch.h: key-value count-min + top-K
+    ("zk_kv_create", C.c_int, [C.POINTER(zk_kv_config), C.POINTER(_P)]),
+    ("zk_kv_destroy", C.c_int, [_P]),
+    ("zk_kv_last_error", C.c_char_p, [_P]),
+    ("zk_kv_geometry", C.c_int, [_P, _U32P, _U32P, _U32P]),
+    ("zk_kv_reset", C.c_int, [_P]),
+    ("zk_kv_accumulate", C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32]),
+    ("zk_kv_topk_all", C.c_int, [_P, C.c_uint32, _P, _P, _P]),
+    ("zk_kv_topk", C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, _P]),
+    ("zk_kv_estimate", C.c_int, [_P, C.c_uint32, _P, C.c_uint64, _P]),
+    ("zk_kv_totals", C.c_int, [_P, _P]),
+    ("zk_kv_partial", C.c_int, [_P, C.POINTER(_P), _U64P, C.POINTER(_P), _U64P]),
+    ("zk_kv_candidates", C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), _U64P, _U64P]),
+    ("zk_kv_merge_candidates", C.c_int, [_P, _P, _P, C.c_uint32]),
 ]
 
 SYMBOLS = [s[0] for s in _SIGNATURES]

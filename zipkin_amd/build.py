@@ -9,8 +9,18 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = PKG / "csrc"
-SOURCES = ["zk_join.hip", "zk_reduce.hip", "zk_finalize.hip", "zk_tracegen.hip", "zk_api.cpp"]
-HEADERS = ["zk_internal.h", "zk_tracegen.h"]
+SOURCES = [
+    "zk_join.hip",
+    "zk_reduce.hip",
+    "zk_finalize.hip",
+    "zk_tracegen.hip",
+    "zk_api.cpp",
+    "zk_partition.hip",
+    "zk_kv.hip",
+    "zk_kv_api.cpp",
+]
+HEADERS = ["zk_internal.h", "zk_tracegen.h", "zk_sketch_internal.h"]
+PUBLIC_HEADERS = ["zkagg.h", "zksketch.h"]
 LIB = PKG / "libzkagg.so"
 ARCH = os.environ.get("ZK_OFFLOAD_ARCH", "gfx950")
 
@@ -26,7 +36,7 @@ def needs_build() -> bool:
     if not LIB.exists():
         return True
     t = LIB.stat().st_mtime
-    deps = [CSRC / s for s in SOURCES + HEADERS] + [ROOT / "include" / "zkagg.h"]
+    deps = [CSRC / s for s in SOURCES + HEADERS] + [ROOT / "include" / h for h in PUBLIC_HEADERS]
     return any(d.stat().st_mtime > t for d in deps)
 
 

@@ -1,0 +1,326 @@
+// zk_kv_api.cpp — C ABI of the key-value count-min + top-K sketch (include/zksketch.h).
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "zk_sketch_internal.h"
+#include "zksketch.h"
+
+using namespace zk;
+
+struct zk_kv {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    uint32_t cus = 256;
+    KvArgs a{};
+    unsigned long long* dropped = nullptr;
+    // batch scratch
+    uint64_t* sorted = nullptr;
+    uint64_t sorted_cap = 0;
+    uint64_t* seg = nullptr;
+    uint32_t* unit_base = nullptr;
+    void* part = nullptr;
+    uint64_t part_bytes = 0;
+    uint64_t* unit_key = nullptr;
+    uint32_t* unit_est = nullptr;
+    uint32_t unit_cap = 0;
+    void* stage = nullptr;  // host-pointer staging: svc | keys
+    uint64_t stage_cap = 0;
+    uint64_t* qkeys = nullptr;  // estimate staging
+    uint32_t* qest = nullptr;
+    uint64_t qcap = 0;
+    std::string err;
+};
+
+namespace {
+
+zk_status kfail(zk_kv* k, zk_status s, const std::string& m) {
+    if (k) k->err = m;
+    return s;
+}
+
+#define KV_HIP(kv, call)                                                                         \
+    do {                                                                                         \
+        hipError_t _e = (call);                                                                  \
+        if (_e != hipSuccess) return kfail(kv, ZK_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+uint32_t ilog2(uint32_t x) {
+    uint32_t r = 0;
+    while ((1u << (r + 1)) <= x) ++r;
+    return r;
+}
+
+zk_status check_state(zk_kv* kv, bool need_totals_ok) {
+    unsigned long long dropped = 0;
+    KV_HIP(kv, hipMemcpyAsync(&dropped, kv->dropped, 8, hipMemcpyDeviceToHost, kv->stream));
+    std::vector<uint64_t> tot(kv->a.S);
+    if (need_totals_ok)
+        KV_HIP(kv, hipMemcpyAsync(tot.data(), kv->a.totals, tot.size() * 8, hipMemcpyDeviceToHost, kv->stream));
+    KV_HIP(kv, hipStreamSynchronize(kv->stream));
+    if (dropped) return kfail(kv, ZK_ERR_SERVICE_RANGE, std::to_string(dropped) + " items with service_id >= S");
+    for (uint64_t t : tot)
+        if (t >= (1ull << 32)) return kfail(kv, ZK_ERR_CAPACITY, "a service counted >= 2^32 keys since reset");
+    return ZK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+zk_status zk_kv_create(const zk_kv_config* cfg, zk_kv** out) {
+    if (!cfg || !out) return ZK_ERR_INVALID_ARG;
+    *out = nullptr;
+    const uint32_t S = cfg->num_services;
+    if (S == 0 || S > 4096) return ZK_ERR_INVALID_ARG;
+    uint32_t width = cfg->width, depth = cfg->depth ? cfg->depth : 4, cand = cfg->candidates ? cfg->candidates : 64;
+    if (width == 0) {
+        width = 1u << ilog2((1u << 20) / S > 0 ? (1u << 20) / S : 1);
+        if (width < 64) width = 64;
+        if (width > kKvMaxWidth) width = kKvMaxWidth;
+    }
+    if (width < 64 || width > kKvMaxWidth || (width & (width - 1))) return ZK_ERR_INVALID_ARG;
+    if (depth > kKvMaxDepth || depth * width > 16384) return ZK_ERR_INVALID_ARG;  // LDS: <= 64 KB of rows
+    if (cand > kKvMaxCand) return ZK_ERR_INVALID_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return ZK_ERR_NO_DEVICE;
+    if (cfg->device < 0 || cfg->device >= ndev) return ZK_ERR_NO_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, cfg->device) != hipSuccess) return ZK_ERR_NO_DEVICE;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return ZK_ERR_NO_DEVICE;
+    zk_kv* k = new zk_kv();
+    k->device = cfg->device;
+    k->cus = prop.multiProcessorCount > 0 ? (uint32_t)prop.multiProcessorCount : 256;
+    KvArgs& a = k->a;
+    a.S = S;
+    a.width = width;
+    a.wbits = ilog2(width);
+    a.depth = depth;
+    a.cand = cand;
+    for (uint32_t r = 0; r < kKvMaxDepth; ++r) a.seeds[r] = sk_mix64(cfg->seed + 0x9E3779B97F4A7C15ull * (r + 1));
+    a.unit_items = kKvUnitItems;
+    hipError_t e = hipSetDevice(k->device);
+    if (e == hipSuccess) {
+        if (cfg->stream) {
+            k->stream = (hipStream_t)cfg->stream;
+        } else {
+            e = hipStreamCreateWithFlags(&k->stream, hipStreamNonBlocking);
+            k->own_stream = true;
+        }
+    }
+    if (e == hipSuccess) e = hipMalloc(&a.cm, (uint64_t)S * depth * width * 4);
+    if (e == hipSuccess) e = hipMalloc(&a.totals, (uint64_t)S * 8);
+    if (e == hipSuccess) e = hipMalloc(&a.cand_key, (uint64_t)S * cand * 8);
+    if (e == hipSuccess) e = hipMalloc(&a.cand_est, (uint64_t)S * cand * 4);
+    if (e == hipSuccess) e = hipMalloc(&k->dropped, 8);
+    if (e == hipSuccess) e = hipMalloc(&k->seg, (uint64_t)(S + 1) * 8);
+    if (e == hipSuccess) e = hipMalloc(&k->unit_base, (uint64_t)(S + 1) * 4);
+    zk_status st = e == hipSuccess ? zk_kv_reset(k) : ZK_ERR_HIP;
+    if (st != ZK_OK) {
+        zk_kv_destroy(k);
+        return st;
+    }
+    *out = k;
+    return ZK_OK;
+}
+
+zk_status zk_kv_destroy(zk_kv* k) {
+    if (!k) return ZK_ERR_INVALID_ARG;
+    hipSetDevice(k->device);
+    if (k->stream) hipStreamSynchronize(k->stream);
+    for (void* p : {(void*)k->a.cm, (void*)k->a.totals, (void*)k->a.cand_key, (void*)k->a.cand_est, (void*)k->dropped,
+                    (void*)k->sorted, (void*)k->seg, (void*)k->unit_base, k->part, (void*)k->unit_key,
+                    (void*)k->unit_est, k->stage, (void*)k->qkeys, (void*)k->qest})
+        if (p) hipFree(p);
+    if (k->own_stream && k->stream) hipStreamDestroy(k->stream);
+    delete k;
+    return ZK_OK;
+}
+
+const char* zk_kv_last_error(const zk_kv* k) { return k ? k->err.c_str() : "null handle"; }
+
+zk_status zk_kv_geometry(const zk_kv* k, uint32_t* width, uint32_t* depth, uint32_t* candidates) {
+    if (!k) return ZK_ERR_INVALID_ARG;
+    if (width) *width = k->a.width;
+    if (depth) *depth = k->a.depth;
+    if (candidates) *candidates = k->a.cand;
+    return ZK_OK;
+}
+
+zk_status zk_kv_reset(zk_kv* k) {
+    if (!k) return ZK_ERR_INVALID_ARG;
+    const KvArgs& a = k->a;
+    KV_HIP(k, hipSetDevice(k->device));
+    KV_HIP(k, hipMemsetAsync(a.cm, 0, (uint64_t)a.S * a.depth * a.width * 4, k->stream));
+    KV_HIP(k, hipMemsetAsync(a.totals, 0, (uint64_t)a.S * 8, k->stream));
+    KV_HIP(k, hipMemsetAsync(a.cand_key, 0, (uint64_t)a.S * a.cand * 8, k->stream));
+    KV_HIP(k, hipMemsetAsync(a.cand_est, 0, (uint64_t)a.S * a.cand * 4, k->stream));
+    KV_HIP(k, hipMemsetAsync(k->dropped, 0, 8, k->stream));
+    return ZK_OK;
+}
+
+zk_status zk_kv_accumulate(zk_kv* k, const uint32_t* svc, const uint64_t* keys, uint64_t n, uint32_t flags) {
+    if (!k) return ZK_ERR_INVALID_ARG;
+    if (n == 0) return ZK_OK;
+    if (!svc || !keys) return kfail(k, ZK_ERR_INVALID_ARG, "null input");
+    if (n >= (1ull << 32)) return kfail(k, ZK_ERR_INVALID_ARG, "batch of >= 2^32 items");
+    KV_HIP(k, hipSetDevice(k->device));
+    if (!(flags & ZK_BATCH_DEVICE_PTRS)) {
+        if (n > k->stage_cap) {
+            if (k->stage) KV_HIP(k, hipFree(k->stage));
+            k->stage = nullptr;
+            KV_HIP(k, hipMalloc(&k->stage, n * 12 + 256));
+            k->stage_cap = n;
+        }
+        uint64_t* dk = (uint64_t*)k->stage;
+        uint32_t* ds = (uint32_t*)((uint8_t*)k->stage + ((n * 8 + 255) & ~255ull));
+        KV_HIP(k, hipMemcpyAsync(dk, keys, n * 8, hipMemcpyHostToDevice, k->stream));
+        KV_HIP(k, hipMemcpyAsync(ds, svc, n * 4, hipMemcpyHostToDevice, k->stream));
+        keys = dk;
+        svc = ds;
+    }
+    KvArgs& a = k->a;
+    const PartitionPlan plan = partition_plan(n, a.S, k->cus);
+    const uint64_t pb = partition_scratch_bytes(plan);
+    if (pb > k->part_bytes) {
+        if (k->part) KV_HIP(k, hipFree(k->part));
+        k->part = nullptr;
+        KV_HIP(k, hipMalloc(&k->part, pb));
+        k->part_bytes = pb;
+    }
+    if (n > k->sorted_cap) {
+        if (k->sorted) KV_HIP(k, hipFree(k->sorted));
+        k->sorted = nullptr;
+        KV_HIP(k, hipMalloc(&k->sorted, n * 8));
+        k->sorted_cap = n;
+    }
+    const uint64_t max_units = (n + a.unit_items - 1) / a.unit_items + a.S;
+    if (max_units > k->unit_cap) {
+        if (k->unit_key) KV_HIP(k, hipFree(k->unit_key));
+        if (k->unit_est) KV_HIP(k, hipFree(k->unit_est));
+        k->unit_key = nullptr;
+        k->unit_est = nullptr;
+        KV_HIP(k, hipMalloc(&k->unit_key, max_units * a.cand * 8));
+        KV_HIP(k, hipMalloc(&k->unit_est, max_units * a.cand * 4));
+        k->unit_cap = (uint32_t)max_units;
+    }
+    KV_HIP(k, launch_partition(plan, svc, keys, n, k->sorted, k->seg, k->dropped, k->part, k->stream));
+    KV_HIP(k, launch_unit_plan(k->seg, a.S, a.unit_items, k->unit_base, k->stream));
+    a.keys = k->sorted;
+    a.seg = k->seg;
+    a.unit_base = k->unit_base;
+    a.max_units = (uint32_t)max_units;
+    a.unit_key = k->unit_key;
+    a.unit_est = k->unit_est;
+    a.extra_key = nullptr;
+    a.extra_est = nullptr;
+    a.extra_lists = 0;
+    KV_HIP(k, launch_kv_sketch(a, k->stream));
+    KV_HIP(k, launch_kv_candidates(a, k->stream));
+    KV_HIP(k, launch_kv_merge(a, k->stream));
+    return ZK_OK;
+}
+
+zk_status zk_kv_topk_all(zk_kv* k, uint32_t kk, uint64_t* keys, uint32_t* est, uint32_t* count) {
+    if (!k) return ZK_ERR_INVALID_ARG;
+    if (kk == 0 || kk > k->a.cand || !keys || !est) return kfail(k, ZK_ERR_INVALID_ARG, "k must be in 1..candidates");
+    const KvArgs& a = k->a;
+    KV_HIP(k, hipSetDevice(k->device));
+    KV_HIP(k, hipMemcpy2DAsync(keys, (size_t)kk * 8, a.cand_key, (size_t)a.cand * 8, (size_t)kk * 8, a.S,
+                               hipMemcpyDeviceToHost, k->stream));
+    KV_HIP(k, hipMemcpy2DAsync(est, (size_t)kk * 4, a.cand_est, (size_t)a.cand * 4, (size_t)kk * 4, a.S,
+                               hipMemcpyDeviceToHost, k->stream));
+    zk_status st = check_state(k, true);  // syncs
+    if (st != ZK_OK) return st;
+    if (count)
+        for (uint32_t s = 0; s < a.S; ++s) {
+            uint32_t c = 0;
+            while (c < kk && est[(uint64_t)s * kk + c]) ++c;
+            count[s] = c;
+        }
+    return ZK_OK;
+}
+
+zk_status zk_kv_topk(zk_kv* k, uint32_t svc, uint32_t kk, uint64_t* keys, uint32_t* est, uint32_t* count) {
+    if (!k) return ZK_ERR_INVALID_ARG;
+    if (svc >= k->a.S) return kfail(k, ZK_ERR_SERVICE_RANGE, "service >= S");
+    if (kk == 0 || kk > k->a.cand || !keys || !est) return kfail(k, ZK_ERR_INVALID_ARG, "k must be in 1..candidates");
+    const KvArgs& a = k->a;
+    KV_HIP(k, hipSetDevice(k->device));
+    KV_HIP(k, hipMemcpyAsync(keys, a.cand_key + (uint64_t)svc * a.cand, (size_t)kk * 8, hipMemcpyDeviceToHost, k->stream));
+    KV_HIP(k, hipMemcpyAsync(est, a.cand_est + (uint64_t)svc * a.cand, (size_t)kk * 4, hipMemcpyDeviceToHost, k->stream));
+    zk_status st = check_state(k, true);
+    if (st != ZK_OK) return st;
+    if (count) {
+        uint32_t c = 0;
+        while (c < kk && est[c]) ++c;
+        *count = c;
+    }
+    return ZK_OK;
+}
+
+zk_status zk_kv_estimate(zk_kv* k, uint32_t svc, const uint64_t* keys, uint64_t n, uint32_t* est) {
+    if (!k) return ZK_ERR_INVALID_ARG;
+    if (svc >= k->a.S) return kfail(k, ZK_ERR_SERVICE_RANGE, "service >= S");
+    if (n == 0) return ZK_OK;
+    if (!keys || !est) return kfail(k, ZK_ERR_INVALID_ARG, "null array");
+    KV_HIP(k, hipSetDevice(k->device));
+    if (n > k->qcap) {
+        if (k->qkeys) KV_HIP(k, hipFree(k->qkeys));
+        if (k->qest) KV_HIP(k, hipFree(k->qest));
+        k->qkeys = nullptr;
+        k->qest = nullptr;
+        KV_HIP(k, hipMalloc(&k->qkeys, n * 8));
+        KV_HIP(k, hipMalloc(&k->qest, n * 4));
+        k->qcap = n;
+    }
+    KV_HIP(k, hipMemcpyAsync(k->qkeys, keys, n * 8, hipMemcpyHostToDevice, k->stream));
+    KV_HIP(k, launch_kv_estimate(k->a, svc, k->qkeys, n, k->qest, k->stream));
+    KV_HIP(k, hipMemcpyAsync(est, k->qest, n * 4, hipMemcpyDeviceToHost, k->stream));
+    KV_HIP(k, hipStreamSynchronize(k->stream));
+    return ZK_OK;
+}
+
+zk_status zk_kv_totals(zk_kv* k, uint64_t* totals) {
+    if (!k || !totals) return ZK_ERR_INVALID_ARG;
+    KV_HIP(k, hipSetDevice(k->device));
+    KV_HIP(k, hipMemcpyAsync(totals, k->a.totals, (uint64_t)k->a.S * 8, hipMemcpyDeviceToHost, k->stream));
+    KV_HIP(k, hipStreamSynchronize(k->stream));
+    return ZK_OK;
+}
+
+zk_status zk_kv_partial(zk_kv* k, void** counters, uint64_t* cb, void** totals, uint64_t* tb) {
+    if (!k || !counters || !cb || !totals || !tb) return ZK_ERR_INVALID_ARG;
+    *counters = k->a.cm;
+    *cb = (uint64_t)k->a.S * k->a.depth * k->a.width * 4;
+    *totals = k->a.totals;
+    *tb = (uint64_t)k->a.S * 8;
+    return ZK_OK;
+}
+
+zk_status zk_kv_candidates(zk_kv* k, void** keys, void** est, uint64_t* bk, uint64_t* be) {
+    if (!k || !keys || !est || !bk || !be) return ZK_ERR_INVALID_ARG;
+    *keys = k->a.cand_key;
+    *est = k->a.cand_est;
+    *bk = (uint64_t)k->a.S * k->a.cand * 8;
+    *be = (uint64_t)k->a.S * k->a.cand * 4;
+    return ZK_OK;
+}
+
+zk_status zk_kv_merge_candidates(zk_kv* k, const uint64_t* keys, const uint32_t* est, uint32_t lists) {
+    if (!k) return ZK_ERR_INVALID_ARG;
+    if (lists && (!keys || !est)) return kfail(k, ZK_ERR_INVALID_ARG, "null lists");
+    KV_HIP(k, hipSetDevice(k->device));
+    KvArgs a = k->a;
+    a.max_units = 0;  // no unit lists: previous candidates + gathered lists only
+    a.extra_key = keys;
+    a.extra_est = est;
+    a.extra_lists = lists;
+    KV_HIP(k, launch_kv_merge(a, k->stream));
+    return ZK_OK;
+}
+
+}  // extern "C"

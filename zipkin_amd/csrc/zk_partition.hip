@@ -1,0 +1,172 @@
+// zk_partition.hip — partition (service, payload) items into service-contiguous runs.
+//
+// Three launches, all streaming: (1) per-workgroup service histogram of a contiguous input range
+// in LDS, written service-major (hist[s * grid + w]); (2) one exclusive scan of that matrix
+// (hipcub), which makes every (service, workgroup) pair a disjoint output range, ordered by
+// service first; (3) the scatter pass re-reads the range and appends each payload at its LDS
+// cursor. Order inside one (service, workgroup) range follows LDS atomic order, which none of the
+// sketches depends on (count-min and HyperLogLog are order-free; candidate selection is by
+// final estimate).
+#include <hipcub/hipcub.hpp>
+
+#include "zk_sketch_internal.h"
+
+namespace zk {
+namespace {
+
+constexpr int kPartWG = 256;
+constexpr int kPartU = 4;  // items per thread per iteration (loads issued before the LDS atomics)
+
+__global__ __launch_bounds__(kPartWG) void k_part_hist(const uint32_t* __restrict__ svc, uint64_t n, uint64_t per,
+                                                        uint32_t S, uint32_t grid, uint32_t* __restrict__ hist,
+                                                        unsigned long long* dropped) {
+    extern __shared__ uint32_t h[];
+    for (uint32_t i = threadIdx.x; i < S; i += kPartWG) h[i] = 0u;
+    __syncthreads();
+    const uint64_t lo = (uint64_t)blockIdx.x * per;
+    const uint64_t hi = lo + per < n ? lo + per : n;
+    uint32_t bad = 0;
+    for (uint64_t b = lo; b < hi; b += (uint64_t)kPartWG * kPartU) {
+        uint32_t v[kPartU];
+#pragma unroll
+        for (int e = 0; e < kPartU; ++e) {
+            const uint64_t i = b + (uint64_t)e * kPartWG + threadIdx.x;
+            v[e] = i < hi ? svc[i] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int e = 0; e < kPartU; ++e) {
+            const uint64_t i = b + (uint64_t)e * kPartWG + threadIdx.x;
+            if (v[e] < S)
+                atomicAdd(&h[v[e]], 1u);
+            else if (i < hi)
+                ++bad;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < S; i += kPartWG) hist[(uint64_t)i * grid + blockIdx.x] = h[i];
+    if (bad) atomicAdd(dropped, (unsigned long long)bad);
+}
+
+__global__ __launch_bounds__(kPartWG) void k_part_scatter(const uint32_t* __restrict__ svc,
+                                                           const uint64_t* __restrict__ payload, uint64_t n,
+                                                           uint64_t per, uint32_t S, uint32_t grid,
+                                                           const uint32_t* __restrict__ offs,
+                                                           uint64_t* __restrict__ out) {
+    extern __shared__ uint32_t cur[];  // absolute output cursor per service
+    for (uint32_t i = threadIdx.x; i < S; i += kPartWG) cur[i] = offs[(uint64_t)i * grid + blockIdx.x];
+    __syncthreads();
+    const uint64_t lo = (uint64_t)blockIdx.x * per;
+    const uint64_t hi = lo + per < n ? lo + per : n;
+    for (uint64_t b = lo; b < hi; b += (uint64_t)kPartWG * kPartU) {
+        uint32_t v[kPartU];
+        uint64_t p[kPartU];
+#pragma unroll
+        for (int e = 0; e < kPartU; ++e) {
+            const uint64_t i = b + (uint64_t)e * kPartWG + threadIdx.x;
+            const bool in = i < hi;
+            v[e] = in ? svc[i] : 0xFFFFFFFFu;
+            p[e] = in ? payload[i] : 0ull;
+        }
+#pragma unroll
+        for (int e = 0; e < kPartU; ++e)
+            if (v[e] < S) out[atomicAdd(&cur[v[e]], 1u)] = p[e];
+    }
+}
+
+// seg[s] = offs[s * grid], seg[S] = number of partitioned items
+__global__ void k_part_seg(const uint32_t* __restrict__ offs, const uint32_t* __restrict__ hist, uint32_t S,
+                           uint32_t grid, uint64_t* __restrict__ seg) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < S) seg[s] = offs[(uint64_t)s * grid];
+    if (s == S) {
+        const uint64_t last = (uint64_t)S * grid - 1;
+        seg[S] = (uint64_t)offs[last] + hist[last];
+    }
+}
+
+// unit_base = exclusive scan of ceil(len_s / unit_items); one workgroup of 1024 threads
+__global__ __launch_bounds__(1024) void k_unit_plan(const uint64_t* __restrict__ seg, uint32_t S,
+                                                     uint64_t unit_items, uint32_t* __restrict__ unit_base) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t b = 0; b < S; b += 1024) {
+        const uint32_t s = b + threadIdx.x;
+        const uint64_t len = s < S ? seg[s + 1] - seg[s] : 0;
+        const uint32_t u = (uint32_t)((len + unit_items - 1) / unit_items);
+        uint32_t incl = u;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t o = __shfl_up(incl, off);
+            if (lane >= off) incl += o;
+        }
+        if (lane == 63) wsum[wave] = incl;
+        __syncthreads();
+        uint32_t before = carry;
+        for (int w = 0; w < wave; ++w) before += wsum[w];
+        if (s < S) unit_base[s] = before + incl - u;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry = before + incl;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) unit_base[S] = carry;
+}
+
+uint64_t scan_temp_bytes(uint64_t m) {
+    size_t bytes = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)m);
+    return (bytes + 255) & ~(uint64_t)255;
+}
+
+}  // namespace
+
+PartitionPlan partition_plan(uint64_t n, uint32_t S, uint32_t cus) {
+    PartitionPlan p;
+    p.S = S;
+    // ~4 resident workgroups per CU; at least 16k items per workgroup so the S-entry histogram
+    // column stays small next to the data
+    uint64_t g = (uint64_t)cus * 4;
+    const uint64_t by_items = (n + 16383) / 16384;
+    if (g > by_items) g = by_items ? by_items : 1;
+    p.grid = (uint32_t)g;
+    p.per_wg = (n + g - 1) / g;
+    if (p.per_wg == 0) p.per_wg = 1;
+    return p;
+}
+
+uint64_t partition_scratch_bytes(const PartitionPlan& p) {
+    const uint64_t m = (uint64_t)p.S * p.grid;
+    const uint64_t a = (m * 4 + 255) & ~255ull;
+    return 2 * a + scan_temp_bytes(m);
+}
+
+hipError_t launch_partition(const PartitionPlan& p, const uint32_t* svc, const uint64_t* payload, uint64_t n,
+                            uint64_t* out, uint64_t* seg, unsigned long long* dropped, void* scratch,
+                            hipStream_t s) {
+    const uint64_t m = (uint64_t)p.S * p.grid;
+    const uint64_t a = (m * 4 + 255) & ~255ull;
+    uint32_t* hist = (uint32_t*)scratch;
+    uint32_t* offs = (uint32_t*)((uint8_t*)scratch + a);
+    void* temp = (uint8_t*)scratch + 2 * a;
+    size_t temp_bytes = scan_temp_bytes(m);
+    const size_t lds = (size_t)p.S * 4;
+    hipLaunchKernelGGL(k_part_hist, dim3(p.grid), dim3(kPartWG), lds, s, svc, n, p.per_wg, p.S, p.grid, hist, dropped);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, hist, offs, (int)m, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_part_scatter, dim3(p.grid), dim3(kPartWG), lds, s, svc, payload, n, p.per_wg, p.S, p.grid,
+                       offs, out);
+    hipLaunchKernelGGL(k_part_seg, dim3((p.S + 256) / 256), dim3(256), 0, s, offs, hist, p.S, p.grid, seg);
+    return hipGetLastError();
+}
+
+hipError_t launch_unit_plan(const uint64_t* seg, uint32_t S, uint64_t unit_items, uint32_t* unit_base,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(k_unit_plan, dim3(1), dim3(1024), 0, s, seg, S, unit_items, unit_base);
+    return hipGetLastError();
+}
+
+}  // namespace zk
