@@ -1,0 +1,109 @@
+/*
+ * zkstore.h — C ABI of the Aggregates store surface of libzkagg (host side, no device work).
+ *
+ * Replaces the storage half of
+ *   trait Aggregates  (zipkin-common/src/main/scala/com/twitter/zipkin/storage/Aggregates.scala:26-37)
+ *     getDependencies(startDate: Option[Time], endDate: Option[Time] = None): Future[Dependencies]   :30
+ *     storeDependencies(dependencies: Dependencies): Future[Unit]                                  :31
+ *     getTopAnnotations(serviceName) / getTopKeyValueAnnotations(serviceName): Future[Seq[String]]  :33-34
+ *     storeTopAnnotations(serviceName, a) / storeTopKeyValueAnnotations(serviceName, a)            :35-36
+ * and the value types it moves:
+ *   Moments(m0: Long, m1..m4: Double)           algebird-core 0.8.1 (project/Project.scala:42,50)
+ *   DependencyLink(parent, child, Moments)      zipkin-common/.../common/Dependencies.scala:34
+ *   Dependencies(startTime, endTime, links)     Dependencies.scala:59-63; wire form
+ *                                               zipkin-thrift/.../zipkinDependencies.thrift:24-43 (us)
+ *
+ * The producer side of the store is the device path: zk_deps_finalize (zkagg.h) gives the dense
+ * link table, zk_link_table_compact turns it into the job's single Dependencies record
+ * (ZipkinAggregateJob.scala:41-45), and zk_kv_topk (zksketch.h) produces the per-service
+ * top key-value annotation list that storeTopKeyValueAnnotations persists.
+ *
+ * Services and annotation strings are dictionary ids owned by the host (like zkagg.h); the store
+ * never sees strings. Unlike a zk_ctx, a zk_store IS thread-safe: every call takes the store's
+ * lock, mirroring the reference's `synchronized` writes (CassandraAggregates.scala:110,122) and
+ * the transaction of AnormAggregates.storeDependencies (AnormAggregates.scala:83-109).
+ */
+#ifndef ZKSTORE_H
+#define ZKSTORE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "zkagg.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* algebird Moments: count, mean, sum (x-mean)^2, sum (x-mean)^3, sum (x-mean)^4 */
+typedef struct zk_moments {
+    int64_t m0;
+    double  m1, m2, m3, m4;
+} zk_moments;
+
+/* DependencyLink(parent = Service(parent name), child = Service(child name), durationMoments) */
+typedef struct zk_dep_link {
+    uint32_t   parent;   /* host dictionary id of the parent service name (case-sensitive) */
+    uint32_t   child;
+    zk_moments moments;
+} zk_dep_link;
+
+/* Time.Top / Time.Bottom of the Dependencies monoid zero (Dependencies.scala:81), in us */
+#define ZK_TIME_TOP    INT64_MAX
+#define ZK_TIME_BOTTOM INT64_MIN
+
+/* getDependencies result shapes of the reference backends:
+ *   ZK_STORE_ANORM   rows with start_ts >= start AND end_ts <= end, links concatenated newest
+ *                    record first; result times = the query window (AnormAggregates.scala:52-76)
+ *   ZK_STORE_SUMMED  the same containment window, records Monoid-summed: start = min, end = max,
+ *                    links merged per (parent, child) with MomentsGroup.plus; no record ->
+ *                    the monoid zero (CassandraAggregates.scala:54-74, HBaseAggregates.scala:39-53)
+ * Defaults when a bound is absent (Option = None): start = now - 1 day, end = now
+ * (AnormAggregates.scala:53-54; `now_us` is passed in so callers and tests control Time.now). */
+#define ZK_STORE_ANORM  0u
+#define ZK_STORE_SUMMED 1u
+
+/* top-annotation lists (CassandraAggregates.scala:79-108: row "<service>:annotation" / ":kv") */
+#define ZK_TOP_ANNOTATIONS    0u
+#define ZK_TOP_KV_ANNOTATIONS 1u
+
+typedef struct zk_store zk_store;
+
+zk_status   zk_store_create(uint32_t mode, zk_store** out);
+zk_status   zk_store_destroy(zk_store* st);                     /* Aggregates.close() */
+const char* zk_store_last_error(const zk_store* st);
+
+/* storeDependencies: one Dependencies record (its links are copied). */
+zk_status zk_store_put_dependencies(zk_store* st, int64_t start_us, int64_t end_us, const zk_dep_link* links,
+                                    uint64_t n_links);
+/* getDependencies(startDate, endDate). start_us/end_us NULL = None. Two-phase: with out == NULL,
+ * *n_links receives the number of links; otherwise up to `cap` links are written
+ * (ZK_ERR_CAPACITY if cap is too small) together with the result's start/end times. */
+zk_status zk_store_get_dependencies(zk_store* st, const int64_t* start_us, const int64_t* end_us, int64_t now_us,
+                                    zk_dep_link* out, uint64_t cap, uint64_t* n_links, int64_t* out_start_us,
+                                    int64_t* out_end_us);
+/* number of stored Dependencies records */
+zk_status zk_store_count(zk_store* st, uint64_t* records);
+
+/* storeTopAnnotations / storeTopKeyValueAnnotations: replace the list of `service` (`kind`
+ * ZK_TOP_*); ids are host dictionary ids of the annotation values / keys, in list order. */
+zk_status zk_store_put_top(zk_store* st, uint32_t kind, uint32_t service, const uint64_t* ids, uint64_t n);
+/* getTopAnnotations / getTopKeyValueAnnotations: two-phase like get_dependencies; a service
+ * without a stored list yields 0 entries (Seq.empty). */
+zk_status zk_store_get_top(zk_store* st, uint32_t kind, uint32_t service, uint64_t* ids, uint64_t cap, uint64_t* n);
+
+/* algebird MomentsGroup.plus (DependencyLink.sg.plus, Dependencies.scala:38-43) */
+zk_status zk_moments_plus(const zk_moments* a, const zk_moments* b, zk_moments* out);
+
+/* The job's output record: the present cells of a finalized HOST link table (zk_deps_finalize
+ * with device_ptrs = 0) as DependencyLinks, cell order (parent-major). Two-phase like above.
+ * ZipkinAggregateJob.scala:41-43 wraps them in Dependencies(Time(0), Time.now, links); when there
+ * is no link the job emits nothing and storeDependencies is not called (:43-45). */
+zk_status zk_link_table_compact(const zk_link_table* table, uint32_t num_services, zk_dep_link* out, uint64_t cap,
+                                uint64_t* n_links);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ZKSTORE_H */

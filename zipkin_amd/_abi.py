@@ -156,6 +156,22 @@ class zk_kv_config(C.Structure):
     ]
 
 
+class zk_moments(C.Structure):
+    _fields_ = [("m0", C.c_int64), ("m1", C.c_double), ("m2", C.c_double), ("m3", C.c_double), ("m4", C.c_double)]
+
+
+class zk_dep_link(C.Structure):
+    _fields_ = [("parent", C.c_uint32), ("child", C.c_uint32), ("moments", zk_moments)]
+
+
+ZK_STORE_ANORM = 0
+ZK_STORE_SUMMED = 1
+ZK_TOP_ANNOTATIONS = 0
+ZK_TOP_KV_ANNOTATIONS = 1
+ZK_TIME_TOP = 2**63 - 1
+ZK_TIME_BOTTOM = -(2**63)
+
+
 # every symbol include/*.h declares: (name, restype, argtypes)
 _P = C.c_void_p
 _U64P = C.POINTER(C.c_uint64)
@@ -199,6 +215,22 @@ _SIGNATURES = [
     ("zk_kv_partial", C.c_int, [_P, C.POINTER(_P), _U64P, C.POINTER(_P), _U64P]),
     ("zk_kv_candidates", C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), _U64P, _U64P]),
     ("zk_kv_merge_candidates", C.c_int, [_P, _P, _P, C.c_uint32]),
+    # include/zkstore.h: the Aggregates store surface (host side)
+    ("zk_store_create", C.c_int, [C.c_uint32, C.POINTER(_P)]),
+    ("zk_store_destroy", C.c_int, [_P]),
+    ("zk_store_last_error", C.c_char_p, [_P]),
+    ("zk_store_put_dependencies", C.c_int, [_P, C.c_int64, C.c_int64, _P, C.c_uint64]),
+    (
+        "zk_store_get_dependencies",
+        C.c_int,
+        [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.c_int64, _P, C.c_uint64, _U64P,
+         C.POINTER(C.c_int64), C.POINTER(C.c_int64)],
+    ),
+    ("zk_store_count", C.c_int, [_P, _U64P]),
+    ("zk_store_put_top", C.c_int, [_P, C.c_uint32, C.c_uint32, _P, C.c_uint64]),
+    ("zk_store_get_top", C.c_int, [_P, C.c_uint32, C.c_uint32, _P, C.c_uint64, _U64P]),
+    ("zk_moments_plus", C.c_int, [C.POINTER(zk_moments), C.POINTER(zk_moments), C.POINTER(zk_moments)]),
+    ("zk_link_table_compact", C.c_int, [C.POINTER(zk_link_table), C.c_uint32, _P, C.c_uint64, _U64P]),
 ]
 
 SYMBOLS = [s[0] for s in _SIGNATURES]

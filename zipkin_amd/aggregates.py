@@ -1,0 +1,380 @@
+"""Host mirror of the reference's Aggregates surface over libzkagg (include/zkstore.h, zkagg.h).
+
+Same names, argument meaning and error behaviour as
+  trait Aggregates            zipkin-common/.../storage/Aggregates.scala:26-37
+  class NullAggregates        Aggregates.scala:39-50
+  Service / DependencyLink / Dependencies   zipkin-common/.../common/Dependencies.scala:25-83
+  algebird Moments            (algebird-core 0.8.1; accessors as zipkin-web momentAnnotations.js:5-19)
+and a driver for the job itself (ZipkinAggregateJob.scala:20-45) that runs the device path and hands
+its single Dependencies record to `storeDependencies`.
+
+Times are microseconds since the epoch (Time.inMicroseconds, zipkinDependencies.thrift:40-41).
+The reference's failed Futures are raised here as ZkError (the C status) or AssertionError
+(DependencyLink.sg's key assert, Dependencies.scala:40). Moments arithmetic runs in the library
+(zk_moments_plus); nothing here computes on the CPU what the device path produces.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import time
+from dataclasses import dataclass, field
+from typing import Dict, Iterable, List, NamedTuple, Optional, Sequence
+
+import numpy as np
+
+from . import _abi
+
+DAY_US = 86_400 * 1_000_000
+
+
+def now_us() -> int:
+    return time.time_ns() // 1000
+
+
+class Moments(NamedTuple):
+    """algebird Moments(m0 = count, m1 = mean, m2..m4 = central moment sums)."""
+
+    m0: int
+    m1: float
+    m2: float
+    m3: float
+    m4: float
+
+    @staticmethod
+    def of(value: float) -> "Moments":  # Moments(value) (ZipkinAggregateJob.scala:35)
+        return Moments(1, float(value), 0.0, 0.0, 0.0)
+
+    @staticmethod
+    def zero() -> "Moments":
+        return Moments(0, 0.0, 0.0, 0.0, 0.0)
+
+    def plus(self, other: "Moments") -> "Moments":
+        """MomentsGroup.plus (through zk_moments_plus)."""
+        out = _abi.zk_moments()
+        st = _abi.lib().zk_moments_plus(C.byref(_to_c(self)), C.byref(_to_c(other)), C.byref(out))
+        if st != _abi.ZK_OK:
+            raise _abi.ZkError(st, _abi.status_str(st))
+        return _from_c(out)
+
+    # momentAnnotations.js:6-11
+    @property
+    def count(self) -> int:
+        return self.m0
+
+    @property
+    def mean(self) -> float:
+        return self.m1
+
+    @property
+    def variance(self) -> float:
+        return self.m2 / self.m0
+
+    @property
+    def stddev(self) -> float:
+        return self.variance ** 0.5
+
+    @property
+    def skewness(self) -> float:
+        return (self.m0 ** 0.5) * self.m3 / (self.m2 ** 1.5)
+
+    @property
+    def kurtosis(self) -> float:
+        return self.m0 * self.m4 / (self.m2 ** 2) - 3
+
+
+def _to_c(m: Moments) -> "_abi.zk_moments":
+    return _abi.zk_moments(int(m.m0), float(m.m1), float(m.m2), float(m.m3), float(m.m4))
+
+
+def _from_c(m) -> Moments:
+    return Moments(int(m.m0), float(m.m1), float(m.m2), float(m.m3), float(m.m4))
+
+
+@dataclass(frozen=True)
+class Service:
+    name: str  # case-sensitive (DependenciesTest.scala:28-40)
+
+
+@dataclass(frozen=True)
+class DependencyLink:
+    parent: Service
+    child: Service
+    duration_moments: Moments
+
+    def plus(self, r: "DependencyLink") -> "DependencyLink":
+        """DependencyLink.sg.plus (Dependencies.scala:38-43)."""
+        assert self.child == r.child and self.parent == r.parent
+        return DependencyLink(self.parent, self.child, self.duration_moments.plus(r.duration_moments))
+
+
+@dataclass(frozen=True)
+class Dependencies:
+    start_time: int
+    end_time: int
+    links: tuple = field(default_factory=tuple)
+
+    @staticmethod
+    def zero() -> "Dependencies":  # Dependencies.scala:81 (Time.Top, Time.Bottom)
+        return Dependencies(_abi.ZK_TIME_TOP, _abi.ZK_TIME_BOTTOM, ())
+
+    def plus(self, r: "Dependencies") -> "Dependencies":
+        """Dependencies.monoid.plus(l = self, r) (Dependencies.scala:68-79)."""
+        lmap = {(l.parent, l.child): l for l in self.links}
+        rmap = {(l.parent, l.child): l for l in r.links}
+        merged = dict(rmap)
+        for k, l in lmap.items():  # Monoid.plus(rLinkMap, lLinkMap): sg.plus(r, l) on shared keys
+            merged[k] = merged[k].plus(l) if k in merged else l
+        return Dependencies(min(r.start_time, self.start_time), max(r.end_time, self.end_time),
+                            tuple(merged.values()))
+
+
+class Dictionary:
+    """Host-owned string <-> id dictionary (service names, annotation values / keys)."""
+
+    def __init__(self, names: Iterable[str] = ()):
+        self._ids: Dict[str, int] = {}
+        self._names: List[str] = []
+        for n in names:
+            self.id(n)
+
+    def id(self, name: str) -> int:
+        i = self._ids.get(name)
+        if i is None:
+            i = len(self._names)
+            self._ids[name] = i
+            self._names.append(name)
+        return i
+
+    def get(self, name: str) -> Optional[int]:
+        return self._ids.get(name)
+
+    def name(self, i: int) -> str:
+        return self._names[i]
+
+    def __len__(self) -> int:
+        return len(self._names)
+
+    def __contains__(self, name: str) -> bool:
+        return name in self._ids
+
+
+class Aggregates:
+    """trait Aggregates (Aggregates.scala:26-37)."""
+
+    def close(self) -> None:
+        raise NotImplementedError
+
+    def getDependencies(self, startDate: Optional[int], endDate: Optional[int] = None) -> Dependencies:
+        raise NotImplementedError
+
+    def storeDependencies(self, dependencies: Dependencies) -> None:
+        raise NotImplementedError
+
+    def getTopAnnotations(self, serviceName: str) -> List[str]:
+        raise NotImplementedError
+
+    def getTopKeyValueAnnotations(self, serviceName: str) -> List[str]:
+        raise NotImplementedError
+
+    def storeTopAnnotations(self, serviceName: str, a: Sequence[str]) -> None:
+        raise NotImplementedError
+
+    def storeTopKeyValueAnnotations(self, serviceName: str, a: Sequence[str]) -> None:
+        raise NotImplementedError
+
+
+class NullAggregates(Aggregates):
+    """NullAggregates (Aggregates.scala:39-50)."""
+
+    def close(self) -> None:
+        pass
+
+    def getDependencies(self, startDate=None, endDate=None) -> Dependencies:
+        return Dependencies.zero()
+
+    def storeDependencies(self, dependencies) -> None:
+        pass
+
+    def getTopAnnotations(self, serviceName) -> List[str]:
+        return []
+
+    def getTopKeyValueAnnotations(self, serviceName) -> List[str]:
+        return []
+
+    def storeTopAnnotations(self, serviceName, a) -> None:
+        pass
+
+    def storeTopKeyValueAnnotations(self, serviceName, a) -> None:
+        pass
+
+
+class GpuAggregates(Aggregates):
+    """Aggregates over a zk_store: mode "anorm" (AnormAggregates window/row semantics) or
+    "summed" (Cassandra/HBase: contained rows Monoid-summed into one Dependencies).
+
+    `clock` supplies Time.now in us (tests pin it)."""
+
+    def __init__(self, mode: str = "anorm", services: Optional[Dictionary] = None,
+                 annotations: Optional[Dictionary] = None, clock=now_us):
+        self._L = _abi.lib()
+        m = {"anorm": _abi.ZK_STORE_ANORM, "summed": _abi.ZK_STORE_SUMMED}[mode]
+        h = C.c_void_p()
+        st = self._L.zk_store_create(m, C.byref(h))
+        if st != _abi.ZK_OK:
+            raise _abi.ZkError(st, _abi.status_str(st))
+        self._h = h
+        self.mode = mode
+        self.services = services if services is not None else Dictionary()
+        self.annotations = annotations if annotations is not None else Dictionary()
+        self.clock = clock
+
+    def _check(self, st: int) -> None:
+        if st != _abi.ZK_OK:
+            raise _abi.ZkError(st, self._L.zk_store_last_error(self._h).decode() or _abi.status_str(st))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.zk_store_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- dependencies -------------------------------------------------------------------------
+    def storeDependencies(self, dependencies: Dependencies) -> None:
+        n = len(dependencies.links)
+        arr = (_abi.zk_dep_link * max(n, 1))()
+        for i, l in enumerate(dependencies.links):
+            arr[i] = _abi.zk_dep_link(self.services.id(l.parent.name), self.services.id(l.child.name),
+                                      _to_c(l.duration_moments))
+        self._check(self._L.zk_store_put_dependencies(self._h, int(dependencies.start_time),
+                                                      int(dependencies.end_time), arr, n))
+
+    def getDependencies(self, startDate: Optional[int], endDate: Optional[int] = None) -> Dependencies:
+        s = C.c_int64(startDate) if startDate is not None else None
+        e = C.c_int64(endDate) if endDate is not None else None
+        now = int(self.clock())
+        n = C.c_uint64()
+        rs, re_ = C.c_int64(), C.c_int64()
+        sp = C.byref(s) if s is not None else None
+        ep = C.byref(e) if e is not None else None
+        self._check(self._L.zk_store_get_dependencies(self._h, sp, ep, now, None, 0, C.byref(n), None, None))
+        arr = (_abi.zk_dep_link * max(n.value, 1))()
+        self._check(self._L.zk_store_get_dependencies(self._h, sp, ep, now, arr, n.value, C.byref(n),
+                                                      C.byref(rs), C.byref(re_)))
+        links = tuple(
+            DependencyLink(Service(self.services.name(arr[i].parent)), Service(self.services.name(arr[i].child)),
+                           _from_c(arr[i].moments))
+            for i in range(n.value)
+        )
+        return Dependencies(int(rs.value), int(re_.value), links)
+
+    def count(self) -> int:
+        n = C.c_uint64()
+        self._check(self._L.zk_store_count(self._h, C.byref(n)))
+        return int(n.value)
+
+    # -- top annotations ----------------------------------------------------------------------
+    def _put_top(self, kind: int, serviceName: str, a: Sequence[str]) -> None:
+        ids = np.array([self.annotations.id(x) for x in a], dtype=np.uint64)
+        self._check(self._L.zk_store_put_top(self._h, kind, self.services.id(serviceName),
+                                             ids.ctypes.data if len(ids) else None, len(ids)))
+
+    def _get_top(self, kind: int, serviceName: str) -> List[str]:
+        svc = self.services.get(serviceName)
+        if svc is None:
+            return []
+        n = C.c_uint64()
+        self._check(self._L.zk_store_get_top(self._h, kind, svc, None, 0, C.byref(n)))
+        ids = np.zeros(max(n.value, 1), np.uint64)
+        self._check(self._L.zk_store_get_top(self._h, kind, svc, ids.ctypes.data, n.value, C.byref(n)))
+        return [self.annotations.name(int(i)) for i in ids[: n.value]]
+
+    def storeTopAnnotations(self, serviceName: str, a: Sequence[str]) -> None:
+        self._put_top(_abi.ZK_TOP_ANNOTATIONS, serviceName, a)
+
+    def storeTopKeyValueAnnotations(self, serviceName: str, a: Sequence[str]) -> None:
+        self._put_top(_abi.ZK_TOP_KV_ANNOTATIONS, serviceName, a)
+
+    def getTopAnnotations(self, serviceName: str) -> List[str]:
+        return self._get_top(_abi.ZK_TOP_ANNOTATIONS, serviceName)
+
+    def getTopKeyValueAnnotations(self, serviceName: str) -> List[str]:
+        return self._get_top(_abi.ZK_TOP_KV_ANNOTATIONS, serviceName)
+
+
+def links_from_table(table, services: Dictionary) -> tuple:
+    """The present cells of a finalized host LinkTable as DependencyLinks (zk_link_table_compact)."""
+    L = _abi.lib()
+    S = table.num_services
+    t = _abi.zk_link_table()
+    t.m0, t.m1, t.m2, t.m3, t.m4 = (a.ctypes.data for a in (table.m0, table.m1, table.m2, table.m3, table.m4))
+    t.present = table.present.ctypes.data
+    t.device_ptrs = 0
+    n = C.c_uint64()
+    st = L.zk_link_table_compact(C.byref(t), S, None, 0, C.byref(n))
+    if st != _abi.ZK_OK:
+        raise _abi.ZkError(st, _abi.status_str(st))
+    arr = (_abi.zk_dep_link * max(n.value, 1))()
+    st = L.zk_link_table_compact(C.byref(t), S, arr, n.value, C.byref(n))
+    if st != _abi.ZK_OK:
+        raise _abi.ZkError(st, _abi.status_str(st))
+    return tuple(
+        DependencyLink(Service(services.name(arr[i].parent)), Service(services.name(arr[i].child)),
+                       _from_c(arr[i].moments))
+        for i in range(n.value)
+    )
+
+
+class ZipkinAggregateJob:
+    """ZipkinAggregateJob.scala:10-46 with the compute on the device.
+
+    run(batches) accumulates trace-clustered column batches (one record per stored span fragment,
+    service ids from `services`), finalizes, and returns Dependencies(Time(0), Time.now, links) --
+    or None when there is no link, in which case the reference writes nothing (:43-45). With an
+    `aggregates` sink the record is stored through storeDependencies (StorageRecordWriter.scala:13-17).
+    """
+
+    def __init__(self, services: Dictionary, *, device: int = 0, strict: bool = True,
+                 aggregates: Optional[Aggregates] = None, clock=now_us):
+        self.services = services
+        self.device = device
+        self.strict = strict
+        self.aggregates = aggregates
+        self.clock = clock
+        self.stats: dict = {}
+
+    def run(self, batches, num_services: Optional[int] = None) -> Optional[Dependencies]:
+        from .columns import SpanColumns
+        from .context import DepsContext
+
+        if isinstance(batches, SpanColumns) or hasattr(batches, "abi"):
+            batches = [batches]
+        S = num_services or max(1, len(self.services))
+        with DepsContext(S, device=self.device, strict=self.strict) as ctx:
+            for b in batches:
+                ctx.accumulate(b)
+            table = ctx.finalize()
+            self.stats = ctx.stats()
+        links = links_from_table(table, self.services)
+        if not links:
+            return None
+        deps = Dependencies(0, int(self.clock()), links)  # Time.fromMilliseconds(0), Time.now (:41-42)
+        if self.aggregates is not None:
+            self.aggregates.storeDependencies(deps)
+        return deps
+
+
+def publish_top_kv(sketch, aggregates: GpuAggregates, keys: Dict[int, str], k: int = 10) -> None:
+    """The removed producer of storeTopKeyValueAnnotations (CHANGELOG:7-8): the device count-min
+    top-K of every service, key hashes mapped back to key strings by `keys` ({hash: key}), stored
+    per service as the reference's per-service list (CassandraAggregates.scala:100-102)."""
+    kk, est, cnt = sketch.topk_all(k)
+    for s in range(sketch.num_services):
+        if cnt[s] == 0 or s >= len(aggregates.services):
+            continue
+        names = [keys[int(h)] for h in kk[s][: cnt[s]]]
+        aggregates.storeTopKeyValueAnnotations(aggregates.services.name(s), names)

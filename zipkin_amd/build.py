@@ -18,9 +18,10 @@ SOURCES = [
     "zk_partition.hip",
     "zk_kv.hip",
     "zk_kv_api.cpp",
+    "zk_store.cpp",
 ]
 HEADERS = ["zk_internal.h", "zk_tracegen.h", "zk_sketch_internal.h"]
-PUBLIC_HEADERS = ["zkagg.h", "zksketch.h"]
+PUBLIC_HEADERS = ["zkagg.h", "zksketch.h", "zkstore.h"]
 LIB = PKG / "libzkagg.so"
 ARCH = os.environ.get("ZK_OFFLOAD_ARCH", "gfx950")
 
@@ -40,23 +41,35 @@ def needs_build() -> bool:
     return any(d.stat().st_mtime > t for d in deps)
 
 
+def _flags() -> list[str]:
+    return [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result", "-Wno-unused-value",
+            f"-I{ROOT / 'include'}"]
+
+
 def build(force: bool = False, verbose: bool = False) -> Path:
+    """Compile every source to an object in build/ (in parallel, only what changed), then link."""
     if not force and not needs_build():
         return LIB
-    cmd = [
-        _hipcc(),
-        f"--offload-arch={ARCH}",
-        "-O3",
-        "-fPIC",
-        "-shared",
-        "-std=c++17",
-        "-Wno-unused-result",
-        "-Wno-unused-value",
-        f"-I{ROOT / 'include'}",
-        *[str(CSRC / s) for s in SOURCES],
-        "-o",
-        str(LIB) + ".tmp",
-    ]
+    from concurrent.futures import ThreadPoolExecutor
+
+    objdir = ROOT / "build" / "zkagg"
+    objdir.mkdir(parents=True, exist_ok=True)
+    hdr_t = max((CSRC / h).stat().st_mtime for h in HEADERS)
+    hdr_t = max([hdr_t] + [(ROOT / "include" / h).stat().st_mtime for h in PUBLIC_HEADERS])
+
+    def compile_one(src: str) -> Path:
+        obj = objdir / (src + ".o")
+        if force or not obj.exists() or obj.stat().st_mtime < max(hdr_t, (CSRC / src).stat().st_mtime):
+            cmd = [_hipcc(), *_flags(), "-c", str(CSRC / src), "-o", str(obj) + ".tmp"]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            subprocess.run(cmd, check=True)
+            os.replace(str(obj) + ".tmp", obj)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *[str(o) for o in objs], "-o", str(LIB) + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
