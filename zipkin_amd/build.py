@@ -46,13 +46,17 @@ def _flags() -> list[str]:
             f"-I{ROOT / 'include'}"]
 
 
-def build(force: bool = False, verbose: bool = False) -> Path:
-    """Compile every source to an object in build/ (in parallel, only what changed), then link."""
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, variant: str = "", defines=()) -> Path:
+    """Compile every source to an object in build/ (in parallel, only what changed), then link.
+
+    variant/defines: a diagnostic build (e.g. "stamps", ["ZK_STAMPS"]) into libzkagg_<variant>.so;
+    the product library is always the plain build."""
+    lib = PKG / f"libzkagg_{variant}.so" if variant else LIB
+    if not variant and not force and not needs_build():
         return LIB
     from concurrent.futures import ThreadPoolExecutor
 
-    objdir = ROOT / "build" / "zkagg"
+    objdir = ROOT / "build" / ("zkagg_" + variant if variant else "zkagg")
     objdir.mkdir(parents=True, exist_ok=True)
     hdr_t = max((CSRC / h).stat().st_mtime for h in HEADERS)
     hdr_t = max([hdr_t] + [(ROOT / "include" / h).stat().st_mtime for h in PUBLIC_HEADERS])
@@ -60,7 +64,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     def compile_one(src: str) -> Path:
         obj = objdir / (src + ".o")
         if force or not obj.exists() or obj.stat().st_mtime < max(hdr_t, (CSRC / src).stat().st_mtime):
-            cmd = [_hipcc(), *_flags(), "-c", str(CSRC / src), "-o", str(obj) + ".tmp"]
+            cmd = [_hipcc(), *_flags(), *[f"-D{d}" for d in defines], "-c", str(CSRC / src), "-o", str(obj) + ".tmp"]
             if verbose:
                 print(" ".join(cmd), file=sys.stderr)
             subprocess.run(cmd, check=True)
@@ -69,13 +73,16 @@ def build(force: bool = False, verbose: bool = False) -> Path:
 
     with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
         objs = list(ex.map(compile_one, SOURCES))
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *[str(o) for o in objs], "-o", str(LIB) + ".tmp"]
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *[str(o) for o in objs], "-o", str(lib) + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(str(LIB) + ".tmp", LIB)
-    return LIB
+    os.replace(str(lib) + ".tmp", lib)
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    if "--stamps" in sys.argv:
+        print(build(verbose=True, variant="stamps", defines=["ZK_STAMPS"]))
+    else:
+        print(build(force="--force" in sys.argv, verbose=True))

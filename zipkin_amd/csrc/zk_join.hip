@@ -23,6 +23,36 @@ namespace {
 
 constexpr int kSpillWG = 256;
 
+// ---- diagnostic phase stamps (separate build with -DZK_STAMPS; never in the product .so) -------
+#ifdef ZK_STAMPS
+__device__ unsigned long long g_zk_stamps[16];
+__device__ __forceinline__ unsigned long long zk_memtime() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define ZK_STAMP_DECL                                 \
+    unsigned long long zk_t_prev = zk_memtime();      \
+    unsigned long long zk_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define ZK_STAMP(k)                                   \
+    do {                                              \
+        const unsigned long long zk_t = zk_memtime(); \
+        zk_acc[k] += zk_t - zk_t_prev;                \
+        zk_t_prev = zk_t;                             \
+    } while (0)
+#define ZK_STAMP_FLUSH()                                                              \
+    do {                                                                              \
+        if ((threadIdx.x & 63) == 0)                                                  \
+            for (int q = 0; q < 8; ++q) atomicAdd(&g_zk_stamps[q], zk_acc[q]);        \
+    } while (0)
+#else
+#define ZK_STAMP_DECL
+#define ZK_STAMP(k)
+#define ZK_STAMP_FLUSH()
+#endif
+
 __device__ __forceinline__ uint32_t slot_hash(uint64_t sid, uint32_t seg) {
     uint64_t x = sid ^ ((uint64_t)(seg + 1) * 0x9E3779B97F4A7C15ull);
     x ^= x >> 33;
@@ -155,6 +185,13 @@ __device__ __forceinline__ uint32_t frag_bits(uint32_t f, uint32_t* once) {
 }
 __device__ __forceinline__ bool slot_valid(uint32_t w) { return ((w >> kSlotB) & 0xFu) == 0u; }
 
+// a wave-uniform lane's 64-bit value into scalar registers
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ uint64_t spread32(uint32_t x) {
     uint64_t v = x;
     v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
@@ -242,7 +279,7 @@ __device__ __forceinline__ void load_window(const JoinArgs& a, uint64_t ws, Wind
 // "seen >= 2" for cs, cr, sr, ss (Span.isValid = no ">= 2" bit); bit 20 some fragment has a
 // parentId, bit 21 some fragment has none.
 // =============================================================================================
-template <int TILE, int WG>
+template <int TILE, int WG, int ABL>
 __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
     constexpr int H = 2 * TILE;
     constexpr int NWORD = TILE / 64;
@@ -269,6 +306,7 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
     }
     const uint64_t R1 = (R0 + a.per_wg < n) ? R0 + a.per_wg : n;
     uint64_t* __restrict__ out = a.links + (uint64_t)blockIdx.x * a.link_stride;
+    const uint64_t trash = a.link_stride - 1;  // never a real link slot (join_geometry)
     uint32_t nout = 0;        // links written by this workgroup (uniform)
     uint64_t nrec = 0;        // records aggregated (uniform)
     StatPack32 st;
@@ -279,6 +317,7 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
     uint64_t seek = R0;       // first record that may start one of our traces
     Window cur, nxt;
     load_window(a, ws, cur);
+    ZK_STAMP_DECL
     for (;;) {
         const int wn = (int)((n - ws) < (uint64_t)TILE ? (n - ws) : (uint64_t)TILE);
         // ---- 1. trace boundaries of the window -------------------------------------------------
@@ -294,24 +333,31 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
             }
         }
         __syncthreads();
+        ZK_STAMP(0);
         // ---- 2. which records are ours, where the next window starts (uniform) ----------------
         const int lo_j = (int)(seek - ws);
         const int r1_j = (R1 - ws < (uint64_t)wn) ? (int)(R1 - ws) : wn;
-        int start = -1, stop = -1, last_b = -1;
-#pragma unroll
-        for (int w = 0; w < NWORD; ++w) {
-            const uint64_t x = s_mask[w];
-            if (!x) continue;
-            last_b = 64 * w + 63 - (int)__clzll((long long)x);
-            // first boundary >= lo_j and first boundary >= r1_j
-            const int base = 64 * w;
-            if (start < 0 && base + 63 >= lo_j) {
-                const uint64_t y = lo_j > base ? (x & (~0ull << (lo_j - base))) : x;
-                if (y) start = base + (int)__ffsll((unsigned long long)y) - 1;
+        // wave-parallel over the NWORD mask words (lane w holds word w): the first boundary >= lo_j
+        // (start), the first >= r1_j (stop) and the last boundary of the window (last_b)
+        int start = -1, stop = -1, last_b = -1;  // wave-uniform (SGPRs)
+        {
+            static_assert(NWORD <= 64, "one mask word per lane");
+            const int base = 64 * lane;
+            const uint64_t x = lane < NWORD ? s_mask[lane] : 0ull;
+            const uint64_t ys = lo_j >= base + 64 ? 0ull : (lo_j > base ? (x & (~0ull << (lo_j - base))) : x);
+            const uint64_t yt = r1_j >= base + 64 ? 0ull : (r1_j > base ? (x & (~0ull << (r1_j - base))) : x);
+            const uint64_t bs = __ballot(ys != 0ull), bt = __ballot(yt != 0ull), bl = __ballot(x != 0ull);
+            if (bs) {
+                const int w = __ffsll((unsigned long long)bs) - 1;
+                start = 64 * w + __ffsll((unsigned long long)readlane64(ys, w)) - 1;
             }
-            if (stop < 0 && base + 63 >= r1_j) {
-                const uint64_t y = r1_j > base ? (x & (~0ull << (r1_j - base))) : x;
-                if (y) stop = base + (int)__ffsll((unsigned long long)y) - 1;
+            if (bt) {
+                const int w = __ffsll((unsigned long long)bt) - 1;
+                stop = 64 * w + __ffsll((unsigned long long)readlane64(yt, w)) - 1;
+            }
+            if (bl) {
+                const int w = 63 - (int)__clzll((long long)bl);
+                last_b = 64 * w + 63 - (int)__clzll((long long)readlane64(x, w));
             }
         }
         const bool at_end = ws + (uint64_t)wn >= n;
@@ -348,8 +394,9 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
         if (!done && next_seek >= R1) done = true;
         const uint64_t next_ws = next_seek & ~1ull;
         load_window(a, done ? ws : next_ws, nxt);  // in flight during the LDS phases below (unconditional: see ld2)
+        ZK_STAMP(1);
         nrec += (uint64_t)(m - start);
-        if (a.ablate != 2) {  // diagnostic: 2 = stream windows only
+        if constexpr (ABL != 2) {  // diagnostic build: 2 = stream windows only
 
         // ---- 3. segment ids and LDS staging ----------------------------------------------------
         int r_seg[2];
@@ -379,6 +426,7 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
         }
         for (int x = tid; x < H; x += WG) s_ht[x] = 0u;
         __syncthreads();
+        ZK_STAMP(2);
 
         // ---- 4. groupBy((id, traceId)): the first fragment to claim a slot leads --------------
         int r_leader[2];
@@ -411,6 +459,7 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
             }
         }
         __syncthreads();
+        ZK_STAMP(3);
 
         // ---- 5. reduce(mergeSpan) ------------------------------------------------------------------
 #pragma unroll
@@ -433,6 +482,7 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
             }
         }
         __syncthreads();
+        ZK_STAMP(4);
 
         // ---- 6. filter(isValid), join on (parentId, traceId), (cell, duration) links ----------
         uint64_t r_link[2];
@@ -488,9 +538,10 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
             }
             const uint64_t cell = (uint64_t)(sp & kSvcIdMask) * a.S + (sL & kSvcIdMask);
             r_link[e] = (cell << 40) | d;
-            if (a.nb && !a.ablate) atomicAdd(&s_hist[cell >> a.cb_shift], 1u);
+            if (a.nb && ABL == 0) atomicAdd(&s_hist[cell >> a.cb_shift], 1u);
             ++nl;
         }
+        ZK_STAMP(5);
         // ---- 7. append the window's links to this workgroup's list -----------------------------
         uint32_t incl = nl;
 #pragma unroll
@@ -507,20 +558,28 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
             if (w2 < wave) base += v;
             total += v;
         }
-        if (!a.ablate) {
+        if constexpr (ABL == 0) {
+            // exactly two stores per thread on every path (absent links go to the list's trash
+            // slot), so the loop-end wait for the prefetched window can count them: vmcnt(2)
             uint32_t pos = nout + base + incl - nl;
 #pragma unroll
-            for (int e = 0; e < 2; ++e)
-                if (r_link[e] != ~0ull) out[pos++] = r_link[e];
+            for (int e = 0; e < 2; ++e) {
+                const bool v = r_link[e] != ~0ull;
+                out[v ? (uint64_t)pos : trash] = r_link[e];
+                pos += v ? 1u : 0u;
+            }
             nout += total;
         }
+        ZK_STAMP(6);
         }  // ablate != 2
         if (done) break;
         ws = next_ws;
         seek = next_seek;
         cur = nxt;
         __syncthreads();  // s_wsum / s_mask reuse
+        ZK_STAMP(7);
     }
+    ZK_STAMP_FLUSH();
     if (tid == 0) {
         a.link_count[blockIdx.x] = nout;
         atomicAdd(&a.stats[(uint64_t)(blockIdx.x % kStatShards) * ST_N + ST_RECORDS], (unsigned long long)nrec);
@@ -767,7 +826,12 @@ uint64_t spill_scratch_bytes_per_wg(uint32_t max_trace) {
 
 hipError_t launch_join(const JoinArgs& a, hipStream_t s) {
     if (a.c.n == 0) return hipSuccess;
-    hipLaunchKernelGGL((k_span_join_stream<kTile, kTileWG>), dim3((unsigned)a.grid), dim3(kTileWG), 0, s, a);
+    if (a.ablate == 1)
+        hipLaunchKernelGGL((k_span_join_stream<kTile, kTileWG, 1>), dim3((unsigned)a.grid), dim3(kTileWG), 0, s, a);
+    else if (a.ablate == 2)
+        hipLaunchKernelGGL((k_span_join_stream<kTile, kTileWG, 2>), dim3((unsigned)a.grid), dim3(kTileWG), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_span_join_stream<kTile, kTileWG, 0>), dim3((unsigned)a.grid), dim3(kTileWG), 0, s, a);
     return hipGetLastError();
 }
 
@@ -779,6 +843,17 @@ hipError_t launch_spill(const JoinArgs& a, uint32_t spill_wgs, hipStream_t s) {
 
 uint64_t join_tile_records() { return kTile; }
 
+#ifdef ZK_STAMPS
+extern "C" int zk_debug_stamps(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_zk_stamps), 16 * 8) != hipSuccess) return 1;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_zk_stamps), z, sizeof(z)) != hipSuccess) return 1;
+    }
+    return 0;
+}
+#endif
+
 void join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, uint64_t* link_stride) {
     const uint64_t windows = (n + kTile - 1) / kTile;
     uint64_t g = (uint64_t)cus * 4;  // four resident workgroups per CU (<= 128 VGPRs, 23 KB LDS)
@@ -786,7 +861,8 @@ void join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, u
     const uint64_t per = ((n + g - 1) / g + kTile - 1) / kTile * kTile;
     *grid = (uint32_t)g;
     *per_wg = per ? per : kTile;
-    *link_stride = *per_wg + kTile;  // a workgroup's last trace may overhang its range by < TILE
+    // a workgroup's last trace may overhang its range by < TILE; +1: the trash slot of K1's stores
+    *link_stride = *per_wg + kTile + 1;
 }
 
 }  // namespace zk
