@@ -429,33 +429,50 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
         ZK_STAMP(2);
 
         // ---- 4. groupBy((id, traceId)): the first fragment to claim a slot leads --------------
+        // Both records of the thread probe together (one LDS round trip per step for the pair).
         int r_leader[2];
         uint32_t r_slot[2];
+        {
+            bool act[2];
+            uint32_t word[2];
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            r_leader[e] = -1;
-            r_slot[e] = 0;
-            if (r_seg[e] >= 0) {
-                const int j = 2 * tid + e;
-                const uint64_t sid = cur.sid[e];
-                const uint16_t seg = (uint16_t)r_seg[e];
+            for (int e = 0; e < 2; ++e) {
+                r_leader[e] = -1;
+                act[e] = r_seg[e] >= 0;
+                r_slot[e] = slot_hash(cur.sid[e], (uint32_t)(r_seg[e] & 0xFFFF)) & (H - 1);
                 uint32_t once;
-                const uint32_t bits = frag_bits(cur.flags[e], &once);
-                uint32_t slot = slot_hash(sid, seg) & (H - 1);
-                for (;;) {
-                    const uint32_t old = atomicCAS(&s_ht[slot], 0u, (uint32_t)(j + 1) | bits);
-                    if (old == 0u) {
-                        r_leader[e] = j;
-                        break;
+                word[e] = (uint32_t)(2 * tid + e + 1) | frag_bits(cur.flags[e], &once);
+            }
+            while (act[0] || act[1]) {
+                uint32_t old[2];
+#pragma unroll
+                for (int e = 0; e < 2; ++e) old[e] = act[e] ? atomicCAS(&s_ht[r_slot[e]], 0u, word[e]) : 0u;
+                int o[2];
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    o[e] = (int)(old[e] & kSlotIdx) - 1;
+                    if (act[e] && old[e] == 0u) {
+                        r_leader[e] = 2 * tid + e;
+                        act[e] = false;
                     }
-                    const int o = (int)(old & kSlotIdx) - 1;
-                    if (s_sid[o] == sid && s_seg[o] == seg) {
-                        r_leader[e] = o;
-                        break;
-                    }
-                    slot = (slot + 1) & (H - 1);
                 }
-                r_slot[e] = slot;
+                uint64_t osid[2];
+                uint16_t oseg[2];
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    osid[e] = act[e] ? s_sid[o[e]] : 0ull;
+                    oseg[e] = act[e] ? s_seg[o[e]] : (uint16_t)0;
+                }
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    if (!act[e]) continue;
+                    if (osid[e] == cur.sid[e] && oseg[e] == (uint16_t)r_seg[e]) {
+                        r_leader[e] = o[e];
+                        act[e] = false;
+                    } else {
+                        r_slot[e] = (r_slot[e] + 1) & (H - 1);
+                    }
+                }
             }
         }
         __syncthreads();
