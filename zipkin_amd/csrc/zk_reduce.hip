@@ -109,64 +109,117 @@ __global__ __launch_bounds__(1024) void k_bucket_base(uint64_t* __restrict__ bas
     if (b == 0) base[nb] = tot;
 }
 
-__global__ __launch_bounds__(256) void k_link_scatter(ReduceArgs r) {
-    constexpr int U = 8;  // links per thread in flight
-    __shared__ uint32_t s_cur[kMaxBuckets];
+// K2c: one workgroup per K1 list. Chunks of C links are counting-sorted by bucket in LDS and
+// written out in sorted order, and each bucket's tail that does not yet fill a 64-byte line stays
+// in an LDS carry until the next chunk completes it: every line of the output is written whole,
+// from one workgroup, within one chunk (the per-link version wrote 64 scattered 8-byte words per
+// store instruction, at ~2.3x write amplification in WRITE_SIZE).
+constexpr int kScatterLine = 8;  // links per 64-byte line (128-byte lines: 4% less WRITE_SIZE, but
+                                 // their LDS carry halves the resident workgroups: 1.4x slower)
+template <int U, int WG>
+__global__ __launch_bounds__(WG) void k_link_scatter(ReduceArgs r) {
+    constexpr int C = WG * U;
+    __shared__ uint32_t s_cur[kMaxBuckets];   // output position of each bucket's first pending link
+    __shared__ uint32_t s_hist[kMaxBuckets];  // links of the chunk per bucket
+    __shared__ uint32_t s_off[kMaxBuckets];   // exclusive offsets in the sorted chunk
+    __shared__ uint32_t s_cc[kMaxBuckets];    // carried links per bucket (< kScatterLine)
+    __shared__ uint64_t s_sorted[C];
+    __shared__ uint32_t s_tmp[32];
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_carry[];  // [nb][kScatterLine]
     const uint32_t w = blockIdx.x;
-    for (uint32_t b = threadIdx.x; b < r.nb; b += 256)
+    const int tid = threadIdx.x;
+    constexpr int BPT = (kMaxBuckets + WG - 1) / WG;  // buckets per thread in the scan
+    for (uint32_t b = tid; b < r.nb; b += WG) {
         s_cur[b] = (uint32_t)r.bucket_base[b] + r.col_off[(uint64_t)b * r.lists + w];
-    __syncthreads();
+        s_hist[b] = 0u;
+        s_cc[b] = 0u;
+    }
     const uint32_t c = r.counts[w];
     const uint64_t* __restrict__ L = r.links + (uint64_t)w * r.stride;
-    const int lane = threadIdx.x & 63;
-    // loads run one iteration ahead of the stores: a wave's vmcnt counts loads and stores in
-    // issue order, so waiting for loads issued after the stores would also wait for the stores
     uint64_t nxt[U];
 #pragma unroll
     for (int k = 0; k < U; ++k) {
-        const uint32_t i = threadIdx.x + 256 * k;
+        const uint32_t i = tid + WG * k;
         nxt[k] = L[i < c ? i : 0];
     }
-    for (uint32_t base = 0; base < c; base += 256 * U) {
+    __syncthreads();
+    for (uint32_t base = 0; base < c; base += C) {
+        const uint32_t cnt = (c - base) < (uint32_t)C ? (c - base) : (uint32_t)C;
+        const bool last = base + C >= c;
         uint64_t v[U];
+        uint32_t bk[U], rank[U];
 #pragma unroll
         for (int k = 0; k < U; ++k) {
             v[k] = nxt[k];
-            const uint32_t i = base + 256 * U + threadIdx.x + 256 * k;
-            nxt[k] = L[i < c ? i : 0];  // branch-free: all U loads in flight together
+            const uint32_t i = base + C + tid + WG * k;
+            nxt[k] = L[i < c ? i : 0];  // next chunk in flight
         }
-        if (r.nb <= 32) {
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const bool in = base + threadIdx.x + 256 * k < c;
-                const uint32_t b = (uint32_t)((v[k] >> 40) >> r.cb_shift);
-                // few buckets: aggregate the wave's lanes per bucket before touching the LDS cursor
-                uint64_t todo = __ballot(in);
-                while (todo) {
-                    const int l0 = __ffsll((unsigned long long)todo) - 1;
-                    const uint32_t b0 = __shfl(b, l0);
-                    const uint64_t same = __ballot(in && b == b0) & todo;
-                    uint32_t basepos = 0;
-                    if (lane == l0) basepos = atomicAdd(&s_cur[b0], (uint32_t)__popcll(same));
-                    basepos = __shfl(basepos, l0);
-                    if ((same >> lane) & 1ull) {
-                        const uint32_t rank = (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
-                        r.sorted[basepos + rank] = v[k];
-                    }
-                    todo &= ~same;
-                }
-            }
-        } else {
-            uint32_t pos[U];
-#pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const bool in = base + threadIdx.x + 256 * k < c;
-                pos[k] = in ? atomicAdd(&s_cur[(uint32_t)((v[k] >> 40) >> r.cb_shift)], 1u) : 0u;
-            }
-#pragma unroll
-            for (int k = 0; k < U; ++k)
-                if (base + threadIdx.x + 256 * k < c) r.sorted[pos[k]] = v[k];
+        for (int k = 0; k < U; ++k) {
+            bk[k] = (uint32_t)((v[k] >> 40) >> r.cb_shift);
+            rank[k] = (tid + WG * k < (int)cnt) ? atomicAdd(&s_hist[bk[k]], 1u) : 0u;
         }
+        __syncthreads();
+        {
+            uint32_t h[BPT], sum = 0;
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) {
+                const uint32_t bin = tid * BPT + q;
+                h[q] = bin < r.nb ? s_hist[bin] : 0u;
+                sum += h[q];
+            }
+            uint32_t tot;
+            uint32_t ex = block_excl_scan<WG / 64>(sum, s_tmp, &tot);
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) {
+                const uint32_t bin = tid * BPT + q;
+                if (bin < r.nb) s_off[bin] = ex;
+                ex += h[q];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+            if (tid + WG * k < (int)cnt) s_sorted[s_off[bk[k]] + rank[k]] = v[k];
+        // carried links: write those whose line the chunk completes, shift the rest down
+        for (uint32_t b = tid; b < r.nb; b += WG) {
+            const uint32_t cc = s_cc[b], pos = s_cur[b];
+            const uint32_t end = pos + cc + s_hist[b];
+            const uint32_t lim = last ? end : max(pos, end & ~(uint32_t)(kScatterLine - 1));
+            uint64_t* cb = s_carry + (uint64_t)b * kScatterLine;
+            for (uint32_t k = 0; k < cc; ++k) {
+                const uint32_t dest = pos + k;
+                if (dest < lim)
+                    r.sorted[dest] = cb[k];
+                else
+                    cb[dest - lim] = cb[k];  // dest - lim <= k: ascending order is safe
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < cnt; i += WG) {
+            const uint64_t x = s_sorted[i];
+            const uint32_t b = (uint32_t)((x >> 40) >> r.cb_shift);
+            const uint32_t pos = s_cur[b], cc = s_cc[b];
+            const uint32_t end = pos + cc + s_hist[b];
+            const uint32_t lim = last ? end : max(pos, end & ~(uint32_t)(kScatterLine - 1));
+            const uint32_t dest = pos + cc + (i - s_off[b]);
+            if (dest < lim)
+                r.sorted[dest] = x;
+            else
+                s_carry[(uint64_t)b * kScatterLine + (dest - lim)] = x;
+        }
+        __syncthreads();
+        for (uint32_t b = tid; b < r.nb; b += WG) {
+            const uint32_t pos = s_cur[b];
+            const uint32_t end = pos + s_cc[b] + s_hist[b];
+            // never below the bucket's own first pending position: the line's head may belong to
+            // the previous workgroup's range of this bucket
+            const uint32_t lim = last ? end : max(pos, end & ~(uint32_t)(kScatterLine - 1));
+            s_cur[b] = lim;
+            s_cc[b] = end - lim;
+            s_hist[b] = 0u;
+        }
+        __syncthreads();
     }
 }
 
@@ -359,7 +412,7 @@ hipError_t launch_partitioned_reduce(const ReduceArgs& r, hipStream_t s) {
     if (!r.nb || !r.lists) return hipSuccess;
     hipLaunchKernelGGL(k_bucket_colscan, dim3(r.nb), dim3(1024), 0, s, r.hist, r.lists, r.col_off, r.bucket_base);
     hipLaunchKernelGGL(k_bucket_base, dim3(1), dim3(1024), 0, s, r.bucket_base, r.nb);
-    hipLaunchKernelGGL(k_link_scatter, dim3(r.lists), dim3(256), 0, s, r);
+    hipLaunchKernelGGL((k_link_scatter<8, 256>), dim3(r.lists), dim3(256), (size_t)r.nb * kScatterLine * 8, s, r);
     const uint32_t splits = r.nb >= 256 ? 1u : (512u + r.nb - 1) / r.nb;
     // CB = 512: 512 threads, 1536-link chunks -> 77.8 KB LDS, two workgroups per CU
     // CB = 1024: 1024 threads, 2048-link chunks -> 147 KB LDS, one workgroup per CU
