@@ -114,7 +114,7 @@ __global__ __launch_bounds__(1024) void k_bucket_base(uint64_t* __restrict__ bas
 // in an LDS carry until the next chunk completes it: every line of the output is written whole,
 // from one workgroup, within one chunk (the per-link version wrote 64 scattered 8-byte words per
 // store instruction, at ~2.3x write amplification in WRITE_SIZE).
-constexpr int kScatterLine = 8;  // links per 64-byte line (128-byte lines: 4% less WRITE_SIZE, but
+constexpr int kScatterLine = 8;  // links per 64-byte line (128-byte lines: WRITE_SIZE 571 -> 396 MB, but
                                  // their LDS carry halves the resident workgroups: 1.4x slower)
 template <int U, int WG>
 __global__ __launch_bounds__(WG) void k_link_scatter(ReduceArgs r) {
