@@ -254,6 +254,27 @@ struct RunSums {
         s4[1] = (uint64_t)a1;
         s4[2] += w2 + (uint64_t)(a1 >> 64);
     }
+    // add the run as 32-bit chunks to 15 register limbs (same layout as flush)
+    __device__ __forceinline__ void to_limbs(uint64_t* l) const {
+        constexpr uint64_t M = 0xFFFFFFFFull;
+        const uint64_t s2lo = (uint64_t)s2, s2hi = (uint64_t)(s2 >> 64);
+        const uint64_t s3lo = (uint64_t)s3, s3mid = (uint64_t)(s3 >> 64);
+        l[0] += n;
+        l[1] += s1 & M;
+        l[2] += s1 >> 32;
+        l[3] += s2lo & M;
+        l[4] += s2lo >> 32;
+        l[5] += s2hi;
+        l[6] += s3lo & M;
+        l[7] += s3lo >> 32;
+        l[8] += s3mid & M;
+        l[9] += (s3mid >> 32) | (s3h << 32);
+        l[10] += s4[0] & M;
+        l[11] += s4[0] >> 32;
+        l[12] += s4[1] & M;
+        l[13] += s4[1] >> 32;
+        l[14] += s4[2];
+    }
     // add the run as 32-bit chunks into the 15 limbs of an LDS cell (the topmost limb of each sum
     // may receive more than 32 bits: the table only needs value = sum of limb_k * 2^(32k))
     __device__ __forceinline__ void flush(uint64_t* cell) const {
@@ -282,113 +303,81 @@ struct RunSums {
     }
 };
 
-// One cell bucket (<= 1024 cells) per workgroup. Links are processed in chunks of C: counting-sort
-// the chunk by cell in LDS, then every thread sums the runs of its P = C/1024 consecutive sorted
-// links exactly in registers and adds each run once (15 chunk limbs) into the LDS cell. Finally the
-// workgroup adds its cells to the table: plain read-modify-write, it is the cells' only owner.
-template <int CB_SHIFT, int C, int WG>
-__global__ __launch_bounds__(WG) void k_bucket_reduce(ReduceArgs r, uint32_t splits) {
-    constexpr int CB = 1 << CB_SHIFT;
-    constexpr int P = C / WG;
-    static_assert(P * WG == C && CB <= 2 * WG, "geometry");
+// One cell bucket (CB = 512 or 1024 cells) per workgroup of CB threads; thread t owns cell t for
+// the whole kernel and keeps its 15 exact limbs in registers. Links come in chunks of C = P*CB:
+// counting-sorted by cell in LDS (histogram, scan, place), after which every owner sums its own
+// cell's run in registers -- no atomics and no LDS accumulator -- and finally adds its limbs to
+// the table with plain stores (the workgroup owns the bucket; atomics only when a small bucket
+// count is split over several workgroups).
+template <int CB_SHIFT, int P>
+__global__ __launch_bounds__(1 << CB_SHIFT) void k_bucket_reduce(ReduceArgs r, uint32_t splits) {
+    constexpr int CB = 1 << CB_SHIFT, WG = CB, C = P * WG;
+    static_assert(WG <= 1024, "one thread per cell");
     __shared__ uint32_t s_tmp[32];
-    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
-    uint64_t* s_acc = smem;                          // [CB][15]
-    uint64_t* s_sorted = smem + CB * 15;             // [C] (local cell << 40) | d
-    uint32_t* s_hist = (uint32_t*)(s_sorted + C);    // [CB]
-    uint32_t* s_cur = s_hist + CB;                   // [CB]
+    __shared__ uint32_t s_hist[CB];
+    __shared__ uint32_t s_off[CB];
+    __shared__ uint64_t s_d[C];  // the chunk's durations grouped by cell
     const int tid = threadIdx.x;
     const uint32_t b = blockIdx.x / splits, part = blockIdx.x % splits;
-    for (int x = tid; x < CB * 15; x += WG) s_acc[x] = 0;
-    for (int x = tid; x < CB; x += WG) s_hist[x] = 0;
+    s_hist[tid] = 0u;
     const uint64_t lo = r.bucket_base[b], hi = r.bucket_base[b + 1];
     const uint64_t per = (hi - lo + splits - 1) / splits;
     const uint64_t s0 = lo + per * part;
     const uint64_t s1 = (s0 + per < hi) ? s0 + per : hi;
     const uint64_t cell0 = (uint64_t)b << CB_SHIFT;
-    __syncthreads();
+    uint64_t lim[15];
+#pragma unroll
+    for (int q = 0; q < 15; ++q) lim[q] = 0;
     uint64_t nxt[P];
 #pragma unroll
     for (int k = 0; k < P; ++k) {
-        const uint64_t i = s0 + tid + k * WG;
+        const uint64_t i = s0 + tid + (uint64_t)k * WG;
         nxt[k] = r.sorted[i < s1 ? i : 0];
     }
+    __syncthreads();
     for (uint64_t base = s0; base < s1; base += C) {
         const int cnt = (int)((s1 - base) < (uint64_t)C ? (s1 - base) : (uint64_t)C);
         uint64_t v[P];
-        uint32_t cl[P];
+        uint32_t cl[P], rank[P];
 #pragma unroll
         for (int k = 0; k < P; ++k) {
             v[k] = nxt[k];
-            const uint64_t i = base + C + tid + k * WG;
+            const uint64_t i = base + C + tid + (uint64_t)k * WG;
             nxt[k] = r.sorted[i < s1 ? i : 0];  // next chunk in flight during this one
         }
 #pragma unroll
         for (int k = 0; k < P; ++k) {
             cl[k] = (uint32_t)((v[k] >> 40) - cell0);
-            if (tid + k * WG < cnt) atomicAdd(&s_hist[cl[k]], 1u);
+            rank[k] = (tid + k * WG < cnt) ? atomicAdd(&s_hist[cl[k]], 1u) : 0u;
         }
         __syncthreads();
-        {
-            // CB <= 2 WG bins: thread t owns the BPT consecutive bins [t*BPT, t*BPT + BPT)
-            constexpr int BPT = (CB + WG - 1) / WG;
-            uint32_t h[BPT], sum = 0;
-#pragma unroll
-            for (int q = 0; q < BPT; ++q) {
-                const int bin = tid * BPT + q;
-                h[q] = bin < CB ? s_hist[bin] : 0u;
-                sum += h[q];
-            }
-            uint32_t tot;
-            uint32_t ex = block_excl_scan<WG / 64>(sum, s_tmp, &tot);
-#pragma unroll
-            for (int q = 0; q < BPT; ++q) {
-                const int bin = tid * BPT + q;
-                if (bin < CB) s_cur[bin] = ex;
-                ex += h[q];
-            }
-        }
+        const uint32_t h = s_hist[tid];
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<WG / 64>(h, s_tmp, &tot);
+        s_off[tid] = ex;
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < P; ++k) {
-            if (tid + k * WG < cnt) {
-                const uint32_t pos = atomicAdd(&s_cur[cl[k]], 1u);
-                s_sorted[pos] = ((uint64_t)cl[k] << 40) | (v[k] & (kMaxDuration - 1));
-            }
-        }
+        for (int k = 0; k < P; ++k)
+            if (tid + k * WG < cnt) s_d[s_off[cl[k]] + rank[k]] = v[k] & (kMaxDuration - 1);
         __syncthreads();
         RunSums run;
         run.clear();
-        int cur = -1;
-#pragma unroll
-        for (int k = 0; k < P; ++k) {
-            const int p = tid * P + k;
-            if (p < cnt) {
-                const uint64_t x = s_sorted[p];
-                const int c = (int)(x >> 40);
-                if (c != cur) {
-                    if (cur >= 0) run.flush(s_acc + cur * 15);
-                    run.clear();
-                    cur = c;
-                }
-                run.add(x & (kMaxDuration - 1));
-            }
-        }
-        if (cur >= 0) run.flush(s_acc + cur * 15);
-        for (int x = tid; x < CB; x += WG) s_hist[x] = 0;
+        for (uint32_t q = 0; q < h; ++q) run.add(s_d[ex + q]);
+        run.to_limbs(lim);
+        s_hist[tid] = 0u;
         __syncthreads();
     }
-    const uint64_t ncell = (cell0 + CB <= r.cells) ? CB : r.cells - cell0;
-    for (uint32_t x = tid; x < ncell * 16; x += WG) {
-        const uint32_t c = x >> 4, l = x & 15;
-        if (l == 15) continue;
-        const uint64_t val = s_acc[c * 15 + l];
-        if (!val) continue;
-        uint64_t* dst = r.table + (cell0 + c) * kLimbs + l;
-        if (splits == 1)
-            *dst += val;  // this workgroup owns the cell
-        else
-            atomicAdd((unsigned long long*)dst, (unsigned long long)val);
+    const uint64_t cell = cell0 + tid;
+    if (cell < r.cells) {
+        uint64_t* dst = r.table + cell * kLimbs;
+#pragma unroll
+        for (int q = 0; q < 15; ++q) {
+            if (!lim[q]) continue;
+            if (splits == 1)
+                dst[q] += lim[q];  // this workgroup owns the cell
+            else
+                atomicAdd((unsigned long long*)&dst[q], (unsigned long long)lim[q]);
+        }
     }
 }
 
@@ -414,22 +403,11 @@ hipError_t launch_partitioned_reduce(const ReduceArgs& r, hipStream_t s) {
     hipLaunchKernelGGL(k_bucket_base, dim3(1), dim3(1024), 0, s, r.bucket_base, r.nb);
     hipLaunchKernelGGL((k_link_scatter<8, 256>), dim3(r.lists), dim3(256), (size_t)r.nb * kScatterLine * 8, s, r);
     const uint32_t splits = r.nb >= 256 ? 1u : (512u + r.nb - 1) / r.nb;
-    // CB = 512: 512 threads, 1536-link chunks -> 77.8 KB LDS, two workgroups per CU
-    // CB = 1024: 1024 threads, 2048-link chunks -> 147 KB LDS, one workgroup per CU
-    constexpr int C9 = 1536, C10 = 2048;
-    const size_t lds9 = (512 * 15 + C9) * 8 + 512 * 8, lds10 = (1024 * 15 + C10) * 8 + 1024 * 8;
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_bucket_reduce<9, C9, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds9);
-        (void)hipFuncSetAttribute((const void*)k_bucket_reduce<10, C10, 1024>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds10);
-        attr_set = true;
-    }
+    // CB = 512: 512 threads, 4096-link chunks (36 KB LDS); CB = 1024: 1024 threads, 4096-link chunks
     if (r.cb_shift == 9)
-        hipLaunchKernelGGL((k_bucket_reduce<9, C9, 512>), dim3(r.nb * splits), dim3(512), lds9, s, r, splits);
+        hipLaunchKernelGGL((k_bucket_reduce<9, 8>), dim3(r.nb * splits), dim3(512), 0, s, r, splits);
     else
-        hipLaunchKernelGGL((k_bucket_reduce<10, C10, 1024>), dim3(r.nb * splits), dim3(1024), lds10, s, r, splits);
+        hipLaunchKernelGGL((k_bucket_reduce<10, 4>), dim3(r.nb * splits), dim3(1024), 0, s, r, splits);
     return hipGetLastError();
 }
 
