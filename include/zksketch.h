@@ -78,6 +78,73 @@ zk_status   zk_kv_partial(zk_kv* kv, void** counters, uint64_t* counter_bytes, v
 zk_status   zk_kv_candidates(zk_kv* kv, void** keys, void** est, uint64_t* bytes_keys, uint64_t* bytes_est);
 zk_status   zk_kv_merge_candidates(zk_kv* kv, const uint64_t* keys, const uint32_t* est, uint32_t lists);
 
+/* ------------------------------------------------------------------------------------------
+ * Realtime span sketches per service: distinct traces (HyperLogLog) and duration quantiles.
+ *
+ * The reference declares these aggregates (RealtimeAggregates.getSpanDurations /
+ * getServiceNamesToTraceIds, zipkin-common/.../storage/RealtimeAggregates.scala:26-38;
+ * zipkinQuery.thrift:242,251) but implements none (QueryService.scala:416-430 returns "Not
+ * Implemented"); BASELINE.json asks for per-service distinct traceIds and duration p50/p99.
+ * One item per MERGED span (after mergeSpan, Span.scala:148-169) that passes isValid
+ * (Span.scala:236-240) and has a service name (Span.serviceName, :125-131): (service, traceId,
+ * duration = last - first annotation, Span.scala:228-230).
+ *
+ * HyperLogLog (Flajolet et al. 2007): 2^p one-byte registers per service; register index = top p
+ * bits of h = mix64(traceId ^ seed ^ 0xD6E8FEB86659FD93) (splitmix64 finalizer, salted apart from
+ * the traceId shard hash), value = leading zeros of the remaining bits + 1. Standard
+ * estimator with linear counting below 2.5 * 2^p; relative standard error ~1.04 / sqrt(2^p)
+ * (0.81 % at p = 14). Mergeable by register-wise MAX (RCCL all-reduce MAX, u8).
+ * Durations: a log-linear histogram (the HDR-histogram layout) instead of a t-digest: bin = the
+ * value itself below 2^m, else (exponent, top m mantissa bits). Every bin spans at most
+ * 2^-m of its lower bound, so the reported quantile bin [lo, hi] contains the exact
+ * nearest-rank quantile and its midpoint is within 2^-(m+1) relative of it. Counts are integers,
+ * so it is order-independent and mergeable by SUM (RCCL all-reduce SUM, u32) -- which a
+ * t-digest is not.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct zk_rt_config {
+    uint32_t num_services;  /* S <= 4096 */
+    int32_t  device;
+    void*    stream;        /* hipStream_t or NULL for a private stream */
+    uint32_t hll_p;         /* register index bits, 4..16; 0 = 14 */
+    uint32_t sub_bits;      /* histogram mantissa bits m, 2..8; 0 = 7 (<= 0.39 % from the midpoint) */
+    uint64_t seed;          /* traceId hash seed */
+    uint32_t reserved[8];
+} zk_rt_config;
+
+typedef struct zk_rt zk_rt;
+
+zk_status   zk_rt_create(const zk_rt_config* cfg, zk_rt** out);
+zk_status   zk_rt_destroy(zk_rt* rt);
+const char* zk_rt_last_error(const zk_rt* rt);
+/* geometry: registers per service (2^p) and histogram bins per service */
+zk_status   zk_rt_geometry(const zk_rt* rt, uint32_t* registers, uint32_t* bins);
+zk_status   zk_rt_reset(zk_rt* rt);
+/* Bind a sketch to a dependency ctx (same device): every later zk_deps_accumulate of the ctx
+ * also feeds the sketch, in the same pass over the span records (K1 emits one item per merged
+ * span). mode ZK_RT_WITH_DEPS keeps the dependency path; ZK_RT_ONLY skips it (no parent join,
+ * no links, parent_id is not read). rt = NULL unbinds. */
+#define ZK_RT_WITH_DEPS 0u
+#define ZK_RT_ONLY      1u
+zk_status   zk_rt_bind(zk_ctx* ctx, zk_rt* rt, uint32_t mode);
+/* Already-merged spans: service_id u32[n], trace_id u64[n], duration i64[n] (us, >= 0);
+ * host or device pointers (ZK_BATCH_DEVICE_PTRS). */
+zk_status   zk_rt_accumulate_merged(zk_rt* rt, const uint32_t* service_id, const uint64_t* trace_id,
+                                    const int64_t* duration, uint64_t n, uint32_t batch_flags);
+/* Distinct-trace estimates of every service (host double[S]). */
+zk_status   zk_rt_distinct_traces(zk_rt* rt, double* estimate);
+/* Duration quantiles of one service: for each q[i] in [0, 1], the histogram bin holding the
+ * nearest-rank quantile (rank = max(1, ceil(q * N))): lo[i] <= exact <= hi[i] (us); count =
+ * N. With N = 0 all outputs are 0. */
+zk_status   zk_rt_quantiles(zk_rt* rt, uint32_t service, const double* q, uint32_t nq, int64_t* lo, int64_t* hi,
+                            uint64_t* count);
+/* Raw state for tests and multi-GPU merging: registers u8[S][2^p] (MAX all-reduce) and histogram
+ * u32[S][bins] (SUM all-reduce), device pointers; and host copies. */
+zk_status   zk_rt_partial(zk_rt* rt, void** registers, uint64_t* register_bytes, void** histogram,
+                          uint64_t* histogram_bytes);
+zk_status   zk_rt_read(zk_rt* rt, uint8_t* registers, uint32_t* histogram);
+/* items dropped since reset: service_id >= S, or duration outside [0, 2^40) us */
+zk_status   zk_rt_dropped(zk_rt* rt, uint64_t* service_range, uint64_t* duration_range);
+
 #ifdef __cplusplus
 }
 #endif

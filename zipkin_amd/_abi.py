@@ -156,6 +156,22 @@ class zk_kv_config(C.Structure):
     ]
 
 
+class zk_rt_config(C.Structure):
+    _fields_ = [
+        ("num_services", C.c_uint32),
+        ("device", C.c_int32),
+        ("stream", C.c_void_p),
+        ("hll_p", C.c_uint32),
+        ("sub_bits", C.c_uint32),
+        ("seed", C.c_uint64),
+        ("reserved", C.c_uint32 * 8),
+    ]
+
+
+ZK_RT_WITH_DEPS = 0
+ZK_RT_ONLY = 1
+
+
 class zk_moments(C.Structure):
     _fields_ = [("m0", C.c_int64), ("m1", C.c_double), ("m2", C.c_double), ("m3", C.c_double), ("m4", C.c_double)]
 
@@ -215,6 +231,19 @@ _SIGNATURES = [
     ("zk_kv_partial", C.c_int, [_P, C.POINTER(_P), _U64P, C.POINTER(_P), _U64P]),
     ("zk_kv_candidates", C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), _U64P, _U64P]),
     ("zk_kv_merge_candidates", C.c_int, [_P, _P, _P, C.c_uint32]),
+    # include/zksketch.h: realtime span sketches (HyperLogLog + duration histogram)
+    ("zk_rt_create", C.c_int, [C.POINTER(zk_rt_config), C.POINTER(_P)]),
+    ("zk_rt_destroy", C.c_int, [_P]),
+    ("zk_rt_last_error", C.c_char_p, [_P]),
+    ("zk_rt_geometry", C.c_int, [_P, _U32P, _U32P]),
+    ("zk_rt_reset", C.c_int, [_P]),
+    ("zk_rt_bind", C.c_int, [_P, _P, C.c_uint32]),
+    ("zk_rt_accumulate_merged", C.c_int, [_P, _P, _P, _P, C.c_uint64, C.c_uint32]),
+    ("zk_rt_distinct_traces", C.c_int, [_P, _P]),
+    ("zk_rt_quantiles", C.c_int, [_P, C.c_uint32, _P, C.c_uint32, _P, _P, _U64P]),
+    ("zk_rt_partial", C.c_int, [_P, C.POINTER(_P), _U64P, C.POINTER(_P), _U64P]),
+    ("zk_rt_read", C.c_int, [_P, _P, _P]),
+    ("zk_rt_dropped", C.c_int, [_P, _U64P, _U64P]),
     # include/zkstore.h: the Aggregates store surface (host side)
     ("zk_store_create", C.c_int, [C.c_uint32, C.POINTER(_P)]),
     ("zk_store_destroy", C.c_int, [_P]),

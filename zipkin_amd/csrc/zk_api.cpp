@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "zk_internal.h"
+#include "zk_rt_internal.h"
 
 using namespace zk;
 
@@ -55,6 +56,9 @@ struct zk_ctx {
     void* fin_stage = nullptr;
     uint64_t records_since_reset = 0;
     std::string err;
+    // bound realtime sketch (zk_rt_bind)
+    zk_rt* rt = nullptr;
+    uint32_t rt_mode = ZK_RT_WITH_DEPS;
     // timing
     std::vector<EventPair> ev_free, ev_join, ev_reduce, ev_spill, ev_fin;
     zk_timing tm{};
@@ -233,6 +237,7 @@ zk_status zk_ctx_destroy(zk_ctx* c) {
     if (!c) return ZK_ERR_INVALID_ARG;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->rt) rt_set_stream(c->rt, nullptr);
     if (c->own_table) hipFree(c->table);
     hipFree(c->stats);
     hipFree(c->spill_count);
@@ -280,7 +285,8 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
     const uint64_t n = cols->n;
     if (n == 0) return ZK_OK;
     if (!cols_ok(cols)) return fail(c, ZK_ERR_INVALID_ARG, "null column pointer");
-    if (c->records_since_reset + n > kMaxRecordsSinceReset)
+    const bool join = !c->rt || c->rt_mode == ZK_RT_WITH_DEPS;
+    if (join && c->records_since_reset + n > kMaxRecordsSinceReset)
         return fail(c, ZK_ERR_CAPACITY, "more than 2^32-1 records since reset");
     ZK_HIP(c, hipSetDevice(c->device));
     SpanColsDev d{cols->trace_id, cols->span_id, cols->parent_id, cols->first_ts,
@@ -349,6 +355,11 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
     a.hist = c->hist;
     a.nb = c->nb;
     a.cb_shift = c->cb_shift;
+    a.join = join ? 1u : 0u;
+    if (c->rt) {
+        st = rt_prepare_lists(c->rt, grid, stride, n, &a, c->stream);
+        if (st != ZK_OK) return fail(c, st, std::string("sketch: ") + rt_error(c->rt));
+    }
     EventPair ej, er, es;
     if (c->timing) {
         ej = take_pair(c);
@@ -361,7 +372,9 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
         er = take_pair(c);
         ZK_HIP(c, hipEventRecord(er.a, c->stream));
     }
-    if (c->nb) {
+    if (!join) {
+        // sketch-only pass: no links to reduce
+    } else if (c->nb) {
         ReduceArgs r{};
         r.links = c->links;
         r.counts = c->link_count;
@@ -390,7 +403,11 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
         ZK_HIP(c, hipEventRecord(es.b, c->stream));
         c->ev_spill.push_back(es);
     }
-    c->records_since_reset += n;
+    if (c->rt) {
+        st = rt_consume_lists(c->rt, grid, stride, n);
+        if (st != ZK_OK) return fail(c, st, std::string("sketch: ") + rt_error(c->rt));
+    }
+    if (join) c->records_since_reset += n;
     return ZK_OK;
 }
 
@@ -487,6 +504,20 @@ zk_status zk_deps_note_merged(zk_ctx* c, uint64_t total_records) {
     if (total_records > kMaxRecordsSinceReset)
         return fail(c, ZK_ERR_CAPACITY, "merged table exceeds 2^32-1 records");
     c->records_since_reset = total_records;
+    return ZK_OK;
+}
+
+zk_status zk_rt_bind(zk_ctx* c, zk_rt* rt, uint32_t mode) {
+    if (!c) return ZK_ERR_INVALID_ARG;
+    if (mode != ZK_RT_WITH_DEPS && mode != ZK_RT_ONLY) return fail(c, ZK_ERR_INVALID_ARG, "unknown sketch mode");
+    if (rt && rt_device(rt) != c->device) return fail(c, ZK_ERR_INVALID_ARG, "sketch and ctx on different devices");
+    if (c->rt && c->rt != rt) {
+        ZK_HIP(c, hipStreamSynchronize(c->stream));
+        rt_set_stream(c->rt, nullptr);
+    }
+    c->rt = rt;
+    c->rt_mode = mode;
+    if (rt) rt_set_stream(rt, c->stream);  // one stream orders the ctx's and the sketch's work
     return ZK_OK;
 }
 

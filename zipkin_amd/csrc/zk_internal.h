@@ -46,6 +46,7 @@ enum Stat : int {
     ST_DUR_RANGE,
     ST_SVC_RANGE,
     ST_TOO_LARGE,
+    ST_RT_DUR_RANGE,  // sketch items dropped for a duration >= 2^40 us (not in zk_stats)
     ST_N = 16
 };
 constexpr int kStatShards = 256;  // stats buffer = kStatShards x ST_N u64
@@ -87,6 +88,16 @@ struct JoinArgs {
     uint32_t* hist;
     uint32_t nb;
     uint32_t cb_shift;  // bucket = cell >> cb_shift
+    uint32_t join;      // 1: the dependency path (parent join + links); 0: sketch items only
+    // realtime sketch items (zk_rt.hip), rt_pay == nullptr: none. K1 workgroup w writes rt_count[w]
+    // items at w * link_stride; the spill kernel appends to list `grid` (capacity rt_spill_cap).
+    uint64_t* rt_pay;
+    uint32_t* rt_svc;
+    uint32_t* rt_count;
+    unsigned long long* rt_dropped;  // [0] spill-list overflow, [1] duration >= 2^40 us
+    uint64_t rt_spill_cap;
+    uint64_t rt_seed;
+    uint32_t rt_p;
 };
 
 // host-side launchers (implemented in the .hip files)

@@ -17,6 +17,7 @@
 // leave LDS. Traces longer than the tile capacity are deferred to k_span_join_spill (global
 // scratch, one trace per workgroup at a time).
 #include "zk_internal.h"
+#include "zk_sketch_internal.h"
 
 namespace zk {
 namespace {
@@ -250,12 +251,17 @@ struct Window {  // two consecutive records per thread
     uint64_t prev;  // traceId of the record before this wave's first record
 };
 
+template <bool JOIN>
 __device__ __forceinline__ void load_window(const JoinArgs& a, uint64_t ws, Window& w) {
     const uint64_t n = a.c.n;
     const uint64_t i = ws + 2 * threadIdx.x;
     ld2_u64(a.c.trace_id, i, n, w.tid);
     ld2_u64(a.c.span_id, i, n, w.sid);
-    ld2_u64(a.c.parent_id, i, n, w.pid);
+    if constexpr (JOIN) {
+        ld2_u64(a.c.parent_id, i, n, w.pid);
+    } else {  // sketch-only pass: parentId is not read (40 B per record)
+        w.pid[0] = w.pid[1] = 0ull;
+    }
     ld2_u64((const uint64_t*)a.c.first_ts, i, n, w.first);
     ld2_u64((const uint64_t*)a.c.last_ts, i, n, w.last);
     ld2_u32(a.c.service_id, i, n, w.svc);
@@ -279,7 +285,11 @@ __device__ __forceinline__ void load_window(const JoinArgs& a, uint64_t ws, Wind
 // "seen >= 2" for cs, cr, sr, ss (Span.isValid = no ">= 2" bit); bit 20 some fragment has a
 // parentId, bit 21 some fragment has none.
 // =============================================================================================
-template <int TILE, int WG, int ABL>
+// MODE bits: kModeJoin = the dependency path (parent join, links); kModeEmit = one sketch item
+// per merged valid span with a service (zk_rt.hip). The product dependency pass is kModeJoin.
+constexpr int kModeJoin = 1;
+constexpr int kModeEmit = 2;
+template <int TILE, int WG, int ABL, int MODE>
 __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
     constexpr int H = 2 * TILE;
     constexpr int NWORD = TILE / 64;
@@ -300,13 +310,19 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
     const uint64_t n = a.c.n;
     const uint64_t R0 = (uint64_t)blockIdx.x * a.per_wg;
     if (R0 >= n) {
-        if (tid == 0) a.link_count[blockIdx.x] = 0u;
+        if (tid == 0) {
+            a.link_count[blockIdx.x] = 0u;
+            if (a.rt_count) a.rt_count[blockIdx.x] = 0u;
+        }
         for (uint32_t x = tid; x < a.nb; x += WG) a.hist[(uint64_t)x * a.grid + blockIdx.x] = 0u;
         return;
     }
     const uint64_t R1 = (R0 + a.per_wg < n) ? R0 + a.per_wg : n;
     uint64_t* __restrict__ out = a.links + (uint64_t)blockIdx.x * a.link_stride;
     const uint64_t trash = a.link_stride - 1;  // never a real link slot (join_geometry)
+    uint64_t* __restrict__ it_pay = a.rt_pay + (uint64_t)blockIdx.x * a.link_stride;
+    uint32_t* __restrict__ it_svc = a.rt_svc + (uint64_t)blockIdx.x * a.link_stride;
+    uint32_t nitem = 0;       // sketch items written by this workgroup (uniform)
     uint32_t nout = 0;        // links written by this workgroup (uniform)
     uint64_t nrec = 0;        // records aggregated (uniform)
     StatPack32 st;
@@ -316,7 +332,8 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
     uint64_t ws = R0;         // window start (even)
     uint64_t seek = R0;       // first record that may start one of our traces
     Window cur, nxt;
-    load_window(a, ws, cur);
+    constexpr bool JOIN = (MODE & kModeJoin) != 0, EMIT = (MODE & kModeEmit) != 0;
+    load_window<JOIN>(a, ws, cur);
     ZK_STAMP_DECL
     for (;;) {
         const int wn = (int)((n - ws) < (uint64_t)TILE ? (n - ws) : (uint64_t)TILE);
@@ -393,7 +410,7 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
         }
         if (!done && next_seek >= R1) done = true;
         const uint64_t next_ws = next_seek & ~1ull;
-        load_window(a, done ? ws : next_ws, nxt);  // in flight during the LDS phases below (unconditional: see ld2)
+        load_window<JOIN>(a, done ? ws : next_ws, nxt);  // in flight during the LDS phases below (unconditional: see ld2)
         ZK_STAMP(1);
         nrec += (uint64_t)(m - start);
         if constexpr (ABL != 2) {  // diagnostic build: 2 = stream windows only
@@ -502,11 +519,14 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
         ZK_STAMP(4);
 
         // ---- 6. filter(isValid), join on (parentId, traceId), (cell, duration) links ----------
-        uint64_t r_link[2];
-        uint32_t nl = 0;
+        uint64_t r_link[2], r_item[2];
+        uint32_t r_isvc[2];
+        uint32_t nl = 0, ni = 0;
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
             r_link[e] = ~0ull;
+            r_item[e] = ~0ull;
+            r_isvc[e] = 0u;
             const int L = r_leader[e];
             if (L < 0) continue;
             const int j = 2 * tid + e;
@@ -523,6 +543,20 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
             st.inc(ST_MERGED);
             const bool valid = slot_valid(w);
             st.inc(valid ? ST_VALID : ST_INVALID);
+            if constexpr (EMIT) {
+                // realtime sketch item: (service, traceId, duration) of the merged span
+                if (valid && sL != kSvcNone && s_first[j] != LLONG_MAX) {
+                    const uint64_t d = (uint64_t)(s_last[j] - s_first[j]);
+                    if (d < kMaxDuration) {
+                        r_item[e] = rt_payload(cur.tid[e], d, a.rt_p, a.rt_seed);
+                        r_isvc[e] = sL & kSvcIdMask;
+                        ++ni;
+                    } else {
+                        st.inc(ST_RT_DUR_RANGE);
+                    }
+                }
+            }
+            if constexpr (!JOIN) continue;
             if (!(valid && (w & kSlotP1))) continue;
             st.inc(ST_CHILD);
             const uint16_t seg = (uint16_t)r_seg[e];
@@ -559,8 +593,10 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
             ++nl;
         }
         ZK_STAMP(5);
-        // ---- 7. append the window's links to this workgroup's list -----------------------------
-        uint32_t incl = nl;
+        // ---- 7. append the window's links (and sketch items) to this workgroup's lists ----------
+        // one scan for both counts: links in bits 0..15, items in 16..31 (a window has <= 512)
+        const uint32_t cnt_pack = nl | (ni << 16);
+        uint32_t incl = cnt_pack;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
             const uint32_t o = __shfl_up(incl, off);
@@ -575,17 +611,30 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
             if (w2 < wave) base += v;
             total += v;
         }
-        if constexpr (ABL == 0) {
+        const uint32_t excl = base + incl - cnt_pack;
+        if constexpr (ABL == 0 && JOIN) {
             // exactly two stores per thread on every path (absent links go to the list's trash
             // slot), so the loop-end wait for the prefetched window can count them: vmcnt(2)
-            uint32_t pos = nout + base + incl - nl;
+            uint32_t pos = nout + (excl & 0xFFFFu);
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const bool v = r_link[e] != ~0ull;
                 out[v ? (uint64_t)pos : trash] = r_link[e];
                 pos += v ? 1u : 0u;
             }
-            nout += total;
+            nout += total & 0xFFFFu;
+        }
+        if constexpr (ABL == 0 && EMIT) {
+            uint32_t pos = nitem + (excl >> 16);
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const bool v = r_item[e] != ~0ull;
+                const uint64_t at = v ? (uint64_t)pos : trash;
+                it_pay[at] = r_item[e];
+                it_svc[at] = r_isvc[e];
+                pos += v ? 1u : 0u;
+            }
+            nitem += total >> 16;
         }
         ZK_STAMP(6);
         }  // ablate != 2
@@ -599,10 +648,18 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
     ZK_STAMP_FLUSH();
     if (tid == 0) {
         a.link_count[blockIdx.x] = nout;
+        if constexpr (EMIT) a.rt_count[blockIdx.x] = nitem;
         atomicAdd(&a.stats[(uint64_t)(blockIdx.x % kStatShards) * ST_N + ST_RECORDS], (unsigned long long)nrec);
     }
     flush_stats32(st, s_stat, a.stats);  // its barrier also publishes s_hist
-    for (uint32_t x = tid; x < a.nb; x += WG) a.hist[(uint64_t)x * a.grid + blockIdx.x] = s_hist[x];
+    if constexpr (EMIT) {
+        if (tid == 0 && s_stat[ST_RT_DUR_RANGE]) atomicAdd(&a.rt_dropped[1], (unsigned long long)s_stat[ST_RT_DUR_RANGE]);
+    }
+    if constexpr (JOIN) {
+        for (uint32_t x = tid; x < a.nb; x += WG) a.hist[(uint64_t)x * a.grid + blockIdx.x] = s_hist[x];
+    } else {
+        for (uint32_t x = tid; x < a.nb; x += WG) a.hist[(uint64_t)x * a.grid + blockIdx.x] = 0u;
+    }
 }
 
 // =============================================================================================
@@ -713,7 +770,7 @@ __global__ __launch_bounds__(kSpillWG) void k_span_join_spill(JoinArgs a) {
             st_sc(&sc.last[j], ha ? (long long)a.c.last_ts[gi] : LLONG_MIN);
             st_sc(&sc.cntA[j], A);
             st_sc(&sc.cntB[j], B);
-            st_sc(&sc.pid[j], (uint64_t)((f & ZK_F_HAS_PARENT) ? a.c.parent_id[gi] : ~0ull));
+            st_sc(&sc.pid[j], (uint64_t)((f & ZK_F_HAS_PARENT) ? (a.join ? a.c.parent_id[gi] : 0ull) : ~0ull));
             st_sc(&sc.svck[j], svc_key(f, a.c.service_id[gi], a.S, &rerr));
             if (rerr) st.inc(ST_SVC_RANGE);
         }
@@ -758,7 +815,8 @@ __global__ __launch_bounds__(kSpillWG) void k_span_join_spill(JoinArgs a) {
                 bool rerr = false;
                 const uint32_t sk = svc_key(f, a.c.service_id[gi], a.S, &rerr);
                 if (sk != kSvcNone) atomicMin(&sc.svck[Ld], sk);
-                if (f & ZK_F_HAS_PARENT) atomicMin((unsigned long long*)&sc.pid[Ld], (unsigned long long)a.c.parent_id[gi]);
+                if (f & ZK_F_HAS_PARENT)
+                    atomicMin((unsigned long long*)&sc.pid[Ld], (unsigned long long)(a.join ? a.c.parent_id[gi] : 0ull));
             }
         }
         __syncthreads();
@@ -783,13 +841,28 @@ __global__ __launch_bounds__(kSpillWG) void k_span_join_spill(JoinArgs a) {
             const uint64_t pL = ld_sc(&sc.pid[Ld]);
             bool rerr = false;
             const uint32_t sk = svc_key(f, a.c.service_id[gi], a.S, &rerr);
-            bool amb = (f & ZK_F_HAS_PARENT) ? (a.c.parent_id[gi] != pL) : (npar > 0);
+            bool amb = (f & ZK_F_HAS_PARENT) ? ((a.join ? a.c.parent_id[gi] : 0ull) != pL) : (npar > 0);
             if (sk != kSvcNone && (sk >> kSvcKindShift) == (sL >> kSvcKindShift) && sk != sL) amb = true;
             if (amb) st.inc(ST_AMBIGUOUS);
             if (Ld != j) continue;
             st.inc(ST_MERGED);
             const bool valid = spill_valid(A, B);
             st.inc(valid ? ST_VALID : ST_INVALID);
+            if (a.rt_pay && valid && sL != kSvcNone) {
+                // sketch item of the merged span, appended to list `grid` (capacity >= records)
+                const long long f0 = ld_sc(&sc.first[Ld]);
+                if (f0 != LLONG_MAX) {
+                    const uint64_t d = (uint64_t)(ld_sc(&sc.last[Ld]) - f0);
+                    if (d < kMaxDuration) {
+                        const uint64_t at = (uint64_t)a.grid * a.link_stride + atomicAdd(&a.rt_count[a.grid], 1u);
+                        a.rt_pay[at] = rt_payload(a.c.trace_id[gi], d, a.rt_p, a.rt_seed);
+                        a.rt_svc[at] = sL & kSvcIdMask;
+                    } else {
+                        atomicAdd(&a.rt_dropped[1], 1ull);
+                    }
+                }
+            }
+            if (!a.join) continue;
             if (!(valid && npar > 0)) continue;
             st.inc(ST_CHILD);
             uint32_t ps = slot_hash(pL, 0) & (H - 1);
@@ -843,12 +916,18 @@ uint64_t spill_scratch_bytes_per_wg(uint32_t max_trace) {
 
 hipError_t launch_join(const JoinArgs& a, hipStream_t s) {
     if (a.c.n == 0) return hipSuccess;
+    const dim3 g((unsigned)a.grid), b(kTileWG);
+    const bool emit = a.rt_pay != nullptr, join = a.join != 0;
     if (a.ablate == 1)
-        hipLaunchKernelGGL((k_span_join_stream<kTile, kTileWG, 1>), dim3((unsigned)a.grid), dim3(kTileWG), 0, s, a);
+        hipLaunchKernelGGL((k_span_join_stream<kTile, kTileWG, 1, kModeJoin>), g, b, 0, s, a);
     else if (a.ablate == 2)
-        hipLaunchKernelGGL((k_span_join_stream<kTile, kTileWG, 2>), dim3((unsigned)a.grid), dim3(kTileWG), 0, s, a);
+        hipLaunchKernelGGL((k_span_join_stream<kTile, kTileWG, 2, kModeJoin>), g, b, 0, s, a);
+    else if (emit && join)
+        hipLaunchKernelGGL((k_span_join_stream<kTile, kTileWG, 0, kModeJoin | kModeEmit>), g, b, 0, s, a);
+    else if (emit)
+        hipLaunchKernelGGL((k_span_join_stream<kTile, kTileWG, 0, kModeEmit>), g, b, 0, s, a);
     else
-        hipLaunchKernelGGL((k_span_join_stream<kTile, kTileWG, 0>), dim3((unsigned)a.grid), dim3(kTileWG), 0, s, a);
+        hipLaunchKernelGGL((k_span_join_stream<kTile, kTileWG, 0, kModeJoin>), g, b, 0, s, a);
     return hipGetLastError();
 }
 

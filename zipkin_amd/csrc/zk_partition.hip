@@ -17,14 +17,26 @@ namespace {
 constexpr int kPartWG = 256;
 constexpr int kPartU = 4;  // items per thread per iteration (loads issued before the LDS atomics)
 
+// range of workgroup w: a slice of one flat array (counts == nullptr) or list w of the lists form
+__device__ __forceinline__ void part_range(uint64_t n, uint64_t per, const uint32_t* counts, uint64_t* lo,
+                                           uint64_t* hi) {
+    if (counts) {
+        *lo = (uint64_t)blockIdx.x * per;
+        *hi = *lo + counts[blockIdx.x];
+    } else {
+        *lo = (uint64_t)blockIdx.x * per;
+        *hi = *lo + per < n ? *lo + per : n;
+    }
+}
+
 __global__ __launch_bounds__(kPartWG) void k_part_hist(const uint32_t* __restrict__ svc, uint64_t n, uint64_t per,
-                                                        uint32_t S, uint32_t grid, uint32_t* __restrict__ hist,
-                                                        unsigned long long* dropped) {
+                                                        const uint32_t* __restrict__ counts, uint32_t S, uint32_t grid,
+                                                        uint32_t* __restrict__ hist, unsigned long long* dropped) {
     extern __shared__ uint32_t h[];
     for (uint32_t i = threadIdx.x; i < S; i += kPartWG) h[i] = 0u;
     __syncthreads();
-    const uint64_t lo = (uint64_t)blockIdx.x * per;
-    const uint64_t hi = lo + per < n ? lo + per : n;
+    uint64_t lo, hi;
+    part_range(n, per, counts, &lo, &hi);
     uint32_t bad = 0;
     for (uint64_t b = lo; b < hi; b += (uint64_t)kPartWG * kPartU) {
         uint32_t v[kPartU];
@@ -49,14 +61,15 @@ __global__ __launch_bounds__(kPartWG) void k_part_hist(const uint32_t* __restric
 
 __global__ __launch_bounds__(kPartWG) void k_part_scatter(const uint32_t* __restrict__ svc,
                                                            const uint64_t* __restrict__ payload, uint64_t n,
-                                                           uint64_t per, uint32_t S, uint32_t grid,
+                                                           uint64_t per, const uint32_t* __restrict__ counts,
+                                                           uint32_t S, uint32_t grid,
                                                            const uint32_t* __restrict__ offs,
                                                            uint64_t* __restrict__ out) {
     extern __shared__ uint32_t cur[];  // absolute output cursor per service
     for (uint32_t i = threadIdx.x; i < S; i += kPartWG) cur[i] = offs[(uint64_t)i * grid + blockIdx.x];
     __syncthreads();
-    const uint64_t lo = (uint64_t)blockIdx.x * per;
-    const uint64_t hi = lo + per < n ? lo + per : n;
+    uint64_t lo, hi;
+    part_range(n, per, counts, &lo, &hi);
     for (uint64_t b = lo; b < hi; b += (uint64_t)kPartWG * kPartU) {
         uint32_t v[kPartU];
         uint64_t p[kPartU];
@@ -142,9 +155,10 @@ uint64_t partition_scratch_bytes(const PartitionPlan& p) {
     return 2 * a + scan_temp_bytes(m);
 }
 
-hipError_t launch_partition(const PartitionPlan& p, const uint32_t* svc, const uint64_t* payload, uint64_t n,
-                            uint64_t* out, uint64_t* seg, unsigned long long* dropped, void* scratch,
-                            hipStream_t s) {
+namespace {
+hipError_t partition_impl(const PartitionPlan& p, const uint32_t* svc, const uint64_t* payload, uint64_t n,
+                          const uint32_t* counts, uint64_t* out, uint64_t* seg, unsigned long long* dropped,
+                          void* scratch, hipStream_t s) {
     const uint64_t m = (uint64_t)p.S * p.grid;
     const uint64_t a = (m * 4 + 255) & ~255ull;
     uint32_t* hist = (uint32_t*)scratch;
@@ -152,15 +166,39 @@ hipError_t launch_partition(const PartitionPlan& p, const uint32_t* svc, const u
     void* temp = (uint8_t*)scratch + 2 * a;
     size_t temp_bytes = scan_temp_bytes(m);
     const size_t lds = (size_t)p.S * 4;
-    hipLaunchKernelGGL(k_part_hist, dim3(p.grid), dim3(kPartWG), lds, s, svc, n, p.per_wg, p.S, p.grid, hist, dropped);
+    hipLaunchKernelGGL(k_part_hist, dim3(p.grid), dim3(kPartWG), lds, s, svc, n, p.per_wg, counts, p.S, p.grid, hist,
+                       dropped);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, hist, offs, (int)m, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_part_scatter, dim3(p.grid), dim3(kPartWG), lds, s, svc, payload, n, p.per_wg, p.S, p.grid,
-                       offs, out);
+    hipLaunchKernelGGL(k_part_scatter, dim3(p.grid), dim3(kPartWG), lds, s, svc, payload, n, p.per_wg, counts, p.S,
+                       p.grid, offs, out);
     hipLaunchKernelGGL(k_part_seg, dim3((p.S + 256) / 256), dim3(256), 0, s, offs, hist, p.S, p.grid, seg);
     return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_partition(const PartitionPlan& p, const uint32_t* svc, const uint64_t* payload, uint64_t n,
+                            uint64_t* out, uint64_t* seg, unsigned long long* dropped, void* scratch,
+                            hipStream_t s) {
+    return partition_impl(p, svc, payload, n, nullptr, out, seg, dropped, scratch, s);
+}
+
+PartitionPlan partition_plan_lists(uint32_t lists, uint32_t S) {
+    PartitionPlan p;
+    p.S = S;
+    p.grid = lists;
+    p.per_wg = 0;  // set by the caller through launch_partition_lists (the list stride)
+    return p;
+}
+
+hipError_t launch_partition_lists(const PartitionPlan& p0, const uint32_t* svc, const uint64_t* payload,
+                                  uint64_t stride, const uint32_t* counts, uint64_t* out, uint64_t* seg,
+                                  unsigned long long* dropped, void* scratch, hipStream_t s) {
+    PartitionPlan p = p0;
+    p.per_wg = stride;
+    return partition_impl(p, svc, payload, 0, counts, out, seg, dropped, scratch, s);
 }
 
 hipError_t launch_unit_plan(const uint64_t* seg, uint32_t S, uint64_t unit_items, uint32_t* unit_base,

@@ -28,6 +28,9 @@ struct PartitionPlan {
 };
 
 PartitionPlan partition_plan(uint64_t n, uint32_t S, uint32_t cus);
+// Partition of per-workgroup lists instead of one flat range: list w is [w*stride, w*stride +
+// counts[w]) of svc/payload (the item lists K1 writes), one partition workgroup per list.
+PartitionPlan partition_plan_lists(uint32_t lists, uint32_t S);
 // scratch bytes needed for hist (S*grid u32), offsets (S*grid+1 u64) and the scan temp storage
 uint64_t partition_scratch_bytes(const PartitionPlan& p);
 // svc/payload: device arrays of n items. out: device array of n payloads (service-contiguous).
@@ -36,6 +39,10 @@ uint64_t partition_scratch_bytes(const PartitionPlan& p);
 hipError_t launch_partition(const PartitionPlan& p, const uint32_t* svc, const uint64_t* payload, uint64_t n,
                             uint64_t* out, uint64_t* seg, unsigned long long* dropped, void* scratch,
                             hipStream_t s);
+// lists form: counts[w] items at offset w * stride (plan from partition_plan_lists)
+hipError_t launch_partition_lists(const PartitionPlan& p, const uint32_t* svc, const uint64_t* payload,
+                                  uint64_t stride, const uint32_t* counts, uint64_t* out, uint64_t* seg,
+                                  unsigned long long* dropped, void* scratch, hipStream_t s);
 
 // Work units: service s's run is cut into ceil(len / unit_items) units. unit_base[s] = first unit
 // of service s (exclusive scan), unit_base[S] = total. Computed on device from `seg`.
@@ -73,5 +80,47 @@ hipError_t launch_kv_candidates(const KvArgs& a, hipStream_t s);
 hipError_t launch_kv_merge(const KvArgs& a, hipStream_t s);  // prev cand + unit lists + extra lists
 hipError_t launch_kv_estimate(const KvArgs& a, uint32_t svc, const uint64_t* keys, uint64_t n, uint32_t* est,
                               hipStream_t s);
+
+// ---- realtime sketches: HyperLogLog distinct traces + log-linear duration histogram ------------
+// item payload: (register index << 46) | (rho << 40) | duration   (p <= 16, rho <= 61, d < 2^40)
+constexpr uint32_t kRtMaxP = 16;
+constexpr uint32_t kRtPayShiftIdx = 46;
+constexpr uint32_t kRtPayShiftRho = 40;
+constexpr uint64_t kRtUnitItems = 65536;
+
+__host__ __device__ inline uint32_t rt_nbins(uint32_t m) { return (41u - m) << m; }
+// bin of a duration d < 2^40: d itself below 2^m, else (exponent - m + 1, top m mantissa bits)
+__host__ __device__ inline uint32_t rt_bin(uint64_t d, uint32_t m) {
+    if (d < (1ull << m)) return (uint32_t)d;
+    const uint32_t e = 63u - (uint32_t)__builtin_clzll(d);
+    return ((e - m + 1u) << m) | (uint32_t)((d >> (e - m)) & ((1ull << m) - 1ull));
+}
+// The salt decorrelates the register hash from the traceId-hash shard of a span (zk_trace_shard
+// also hashes traceIds with splitmix64: a shard's traceIds would otherwise share hash bits).
+constexpr uint64_t kRtSalt = 0xD6E8FEB86659FD93ull;
+__host__ __device__ inline uint64_t rt_payload(uint64_t trace_id, uint64_t d, uint32_t p, uint64_t seed) {
+    const uint64_t h = sk_mix64(trace_id ^ seed ^ kRtSalt);
+    const uint64_t idx = h >> (64u - p);
+    const uint64_t w = h << p;
+    const uint64_t rho = w ? (uint64_t)__builtin_clzll(w) + 1u : (uint64_t)(64u - p + 1u);
+    return (idx << kRtPayShiftIdx) | (rho << kRtPayShiftRho) | d;
+}
+
+struct RtArgs {
+    uint32_t S, p, m, nbins;
+    uint8_t* regs;               // [S][2^p] (u32-aligned rows)
+    uint32_t* hist;              // [S][nbins]
+    const uint64_t* items;       // service-contiguous payloads
+    const uint64_t* seg;         // [S+1]
+    const uint32_t* unit_base;   // [S+1]
+    uint64_t unit_items;
+    uint32_t max_units;
+};
+hipError_t launch_rt_sketch(const RtArgs& a, hipStream_t s);
+// merged-span input -> (svc, payload) items; invalid items get svc = 0xFFFFFFFF (dropped by the
+// partition) and are counted in dropped[0] (service) / dropped[1] (duration)
+hipError_t launch_rt_items(const uint32_t* svc, const uint64_t* trace_id, const int64_t* dur, uint64_t n, uint32_t S,
+                           uint32_t p, uint64_t seed, uint32_t* out_svc, uint64_t* out_pay,
+                           unsigned long long* dropped, hipStream_t s);
 
 }  // namespace zk
