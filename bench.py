@@ -43,12 +43,21 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=20_000_000, help="records for the CPU baseline leg (0: skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--ablate", type=int, default=0, help="diagnostic: 1 = K1 without link emission (not a valid result)")
+    ap.add_argument("--workload", default="c2", choices=("c2", "c4", "c5"),
+                    help="c2 (default, the headline): dependency path; c4: key-value top-K sketch over "
+                         "binary annotations; c5: per-service HLL + duration histogram from span fragments")
+    ap.add_argument("--items", type=int, default=250_000_000, help="c4: binary annotations per step")
     return ap.parse_args()
 
 
 def main():
     a = parse()
     import torch
+
+    if a.workload == "c4":
+        return bench_c4(a)
+    if a.workload == "c5":
+        return bench_c5(a)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -68,7 +77,10 @@ def main():
 
     S = a.services
     cells = S * S
-    stream = torch.cuda.current_stream(dev)
+    # one dedicated stream orders the library's kernels, torch's allocations and RCCL (a handle of
+    # 0 -- torch's legacy default stream -- would make the library create an unordered private one)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
     table = torch.zeros(cells * 16, dtype=torch.int64, device=dev)
     ctx = DepsContext(S, device=local, stream=stream.cuda_stream, timing=True,
                       table_ptr=table.data_ptr(), table_bytes=table.numel() * 8, ablate=a.ablate)
@@ -210,6 +222,140 @@ def cpu_baseline(cols, sample, S, threads):
         "sample": f"first {cut} records (whole traces) of the benchmark batch; oracle/zk_oracle.c, "
         f"{threads} threads, {r.seconds:.2f} s",
     }
+
+
+def _timed(step, steps, warmup, stream):
+    import torch
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0, ev0.elapsed_time(ev1)
+
+
+def bench_c5(a):
+    """BASELINE configs[4] (one GPU): per-service HyperLogLog of distinct traceIds + duration
+    histogram (p50/p99) over the C2 span batch, fed by K1 in sketch-only mode (40 B/record:
+    parentId is not read) + service partition + LDS sketch units."""
+    import torch
+
+    from zipkin_amd import DepsContext, DeviceColumns, tracegen_params
+    from zipkin_amd.realtime import RtSketch
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
+    S = a.services
+    ctx = DepsContext(S, device=0, stream=stream.cuda_stream, timing=True)
+    rt = RtSketch(S, stream=stream.cuda_stream)
+    rt.bind(ctx, only=True)
+    p = tracegen_params(a.seed, int(a.records / 15) + 1000, target_records=a.records, max_depth=a.max_depth,
+                        num_services=S)
+    cols = DeviceColumns(a.records, device="cuda:0")
+    n, ntr = ctx.tracegen_device(p, cols)
+
+    def step():
+        ctx.reset()
+        rt.reset()
+        ctx.accumulate(cols)
+
+    tm0 = ctx.timing()
+    wall, ev_ms = _timed(step, a.steps, a.warmup, stream)
+    tm1 = ctx.timing()
+    calls = tm1["join_calls"] - tm0["join_calls"]
+    join_ms = (tm1["join_ms_total"] - tm0["join_ms_total"]) / max(1, calls)
+    t0 = time.perf_counter()
+    est = rt.distinct_traces()
+    q = [rt.quantiles(s, (0.5, 0.99)) for s in range(S)]
+    query_ms = (time.perf_counter() - t0) * 1e3
+    achieved = n * 40 / (join_ms * 1e-3) / 1e9
+    print(json.dumps({
+        "metric": "spans/sec into per-service HLL distinct traceIds + duration p50/p99 (BASELINE configs[4], 1 GPU)",
+        "value": n * a.steps / wall, "unit": "spans/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": wall * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u64", "data": "synthetic (zipkin-tracegen-shaped, generated on device)",
+        "config": {"workload": "C5: 1e8 span records, 500 services, HLL p=14 + log-linear histogram m=7",
+                   "records": n, "traces": ntr, "services": S,
+                   "step": "reset + K1 (merge, isValid, serviceName, duration; sketch items) + partition + sketch"},
+        "roofline": {"bound": "hbm", "kernel": "k_span_join_stream<..., kModeEmit>", "achieved": achieved,
+                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
+                     "algorithmic_bytes_per_launch": n * 40, "avg_launch_ms": join_ms},
+        "detail": {"event_ms_per_step": ev_ms / a.steps, "query_ms_all_services": query_ms,
+                   "median_distinct_estimate": float(sorted(est)[S // 2]),
+                   "p50_p99_bins_service0": q[0][0]},
+    }), flush=True)
+
+
+def bench_c4(a):
+    """BASELINE configs[3] (one GPU slice): getTopKeyValueAnnotations via count-min + top-K over
+    binary annotations (service u32, key hash u64 = 12 B/item), Zipf(1.1) keys over 1e6 ids,
+    services uniform over 500, generated on device."""
+    import torch
+
+    from zipkin_amd.kv import KvSketch
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
+    S, n = a.services, a.items
+    g = torch.Generator(device=dev)
+    g.manual_seed(4)
+    w = 1.0 / torch.arange(1, 1_000_001, dtype=torch.float64, device=dev) ** 1.1
+    cdf = torch.cumsum(w, 0)
+    cdf /= cdf[-1].clone()
+    keys = torch.empty(n, dtype=torch.int64, device=dev)
+    svc = torch.randint(0, S, (n,), dtype=torch.int32, device=dev, generator=g)
+    M = (1 << 64) - 1
+
+    def s64(c):  # a uint64 constant as the int64 torch multiplies with (two's complement wrap)
+        return c - (1 << 64) if c >= 1 << 63 else c
+
+    def shr(x, k):  # logical right shift on int64
+        return (x >> k) & ((1 << (64 - k)) - 1)
+
+    chunk = 50_000_000
+    for b in range(0, n, chunk):
+        e = min(n, b + chunk)
+        r = torch.searchsorted(cdf, torch.rand(e - b, dtype=torch.float64, device=dev, generator=g), right=True)
+        z = r.to(torch.int64) + 0x5EED
+        z = (z ^ shr(z, 30)) * s64(0xBF58476D1CE4E5B9)
+        z = (z ^ shr(z, 27)) * s64(0x94D049BB133111EB)
+        keys[b:e] = z ^ shr(z, 31)
+    del M
+    kv = KvSketch(S, stream=stream.cuda_stream, seed=4)
+
+    def step():
+        kv.reset()
+        kv.accumulate(svc, keys)
+
+    wall, ev_ms = _timed(step, a.steps, a.warmup, stream)
+    t0 = time.perf_counter()
+    kk, est, cnt = kv.topk_all(10)
+    query_ms = (time.perf_counter() - t0) * 1e3
+    value = n * a.steps / wall
+    achieved = n * 12 / (ev_ms / a.steps * 1e-3) / 1e9  # HIP events on the step's stream
+    print(json.dumps({
+        "metric": "binary annotations/sec into per-service count-min + top-K (BASELINE configs[3], 1 GPU)",
+        "value": value, "unit": "annotations/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": wall * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u32", "data": "synthetic (Zipf(1.1) keys over 1e6 ids, 500 services, generated on device)",
+        "config": {"workload": f"C4: {n:.3g} binary annotations per step, count-min 4 x 2048 per service, K=64 kept",
+                   "items": n, "services": S},
+        "roofline": {"bound": "hbm", "kernel": "whole step (partition + sketch + candidates + merge)",
+                     "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
+                     "algorithmic_bytes_per_step": n * 12},
+        "detail": {"event_ms_per_step": ev_ms / a.steps, "topk_query_ms": query_ms,
+                   "service0_top3": [(int(k), int(e)) for k, e in zip(kk[0][:3], est[0][:3])]},
+    }), flush=True)
 
 
 if __name__ == "__main__":

@@ -68,15 +68,21 @@ class ShardedDeps:
         self.group = group
         self.num_services = num_services
         dev = torch.device("cuda", device)
+        # the library's kernels and the RCCL all-reduce must be ordered on ONE stream
+        self.stream = torch.cuda.Stream(device=dev) if stream is None else stream
         self.table = torch.zeros(num_services * num_services * 16, dtype=torch.int64, device=dev)
-        self.ctx = DepsContext(num_services, device=device, stream=stream, timing=timing,
+        torch.cuda.current_stream(dev).synchronize()  # the zeroed table, before the library's stream
+        self.ctx = DepsContext(num_services, device=device, stream=self.stream.cuda_stream, timing=timing,
                                table_ptr=self.table.data_ptr(), table_bytes=self.table.numel() * 8, ablate=ablate)
 
     def step(self, cols, total_records: int | None = None, out_device=None):
+        import torch
+
         self.ctx.reset()
         self.ctx.accumulate(cols)
         if self.world > 1:
-            allreduce_table(self.table, self.group)
+            with torch.cuda.stream(self.stream):  # RCCL waits for the accumulate on this stream
+                allreduce_table(self.table, self.group)
             if total_records is not None:
                 self.ctx.note_merged(total_records)
         return self.ctx.finalize(out_device=out_device)
