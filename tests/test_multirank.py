@@ -68,6 +68,48 @@ def _worker(rank, world, port, mode):
         dist.destroy_process_group()
 
 
+def _sketch_worker(rank, world, port):
+    import torch
+    import torch.distributed as dist
+
+    from oracle.kv import KvOracle, zipf_items
+    from oracle.realtime import RtOracle, merged_span_items
+    from zipkin_amd.shards import allreduce_kv_counters, allreduce_sketch
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        full = tracegen_host(seed=8, num_traces=800, max_depth=6, num_services=S)
+        shards = split(full, world)
+        # realtime sketch: per-shard state, merged by MAX / SUM, equals the sketch of the union
+        mine = RtOracle(S, p=10, seed=3)
+        mine.accumulate_merged(*merged_span_items(shards[rank], S)[:3])
+        regs = torch.from_numpy(mine.regs.copy())
+        hist = torch.from_numpy(mine.hist.astype(np.int32))
+        allreduce_sketch(regs, hist)
+        union = RtOracle(S, p=10, seed=3)
+        union.accumulate_merged(*merged_span_items(full, S)[:3])
+        assert np.array_equal(regs.numpy(), union.regs)
+        assert np.array_equal(hist.numpy().astype(np.uint64), union.hist)
+        # count-min counters of item shards add up to the counters of all items
+        svc, keys = zipf_items(20_000, S, num_keys=3000, seed=1)
+        part = np.arange(len(svc)) % world == rank
+        kv = KvOracle(S, width=256, depth=4, candidates=16, seed=2)
+        kv.accumulate(svc[part], keys[part])
+        cm = torch.from_numpy(kv.cm.astype(np.int64))
+        tot = torch.from_numpy(kv.totals.astype(np.int64))
+        allreduce_kv_counters(cm, tot)
+        allkv = KvOracle(S, width=256, depth=4, candidates=16, seed=2)
+        allkv.accumulate(svc, keys)
+        assert np.array_equal(cm.numpy().astype(np.uint64), allkv.cm)
+        assert np.array_equal(tot.numpy().astype(np.uint64), allkv.totals)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_sketch_merges_are_exact():
+    mp.spawn(_sketch_worker, args=(WORLD, _free_port()), nprocs=WORLD, join=True)
+
+
 @pytest.mark.parametrize("mode", ["tracegen", "split"])
 def test_two_rank_allreduce_is_exact(mode):
     mp.spawn(_worker, args=(WORLD, _free_port(), mode), nprocs=WORLD, join=True)

@@ -39,6 +39,25 @@ def allreduce_table(table, group=None) -> None:
     dist.all_reduce(table, op=dist.ReduceOp.SUM, group=group)
 
 
+def allreduce_sketch(registers, histogram, group=None) -> None:
+    """In-place merge of realtime sketches of disjoint shards (zk_rt_partial): HyperLogLog
+    registers by element-wise MAX (uint8), duration histogram bins by SUM (int32 as the u32 bins:
+    two's-complement addition is the same below 2^31 per bin and shard sum)."""
+    import torch.distributed as dist
+
+    dist.all_reduce(registers, op=dist.ReduceOp.MAX, group=group)
+    dist.all_reduce(histogram, op=dist.ReduceOp.SUM, group=group)
+
+
+def allreduce_kv_counters(counters, totals, group=None) -> None:
+    """In-place SUM of count-min counters and per-service totals (zk_kv_partial); the candidate
+    lists are then all-gathered and re-estimated on every rank (zk_kv_merge_candidates)."""
+    import torch.distributed as dist
+
+    dist.all_reduce(counters, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(totals, op=dist.ReduceOp.SUM, group=group)
+
+
 def allreduce_stats(stats: dict, device="cpu", group=None) -> dict:
     """Job-wide zk_stats: every counter is a sum over ranks."""
     import torch
