@@ -50,7 +50,10 @@ typedef enum zk_status {
     ZK_ERR_NOT_CLUSTERED = 7,    /* batch flags did not promise trace-clustered input */
     ZK_ERR_NO_DEVICE = 8,        /* no HIP device / not gfx950 */
     ZK_ERR_SERVICE_RANGE = 9,    /* a record carries service_id >= num_services */
-    ZK_ERR_UNSUPPORTED = 10
+    ZK_ERR_UNSUPPORTED = 10,
+    ZK_ERR_INVALID_SPAN = 11,    /* ingest: a span the reference's thrift conversion rejects (null
+                                    name, annotation timestamp <= 0 or empty value,
+                                    thrift.scala:64-121), or bytes that do not decode */
 } zk_status;
 
 /* ------------------------------------------------------------------------------------------

@@ -1,0 +1,94 @@
+/*
+ * zkingest.h — C ABI of the span ingest decoder of libzkagg (host side).
+ *
+ * Turns stored span fragments into the 48-B columnar records of zkagg.h, replacing the job's
+ * input decode: the Cassandra column value of one span fragment is
+ *   Snappy(TBinaryProtocol(thrift Span))      CassieSpanStoreDefaults.SpanCodec
+ *                                             (zipkin-cassandra/.../storage/cassandra/CassieSpanStore.scala:52;
+ *                                             SnappyCodec.scala:32-51, ScroogeThriftCodec.scala:23-40)
+ * with the Span / Annotation / BinaryAnnotation / Endpoint structs of
+ *   zipkin-thrift/src/main/thrift/com/twitter/zipkin/zipkinCore.thrift:27-58.
+ * The reference decodes each fragment twice (StorageRecordReader.scala:58 for the key, then
+ * SpanSource.scala:20-22); this decodes once, straight into columns.
+ *
+ * Validation is the reference's thrift -> Span conversion (zipkin-scrooge/.../conversions/
+ * thrift.scala): a null span name throws IncompleteTraceDataException (:101-104); an annotation
+ * with timestamp <= 0 or an empty value throws IllegalArgumentException (:66-71); a null or empty
+ * endpoint service name becomes "Unknown service name" (:36-43). ZK_INGEST_STRICT mirrors the
+ * throw (the batch fails with ZK_ERR_INVALID_SPAN at the first bad span); otherwise bad spans are
+ * skipped and counted. Bytes that do not decode are always ZK_ERR_INVALID_SPAN in strict mode.
+ *
+ * Record derivation (Span.scala:72-74,125-131,174-191,216-240): first/last
+ * = min/max annotation timestamp; service = host of the first sr/ss annotation with a host, else
+ * of the first cs/cr; 2-bit saturating counts of cs/cr/sr/ss; parentId presence.
+ *
+ * Side outputs for the sketches (zksketch.h), following the span indexer
+ * (CassieSpanStore.scala:214-242; only spans with >= 1 annotation are indexed):
+ *   key-value items   one per binary annotation with a host: (host service id, key hash)
+ *   annotation items  one per distinct non-core annotation value with a host: (service id, value hash)
+ * Hashes are zk_hash_string (64-bit FNV-1a, then the splitmix64 finalizer); the decoder keeps the
+ * strings so hashes map back to names (zk_ingest_string).
+ *
+ * A zk_ingest owns the service-name dictionary (ids in order of first appearance, names
+ * case-sensitive as Service(name) compares them, Dependencies.scala:25). It is not thread-safe.
+ */
+#ifndef ZKINGEST_H
+#define ZKINGEST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "zkagg.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZK_CODEC_THRIFT        0u  /* TBinaryProtocol-encoded Span */
+#define ZK_CODEC_SNAPPY_THRIFT 1u  /* raw Snappy block of the above (the stored Cassandra value) */
+
+#define ZK_INGEST_STRICT 1u        /* fail the batch on the first span the reference rejects */
+
+typedef struct zk_ingest zk_ingest;
+
+/* caller buffers for the sketch items (any may be NULL / cap 0: not produced) */
+typedef struct zk_ingest_items {
+    uint32_t* kv_service;     /* binary annotations: host service id */
+    uint64_t* kv_key;         /* zk_hash_string(key) */
+    uint64_t  kv_cap;
+    uint64_t  kv_n;           /* out: items written */
+    uint32_t* ann_service;    /* non-core annotation values */
+    uint64_t* ann_value;      /* zk_hash_string(value) */
+    uint64_t  ann_cap;
+    uint64_t  ann_n;          /* out */
+} zk_ingest_items;
+
+zk_status   zk_ingest_create(zk_ingest** out);
+zk_status   zk_ingest_destroy(zk_ingest* ing);
+const char* zk_ingest_last_error(const zk_ingest* ing);
+
+/* Decode n stored fragments: fragment i is buf[offsets[i] .. offsets[i+1]) (offsets has n+1
+ * entries). Records go to the host columns of `out` (capacity >= n); *n_out = records written
+ * (in input order), *n_rejected = spans skipped (lenient mode). items may be NULL.
+ * ZK_ERR_CAPACITY when an item buffer is too small (the records are still written). */
+zk_status zk_ingest_spans(zk_ingest* ing, const uint8_t* buf, const uint64_t* offsets, uint64_t n, uint32_t codec,
+                          uint32_t flags, const zk_span_cols* out, uint64_t* n_out, uint64_t* n_rejected,
+                          zk_ingest_items* items);
+
+/* the service dictionary */
+zk_status zk_ingest_num_services(const zk_ingest* ing, uint32_t* n);
+zk_status zk_ingest_service_id(zk_ingest* ing, const char* name, uint64_t len, uint32_t* id);  /* adds if new */
+zk_status zk_ingest_service_name(const zk_ingest* ing, uint32_t id, char* buf, uint64_t cap, uint64_t* len);
+/* the string behind a key / value hash seen by this decoder (two-phase: buf NULL -> *len) */
+zk_status zk_ingest_string(const zk_ingest* ing, uint64_t hash, char* buf, uint64_t cap, uint64_t* len);
+
+uint64_t  zk_hash_string(const char* s, uint64_t len);
+/* raw Snappy block decompression (exposed for tools/tests): *out_len = uncompressed size; with
+ * out == NULL only the size is read from the header */
+zk_status zk_snappy_uncompress(const uint8_t* in, uint64_t in_len, uint8_t* out, uint64_t cap, uint64_t* out_len);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ZKINGEST_H */

@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_status_strings():
-    for s in range(0, 11):
+    for s in range(0, 12):
         assert _abi.status_str(s) and _abi.status_str(s) != "unknown status"
 
 

@@ -1,0 +1,307 @@
+"""Span ingest decoder (include/zkingest.h): stored fragment bytes -> columnar records + indexer items.
+
+Pinned three ways: the reference's own base64 thrift fixtures (tests/golden/thrift_spans.json), an
+independent Snappy implementation (pyarrow's libsnappy) for the codec, and the span-level oracle
+(oracle/spans.py span_to_record / thrift_* validation) for every decoded field. Host-only: runs
+without a GPU. The GPU test at the end feeds decoded bytes through the HIP job."""
+import base64
+import json
+import random
+from collections import Counter
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from oracle.spans import (CORE_ANNOTATIONS, UNKNOWN_SERVICE_NAME, Annotation, BinaryAnnotation, Endpoint, Span,
+                          aggregate_job, span_to_record)
+from tests import thriftenc as T
+from tests.richgen import gen_traces
+from zipkin_amd import ZkError, _abi
+from zipkin_amd.ingest import SpanDecoder, hash_string, snappy_uncompress
+
+COLS = ("trace_id", "span_id", "parent_id", "first_ts", "last_ts", "service_id", "flags")
+GOLDEN = json.loads((Path(__file__).parent / "golden" / "thrift_spans.json").read_text())
+
+
+def records(cols):
+    return [{k: int(getattr(cols, k)[i]) for k in COLS} for i in range(len(cols))]
+
+
+def expected_records(spans):
+    ids: dict = {}
+    return [span_to_record(s, ids) for s in spans], ids
+
+
+def encode_all(spans, snappy=True):
+    return [T.snappy(T.span(s)) if snappy else T.span(s) for s in spans]
+
+
+def expected_items(spans):
+    """The span indexer (CassieSpanStore.scala:214-242) restated: only spans with annotations;
+    one key-value item per binary annotation with a host; per distinct non-core annotation value
+    the min annotation (Annotation.scala:36-38 truncated compare, first of equals), if it has a host."""
+    kv, ann = [], []
+    for s in spans:
+        if not s.annotations:
+            continue
+        for b in s.binary_annotations:
+            if b.host is not None:
+                kv.append((b.host.service_name, b.key))
+        groups: dict = {}
+        for a in s.annotations:
+            if a.value in CORE_ANNOTATIONS:
+                continue
+            m = groups.get(a.value)
+            if m is None:
+                groups[a.value] = a
+            else:
+                d = (m.timestamp - a.timestamp) & 0xFFFFFFFF
+                if d >= 2**31:
+                    d -= 2**32
+                if d > 0:
+                    groups[a.value] = a
+        for a in groups.values():
+            if a.host is not None:
+                ann.append((a.host.service_name, a.value))
+    return Counter(kv), Counter(ann)
+
+
+# ---- the reference's fixtures -------------------------------------------------------------------
+def test_encoder_is_byte_exact_with_reference_fixtures():
+    g = GOLDEN["span"]
+    s = Span(g["trace_id"], g["name"], g["id"], g["parent_id"], tuple(Annotation(t, v) for t, v in g["annotations"]))
+    assert T.span(s) == base64.b64decode(GOLDEN["with_debug"])
+    assert T.span(s, write_debug=False) == base64.b64decode(GOLDEN["without_debug"])
+
+
+@pytest.mark.parametrize("key", ["with_debug", "without_debug"])
+def test_decode_reference_fixtures(key):
+    raw = base64.b64decode(GOLDEN[key])
+    for snappy, blob in ((False, raw), (True, T.snappy(raw))):
+        dec = SpanDecoder()
+        cols, rej = dec.decode([blob], snappy=snappy)
+        assert rej == 0 and records(cols) == [GOLDEN["record"]]
+        assert dec.num_services == 0  # the annotation has no host
+
+
+# ---- Snappy --------------------------------------------------------------------------------------
+@pytest.mark.parametrize("kind", ["empty", "tiny", "random", "repetitive", "long_literal", "big"])
+def test_snappy_against_libsnappy(kind):
+    rnd = random.Random(7)
+    data = {
+        "empty": b"",
+        "tiny": b"a",
+        "random": bytes(rnd.getrandbits(8) for _ in range(5000)),
+        "repetitive": b"".join(rnd.choice([b"zipkin", b"span", b"sr", b"ss", b"\x00" * 9]) for _ in range(20000)),
+        "long_literal": bytes(rnd.getrandbits(8) for _ in range(70000)) + b"x" * 70000,
+        "big": b"".join(T.span(s) for s in gen_traces(3, 300)),
+    }[kind]
+    assert snappy_uncompress(T.snappy(data)) == data
+
+
+def test_snappy_hand_vectors():
+    # varint length 5, literal tag (len-1)<<2, then a copy-1 (len 4, offset 1) of the last byte
+    assert snappy_uncompress(b"\x05\x00a" + bytes([((4 - 4) << 2) | 1, 1])) == b"aaaaa"
+    assert snappy_uncompress(b"\x03\x08abc") == b"abc"
+    # copy-2 and copy-4 with offset 3, length 6 (overlapping copy)
+    assert snappy_uncompress(b"\x09\x08abc" + bytes([(5 << 2) | 2, 3, 0])) == b"abcabcabc"
+    assert snappy_uncompress(b"\x09\x08abc" + bytes([(5 << 2) | 3, 3, 0, 0, 0])) == b"abcabcabc"
+    # literal length in one extra byte (tag 60)
+    assert snappy_uncompress(bytes([100, 60 << 2, 99]) + b"q" * 100) == b"q" * 100
+
+
+@pytest.mark.parametrize("bad", [b"", b"\x05", b"\x05\x10ab", b"\x05\x00a" + bytes([1, 2]), b"\x03\x00a" + bytes([1, 0]),
+                                 b"\x80\x80\x80\x80\x80\x01", b"\x02\x08abc"])
+def test_snappy_corrupt_is_an_error(bad):
+    with pytest.raises(ZkError) as e:
+        snappy_uncompress(bad)
+    assert e.value.status == _abi.ZK_ERR_INVALID_SPAN
+
+
+# ---- record parity with the span oracle ----------------------------------------------------------
+@pytest.mark.parametrize("seed,anomalies,snappy", [(11, 0.0, True), (12, 0.4, True), (13, 0.4, False)])
+def test_records_equal_span_oracle(seed, anomalies, snappy):
+    spans = gen_traces(seed, 250, max_depth=5, anomalies=anomalies)
+    want, ids = expected_records(spans)
+    dec = SpanDecoder()
+    cols, rej = dec.decode(encode_all(spans, snappy), snappy=snappy)
+    assert rej == 0
+    assert records(cols) == want
+    assert dec.service_names() == list(ids)  # ids in order of first appearance
+
+
+def test_decoder_keeps_its_dictionary_across_batches():
+    spans = gen_traces(21, 120, anomalies=0.2)
+    want, ids = expected_records(spans)
+    dec = SpanDecoder()
+    got = []
+    for lo in range(0, len(spans), 37):
+        cols, _ = dec.decode(encode_all(spans[lo:lo + 37]))
+        got += records(cols)
+    assert got == want and dec.service_names() == list(ids)
+    assert dec.service_id(list(ids)[3]) == 3
+    assert dec.service_id("a-new-service") == len(ids)
+
+
+def test_edge_spans_decode_like_the_oracle():
+    e1, e2 = Endpoint(1, 80, "alpha"), Endpoint(2, 81, "Alpha")  # names are case-sensitive
+    spans = [
+        Span(1, "", 10, None),                                                 # no annotations at all
+        Span(1, "x", 11, 10, (Annotation(5, "cs", e1), Annotation(9, "cr", e1))),
+        Span(1, "x", 11, 10, (Annotation(6, "sr", e2), Annotation(8, "ss", e2))),
+        Span(-1, "x", -2, -3, (Annotation(2**62, "sr", None), Annotation(3, "cs", e1))),  # negative ids, host-less sr
+        Span(2, "x", 20, None, tuple(Annotation(t, "sr", e1) for t in (7, 3, 9, 1))),     # 4 x sr saturates at 2
+        Span(3, "x", 30, 30, (Annotation(4, "custom", e2), Annotation(1, "ss", None))),   # self-parent, no service
+    ]
+    want, ids = expected_records(spans)
+    dec = SpanDecoder()
+    cols, rej = dec.decode(encode_all(spans))
+    assert rej == 0 and records(cols) == want and dec.service_names() == list(ids) == ["alpha", "Alpha"]
+
+
+def test_missing_or_empty_service_name_is_unknown():
+    # thrift.scala:36-43: a null or "" service_name becomes Endpoint.UnknownServiceName
+    a = T._fh(T.T_I64, 1) + T._i64(5) + T._fh(T.T_STRING, 2) + T._str("sr")
+    no_name = a + T._fh(T.T_STRUCT, 3) + T.endpoint(Endpoint(1, 2, ""), service_name=None) + b"\0"
+    empty = a + T._fh(T.T_STRUCT, 3) + T.endpoint(Endpoint(1, 2, "")) + b"\0"
+    for ann in (no_name, empty):
+        body = T._fh(T.T_I64, 1) + T._i64(1) + T._fh(T.T_STRING, 3) + T._str("n") + T._fh(T.T_I64, 4) + T._i64(2)
+        body += T._fh(T.T_LIST, 6) + bytes([T.T_STRUCT]) + (1).to_bytes(4, "big") + ann + b"\0"
+        dec = SpanDecoder()
+        cols, _ = dec.decode([T.snappy(body)])
+        assert dec.service_names() == [UNKNOWN_SERVICE_NAME] and int(cols.service_id[0]) == 0
+        assert int(cols.flags[0]) & _abi.ZK_F_SVC_SERVER
+
+
+def test_unknown_fields_and_types_are_skipped():
+    s = Span(9, "n", 8, 7, (Annotation(3, "sr", Endpoint(1, 2, "svc"), duration=44), Annotation(4, "ss", None)),
+             (BinaryAnnotation("k", b"\x00\x01", "BYTES", Endpoint(1, 2, "svc")),))
+    body = T.span(s)[:-1]
+    # extra fields a newer writer could add: a map, a set of strings, a nested struct, a double
+    extra = T._fh(13, 20) + bytes([T.T_STRING, T.T_I32]) + (2).to_bytes(4, "big")
+    extra += T._str("a") + (1).to_bytes(4, "big") + T._str("b") + (2).to_bytes(4, "big")
+    extra += T._fh(14, 21) + bytes([T.T_STRING]) + (1).to_bytes(4, "big") + T._str("zz")
+    extra += T._fh(T.T_STRUCT, 22) + T._fh(4, 1) + b"\x40" + b"\0" * 7 + b"\0"
+    extra += T._fh(4, 23) + b"\x3f\xf0" + b"\0" * 6
+    want, _ = expected_records([s])
+    cols, rej = SpanDecoder().decode([T.snappy(body + extra + b"\0")])
+    assert rej == 0 and records(cols) == want
+
+
+# ---- validation (thrift.scala) -------------------------------------------------------------------
+def bad_spans():
+    e = Endpoint(1, 2, "svc")
+    ok = Span(5, "n", 50, None, (Annotation(10, "sr", e), Annotation(20, "ss", e)))
+    return ok, [
+        ("No name set in Span", T.span(ok, name=None)),
+        ("Annotation must have a timestamp", T.span(Span(5, "n", 51, 50, (Annotation(0, "sr", e),)))),
+        ("Annotation must have a timestamp", T.span(Span(5, "n", 52, 50, (Annotation(-7, "cs", e),)))),
+        ("Annotation must have a value", T.span(Span(5, "n", 53, 50, (Annotation(3, "", e),)))),
+        ("undecodable thrift span", T.span(ok)[:-9]),
+    ]
+
+
+def test_strict_rejects_like_the_reference():
+    ok, bads = bad_spans()
+    for why, blob in bads:
+        dec = SpanDecoder()
+        with pytest.raises(ZkError) as ex:
+            dec.decode([T.snappy(T.span(ok)), T.snappy(blob)])
+        assert ex.value.status == _abi.ZK_ERR_INVALID_SPAN and why in ex.value.message and "span 1" in ex.value.message
+
+
+def test_lenient_skips_and_counts():
+    ok, bads = bad_spans()
+    blobs = [T.snappy(T.span(ok))] + [T.snappy(b) for _, b in bads] + [b"\x7f\x00garbage", T.snappy(T.span(ok))]
+    want, _ = expected_records([ok, ok])
+    cols, rej = SpanDecoder().decode(blobs, strict=False)
+    assert rej == len(bads) + 1 and records(cols) == want
+
+
+def test_fuzzed_bytes_never_crash():
+    spans = gen_traces(5, 40)
+    raw = [T.span(s) for s in spans]
+    rnd = random.Random(99)
+    blobs = []
+    for r in raw:
+        b = bytearray(r)
+        for _ in range(rnd.randint(1, 6)):
+            b[rnd.randrange(len(b))] = rnd.getrandbits(8)
+        blobs.append(bytes(b[: rnd.randrange(1, len(b) + 1)] if rnd.random() < 0.3 else b))
+    for snappy in (False, True):
+        dec = SpanDecoder()
+        cols, rej = dec.decode([T.snappy(b) if snappy else b for b in blobs], strict=False)
+        assert len(cols) + rej == len(blobs)
+
+
+def test_empty_batch_and_bad_arguments():
+    cols, rej = SpanDecoder().decode([])
+    assert len(cols) == 0 and rej == 0
+    L = _abi.lib()
+    assert L.zk_ingest_create(None) == _abi.ZK_ERR_INVALID_ARG
+    dec = SpanDecoder()
+    with pytest.raises(ZkError):
+        dec.service_name(0)
+
+
+# ---- indexer items -------------------------------------------------------------------------------
+@pytest.mark.parametrize("seed", [41, 42])
+def test_items_equal_the_indexer(seed):
+    spans = gen_traces(seed, 150, anomalies=0.3)
+    # add annotation groups whose min needs the truncated (timestamp diff).toInt compare
+    e = Endpoint(3, 4, "lorem")
+    spans.append(Span(77, "n", 1, None, (Annotation(2**32 + 10, "tick", None), Annotation(5, "tick", e),
+                                          Annotation(7, "tock", e), Annotation(7, "tock", None),
+                                          Annotation(9, "sr", e))))
+    spans.append(Span(77, "n", 2, 1, (), (BinaryAnnotation("k", b"v", "String", e),)))  # no annotations: no items
+    kv_want, ann_want = expected_items(spans)
+    dec = SpanDecoder()
+    cols, rej, (kv_s, kv_k), (an_s, an_v) = dec.decode(encode_all(spans), items=True)
+    assert rej == 0
+    names = dec.service_names()
+    assert Counter((names[s], dec.string(int(h))) for s, h in zip(kv_s, kv_k)) == kv_want
+    assert Counter((names[s], dec.string(int(h))) for s, h in zip(an_s, an_v)) == ann_want
+    assert all(int(h) == hash_string(dec.string(int(h))) for h in kv_k[:50])
+
+
+def test_items_capacity_error_still_writes_records():
+    spans = gen_traces(43, 30)
+    dec = SpanDecoder()
+    with pytest.raises(ZkError) as ex:
+        dec.decode(encode_all(spans), items=True, item_cap=3)
+    assert ex.value.status == _abi.ZK_ERR_CAPACITY
+
+
+def test_hash_string_is_stable():
+    # FNV-1a 64 then the splitmix64 finalizer: fixed values (a change breaks persisted sketches)
+    def ref(b: bytes) -> int:
+        h = 0xCBF29CE484222325
+        for x in b:
+            h = ((h ^ x) * 0x100000001B3) & (2**64 - 1)
+        h = ((h ^ (h >> 30)) * 0xBF58476D1CE4E5B9) & (2**64 - 1)
+        h = ((h ^ (h >> 27)) * 0x94D049BB133111EB) & (2**64 - 1)
+        return h ^ (h >> 31)
+
+    for s in ["", "a", "http.uri", "Unknown service name", "ünïcode"]:
+        assert hash_string(s) == ref(s.encode())
+
+
+# ---- stored bytes -> dependencies on the GPU -----------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,anomalies", [(51, 0.0), (52, 0.4)])
+def test_stored_bytes_to_dependencies(gpu, seed, anomalies):
+    from zipkin_amd import DepsContext
+
+    spans = gen_traces(seed, 300, max_depth=5, anomalies=anomalies)
+    dec = SpanDecoder()
+    cols, rej = dec.decode(encode_all(spans))
+    assert rej == 0
+    names = dec.service_names()
+    with DepsContext(len(names), strict=False) as ctx:
+        ctx.accumulate(cols)
+        got = ctx.finalize()
+    ref = aggregate_job(spans, strict=False)
+    gl = {(names[p], names[c]): tuple(m) for p, c, m in got.links()}
+    want = {k: tuple(m) for k, m in ref.exact().items()}
+    assert gl == want

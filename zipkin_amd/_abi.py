@@ -25,6 +25,7 @@ ZK_ERR_NOT_CLUSTERED = 7
 ZK_ERR_NO_DEVICE = 8
 ZK_ERR_SERVICE_RANGE = 9
 ZK_ERR_UNSUPPORTED = 10
+ZK_ERR_INVALID_SPAN = 11
 
 # record flags
 ZK_F_HAS_PARENT = 1 << 0
@@ -172,6 +173,24 @@ ZK_RT_WITH_DEPS = 0
 ZK_RT_ONLY = 1
 
 
+class zk_ingest_items(C.Structure):
+    _fields_ = [
+        ("kv_service", C.c_void_p),
+        ("kv_key", C.c_void_p),
+        ("kv_cap", C.c_uint64),
+        ("kv_n", C.c_uint64),
+        ("ann_service", C.c_void_p),
+        ("ann_value", C.c_void_p),
+        ("ann_cap", C.c_uint64),
+        ("ann_n", C.c_uint64),
+    ]
+
+
+ZK_CODEC_THRIFT = 0
+ZK_CODEC_SNAPPY_THRIFT = 1
+ZK_INGEST_STRICT = 1
+
+
 class zk_moments(C.Structure):
     _fields_ = [("m0", C.c_int64), ("m1", C.c_double), ("m2", C.c_double), ("m3", C.c_double), ("m4", C.c_double)]
 
@@ -244,6 +263,22 @@ _SIGNATURES = [
     ("zk_rt_partial", C.c_int, [_P, C.POINTER(_P), _U64P, C.POINTER(_P), _U64P]),
     ("zk_rt_read", C.c_int, [_P, _P, _P]),
     ("zk_rt_dropped", C.c_int, [_P, _U64P, _U64P]),
+    # include/zkingest.h: stored span fragments -> columnar records
+    ("zk_ingest_create", C.c_int, [C.POINTER(_P)]),
+    ("zk_ingest_destroy", C.c_int, [_P]),
+    ("zk_ingest_last_error", C.c_char_p, [_P]),
+    (
+        "zk_ingest_spans",
+        C.c_int,
+        [_P, _P, _P, C.c_uint64, C.c_uint32, C.c_uint32, C.POINTER(zk_span_cols), _U64P, _U64P,
+         C.POINTER(zk_ingest_items)],
+    ),
+    ("zk_ingest_num_services", C.c_int, [_P, _U32P]),
+    ("zk_ingest_service_id", C.c_int, [_P, C.c_char_p, C.c_uint64, _U32P]),
+    ("zk_ingest_service_name", C.c_int, [_P, C.c_uint32, C.c_char_p, C.c_uint64, _U64P]),
+    ("zk_ingest_string", C.c_int, [_P, C.c_uint64, C.c_char_p, C.c_uint64, _U64P]),
+    ("zk_hash_string", C.c_uint64, [C.c_char_p, C.c_uint64]),
+    ("zk_snappy_uncompress", C.c_int, [_P, C.c_uint64, _P, C.c_uint64, _U64P]),
     # include/zkstore.h: the Aggregates store surface (host side)
     ("zk_store_create", C.c_int, [C.c_uint32, C.POINTER(_P)]),
     ("zk_store_destroy", C.c_int, [_P]),

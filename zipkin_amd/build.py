@@ -21,9 +21,10 @@ SOURCES = [
     "zk_store.cpp",
     "zk_rt.hip",
     "zk_rt_api.cpp",
+    "zk_ingest.cpp",
 ]
 HEADERS = ["zk_internal.h", "zk_tracegen.h", "zk_sketch_internal.h", "zk_rt_internal.h"]
-PUBLIC_HEADERS = ["zkagg.h", "zksketch.h", "zkstore.h"]
+PUBLIC_HEADERS = ["zkagg.h", "zksketch.h", "zkstore.h", "zkingest.h"]
 LIB = PKG / "libzkagg.so"
 ARCH = os.environ.get("ZK_OFFLOAD_ARCH", "gfx950")
 

@@ -173,6 +173,7 @@ const char* zk_status_str(zk_status s) {
         case ZK_ERR_NO_DEVICE: return "no gfx950 HIP device";
         case ZK_ERR_SERVICE_RANGE: return "service_id >= num_services";
         case ZK_ERR_UNSUPPORTED: return "unsupported";
+        case ZK_ERR_INVALID_SPAN: return "invalid or undecodable span";
     }
     return "unknown status";
 }

@@ -1,0 +1,569 @@
+// zk_ingest.cpp — stored span fragments -> 48-B columnar records (include/zkingest.h).
+//
+// One pass per fragment: [raw Snappy block ->] TBinaryProtocol Span (zipkinCore.thrift:27-58) ->
+// the reference's thrift validation (thrift.scala:36-121) -> the record of SURVEY Appendix A.1,
+// plus the span indexer's key-value / annotation items (CassieSpanStore.scala:214-242).
+// Every read is bounds-checked: corrupt input is an error, never a crash.
+#include <string.h>
+
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "zkingest.h"
+
+namespace {
+
+const char kUnknownService[] = "Unknown service name";  // Endpoint.UnknownServiceName
+
+// ---- raw Snappy block (the format iq80 Snappy.compress writes, SnappyCodec.scala:34-41) -------
+bool snappy_len(const uint8_t* in, uint64_t n, uint64_t* len, uint64_t* hdr) {
+    uint64_t v = 0;
+    for (uint64_t i = 0; i < n && i < 5; ++i) {
+        v |= (uint64_t)(in[i] & 0x7F) << (7 * i);
+        if (!(in[i] & 0x80)) {
+            *len = v;
+            *hdr = i + 1;
+            return v <= 0xFFFFFFFFull;
+        }
+    }
+    return false;
+}
+
+bool snappy_uncompress(const uint8_t* in, uint64_t n, std::vector<uint8_t>* out) {
+    uint64_t len, hdr;
+    if (!snappy_len(in, n, &len, &hdr)) return false;
+    out->resize(len);
+    uint8_t* op = out->data();
+    uint64_t o = 0;
+    uint64_t i = hdr;
+    while (i < n) {
+        const uint8_t tag = in[i++];
+        uint64_t l, off;
+        switch (tag & 3) {
+            case 0: {  // literal
+                l = tag >> 2;
+                if (l >= 60) {
+                    const uint32_t nb = (uint32_t)l - 59;
+                    if (i + nb > n) return false;
+                    l = 0;
+                    for (uint32_t k = 0; k < nb; ++k) l |= (uint64_t)in[i + k] << (8 * k);
+                    i += nb;
+                }
+                l += 1;
+                if (i + l > n || o + l > len) return false;
+                memcpy(op + o, in + i, l);
+                i += l;
+                o += l;
+                continue;
+            }
+            case 1:
+                if (i + 1 > n) return false;
+                l = ((tag >> 2) & 7) + 4;
+                off = ((uint64_t)(tag >> 5) << 8) | in[i];
+                i += 1;
+                break;
+            case 2:
+                if (i + 2 > n) return false;
+                l = (tag >> 2) + 1;
+                off = (uint64_t)in[i] | ((uint64_t)in[i + 1] << 8);
+                i += 2;
+                break;
+            default:
+                if (i + 4 > n) return false;
+                l = (tag >> 2) + 1;
+                off = (uint64_t)in[i] | ((uint64_t)in[i + 1] << 8) | ((uint64_t)in[i + 2] << 16) |
+                      ((uint64_t)in[i + 3] << 24);
+                i += 4;
+                break;
+        }
+        if (off == 0 || off > o || o + l > len) return false;
+        for (uint64_t k = 0; k < l; ++k) op[o + k] = op[o - off + k];  // may overlap: bytewise
+        o += l;
+    }
+    return o == len;
+}
+
+// ---- TBinaryProtocol ----------------------------------------------------------------------
+enum TType : uint8_t {
+    T_STOP = 0, T_BOOL = 2, T_BYTE = 3, T_DOUBLE = 4, T_I16 = 6, T_I32 = 8, T_I64 = 10, T_STRING = 11,
+    T_STRUCT = 12, T_MAP = 13, T_SET = 14, T_LIST = 15
+};
+
+struct Rd {
+    const uint8_t* p;
+    const uint8_t* e;
+    bool ok = true;
+    bool need(uint64_t k) {
+        if (!ok || (uint64_t)(e - p) < k) ok = false;
+        return ok;
+    }
+    uint8_t u8() {
+        if (!need(1)) return 0;
+        return *p++;
+    }
+    int16_t i16() {
+        if (!need(2)) return 0;
+        const int16_t v = (int16_t)((p[0] << 8) | p[1]);
+        p += 2;
+        return v;
+    }
+    int32_t i32() {
+        if (!need(4)) return 0;
+        const uint32_t v = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+        p += 4;
+        return (int32_t)v;
+    }
+    int64_t i64() {
+        if (!need(8)) return 0;
+        uint64_t v = 0;
+        for (int k = 0; k < 8; ++k) v = (v << 8) | p[k];
+        p += 8;
+        return (int64_t)v;
+    }
+    bool str(const char** s, uint32_t* len) {
+        const int32_t l = i32();
+        if (!ok || l < 0 || !need((uint64_t)l)) return ok = false;
+        *s = (const char*)p;
+        *len = (uint32_t)l;
+        p += l;
+        return true;
+    }
+    void skip(uint8_t t, int depth = 0) {
+        if (depth > 64) {
+            ok = false;
+            return;
+        }
+        switch (t) {
+            case T_BOOL:
+            case T_BYTE: u8(); break;
+            case T_I16: i16(); break;
+            case T_I32: i32(); break;
+            case T_DOUBLE:
+            case T_I64: i64(); break;
+            case T_STRING: {
+                const char* s;
+                uint32_t l;
+                str(&s, &l);
+                break;
+            }
+            case T_STRUCT:
+                for (;;) {
+                    const uint8_t ft = u8();
+                    if (!ok || ft == T_STOP) break;
+                    i16();
+                    skip(ft, depth + 1);
+                }
+                break;
+            case T_MAP: {
+                const uint8_t kt = u8(), vt = u8();
+                const int32_t n = i32();
+                if (n < 0) ok = false;
+                for (int32_t k = 0; ok && k < n; ++k) {
+                    skip(kt, depth + 1);
+                    skip(vt, depth + 1);
+                }
+                break;
+            }
+            case T_SET:
+            case T_LIST: {
+                const uint8_t et = u8();
+                const int32_t n = i32();
+                if (n < 0) ok = false;
+                for (int32_t k = 0; ok && k < n; ++k) skip(et, depth + 1);
+                break;
+            }
+            default: ok = false;
+        }
+    }
+};
+
+struct Host {
+    bool present = false;
+    const char* svc = nullptr;  // null: absent field
+    uint32_t svc_len = 0;
+};
+struct Ann {
+    int64_t ts = 0;
+    const char* value = nullptr;
+    uint32_t value_len = 0;
+    Host host;
+};
+struct BinAnn {
+    const char* key = nullptr;
+    uint32_t key_len = 0;
+    Host host;
+};
+struct SpanT {
+    int64_t trace_id = 0, id = 0, parent_id = 0;
+    bool has_parent = false, has_name = false;
+    std::vector<Ann> anns;
+    std::vector<BinAnn> banns;
+    void clear() {
+        trace_id = id = parent_id = 0;
+        has_parent = has_name = false;
+        anns.clear();
+        banns.clear();
+    }
+};
+
+void read_endpoint(Rd& r, Host* h) {
+    h->present = true;
+    for (;;) {
+        const uint8_t t = r.u8();
+        if (!r.ok || t == T_STOP) return;
+        const int16_t id = r.i16();
+        if (id == 3 && t == T_STRING)
+            r.str(&h->svc, &h->svc_len);
+        else
+            r.skip(t);
+    }
+}
+
+void read_annotation(Rd& r, Ann* a) {
+    for (;;) {
+        const uint8_t t = r.u8();
+        if (!r.ok || t == T_STOP) return;
+        const int16_t id = r.i16();
+        if (id == 1 && t == T_I64)
+            a->ts = r.i64();
+        else if (id == 2 && t == T_STRING)
+            r.str(&a->value, &a->value_len);
+        else if (id == 3 && t == T_STRUCT)
+            read_endpoint(r, &a->host);
+        else
+            r.skip(t);
+    }
+}
+
+void read_binary_annotation(Rd& r, BinAnn* b) {
+    for (;;) {
+        const uint8_t t = r.u8();
+        if (!r.ok || t == T_STOP) return;
+        const int16_t id = r.i16();
+        if (id == 1 && t == T_STRING)
+            r.str(&b->key, &b->key_len);
+        else if (id == 4 && t == T_STRUCT)
+            read_endpoint(r, &b->host);
+        else
+            r.skip(t);
+    }
+}
+
+bool read_span(Rd& r, SpanT* s) {
+    for (;;) {
+        const uint8_t t = r.u8();
+        if (!r.ok) return false;
+        if (t == T_STOP) return true;
+        const int16_t id = r.i16();
+        if (id == 1 && t == T_I64) {
+            s->trace_id = r.i64();
+        } else if (id == 3 && t == T_STRING) {
+            const char* nm;
+            uint32_t l;
+            s->has_name = r.str(&nm, &l);
+        } else if (id == 4 && t == T_I64) {
+            s->id = r.i64();
+        } else if (id == 5 && t == T_I64) {
+            s->parent_id = r.i64();
+            s->has_parent = true;
+        } else if ((id == 6 || id == 8) && t == T_LIST) {
+            const uint8_t et = r.u8();
+            const int32_t n = r.i32();
+            if (!r.ok || n < 0 || et != T_STRUCT) {
+                if (r.ok && n >= 0) {  // a list of something else: skip it
+                    for (int32_t k = 0; r.ok && k < n; ++k) r.skip(et);
+                    continue;
+                }
+                return false;
+            }
+            for (int32_t k = 0; r.ok && k < n; ++k) {
+                if (id == 6) {
+                    s->anns.emplace_back();
+                    read_annotation(r, &s->anns.back());
+                } else {
+                    s->banns.emplace_back();
+                    read_binary_annotation(r, &s->banns.back());
+                }
+            }
+        } else {
+            r.skip(t);
+        }
+        if (!r.ok) return false;
+    }
+}
+
+bool is_core(const char* v, uint32_t l) {
+    return v && l == 2 && ((v[0] == 'c' && (v[1] == 's' || v[1] == 'r')) || (v[0] == 's' && (v[1] == 'r' || v[1] == 's')));
+}
+
+uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+}  // namespace
+
+struct zk_ingest {
+    std::unordered_map<std::string, uint32_t> svc_ids;
+    std::vector<std::string> svc_names;
+    std::unordered_map<uint64_t, std::string> strings;
+    std::vector<uint8_t> scratch;
+    SpanT span;
+    std::string err;
+
+    uint32_t service(const Host& h) {
+        // thrift.scala:36-43: null or "" service name -> Endpoint.UnknownServiceName
+        std::string name = (h.svc && h.svc_len) ? std::string(h.svc, h.svc_len) : std::string(kUnknownService);
+        auto it = svc_ids.find(name);
+        if (it != svc_ids.end()) return it->second;
+        const uint32_t id = (uint32_t)svc_names.size();
+        svc_ids.emplace(name, id);
+        svc_names.push_back(std::move(name));
+        return id;
+    }
+    uint64_t intern(const char* s, uint32_t l) {
+        const uint64_t h = zk_hash_string(s, l);
+        if (strings.find(h) == strings.end()) strings.emplace(h, std::string(s ? s : "", s ? l : 0));
+        return h;
+    }
+};
+
+extern "C" {
+
+uint64_t zk_hash_string(const char* s, uint64_t len) {
+    uint64_t h = 0xCBF29CE484222325ull;  // FNV-1a 64
+    for (uint64_t i = 0; s && i < len; ++i) {
+        h ^= (uint8_t)s[i];
+        h *= 0x100000001B3ull;
+    }
+    return mix64(h);
+}
+
+zk_status zk_snappy_uncompress(const uint8_t* in, uint64_t in_len, uint8_t* out, uint64_t cap, uint64_t* out_len) {
+    if (!in || !out_len) return ZK_ERR_INVALID_ARG;
+    uint64_t len, hdr;
+    if (!snappy_len(in, in_len, &len, &hdr)) return ZK_ERR_INVALID_SPAN;
+    *out_len = len;
+    if (!out) return ZK_OK;
+    if (cap < len) return ZK_ERR_CAPACITY;
+    std::vector<uint8_t> tmp;
+    if (!snappy_uncompress(in, in_len, &tmp)) return ZK_ERR_INVALID_SPAN;
+    memcpy(out, tmp.data(), len);
+    return ZK_OK;
+}
+
+zk_status zk_ingest_create(zk_ingest** out) {
+    if (!out) return ZK_ERR_INVALID_ARG;
+    *out = new zk_ingest();
+    return ZK_OK;
+}
+
+zk_status zk_ingest_destroy(zk_ingest* g) {
+    if (!g) return ZK_ERR_INVALID_ARG;
+    delete g;
+    return ZK_OK;
+}
+
+const char* zk_ingest_last_error(const zk_ingest* g) { return g ? g->err.c_str() : "null decoder"; }
+
+zk_status zk_ingest_spans(zk_ingest* g, const uint8_t* buf, const uint64_t* offsets, uint64_t n, uint32_t codec,
+                          uint32_t flags, const zk_span_cols* out, uint64_t* n_out, uint64_t* n_rejected,
+                          zk_ingest_items* items) {
+    if (!g || !n_out || !n_rejected) return ZK_ERR_INVALID_ARG;
+    *n_out = *n_rejected = 0;
+    if (items) items->kv_n = items->ann_n = 0;
+    if (n == 0) return ZK_OK;
+    if (!buf || !offsets || !out || !out->trace_id || !out->span_id || !out->parent_id || !out->first_ts ||
+        !out->last_ts || !out->service_id || !out->flags)
+        return ZK_ERR_INVALID_ARG;
+    if (codec != ZK_CODEC_THRIFT && codec != ZK_CODEC_SNAPPY_THRIFT) {
+        g->err = "unknown codec";
+        return ZK_ERR_INVALID_ARG;
+    }
+    uint64_t* o_tid = (uint64_t*)out->trace_id;
+    uint64_t* o_sid = (uint64_t*)out->span_id;
+    uint64_t* o_pid = (uint64_t*)out->parent_id;
+    int64_t* o_first = (int64_t*)out->first_ts;
+    int64_t* o_last = (int64_t*)out->last_ts;
+    uint32_t* o_svc = (uint32_t*)out->service_id;
+    uint32_t* o_flags = (uint32_t*)out->flags;
+    const bool strict = (flags & ZK_INGEST_STRICT) != 0;
+    bool item_overflow = false;
+    uint64_t k = 0;
+    std::vector<const Ann*> distinct;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (offsets[i + 1] < offsets[i]) {
+            g->err = "offsets not ascending at span " + std::to_string(i);
+            return ZK_ERR_INVALID_ARG;
+        }
+        const uint8_t* p = buf + offsets[i];
+        uint64_t len = offsets[i + 1] - offsets[i];
+        if (codec == ZK_CODEC_SNAPPY_THRIFT) {
+            if (!snappy_uncompress(p, len, &g->scratch)) {
+                if (strict) {
+                    g->err = "span " + std::to_string(i) + ": corrupt snappy block";
+                    return ZK_ERR_INVALID_SPAN;
+                }
+                ++*n_rejected;
+                continue;
+            }
+            p = g->scratch.data();
+            len = g->scratch.size();
+        }
+        SpanT& s = g->span;
+        s.clear();
+        Rd r{p, p + len};
+        const char* why = nullptr;
+        if (!read_span(r, &s))
+            why = "undecodable thrift span";
+        else if (!s.has_name)
+            why = "No name set in Span";  // IncompleteTraceDataException (thrift.scala:101-104)
+        else
+            for (const Ann& a : s.anns) {
+                if (a.ts <= 0) {
+                    why = "Annotation must have a timestamp";  // thrift.scala:66-67
+                    break;
+                }
+                if (a.value && a.value_len == 0) {
+                    why = "Annotation must have a value";  // thrift.scala:69-70
+                    break;
+                }
+            }
+        if (why) {
+            if (strict) {
+                g->err = "span " + std::to_string(i) + ": " + why;
+                return ZK_ERR_INVALID_SPAN;
+            }
+            ++*n_rejected;
+            continue;
+        }
+        // ---- the record ----
+        uint32_t f = s.has_parent ? ZK_F_HAS_PARENT : 0u;
+        int64_t first = 0, last = 0;
+        uint32_t cnt[4] = {0, 0, 0, 0};  // cs, cr, sr, ss
+        const Host* srv = nullptr;
+        const Host* cli = nullptr;
+        for (size_t q = 0; q < s.anns.size(); ++q) {
+            const Ann& a = s.anns[q];
+            if (q == 0 || a.ts < first) first = a.ts;
+            if (q == 0 || a.ts > last) last = a.ts;
+            if (is_core(a.value, a.value_len)) {
+                const int c = a.value[0] == 'c' ? (a.value[1] == 's' ? 0 : 1) : (a.value[1] == 'r' ? 2 : 3);
+                if (cnt[c] < 2) ++cnt[c];
+                if (a.host.present) {
+                    if (c >= 2 && !srv) srv = &a.host;
+                    if (c < 2 && !cli) cli = &a.host;
+                }
+            }
+        }
+        if (!s.anns.empty()) f |= ZK_F_HAS_ANNOTATIONS;
+        uint32_t svc = 0;
+        if (srv) {
+            f |= ZK_F_SVC_SERVER;
+            svc = g->service(*srv);
+        } else if (cli) {
+            f |= ZK_F_SVC_CLIENT;
+            svc = g->service(*cli);
+        }
+        f |= (cnt[0] << ZK_F_CS_SHIFT) | (cnt[1] << ZK_F_CR_SHIFT) | (cnt[2] << ZK_F_SR_SHIFT) | (cnt[3] << ZK_F_SS_SHIFT);
+        o_tid[k] = (uint64_t)s.trace_id;
+        o_sid[k] = (uint64_t)s.id;
+        o_pid[k] = s.has_parent ? (uint64_t)s.parent_id : 0ull;
+        o_first[k] = s.anns.empty() ? 0 : first;
+        o_last[k] = s.anns.empty() ? 0 : last;
+        o_svc[k] = svc;
+        o_flags[k] = f;
+        ++k;
+        // ---- indexer items: only spans with a last annotation (CassieSpanStore.scala:214-218) ----
+        if (!items || s.anns.empty()) continue;
+        if (items->kv_service && items->kv_key) {
+            for (const BinAnn& b : s.banns) {  // :235-241 one per binary annotation with a host
+                if (!b.host.present) continue;
+                if (items->kv_n >= items->kv_cap) {
+                    item_overflow = true;
+                    continue;
+                }
+                items->kv_service[items->kv_n] = g->service(b.host);
+                items->kv_key[items->kv_n] = g->intern(b.key, b.key_len);
+                ++items->kv_n;
+            }
+        }
+        if (items->ann_service && items->ann_value) {
+            // :222-233 non-core annotations grouped by value; the group's min (Annotation.compare:
+            // (a.timestamp - b.timestamp).toInt, Annotation.scala:36-38; min keeps the first of
+            // equals) yields one item if it has a host
+            distinct.clear();
+            for (const Ann& a : s.anns) {
+                if (is_core(a.value, a.value_len)) continue;
+                bool seen = false;
+                for (const Ann*& d : distinct) {
+                    if (d->value_len == a.value_len && (a.value_len == 0 || memcmp(d->value, a.value, a.value_len) == 0) &&
+                        (d->value == nullptr) == (a.value == nullptr)) {
+                        if ((int32_t)(uint32_t)((uint64_t)d->ts - (uint64_t)a.ts) > 0) d = &a;  // truncated compare
+                        seen = true;
+                        break;
+                    }
+                }
+                if (!seen) distinct.push_back(&a);
+            }
+            for (const Ann* a : distinct) {
+                if (!a->host.present) continue;
+                if (items->ann_n >= items->ann_cap) {
+                    item_overflow = true;
+                    continue;
+                }
+                items->ann_service[items->ann_n] = g->service(a->host);
+                items->ann_value[items->ann_n] = g->intern(a->value, a->value_len);
+                ++items->ann_n;
+            }
+        }
+    }
+    *n_out = k;
+    if (item_overflow) {
+        g->err = "item buffer too small";
+        return ZK_ERR_CAPACITY;
+    }
+    return ZK_OK;
+}
+
+zk_status zk_ingest_num_services(const zk_ingest* g, uint32_t* n) {
+    if (!g || !n) return ZK_ERR_INVALID_ARG;
+    *n = (uint32_t)g->svc_names.size();
+    return ZK_OK;
+}
+
+zk_status zk_ingest_service_id(zk_ingest* g, const char* name, uint64_t len, uint32_t* id) {
+    if (!g || !id || (!name && len)) return ZK_ERR_INVALID_ARG;
+    Host h;
+    h.present = true;
+    h.svc = name;
+    h.svc_len = (uint32_t)len;
+    *id = g->service(h);
+    return ZK_OK;
+}
+
+zk_status zk_ingest_service_name(const zk_ingest* g, uint32_t id, char* buf, uint64_t cap, uint64_t* len) {
+    if (!g || !len) return ZK_ERR_INVALID_ARG;
+    if (id >= g->svc_names.size()) return ZK_ERR_SERVICE_RANGE;
+    const std::string& s = g->svc_names[id];
+    *len = s.size();
+    if (!buf) return ZK_OK;
+    if (cap < s.size()) return ZK_ERR_CAPACITY;
+    memcpy(buf, s.data(), s.size());
+    return ZK_OK;
+}
+
+zk_status zk_ingest_string(const zk_ingest* g, uint64_t hash, char* buf, uint64_t cap, uint64_t* len) {
+    if (!g || !len) return ZK_ERR_INVALID_ARG;
+    auto it = g->strings.find(hash);
+    if (it == g->strings.end()) return ZK_ERR_INVALID_ARG;
+    *len = it->second.size();
+    if (!buf) return ZK_OK;
+    if (cap < it->second.size()) return ZK_ERR_CAPACITY;
+    memcpy(buf, it->second.data(), it->second.size());
+    return ZK_OK;
+}
+
+}  // extern "C"

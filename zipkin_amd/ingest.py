@@ -1,0 +1,118 @@
+"""SpanDecoder: stored span fragments (Snappy + TBinaryProtocol thrift Span) -> SpanColumns.
+
+Binds include/zkingest.h. The decoder owns the service-name dictionary; its ids are the
+service ids of the columnar records (zkagg.h), the dependency table and the sketches.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Sequence
+
+import numpy as np
+
+from . import _abi
+from .columns import SpanColumns
+
+
+def hash_string(s: str | bytes) -> int:
+    b = s.encode() if isinstance(s, str) else s
+    return int(_abi.lib().zk_hash_string(b, len(b)))
+
+
+class SpanDecoder:
+    def __init__(self):
+        self._L = _abi.lib()
+        h = C.c_void_p()
+        st = self._L.zk_ingest_create(C.byref(h))
+        if st != _abi.ZK_OK:
+            raise _abi.ZkError(st, _abi.status_str(st))
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.zk_ingest_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, st: int) -> None:
+        if st != _abi.ZK_OK:
+            raise _abi.ZkError(st, self._L.zk_ingest_last_error(self._h).decode() or _abi.status_str(st))
+
+    def decode(self, blobs: Sequence[bytes], *, snappy: bool = True, strict: bool = True, items: bool = False,
+               item_cap: int | None = None):
+        """Decode stored fragments (one bytes object each). Returns (SpanColumns, rejected) or, with
+        items=True, (SpanColumns, rejected, (kv_service, kv_key), (ann_service, ann_value))."""
+        n = len(blobs)
+        offsets = np.zeros(n + 1, np.uint64)
+        if n:
+            offsets[1:] = np.cumsum([len(b) for b in blobs], dtype=np.uint64)
+        buf = np.frombuffer(b"".join(blobs) or b"\0", dtype=np.uint8)
+        cols = SpanColumns.empty(n)
+        nout, nrej = C.c_uint64(), C.c_uint64()
+        it = None
+        arrs = None
+        if items:
+            cap = item_cap if item_cap is not None else max(16, 8 * n)
+            arrs = (np.zeros(cap, np.uint32), np.zeros(cap, np.uint64), np.zeros(cap, np.uint32), np.zeros(cap, np.uint64))
+            it = _abi.zk_ingest_items(arrs[0].ctypes.data, arrs[1].ctypes.data, cap, 0,
+                                      arrs[2].ctypes.data, arrs[3].ctypes.data, cap, 0)
+        codec = _abi.ZK_CODEC_SNAPPY_THRIFT if snappy else _abi.ZK_CODEC_THRIFT
+        flags = _abi.ZK_INGEST_STRICT if strict else 0
+        ab = cols.abi()
+        self._check(self._L.zk_ingest_spans(self._h, buf.ctypes.data, offsets.ctypes.data, n, codec, flags,
+                                            C.byref(ab), C.byref(nout), C.byref(nrej),
+                                            C.byref(it) if it is not None else None))
+        cols = cols.take(slice(0, nout.value))
+        if not items:
+            return cols, int(nrej.value)
+        kv = (arrs[0][: it.kv_n].copy(), arrs[1][: it.kv_n].copy())
+        ann = (arrs[2][: it.ann_n].copy(), arrs[3][: it.ann_n].copy())
+        return cols, int(nrej.value), kv, ann
+
+    @property
+    def num_services(self) -> int:
+        n = C.c_uint32()
+        self._check(self._L.zk_ingest_num_services(self._h, C.byref(n)))
+        return int(n.value)
+
+    def service_id(self, name: str) -> int:
+        b = name.encode()
+        i = C.c_uint32()
+        self._check(self._L.zk_ingest_service_id(self._h, b, len(b), C.byref(i)))
+        return int(i.value)
+
+    def service_name(self, i: int) -> str:
+        ln = C.c_uint64()
+        self._check(self._L.zk_ingest_service_name(self._h, i, None, 0, C.byref(ln)))
+        buf = C.create_string_buffer(max(1, ln.value))
+        self._check(self._L.zk_ingest_service_name(self._h, i, buf, ln.value, C.byref(ln)))
+        return buf.raw[: ln.value].decode()
+
+    def service_names(self) -> List[str]:
+        return [self.service_name(i) for i in range(self.num_services)]
+
+    def string(self, h: int) -> str:
+        ln = C.c_uint64()
+        self._check(self._L.zk_ingest_string(self._h, h, None, 0, C.byref(ln)))
+        buf = C.create_string_buffer(max(1, ln.value))
+        self._check(self._L.zk_ingest_string(self._h, h, buf, ln.value, C.byref(ln)))
+        return buf.raw[: ln.value].decode()
+
+
+def snappy_uncompress(data: bytes) -> bytes:
+    L = _abi.lib()
+    src = np.frombuffer(data or b"\0", dtype=np.uint8)
+    n = C.c_uint64()
+    st = L.zk_snappy_uncompress(src.ctypes.data, len(data), None, 0, C.byref(n))
+    if st != _abi.ZK_OK:
+        raise _abi.ZkError(st, _abi.status_str(st))
+    out = np.zeros(max(1, n.value), np.uint8)
+    st = L.zk_snappy_uncompress(src.ctypes.data, len(data), out.ctypes.data, n.value, C.byref(n))
+    if st != _abi.ZK_OK:
+        raise _abi.ZkError(st, _abi.status_str(st))
+    return out[: n.value].tobytes()
