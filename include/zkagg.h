@@ -46,7 +46,8 @@ typedef enum zk_status {
     ZK_ERR_DURATION_RANGE = 4,   /* a joined child duration >= 2^40 us (12.7 days, longer than the
                                     7-day span TTL, CassieSpanStore.scala:47); link not counted */
     ZK_ERR_TRACE_TOO_LARGE = 5,  /* a trace longer than zk_config.max_trace_records */
-    ZK_ERR_CAPACITY = 6,         /* exact-accumulator headroom exhausted (> 2^32-1 records since reset) */
+    ZK_ERR_CAPACITY = 6,         /* exact-accumulator headroom exhausted (> 2^32-1 records since reset),
+                                    or a caller buffer too small */
     ZK_ERR_NOT_CLUSTERED = 7,    /* batch flags did not promise trace-clustered input */
     ZK_ERR_NO_DEVICE = 8,        /* no HIP device / not gfx950 */
     ZK_ERR_SERVICE_RANGE = 9,    /* a record carries service_id >= num_services */

@@ -219,6 +219,56 @@ def test_empty_single_and_unclustered(gpu):
         assert e.value.status == _abi.ZK_ERR_NOT_CLUSTERED
 
 
+M32 = 0xFFFFFFFF
+
+
+def sid_key(sid):
+    """A 32-bit fold of a span id (low word ^ high word * golden ratio)."""
+    return ((sid & M32) ^ (((sid >> 32) * 0x9E3779B1) & M32)) & M32
+
+
+def colliding(sid, hi):
+    """A different span id with high word `hi` and the same 32-bit key as `sid`."""
+    lo = ((sid & M32) ^ (((sid >> 32) * 0x9E3779B1) & M32) ^ ((hi * 0x9E3779B1) & M32)) & M32
+    out = (hi << 32) | lo
+    assert out != sid and sid_key(out) == sid_key(sid)
+    return out
+
+
+def collision_trace(tid, rng, nsvc=9):
+    """A trace whose span ids agree in a 32-bit fold: sibling spans A and B, a grandchild under B,
+    and a child whose absent parent folds like the root. Any key or hash narrower than the full
+    64-bit span id would merge or join them wrongly."""
+    t0 = 1_000_000 + tid
+    root = int(rng.integers(1, 2**63))
+    a = int(rng.integers(1, 2**63))
+    b = colliding(a, int(rng.integers(1, 2**31)))
+    c = int(rng.integers(1, 2**63))
+    ghost = colliding(root, int(rng.integers(1, 2**31)))  # never stored
+    d = int(rng.integers(1, 2**63))
+    sv = lambda: int(rng.integers(0, nsvc))
+    rows = [(tid, root, 0, t0, t0 + 900, sv(), SERVER)]
+    for sid, par, dt in ((a, root, 10), (b, root, 20), (c, b, 30), (d, ghost, 40)):
+        s1 = sv()
+        rows.append((tid, sid, par, t0 + dt + 5, t0 + dt + 50, s1, SERVER | 1))
+        rows.append((tid, sid, par, t0 + dt, t0 + dt + 60 + (tid % 7), s1, CLIENT | 1))
+    order = rng.permutation(len(rows))
+    return [rows[i] for i in order]
+
+
+def test_span_id_key_collisions_are_exact(gpu):
+    rng = np.random.default_rng(77)
+    rows = []
+    for t in range(3000):
+        if t % 10 == 3:
+            rows += collision_trace(10_000 + t, rng)
+        else:
+            rows += star_trace(10_000 + t, int(rng.integers(0, 40)), svc_root=int(rng.integers(0, 9)), nsvc=9)
+    cols = cols_from_rows(rows)
+    got, st = run_gpu(cols, 9)
+    assert_parity(got, st, oracle.aggregate(cols, 9))
+
+
 def test_trace_too_large(gpu):
     cols = cols_from_rows(star_trace(5, 4000))
     with DepsContext(7, max_trace_records=5000) as ctx:

@@ -126,7 +126,7 @@ zk_status ensure_links(zk_ctx* c, uint32_t grid, uint64_t stride) {
 bool aligned(const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; }
 
 zk_status ensure_spill(zk_ctx* c, uint64_t n) {
-    const uint64_t need = tiles_for(n) + 1;
+    const uint64_t need = tiles_for(n) + 1;  // a spilled trace is longer than a tile
     if (need > c->spill_cap) {
         if (c->spill_list) ZK_HIP(c, hipFree(c->spill_list));
         uint64_t cap = need < (1ull << 16) ? (1ull << 16) : need;
@@ -451,6 +451,8 @@ zk_status zk_deps_finalize(zk_ctx* c, const zk_link_table* out) {
     zk_status st = stats_sum(c, s);
     if (st != ZK_OK) return st;
     if (s[ST_TOO_LARGE]) return fail(c, ZK_ERR_TRACE_TOO_LARGE, "trace longer than max_trace_records skipped");
+    if (s[ST_SPILL_OVERFLOW])
+        return fail(c, ZK_ERR_CAPACITY, "spill list overflow");
     if (s[ST_SVC_RANGE]) return fail(c, ZK_ERR_SERVICE_RANGE, "record with service_id >= num_services");
     if (s[ST_DUR_RANGE]) return fail(c, ZK_ERR_DURATION_RANGE, "link with duration >= 2^40 us dropped");
     if (c->strict && s[ST_NO_SERVICE])

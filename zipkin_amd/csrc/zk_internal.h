@@ -46,7 +46,8 @@ enum Stat : int {
     ST_DUR_RANGE,
     ST_SVC_RANGE,
     ST_TOO_LARGE,
-    ST_RT_DUR_RANGE,  // sketch items dropped for a duration >= 2^40 us (not in zk_stats)
+    ST_RT_DUR_RANGE,     // sketch items dropped for a duration >= 2^40 us (not in zk_stats)
+    ST_SPILL_OVERFLOW,   // spill-list pushes past its capacity (cannot happen: one per tile at most)
     ST_N = 16
 };
 constexpr int kStatShards = 256;  // stats buffer = kStatShards x ST_N u64

@@ -19,6 +19,10 @@
 #include "zk_internal.h"
 #include "zk_sketch_internal.h"
 
+#ifndef ZK_HASH_FACTOR
+#define ZK_HASH_FACTOR 8
+#endif
+
 namespace zk {
 namespace {
 
@@ -154,12 +158,7 @@ __device__ __forceinline__ void flush_stats(StatPack& sp, uint32_t* s_stat, unsi
 }
 
 // =============================================================================================
-// K1: tile kernel
-//
-// Workgroup = 256 threads owning the traces that START in records [lo, lo + TILE); a trace may
-// overhang the tile by up to TILE records (CAP = 2 TILE), longer ones are spilled. Thread t holds
-// records 2t, 2t+1 (+TILE for the overhang), so every u64 column is read with one 16-byte load
-// per lane. LDS is 46 KB, i.e. three workgroups per CU: one loads while the others merge/join.
+// K1 LDS hash
 //
 // Hash slot word (u32): bits 0..10 leader index + 1; bits 12..15 "seen >= 1" and 16..19
 // "seen >= 2" for cs, cr, sr, ss (Span.isValid = no ">= 2" bit); bit 20 some fragment has a
@@ -221,22 +220,28 @@ __device__ __forceinline__ void ld2_u32(const uint32_t* __restrict__ p, uint64_t
     v[1] = x.y;
 }
 
-// per-thread stat counters: 16 x 32-bit fields (flushed once per workgroup)
-struct StatPack32 {
-    uint64_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    __device__ __forceinline__ void inc(int s) { w[s >> 1] += 1ull << (32 * (s & 1)); }
-};
+// K1 stat counters: the per-thread 16-bit pack (StatPack) is folded into the workgroup's u32 LDS
+// totals every kFoldWindows windows (a lane adds <= 2 per stat per window, so a wave sum of 64
+// lanes stays below 2^16), and the totals go to a sharded global slot once at the end.
+constexpr int kFoldWindows = 256;
 
-__device__ __forceinline__ void flush_stats32(StatPack32& sp, uint32_t* s_stat, unsigned long long* g_stats) {
+__device__ __forceinline__ void fold_stats(StatPack& sp, uint32_t* s_stat) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 4; ++i) {
         const uint64_t v = wave_sum_u64(sp.w[i]);
         if (lane == 0 && v) {
-            if ((uint32_t)v) atomicAdd(&s_stat[2 * i], (uint32_t)v);
-            if ((uint32_t)(v >> 32)) atomicAdd(&s_stat[2 * i + 1], (uint32_t)(v >> 32));
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+                const uint32_t x = (uint32_t)((v >> (16 * f)) & 0xFFFFull);
+                if (x) atomicAdd(&s_stat[i * 4 + f], x);
+            }
         }
+        sp.w[i] = 0;
     }
+}
+
+__device__ __forceinline__ void publish_stats(const uint32_t* s_stat, unsigned long long* g_stats) {
     __syncthreads();
     if (threadIdx.x < ST_N) {
         const uint32_t v = s_stat[threadIdx.x];
@@ -279,7 +284,7 @@ __device__ __forceinline__ void load_window(const JoinArgs& a, uint64_t ws, Wind
 // merged, validated and joined in LDS; the incomplete last trace starts the next window (its
 // records are re-read, mostly from L2). The next window's columns are prefetched into registers
 // right after its start is known, so HBM streams while the LDS phases run. A trace longer than a
-// window goes to the spill kernel. Three workgroups per CU (23 KB LDS, <= 168 VGPRs).
+// window goes to the spill kernel. Four workgroups per CU (<= 32 KB LDS, <= 128 VGPRs).
 //
 // Hash slot word (u32): bits 0..10 leader index + 1; bits 12..15 "seen >= 1" and 16..19
 // "seen >= 2" for cs, cr, sr, ss (Span.isValid = no ">= 2" bit); bit 20 some fragment has a
@@ -291,16 +296,16 @@ constexpr int kModeJoin = 1;
 constexpr int kModeEmit = 2;
 template <int TILE, int WG, int ABL, int MODE>
 __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
-    constexpr int H = 2 * TILE;
+    constexpr int H = ZK_HASH_FACTOR * TILE;  // load <= 1/16 (distinct spans / slots): short probe chains, since a wave waits for its longest
     constexpr int NWORD = TILE / 64;
     static_assert(TILE == 2 * WG && TILE <= 2047, "two records per thread");
-    __shared__ uint64_t s_sid[TILE];
-    __shared__ long long s_first[TILE];
-    __shared__ long long s_last[TILE];
-    __shared__ uint64_t s_pid[TILE];
-    __shared__ uint32_t s_svck[TILE];
-    __shared__ uint16_t s_seg[TILE];
-    __shared__ uint32_t s_ht[H];
+    __shared__ __align__(16) uint64_t s_sid[TILE];
+    __shared__ __align__(16) long long s_first[TILE];
+    __shared__ __align__(16) long long s_last[TILE];
+    __shared__ __align__(16) uint64_t s_pid[TILE];
+    __shared__ __align__(16) uint32_t s_svck[TILE];
+    __shared__ __align__(16) uint16_t s_seg[TILE];
+    __shared__ __align__(16) uint32_t s_ht[H];
     __shared__ uint64_t s_mask[NWORD];
     __shared__ uint32_t s_stat[ST_N];
     __shared__ uint32_t s_wsum[WG / 64];
@@ -325,7 +330,8 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
     uint32_t nitem = 0;       // sketch items written by this workgroup (uniform)
     uint32_t nout = 0;        // links written by this workgroup (uniform)
     uint64_t nrec = 0;        // records aggregated (uniform)
-    StatPack32 st;
+    StatPack st;
+    int fold_in = kFoldWindows;  // windows until the next stat fold (uniform)
     if (tid < ST_N) s_stat[tid] = 0u;
     for (uint32_t x = tid; x < a.nb; x += WG) s_hist[x] = 0u;
 
@@ -357,12 +363,20 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
         // wave-parallel over the NWORD mask words (lane w holds word w): the first boundary >= lo_j
         // (start), the first >= r1_j (stop) and the last boundary of the window (last_b)
         int start = -1, stop = -1, last_b = -1;  // wave-uniform (SGPRs)
+        int lastb;                                // per lane w < NWORD
         {
             static_assert(NWORD <= 64, "one mask word per lane");
             const int base = 64 * lane;
             const uint64_t x = lane < NWORD ? s_mask[lane] : 0ull;
             const uint64_t ys = lo_j >= base + 64 ? 0ull : (lo_j > base ? (x & (~0ull << (lo_j - base))) : x);
             const uint64_t yt = r1_j >= base + 64 ? 0ull : (r1_j > base ? (x & (~0ull << (r1_j - base))) : x);
+            // lastb: the last boundary in words 0..lane (max-scan); phase 3 reads it by shuffle
+            lastb = x ? base + 63 - (int)__clzll((long long)x) : -1;
+#pragma unroll
+            for (int off = 1; off < NWORD; off <<= 1) {
+                const int o = __shfl_up(lastb, off);
+                if (lane >= off) lastb = o > lastb ? o : lastb;
+            }
             const uint64_t bs = __ballot(ys != 0ull), bt = __ballot(yt != 0ull), bl = __ballot(x != 0ull);
             if (bs) {
                 const int w = __ffsll((unsigned long long)bs) - 1;
@@ -402,7 +416,10 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
             // the trace at `start` is longer than a window: spill it, then seek past it
             if (tid == 0) {
                 const unsigned int idx = atomicAdd(a.spill_count, 1u);
-                if (idx < a.spill_cap) a.spill_list[idx] = ws + (uint64_t)start;
+                if (idx < a.spill_cap)
+                    a.spill_list[idx] = ws + (uint64_t)start;
+                else
+                    atomicAdd(&a.stats[ST_SPILL_OVERFLOW], 1ull);
                 atomicAdd(&a.stats[ST_SPILLED], 1ull);
             }
             m = start;
@@ -416,32 +433,45 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
         if constexpr (ABL != 2) {  // diagnostic build: 2 = stream windows only
 
         // ---- 3. segment ids and LDS staging ----------------------------------------------------
+        // seg = index of the trace's first record in the window (the last boundary <= j). One mask
+        // read per thread: record 2t+1 is its own segment start or shares 2t's. Staging stores are
+        // unconditional 16-B pairs (entries outside [start, m) are never read).
         int r_seg[2];
         uint32_t r_svck[2];
         bool r_rerr[2];
+        {
+            const int j0 = 2 * tid;
+            const int w = j0 >> 6;
+            uint64_t bits = s_mask[w];
+            const bool b1 = (bits >> ((j0 + 1) & 63)) & 1ull;
+            bits &= (2ull << (j0 & 63)) - 1ull;
+            // no boundary in this word up to j0: the last one of the earlier words (it exists when
+            // j0 >= start, since start is a boundary)
+            const int prevw = __shfl(lastb, w > 0 ? w - 1 : 0);
+            int seg0 = -1;
+            if (j0 >= start && j0 < m) seg0 = bits ? 64 * w + 63 - (int)__clzll((long long)bits) : prevw;
+            r_seg[0] = seg0;
+            r_seg[1] = (j0 + 1 >= start && j0 + 1 < m) ? (b1 ? j0 + 1 : seg0) : -1;
+            uint64_t v_first[2], v_last[2], v_pid[2];
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const int j = 2 * tid + e;
-            r_rerr[e] = false;
-            r_svck[e] = svc_key(cur.flags[e], cur.svc[e], a.S, &r_rerr[e]);
-            r_seg[e] = -1;
-            if (j >= start && j < m) {
-                int w = j >> 6;
-                uint64_t bits = s_mask[w] & ((2ull << (j & 63)) - 1ull);
-                while (!bits) bits = s_mask[--w];  // start is a boundary, so this terminates
-                const int seg = 64 * w + 63 - (int)__clzll((long long)bits);
-                r_seg[e] = seg;
+            for (int e = 0; e < 2; ++e) {
+                r_rerr[e] = false;
+                r_svck[e] = svc_key(cur.flags[e], cur.svc[e], a.S, &r_rerr[e]);
                 const uint32_t f = cur.flags[e];
                 const bool ha = (f & ZK_F_HAS_ANNOTATIONS) != 0;
-                s_sid[j] = cur.sid[e];
-                s_seg[j] = (uint16_t)seg;
-                s_first[j] = ha ? (long long)cur.first[e] : LLONG_MAX;
-                s_last[j] = ha ? (long long)cur.last[e] : LLONG_MIN;
-                s_pid[j] = (f & ZK_F_HAS_PARENT) ? cur.pid[e] : ~0ull;
-                s_svck[j] = r_svck[e];
+                v_first[e] = ha ? cur.first[e] : (uint64_t)LLONG_MAX;
+                v_last[e] = ha ? cur.last[e] : (uint64_t)LLONG_MIN;
+                v_pid[e] = (f & ZK_F_HAS_PARENT) ? cur.pid[e] : ~0ull;
             }
+            *reinterpret_cast<ulonglong2*>(&s_sid[j0]) = make_ulonglong2(cur.sid[0], cur.sid[1]);
+            *reinterpret_cast<ulonglong2*>(&s_first[j0]) = make_ulonglong2(v_first[0], v_first[1]);
+            *reinterpret_cast<ulonglong2*>(&s_last[j0]) = make_ulonglong2(v_last[0], v_last[1]);
+            *reinterpret_cast<ulonglong2*>(&s_pid[j0]) = make_ulonglong2(v_pid[0], v_pid[1]);
+            *reinterpret_cast<uint2*>(&s_svck[j0]) = make_uint2(r_svck[0], r_svck[1]);
+            *reinterpret_cast<uint32_t*>(&s_seg[j0]) = ((uint32_t)r_seg[0] & 0xFFFFu) | ((uint32_t)r_seg[1] << 16);
         }
-        for (int x = tid; x < H; x += WG) s_ht[x] = 0u;
+#pragma unroll
+        for (int x = tid; x < H / 4; x += WG) reinterpret_cast<uint4*>(s_ht)[x] = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
         ZK_STAMP(2);
 
@@ -638,6 +668,10 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
         }
         ZK_STAMP(6);
         }  // ablate != 2
+        if (--fold_in == 0) {
+            fold_stats(st, s_stat);
+            fold_in = kFoldWindows;
+        }
         if (done) break;
         ws = next_ws;
         seek = next_seek;
@@ -651,7 +685,8 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
         if constexpr (EMIT) a.rt_count[blockIdx.x] = nitem;
         atomicAdd(&a.stats[(uint64_t)(blockIdx.x % kStatShards) * ST_N + ST_RECORDS], (unsigned long long)nrec);
     }
-    flush_stats32(st, s_stat, a.stats);  // its barrier also publishes s_hist
+    fold_stats(st, s_stat);
+    publish_stats(s_stat, a.stats);  // its barrier also publishes s_hist
     if constexpr (EMIT) {
         if (tid == 0 && s_stat[ST_RT_DUR_RANGE]) atomicAdd(&a.rt_dropped[1], (unsigned long long)s_stat[ST_RT_DUR_RANGE]);
     }
