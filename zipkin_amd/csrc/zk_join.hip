@@ -192,16 +192,6 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-__device__ __forceinline__ uint64_t spread32(uint32_t x) {
-    uint64_t v = x;
-    v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
-    v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
-    v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
-    v = (v | (v << 2)) & 0x3333333333333333ull;
-    v = (v | (v << 1)) & 0x5555555555555555ull;
-    return v;
-}
-
 // two consecutive elements starting at i (i even, columns 16-byte aligned); zeros past `lim`
 // Two consecutive elements starting at i (i even), RAW: elements at or past `lim` are garbage and
 // every consumer masks by record index. Branch-free and unmasked on purpose: a conditional tail
@@ -306,7 +296,7 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
     __shared__ __align__(16) uint32_t s_svck[TILE];
     __shared__ __align__(16) uint16_t s_seg[TILE];
     __shared__ __align__(16) uint32_t s_ht[H];
-    __shared__ uint64_t s_mask[NWORD];
+    __shared__ __align__(16) uint64_t s_mask[NWORD];
     __shared__ uint32_t s_stat[ST_N];
     __shared__ uint32_t s_wsum[WG / 64];
     __shared__ uint32_t s_hist[kMaxBuckets];  // links per cell bucket (K2's scatter offsets)
@@ -349,11 +339,14 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
             if (lane == 0) prev = (ws + 2 * tid > 0) ? cur.prev : ~cur.tid[0];
             const bool b0 = (2 * tid < wn) && cur.tid[0] != prev;
             const bool b1 = (2 * tid + 1 < wn) && cur.tid[1] != cur.tid[0];
-            const uint64_t m0 = __ballot(b0), m1 = __ballot(b1);
-            if (lane == 0) {
-                s_mask[2 * wave] = spread32((uint32_t)m0) | (spread32((uint32_t)m1) << 1);
-                s_mask[2 * wave + 1] = spread32((uint32_t)(m0 >> 32)) | (spread32((uint32_t)(m1 >> 32)) << 1);
-            }
+            // the wave's 128 records in order: bit q of word 2w+h is record 128w + 64h + q, held by
+            // lane 32h + q/2 as its element q&1 (a shuffle per word instead of bit interleaving)
+            const uint32_t bb = (b0 ? 1u : 0u) | (b1 ? 2u : 0u);
+            const uint32_t v0 = (uint32_t)__shfl((int)bb, lane >> 1);
+            const uint32_t v1 = (uint32_t)__shfl((int)bb, 32 + (lane >> 1));
+            const uint64_t w0 = __ballot((v0 >> (lane & 1)) & 1u);
+            const uint64_t w1 = __ballot((v1 >> (lane & 1)) & 1u);
+            if (lane == 0) *reinterpret_cast<ulonglong2*>(&s_mask[2 * wave]) = make_ulonglong2(w0, w1);
         }
         __syncthreads();
         ZK_STAMP(0);
@@ -522,10 +515,12 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
                 }
             }
         }
-        __syncthreads();
         ZK_STAMP(3);
 
         // ---- 5. reduce(mergeSpan) ------------------------------------------------------------------
+        // No barrier before this: a fragment merges into its leader as soon as it has found it (the
+        // leader's staged values are in place since phase 3; OR-ing bits into a claimed slot leaves
+        // its index field, which is all a concurrent probe reads, unchanged).
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
             const int j = 2 * tid + e;
@@ -676,7 +671,9 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
         ws = next_ws;
         seek = next_seek;
         cur = nxt;
-        __syncthreads();  // s_wsum / s_mask reuse
+        // no loop-end barrier: the next window's phase-1 barrier already separates this window's
+        // last LDS reads (phase 6-7) from its writes (phase 3 on), and phase 1's s_mask writes
+        // from this window's reads (phases 2-3, before the barrier that ends phase 3)
         ZK_STAMP(7);
     }
     ZK_STAMP_FLUSH();
