@@ -3,10 +3,10 @@
 # Prints ms/step and K1 avg launch ms per variant, two rounds interleaved.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for r in 1 2; do
+for r in 1 2 3; do
   for v in "$@"; do
     if [ "$v" = cur ]; then L=$PWD/zipkin_amd/libzkagg.so; else L=$PWD/zipkin_amd/libzkagg_$v.so; fi
-    ZKAGG_LIB=$L timeout -k 10 120 python bench.py --cpu-sample 0 ${BENCH_ARGS:-} > gpurun_out/ab_$v.log 2>&1 || { echo "$v failed"; tail -5 gpurun_out/ab_$v.log; exit 1; }
+    ZKAGG_LIB=$L timeout -k 10 120 python bench.py --cpu-sample 0 --steps 40 ${BENCH_ARGS:-} > gpurun_out/ab_$v.log 2>&1 || { echo "$v failed"; tail -5 gpurun_out/ab_$v.log; exit 1; }
     python - "$v" <<'PY'
 import json, sys
 v = sys.argv[1]

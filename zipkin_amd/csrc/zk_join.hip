@@ -22,6 +22,9 @@
 #ifndef ZK_HASH_FACTOR
 #define ZK_HASH_FACTOR 8
 #endif
+#ifndef ZK_K1_WGS_PER_CU
+#define ZK_K1_WGS_PER_CU 4  // resident K1 workgroups per CU (one wave per SIMD each)
+#endif
 
 namespace zk {
 namespace {
@@ -185,13 +188,6 @@ __device__ __forceinline__ uint32_t frag_bits(uint32_t f, uint32_t* once) {
 }
 __device__ __forceinline__ bool slot_valid(uint32_t w) { return ((w >> kSlotB) & 0xFu) == 0u; }
 
-// a wave-uniform lane's 64-bit value into scalar registers
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
-    return ((uint64_t)hi << 32) | lo;
-}
-
 // two consecutive elements starting at i (i even, columns 16-byte aligned); zeros past `lim`
 // Two consecutive elements starting at i (i even), RAW: elements at or past `lim` are garbage and
 // every consumer masks by record index. Branch-free and unmasked on purpose: a conditional tail
@@ -240,6 +236,35 @@ __device__ __forceinline__ void publish_stats(const uint32_t* s_stat, unsigned l
     }
 }
 
+// ---- window boundary masks ---------------------------------------------------------------------
+// A wave's 128 records (thread t holds records 2t, 2t+1) are described by two ballots: ev (bit t:
+// record 2t starts a trace) and od (bit t: record 2t+1 does). Positions below are local (0..127).
+__device__ __forceinline__ int first_ge(uint64_t ev, uint64_t od, int q) {  // first boundary >= q
+    if (q < 0) q = 0;
+    if (q >= 128) return -1;
+    const int se = (q + 1) >> 1, so = q >> 1;  // 2t >= q <=> t >= se;  2t+1 >= q <=> t >= so
+    const uint64_t me = se >= 64 ? 0ull : (ev & (~0ull << se));
+    const uint64_t mo = od & (~0ull << so);
+    const int pe = me ? 2 * (__ffsll((unsigned long long)me) - 1) : 256;
+    const int po = mo ? 2 * (__ffsll((unsigned long long)mo) - 1) + 1 : 256;
+    const int p = pe < po ? pe : po;
+    return p < 256 ? p : -1;
+}
+__device__ __forceinline__ int last_of(uint64_t ev, uint64_t od) {  // last boundary, or -1
+    const int pe = ev ? 2 * (63 - (int)__clzll((long long)ev)) : -1;
+    const int po = od ? 2 * (63 - (int)__clzll((long long)od)) + 1 : -1;
+    return pe > po ? pe : po;
+}
+// lane l-1's value (wave_shr:1 DPP, no LDS round trip); lane 0 gets garbage
+__device__ __forceinline__ uint64_t lane_shr1(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x138, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x138, 0xF, 0xF, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {  // set bits of m in lanes < this lane
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 struct Window {  // two consecutive records per thread
     uint64_t tid[2], sid[2], pid[2], first[2], last[2];
     uint32_t svc[2], flags[2];
@@ -285,7 +310,7 @@ __device__ __forceinline__ void load_window(const JoinArgs& a, uint64_t ws, Wind
 constexpr int kModeJoin = 1;
 constexpr int kModeEmit = 2;
 template <int TILE, int WG, int ABL, int MODE>
-__global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
+__global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU) void k_span_join_stream(JoinArgs a) {
     constexpr int H = ZK_HASH_FACTOR * TILE;  // load <= 1/16 (distinct spans / slots): short probe chains, since a wave waits for its longest
     constexpr int NWORD = TILE / 64;
     static_assert(TILE == 2 * WG && TILE <= 2047, "two records per thread");
@@ -330,58 +355,59 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
     Window cur, nxt;
     constexpr bool JOIN = (MODE & kModeJoin) != 0, EMIT = (MODE & kModeEmit) != 0;
     load_window<JOIN>(a, ws, cur);
+#pragma unroll
+    for (int x = tid; x < H / 4; x += WG) reinterpret_cast<uint4*>(s_ht)[x] = make_uint4(0u, 0u, 0u, 0u);
     ZK_STAMP_DECL
     for (;;) {
         const int wn = (int)((n - ws) < (uint64_t)TILE ? (n - ws) : (uint64_t)TILE);
         // ---- 1. trace boundaries of the window -------------------------------------------------
+        uint64_t m_ev, m_od;  // this wave's boundary ballots (uniform; phase 3 reuses them)
         {
-            uint64_t prev = __shfl_up(cur.tid[1], 1);
+            uint64_t prev = lane_shr1(cur.tid[1]);
             if (lane == 0) prev = (ws + 2 * tid > 0) ? cur.prev : ~cur.tid[0];
             const bool b0 = (2 * tid < wn) && cur.tid[0] != prev;
             const bool b1 = (2 * tid + 1 < wn) && cur.tid[1] != cur.tid[0];
-            // the wave's 128 records in order: bit q of word 2w+h is record 128w + 64h + q, held by
-            // lane 32h + q/2 as its element q&1 (a shuffle per word instead of bit interleaving)
-            const uint32_t bb = (b0 ? 1u : 0u) | (b1 ? 2u : 0u);
-            const uint32_t v0 = (uint32_t)__shfl((int)bb, lane >> 1);
-            const uint32_t v1 = (uint32_t)__shfl((int)bb, 32 + (lane >> 1));
-            const uint64_t w0 = __ballot((v0 >> (lane & 1)) & 1u);
-            const uint64_t w1 = __ballot((v1 >> (lane & 1)) & 1u);
-            if (lane == 0) *reinterpret_cast<ulonglong2*>(&s_mask[2 * wave]) = make_ulonglong2(w0, w1);
+            m_ev = __ballot(b0);
+            m_od = __ballot(b1);
+            if (lane == 0) *reinterpret_cast<ulonglong2*>(&s_mask[2 * wave]) = make_ulonglong2(m_ev, m_od);
         }
         __syncthreads();
         ZK_STAMP(0);
         // ---- 2. which records are ours, where the next window starts (uniform) ----------------
         const int lo_j = (int)(seek - ws);
         const int r1_j = (R1 - ws < (uint64_t)wn) ? (int)(R1 - ws) : wn;
-        // wave-parallel over the NWORD mask words (lane w holds word w): the first boundary >= lo_j
-        // (start), the first >= r1_j (stop) and the last boundary of the window (last_b)
-        int start = -1, stop = -1, last_b = -1;  // wave-uniform (SGPRs)
-        int lastb;                                // per lane w < NWORD
+        // lane w < NW holds wave w's masks: the first boundary >= lo_j (start), the first >= r1_j
+        // (stop), the last of the window (last_b) and the last before this wave's records (prev_b)
+        int start = -1, stop = -1, last_b = -1, prev_b = -1;  // wave-uniform (SGPRs)
         {
-            static_assert(NWORD <= 64, "one mask word per lane");
-            const int base = 64 * lane;
-            const uint64_t x = lane < NWORD ? s_mask[lane] : 0ull;
-            const uint64_t ys = lo_j >= base + 64 ? 0ull : (lo_j > base ? (x & (~0ull << (lo_j - base))) : x);
-            const uint64_t yt = r1_j >= base + 64 ? 0ull : (r1_j > base ? (x & (~0ull << (r1_j - base))) : x);
-            // lastb: the last boundary in words 0..lane (max-scan); phase 3 reads it by shuffle
-            lastb = x ? base + 63 - (int)__clzll((long long)x) : -1;
-#pragma unroll
-            for (int off = 1; off < NWORD; off <<= 1) {
-                const int o = __shfl_up(lastb, off);
-                if (lane >= off) lastb = o > lastb ? o : lastb;
+            constexpr int NW = WG / 64;
+            uint64_t ev = 0ull, od = 0ull;
+            if (lane < NW) {
+                const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(&s_mask[2 * lane]);
+                ev = x.x;
+                od = x.y;
             }
-            const uint64_t bs = __ballot(ys != 0ull), bt = __ballot(yt != 0ull), bl = __ballot(x != 0ull);
+            const int base = 128 * lane;
+            const int fs = lane < NW ? first_ge(ev, od, lo_j - base) : -1;
+            const int ft = lane < NW ? first_ge(ev, od, r1_j - base) : -1;
+            const int lb = last_of(ev, od);
+            const uint64_t bs = __ballot(fs >= 0), bt = __ballot(ft >= 0), bl = __ballot(lb >= 0);
             if (bs) {
                 const int w = __ffsll((unsigned long long)bs) - 1;
-                start = 64 * w + __ffsll((unsigned long long)readlane64(ys, w)) - 1;
+                start = 128 * w + __builtin_amdgcn_readlane(fs, w);
             }
             if (bt) {
                 const int w = __ffsll((unsigned long long)bt) - 1;
-                stop = 64 * w + __ffsll((unsigned long long)readlane64(yt, w)) - 1;
+                stop = 128 * w + __builtin_amdgcn_readlane(ft, w);
             }
             if (bl) {
                 const int w = 63 - (int)__clzll((long long)bl);
-                last_b = 64 * w + 63 - (int)__clzll((long long)readlane64(x, w));
+                last_b = 128 * w + __builtin_amdgcn_readlane(lb, w);
+            }
+            const uint64_t bp = bl & ((1ull << wave) - 1ull);
+            if (bp) {
+                const int w = 63 - (int)__clzll((long long)bp);
+                prev_b = 128 * w + __builtin_amdgcn_readlane(lb, w);
             }
         }
         const bool at_end = ws + (uint64_t)wn >= n;
@@ -426,23 +452,20 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
         if constexpr (ABL != 2) {  // diagnostic build: 2 = stream windows only
 
         // ---- 3. segment ids and LDS staging ----------------------------------------------------
-        // seg = index of the trace's first record in the window (the last boundary <= j). One mask
-        // read per thread: record 2t+1 is its own segment start or shares 2t's. Staging stores are
-        // unconditional 16-B pairs (entries outside [start, m) are never read).
+        // seg = index of the trace's first record in the window (the last boundary <= j), from the
+        // wave's own ballots: record 2t+1 is its own segment start or shares 2t's. Staging stores
+        // are unconditional 16-B pairs (entries outside [start, m) are never read).
         int r_seg[2];
         uint32_t r_svck[2];
         bool r_rerr[2];
         {
             const int j0 = 2 * tid;
-            const int w = j0 >> 6;
-            uint64_t bits = s_mask[w];
-            const bool b1 = (bits >> ((j0 + 1) & 63)) & 1ull;
-            bits &= (2ull << (j0 & 63)) - 1ull;
-            // no boundary in this word up to j0: the last one of the earlier words (it exists when
-            // j0 >= start, since start is a boundary)
-            const int prevw = __shfl(lastb, w > 0 ? w - 1 : 0);
+            // last boundary <= j0 among this wave's records, else the one before the wave (it exists
+            // when j0 >= start, since start is a boundary)
+            const int p = last_of(m_ev & ((2ull << lane) - 1ull), m_od & ((1ull << lane) - 1ull));
+            const bool b1 = (m_od >> lane) & 1ull;
             int seg0 = -1;
-            if (j0 >= start && j0 < m) seg0 = bits ? 64 * w + 63 - (int)__clzll((long long)bits) : prevw;
+            if (j0 >= start && j0 < m) seg0 = p >= 0 ? 128 * wave + p : prev_b;
             r_seg[0] = seg0;
             r_seg[1] = (j0 + 1 >= start && j0 + 1 < m) ? (b1 ? j0 + 1 : seg0) : -1;
             uint64_t v_first[2], v_last[2], v_pid[2];
@@ -463,9 +486,7 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
             *reinterpret_cast<uint2*>(&s_svck[j0]) = make_uint2(r_svck[0], r_svck[1]);
             *reinterpret_cast<uint32_t*>(&s_seg[j0]) = ((uint32_t)r_seg[0] & 0xFFFFu) | ((uint32_t)r_seg[1] << 16);
         }
-#pragma unroll
-        for (int x = tid; x < H / 4; x += WG) reinterpret_cast<uint4*>(s_ht)[x] = make_uint4(0u, 0u, 0u, 0u);
-        __syncthreads();
+        __syncthreads();  // (the hash table is empty here: cleared once, then by its leaders)
         ZK_STAMP(2);
 
         // ---- 4. groupBy((id, traceId)): the first fragment to claim a slot leads --------------
@@ -619,15 +640,13 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
         }
         ZK_STAMP(5);
         // ---- 7. append the window's links (and sketch items) to this workgroup's lists ----------
-        // one scan for both counts: links in bits 0..15, items in 16..31 (a window has <= 512)
-        const uint32_t cnt_pack = nl | (ni << 16);
-        uint32_t incl = cnt_pack;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t o = __shfl_up(incl, off);
-            if (lane >= off) incl += o;
-        }
-        if (lane == 63) s_wsum[wave] = incl;
+        // one exclusive scan for both counts: links in bits 0..15, items in 16..31 (<= 512 each)
+        // per-wave counts and lane offsets from ballots (nl, ni are 0..2: two bits each)
+        const uint64_t l1 = __ballot(nl >= 1u), l2 = __ballot(nl >= 2u);
+        const uint64_t i1 = EMIT ? __ballot(ni >= 1u) : 0ull, i2 = EMIT ? __ballot(ni >= 2u) : 0ull;
+        const uint32_t below = (lanes_below(l1) + lanes_below(l2)) | ((lanes_below(i1) + lanes_below(i2)) << 16);
+        if (lane == 0)
+            s_wsum[wave] = (uint32_t)(__popcll(l1) + __popcll(l2)) | ((uint32_t)(__popcll(i1) + __popcll(i2)) << 16);
         __syncthreads();
         uint32_t base = 0, total = 0;
 #pragma unroll
@@ -636,7 +655,7 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
             if (w2 < wave) base += v;
             total += v;
         }
-        const uint32_t excl = base + incl - cnt_pack;
+        const uint32_t excl = base + below;
         if constexpr (ABL == 0 && JOIN) {
             // exactly two stores per thread on every path (absent links go to the list's trash
             // slot), so the loop-end wait for the prefetched window can count them: vmcnt(2)
@@ -661,6 +680,11 @@ __global__ __launch_bounds__(WG, 4) void k_span_join_stream(JoinArgs a) {
             }
             nitem += total >> 16;
         }
+        // every leader empties its own slot (phase 7's barrier is past all probes of this window;
+        // the next window inserts only after its phase-1 and phase-3 barriers)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+            if (r_leader[e] == 2 * tid + e) s_ht[r_slot[e]] = 0u;
         ZK_STAMP(6);
         }  // ablate != 2
         if (--fold_in == 0) {
@@ -984,7 +1008,7 @@ extern "C" int zk_debug_stamps(unsigned long long* out, int reset) {
 
 void join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, uint64_t* link_stride) {
     const uint64_t windows = (n + kTile - 1) / kTile;
-    uint64_t g = (uint64_t)cus * 4;  // four resident workgroups per CU (<= 128 VGPRs, 23 KB LDS)
+    uint64_t g = (uint64_t)cus * ZK_K1_WGS_PER_CU;  // all resident at once (<= 128 VGPRs, <= 40 KB LDS)
     if (g > windows) g = windows ? windows : 1;
     const uint64_t per = ((n + g - 1) / g + kTile - 1) / kTile * kTile;
     *grid = (uint32_t)g;
