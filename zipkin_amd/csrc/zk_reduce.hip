@@ -254,6 +254,25 @@ struct RunSums {
         s4[1] = (uint64_t)a1;
         s4[2] += w2 + (uint64_t)(a1 >> 64);
     }
+    // d < 2^32 (durations under 71 minutes, i.e. nearly all): d^2 fits 64 bits, so d^3 and d^4
+    // are 64x32 and 64x64 products (5 32-bit multiplies instead of ~18)
+    __device__ __forceinline__ void add_small(uint32_t d) {
+        const uint64_t d2 = (uint64_t)d * d;
+        const unsigned __int128 d3 = (unsigned __int128)d2 * d;   // < 2^96
+        const unsigned __int128 d4 = (unsigned __int128)d2 * d2;  // < 2^128
+        ++n;
+        s1 += d;
+        s2 += d2;
+        const unsigned __int128 t3 = s3 + d3;
+        s3h += (t3 < s3);
+        s3 = t3;
+        const uint64_t w0 = (uint64_t)d4, w1 = (uint64_t)(d4 >> 64);
+        const unsigned __int128 a0 = (unsigned __int128)s4[0] + w0;
+        const unsigned __int128 a1 = (unsigned __int128)s4[1] + w1 + (uint64_t)(a0 >> 64);
+        s4[0] = (uint64_t)a0;
+        s4[1] = (uint64_t)a1;
+        s4[2] += (uint64_t)(a1 >> 64);
+    }
     // add the run as 32-bit chunks to 15 register limbs (same layout as flush)
     __device__ __forceinline__ void to_limbs(uint64_t* l) const {
         constexpr uint64_t M = 0xFFFFFFFFull;
@@ -362,7 +381,13 @@ __global__ __launch_bounds__(1 << CB_SHIFT) void k_bucket_reduce(ReduceArgs r, u
         __syncthreads();
         RunSums run;
         run.clear();
-        for (uint32_t q = 0; q < h; ++q) run.add(s_d[ex + q]);
+        for (uint32_t q = 0; q < h; ++q) {
+            const uint64_t d = s_d[ex + q];
+            if (d >> 32)
+                run.add(d);
+            else
+                run.add_small((uint32_t)d);
+        }
         run.to_limbs(lim);
         s_hist[tid] = 0u;
         __syncthreads();
