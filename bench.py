@@ -191,7 +191,9 @@ def main():
                 "event_ms_per_step": ev_ms / a.steps,
                 "finalize_ms_last": tm1["finalize_ms"],
                 "spill_ms_last": tm1["spill_ms"],
-                "links": int(st["joined_links"]) // max(1, a.steps + a.warmup),
+                "joined_links_per_step": int(st["joined_links"]),  # stats cover the last step (reset per step)
+                "merged_spans_per_step": int(st["merged_spans"]),
+                "merged_spans_per_s": int(st["merged_spans"]) * world * a.steps / elapsed,
             },
         }
         print(json.dumps(line), flush=True)

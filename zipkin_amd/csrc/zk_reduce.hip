@@ -426,7 +426,7 @@ hipError_t launch_partitioned_reduce(const ReduceArgs& r, hipStream_t s) {
     if (!r.nb || !r.lists) return hipSuccess;
     hipLaunchKernelGGL(k_bucket_colscan, dim3(r.nb), dim3(1024), 0, s, r.hist, r.lists, r.col_off, r.bucket_base);
     hipLaunchKernelGGL(k_bucket_base, dim3(1), dim3(1024), 0, s, r.bucket_base, r.nb);
-    hipLaunchKernelGGL((k_link_scatter<8, 256>), dim3(r.lists), dim3(256), (size_t)r.nb * kScatterLine * 8, s, r);
+    hipLaunchKernelGGL((k_link_scatter<8, 512>), dim3(r.lists), dim3(512), (size_t)r.nb * kScatterLine * 8, s, r);
     const uint32_t splits = r.nb >= 256 ? 1u : (512u + r.nb - 1) / r.nb;
     // CB = 512: 512 threads, 4096-link chunks (36 KB LDS); CB = 1024: 1024 threads, 4096-link chunks
     if (r.cb_shift == 9)
