@@ -305,3 +305,62 @@ def test_stored_bytes_to_dependencies(gpu, seed, anomalies):
     gl = {(names[p], names[c]): tuple(m) for p, c, m in got.links()}
     want = {k: tuple(m) for k, m in ref.exact().items()}
     assert gl == want
+
+
+@pytest.mark.gpu
+def test_stored_span_job_end_to_end(gpu):
+    """Stored bytes -> decoder -> device job + top-annotation sketches -> Aggregates store, against
+    the span oracle (dependencies) and the count-min restatement fed the indexer items (tops)."""
+    from oracle.kv import KvOracle
+    from zipkin_amd.aggregates import GpuAggregates, StoredSpanJob
+
+    spans = gen_traces(61, 400, max_depth=5, anomalies=0.3)
+    by_trace: dict = {}
+    for sp in spans:
+        by_trace.setdefault(sp.trace_id, []).append(sp)
+    traces = list(by_trace.values())
+    batches = [encode_all([sp for t in traces[i:i + 90] for sp in t]) for i in range(0, len(traces), 90)]
+    store = GpuAggregates("anorm")
+    job = StoredSpanJob(strict=False, aggregates=store, top_k=5, clock=lambda: 10**15)
+    deps = job.run(batches)
+    ref = aggregate_job(spans, strict=False)
+    got = {(l.parent.name, l.child.name): tuple(l.duration_moments) for l in deps.links}
+    assert got == {k: tuple(m) for k, m in ref.exact().items()}
+    assert job.stats["records"] == len(spans) and job.rejected == 0
+    stored = store.getDependencies(0, 10**15)
+    assert {(l.parent.name, l.child.name) for l in stored.links} == set(got)
+
+    names = job.services
+    S = len(names)
+    strings = {}
+    kvo, ano = KvOracle(S), KvOracle(S)
+    kv_s, kv_k, an_s, an_v = [], [], [], []
+    for sp in spans:  # the indexer items, in decode order (ids from the job's dictionary)
+        if not sp.annotations:
+            continue
+        for b in sp.binary_annotations:
+            if b.host is not None:
+                kv_s.append(names.get(b.host.service_name))
+                kv_k.append(hash_string(b.key))
+                strings[kv_k[-1]] = b.key
+        seen = {}
+        for a in sp.annotations:
+            if a.value in CORE_ANNOTATIONS:
+                continue
+            m = seen.get(a.value)
+            if m is None or (((m.timestamp - a.timestamp) & 0xFFFFFFFF) ^ 0x80000000) - 0x80000000 > 0:
+                seen[a.value] = a
+        for a in seen.values():
+            if a.host is not None:
+                an_s.append(names.get(a.host.service_name))
+                an_v.append(hash_string(a.value))
+                strings[an_v[-1]] = a.value
+    kvo.accumulate(np.array(kv_s, np.uint32), np.array(kv_k, np.uint64))
+    ano.accumulate(np.array(an_s, np.uint32), np.array(an_v, np.uint64))
+    for o, tops, getter in ((kvo, job.top_kv, store.getTopKeyValueAnnotations),
+                            (ano, job.top_annotations, store.getTopAnnotations)):
+        keys, _, cnt = o.topk_all(5)
+        want = {names.name(s): [strings[int(h)] for h in keys[s][: cnt[s]]] for s in range(S) if cnt[s]}
+        assert tops == want
+        for svc, lst in want.items():
+            assert getter(svc) == lst

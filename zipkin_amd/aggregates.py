@@ -378,3 +378,82 @@ def publish_top_kv(sketch, aggregates: GpuAggregates, keys: Dict[int, str], k: i
             continue
         names = [keys[int(h)] for h in kk[s][: cnt[s]]]
         aggregates.storeTopKeyValueAnnotations(aggregates.services.name(s), names)
+
+
+class StoredSpanJob:
+    """The aggregation job fed from the stored span bytes, with the removed producers of the
+    top-annotation lists (CHANGELOG:7-8) restored next to it.
+
+    Input: trace-clustered batches of stored fragments (the Cassandra column values, i.e.
+    Snappy(TBinaryProtocol(Span)), CassieSpanStore.scala:52). Per batch the host decoder
+    (include/zkingest.h) writes the 48-B records plus the span indexer's items
+    (CassieSpanStore.scala:214-242); the device then runs the dependency job
+    (ZipkinAggregateJob.scala:20-43) and one count-min + top-K sketch each for binary-annotation
+    keys and non-core annotation values. Output, through `aggregates`: storeDependencies,
+    storeTopKeyValueAnnotations and storeTopAnnotations per service (Aggregates.scala:31-36).
+    """
+
+    def __init__(self, *, device: int = 0, strict: bool = True, aggregates: Optional[Aggregates] = None,
+                 clock=now_us, top_k: int = 10, snappy: bool = True, kv_width: int = 0, seed: int = 0):
+        self.device = device
+        self.strict = strict
+        self.aggregates = aggregates
+        self.clock = clock
+        self.top_k = top_k
+        self.snappy = snappy
+        self.kv_width = kv_width
+        self.seed = seed
+        self.stats: dict = {}
+        self.rejected = 0
+        self.services: Optional[Dictionary] = None
+        self.top_kv: Dict[str, List[str]] = {}
+        self.top_annotations: Dict[str, List[str]] = {}
+
+    def _decode(self, dec, blobs):
+        cap = max(16, 8 * len(blobs))
+        while True:
+            try:
+                return dec.decode(blobs, snappy=self.snappy, strict=self.strict, items=True, item_cap=cap)
+            except _abi.ZkError as e:
+                if e.status != _abi.ZK_ERR_CAPACITY:
+                    raise
+                cap *= 4  # more binary annotations than guessed: decode the batch again
+
+    def _tops(self, dec, sketch) -> Dict[str, List[str]]:
+        keys, _, cnt = sketch.topk_all(self.top_k)
+        return {dec.service_name(s_): [dec.string(int(h)) for h in keys[s_][: cnt[s_]]]
+                for s_ in range(sketch.num_services) if cnt[s_]}
+
+    def run(self, batches) -> Optional[Dependencies]:
+        from .ingest import SpanDecoder
+        from .kv import KvSketch
+
+        dec = SpanDecoder()
+        decoded = []
+        self.rejected = 0
+        for blobs in batches:
+            cols, rej, kv, ann = self._decode(dec, blobs)
+            self.rejected += rej
+            decoded.append((cols, kv, ann))
+        self.services = Dictionary(dec.service_names())
+        S = max(1, len(self.services))
+        job = ZipkinAggregateJob(self.services, device=self.device, strict=self.strict, clock=self.clock)
+        deps = job.run([c for c, _, _ in decoded], num_services=S)
+        self.stats = job.stats
+        with KvSketch(S, device=self.device, width=self.kv_width, seed=self.seed) as kvs, \
+                KvSketch(S, device=self.device, width=self.kv_width, seed=self.seed) as anns:
+            for _, (ks, kh), (as_, ah) in decoded:
+                if len(ks):
+                    kvs.accumulate(ks, kh)
+                if len(as_):
+                    anns.accumulate(as_, ah)
+            self.top_kv = self._tops(dec, kvs)
+            self.top_annotations = self._tops(dec, anns)
+        if self.aggregates is not None:
+            if deps is not None:
+                self.aggregates.storeDependencies(deps)
+            for name, keys in self.top_kv.items():
+                self.aggregates.storeTopKeyValueAnnotations(name, keys)
+            for name, values in self.top_annotations.items():
+                self.aggregates.storeTopAnnotations(name, values)
+        return deps
