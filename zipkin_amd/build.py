@@ -23,7 +23,7 @@ SOURCES = [
     "zk_rt_api.cpp",
     "zk_ingest.cpp",
 ]
-HEADERS = ["zk_internal.h", "zk_tracegen.h", "zk_sketch_internal.h", "zk_rt_internal.h"]
+HEADERS = ["zk_internal.h", "zk_tracegen.h", "zk_sketch_internal.h", "zk_rt_internal.h", "zk_block.h"]
 PUBLIC_HEADERS = ["zkagg.h", "zksketch.h", "zkstore.h", "zkingest.h"]
 LIB = PKG / "libzkagg.so"
 ARCH = os.environ.get("ZK_OFFLOAD_ARCH", "gfx950")

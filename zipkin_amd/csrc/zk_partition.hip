@@ -9,6 +9,7 @@
 // final estimate).
 #include <hipcub/hipcub.hpp>
 
+#include "zk_block.h"
 #include "zk_sketch_internal.h"
 
 namespace zk {
@@ -83,6 +84,132 @@ __global__ __launch_bounds__(kPartWG) void k_part_scatter(const uint32_t* __rest
 #pragma unroll
         for (int e = 0; e < kPartU; ++e)
             if (v[e] < S) out[atomicAdd(&cur[v[e]], 1u)] = p[e];
+    }
+}
+
+// The same scatter with whole output lines (S <= kLineMaxS): chunks of C items are counting-sorted
+// by service in LDS and written in runs; each service's tail that does not yet fill a 64-byte line
+// stays in an LDS carry until a later chunk completes it (the item-by-item version above writes
+// 8-byte pieces of 500 interleaved streams, ~8x write amplification). Same pattern as K2
+// (zk_reduce.hip k_link_scatter), with the service taken from its own column.
+constexpr uint32_t kLineMaxS = 1024;
+constexpr int kLineItems = 8;  // items per 64-byte line
+template <int U, int WG>
+__global__ __launch_bounds__(WG) void k_part_scatter_lines(const uint32_t* __restrict__ svc,
+                                                            const uint64_t* __restrict__ payload, uint64_t n,
+                                                            uint64_t per, const uint32_t* __restrict__ counts,
+                                                            uint32_t S, uint32_t grid,
+                                                            const uint32_t* __restrict__ offs,
+                                                            uint64_t* __restrict__ out) {
+    constexpr int C = WG * U;
+    constexpr int BPT = (kLineMaxS + WG - 1) / WG;  // services per thread in the scan
+    __shared__ uint32_t s_cur[kLineMaxS];  // output position of each service's first pending item
+    __shared__ uint32_t s_hist[kLineMaxS];  // items of the chunk per service
+    __shared__ uint32_t s_off[kLineMaxS];   // exclusive offsets in the sorted chunk
+    __shared__ uint32_t s_cc[kLineMaxS];    // carried items per service (< kLineItems)
+    __shared__ uint64_t s_sorted[C];
+    __shared__ uint16_t s_svc[C];
+    __shared__ uint32_t s_tmp[32];
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_carry[];  // [S][kLineItems]
+    const int tid = threadIdx.x;
+    for (uint32_t b = tid; b < S; b += WG) {
+        s_cur[b] = offs[(uint64_t)b * grid + blockIdx.x];
+        s_hist[b] = 0u;
+        s_cc[b] = 0u;
+    }
+    uint64_t lo, hi;
+    part_range(n, per, counts, &lo, &hi);
+    const uint64_t lo0 = hi > lo ? lo : 0;  // an in-range index for the unconditional loads
+    uint64_t nv[U];
+    uint32_t ns[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        const uint64_t i = lo + tid + (uint64_t)WG * k;
+        ns[k] = i < hi ? svc[i] : 0xFFFFFFFFu;
+        nv[k] = payload[i < hi ? i : lo0];
+    }
+    __syncthreads();
+    for (uint64_t base = lo; base < hi; base += C) {
+        const bool last = base + C >= hi;
+        uint64_t v[U];
+        uint32_t bk[U], rank[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            v[k] = nv[k];
+            bk[k] = ns[k];
+            const uint64_t i = base + C + tid + (uint64_t)WG * k;  // next chunk in flight
+            ns[k] = i < hi ? svc[i] : 0xFFFFFFFFu;
+            nv[k] = payload[i < hi ? i : lo0];
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) rank[k] = bk[k] < S ? atomicAdd(&s_hist[bk[k]], 1u) : 0u;
+        __syncthreads();
+        {
+            uint32_t h[BPT], sum = 0;
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) {
+                const uint32_t bin = tid * BPT + q;
+                h[q] = bin < S ? s_hist[bin] : 0u;
+                sum += h[q];
+            }
+            uint32_t tot;
+            uint32_t ex = block_excl_scan<WG / 64>(sum, s_tmp, &tot);
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) {
+                const uint32_t bin = tid * BPT + q;
+                if (bin < S) s_off[bin] = ex;
+                ex += h[q];
+            }
+            if (tid == 0) s_tmp[31] = tot;  // valid items of the chunk
+        }
+        __syncthreads();
+        const uint32_t cnt = s_tmp[31];
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+            if (bk[k] < S) {
+                const uint32_t p = s_off[bk[k]] + rank[k];
+                s_sorted[p] = v[k];
+                s_svc[p] = (uint16_t)bk[k];
+            }
+        // carried items: write those whose line the chunk completes, shift the rest down
+        for (uint32_t b = tid; b < S; b += WG) {
+            const uint32_t cc = s_cc[b], pos = s_cur[b];
+            const uint32_t end = pos + cc + s_hist[b];
+            const uint32_t lim = last ? end : max(pos, end & ~(uint32_t)(kLineItems - 1));
+            uint64_t* cb = s_carry + (uint64_t)b * kLineItems;
+            for (uint32_t k = 0; k < cc; ++k) {
+                const uint32_t dest = pos + k;
+                if (dest < lim)
+                    out[dest] = cb[k];
+                else
+                    cb[dest - lim] = cb[k];  // dest - lim <= k: ascending order is safe
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < cnt; i += WG) {
+            const uint64_t x = s_sorted[i];
+            const uint32_t b = s_svc[i];
+            const uint32_t pos = s_cur[b], cc = s_cc[b];
+            const uint32_t end = pos + cc + s_hist[b];
+            const uint32_t lim = last ? end : max(pos, end & ~(uint32_t)(kLineItems - 1));
+            const uint32_t dest = pos + cc + (i - s_off[b]);
+            if (dest < lim)
+                out[dest] = x;
+            else
+                s_carry[(uint64_t)b * kLineItems + (dest - lim)] = x;
+        }
+        __syncthreads();
+        for (uint32_t b = tid; b < S; b += WG) {
+            const uint32_t pos = s_cur[b];
+            const uint32_t end = pos + s_cc[b] + s_hist[b];
+            // never below the service's own first pending position: the line's head may belong to
+            // the previous workgroup's range of this service
+            const uint32_t lim = last ? end : max(pos, end & ~(uint32_t)(kLineItems - 1));
+            s_cur[b] = lim;
+            s_cc[b] = end - lim;
+            s_hist[b] = 0u;
+        }
+        __syncthreads();
     }
 }
 
@@ -172,8 +299,12 @@ hipError_t partition_impl(const PartitionPlan& p, const uint32_t* svc, const uin
     if (e != hipSuccess) return e;
     e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, hist, offs, (int)m, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_part_scatter, dim3(p.grid), dim3(kPartWG), lds, s, svc, payload, n, p.per_wg, counts, p.S,
-                       p.grid, offs, out);
+    if (p.S <= kLineMaxS)
+        hipLaunchKernelGGL((k_part_scatter_lines<4, 512>), dim3(p.grid), dim3(512), (size_t)p.S * kLineItems * 8, s,
+                           svc, payload, n, p.per_wg, counts, p.S, p.grid, offs, out);
+    else
+        hipLaunchKernelGGL(k_part_scatter, dim3(p.grid), dim3(kPartWG), lds, s, svc, payload, n, p.per_wg, counts,
+                           p.S, p.grid, offs, out);
     hipLaunchKernelGGL(k_part_seg, dim3((p.S + 256) / 256), dim3(256), 0, s, offs, hist, p.S, p.grid, seg);
     return hipGetLastError();
 }

@@ -6,6 +6,7 @@
 // of a lane group own one link and add the 15 limbs of one 128-byte cell, so a wave instruction
 // issues four contiguous 128-B cell updates instead of 64 scattered 8-B ones (measured 5.7x faster,
 // profiles/r01_atomics_microbench.txt).
+#include "zk_block.h"
 #include "zk_internal.h"
 
 namespace zk {
@@ -54,31 +55,6 @@ __global__ __launch_bounds__(256) void k_link_reduce_atomic(const uint64_t* __re
 // x 15 limbs fits one CU) and adds it to the table with plain loads/stores: every cell has exactly
 // one owner, so no global atomic is issued (when a bucket is split over several workgroups for
 // parallelism, the few flush adds are atomic).
-
-template <int NW>  // waves per block (blockDim.x == 64 * NW, NW <= 16)
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_tmp, uint32_t* total) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t incl = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t o = __shfl_up(incl, off);
-        if (lane >= off) incl += o;
-    }
-    if (lane == 63) s_tmp[wave] = incl;
-    __syncthreads();
-    if (wave == 0) {
-        uint32_t w = lane < NW ? s_tmp[lane] : 0u;
-#pragma unroll
-        for (int off = 1; off < NW; off <<= 1) {
-            const uint32_t o = __shfl_up(w, off);
-            if (lane >= off) w += o;
-        }
-        if (lane < NW) s_tmp[16 + lane] = w;  // inclusive wave totals
-    }
-    __syncthreads();
-    *total = s_tmp[16 + NW - 1];
-    return (wave ? s_tmp[16 + wave - 1] : 0u) + incl - v;
-}
 
 __global__ __launch_bounds__(1024) void k_bucket_colscan(const uint32_t* __restrict__ hist, uint32_t lists,
                                                          uint32_t* __restrict__ col_off, uint64_t* __restrict__ totals) {
