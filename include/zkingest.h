@@ -39,6 +39,7 @@
 #include <stdint.h>
 
 #include "zkagg.h"
+#include "zkstore.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -81,6 +82,24 @@ zk_status zk_ingest_service_id(zk_ingest* ing, const char* name, uint64_t len, u
 zk_status zk_ingest_service_name(const zk_ingest* ing, uint32_t id, char* buf, uint64_t cap, uint64_t* len);
 /* the string behind a key / value hash seen by this decoder (two-phase: buf NULL -> *len) */
 zk_status zk_ingest_string(const zk_ingest* ing, uint64_t hash, char* buf, uint64_t cap, uint64_t* len);
+
+/* ---- the Dependencies record on the wire ----------------------------------------------------
+ * TBinaryProtocol thriftscala.Dependencies (zipkinDependencies.thrift:24-43) as the Cassandra
+ * store writes it: WrappedDependencies.toThrift (zipkin-scrooge/.../conversions/thrift.scala:
+ * 330-333) through ScroogeThriftCodec (zipkin-cassandra/.../cassandra/AggregatesBuilder.scala:31),
+ * one column per record (CassandraAggregates.scala:111-116). Fields in id order, all written.
+ * encode: service ids resolve through names[id] (name_lens[id] bytes, case-sensitive);
+ * two-phase (out == NULL -> *len). decode: names map to ids through the dictionary of `dict`
+ * exactly as stored ("" stays ""; new names are added); two-phase on the link count; bytes that
+ * do not decode -> ZK_ERR_INVALID_SPAN. */
+zk_status zk_dependencies_encode(int64_t start_us, int64_t end_us, const zk_dep_link* links, uint64_t n_links,
+                                 const char* const* names, const uint32_t* name_lens, uint32_t num_names,
+                                 uint8_t* out, uint64_t cap, uint64_t* len);
+zk_status zk_dependencies_decode(zk_ingest* dict, const uint8_t* buf, uint64_t len, int64_t* start_us,
+                                 int64_t* end_us, zk_dep_link* out, uint64_t cap, uint64_t* n_links);
+/* the record's Cassandra row key: deps.startTime.floor(1.day).inMicroseconds
+ * (CassandraAggregates.scala:111-113), integer division toward zero */
+int64_t   zk_dependencies_row_key(int64_t start_us);
 
 uint64_t  zk_hash_string(const char* s, uint64_t len);
 /* raw Snappy block decompression (exposed for tools/tests): *out_len = uncompressed size; with

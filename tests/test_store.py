@@ -298,3 +298,56 @@ def test_gpu_job_with_no_links_writes_nothing(gpu):
     agg = GpuAggregates("anorm", services=names, clock=lambda: NOW)
     assert ZipkinAggregateJob(names, aggregates=agg).run(SpanColumns.empty(0), 2) is None
     assert agg.count() == 0
+
+
+# ---- the Dependencies record on the wire (Cassandra column value) ------------------------------
+def _fixture_deps():
+    fx = json.loads((GOLD / "aggregates_sql.json").read_text())
+    row = fx["dependencies"][0]
+    links = tuple(link(l["parent"], l["child"], Moments(l["m0"], l["m1"], l["m2"], l["m3"], l["m4"]))
+                  for l in fx["links"])
+    return Dependencies(row["start_ts"], row["end_ts"], links)
+
+
+def test_dependencies_thrift_is_byte_exact_and_round_trips():
+    from tests import thriftenc as T
+    from zipkin_amd.aggregates import dependencies_from_thrift, dependencies_to_thrift
+
+    deps = _fixture_deps()
+    raw = dependencies_to_thrift(deps)
+    want = T.dependencies(deps.start_time, deps.end_time,
+                          [(l.parent.name, l.child.name, tuple(l.duration_moments)) for l in deps.links])
+    assert raw == want
+    back = dependencies_from_thrift(raw)
+    assert (back.start_time, back.end_time) == (deps.start_time, deps.end_time)
+    assert back.links == deps.links  # same order, names and Moments
+    assert all(_same_bits(a.duration_moments, b.duration_moments) for a, b in zip(back.links, deps.links))
+
+
+def test_dependencies_thrift_edge_cases():
+    from tests import thriftenc as T
+    from zipkin_amd.aggregates import cassandra_row_key, dependencies_from_thrift, dependencies_to_thrift
+
+    # empty record (the monoid zero's times), case-sensitive and empty names, extreme Moments
+    zero = Dependencies(_abi.ZK_TIME_TOP, -2**63, ())
+    assert dependencies_from_thrift(dependencies_to_thrift(zero)) == zero
+    odd = Dependencies(5, 7, (link("", "a", Moments(1, -0.0, float("inf"), 1e-308, 5e-324)),
+                              link("A", "a", Moments(2**62, 1.5, 2.5, -3.5, 4.5))))
+    back = dependencies_from_thrift(dependencies_to_thrift(odd))
+    assert [(l.parent.name, l.child.name) for l in back.links] == [("", "a"), ("A", "a")]
+    assert all(_same_bits(a.duration_moments, b.duration_moments) for a, b in zip(back.links, odd.links))
+    # fields a newer writer might add are skipped; absent fields keep thrift defaults
+    raw = T.dependencies(1, 2, [("p", "c", (3, 1.0, 2.0, 3.0, 4.0))])
+    extra = T._fh(T.T_STRING, 9) + T._str("future") + b"\0"
+    got = dependencies_from_thrift(raw[:-1] + extra)
+    assert got.links == (link("p", "c", Moments(3, 1.0, 2.0, 3.0, 4.0)),)
+    assert dependencies_from_thrift(b"\0") == Dependencies(0, 0, ())
+    for bad in (raw[:-3], raw[:20], b"\x0f\x00\x03\x0c\x7f\xff\xff\xff"):
+        with pytest.raises(ZkError) as e:
+            dependencies_from_thrift(bad)
+        assert e.value.status == _abi.ZK_ERR_INVALID_SPAN
+    # row key: startTime.floor(1.day)
+    day = 86_400_000_000
+    assert cassandra_row_key(0) == 0
+    assert cassandra_row_key(NOW) == NOW // day * day
+    assert cassandra_row_key(3 * day - 1) == 2 * day

@@ -75,6 +75,23 @@ def span(s: Span, *, name: Optional[str] = "__from_s__", write_debug: bool = Tru
     return out + bytes([T_STOP])
 
 
+def dependencies(start_time: int, end_time: int, links) -> bytes:
+    """thriftscala.Dependencies (zipkinDependencies.thrift:24-43); links = [(parent, child,
+    (m0, m1, m2, m3, m4))]. Scrooge writes every field of these structs (none is optional)."""
+    out = _fh(T_I64, 1) + _i64(start_time) + _fh(T_I64, 2) + _i64(end_time)
+    out += _fh(T_LIST, 3) + struct.pack(">bi", T_STRUCT, len(links))
+    for parent, child, m in links:
+        out += _fh(T_STRING, 1) + _str(parent) + _fh(T_STRING, 2) + _str(child) + _fh(T_STRUCT, 3)
+        out += _fh(T_I64, 1) + _i64(m[0])
+        for fid, v in zip((2, 3, 4, 5), m[1:]):
+            out += _fh(T_DOUBLE, fid) + struct.pack(">d", v)
+        out += bytes([T_STOP, T_STOP])
+    return out + bytes([T_STOP])
+
+
+T_DOUBLE = 4
+
+
 def snappy(data: bytes) -> bytes:
     """Raw Snappy block, as iq80 Snappy.compress writes it (SnappyCodec.scala:34-41); pyarrow's
     bundled libsnappy is an independent implementation of the same format."""

@@ -279,6 +279,11 @@ _SIGNATURES = [
     ("zk_ingest_string", C.c_int, [_P, C.c_uint64, C.c_char_p, C.c_uint64, _U64P]),
     ("zk_hash_string", C.c_uint64, [C.c_char_p, C.c_uint64]),
     ("zk_snappy_uncompress", C.c_int, [_P, C.c_uint64, _P, C.c_uint64, _U64P]),
+    ("zk_dependencies_encode", C.c_int, [C.c_int64, C.c_int64, _P, C.c_uint64, _P, _P, C.c_uint32, _P, C.c_uint64,
+                                         _U64P]),
+    ("zk_dependencies_decode", C.c_int, [_P, _P, C.c_uint64, C.POINTER(C.c_int64), C.POINTER(C.c_int64), _P,
+                                         C.c_uint64, _U64P]),
+    ("zk_dependencies_row_key", C.c_int64, [C.c_int64]),
     # include/zkstore.h: the Aggregates store surface (host side)
     ("zk_store_create", C.c_int, [C.c_uint32, C.POINTER(_P)]),
     ("zk_store_destroy", C.c_int, [_P]),

@@ -306,6 +306,53 @@ class GpuAggregates(Aggregates):
         return self._get_top(_abi.ZK_TOP_KV_ANNOTATIONS, serviceName)
 
 
+def dependencies_to_thrift(deps: Dependencies) -> bytes:
+    """The record as the Cassandra store keeps it: TBinaryProtocol thriftscala.Dependencies
+    (zipkinDependencies.thrift:24-43 via WrappedDependencies.toThrift, thrift.scala:330-333)."""
+    names = Dictionary()
+    arr = (_abi.zk_dep_link * max(1, len(deps.links)))()
+    for i, l in enumerate(deps.links):
+        arr[i].parent = names.id(l.parent.name)
+        arr[i].child = names.id(l.child.name)
+        arr[i].moments = _to_c(l.duration_moments)
+    raw = [names.name(i).encode() for i in range(len(names))]
+    ptrs = (C.c_char_p * max(1, len(raw)))(*raw)
+    lens = (C.c_uint32 * max(1, len(raw)))(*[len(b) for b in raw])
+    L = _abi.lib()
+    n = C.c_uint64()
+    args = (int(deps.start_time), int(deps.end_time), arr, len(deps.links), ptrs, lens, len(raw))
+    st = L.zk_dependencies_encode(*args, None, 0, C.byref(n))
+    if st != _abi.ZK_OK:
+        raise _abi.ZkError(st, _abi.status_str(st))
+    buf = (C.c_uint8 * max(1, n.value))()
+    st = L.zk_dependencies_encode(*args, buf, n.value, C.byref(n))
+    if st != _abi.ZK_OK:
+        raise _abi.ZkError(st, _abi.status_str(st))
+    return bytes(buf)[: n.value]
+
+
+def dependencies_from_thrift(data: bytes) -> Dependencies:
+    """ThriftDependencies.toDependencies (thrift.scala:335-340) of a stored column value."""
+    from .ingest import SpanDecoder
+
+    dec = SpanDecoder()  # its dictionary maps the stored names to link ids
+    L = _abi.lib()
+    src = (C.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+    start, end, n = C.c_int64(), C.c_int64(), C.c_uint64()
+    dec._check(L.zk_dependencies_decode(dec._h, src, len(data), C.byref(start), C.byref(end), None, 0, C.byref(n)))
+    arr = (_abi.zk_dep_link * max(1, n.value))()
+    dec._check(L.zk_dependencies_decode(dec._h, src, len(data), C.byref(start), C.byref(end), arr, n.value,
+                                        C.byref(n)))
+    links = tuple(DependencyLink(Service(dec.service_name(arr[i].parent)), Service(dec.service_name(arr[i].child)),
+                                 _from_c(arr[i].moments)) for i in range(n.value))
+    return Dependencies(start.value, end.value, links)
+
+
+def cassandra_row_key(start_time_us: int) -> int:
+    """CassandraAggregates.storeDependencies row key: startTime.floor(1.day) in us."""
+    return int(_abi.lib().zk_dependencies_row_key(int(start_time_us)))
+
+
 def links_from_table(table, services: Dictionary) -> tuple:
     """The present cells of a finalized host LinkTable as DependencyLinks (zk_link_table_compact)."""
     L = _abi.lib()

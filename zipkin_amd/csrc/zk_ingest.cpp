@@ -297,6 +297,47 @@ bool is_core(const char* v, uint32_t l) {
     return v && l == 2 && ((v[0] == 'c' && (v[1] == 's' || v[1] == 'r')) || (v[0] == 's' && (v[1] == 'r' || v[1] == 's')));
 }
 
+// ---- TBinaryProtocol writer (the Dependencies record) -----------------------------------------
+struct Wr {
+    uint8_t* out;
+    uint64_t cap, len = 0;
+    void put(const void* p, uint64_t k) {
+        if (out && len + k <= cap) memcpy(out + len, p, k);
+        len += k;
+    }
+    void u8(uint8_t v) { put(&v, 1); }
+    void be(uint64_t v, int bytes) {
+        uint8_t b[8];
+        for (int i = 0; i < bytes; ++i) b[i] = (uint8_t)(v >> (8 * (bytes - 1 - i)));
+        put(b, bytes);
+    }
+    void field(uint8_t t, int16_t id) {
+        u8(t);
+        be((uint16_t)id, 2);
+    }
+    void i64(int16_t id, int64_t v) {
+        field(T_I64, id);
+        be((uint64_t)v, 8);
+    }
+    void dbl(int16_t id, double v) {
+        uint64_t bits;
+        memcpy(&bits, &v, 8);
+        field(T_DOUBLE, id);
+        be(bits, 8);
+    }
+    void str(int16_t id, const char* s, uint32_t l) {
+        field(T_STRING, id);
+        be(l, 4);
+        put(s, l);
+    }
+};
+
+double bits_double(int64_t v) {
+    double d;
+    memcpy(&d, &v, 8);
+    return d;
+}
+
 uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
@@ -316,6 +357,14 @@ struct zk_ingest {
     uint32_t service(const Host& h) {
         // thrift.scala:36-43: null or "" service name -> Endpoint.UnknownServiceName
         std::string name = (h.svc && h.svc_len) ? std::string(h.svc, h.svc_len) : std::string(kUnknownService);
+        auto it = svc_ids.find(name);
+        if (it != svc_ids.end()) return it->second;
+        const uint32_t id = (uint32_t)svc_names.size();
+        svc_ids.emplace(name, id);
+        svc_names.push_back(std::move(name));
+        return id;
+    }
+    uint32_t exact(std::string name) {  // Service(name) as is (no "Unknown service name" rule)
         auto it = svc_ids.find(name);
         if (it != svc_ids.end()) return it->second;
         const uint32_t id = (uint32_t)svc_names.size();
@@ -553,6 +602,123 @@ zk_status zk_ingest_service_name(const zk_ingest* g, uint32_t id, char* buf, uin
     if (cap < s.size()) return ZK_ERR_CAPACITY;
     memcpy(buf, s.data(), s.size());
     return ZK_OK;
+}
+
+// ---- Dependencies wire format (zipkinDependencies.thrift:24-43, ScroogeThriftCodec) -------------
+zk_status zk_dependencies_encode(int64_t start_us, int64_t end_us, const zk_dep_link* links, uint64_t n_links,
+                                 const char* const* names, const uint32_t* name_lens, uint32_t num_names,
+                                 uint8_t* out, uint64_t cap, uint64_t* len) {
+    if (!len || (n_links && !links) || (num_names && (!names || !name_lens))) return ZK_ERR_INVALID_ARG;
+    if (n_links > 0x7FFFFFFFull) return ZK_ERR_INVALID_ARG;
+    for (uint64_t i = 0; i < n_links; ++i)
+        if (links[i].parent >= num_names || links[i].child >= num_names) return ZK_ERR_SERVICE_RANGE;
+    Wr w{out, out ? cap : 0};
+    // Dependencies {1: i64 start_time, 2: i64 end_time, 3: list<DependencyLink> links}
+    w.i64(1, start_us);
+    w.i64(2, end_us);
+    w.field(T_LIST, 3);
+    w.u8(T_STRUCT);
+    w.be((uint32_t)n_links, 4);
+    for (uint64_t i = 0; i < n_links; ++i) {
+        const zk_dep_link& l = links[i];
+        // DependencyLink {1: string parent, 2: string child, 3: Moments duration_moments}
+        w.str(1, names[l.parent], name_lens[l.parent]);
+        w.str(2, names[l.child], name_lens[l.child]);
+        w.field(T_STRUCT, 3);
+        // Moments {1: i64 m0, 2..5: double m1..m4}
+        w.i64(1, l.moments.m0);
+        w.dbl(2, l.moments.m1);
+        w.dbl(3, l.moments.m2);
+        w.dbl(4, l.moments.m3);
+        w.dbl(5, l.moments.m4);
+        w.u8(T_STOP);
+        w.u8(T_STOP);
+    }
+    w.u8(T_STOP);
+    *len = w.len;
+    if (out && w.len > cap) return ZK_ERR_CAPACITY;
+    return ZK_OK;
+}
+
+zk_status zk_dependencies_decode(zk_ingest* g, const uint8_t* buf, uint64_t len, int64_t* start_us,
+                                 int64_t* end_us, zk_dep_link* out, uint64_t cap, uint64_t* n_links) {
+    if (!g || !buf || !start_us || !end_us || !n_links) return ZK_ERR_INVALID_ARG;
+    Rd r{buf, buf + len};
+    int64_t st = 0, en = 0;  // absent fields keep the thrift defaults
+    uint64_t k = 0;
+    bool overflow = false;
+    for (;;) {
+        const uint8_t t = r.u8();
+        if (!r.ok || t == T_STOP) break;
+        const int16_t id = r.i16();
+        if (id == 1 && t == T_I64) {
+            st = r.i64();
+        } else if (id == 2 && t == T_I64) {
+            en = r.i64();
+        } else if (id == 3 && t == T_LIST) {
+            const uint8_t et = r.u8();
+            const int32_t n = r.i32();
+            if (!r.ok || n < 0) break;
+            if (et != T_STRUCT) {
+                for (int32_t q = 0; r.ok && q < n; ++q) r.skip(et);
+                continue;
+            }
+            for (int32_t q = 0; r.ok && q < n; ++q) {
+                std::string parent, child;
+                zk_moments m = {0, 0.0, 0.0, 0.0, 0.0};
+                for (;;) {
+                    const uint8_t lt = r.u8();
+                    if (!r.ok || lt == T_STOP) break;
+                    const int16_t lid = r.i16();
+                    const char* s;
+                    uint32_t sl;
+                    if ((lid == 1 || lid == 2) && lt == T_STRING) {
+                        if (r.str(&s, &sl)) (lid == 1 ? parent : child).assign(s, sl);
+                    } else if (lid == 3 && lt == T_STRUCT) {
+                        for (;;) {
+                            const uint8_t mt = r.u8();
+                            if (!r.ok || mt == T_STOP) break;
+                            const int16_t mid = r.i16();
+                            if (mid == 1 && mt == T_I64)
+                                m.m0 = r.i64();
+                            else if (mid >= 2 && mid <= 5 && mt == T_DOUBLE)
+                                (mid == 2 ? m.m1 : mid == 3 ? m.m2 : mid == 4 ? m.m3 : m.m4) = bits_double(r.i64());
+                            else
+                                r.skip(mt);
+                        }
+                    } else {
+                        r.skip(lt);
+                    }
+                }
+                if (!r.ok) break;
+                if (out && k < cap) {
+                    out[k].parent = g->exact(parent);
+                    out[k].child = g->exact(child);
+                    out[k].moments = m;
+                } else if (out) {
+                    overflow = true;
+                }
+                ++k;
+            }
+        } else {
+            r.skip(t);
+        }
+        if (!r.ok) break;
+    }
+    if (!r.ok) {
+        g->err = "undecodable thrift Dependencies";
+        return ZK_ERR_INVALID_SPAN;
+    }
+    *start_us = st;
+    *end_us = en;
+    *n_links = k;
+    return overflow ? ZK_ERR_CAPACITY : ZK_OK;
+}
+
+int64_t zk_dependencies_row_key(int64_t start_us) {
+    // Time.floor(1.day) (twitter util: integer division of the time, i.e. toward zero)
+    constexpr int64_t kDayUs = 86400LL * 1000000LL;
+    return (start_us / kDayUs) * kDayUs;
 }
 
 zk_status zk_ingest_string(const zk_ingest* g, uint64_t hash, char* buf, uint64_t cap, uint64_t* len) {
