@@ -1,5 +1,5 @@
 /*
- * zkingest.h — C ABI of the span ingest decoder of libzkagg (host side).
+ * zkingest.h — C ABI of the span ingest decoders of libzkagg (host, and device: zk_ingest_dev).
  *
  * Turns stored span fragments into the 48-B columnar records of zkagg.h, replacing the job's
  * input decode: the Cassandra column value of one span fragment is
@@ -82,6 +82,25 @@ zk_status zk_ingest_service_id(zk_ingest* ing, const char* name, uint64_t len, u
 zk_status zk_ingest_service_name(const zk_ingest* ing, uint32_t id, char* buf, uint64_t cap, uint64_t* len);
 /* the string behind a key / value hash seen by this decoder (two-phase: buf NULL -> *len) */
 zk_status zk_ingest_string(const zk_ingest* ing, uint64_t hash, char* buf, uint64_t cap, uint64_t* len);
+
+/* ---- the same decoder on the device -------------------------------------------------------
+ * zk_ingest_dev decodes fragments that are already in HBM (buf and offsets are device pointers)
+ * into device columns, one lane per fragment (Snappy block, thrift walk, validation and record as
+ * above; no indexer items). Its service dictionary lives on the device: a batch's new names get ids
+ * in the order of their hash-table slots (not in order of first appearance; names whose hashes
+ * collide in the table may swap ids between runs), names are compared byte for byte. At most `max_services` distinct names
+ * (ZK_ERR_SERVICE_RANGE past that). Thrift nesting deeper than 16 levels inside skipped fields is
+ * treated as undecodable. Results are synchronous with respect to the host (the call waits). */
+typedef struct zk_ingest_dev zk_ingest_dev;
+zk_status   zk_ingest_dev_create(int32_t device, void* stream, uint32_t max_services, zk_ingest_dev** out);
+zk_status   zk_ingest_dev_destroy(zk_ingest_dev* ing);
+const char* zk_ingest_dev_last_error(const zk_ingest_dev* ing);
+zk_status   zk_ingest_dev_spans(zk_ingest_dev* ing, const uint8_t* buf, const uint64_t* offsets, uint64_t n,
+                                uint32_t codec, uint32_t flags, const zk_span_cols* out, uint64_t* n_out,
+                                uint64_t* n_rejected);
+zk_status   zk_ingest_dev_num_services(const zk_ingest_dev* ing, uint32_t* n);
+zk_status   zk_ingest_dev_service_name(const zk_ingest_dev* ing, uint32_t id, char* buf, uint64_t cap,
+                                       uint64_t* len);
 
 /* ---- the Dependencies record on the wire ----------------------------------------------------
  * TBinaryProtocol thriftscala.Dependencies (zipkinDependencies.thrift:24-43) as the Cassandra

@@ -364,3 +364,105 @@ def test_stored_span_job_end_to_end(gpu):
         assert tops == want
         for svc, lst in want.items():
             assert getter(svc) == lst
+
+
+# ---- the device decoder (zk_ingest_dev) against the host decoder ---------------------------------
+def _named(cols, names):
+    recs = records(cols)
+    for r in recs:
+        r["service"] = names[r.pop("service_id")] if r["flags"] & (_abi.ZK_F_SVC_SERVER | _abi.ZK_F_SVC_CLIENT) else None
+    return recs
+
+
+def _fuzz(blobs, seed):
+    rnd = random.Random(seed)
+    out = []
+    for r in blobs:
+        b = bytearray(r)
+        for _ in range(rnd.randint(0, 4)):
+            b[rnd.randrange(len(b))] = rnd.getrandbits(8)
+        out.append(bytes(b[: rnd.randrange(1, len(b) + 1)] if rnd.random() < 0.2 else b))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,anomalies,snappy,strict", [(71, 0.0, True, True), (72, 0.4, True, False),
+                                                          (73, 0.4, False, False)])
+def test_device_decoder_equals_host_decoder(gpu, seed, anomalies, snappy, strict):
+    from zipkin_amd.ingest import DeviceSpanDecoder
+
+    spans = gen_traces(seed, 300, max_depth=5, anomalies=anomalies)
+    ok, bads = bad_spans()
+    blobs = [T.span(s) for s in spans] + ([] if strict else [b for _, b in bads] + [T.span(ok)])
+    blobs = [T.snappy(b) for b in blobs] if snappy else blobs
+    hd = SpanDecoder()
+    hcols, hrej = hd.decode(blobs, snappy=snappy, strict=strict)
+    dd = DeviceSpanDecoder(64)
+    dcols, drej = dd.decode(blobs, snappy=snappy, strict=strict)
+    assert drej == hrej
+    assert _named(dcols.to_host(), dd.service_names()) == _named(hcols, hd.service_names())
+    assert sorted(dd.service_names()) == sorted(hd.service_names())
+
+
+@pytest.mark.gpu
+def test_device_decoder_strict_errors_and_fuzz(gpu):
+    from zipkin_amd.ingest import DeviceSpanDecoder
+
+    ok, bads = bad_spans()
+    for why, blob in bads:
+        dd = DeviceSpanDecoder(16)
+        with pytest.raises(ZkError) as ex:
+            dd.decode([T.snappy(T.span(ok)), T.snappy(blob)])
+        assert ex.value.status == _abi.ZK_ERR_INVALID_SPAN and "span 1" in ex.value.message
+    spans = gen_traces(74, 80)
+    raw = [T.span(s) for s in spans]
+    for snappy in (False, True):
+        blobs = _fuzz([T.snappy(b) for b in raw] if snappy else raw, 5 + snappy)
+        hd, dd = SpanDecoder(), DeviceSpanDecoder(4096)
+        hcols, hrej = hd.decode(blobs, snappy=snappy, strict=False)
+        dcols, drej = dd.decode(blobs, snappy=snappy, strict=False)
+        assert dcols.n + drej == len(blobs)
+        assert drej == hrej
+        assert _named(dcols.to_host(), dd.service_names()) == _named(hcols, hd.service_names())
+    # reference fixtures
+    for key in ("with_debug", "without_debug"):
+        cols, rej = DeviceSpanDecoder(4).decode([T.snappy(base64.b64decode(GOLDEN[key]))])
+        assert rej == 0 and records(cols.to_host()) == [GOLDEN["record"]]
+
+
+@pytest.mark.gpu
+def test_device_decoder_dictionary_across_batches_and_capacity(gpu):
+    from zipkin_amd.ingest import DeviceSpanDecoder
+
+    spans = gen_traces(75, 200, anomalies=0.2)
+    want, ids = expected_records(spans)
+    names = list(ids)
+    dd = DeviceSpanDecoder(len(names))
+    got = []
+    for lo in range(0, len(spans), 53):
+        cols, _ = dd.decode(encode_all(spans[lo:lo + 53]))
+        got += _named(cols.to_host(), dd.service_names())
+    for r in want:
+        r["service"] = names[r.pop("service_id")] if r["flags"] & 12 else None
+    assert got == want and sorted(dd.service_names()) == sorted(names)
+    small = DeviceSpanDecoder(3)
+    with pytest.raises(ZkError) as ex:
+        small.decode(encode_all(spans))
+    assert ex.value.status == _abi.ZK_ERR_SERVICE_RANGE
+
+
+@pytest.mark.gpu
+def test_device_decoded_bytes_to_dependencies(gpu):
+    from zipkin_amd import DepsContext
+    from zipkin_amd.ingest import DeviceSpanDecoder
+
+    spans = gen_traces(76, 400, max_depth=5, anomalies=0.3)
+    dd = DeviceSpanDecoder(128)
+    cols, rej = dd.decode(encode_all(spans))
+    assert rej == 0
+    names = dd.service_names()
+    with DepsContext(len(names), strict=False) as ctx:
+        ctx.accumulate(cols)
+        got = ctx.finalize()
+    ref = aggregate_job(spans, strict=False)
+    assert {(names[p], names[c]): tuple(m) for p, c, m in got.links()} == {k: tuple(m) for k, m in ref.exact().items()}

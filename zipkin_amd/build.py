@@ -22,6 +22,7 @@ SOURCES = [
     "zk_rt.hip",
     "zk_rt_api.cpp",
     "zk_ingest.cpp",
+    "zk_ingest_dev.hip",
 ]
 HEADERS = ["zk_internal.h", "zk_tracegen.h", "zk_sketch_internal.h", "zk_rt_internal.h", "zk_block.h"]
 PUBLIC_HEADERS = ["zkagg.h", "zksketch.h", "zkstore.h", "zkingest.h"]

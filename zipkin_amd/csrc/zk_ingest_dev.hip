@@ -1,0 +1,819 @@
+// zk_ingest_dev.hip — the span ingest decoder on the device (include/zkingest.h, zk_ingest_dev_*).
+//
+// The same contract as the host decoder (zk_ingest.cpp): stored fragments
+// Snappy(TBinaryProtocol(thrift Span)) (CassieSpanStore.scala:52; SnappyCodec.scala:32-51;
+// zipkinCore.thrift:27-58) -> thrift.scala validation (:36-121) -> the 48-B record of SURVEY
+// Appendix A.1, written straight into HBM columns. One lane per fragment: the Snappy block and the
+// thrift walk are sequential within a fragment, fragments are independent.
+//
+//   D1 k_ing_rawlen     Snappy header varint -> uncompressed length per fragment
+//   (hipcub scan)       -> scratch offset per fragment
+//   D2 k_ing_decode     decompress into scratch, walk the Span, validate, derive the record and the
+//                       service name (FNV-1a 64 + splitmix64 of its bytes, as zk_hash_string)
+//   D3 k_ing_dict_insert  claim a slot per new service hash in the persistent open-addressing table
+//   (host)              give new slots ids in slot order and copy their names to the device arena
+//   D4 k_ing_lookup     service hash -> id, the name bytes compared with the arena's (exact)
+//   (hipcub scan)       of accepted records -> output positions
+//   D5 k_ing_compact    accepted records -> the caller's columns, input order kept
+//
+// Every byte read is bounds-checked: corrupt input marks the fragment undecodable, never faults.
+#include <string.h>
+
+#include <hipcub/hipcub.hpp>
+#include <string>
+#include <vector>
+
+#include "zkingest.h"
+
+namespace zk {
+namespace {
+
+constexpr uint32_t kIngWG = 256;
+constexpr uint32_t kMaxRaw = 1u << 24;       // largest uncompressed fragment accepted (16 MiB)
+constexpr uint32_t kBadLen = 0xFFFFFFFFu;
+constexpr uint64_t kEmpty = 0ull;            // empty dictionary slot (hash 0 is stored as 1)
+constexpr uint32_t kNoId = 0xFFFFFFFFu;
+constexpr uint8_t kStOk = 0, kStInvalid = 1, kStUndecodable = 2, kStCollision = 3, kStRange = 4;
+const char kUnknown[] = "Unknown service name";  // Endpoint.UnknownServiceName (thrift.scala:36-43)
+
+enum : uint8_t { T_STOP = 0, T_BOOL = 2, T_BYTE = 3, T_DOUBLE = 4, T_I16 = 6, T_I32 = 8, T_I64 = 10,
+                 T_STRING = 11, T_STRUCT = 12, T_MAP = 13, T_SET = 14, T_LIST = 15 };
+
+__device__ __forceinline__ uint64_t d_mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t d_hash(const uint8_t* s, uint32_t n) {  // == zk_hash_string
+    uint64_t h = 0xCBF29CE484222325ull;
+    for (uint32_t i = 0; i < n; ++i) {
+        h ^= s[i];
+        h *= 0x100000001B3ull;
+    }
+    h = d_mix64(h);
+    return h ? h : 1ull;
+}
+
+// bounds-checked big-endian reader over [p, e)
+struct DRd {
+    const uint8_t* p;
+    const uint8_t* e;
+    bool ok;
+    __device__ bool need(uint64_t k) {
+        if (!ok || (uint64_t)(e - p) < k) ok = false;
+        return ok;
+    }
+    __device__ uint8_t u8() { return need(1) ? *p++ : 0; }
+    __device__ int16_t i16() {
+        if (!need(2)) return 0;
+        const int16_t v = (int16_t)((p[0] << 8) | p[1]);
+        p += 2;
+        return v;
+    }
+    __device__ int32_t i32() {
+        if (!need(4)) return 0;
+        const uint32_t v = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+        p += 4;
+        return (int32_t)v;
+    }
+    __device__ int64_t i64() {
+        if (!need(8)) return 0;
+        uint64_t v = 0;
+        for (int k = 0; k < 8; ++k) v = (v << 8) | p[k];
+        p += 8;
+        return (int64_t)v;
+    }
+    __device__ bool str(const uint8_t** s, uint32_t* len) {
+        const int32_t l = i32();
+        if (!ok || l < 0 || !need((uint64_t)l)) return ok = false;
+        *s = p;
+        *len = (uint32_t)l;
+        p += l;
+        return true;
+    }
+    // skip one value of type t; nested containers/structs iteratively up to a fixed depth
+    __device__ void skip(uint8_t t) {
+        // explicit stack: (type, remaining) for containers; structs use remaining = -1
+        uint8_t st_t[16], st_k[16], st_v[16];
+        int32_t st_n[16];
+        int sp = 0;
+        uint8_t cur = t;
+        for (;;) {
+            if (!ok) return;
+            switch (cur) {
+                case T_BOOL:
+                case T_BYTE: u8(); break;
+                case T_I16: i16(); break;
+                case T_I32: i32(); break;
+                case T_DOUBLE:
+                case T_I64: i64(); break;
+                case T_STRING: {
+                    const uint8_t* s;
+                    uint32_t l;
+                    str(&s, &l);
+                    break;
+                }
+                case T_STRUCT:
+                case T_MAP:
+                case T_SET:
+                case T_LIST: {
+                    if (sp == 16) {
+                        ok = false;
+                        return;
+                    }
+                    if (cur == T_STRUCT) {
+                        st_t[sp] = T_STRUCT;
+                        st_n[sp] = -1;
+                    } else if (cur == T_MAP) {
+                        st_t[sp] = T_MAP;
+                        st_k[sp] = u8();
+                        st_v[sp] = u8();
+                        const int32_t mc = i32();
+                        st_n[sp] = (mc < 0 || mc > (1 << 29)) ? -1 : mc * 2;  // keys and values alternate
+                    } else {
+                        st_t[sp] = cur;
+                        st_k[sp] = u8();
+                        st_n[sp] = i32();
+                    }
+                    if (!ok || (st_t[sp] != T_STRUCT && st_n[sp] < 0)) {
+                        ok = false;
+                        return;
+                    }
+                    ++sp;
+                    break;
+                }
+                default: ok = false; return;
+            }
+            // the next value to skip: from the innermost open container, closing finished ones
+            for (;;) {
+                if (sp == 0) return;
+                const int q = sp - 1;
+                if (st_t[q] == T_STRUCT) {
+                    const uint8_t ft = u8();
+                    if (!ok) return;
+                    if (ft == T_STOP) {
+                        --sp;
+                        continue;
+                    }
+                    i16();
+                    cur = ft;
+                    break;
+                }
+                if (st_n[q] == 0) {
+                    --sp;
+                    continue;
+                }
+                const int32_t left = st_n[q]--;
+                cur = st_t[q] == T_MAP ? ((left & 1) ? st_v[q] : st_k[q]) : st_k[q];
+                break;
+            }
+        }
+    }
+};
+
+__device__ __forceinline__ bool snappy_hdr(const uint8_t* in, uint64_t n, uint64_t* len, uint64_t* hdr) {
+    uint64_t v = 0;
+    for (uint64_t i = 0; i < n && i < 5; ++i) {
+        v |= (uint64_t)(in[i] & 0x7F) << (7 * i);
+        if (!(in[i] & 0x80)) {
+            *len = v;
+            *hdr = i + 1;
+            return v <= 0xFFFFFFFFull;
+        }
+    }
+    return false;
+}
+
+__device__ bool snappy_block(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t len) {
+    uint64_t dl, hdr;
+    if (!snappy_hdr(in, n, &dl, &hdr) || dl != len) return false;
+    uint64_t o = 0, i = hdr;
+    while (i < n) {
+        const uint8_t tag = in[i++];
+        uint64_t l, off;
+        const uint32_t kind = tag & 3;
+        if (kind == 0) {
+            l = tag >> 2;
+            if (l >= 60) {
+                const uint32_t nb = (uint32_t)l - 59;
+                if (i + nb > n) return false;
+                l = 0;
+                for (uint32_t k = 0; k < nb; ++k) l |= (uint64_t)in[i + k] << (8 * k);
+                i += nb;
+            }
+            l += 1;
+            if (i + l > n || o + l > len) return false;
+            for (uint64_t k = 0; k < l; ++k) out[o + k] = in[i + k];
+            i += l;
+            o += l;
+            continue;
+        }
+        if (kind == 1) {
+            if (i + 1 > n) return false;
+            l = ((tag >> 2) & 7) + 4;
+            off = ((uint64_t)(tag >> 5) << 8) | in[i];
+            i += 1;
+        } else if (kind == 2) {
+            if (i + 2 > n) return false;
+            l = (tag >> 2) + 1;
+            off = (uint64_t)in[i] | ((uint64_t)in[i + 1] << 8);
+            i += 2;
+        } else {
+            if (i + 4 > n) return false;
+            l = (tag >> 2) + 1;
+            off = (uint64_t)in[i] | ((uint64_t)in[i + 1] << 8) | ((uint64_t)in[i + 2] << 16) |
+                  ((uint64_t)in[i + 3] << 24);
+            i += 4;
+        }
+        if (off == 0 || off > o || o + l > len) return false;
+        for (uint64_t k = 0; k < l; ++k) out[o + k] = out[o - off + k];  // may overlap: bytewise
+        o += l;
+    }
+    return o == len;
+}
+
+struct IngArgs {
+    const uint8_t* buf;
+    const uint64_t* offsets;
+    uint64_t n;
+    uint32_t snappy;
+    uint64_t* raw_len;   // n (+1 for the scan)
+    uint64_t* raw_off;   // n + 1
+    uint8_t* scratch;
+    // per-fragment results
+    uint8_t* status;
+    uint64_t* tid;
+    uint64_t* sid;
+    uint64_t* pid;
+    int64_t* first;
+    int64_t* last;
+    uint32_t* flags;
+    uint32_t* svc;       // dictionary id after D4
+    uint64_t* svc_hash;  // 0: no service
+    uint64_t* name_ptr;  // device address of the service name bytes
+    uint32_t* name_len;
+    uint32_t* keep;      // 1 = record goes to the output (n + 1 for the scan)
+    uint32_t* pos;       // n + 1
+    // dictionary
+    uint64_t* d_key;
+    uint32_t* d_id;
+    uint64_t* d_ptr;     // device address of the slot's name (arena after assignment)
+    uint32_t* d_len;
+    uint32_t d_mask;
+    uint32_t max_services;
+    const uint8_t* unknown;  // device copy of kUnknown
+};
+
+__global__ __launch_bounds__(kIngWG) void k_ing_rawlen(IngArgs a) {
+    const uint64_t i = (uint64_t)blockIdx.x * kIngWG + threadIdx.x;
+    if (i >= a.n) return;
+    const uint64_t b = a.offsets[i], e = a.offsets[i + 1];
+    uint64_t len = e >= b ? e - b : 0, hdr;
+    if (e < b)
+        len = kBadLen;
+    else if (a.snappy && !(snappy_hdr(a.buf + b, e - b, &len, &hdr) && len <= kMaxRaw))
+        len = kBadLen;
+    a.raw_len[i] = len == kBadLen ? 0 : len;
+    a.status[i] = len == kBadLen ? kStUndecodable : kStOk;
+}
+
+__device__ __forceinline__ bool is_core(const uint8_t* v, uint32_t l, int* c) {
+    if (!v || l != 2) return false;
+    if (v[0] == 'c' && (v[1] == 's' || v[1] == 'r')) {
+        *c = v[1] == 's' ? 0 : 1;
+        return true;
+    }
+    if (v[0] == 's' && (v[1] == 'r' || v[1] == 's')) {
+        *c = v[1] == 'r' ? 2 : 3;
+        return true;
+    }
+    return false;
+}
+
+// the service name of an endpoint struct: field 3 (string); absent or "" -> kUnknown
+__device__ void read_endpoint(DRd& r, const uint8_t** name, uint32_t* nlen) {
+    *name = nullptr;
+    *nlen = 0;
+    for (;;) {
+        const uint8_t t = r.u8();
+        if (!r.ok || t == T_STOP) return;
+        const int16_t id = r.i16();
+        if (id == 3 && t == T_STRING)
+            r.str(name, nlen);
+        else
+            r.skip(t);
+    }
+}
+
+__global__ __launch_bounds__(kIngWG) void k_ing_decode(IngArgs a) {
+    const uint64_t i = (uint64_t)blockIdx.x * kIngWG + threadIdx.x;
+    if (i >= a.n) return;
+    a.keep[i] = 0u;
+    a.svc_hash[i] = 0ull;
+    if (a.status[i] != kStOk) return;
+    const uint64_t b = a.offsets[i], e = a.offsets[i + 1];
+    const uint8_t* src = a.buf + b;
+    uint64_t len = e - b;
+    if (a.snappy) {
+        uint8_t* dst = a.scratch + a.raw_off[i];
+        if (!snappy_block(src, len, dst, a.raw_len[i])) {
+            a.status[i] = kStUndecodable;
+            return;
+        }
+        src = dst;
+        len = a.raw_len[i];
+    }
+    DRd r{src, src + len, true};
+    int64_t trace = 0, id = 0, parent = 0;
+    bool has_parent = false, has_name = false, invalid = false;
+    int64_t first = 0, last = 0;
+    uint32_t nann = 0, cnt[4] = {0, 0, 0, 0};
+    const uint8_t* srv = nullptr;  // first sr/ss host's name (srv_set: a host was seen)
+    const uint8_t* cli = nullptr;
+    uint32_t srv_len = 0, cli_len = 0;
+    bool srv_set = false, cli_set = false;
+    for (;;) {
+        const uint8_t t = r.u8();
+        if (!r.ok || t == T_STOP) break;
+        const int16_t fid = r.i16();
+        if (fid == 1 && t == T_I64) {
+            trace = r.i64();
+        } else if (fid == 3 && t == T_STRING) {
+            const uint8_t* s;
+            uint32_t l;
+            has_name = r.str(&s, &l);
+        } else if (fid == 4 && t == T_I64) {
+            id = r.i64();
+        } else if (fid == 5 && t == T_I64) {
+            parent = r.i64();
+            has_parent = true;
+        } else if (fid == 6 && t == T_LIST) {
+            const uint8_t et = r.u8();
+            const int32_t cntl = r.i32();
+            if (!r.ok || cntl < 0) {
+                r.ok = false;
+                break;
+            }
+            if (et != T_STRUCT) {
+                for (int32_t q = 0; r.ok && q < cntl; ++q) r.skip(et);
+                continue;
+            }
+            for (int32_t q = 0; r.ok && q < cntl; ++q) {
+                // Annotation {1: i64 timestamp, 2: string value, 3: optional Endpoint host}
+                int64_t ts = 0;
+                const uint8_t* v = nullptr;
+                uint32_t vl = 0;
+                bool host = false;
+                const uint8_t* hn = nullptr;
+                uint32_t hl = 0;
+                for (;;) {
+                    const uint8_t at = r.u8();
+                    if (!r.ok || at == T_STOP) break;
+                    const int16_t aid = r.i16();
+                    if (aid == 1 && at == T_I64)
+                        ts = r.i64();
+                    else if (aid == 2 && at == T_STRING)
+                        r.str(&v, &vl);
+                    else if (aid == 3 && at == T_STRUCT) {
+                        host = true;
+                        read_endpoint(r, &hn, &hl);
+                    } else
+                        r.skip(at);
+                }
+                if (!r.ok) break;
+                if (ts <= 0 || (v && vl == 0)) invalid = true;  // thrift.scala:66-71
+                if (nann == 0 || ts < first) first = ts;
+                if (nann == 0 || ts > last) last = ts;
+                ++nann;
+                int c;
+                if (is_core(v, vl, &c)) {
+                    if (cnt[c] < 2) ++cnt[c];
+                    if (host) {
+                        if (c >= 2 && !srv_set) {
+                            srv_set = true;
+                            srv = hn;
+                            srv_len = hl;
+                        }
+                        if (c < 2 && !cli_set) {
+                            cli_set = true;
+                            cli = hn;
+                            cli_len = hl;
+                        }
+                    }
+                }
+            }
+        } else {
+            r.skip(t);
+        }
+        if (!r.ok) break;
+    }
+    if (!r.ok) {
+        a.status[i] = kStUndecodable;
+        return;
+    }
+    if (!has_name || invalid) {  // IncompleteTraceDataException / IllegalArgumentException
+        a.status[i] = kStInvalid;
+        return;
+    }
+    uint32_t f = has_parent ? ZK_F_HAS_PARENT : 0u;
+    if (nann) f |= ZK_F_HAS_ANNOTATIONS;
+    const uint8_t* nm = nullptr;
+    uint32_t nl = 0;
+    if (srv_set) {
+        f |= ZK_F_SVC_SERVER;
+        nm = srv;
+        nl = srv_len;
+    } else if (cli_set) {
+        f |= ZK_F_SVC_CLIENT;
+        nm = cli;
+        nl = cli_len;
+    }
+    if ((srv_set || cli_set) && (!nm || nl == 0)) {
+        nm = a.unknown;
+        nl = sizeof(kUnknown) - 1;
+    }
+    f |= (cnt[0] << ZK_F_CS_SHIFT) | (cnt[1] << ZK_F_CR_SHIFT) | (cnt[2] << ZK_F_SR_SHIFT) | (cnt[3] << ZK_F_SS_SHIFT);
+    a.tid[i] = (uint64_t)trace;
+    a.sid[i] = (uint64_t)id;
+    a.pid[i] = has_parent ? (uint64_t)parent : 0ull;
+    a.first[i] = nann ? first : 0;
+    a.last[i] = nann ? last : 0;
+    a.flags[i] = f;
+    a.svc[i] = 0u;
+    if (srv_set || cli_set) {
+        a.svc_hash[i] = d_hash(nm, nl);
+        a.name_ptr[i] = (uint64_t)(uintptr_t)nm;
+        a.name_len[i] = nl;
+    }
+    a.keep[i] = 1u;
+}
+
+__global__ __launch_bounds__(kIngWG) void k_ing_dict_insert(IngArgs a) {
+    const uint64_t i = (uint64_t)blockIdx.x * kIngWG + threadIdx.x;
+    if (i >= a.n || !a.keep[i]) return;
+    const uint64_t h = a.svc_hash[i];
+    if (!h) return;
+    uint32_t slot = (uint32_t)h & a.d_mask;
+    for (uint32_t step = 0; step <= a.d_mask; ++step) {
+        const unsigned long long old = atomicCAS((unsigned long long*)&a.d_key[slot], (unsigned long long)kEmpty,
+                                                 (unsigned long long)h);
+        if (old == kEmpty) {  // the first claimant names the slot (verified against the others in D4)
+            a.d_ptr[slot] = a.name_ptr[i];
+            a.d_len[slot] = a.name_len[i];
+            return;
+        }
+        if (old == h) return;
+        slot = (slot + 1) & a.d_mask;
+    }
+}
+
+__global__ __launch_bounds__(kIngWG) void k_ing_lookup(IngArgs a) {
+    const uint64_t i = (uint64_t)blockIdx.x * kIngWG + threadIdx.x;
+    if (i >= a.n || !a.keep[i]) return;
+    const uint64_t h = a.svc_hash[i];
+    if (!h) return;
+    uint32_t slot = (uint32_t)h & a.d_mask;
+    for (uint32_t step = 0; step <= a.d_mask; ++step) {
+        const uint64_t k = a.d_key[slot];
+        if (k == h) break;
+        if (k == kEmpty) {
+            slot = kNoId;
+            break;
+        }
+        slot = (slot + 1) & a.d_mask;
+    }
+    const uint32_t id = slot == kNoId ? kNoId : a.d_id[slot];
+    if (id == kNoId || id >= a.max_services) {
+        a.status[i] = kStRange;  // more distinct services than the decoder was sized for
+        a.keep[i] = 0u;
+        return;
+    }
+    // exact: the name bytes equal the slot's (a 64-bit hash collision is an error, not a merge)
+    const uint8_t* x = (const uint8_t*)(uintptr_t)a.name_ptr[i];
+    const uint8_t* y = (const uint8_t*)(uintptr_t)a.d_ptr[slot];
+    const uint32_t l = a.name_len[i];
+    bool same = l == a.d_len[slot];
+    for (uint32_t q = 0; same && q < l; ++q) same = x[q] == y[q];
+    if (!same) {
+        a.status[i] = kStCollision;
+        a.keep[i] = 0u;
+        return;
+    }
+    a.svc[i] = id;
+}
+
+__global__ __launch_bounds__(kIngWG) void k_ing_compact(IngArgs a, zk_span_cols o) {
+    const uint64_t i = (uint64_t)blockIdx.x * kIngWG + threadIdx.x;
+    if (i >= a.n || !a.keep[i]) return;
+    const uint32_t p = a.pos[i];
+    ((uint64_t*)o.trace_id)[p] = a.tid[i];
+    ((uint64_t*)o.span_id)[p] = a.sid[i];
+    ((uint64_t*)o.parent_id)[p] = a.pid[i];
+    ((int64_t*)o.first_ts)[p] = a.first[i];
+    ((int64_t*)o.last_ts)[p] = a.last[i];
+    ((uint32_t*)o.service_id)[p] = a.svc[i];
+    ((uint32_t*)o.flags)[p] = a.flags[i];
+}
+
+__global__ void k_ing_count(const uint8_t* status, uint64_t n, unsigned long long* counts, unsigned int* first_bad) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t s = status[i];
+    if (s == kStOk) return;
+    atomicAdd(&counts[s], 1ull);
+    atomicMin(first_bad, (unsigned int)(i < 0xFFFFFFFFull ? i : 0xFFFFFFFEull));
+}
+
+}  // namespace
+}  // namespace zk
+
+using namespace zk;
+
+struct zk_ingest_dev {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    uint32_t max_services = 0;
+    uint32_t table = 0;
+    // persistent dictionary
+    uint64_t* d_key = nullptr;
+    uint32_t* d_id = nullptr;
+    uint64_t* d_ptr = nullptr;
+    uint32_t* d_len = nullptr;
+    uint8_t* arena = nullptr;  // names, device copy (kUnknown first)
+    uint64_t arena_cap = 0, arena_used = 0;
+    std::vector<std::string> names;
+    std::vector<uint32_t> slot_id;  // host mirror of d_id
+    // per-batch scratch
+    void* batch = nullptr;
+    uint64_t batch_cap = 0;
+    uint8_t* scratch = nullptr;
+    uint64_t scratch_cap = 0;
+    void* cub = nullptr;
+    size_t cub_cap = 0;
+    unsigned long long* counts = nullptr;  // [8] per status + first_bad
+    std::string err;
+};
+
+namespace {
+
+zk_status dfail(zk_ingest_dev* g, zk_status s, const std::string& m) {
+    if (g) g->err = m;
+    return s;
+}
+
+#define ING_HIP(g, call)                                                                                \
+    do {                                                                                                \
+        hipError_t _e = (call);                                                                         \
+        if (_e != hipSuccess) return dfail(g, ZK_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
+
+}  // namespace
+
+extern "C" {
+
+zk_status zk_ingest_dev_create(int32_t device, void* stream, uint32_t max_services, zk_ingest_dev** out) {
+    if (!out || max_services == 0 || max_services > (1u << 20)) return ZK_ERR_INVALID_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0 || device < 0 || device >= ndev) return ZK_ERR_NO_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return ZK_ERR_NO_DEVICE;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return ZK_ERR_NO_DEVICE;
+    zk_ingest_dev* g = new zk_ingest_dev();
+    g->device = device;
+    g->max_services = max_services;
+    uint32_t t = 1024;
+    while (t < 2 * max_services) t <<= 1;
+    g->table = t;
+    g->slot_id.assign(t, kNoId);
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) {
+        if (stream) {
+            g->stream = (hipStream_t)stream;
+        } else {
+            e = hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking);
+            g->own_stream = true;
+        }
+    }
+    g->arena_cap = 1 << 16;
+    if (e == hipSuccess) e = hipMalloc(&g->d_key, (uint64_t)t * 8);
+    if (e == hipSuccess) e = hipMalloc(&g->d_id, (uint64_t)t * 4);
+    if (e == hipSuccess) e = hipMalloc(&g->d_ptr, (uint64_t)t * 8);
+    if (e == hipSuccess) e = hipMalloc(&g->d_len, (uint64_t)t * 4);
+    if (e == hipSuccess) e = hipMalloc(&g->arena, g->arena_cap);
+    if (e == hipSuccess) e = hipMalloc(&g->counts, 16 * 8);
+    if (e == hipSuccess) e = hipMemsetAsync(g->d_key, 0, (uint64_t)t * 8, g->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(g->d_id, 0xFF, (uint64_t)t * 4, g->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(g->arena, kUnknown, sizeof(kUnknown) - 1, hipMemcpyHostToDevice, g->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(g->stream);
+    g->arena_used = sizeof(kUnknown) - 1;
+    if (e != hipSuccess) {
+        zk_ingest_dev_destroy(g);
+        return ZK_ERR_HIP;
+    }
+    *out = g;
+    return ZK_OK;
+}
+
+zk_status zk_ingest_dev_destroy(zk_ingest_dev* g) {
+    if (!g) return ZK_ERR_INVALID_ARG;
+    hipSetDevice(g->device);
+    if (g->stream) hipStreamSynchronize(g->stream);
+    hipFree(g->d_key);
+    hipFree(g->d_id);
+    hipFree(g->d_ptr);
+    hipFree(g->d_len);
+    hipFree(g->arena);
+    hipFree(g->counts);
+    hipFree(g->batch);
+    hipFree(g->scratch);
+    hipFree(g->cub);
+    if (g->own_stream && g->stream) hipStreamDestroy(g->stream);
+    delete g;
+    return ZK_OK;
+}
+
+const char* zk_ingest_dev_last_error(const zk_ingest_dev* g) { return g ? g->err.c_str() : "null decoder"; }
+
+zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* offsets, uint64_t n,
+                              uint32_t codec, uint32_t flags, const zk_span_cols* out, uint64_t* n_out,
+                              uint64_t* n_rejected) {
+    if (!g || !n_out || !n_rejected) return ZK_ERR_INVALID_ARG;
+    *n_out = *n_rejected = 0;
+    if (n == 0) return ZK_OK;
+    if (!buf || !offsets || !out || !out->trace_id || !out->span_id || !out->parent_id || !out->first_ts ||
+        !out->last_ts || !out->service_id || !out->flags)
+        return ZK_ERR_INVALID_ARG;
+    if (codec != ZK_CODEC_THRIFT && codec != ZK_CODEC_SNAPPY_THRIFT) return dfail(g, ZK_ERR_INVALID_ARG, "unknown codec");
+    if (n >= 0x7FFFFFFFull) return dfail(g, ZK_ERR_INVALID_ARG, "batch of 2^31 fragments or more");
+    ING_HIP(g, hipSetDevice(g->device));
+    // per-fragment arrays: 8-byte columns first, then 4-byte, then 1-byte
+    const uint64_t n1 = n + 1;
+    const uint64_t bytes = align256(8 * n1) * 10 + align256(4 * n1) * 5 + align256(n1);
+    if (bytes > g->batch_cap) {
+        hipFree(g->batch);
+        g->batch = nullptr;
+        ING_HIP(g, hipMalloc(&g->batch, bytes));
+        g->batch_cap = bytes;
+    }
+    uint8_t* p = (uint8_t*)g->batch;
+    auto take = [&](uint64_t b) {
+        uint8_t* q = p;
+        p += align256(b);
+        return q;
+    };
+    IngArgs a{};
+    a.buf = buf;
+    a.offsets = offsets;
+    a.n = n;
+    a.snappy = codec == ZK_CODEC_SNAPPY_THRIFT;
+    a.raw_len = (uint64_t*)take(8 * n1);
+    a.raw_off = (uint64_t*)take(8 * n1);
+    a.tid = (uint64_t*)take(8 * n1);
+    a.sid = (uint64_t*)take(8 * n1);
+    a.pid = (uint64_t*)take(8 * n1);
+    a.first = (int64_t*)take(8 * n1);
+    a.last = (int64_t*)take(8 * n1);
+    a.svc_hash = (uint64_t*)take(8 * n1);
+    a.name_ptr = (uint64_t*)take(8 * n1);
+    take(8 * n1);  // (spare)
+    a.flags = (uint32_t*)take(4 * n1);
+    a.svc = (uint32_t*)take(4 * n1);
+    a.name_len = (uint32_t*)take(4 * n1);
+    a.keep = (uint32_t*)take(4 * n1);
+    a.pos = (uint32_t*)take(4 * n1);
+    a.status = take(n1);
+    a.d_key = g->d_key;
+    a.d_id = g->d_id;
+    a.d_ptr = g->d_ptr;
+    a.d_len = g->d_len;
+    a.d_mask = g->table - 1;
+    a.max_services = g->max_services;
+    a.unknown = g->arena;
+    const dim3 grid((unsigned)((n + kIngWG - 1) / kIngWG)), blk(kIngWG);
+    hipStream_t s = g->stream;
+    // D1 + scan: scratch offsets
+    hipLaunchKernelGGL(k_ing_rawlen, grid, blk, 0, s, a);
+    ING_HIP(g, hipGetLastError());
+    size_t need = 0, need2 = 0;
+    ING_HIP(g, hipcub::DeviceScan::ExclusiveSum(nullptr, need, a.raw_len, a.raw_off, (int)n1, s));
+    ING_HIP(g, hipcub::DeviceScan::ExclusiveSum(nullptr, need2, a.keep, a.pos, (int)n1, s));
+    if (need2 > need) need = need2;
+    if (need > g->cub_cap) {
+        hipFree(g->cub);
+        g->cub = nullptr;
+        ING_HIP(g, hipMalloc(&g->cub, need));
+        g->cub_cap = need;
+    }
+    ING_HIP(g, hipMemsetAsync(a.raw_len + n, 0, 8, s));
+    ING_HIP(g, hipcub::DeviceScan::ExclusiveSum(g->cub, need, a.raw_len, a.raw_off, (int)n1, s));
+    uint64_t total = 0;
+    if (a.snappy) {
+        ING_HIP(g, hipMemcpyAsync(&total, a.raw_off + n, 8, hipMemcpyDeviceToHost, s));
+        ING_HIP(g, hipStreamSynchronize(s));
+        if (total + 1 > g->scratch_cap) {
+            hipFree(g->scratch);
+            g->scratch = nullptr;
+            ING_HIP(g, hipMalloc(&g->scratch, total + 1));
+            g->scratch_cap = total + 1;
+        }
+    }
+    a.scratch = g->scratch;
+    // D2, D3
+    hipLaunchKernelGGL(k_ing_decode, grid, blk, 0, s, a);
+    hipLaunchKernelGGL(k_ing_dict_insert, grid, blk, 0, s, a);
+    ING_HIP(g, hipGetLastError());
+    // ids for new slots, in slot order; their names into the device arena
+    std::vector<uint64_t> key(g->table), ptr(g->table);
+    std::vector<uint32_t> len(g->table);
+    ING_HIP(g, hipMemcpyAsync(key.data(), g->d_key, key.size() * 8, hipMemcpyDeviceToHost, s));
+    ING_HIP(g, hipMemcpyAsync(ptr.data(), g->d_ptr, ptr.size() * 8, hipMemcpyDeviceToHost, s));
+    ING_HIP(g, hipMemcpyAsync(len.data(), g->d_len, len.size() * 4, hipMemcpyDeviceToHost, s));
+    ING_HIP(g, hipStreamSynchronize(s));
+    bool changed = false;
+    std::vector<uint8_t*> retired;  // old arenas stay valid until this batch's lookups are done
+    for (uint32_t q = 0; q < g->table; ++q) {
+        if (key[q] == kEmpty || g->slot_id[q] != kNoId) continue;
+        std::string nm(len[q], '\0');
+        if (len[q]) ING_HIP(g, hipMemcpy(&nm[0], (const void*)(uintptr_t)ptr[q], len[q], hipMemcpyDeviceToHost));
+        if (g->arena_used + len[q] > g->arena_cap) {
+            uint64_t cap = g->arena_cap;
+            while (cap < g->arena_used + len[q]) cap *= 2;
+            uint8_t* na = nullptr;
+            ING_HIP(g, hipMalloc(&na, cap));
+            ING_HIP(g, hipMemcpy(na, g->arena, g->arena_used, hipMemcpyDeviceToDevice));
+            // repoint the named slots at the new arena
+            for (uint32_t r = 0; r < g->table; ++r)
+                if (g->slot_id[r] != kNoId) ptr[r] = (uint64_t)(uintptr_t)na + (ptr[r] - (uint64_t)(uintptr_t)g->arena);
+            retired.push_back(g->arena);
+            g->arena = na;
+            g->arena_cap = cap;
+            a.unknown = na;
+        }
+        if (len[q]) ING_HIP(g, hipMemcpy(g->arena + g->arena_used, nm.data(), len[q], hipMemcpyHostToDevice));
+        ptr[q] = (uint64_t)(uintptr_t)(g->arena + g->arena_used);
+        g->arena_used += len[q];
+        g->slot_id[q] = (uint32_t)g->names.size();
+        g->names.push_back(std::move(nm));
+        changed = true;
+    }
+    if (changed) {
+        ING_HIP(g, hipMemcpyAsync(g->d_id, g->slot_id.data(), g->slot_id.size() * 4, hipMemcpyHostToDevice, s));
+        ING_HIP(g, hipMemcpyAsync(g->d_ptr, ptr.data(), ptr.size() * 8, hipMemcpyHostToDevice, s));
+    }
+    // D4, scan, D5
+    hipLaunchKernelGGL(k_ing_lookup, grid, blk, 0, s, a);
+    ING_HIP(g, hipMemsetAsync(a.keep + n, 0, 4, s));
+    ING_HIP(g, hipcub::DeviceScan::ExclusiveSum(g->cub, need, a.keep, a.pos, (int)n1, s));
+    ING_HIP(g, hipMemsetAsync(g->counts, 0, 8 * 8, s));
+    ING_HIP(g, hipMemsetAsync(g->counts + 8, 0xFF, 8, s));
+    hipLaunchKernelGGL(k_ing_count, grid, blk, 0, s, (const uint8_t*)a.status, n, g->counts,
+                       (unsigned int*)(g->counts + 8));
+    ING_HIP(g, hipGetLastError());
+    unsigned long long c[9];
+    uint32_t kept = 0;
+    ING_HIP(g, hipMemcpyAsync(c, g->counts, 9 * 8, hipMemcpyDeviceToHost, s));
+    ING_HIP(g, hipMemcpyAsync(&kept, a.pos + n, 4, hipMemcpyDeviceToHost, s));
+    ING_HIP(g, hipStreamSynchronize(s));
+    for (uint8_t* r : retired) hipFree(r);
+    const unsigned first_bad = (unsigned)(c[8] & 0xFFFFFFFFu);
+    if (c[kStCollision])
+        return dfail(g, ZK_ERR_INVALID_SPAN, "two service names share a 64-bit hash (fragment " +
+                                                  std::to_string(first_bad) + ")");
+    if (c[kStRange])
+        return dfail(g, ZK_ERR_SERVICE_RANGE, "more distinct service names than max_services");
+    const bool strict = (flags & ZK_INGEST_STRICT) != 0;
+    const uint64_t bad = c[kStInvalid] + c[kStUndecodable];
+    if (strict && bad)
+        return dfail(g, ZK_ERR_INVALID_SPAN, "span " + std::to_string(first_bad) + ": " +
+                                                 (c[kStUndecodable] ? "undecodable or invalid span" : "invalid span"));
+    hipLaunchKernelGGL(k_ing_compact, grid, blk, 0, s, a, *out);
+    ING_HIP(g, hipGetLastError());
+    ING_HIP(g, hipStreamSynchronize(s));
+    *n_out = kept;
+    *n_rejected = bad;
+    return ZK_OK;
+}
+
+zk_status zk_ingest_dev_num_services(const zk_ingest_dev* g, uint32_t* n) {
+    if (!g || !n) return ZK_ERR_INVALID_ARG;
+    *n = (uint32_t)g->names.size();
+    return ZK_OK;
+}
+
+zk_status zk_ingest_dev_service_name(const zk_ingest_dev* g, uint32_t id, char* buf, uint64_t cap, uint64_t* len) {
+    if (!g || !len) return ZK_ERR_INVALID_ARG;
+    if (id >= g->names.size()) return ZK_ERR_SERVICE_RANGE;
+    const std::string& s = g->names[id];
+    *len = s.size();
+    if (!buf) return ZK_OK;
+    if (cap < s.size()) return ZK_ERR_CAPACITY;
+    memcpy(buf, s.data(), s.size());
+    return ZK_OK;
+}
+
+}  // extern "C"

@@ -91,7 +91,7 @@ class SpanDecoder:
         self._check(self._L.zk_ingest_service_name(self._h, i, None, 0, C.byref(ln)))
         buf = C.create_string_buffer(max(1, ln.value))
         self._check(self._L.zk_ingest_service_name(self._h, i, buf, ln.value, C.byref(ln)))
-        return buf.raw[: ln.value].decode()
+        return buf.raw[: ln.value].decode("utf-8", "surrogateescape")
 
     def service_names(self) -> List[str]:
         return [self.service_name(i) for i in range(self.num_services)]
@@ -101,7 +101,7 @@ class SpanDecoder:
         self._check(self._L.zk_ingest_string(self._h, h, None, 0, C.byref(ln)))
         buf = C.create_string_buffer(max(1, ln.value))
         self._check(self._L.zk_ingest_string(self._h, h, buf, ln.value, C.byref(ln)))
-        return buf.raw[: ln.value].decode()
+        return buf.raw[: ln.value].decode("utf-8", "surrogateescape")
 
 
 def snappy_uncompress(data: bytes) -> bytes:
@@ -116,3 +116,76 @@ def snappy_uncompress(data: bytes) -> bytes:
     if st != _abi.ZK_OK:
         raise _abi.ZkError(st, _abi.status_str(st))
     return out[: n.value].tobytes()
+
+
+class DeviceSpanDecoder:
+    """zk_ingest_dev: stored fragments already in HBM -> device columns (one lane per fragment).
+
+    `decode_device(buf, offsets, n)` takes torch tensors (uint8 bytes, int64 offsets[n+1]) on the
+    device; `decode(blobs)` uploads a list of bytes objects first (tests, small batches)."""
+
+    def __init__(self, max_services: int = 4096, *, device: int = 0, stream: int | None = None):
+        self._L = _abi.lib()
+        h = C.c_void_p()
+        st = self._L.zk_ingest_dev_create(device, stream, max_services, C.byref(h))
+        if st != _abi.ZK_OK:
+            raise _abi.ZkError(st, _abi.status_str(st))
+        self._h = h
+        self.device = device
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.zk_ingest_dev_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, st: int) -> None:
+        if st != _abi.ZK_OK:
+            raise _abi.ZkError(st, self._L.zk_ingest_dev_last_error(self._h).decode() or _abi.status_str(st))
+
+    def decode_device(self, buf, offsets, n: int, *, snappy: bool = True, strict: bool = True, out=None):
+        """-> (DeviceColumns with .n = records written, rejected)."""
+        from .columns import DeviceColumns
+
+        cols = out if out is not None else DeviceColumns(max(1, n), device=f"cuda:{self.device}")
+        nout, nrej = C.c_uint64(), C.c_uint64()
+        ab = cols.abi(n)
+        codec = _abi.ZK_CODEC_SNAPPY_THRIFT if snappy else _abi.ZK_CODEC_THRIFT
+        self._check(self._L.zk_ingest_dev_spans(self._h, buf.data_ptr(), offsets.data_ptr(), n, codec,
+                                                _abi.ZK_INGEST_STRICT if strict else 0, C.byref(ab),
+                                                C.byref(nout), C.byref(nrej)))
+        cols.n = int(nout.value)
+        return cols, int(nrej.value)
+
+    def decode(self, blobs: Sequence[bytes], *, snappy: bool = True, strict: bool = True):
+        import torch
+
+        dev = f"cuda:{self.device}"
+        offsets = np.zeros(len(blobs) + 1, np.int64)
+        if blobs:
+            offsets[1:] = np.cumsum([len(b) for b in blobs])
+        raw = np.frombuffer(b"".join(blobs) or b"\0", dtype=np.uint8)
+        buf = torch.from_numpy(raw.copy()).to(dev)
+        off = torch.from_numpy(offsets).to(dev)
+        return self.decode_device(buf, off, len(blobs), snappy=snappy, strict=strict)
+
+    @property
+    def num_services(self) -> int:
+        n = C.c_uint32()
+        self._check(self._L.zk_ingest_dev_num_services(self._h, C.byref(n)))
+        return int(n.value)
+
+    def service_name(self, i: int) -> str:
+        ln = C.c_uint64()
+        self._check(self._L.zk_ingest_dev_service_name(self._h, i, None, 0, C.byref(ln)))
+        buf = C.create_string_buffer(max(1, ln.value))
+        self._check(self._L.zk_ingest_dev_service_name(self._h, i, buf, ln.value, C.byref(ln)))
+        return buf.raw[: ln.value].decode("utf-8", "surrogateescape")
+
+    def service_names(self) -> List[str]:
+        return [self.service_name(i) for i in range(self.num_services)]
