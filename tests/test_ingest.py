@@ -405,6 +405,33 @@ def test_device_decoder_equals_host_decoder(gpu, seed, anomalies, snappy, strict
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("snappy", [True, False])
+def test_device_decoder_large_fragments_take_the_global_path(gpu, snappy):
+    """Waves of 64 fragments whose bytes exceed the LDS staging (16 KiB in / 24 KiB out) are
+    deferred to the global-memory decoder: mixed batches give the same records either way."""
+    import dataclasses
+
+    from zipkin_amd.ingest import DeviceSpanDecoder
+
+    rnd = random.Random(77)
+    spans = gen_traces(77, 300, max_depth=5, anomalies=0.2)
+    out = []
+    for k, s in enumerate(spans):
+        if k % 97 == 5 or 640 <= k < 704:  # isolated giants, and one whole wave of mid-size ones
+            size = 20000 if k % 97 == 5 else 700
+            pad = BinaryAnnotation("blob", bytes(rnd.getrandbits(8) for _ in range(size)), "BYTES", None)
+            s = dataclasses.replace(s, binary_annotations=s.binary_annotations + (pad,))
+        out.append(s)
+    blobs = encode_all(out, snappy)
+    hd = SpanDecoder()
+    hcols, hrej = hd.decode(blobs, snappy=snappy, strict=False)
+    dd = DeviceSpanDecoder(64)
+    dcols, drej = dd.decode(blobs, snappy=snappy, strict=False)
+    assert drej == hrej
+    assert _named(dcols.to_host(), dd.service_names()) == _named(hcols, hd.service_names())
+
+
+@pytest.mark.gpu
 def test_device_decoder_strict_errors_and_fuzz(gpu):
     from zipkin_amd.ingest import DeviceSpanDecoder
 

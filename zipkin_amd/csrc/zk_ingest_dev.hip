@@ -33,7 +33,7 @@ constexpr uint32_t kMaxRaw = 1u << 24;       // largest uncompressed fragment ac
 constexpr uint32_t kBadLen = 0xFFFFFFFFu;
 constexpr uint64_t kEmpty = 0ull;            // empty dictionary slot (hash 0 is stored as 1)
 constexpr uint32_t kNoId = 0xFFFFFFFFu;
-constexpr uint8_t kStOk = 0, kStInvalid = 1, kStUndecodable = 2, kStCollision = 3, kStRange = 4;
+constexpr uint8_t kStOk = 0, kStInvalid = 1, kStUndecodable = 2, kStCollision = 3, kStRange = 4, kStDefer = 5;
 const char kUnknown[] = "Unknown service name";  // Endpoint.UnknownServiceName (thrift.scala:36-43)
 
 enum : uint8_t { T_STOP = 0, T_BOOL = 2, T_BYTE = 3, T_DOUBLE = 4, T_I16 = 6, T_I32 = 8, T_I64 = 10,
@@ -185,7 +185,7 @@ __device__ __forceinline__ bool snappy_hdr(const uint8_t* in, uint64_t n, uint64
     return false;
 }
 
-__device__ bool snappy_block(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t len) {
+__device__ __forceinline__ bool snappy_block(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t len) {
     uint64_t dl, hdr;
     if (!snappy_hdr(in, n, &dl, &hdr) || dl != len) return false;
     uint64_t o = 0, i = hdr;
@@ -292,7 +292,7 @@ __device__ __forceinline__ bool is_core(const uint8_t* v, uint32_t l, int* c) {
 }
 
 // the service name of an endpoint struct: field 3 (string); absent or "" -> kUnknown
-__device__ void read_endpoint(DRd& r, const uint8_t** name, uint32_t* nlen) {
+__device__ __forceinline__ void read_endpoint(DRd& r, const uint8_t** name, uint32_t* nlen) {
     *name = nullptr;
     *nlen = 0;
     for (;;) {
@@ -306,24 +306,10 @@ __device__ void read_endpoint(DRd& r, const uint8_t** name, uint32_t* nlen) {
     }
 }
 
-__global__ __launch_bounds__(kIngWG) void k_ing_decode(IngArgs a) {
-    const uint64_t i = (uint64_t)blockIdx.x * kIngWG + threadIdx.x;
-    if (i >= a.n) return;
-    a.keep[i] = 0u;
-    a.svc_hash[i] = 0ull;
-    if (a.status[i] != kStOk) return;
-    const uint64_t b = a.offsets[i], e = a.offsets[i + 1];
-    const uint8_t* src = a.buf + b;
-    uint64_t len = e - b;
-    if (a.snappy) {
-        uint8_t* dst = a.scratch + a.raw_off[i];
-        if (!snappy_block(src, len, dst, a.raw_len[i])) {
-            a.status[i] = kStUndecodable;
-            return;
-        }
-        src = dst;
-        len = a.raw_len[i];
-    }
+// The thrift walk of one decompressed Span at [src, src + len): validation (status on failure,
+// -1), the record columns, and the service name (1: *nm/*nl set; 0: the span has no service).
+__device__ __forceinline__ int parse_record(const IngArgs& a, uint64_t i, const uint8_t* src, uint64_t len,
+                                            const uint8_t** nm_out, uint32_t* nl_out) {
     DRd r{src, src + len, true};
     int64_t trace = 0, id = 0, parent = 0;
     bool has_parent = false, has_name = false, invalid = false;
@@ -410,11 +396,11 @@ __global__ __launch_bounds__(kIngWG) void k_ing_decode(IngArgs a) {
     }
     if (!r.ok) {
         a.status[i] = kStUndecodable;
-        return;
+        return -1;
     }
     if (!has_name || invalid) {  // IncompleteTraceDataException / IllegalArgumentException
         a.status[i] = kStInvalid;
-        return;
+        return -1;
     }
     uint32_t f = has_parent ? ZK_F_HAS_PARENT : 0u;
     if (nann) f |= ZK_F_HAS_ANNOTATIONS;
@@ -441,10 +427,114 @@ __global__ __launch_bounds__(kIngWG) void k_ing_decode(IngArgs a) {
     a.last[i] = nann ? last : 0;
     a.flags[i] = f;
     a.svc[i] = 0u;
-    if (srv_set || cli_set) {
-        a.svc_hash[i] = d_hash(nm, nl);
-        a.name_ptr[i] = (uint64_t)(uintptr_t)nm;
-        a.name_len[i] = nl;
+    *nm_out = nm;
+    *nl_out = nl;
+    return (srv_set || cli_set) ? 1 : 0;
+}
+
+__device__ __forceinline__ void publish_name(const IngArgs& a, uint64_t i, const uint8_t* nm, uint32_t nl) {
+    a.svc_hash[i] = d_hash(nm, nl);
+    a.name_ptr[i] = (uint64_t)(uintptr_t)nm;
+    a.name_len[i] = nl;
+}
+
+// D2 (global memory): every fragment, or only those the LDS kernel deferred
+__global__ __launch_bounds__(kIngWG) void k_ing_decode(IngArgs a, uint32_t deferred_only) {
+    const uint64_t i = (uint64_t)blockIdx.x * kIngWG + threadIdx.x;
+    if (i >= a.n) return;
+    if (deferred_only) {
+        if (a.status[i] != kStDefer) return;
+        a.status[i] = kStOk;
+    }
+    a.keep[i] = 0u;
+    a.svc_hash[i] = 0ull;
+    if (a.status[i] != kStOk) return;
+    const uint64_t b = a.offsets[i], e = a.offsets[i + 1];
+    const uint8_t* src = a.buf + b;
+    uint64_t len = e - b;
+    if (a.snappy) {
+        uint8_t* dst = a.scratch + a.raw_off[i];
+        if (!snappy_block(src, len, dst, a.raw_len[i])) {
+            a.status[i] = kStUndecodable;
+            return;
+        }
+        src = dst;
+        len = a.raw_len[i];
+    }
+    const uint8_t* nm;
+    uint32_t nl;
+    const int r = parse_record(a, i, src, len, &nm, &nl);
+    if (r < 0) return;
+    if (r) publish_name(a, i, nm, nl);
+    a.keep[i] = 1u;
+}
+
+// D2 (LDS): one wave per 64 consecutive fragments. Their compressed bytes are one contiguous range
+// of the input: copied into LDS with 16-B loads, decompressed into LDS, parsed from LDS (every
+// dependent byte read is an LDS round trip instead of an L1/L2 one). A wave whose bytes do not fit
+// marks its fragments deferred for the global-memory kernel. Service names are copied out to the
+// global scratch (the dictionary kernels read them after this kernel).
+constexpr uint32_t kLdsWG = 64;
+constexpr uint32_t kInCap = 16384;
+constexpr uint32_t kOutCap = 24576;
+__global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
+    __shared__ __align__(16) uint8_t s_in[kInCap + 16];
+    __shared__ __align__(16) uint8_t s_out[kOutCap];
+    const uint64_t i0 = (uint64_t)blockIdx.x * kLdsWG;
+    const uint64_t i1 = i0 + kLdsWG < a.n ? i0 + kLdsWG : a.n;
+    const uint64_t i = i0 + threadIdx.x;
+    const uint64_t b0 = a.offsets[i0], b1 = a.offsets[i1];
+    // 16-B aligned blocks of absolute addresses: a block holding a valid byte never crosses a page
+    const uint8_t* gstart = (const uint8_t*)((uintptr_t)(a.buf + b0) & ~(uintptr_t)15);
+    const uint64_t span = b1 >= b0 ? (uint64_t)((a.buf + b1) - gstart) : ~0ull;
+    const uint64_t r0 = a.snappy ? a.raw_off[i0] : 0, r1 = a.snappy ? a.raw_off[i1] : 0;
+    const bool fits = span <= kInCap && r1 - r0 <= kOutCap;
+    if (!fits) {  // uniform
+        if (i < i1) {
+            a.keep[i] = 0u;
+            a.svc_hash[i] = 0ull;
+            if (a.status[i] == kStOk) a.status[i] = kStDefer;
+        }
+        return;
+    }
+    // cooperative copy of the aligned blocks covering [b0, b1)
+    const uint64_t nchunk = (span + 15) >> 4;
+    for (uint64_t c = threadIdx.x; c < nchunk; c += kLdsWG)
+        *reinterpret_cast<uint4*>(s_in + 16 * c) = *reinterpret_cast<const uint4*>(gstart + 16 * c);
+    __syncthreads();
+    if (i >= i1) return;
+    a.keep[i] = 0u;
+    a.svc_hash[i] = 0ull;
+    if (a.status[i] != kStOk) return;
+    const uint64_t b = a.offsets[i], e = a.offsets[i + 1];
+    const uint8_t* src = s_in + ((a.buf + b) - gstart);
+    uint64_t len = e - b;
+    uint8_t* dst = nullptr;
+    if (a.snappy) {
+        dst = s_out + (a.raw_off[i] - r0);
+        if (!snappy_block(src, len, dst, a.raw_len[i])) {
+            a.status[i] = kStUndecodable;
+            return;
+        }
+        src = dst;
+        len = a.raw_len[i];
+    }
+    const uint8_t* nm;
+    uint32_t nl;
+    const int r = parse_record(a, i, src, len, &nm, &nl);
+    if (r < 0) return;
+    if (r) {
+        if (nm != a.unknown) {  // the name lies in this lane's own bytes: [src, src + len)
+            const uint64_t off = (uint64_t)((uintptr_t)nm - (uintptr_t)src);
+            if (a.snappy) {
+                uint8_t* g = a.scratch + a.raw_off[i] + off;  // copy it out to the scratch
+                for (uint32_t q = 0; q < nl; ++q) g[q] = nm[q];
+                nm = g;
+            } else {
+                nm = a.buf + b + off;  // thrift codec: the name is in the input buffer
+            }
+        }
+        publish_name(a, i, nm, nl);
     }
     a.keep[i] = 1u;
 }
@@ -724,7 +814,8 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     }
     a.scratch = g->scratch;
     // D2, D3
-    hipLaunchKernelGGL(k_ing_decode, grid, blk, 0, s, a);
+    hipLaunchKernelGGL(k_ing_decode_lds, dim3((unsigned)((n + kLdsWG - 1) / kLdsWG)), dim3(kLdsWG), 0, s, a);
+    hipLaunchKernelGGL(k_ing_decode, grid, blk, 0, s, a, 1u);  // the deferred waves
     hipLaunchKernelGGL(k_ing_dict_insert, grid, blk, 0, s, a);
     ING_HIP(g, hipGetLastError());
     // ids for new slots, in slot order; their names into the device arena
