@@ -172,6 +172,57 @@ struct DRd {
     }
 };
 
+// The generic skip out of line (nested containers are rare in stored spans): keeps its stack and
+// switch out of the decoders' register budget. DRd travels by value, so nothing goes to scratch.
+__device__ __noinline__ DRd skip_call(DRd r, uint8_t t) {
+    r.skip(t);
+    return r;
+}
+
+// skip one value: fixed-width fields and strings inline, anything else through skip_call
+__device__ __forceinline__ void skip_flat(DRd& r, uint8_t t) {
+    uint32_t w = 0;
+    switch (t) {
+        case T_BOOL:
+        case T_BYTE: w = 1; break;
+        case T_I16: w = 2; break;
+        case T_I32: w = 4; break;
+        case T_DOUBLE:
+        case T_I64: w = 8; break;
+        case T_STRING: {
+            const int32_t l = r.i32();
+            if (!r.ok || l < 0 || !r.need((uint64_t)l)) {
+                r.ok = false;
+                return;
+            }
+            r.p += l;
+            return;
+        }
+        default: r = skip_call(r, t); return;
+    }
+    if (r.need(w)) r.p += w;
+}
+
+// skip a struct whose fields are flat or flat structs (BinaryAnnotation with its Endpoint host)
+__device__ __forceinline__ void skip_struct2(DRd& r) {
+    for (;;) {
+        const uint8_t t = r.u8();
+        if (!r.ok || t == T_STOP) return;
+        r.i16();
+        if (t != T_STRUCT) {
+            skip_flat(r, t);
+            continue;
+        }
+        for (;;) {
+            const uint8_t u = r.u8();
+            if (!r.ok || u == T_STOP) break;
+            r.i16();
+            skip_flat(r, u);
+        }
+        if (!r.ok) return;
+    }
+}
+
 __device__ __forceinline__ bool snappy_hdr(const uint8_t* in, uint64_t n, uint64_t* len, uint64_t* hdr) {
     uint64_t v = 0;
     for (uint64_t i = 0; i < n && i < 5; ++i) {
@@ -204,7 +255,15 @@ __device__ __forceinline__ bool snappy_block(const uint8_t* in, uint64_t n, uint
             }
             l += 1;
             if (i + l > n || o + l > len) return false;
-            for (uint64_t k = 0; k < l; ++k) out[o + k] = in[i + k];
+            uint64_t k = 0;
+            for (; k + 4 <= l; k += 4) {
+                const uint8_t x0 = in[i + k], x1 = in[i + k + 1], x2 = in[i + k + 2], x3 = in[i + k + 3];
+                out[o + k] = x0;
+                out[o + k + 1] = x1;
+                out[o + k + 2] = x2;
+                out[o + k + 3] = x3;
+            }
+            for (; k < l; ++k) out[o + k] = in[i + k];
             i += l;
             o += l;
             continue;
@@ -227,7 +286,18 @@ __device__ __forceinline__ bool snappy_block(const uint8_t* in, uint64_t n, uint
             i += 4;
         }
         if (off == 0 || off > o || o + l > len) return false;
-        for (uint64_t k = 0; k < l; ++k) out[o + k] = out[o - off + k];  // may overlap: bytewise
+        uint64_t k = 0;
+        if (off >= 4) {  // a 4-byte step never reads what it writes
+            for (; k + 4 <= l; k += 4) {
+                const uint8_t* q = out + o - off + k;
+                const uint8_t x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
+                out[o + k] = x0;
+                out[o + k + 1] = x1;
+                out[o + k + 2] = x2;
+                out[o + k + 3] = x3;
+            }
+        }
+        for (; k < l; ++k) out[o + k] = out[o - off + k];  // overlapping tail: bytewise
         o += l;
     }
     return o == len;
@@ -302,7 +372,7 @@ __device__ __forceinline__ void read_endpoint(DRd& r, const uint8_t** name, uint
         if (id == 3 && t == T_STRING)
             r.str(name, nlen);
         else
-            r.skip(t);
+            skip_flat(r, t);
     }
 }
 
@@ -342,7 +412,7 @@ __device__ __forceinline__ int parse_record(const IngArgs& a, uint64_t i, const 
                 break;
             }
             if (et != T_STRUCT) {
-                for (int32_t q = 0; r.ok && q < cntl; ++q) r.skip(et);
+                for (int32_t q = 0; r.ok && q < cntl; ++q) skip_flat(r, et);
                 continue;
             }
             for (int32_t q = 0; r.ok && q < cntl; ++q) {
@@ -365,7 +435,7 @@ __device__ __forceinline__ int parse_record(const IngArgs& a, uint64_t i, const 
                         host = true;
                         read_endpoint(r, &hn, &hl);
                     } else
-                        r.skip(at);
+                        skip_flat(r, at);
                 }
                 if (!r.ok) break;
                 if (ts <= 0 || (v && vl == 0)) invalid = true;  // thrift.scala:66-71
@@ -389,8 +459,19 @@ __device__ __forceinline__ int parse_record(const IngArgs& a, uint64_t i, const 
                     }
                 }
             }
+        } else if (t == T_LIST) {  // binary_annotations (fid 8) and any other list
+            const uint8_t et = r.u8();
+            const int32_t cntl = r.i32();
+            if (!r.ok || cntl < 0) {
+                r.ok = false;
+                break;
+            }
+            if (et == T_STRUCT)
+                for (int32_t q = 0; r.ok && q < cntl; ++q) skip_struct2(r);
+            else
+                for (int32_t q = 0; r.ok && q < cntl; ++q) skip_flat(r, et);
         } else {
-            r.skip(t);
+            skip_flat(r, t);
         }
         if (!r.ok) break;
     }
