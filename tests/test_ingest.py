@@ -417,8 +417,8 @@ def test_device_decoder_large_fragments_take_the_global_path(gpu, snappy):
     spans = gen_traces(77, 300, max_depth=5, anomalies=0.2)
     out = []
     for k, s in enumerate(spans):
-        if k % 97 == 5 or 640 <= k < 704:  # isolated giants, and one whole wave of mid-size ones
-            size = 20000 if k % 97 == 5 else 700
+        if k % 97 == 5 or k % 89 == 7 or 640 <= k < 704:  # giants, near-budget ones, a run of mid-size ones
+            size = 24000 if k % 97 == 5 else 18000 if k % 89 == 7 else 700
             pad = BinaryAnnotation("blob", bytes(rnd.getrandbits(8) for _ in range(size)), "BYTES", None)
             s = dataclasses.replace(s, binary_annotations=s.binary_annotations + (pad,))
         out.append(s)
@@ -428,6 +428,57 @@ def test_device_decoder_large_fragments_take_the_global_path(gpu, snappy):
     dd = DeviceSpanDecoder(64)
     dcols, drej = dd.decode(blobs, snappy=snappy, strict=False)
     assert drej == hrej
+    assert _named(dcols.to_host(), dd.service_names()) == _named(hcols, hd.service_names())
+
+
+def _snappy_runs_then_literals(data: bytes) -> bytes:
+    """A legal Snappy block no standard compressor writes: runs of one byte as a literal plus
+    64-byte copies (offset 1), every other byte as its own 1-byte literal. After a long run the
+    output is far ahead of the input, and the literal tail then eats into that lead, so in-place
+    decompression must stop before it overwrites input it has not read."""
+    out = bytearray()
+    n = len(data)
+    while True:  # varint length
+        b = n & 0x7F
+        n >>= 7
+        out.append(b | (0x80 if n else 0))
+        if not n:
+            break
+    i = 0
+    while i < len(data):
+        j = i
+        while j < len(data) and data[j] == data[i]:
+            j += 1
+        out += bytes([0, data[i]])  # 1-byte literal
+        run = j - i - 1
+        while run >= 4:
+            ln = min(64, run)
+            out += bytes([((ln - 1) << 2) | 2, 1, 0])  # copy-2, offset 1
+            run -= ln
+        for _ in range(run):
+            out += bytes([0, data[i]])
+        i = j
+    return bytes(out)
+
+
+@pytest.mark.gpu
+def test_device_decoder_unsafe_in_place_streams(gpu):
+    from zipkin_amd.ingest import DeviceSpanDecoder
+
+    spans = gen_traces(78, 120, max_depth=4)
+    raw = []
+    for k, s in enumerate(spans):
+        if k % 3 == 0:  # a long run early in the span, then hundreds of single-byte literals
+            run = BinaryAnnotation("fill", b"a" * (3000 + 50 * (k % 7)), "BYTES", None)
+            s = Span(s.trace_id, s.name, s.id, s.parent_id, s.annotations, (run,) + s.binary_annotations, s.debug)
+        raw.append(T.span(s))
+    blobs = [_snappy_runs_then_literals(b) for b in raw]
+    assert all(snappy_uncompress(c) == b for c, b in zip(blobs, raw))
+    hd = SpanDecoder()
+    hcols, hrej = hd.decode(blobs)
+    dd = DeviceSpanDecoder(64)
+    dcols, drej = dd.decode(blobs)
+    assert drej == hrej == 0
     assert _named(dcols.to_host(), dd.service_names()) == _named(hcols, hd.service_names())
 
 

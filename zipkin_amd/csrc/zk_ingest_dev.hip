@@ -550,74 +550,183 @@ __global__ __launch_bounds__(kIngWG) void k_ing_decode(IngArgs a, uint32_t defer
     a.keep[i] = 1u;
 }
 
-// D2 (LDS): one wave per 64 consecutive fragments. Their compressed bytes are one contiguous range
-// of the input: copied into LDS with 16-B loads, decompressed into LDS, parsed from LDS (every
-// dependent byte read is an LDS round trip instead of an L1/L2 one). A wave whose bytes do not fit
-// marks its fragments deferred for the global-memory kernel. Service names are copied out to the
+// D2 (LDS): one wave per block of kLdsBlock consecutive fragments, in rounds. A round takes the
+// next fragments (at most 64, one per lane) whose LDS regions fit the wave's kLdsBudget bytes. A
+// lane's region holds its decompressed Span at the front and its compressed bytes at the back
+// (copied in with aligned 16-B loads): Snappy decompresses in place, front to back, and a step
+// that would write over input not yet read defers the fragment instead (checked per element, so it
+// never corrupts). The Span is then parsed from LDS (every dependent byte read is an LDS round trip
+// instead of an L1/L2 one). At 20 KiB per wave, 8 waves fit a CU (separate in/out buffers for 64
+// fragments needed 40 KiB: one wave per SIMD). Deferred fragments (a region larger than the budget,
+// or an unsafe in-place step) go to the global-memory kernel. Service names are copied out to the
 // global scratch (the dictionary kernels read them after this kernel).
 constexpr uint32_t kLdsWG = 64;
-constexpr uint32_t kInCap = 16384;
-constexpr uint32_t kOutCap = 24576;
-__global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
-    __shared__ __align__(16) uint8_t s_in[kInCap + 16];
-    __shared__ __align__(16) uint8_t s_out[kOutCap];
-    const uint64_t i0 = (uint64_t)blockIdx.x * kLdsWG;
-    const uint64_t i1 = i0 + kLdsWG < a.n ? i0 + kLdsWG : a.n;
-    const uint64_t i = i0 + threadIdx.x;
-    const uint64_t b0 = a.offsets[i0], b1 = a.offsets[i1];
-    // 16-B aligned blocks of absolute addresses: a block holding a valid byte never crosses a page
-    const uint8_t* gstart = (const uint8_t*)((uintptr_t)(a.buf + b0) & ~(uintptr_t)15);
-    const uint64_t span = b1 >= b0 ? (uint64_t)((a.buf + b1) - gstart) : ~0ull;
-    const uint64_t r0 = a.snappy ? a.raw_off[i0] : 0, r1 = a.snappy ? a.raw_off[i1] : 0;
-    const bool fits = span <= kInCap && r1 - r0 <= kOutCap;
-    if (!fits) {  // uniform
-        if (i < i1) {
-            a.keep[i] = 0u;
-            a.svc_hash[i] = 0ull;
-            if (a.status[i] == kStOk) a.status[i] = kStDefer;
+constexpr uint32_t kLdsBudget = 20480;
+constexpr uint32_t kLdsBlock = 1024;
+constexpr uint32_t kLdsSlack = 64;  // region bytes beyond max(raw, compressed): in-place headroom + alignment
+
+// Snappy block from in = out + D (the same region), in place: false with *unsafe set when a step
+// would write over input bytes not yet read.
+__device__ __forceinline__ bool snappy_inplace(uint8_t* out, uint64_t D, uint64_t n, uint64_t len, bool* unsafe) {
+    const uint8_t* in = out + D;
+    uint64_t dl, hdr;
+    if (!snappy_hdr(in, n, &dl, &hdr) || dl != len) return false;
+    uint64_t o = 0, i = hdr;
+    while (i < n) {
+        const uint8_t tag = in[i++];
+        uint64_t l, off;
+        const uint32_t kind = tag & 3;
+        if (kind == 0) {
+            l = tag >> 2;
+            if (l >= 60) {
+                const uint32_t nb = (uint32_t)l - 59;
+                if (i + nb > n) return false;
+                l = 0;
+                for (uint32_t k = 0; k < nb; ++k) l |= (uint64_t)in[i + k] << (8 * k);
+                i += nb;
+            }
+            l += 1;
+            if (i + l > n || o + l > len) return false;
+            if (o > D + i) {  // output byte o + k is written after input byte i + k + 3 is read
+                *unsafe = true;
+                return false;
+            }
+            uint64_t k = 0;
+            for (; k + 4 <= l; k += 4) {
+                const uint8_t x0 = in[i + k], x1 = in[i + k + 1], x2 = in[i + k + 2], x3 = in[i + k + 3];
+                out[o + k] = x0;
+                out[o + k + 1] = x1;
+                out[o + k + 2] = x2;
+                out[o + k + 3] = x3;
+            }
+            for (; k < l; ++k) out[o + k] = in[i + k];
+            i += l;
+            o += l;
+            continue;
         }
-        return;
-    }
-    // cooperative copy of the aligned blocks covering [b0, b1)
-    const uint64_t nchunk = (span + 15) >> 4;
-    for (uint64_t c = threadIdx.x; c < nchunk; c += kLdsWG)
-        *reinterpret_cast<uint4*>(s_in + 16 * c) = *reinterpret_cast<const uint4*>(gstart + 16 * c);
-    __syncthreads();
-    if (i >= i1) return;
-    a.keep[i] = 0u;
-    a.svc_hash[i] = 0ull;
-    if (a.status[i] != kStOk) return;
-    const uint64_t b = a.offsets[i], e = a.offsets[i + 1];
-    const uint8_t* src = s_in + ((a.buf + b) - gstart);
-    uint64_t len = e - b;
-    uint8_t* dst = nullptr;
-    if (a.snappy) {
-        dst = s_out + (a.raw_off[i] - r0);
-        if (!snappy_block(src, len, dst, a.raw_len[i])) {
-            a.status[i] = kStUndecodable;
-            return;
+        if (kind == 1) {
+            if (i + 1 > n) return false;
+            l = ((tag >> 2) & 7) + 4;
+            off = ((uint64_t)(tag >> 5) << 8) | in[i];
+            i += 1;
+        } else if (kind == 2) {
+            if (i + 2 > n) return false;
+            l = (tag >> 2) + 1;
+            off = (uint64_t)in[i] | ((uint64_t)in[i + 1] << 8);
+            i += 2;
+        } else {
+            if (i + 4 > n) return false;
+            l = (tag >> 2) + 1;
+            off = (uint64_t)in[i] | ((uint64_t)in[i + 1] << 8) | ((uint64_t)in[i + 2] << 16) |
+                  ((uint64_t)in[i + 3] << 24);
+            i += 4;
         }
-        src = dst;
-        len = a.raw_len[i];
-    }
-    const uint8_t* nm;
-    uint32_t nl;
-    const int r = parse_record(a, i, src, len, &nm, &nl);
-    if (r < 0) return;
-    if (r) {
-        if (nm != a.unknown) {  // the name lies in this lane's own bytes: [src, src + len)
-            const uint64_t off = (uint64_t)((uintptr_t)nm - (uintptr_t)src);
-            if (a.snappy) {
-                uint8_t* g = a.scratch + a.raw_off[i] + off;  // copy it out to the scratch
-                for (uint32_t q = 0; q < nl; ++q) g[q] = nm[q];
-                nm = g;
-            } else {
-                nm = a.buf + b + off;  // thrift codec: the name is in the input buffer
+        if (off == 0 || off > o || o + l > len) return false;
+        if (o + l > D + i) {  // the copy would reach the next unread input byte
+            *unsafe = true;
+            return false;
+        }
+        uint64_t k = 0;
+        if (off >= 4) {  // a 4-byte step never reads what it writes
+            for (; k + 4 <= l; k += 4) {
+                const uint8_t* q = out + o - off + k;
+                const uint8_t x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
+                out[o + k] = x0;
+                out[o + k + 1] = x1;
+                out[o + k + 2] = x2;
+                out[o + k + 3] = x3;
             }
         }
-        publish_name(a, i, nm, nl);
+        for (; k < l; ++k) out[o + k] = out[o - off + k];  // overlapping tail: bytewise
+        o += l;
     }
-    a.keep[i] = 1u;
+    return o == len;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(v, d);
+        if ((int)(threadIdx.x & 63) >= d) v += o;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
+    __shared__ __align__(16) uint8_t s_buf[kLdsBudget];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t blk0 = (uint64_t)blockIdx.x * kLdsBlock;
+    const uint64_t blk1 = blk0 + kLdsBlock < a.n ? blk0 + kLdsBlock : a.n;
+    for (uint64_t f0 = blk0; f0 < blk1;) {  // uniform
+        const uint64_t i = f0 + lane;
+        const bool have = i < blk1;
+        uint64_t b = 0, clen = 0, raw = 0;
+        uint32_t need = 0;
+        uint8_t st = kStInvalid;
+        if (have) {
+            st = a.status[i];
+            b = a.offsets[i];
+            clen = a.offsets[i + 1] - b;  // (not monotone offsets were marked undecodable by D1)
+            raw = a.snappy ? a.raw_len[i] : 0;
+            const uint64_t r = ((raw > clen ? raw : clen) + kLdsSlack + 15) & ~15ull;
+            need = st == kStOk ? (r > kLdsBudget ? kLdsBudget + 1 : (uint32_t)r) : 0u;
+        }
+        const uint32_t incl = wave_incl_scan(need);
+        // this round: the longest prefix of lanes that fits (at least lane 0, to make progress)
+        uint32_t k = (uint32_t)__popcll(__ballot(have && incl <= kLdsBudget));
+        if (k == 0) k = 1;  // lane 0 alone does not fit: deferred below
+        if (lane < k && have) {
+            a.keep[i] = 0u;
+            a.svc_hash[i] = 0ull;
+            if (st == kStOk && incl > kLdsBudget) {
+                a.status[i] = kStDefer;
+            } else if (st == kStOk) {
+                const uint32_t R = need, R0 = incl - need;
+                const uint32_t mis = (uint32_t)((uintptr_t)(a.buf + b) & 15u);
+                // input at offset D of the region (D = mis mod 16): its aligned 16-B blocks cover
+                // [D - mis, D + clen + 15] inside [0, R) since R >= clen + kLdsSlack
+                const uint32_t D = ((R - 16u - (uint32_t)clen - mis) & ~15u) + mis;
+                uint8_t* reg = s_buf + R0;
+                const uint4* g = reinterpret_cast<const uint4*>((uintptr_t)(a.buf + b) & ~(uintptr_t)15);
+                const uint32_t nblk = (uint32_t)((clen + mis + 15) >> 4);
+                uint4* dst = reinterpret_cast<uint4*>(reg + D - mis);
+                for (uint32_t c = 0; c < nblk; ++c) dst[c] = g[c];
+                const uint8_t* src = reg + D;
+                uint64_t len = clen;
+                bool ok = true, unsafe = false;
+                if (a.snappy) {
+                    ok = snappy_inplace(reg, D, clen, raw, &unsafe);
+                    src = reg;
+                    len = raw;
+                }
+                if (!ok) {
+                    a.status[i] = unsafe ? kStDefer : kStUndecodable;
+                } else {
+                    const uint8_t* nm;
+                    uint32_t nl;
+                    const int r = parse_record(a, i, src, len, &nm, &nl);
+                    if (r >= 0) {
+                        if (r) {
+                            if (nm != a.unknown) {  // the name lies in this lane's own bytes
+                                const uint64_t off = (uint64_t)((uintptr_t)nm - (uintptr_t)src);
+                                if (a.snappy) {
+                                    uint8_t* gd = a.scratch + a.raw_off[i] + off;  // copy out to the scratch
+                                    for (uint32_t q = 0; q < nl; ++q) gd[q] = nm[q];
+                                    nm = gd;
+                                } else {
+                                    nm = a.buf + b + off;  // thrift codec: the name is in the input buffer
+                                }
+                            }
+                            publish_name(a, i, nm, nl);
+                        }
+                        a.keep[i] = 1u;
+                    }
+                }
+            }
+        }
+        f0 += k;
+        __syncthreads();  // one wave: this round's LDS accesses complete before the next round's copies
+    }
 }
 
 __global__ __launch_bounds__(kIngWG) void k_ing_dict_insert(IngArgs a) {
@@ -895,7 +1004,7 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     }
     a.scratch = g->scratch;
     // D2, D3
-    hipLaunchKernelGGL(k_ing_decode_lds, dim3((unsigned)((n + kLdsWG - 1) / kLdsWG)), dim3(kLdsWG), 0, s, a);
+    hipLaunchKernelGGL(k_ing_decode_lds, dim3((unsigned)((n + kLdsBlock - 1) / kLdsBlock)), dim3(kLdsWG), 0, s, a);
     hipLaunchKernelGGL(k_ing_decode, grid, blk, 0, s, a, 1u);  // the deferred waves
     hipLaunchKernelGGL(k_ing_dict_insert, grid, blk, 0, s, a);
     ING_HIP(g, hipGetLastError());
