@@ -550,6 +550,28 @@ __global__ __launch_bounds__(kIngWG) void k_ing_decode(IngArgs a, uint32_t defer
     a.keep[i] = 1u;
 }
 
+// A name the dictionary already holds (an id assigned by an earlier batch) resolves right here:
+// the slot of its hash, its bytes compared exactly with the arena's. svc_hash stays 0, so D3/D4
+// skip the fragment. Anything else (a new name, a hash collision, an id out of range) is published
+// for D3/D4, which decide it as before.
+__device__ __forceinline__ bool try_resolve(const IngArgs& a, uint64_t i, const uint8_t* nm, uint32_t nl, uint64_t h) {
+    uint32_t slot = (uint32_t)h & a.d_mask;
+    for (uint32_t step = 0; step <= a.d_mask; ++step) {
+        const uint64_t k = a.d_key[slot];
+        if (k == kEmpty) return false;
+        if (k == h) break;
+        slot = (slot + 1) & a.d_mask;
+    }
+    if (a.d_key[slot] != h) return false;
+    const uint32_t id = a.d_id[slot];
+    if (id == kNoId || id >= a.max_services || a.d_len[slot] != nl) return false;
+    const uint8_t* y = (const uint8_t*)(uintptr_t)a.d_ptr[slot];
+    for (uint32_t q = 0; q < nl; ++q)
+        if (nm[q] != y[q]) return false;
+    a.svc[i] = id;
+    return true;
+}
+
 // D2 (LDS): one wave per block of kLdsBlock consecutive fragments, in rounds. A round takes the
 // next fragments (at most 64, one per lane) whose LDS regions fit the wave's kLdsBudget bytes. A
 // lane's region holds its decompressed Span at the front and its compressed bytes at the back
@@ -706,7 +728,7 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                     uint32_t nl;
                     const int r = parse_record(a, i, src, len, &nm, &nl);
                     if (r >= 0) {
-                        if (r) {
+                        if (r && !try_resolve(a, i, nm, nl, d_hash(nm, nl))) {
                             if (nm != a.unknown) {  // the name lies in this lane's own bytes
                                 const uint64_t off = (uint64_t)((uintptr_t)nm - (uintptr_t)src);
                                 if (a.snappy) {
@@ -736,6 +758,12 @@ __global__ __launch_bounds__(kIngWG) void k_ing_dict_insert(IngArgs a) {
     if (!h) return;
     uint32_t slot = (uint32_t)h & a.d_mask;
     for (uint32_t step = 0; step <= a.d_mask; ++step) {
+        const uint64_t seen = a.d_key[slot];  // read first: after the first batches every name is there
+        if (seen == h) return;
+        if (seen != kEmpty) {
+            slot = (slot + 1) & a.d_mask;
+            continue;
+        }
         const unsigned long long old = atomicCAS((unsigned long long*)&a.d_key[slot], (unsigned long long)kEmpty,
                                                  (unsigned long long)h);
         if (old == kEmpty) {  // the first claimant names the slot (verified against the others in D4)
