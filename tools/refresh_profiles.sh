@@ -18,6 +18,7 @@ step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 250 python bench.py
 step bench_c4 250 python bench.py --workload c4
 step bench_c5 250 python bench.py --workload c5
+step bench_ingest 250 python bench.py --workload ingest
 step prof 250 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --cpu-sample 0
 rm -rf gpurun_out/pmc
 step pmc 300 bash tools/pmc.sh FETCH_SIZE WRITE_SIZE
