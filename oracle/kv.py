@@ -5,8 +5,9 @@ checker. It restates, in numpy, what include/zksketch.h promises for
 Aggregates.getTopKeyValueAnnotations (zipkin-common/.../storage/Aggregates.scala:34):
 
   * per service a count-min sketch (Cormode & Muthukrishnan 2005) of `depth` rows x `width`
-    counters; row r of key k is the top log2(width) bits of mix64(k ^ seed_r) with
-    seed_r = mix64(seed + 0x9E3779B97F4A7C15 * (r + 1)) and mix64 the splitmix64 finalizer;
+    counters; with h = mix64(k ^ seed_0), seed_0 = mix64(seed + 0x9E3779B97F4A7C15) and mix64 the
+    splitmix64 finalizer, row r of key k is the top log2(width) bits of the 32-bit
+    h1 + r * h2 (h1 = low half of h, h2 = high half | 1: double hashing, Kirsch & Mitzenmacher);
   * per service the best `candidates` keys, ordered by (estimate desc, key asc); after every
     batch the list is the best among (previous list U this batch's distinct keys), all estimated
     with the counters including the batch.
@@ -60,8 +61,13 @@ class KvOracle:
     def rows(self, keys: np.ndarray) -> np.ndarray:
         """[depth, n] counter index of every key in every row."""
         keys = np.asarray(keys, dtype=np.uint64)
-        return np.stack([(mix64(keys ^ np.uint64(s)) >> np.uint64(64 - self.wbits)).astype(np.int64)
-                         for s in self.seeds])
+        h = mix64(keys ^ np.uint64(self.seeds[0]))
+        h1 = h & np.uint64(0xFFFFFFFF)
+        h2 = (h >> np.uint64(32)) | np.uint64(1)
+        sh = np.uint64(32 - self.wbits)
+        with np.errstate(over="ignore"):
+            return np.stack([(((h1 + np.uint64(r) * h2) & np.uint64(0xFFFFFFFF)) >> sh).astype(np.int64)
+                             for r in range(self.depth)])
 
     def estimate(self, service: int, keys) -> np.ndarray:
         keys = np.asarray(keys, dtype=np.uint64)

@@ -22,23 +22,44 @@ namespace zk {
 namespace {
 
 constexpr int kKvWG = 256;
-constexpr uint32_t kSetCap = 2048;  // LDS hash-set slots (load <= 0.5)
+constexpr uint32_t kSetCap = 2048;  // 2^11: RowHash.set is 11 bits  // LDS hash-set slots (load <= 0.5)
 constexpr uint32_t kSortCap = 1024; // compaction sort buffer
 constexpr uint32_t kRound = 2 * kKvWG;
+constexpr int kPrefetch = 8;        // candidate rounds of keys in flight per thread
 constexpr uint64_t kEmptyKey = ~0ull;
 
 __device__ __forceinline__ bool beats(uint32_t e1, uint64_t k1, uint32_t e2, uint64_t k2) {
     return e1 > e2 || (e1 == e2 && k1 < k2);
 }
 
-__device__ __forceinline__ uint32_t row_index(uint64_t key, uint64_t seed, uint32_t wbits) {
-    return (uint32_t)(sk_mix64(key ^ seed) >> (64 - wbits));
-}
+// Row indices of a key: ONE splitmix64 of (key ^ seed_0), split into h1 (low half) and h2 (high
+// half, odd); row r uses the top log2(width) bits of h1 + r * h2 (mod 2^32) -- double hashing
+// (Kirsch & Mitzenmacher 2006), so a key costs one 64-bit mix instead of one per row, and the next
+// row's index is one 32-bit add away.
+struct RowHash {
+    uint32_t x, h2, sh, set;  // set: the key's first slot in a workgroup's candidate hash set
+    RowHash() = default;
+    __device__ __forceinline__ RowHash(uint64_t key, uint64_t seed, uint32_t wbits) {
+        const uint64_t h = sk_mix64(key ^ seed);
+        set = (uint32_t)(h >> 53);  // top 11 bits (kSetCap = 2^11)
+        x = (uint32_t)h;
+        h2 = (uint32_t)(h >> 32) | 1u;
+        sh = 32u - wbits;
+    }
+    __device__ __forceinline__ uint32_t next() {  // index in the current row, then advance a row
+        const uint32_t i = x >> sh;
+        x += h2;
+        return i;
+    }
+};
 
-__device__ __forceinline__ uint32_t estimate(const uint32_t* cm, const KvArgs& a, uint64_t key) {
+__device__ __forceinline__ uint32_t estimate_rh(const uint32_t* cm, const KvArgs& a, RowHash rh) {
     uint32_t e = 0xFFFFFFFFu;
-    for (uint32_t r = 0; r < a.depth; ++r) e = min(e, cm[r * a.width + row_index(key, a.seeds[r], a.wbits)]);
+    for (uint32_t r = 0; r < a.depth; ++r) e = min(e, cm[r * a.width + rh.next()]);
     return e;
+}
+__device__ __forceinline__ uint32_t estimate(const uint32_t* cm, const KvArgs& a, uint64_t key) {
+    return estimate_rh(cm, a, RowHash(key, a.seeds[0], a.wbits));
 }
 
 // Distinct (key, estimate) set keeping the best `keep` entries (estimate desc, key asc).
@@ -48,6 +69,7 @@ struct TopSet {
     uint64_t sk[kSortCap];
     uint32_t se[kSortCap];
     uint32_t count, gcount;
+    uint32_t pending[2];  // survivors of the current block (candidates kernel), by block parity
     uint32_t has_thr, thr_est;
     uint64_t thr_key;
     uint32_t special, special_est;  // the key equal to the empty sentinel
@@ -63,7 +85,7 @@ __device__ void ts_init(TopSet& t) {
     __syncthreads();
 }
 
-__device__ __forceinline__ void ts_insert(TopSet& t, uint64_t key, uint32_t est) {
+__device__ __forceinline__ void ts_insert(TopSet& t, uint64_t key, uint32_t est, uint32_t slot) {
     if (key == kEmptyKey) {
         if (atomicCAS(&t.special, 0u, 1u) == 0u) {
             t.special_est = est;
@@ -71,24 +93,44 @@ __device__ __forceinline__ void ts_insert(TopSet& t, uint64_t key, uint32_t est)
         }
         return;
     }
-    uint32_t slot = (uint32_t)sk_mix64(key ^ 0x2545F4914F6CDD1Dull) & (kSetCap - 1);
+    // Read before CAS: the heavy keys (the ones that keep beating the threshold, i.e. most offers
+    // under a skewed key distribution) are already in the set, and a CAS on their slot from many
+    // lanes at once serialises. Slots only go empty -> key between compactions, so a plain read
+    // that shows the key (or another key) is final; one that shows empty is settled by the CAS.
     for (;;) {
-        const unsigned long long old =
-            atomicCAS((unsigned long long*)&t.hk[slot], (unsigned long long)kEmptyKey, (unsigned long long)key);
-        if (old == kEmptyKey) {
-            t.he[slot] = est;
-            atomicAdd(&t.count, 1u);
-            return;
+        const uint64_t cur = __hip_atomic_load(&t.hk[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (cur == key) return;
+        if (cur == kEmptyKey) {
+            const unsigned long long old =
+                atomicCAS((unsigned long long*)&t.hk[slot], (unsigned long long)kEmptyKey, (unsigned long long)key);
+            if (old == kEmptyKey) {
+                t.he[slot] = est;
+                atomicAdd(&t.count, 1u);
+                return;
+            }
+            if (old == key) return;
         }
-        if (old == key) return;
         slot = (slot + 1) & (kSetCap - 1);
     }
 }
 
-__device__ __forceinline__ void ts_offer(TopSet& t, uint64_t key, uint32_t est) {
+// read-only membership probe (the set only grows between compactions)
+__device__ __forceinline__ bool ts_contains(TopSet& t, uint64_t key, uint32_t slot) {
+    if (key == kEmptyKey) return __hip_atomic_load(&t.special, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u;
+    for (;;) {
+        const uint64_t cur = __hip_atomic_load(&t.hk[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (cur == key) return true;
+        if (cur == kEmptyKey) return false;
+        slot = (slot + 1) & (kSetCap - 1);
+    }
+}
+
+__device__ __forceinline__ uint32_t set_slot(uint64_t key, uint64_t seed) { return (uint32_t)(sk_mix64(key ^ seed) >> 53); }
+
+__device__ __forceinline__ void ts_offer(TopSet& t, uint64_t key, uint32_t est, uint32_t slot) {
     if (est == 0u) return;
     if (t.has_thr && !beats(est, key, t.thr_est, t.thr_key)) return;
-    ts_insert(t, key, est);
+    ts_insert(t, key, est, slot);
 }
 
 // gather + sort (best first) into sk/se; returns the number of entries. Clears the set.
@@ -146,7 +188,7 @@ __device__ uint32_t ts_sort(TopSet& t) {
 }
 
 // keep the best `keep`, raise the threshold when the kept set is full
-__device__ void ts_compact(TopSet& t, uint32_t keep) {
+__device__ void ts_compact(TopSet& t, uint32_t keep, uint64_t seed) {
     const uint32_t n = ts_sort(t);
     const uint32_t m = n < keep ? n : keep;
     if (threadIdx.x == 0 && m == keep && keep > 0) {
@@ -154,7 +196,7 @@ __device__ void ts_compact(TopSet& t, uint32_t keep) {
         t.thr_est = t.se[m - 1];
         t.thr_key = t.sk[m - 1];
     }
-    for (uint32_t x = threadIdx.x; x < m; x += kKvWG) ts_insert(t, t.sk[x], t.se[x]);
+    for (uint32_t x = threadIdx.x; x < m; x += kKvWG) ts_insert(t, t.sk[x], t.se[x], set_slot(t.sk[x], seed));
     __syncthreads();
 }
 
@@ -171,18 +213,27 @@ __device__ __forceinline__ uint32_t find_service(const uint32_t* __restrict__ un
     return lo;
 }
 
+// Unit u of service s: the service's run is cut into unit_base[s+1] - unit_base[s] equal parts
+// (at most unit_items keys each), so no unit is a small remainder.
+__device__ __forceinline__ void unit_range(const KvArgs& a, uint32_t s, uint32_t u, uint64_t* lo, uint64_t* hi) {
+    const uint64_t b = a.seg[s], e = a.seg[s + 1];
+    const uint64_t parts = a.unit_base[s + 1] - a.unit_base[s];
+    const uint64_t len = (e - b + parts - 1) / parts;
+    *lo = b + (uint64_t)(u - a.unit_base[s]) * len;
+    *hi = *lo + len < e ? *lo + len : e;
+}
+
 __global__ __launch_bounds__(kKvWG) void k_kv_sketch(KvArgs a) {
     extern __shared__ uint32_t cm[];
     const uint32_t u = blockIdx.x;
     if (u >= a.unit_base[a.S]) return;
     const uint32_t s = find_service(a.unit_base, a.S, u);
-    const uint64_t lo = a.seg[s] + (uint64_t)(u - a.unit_base[s]) * a.unit_items;
-    const uint64_t end = a.seg[s + 1];
-    const uint64_t hi = lo + a.unit_items < end ? lo + a.unit_items : end;
+    uint64_t lo, hi;
+    unit_range(a, s, u, &lo, &hi);
     const uint32_t cells = a.depth * a.width;
     for (uint32_t x = threadIdx.x; x < cells; x += kKvWG) cm[x] = 0u;
     __syncthreads();
-    constexpr int U = 4;
+    constexpr int U = 8;  // keys per thread in flight
     for (uint64_t b = lo; b < hi; b += (uint64_t)kKvWG * U) {
         uint64_t k[U];
 #pragma unroll
@@ -190,11 +241,14 @@ __global__ __launch_bounds__(kKvWG) void k_kv_sketch(KvArgs a) {
             const uint64_t i = b + (uint64_t)e * kKvWG + threadIdx.x;
             k[e] = a.keys[i < hi ? i : lo];
         }
+        // row hashes unconditionally, so the loads are not sunk into the conditional (see candidates)
+        RowHash rh[U];
+#pragma unroll
+        for (int e = 0; e < U; ++e) rh[e] = RowHash(k[e], a.seeds[0], a.wbits);
 #pragma unroll
         for (int e = 0; e < U; ++e) {
             if (b + (uint64_t)e * kKvWG + threadIdx.x < hi)
-                for (uint32_t r = 0; r < a.depth; ++r)
-                    atomicAdd(&cm[r * a.width + row_index(k[e], a.seeds[r], a.wbits)], 1u);
+                for (uint32_t r = 0; r < a.depth; ++r) atomicAdd(&cm[r * a.width + rh[e].next()], 1u);
         }
     }
     __syncthreads();
@@ -218,23 +272,66 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
     const uint32_t u = blockIdx.x;
     if (u >= a.unit_base[a.S]) return;
     const uint32_t s = find_service(a.unit_base, a.S, u);
-    const uint64_t lo = a.seg[s] + (uint64_t)(u - a.unit_base[s]) * a.unit_items;
-    const uint64_t end = a.seg[s + 1];
-    const uint64_t hi = lo + a.unit_items < end ? lo + a.unit_items : end;
+    uint64_t lo, hi;
+    unit_range(a, s, u, &lo, &hi);
     load_cm(cm, a, s);
     ts_init(t);  // contains the barrier that publishes cm
-    for (uint64_t b = lo; b < hi; b += kRound) {
-        uint64_t k[2];
+    // Blocks of J = 16 keys per thread (4096 per workgroup). All of a block's loads are issued
+    // together and nothing is carried across the loop's back edge (a register ring of prefetched
+    // keys makes the compiler copy it at the loop head, waiting for every load in flight). Per
+    // block: every key is estimated and filtered against the current threshold and the set
+    // (read-only probes: under a skewed key distribution most survivors are already in the set);
+    // the survivors are counted (B1) and, when they fit the sort buffer, inserted at once (B2) --
+    // two barriers per 4096 keys instead of one per 512. A block with too many survivors (the
+    // start of a unit) is inserted 256 at a time with a compaction check in between.
+    constexpr int J = 2 * kPrefetch;
+    uint32_t parity = 0;
+    if (threadIdx.x == 0) t.pending[0] = t.pending[1] = 0u;
+    __syncthreads();
+    for (uint64_t b = lo; b < hi; b += (uint64_t)kKvWG * J) {
+        uint64_t kq[J];
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const uint64_t i = b + (uint64_t)e * kKvWG + threadIdx.x;
-            k[e] = a.keys[i < hi ? i : lo];
+        for (int j = 0; j < J; ++j) {
+            const uint64_t i = b + (uint64_t)j * kKvWG + threadIdx.x;
+            kq[j] = a.keys[i < hi ? i : lo];
         }
+        // estimates unconditionally (clamped keys past the end are harmless): a load whose only
+        // uses sit in a conditional block is sunk into it, and then every key waits for HBM
+        uint32_t est[J], slot[J];
 #pragma unroll
-        for (int e = 0; e < 2; ++e)
-            if (b + (uint64_t)e * kKvWG + threadIdx.x < hi) ts_offer(t, k[e], estimate(cm, a, k[e]));
-        __syncthreads();
-        if (t.count > kSortCap - kRound) ts_compact(t, a.cand);
+        for (int j = 0; j < J; ++j) {
+            const RowHash rh(kq[j], a.seeds[0], a.wbits);
+            est[j] = estimate_rh(cm, a, rh);
+            slot[j] = rh.set;
+        }
+        const uint32_t has_thr = t.has_thr, thr_est = t.thr_est;
+        const uint64_t thr_key = t.thr_key;
+        uint32_t need = 0;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const bool live = b + (uint64_t)j * kKvWG + threadIdx.x < hi && est[j] != 0u &&
+                              (!has_thr || beats(est[j], kq[j], thr_est, thr_key));
+            if (live && !ts_contains(t, kq[j], slot[j])) need |= 1u << j;
+        }
+        if (need) atomicAdd(&t.pending[parity], (uint32_t)__popc(need));
+        __syncthreads();  // B1: survivors counted
+        if (threadIdx.x == 0) t.pending[parity ^ 1u] = 0u;  // the previous block's count: read by all before B1
+        const uint32_t pend = t.pending[parity];
+        if (t.count + pend > kSortCap && t.count > a.cand) ts_compact(t, a.cand, a.seeds[0]);
+        if (t.count + pend <= kSortCap) {
+#pragma unroll
+            for (int j = 0; j < J; ++j)
+                if (need & (1u << j)) ts_insert(t, kq[j], est[j], slot[j]);
+            __syncthreads();  // B2: the set and count are complete for the next block's filter
+        } else {
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                if (need & (1u << j)) ts_insert(t, kq[j], est[j], slot[j]);
+                __syncthreads();
+                if (t.count > kSortCap - kKvWG) ts_compact(t, a.cand, a.seeds[0]);
+            }
+        }
+        parity ^= 1u;
     }
     const uint32_t n = ts_sort(t);
     uint64_t* ok = a.unit_key + (uint64_t)u * a.cand;
@@ -276,10 +373,13 @@ __global__ __launch_bounds__(kKvWG) void k_kv_merge(KvArgs a, uint32_t use_units
                 key = a.extra_key[(l * a.S + s) * C + x];
                 old = a.extra_est[(l * a.S + s) * C + x];
             }
-            if (old) ts_offer(t, key, estimate(cm, a, key));
+            if (old) {
+                const RowHash rh(key, a.seeds[0], a.wbits);
+                ts_offer(t, key, estimate_rh(cm, a, rh), rh.set);
+            }
         }
         __syncthreads();
-        if (t.count > kSortCap - kRound) ts_compact(t, C);
+        if (t.count > kSortCap - kRound) ts_compact(t, C, a.seeds[0]);
     }
     const uint32_t n = ts_sort(t);
     for (uint32_t x = threadIdx.x; x < C; x += kKvWG) {
