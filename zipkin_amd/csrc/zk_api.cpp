@@ -31,6 +31,8 @@ struct zk_ctx {
     uint64_t* table = nullptr;            // S*S*kLimbs
     bool own_table = true;
     unsigned long long* stats = nullptr;  // kStatShards*ST_N
+    unsigned long long* h_stats = nullptr;  // pinned host copy of stats
+    hipEvent_t ev_stats = nullptr;          // recorded after the stats copy (polled, not slept on)
     unsigned int* spill_count = nullptr;
     uint64_t* spill_list = nullptr;
     uint64_t spill_cap = 0;
@@ -141,9 +143,19 @@ zk_status ensure_spill(zk_ctx* c, uint64_t n) {
 }
 
 zk_status stats_sum(zk_ctx* c, uint64_t out[ST_N]) {
-    std::vector<unsigned long long> h((size_t)kStatShards * ST_N);
-    ZK_HIP(c, hipMemcpyAsync(h.data(), c->stats, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
-    ZK_HIP(c, hipStreamSynchronize(c->stream));
+    // The counters end every finalize (the job's status), so their round trip is on the step's
+    // critical path: a pinned destination and a polled event instead of a blocking stream sync
+    // (whose wake-up leaves the GPU idle for tens of microseconds before the next step's work).
+    const size_t bytes = (size_t)kStatShards * ST_N * 8;
+    if (!c->h_stats) ZK_HIP(c, hipHostMalloc((void**)&c->h_stats, bytes, hipHostMallocDefault));
+    if (!c->ev_stats) ZK_HIP(c, hipEventCreateWithFlags(&c->ev_stats, hipEventDisableTiming));
+    ZK_HIP(c, hipMemcpyAsync(c->h_stats, c->stats, bytes, hipMemcpyDeviceToHost, c->stream));
+    ZK_HIP(c, hipEventRecord(c->ev_stats, c->stream));
+    hipError_t q;
+    while ((q = hipEventQuery(c->ev_stats)) == hipErrorNotReady) {
+    }
+    if (q != hipSuccess) return fail(c, ZK_ERR_HIP, std::string("stats copy: ") + hipGetErrorString(q));
+    const unsigned long long* h = c->h_stats;
     for (int s = 0; s < ST_N; ++s) out[s] = 0;
     for (int sh = 0; sh < kStatShards; ++sh)
         for (int s = 0; s < ST_N; ++s) out[s] += h[(size_t)sh * ST_N + s];
@@ -241,6 +253,8 @@ zk_status zk_ctx_destroy(zk_ctx* c) {
     if (c->rt) rt_set_stream(c->rt, nullptr);
     if (c->own_table) hipFree(c->table);
     hipFree(c->stats);
+    if (c->h_stats) hipHostFree(c->h_stats);
+    if (c->ev_stats) hipEventDestroy(c->ev_stats);
     hipFree(c->spill_count);
     hipFree(c->spill_list);
     hipFree(c->spill_scratch);
