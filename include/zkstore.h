@@ -84,6 +84,9 @@ zk_status zk_store_get_dependencies(zk_store* st, const int64_t* start_us, const
                                     int64_t* out_end_us);
 /* number of stored Dependencies records */
 zk_status zk_store_count(zk_store* st, uint64_t* records);
+/* The incremental driver's watermark: IFNULL(MAX(end_ts), 0) over every stored row
+ * (replaces AnormAggregator.scala:62-66's `SELECT IFNULL(MAX(END_TS), 0) FROM zipkin_dependencies`). */
+zk_status zk_store_watermark(zk_store* st, int64_t* end_us);
 
 /* storeTopAnnotations / storeTopKeyValueAnnotations: replace the list of `service` (`kind`
  * ZK_TOP_*); ids are host dictionary ids of the annotation values / keys, in list order. */

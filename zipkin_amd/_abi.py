@@ -302,6 +302,7 @@ _SIGNATURES = [
          C.POINTER(C.c_int64), C.POINTER(C.c_int64)],
     ),
     ("zk_store_count", C.c_int, [_P, _U64P]),
+    ("zk_store_watermark", C.c_int, [_P, C.POINTER(C.c_int64)]),
     ("zk_store_put_top", C.c_int, [_P, C.c_uint32, C.c_uint32, _P, C.c_uint64]),
     ("zk_store_get_top", C.c_int, [_P, C.c_uint32, C.c_uint32, _P, C.c_uint64, _U64P]),
     ("zk_moments_plus", C.c_int, [C.POINTER(zk_moments), C.POINTER(zk_moments), C.POINTER(zk_moments)]),

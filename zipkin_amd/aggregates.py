@@ -277,6 +277,12 @@ class GpuAggregates(Aggregates):
         self._check(self._L.zk_store_count(self._h, C.byref(n)))
         return int(n.value)
 
+    def watermark(self) -> int:
+        """IFNULL(MAX(end_ts), 0) over every stored row (AnormAggregator.scala:62-66)."""
+        w = C.c_int64()
+        self._check(self._L.zk_store_watermark(self._h, C.byref(w)))
+        return int(w.value)
+
     # -- top annotations ----------------------------------------------------------------------
     def _put_top(self, kind: int, serviceName: str, a: Sequence[str]) -> None:
         ids = np.array([self.annotations.id(x) for x in a], dtype=np.uint64)

@@ -186,6 +186,19 @@ zk_status zk_store_count(zk_store* s, uint64_t* records) {
     return ZK_OK;
 }
 
+zk_status zk_store_watermark(zk_store* s, int64_t* end_us) {
+    if (!s || !end_us) return ZK_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(s->mu);
+    int64_t w = 0;
+    bool any = false;
+    for (const StoredDeps& d : s->rows) {
+        w = any ? std::max(w, d.end) : d.end;
+        any = true;
+    }
+    *end_us = any ? w : 0;
+    return ZK_OK;
+}
+
 zk_status zk_store_put_top(zk_store* s, uint32_t kind, uint32_t service, const uint64_t* ids, uint64_t n) {
     if (!s) return ZK_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(s->mu);
