@@ -21,10 +21,13 @@
 namespace zk {
 namespace {
 
-constexpr int kKvWG = 256;
+#ifndef ZK_KV_WG
+#define ZK_KV_WG 512  // (256: candidates 1.55 -> 1.41 ms with 512 on C4)
+#endif
+constexpr int kKvWG = ZK_KV_WG;
 constexpr uint32_t kSetCap = 2048;  // 2^11: RowHash.set is 11 bits  // LDS hash-set slots (load <= 0.5)
 constexpr uint32_t kSortCap = 1024; // compaction sort buffer
-constexpr uint32_t kRound = 2 * kKvWG;
+constexpr uint32_t kRound = 512;  // merge: entries offered between compaction checks (<= kSortCap / 2)
 constexpr int kPrefetch = 8;        // candidate rounds of keys in flight per thread
 constexpr uint64_t kEmptyKey = ~0ull;
 
@@ -355,7 +358,7 @@ __global__ __launch_bounds__(kKvWG) void k_kv_merge(KvArgs a, uint32_t use_units
     const uint64_t nsrc = (uint64_t)(1 + (u1 - u0) + a.extra_lists) * C;
     for (uint64_t b = 0; b < nsrc; b += kRound) {
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
+        for (int e = 0; e < (int)(kRound / kKvWG); ++e) {
             const uint64_t i = b + (uint64_t)e * kKvWG + threadIdx.x;
             if (i >= nsrc) continue;
             const uint64_t list = i / C, x = i % C;

@@ -97,7 +97,7 @@ constexpr uint32_t kLineMaxS = 1024;
 #define ZK_PART_U 8      // items per thread per chunk (line scatter): 8192-item chunks (4: 1.80 -> 1.43 ms on C4)
 #endif
 #ifndef ZK_PART_WG
-#define ZK_PART_WG 1024  // line-scatter workgroup: 4096-item chunks (512 threads: 2.38 -> 1.76 ms on C4)
+#define ZK_PART_WG 1024  // line-scatter workgroup (512 threads x 4 items: 2.38 -> 1.76 ms on C4)
 #endif
 constexpr int kLineItems = 8;  // items per 64-byte line
 template <int U, int WG>
