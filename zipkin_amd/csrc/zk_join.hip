@@ -310,7 +310,8 @@ __device__ __forceinline__ void load_window(const JoinArgs& a, uint64_t ws, Wind
 constexpr int kModeJoin = 1;
 constexpr int kModeEmit = 2;
 template <int TILE, int WG, int ABL, int MODE>
-__global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU) void k_span_join_stream(JoinArgs a) {
+// launch bounds: minimum waves per SIMD = resident workgroups per CU x waves per workgroup / 4 SIMDs
+__global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_stream(JoinArgs a) {
     constexpr int H = ZK_HASH_FACTOR * TILE;  // load <= 1/16 (distinct spans / slots): short probe chains, since a wave waits for its longest
     constexpr int NWORD = TILE / 64;
     static_assert(TILE == 2 * WG && TILE <= 2047, "two records per thread");
@@ -959,7 +960,10 @@ __global__ __launch_bounds__(kSpillWG) void k_span_join_spill(JoinArgs a) {
 }
 
 // tile geometry of the shipped K1
-constexpr int kTileWG = 256;
+#ifndef ZK_K1_WG
+#define ZK_K1_WG 256  // K1 workgroup; a window is two records per thread
+#endif
+constexpr int kTileWG = ZK_K1_WG;
 constexpr int kTile = 2 * kTileWG;
 
 }  // namespace
