@@ -13,8 +13,12 @@ Fixtures are DATA only — inputs and expected outputs — never reference sourc
                         the aggregates.sql moments
 * moments_kats.json     exact and Algebird-fold Moments of small duration sets (oracle/moments.py)
 * job_kats.json         hand-built span sets through the span-level oracle (oracle/spans.py)
+* bulk_job.json         TraceGen-shaped batches of 1e3 / 1e4 / 1e5 traces (fixed seeds, 57 services)
+                        through the C restatement (oracle/zk_oracle.c): record / link / stat
+                        totals and SHA-256 digests of the exact per-cell power sums and of the
+                        exactly rounded dense m0..m4 (the device's finalize output, bit for bit)
 
-Usage: python tools/make_golden.py
+Usage: python tools/make_golden.py [--only FILE.json]
 """
 from __future__ import annotations
 
@@ -212,8 +216,50 @@ def job_kats() -> dict:
     return {"source": "oracle/spans.py aggregate_job (ZipkinAggregateJob.scala:20-43)", "cases": cases}
 
 
+BULK_CASES = ((101, 1_000), (102, 10_000), (103, 100_000))  # (seed, traces); max_depth 7, S = 57
+
+
+def bulk_digests(cols, S: int) -> dict:
+    """Totals and digests of one oracle run (shared with tests/test_oracle_kats.py)."""
+    import hashlib
+
+    import numpy as np
+
+    from oracle import oracle
+
+    ref = oracle.aggregate(cols, S)
+    m0, ms = ref.dense()
+    dense = b"".join([np.ascontiguousarray(m0, dtype=np.uint64).tobytes()] +
+                     [np.ascontiguousarray(m, dtype=np.float64).tobytes() for m in ms])
+    return {
+        "records": len(cols),
+        "links": int((m0 > 0).sum()),
+        "joined": int(m0.sum()),
+        "stats": {k: v for k, v in ref.stats.items() if k != "spilled_traces"},
+        "power_sums_sha256": hashlib.sha256(np.ascontiguousarray(ref.cells).tobytes()).hexdigest(),
+        "dense_moments_sha256": hashlib.sha256(dense).hexdigest(),
+    }
+
+
+def bulk_job() -> dict:
+    from zipkin_amd import tracegen_host
+
+    cases = {}
+    for seed, ntr in BULK_CASES:
+        cols = tracegen_host(seed=seed, num_traces=ntr, max_depth=7, num_services=57)
+        cases[f"tracegen_s{seed}_t{ntr}"] = {"seed": seed, "traces": ntr, "max_depth": 7, "services": 57,
+                                             **bulk_digests(cols, 57)}
+    return {"source": "oracle/zk_oracle.c on zk_tracegen.h batches (ZipkinAggregateJob.scala:20-43)",
+            "cases": cases}
+
+
 def main() -> None:
     OUT.mkdir(parents=True, exist_ok=True)
+    if len(sys.argv) == 3 and sys.argv[1] == "--only":
+        gen = {"bulk_job.json": bulk_job}[sys.argv[2]]
+        (OUT / sys.argv[2]).write_text(json.dumps(gen(), indent=1) + "\n")
+        print("wrote", OUT / sys.argv[2])
+        return
     sql = aggregates_sql()
     files = {
         "reference_kats.json": reference_kats(),
@@ -221,6 +267,7 @@ def main() -> None:
         "moment_accessors.json": moment_accessors(sql),
         "moments_kats.json": moments_kats(),
         "job_kats.json": job_kats(),
+        "bulk_job.json": bulk_job(),
     }
     for name, obj in files.items():
         (OUT / name).write_text(json.dumps(obj, indent=1, sort_keys=False) + "\n")
