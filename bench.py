@@ -70,8 +70,16 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
+        # ZK_BENCH_BACKEND=gloo: a correctness rehearsal of the N>1 path with several ranks on one
+        # GPU (not a measurement); the driver's runs use RCCL, one rank per GPU
+        backend = os.environ.get("ZK_BENCH_BACKEND", "nccl")
+        if backend != "nccl":
+            local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local)
@@ -105,13 +113,49 @@ def main():
     def step():
         ctx.reset()
         ctx.accumulate(cols)
-        if dist is not None:
-            allreduce_table(table)  # exact u64-limb SUM over xGMI (RCCL): shards are disjoint traces
-            ctx.note_merged(n * world)
         ctx.finalize(out_device=out)
+
+    def drain():
+        pass
+
+    if dist is not None:
+        # N > 1: two table/stream sets, software-pipelined. Batch k's join runs on its stream while
+        # batch k-1's all-reduce (RCCL over xGMI, exact u64-limb SUM: shards are disjoint traces)
+        # and finalize complete on the other; every batch is still reduced and finalized inside
+        # the timed region (drain() finalizes the last one).
+        stream2 = torch.cuda.Stream(device=dev)
+        table2 = torch.zeros_like(table)
+        ctx2 = DepsContext(S, device=local, stream=stream2.cuda_stream, timing=False,
+                           table_ptr=table2.data_ptr(), table_bytes=table2.numel() * 8, ablate=a.ablate)
+        out2 = {k: torch.empty_like(v) for k, v in out.items()}
+        sets = [(ctx, table, stream, out), (ctx2, table2, stream2, out2)]
+        state = {"k": 0, "pending": None}
+
+        def step():  # noqa: F811
+            c, t, s, o = sets[state["k"] % 2]
+            state["k"] += 1
+            torch.cuda.set_stream(s)
+            c.reset()
+            c.accumulate(cols)
+            allreduce_table(t)  # ordered on s; the host does not wait for it
+            c.note_merged(n * world)
+            if state["pending"] is not None:
+                pc, _, ps, po = state["pending"]
+                torch.cuda.set_stream(ps)
+                pc.finalize(out_device=po)
+            state["pending"] = (c, t, s, o)
+
+        def drain():  # noqa: F811
+            if state["pending"] is not None:
+                pc, _, ps, po = state["pending"]
+                torch.cuda.set_stream(ps)
+                pc.finalize(out_device=po)
+                state["pending"] = None
+            torch.cuda.set_stream(stream)
 
     for _ in range(a.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     tm0 = ctx.timing()
     if dist is not None:
@@ -122,6 +166,9 @@ def main():
     ev0.record(stream)
     for _ in range(a.steps):
         step()
+    drain()
+    if dist is not None:
+        stream.wait_stream(stream2)
     ev1.record(stream)
     torch.cuda.synchronize()
     if dist is not None:
@@ -141,6 +188,12 @@ def main():
     join_avg_ms = (tm1["join_ms_total"] - tm0["join_ms_total"]) / max(1, join_calls)
     achieved = n * BYTES_PER_RECORD / (join_avg_ms * 1e-3) / 1e9
     st = ctx.stats()
+    if dist is not None:
+        # both pipeline sets finalized the same batch: their outputs must agree bit for bit
+        for k in out:
+            if not torch.equal(out[k], out2[k]):
+                raise RuntimeError(f"pipelined N>1 step: output '{k}' differs between the two table sets")
+        ctx2.close()
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_sample > 0:
@@ -177,7 +230,9 @@ def main():
                 "services": S,
                 "max_depth": a.max_depth,
                 "parallelism": f"traceId-hash shards x{world}" + (", RCCL all-reduce of the link table" if world > 1 else ""),
-                "step": "reset + span_join + spill + [all-reduce] + finalize(m0..m4) + status check",
+                "step": "reset + span_join + spill + [all-reduce] + finalize(m0..m4) + status check"
+                        + (" (N>1: two table sets, batch k's join overlaps batch k-1's all-reduce + finalize)"
+                           if world > 1 else ""),
             },
             "roofline": {
                 "bound": "hbm",
