@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=20_000_000, help="records for the CPU baseline leg (0: skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--ablate", type=int, default=0, help="diagnostic: 1 = K1 without link emission (not a valid result)")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="c2: 1 (default) = two table/stream sets (batch k's join overlaps batch k-1's "
+                         "tail); 0 = one set, serial steps")
     ap.add_argument("--workload", default="c2", choices=("c2", "c4", "c5", "ingest"),
                     help="c2 (default, the headline): dependency path; c4: key-value top-K sketch over "
                          "binary annotations; c5: per-service HLL + duration histogram from span fragments; "
@@ -110,19 +113,25 @@ def main():
         "present": torch.empty(cells, dtype=torch.uint8, device=dev),
     }
 
-    def step():
+    def step_serial():
         ctx.reset()
         ctx.accumulate(cols)
+        if dist is not None:
+            allreduce_table(table)  # exact u64-limb SUM over xGMI (RCCL): shards are disjoint traces
+            ctx.note_merged(n * world)
         ctx.finalize(out_device=out)
+
+    step = step_serial
 
     def drain():
         pass
 
-    if dist is not None:
-        # N > 1: two table/stream sets, software-pipelined. Batch k's join runs on its stream while
-        # batch k-1's all-reduce (RCCL over xGMI, exact u64-limb SUM: shards are disjoint traces)
-        # and finalize complete on the other; every batch is still reduced and finalized inside
-        # the timed region (drain() finalizes the last one).
+    pipeline = a.pipeline != 0
+    if pipeline:
+        # Two table/stream sets, software-pipelined: batch k's join runs on its stream while batch
+        # k-1's tail (K2/K3, at N > 1 the all-reduce over RCCL, finalize and status check) completes
+        # on the other; every batch is still joined, reduced and finalized inside the timed region
+        # (drain() finalizes the last one).
         stream2 = torch.cuda.Stream(device=dev)
         table2 = torch.zeros_like(table)
         ctx2 = DepsContext(S, device=local, stream=stream2.cuda_stream, timing=False,
@@ -137,8 +146,9 @@ def main():
             torch.cuda.set_stream(s)
             c.reset()
             c.accumulate(cols)
-            allreduce_table(t)  # ordered on s; the host does not wait for it
-            c.note_merged(n * world)
+            if dist is not None:
+                allreduce_table(t)  # ordered on s; the host does not wait for it
+                c.note_merged(n * world)
             if state["pending"] is not None:
                 pc, _, ps, po = state["pending"]
                 torch.cuda.set_stream(ps)
@@ -153,9 +163,22 @@ def main():
                 state["pending"] = None
             torch.cuda.set_stream(stream)
 
-    for _ in range(a.warmup):
-        step()
-    drain()
+    # warmup: serial steps first (their K1 launches give the isolated K1 duration), then two
+    # pipelined steps so that the second set's buffers exist before the timed region
+    tmf = None
+    for i in range(a.warmup):
+        step_serial()
+        if i == 0:  # the first launch is cold: the isolated figure averages the later ones
+            tmf = dict(ctx.timing())
+    torch.cuda.synchronize()
+    tmw = ctx.timing()
+    k1_isolated_ms = None
+    if a.warmup >= 2:
+        k1_isolated_ms = (tmw["join_ms_total"] - tmf["join_ms_total"]) / (tmw["join_calls"] - tmf["join_calls"])
+    if pipeline:
+        for _ in range(2):
+            step()
+        drain()
     torch.cuda.synchronize()
     tm0 = ctx.timing()
     if dist is not None:
@@ -167,7 +190,7 @@ def main():
     for _ in range(a.steps):
         step()
     drain()
-    if dist is not None:
+    if pipeline:
         stream.wait_stream(stream2)
     ev1.record(stream)
     torch.cuda.synchronize()
@@ -188,11 +211,11 @@ def main():
     join_avg_ms = (tm1["join_ms_total"] - tm0["join_ms_total"]) / max(1, join_calls)
     achieved = n * BYTES_PER_RECORD / (join_avg_ms * 1e-3) / 1e9
     st = ctx.stats()
-    if dist is not None:
+    if pipeline:
         # both pipeline sets finalized the same batch: their outputs must agree bit for bit
         for k in out:
             if not torch.equal(out[k], out2[k]):
-                raise RuntimeError(f"pipelined N>1 step: output '{k}' differs between the two table sets")
+                raise RuntimeError(f"pipelined step: output '{k}' differs between the two table sets")
         ctx2.close()
 
     cpu = None
@@ -231,8 +254,8 @@ def main():
                 "max_depth": a.max_depth,
                 "parallelism": f"traceId-hash shards x{world}" + (", RCCL all-reduce of the link table" if world > 1 else ""),
                 "step": "reset + span_join + spill + [all-reduce] + finalize(m0..m4) + status check"
-                        + (" (N>1: two table sets, batch k's join overlaps batch k-1's all-reduce + finalize)"
-                           if world > 1 else ""),
+                        + (" (two table sets: batch k's join overlaps batch k-1's reduce, [all-reduce,] finalize)"
+                           if pipeline else ""),
             },
             "roofline": {
                 "bound": "hbm",
@@ -244,6 +267,11 @@ def main():
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": n * BYTES_PER_RECORD,
                 "avg_launch_ms": join_avg_ms,
+                # K1 alone (serial warmup steps): with the pipeline, the timed launches share the
+                # chip with the other set's K2/K3/finalize, so avg_launch_ms above is longer
+                "isolated_avg_launch_ms": k1_isolated_ms,
+                "isolated_frac": (n * BYTES_PER_RECORD / (k1_isolated_ms * 1e-3) / 1e9 / PEAK_HBM_GBS
+                                  if k1_isolated_ms else None),
             },
             "cpu_baseline": cpu,
             "detail": {
