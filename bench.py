@@ -436,6 +436,8 @@ def bench_c5(a):
     import torch
 
     from zipkin_amd import DepsContext, DeviceColumns, tracegen_params
+    import numpy as np
+
     from zipkin_amd.realtime import RtSketch
 
     torch.cuda.set_device(0)
@@ -451,16 +453,51 @@ def bench_c5(a):
     cols = DeviceColumns(a.records, device="cuda:0")
     n, ntr = ctx.tracegen_device(p, cols)
 
-    def step():
+    def step_serial():
         ctx.reset()
         rt.reset()
         ctx.accumulate(cols)
 
+    # K1 alone: a few serial steps before the timed run (untimed)
+    step_serial()
+    torch.cuda.synchronize()
+    tmi = ctx.timing()
+    for _ in range(3):
+        step_serial()
+    tmj = ctx.timing()
+    k1_isolated_ms = (tmj["join_ms_total"] - tmi["join_ms_total"]) / (tmj["join_calls"] - tmi["join_calls"])
+
+    step = step_serial
+    if a.pipeline != 0:
+        # two context/sketch/stream sets: batch k's K1 overlaps batch k-1's partition + sketch
+        stream2 = torch.cuda.Stream(device=dev)
+        ctx2 = DepsContext(S, device=0, stream=stream2.cuda_stream, timing=False)
+        rt2 = RtSketch(S, stream=stream2.cuda_stream)
+        rt2.bind(ctx2, only=True)
+        sets = [(ctx, rt, stream), (ctx2, rt2, stream2)]
+        k = [0]
+
+        def step():  # noqa: F811
+            c, r, s = sets[k[0] % 2]
+            k[0] += 1
+            torch.cuda.set_stream(s)
+            c.reset()
+            r.reset()
+            c.accumulate(cols)
+
     tm0 = ctx.timing()
-    wall, ev_ms = _timed(step, a.steps, a.warmup, stream)
+    wall, ev_ms = _timed(step, a.steps, max(2, a.warmup), stream)
+    torch.cuda.set_stream(stream)
     tm1 = ctx.timing()
     calls = tm1["join_calls"] - tm0["join_calls"]
     join_ms = (tm1["join_ms_total"] - tm0["join_ms_total"]) / max(1, calls)
+    if a.pipeline != 0:
+        # both sets sketched the same batch: registers and bins must agree exactly
+        (ra, ha), (rb, hb) = rt.read(), rt2.read()
+        if not (np.array_equal(ra, rb) and np.array_equal(ha, hb)):
+            raise RuntimeError("pipelined C5 step: the two sketch sets differ")
+        rt2.close()
+        ctx2.close()
     t0 = time.perf_counter()
     est = rt.distinct_traces()
     q = [rt.quantiles(s, (0.5, 0.99)) for s in range(S)]
@@ -473,10 +510,13 @@ def bench_c5(a):
         "dtype": "u64", "data": "synthetic (zipkin-tracegen-shaped, generated on device)",
         "config": {"workload": "C5: 1e8 span records, 500 services, HLL p=14 + log-linear histogram m=7",
                    "records": n, "traces": ntr, "services": S,
-                   "step": "reset + K1 (merge, isValid, serviceName, duration; sketch items) + partition + sketch"},
+                   "step": "reset + K1 (merge, isValid, serviceName, duration; sketch items) + partition + sketch"
+                           + (" (two sets: batch k's K1 overlaps batch k-1's partition + sketch)" if a.pipeline else "")},
         "roofline": {"bound": "hbm", "kernel": "k_span_join_stream<..., kModeEmit>", "achieved": achieved,
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
-                     "algorithmic_bytes_per_launch": n * 40, "avg_launch_ms": join_ms},
+                     "algorithmic_bytes_per_launch": n * 40, "avg_launch_ms": join_ms,
+                     "isolated_avg_launch_ms": k1_isolated_ms,
+                     "isolated_frac": n * 40 / (k1_isolated_ms * 1e-3) / 1e9 / PEAK_HBM_GBS},
         "detail": {"event_ms_per_step": ev_ms / a.steps, "query_ms_all_services": query_ms,
                    "median_distinct_estimate": float(sorted(est)[S // 2]),
                    "p50_p99_bins_service0": q[0][0]},
