@@ -313,7 +313,7 @@ def cpu_baseline(cols, sample, S, threads):
     }
 
 
-def _timed(step, steps, warmup, stream):
+def _timed(step, steps, warmup, stream, others=()):
     import torch
 
     for _ in range(warmup):
@@ -324,6 +324,8 @@ def _timed(step, steps, warmup, stream):
     ev0.record(stream)
     for _ in range(steps):
         step()
+    for o in others:  # pipelined sets: the end event follows every stream's last step
+        stream.wait_stream(o)
     ev1.record(stream)
     torch.cuda.synchronize()
     return time.perf_counter() - t0, ev0.elapsed_time(ev1)
@@ -529,6 +531,8 @@ def bench_c4(a):
     services uniform over 500, generated on device."""
     import torch
 
+    import numpy as np
+
     from zipkin_amd.kv import KvSketch
 
     torch.cuda.set_device(0)
@@ -566,10 +570,32 @@ def bench_c4(a):
         kv.reset()
         kv.accumulate(svc, keys)
 
-    wall, ev_ms = _timed(step, a.steps, a.warmup, stream)
+    others = ()
+    if a.pipeline != 0:
+        # two sketch/stream sets: batch k's partition overlaps batch k-1's sketch + candidates
+        stream2 = torch.cuda.Stream(device=dev)
+        kv2 = KvSketch(S, stream=stream2.cuda_stream, seed=4)
+        sets = [(kv, stream), (kv2, stream2)]
+        others = (stream2,)
+        k = [0]
+
+        def step():  # noqa: F811
+            c, s = sets[k[0] % 2]
+            k[0] += 1
+            torch.cuda.set_stream(s)
+            c.reset()
+            c.accumulate(svc, keys)
+
+    wall, ev_ms = _timed(step, a.steps, max(2, a.warmup), stream, others)
+    torch.cuda.set_stream(stream)
     t0 = time.perf_counter()
     kk, est, cnt = kv.topk_all(10)
     query_ms = (time.perf_counter() - t0) * 1e3
+    if a.pipeline != 0:
+        kk2, est2, cnt2 = kv2.topk_all(10)
+        if not (np.array_equal(kk, kk2) and np.array_equal(est, est2) and np.array_equal(cnt, cnt2)):
+            raise RuntimeError("pipelined C4 step: the two sketch sets differ")
+        kv2.close()
     value = n * a.steps / wall
     achieved = n * 12 / (ev_ms / a.steps * 1e-3) / 1e9  # HIP events on the step's stream
     print(json.dumps({
@@ -578,7 +604,9 @@ def bench_c4(a):
         "ms_per_step": wall * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u32", "data": "synthetic (Zipf(1.1) keys over 1e6 ids, 500 services, generated on device)",
         "config": {"workload": f"C4: {n:.3g} binary annotations per step, count-min 4 x 2048 per service, K=64 kept",
-                   "items": n, "services": S},
+                   "items": n, "services": S,
+                   "step": "reset + partition + sketch + candidates + merge"
+                           + (" (two sets: batch k overlaps batch k-1)" if a.pipeline else "")},
         "roofline": {"bound": "hbm", "kernel": "whole step (partition + sketch + candidates + merge)",
                      "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                      "algorithmic_bytes_per_step": n * 12},
