@@ -43,9 +43,10 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=20_000_000, help="records for the CPU baseline leg (0: skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--ablate", type=int, default=0, help="diagnostic: 1 = K1 without link emission (not a valid result)")
-    ap.add_argument("--pipeline", type=int, default=1,
-                    help="c2: 1 (default) = two table/stream sets (batch k's join overlaps batch k-1's "
-                         "tail); 0 = one set, serial steps")
+    ap.add_argument("--pipeline", type=int, default=2,
+                    help="batches in flight behind the one being joined: 2 (default) = three table/stream "
+                         "sets, 1 = two (batch k's join overlaps batch k-1's tail), 0 = one set, serial steps "
+                         "(c2 takes any depth, c4/c5 use two sets when > 0)")
     ap.add_argument("--workload", default="c2", choices=("c2", "c4", "c5", "ingest"),
                     help="c2 (default, the headline): dependency path; c4: key-value top-K sketch over "
                          "binary annotations; c5: per-service HLL + duration histogram from span fragments; "
@@ -132,16 +133,22 @@ def main():
         # k-1's tail (K2/K3, at N > 1 the all-reduce over RCCL, finalize and status check) completes
         # on the other; every batch is still joined, reduced and finalized inside the timed region
         # (drain() finalizes the last one).
-        stream2 = torch.cuda.Stream(device=dev)
-        table2 = torch.zeros_like(table)
-        ctx2 = DepsContext(S, device=local, stream=stream2.cuda_stream, timing=False,
-                           table_ptr=table2.data_ptr(), table_bytes=table2.numel() * 8, ablate=a.ablate)
-        out2 = {k: torch.empty_like(v) for k, v in out.items()}
-        sets = [(ctx, table, stream, out), (ctx2, table2, stream2, out2)]
-        state = {"k": 0, "pending": None}
+        sets = [(ctx, table, stream, out)]
+        for _ in range(a.pipeline):  # a.pipeline batches in flight behind the one being joined
+            s2 = torch.cuda.Stream(device=dev)
+            t2 = torch.zeros_like(table)
+            c2 = DepsContext(S, device=local, stream=s2.cuda_stream, timing=False,
+                             table_ptr=t2.data_ptr(), table_bytes=t2.numel() * 8, ablate=a.ablate)
+            sets.append((c2, t2, s2, {k: torch.empty_like(v) for k, v in out.items()}))
+        state = {"k": 0, "pending": []}
+
+        def finalize_oldest():
+            pc, _, ps, po = state["pending"].pop(0)
+            torch.cuda.set_stream(ps)
+            pc.finalize(out_device=po)
 
         def step():  # noqa: F811
-            c, t, s, o = sets[state["k"] % 2]
+            c, t, s, o = sets[state["k"] % len(sets)]
             state["k"] += 1
             torch.cuda.set_stream(s)
             c.reset()
@@ -149,18 +156,13 @@ def main():
             if dist is not None:
                 allreduce_table(t)  # ordered on s; the host does not wait for it
                 c.note_merged(n * world)
-            if state["pending"] is not None:
-                pc, _, ps, po = state["pending"]
-                torch.cuda.set_stream(ps)
-                pc.finalize(out_device=po)
-            state["pending"] = (c, t, s, o)
+            state["pending"].append((c, t, s, o))
+            if len(state["pending"]) > a.pipeline:
+                finalize_oldest()
 
         def drain():  # noqa: F811
-            if state["pending"] is not None:
-                pc, _, ps, po = state["pending"]
-                torch.cuda.set_stream(ps)
-                pc.finalize(out_device=po)
-                state["pending"] = None
+            while state["pending"]:
+                finalize_oldest()
             torch.cuda.set_stream(stream)
 
     # warmup: serial steps first (their K1 launches give the isolated K1 duration), then two
@@ -176,7 +178,7 @@ def main():
     if a.warmup >= 2:
         k1_isolated_ms = (tmw["join_ms_total"] - tmf["join_ms_total"]) / (tmw["join_calls"] - tmf["join_calls"])
     if pipeline:
-        for _ in range(2):
+        for _ in range(len(sets)):
             step()
         drain()
     torch.cuda.synchronize()
@@ -191,7 +193,8 @@ def main():
         step()
     drain()
     if pipeline:
-        stream.wait_stream(stream2)
+        for st2 in sets[1:]:
+            stream.wait_stream(st2[2])
     ev1.record(stream)
     torch.cuda.synchronize()
     if dist is not None:
@@ -213,10 +216,11 @@ def main():
     st = ctx.stats()
     if pipeline:
         # both pipeline sets finalized the same batch: their outputs must agree bit for bit
-        for k in out:
-            if not torch.equal(out[k], out2[k]):
-                raise RuntimeError(f"pipelined step: output '{k}' differs between the two table sets")
-        ctx2.close()
+        for c2, _, _, o2 in sets[1:]:
+            for k in out:
+                if not torch.equal(out[k], o2[k]):
+                    raise RuntimeError(f"pipelined step: output '{k}' differs between the table sets")
+            c2.close()
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_sample > 0:
@@ -254,7 +258,7 @@ def main():
                 "max_depth": a.max_depth,
                 "parallelism": f"traceId-hash shards x{world}" + (", RCCL all-reduce of the link table" if world > 1 else ""),
                 "step": "reset + span_join + spill + [all-reduce] + finalize(m0..m4) + status check"
-                        + (" (two table sets: batch k's join overlaps batch k-1's reduce, [all-reduce,] finalize)"
+                        + (f" ({a.pipeline + 1} table sets: batch k's join overlaps earlier batches' reduce, [all-reduce,] finalize)"
                            if pipeline else ""),
             },
             "roofline": {
