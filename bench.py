@@ -43,9 +43,9 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=20_000_000, help="records for the CPU baseline leg (0: skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--ablate", type=int, default=0, help="diagnostic: 1 = K1 without link emission (not a valid result)")
-    ap.add_argument("--pipeline", type=int, default=2,
-                    help="batches in flight behind the one being joined: 2 (default) = three table/stream "
-                         "sets, 1 = two (batch k's join overlaps batch k-1's tail), 0 = one set, serial steps "
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="batches in flight behind the one being joined: 1 (default) = two table/stream "
+                         "sets (batch k's join overlaps batch k-1's tail), 2 = three, 0 = one set, serial steps "
                          "(c2 takes any depth, c4/c5 use two sets when > 0)")
     ap.add_argument("--workload", default="c2", choices=("c2", "c4", "c5", "ingest"),
                     help="c2 (default, the headline): dependency path; c4: key-value top-K sketch over "
