@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--cpu-sample", type=int, default=20_000_000, help="records for the CPU baseline leg (0: skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--verify", type=int, default=0,
+                    help="1: ZK_BATCH_VERIFY_TRACES on every step (exact device check of the clustering promise)")
     ap.add_argument("--ablate", type=int, default=0, help="diagnostic: 1 = K1 without link emission (not a valid result)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="batches in flight behind the one being joined: 1 (default) = two table/stream "
@@ -97,7 +99,9 @@ def main():
     # 0 -- torch's legacy default stream -- would make the library create an unordered private one)
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
-    table = torch.zeros(cells * 16, dtype=torch.int64, device=dev)
+    from zipkin_amd._abi import table_words
+
+    table = torch.zeros(table_words(S), dtype=torch.int64, device=dev)
     ctx = DepsContext(S, device=local, stream=stream.cuda_stream, timing=True,
                       table_ptr=table.data_ptr(), table_bytes=table.numel() * 8, ablate=a.ablate)
     traces_cap = int(a.records / 15) + 1000
@@ -116,9 +120,11 @@ def main():
 
     def step_serial():
         ctx.reset()
-        ctx.accumulate(cols)
+        # device-generated batches are trace-clustered by construction (zk_tracegen_device)
+        ctx.accumulate(cols, clustered=True, verify=a.verify)
         if dist is not None:
-            allreduce_table(table)  # exact u64-limb SUM over xGMI (RCCL): shards are disjoint traces
+            ctx.partial()  # fold the counters into the table tail (same stream)
+            allreduce_table(table)  # exact u64-limb + counter SUM over xGMI (RCCL): shards are disjoint traces
             ctx.note_merged(n * world)
         ctx.finalize(out_device=out)
 
@@ -152,8 +158,9 @@ def main():
             state["k"] += 1
             torch.cuda.set_stream(s)
             c.reset()
-            c.accumulate(cols)
+            c.accumulate(cols, clustered=True, verify=a.verify)
             if dist is not None:
+                c.partial()
                 allreduce_table(t)  # ordered on s; the host does not wait for it
                 c.note_merged(n * world)
             state["pending"].append((c, t, s, o))
@@ -222,9 +229,9 @@ def main():
                     raise RuntimeError(f"pipelined step: output '{k}' differs between the table sets")
             c2.close()
 
-    cpu = None
+    cpu = parity = None
     if rank == 0 and world == 1 and a.cpu_sample > 0:
-        cpu = cpu_baseline(cols, min(a.cpu_sample, n), S, a.cpu_threads)
+        cpu, parity = cpu_baseline(cols, min(a.cpu_sample, n), S, a.cpu_threads, dev)
 
     traffic = None
     pmc = ROOT / "profiles" / "pmc_latest.json"
@@ -278,6 +285,7 @@ def main():
                                   if k1_isolated_ms else None),
             },
             "cpu_baseline": cpu,
+            "parity": parity,
             "detail": {
                 "event_ms_per_step": ev_ms / a.steps,
                 "finalize_ms_last": tm1["finalize_ms"],
@@ -293,10 +301,17 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(cols, sample, S, threads):
+def cpu_baseline(cols, sample, S, threads, dev):
     """The oracle's multithreaded C restatement (kind "port") on the first `sample` records of the
-    same batch, on this box's host cores. A reported baseline only."""
+    same batch, on this box's host cores. A reported baseline only.
+
+    The same oracle run is the bench's parity check: the HIP path aggregates the same prefix of the
+    device batch, and m0..m4 and every counter must equal the oracle's bit for bit, or the bench
+    fails (the timed steps above process the full batch with the same kernels)."""
+    import numpy as np
+
     from oracle import oracle
+    from zipkin_amd import DepsContext
 
     host = cols.to_host()
     # cut at a trace boundary so the sample is trace-complete
@@ -307,7 +322,17 @@ def cpu_baseline(cols, sample, S, threads):
     part = host.take(slice(0, cut))
     oracle.aggregate(part.take(slice(0, min(cut, 100_000))), S, threads=threads)  # warm the library
     r = oracle.aggregate(part, S, threads=threads)
-    return {
+    with DepsContext(S, device=dev.index or 0) as ctx:
+        ctx.accumulate(cols, clustered=True, verify=True, n=cut)
+        got = ctx.finalize()
+        st = ctx.stats()
+    m0, ms = r.dense()
+    bad = [k for k, x, y in zip(("m0", "m1", "m2", "m3", "m4"), (got.m0, got.m1, got.m2, got.m3, got.m4), (m0, *ms))
+           if not np.array_equal(x, y)]
+    bad += [k for k, v in r.stats.items() if k != "spilled_traces" and st[k] != v]
+    if bad:
+        raise RuntimeError(f"parity failure on the {cut}-record prefix of the bench batch: {bad}")
+    cpu = {
         "value": cut / r.seconds,
         "unit": "spans/s",
         "cores": threads,
@@ -315,6 +340,9 @@ def cpu_baseline(cols, sample, S, threads):
         "sample": f"first {cut} records (whole traces) of the benchmark batch; oracle/zk_oracle.c, "
         f"{threads} threads, {r.seconds:.2f} s",
     }
+    parity = {"result": "exact", "records": cut, "links": int(got.present.sum()),
+              "checked": "m0..m4 bit-identical + all counters, HIP path vs oracle/zk_oracle.c, same prefix"}
+    return cpu, parity
 
 
 def _timed(step, steps, warmup, stream, others=()):
@@ -462,7 +490,7 @@ def bench_c5(a):
     def step_serial():
         ctx.reset()
         rt.reset()
-        ctx.accumulate(cols)
+        ctx.accumulate(cols, clustered=True, verify=False)
 
     # K1 alone: a few serial steps before the timed run (untimed)
     step_serial()
@@ -489,7 +517,7 @@ def bench_c5(a):
             torch.cuda.set_stream(s)
             c.reset()
             r.reset()
-            c.accumulate(cols)
+            c.accumulate(cols, clustered=True, verify=False)
 
     tm0 = ctx.timing()
     wall, ev_ms = _timed(step, a.steps, max(2, a.warmup), stream)

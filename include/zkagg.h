@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define ZK_ABI_VERSION 1
+#define ZK_ABI_VERSION 2
 
 typedef enum zk_status {
     ZK_OK = 0,
@@ -48,7 +48,8 @@ typedef enum zk_status {
     ZK_ERR_TRACE_TOO_LARGE = 5,  /* a trace longer than zk_config.max_trace_records */
     ZK_ERR_CAPACITY = 6,         /* exact-accumulator headroom exhausted (> 2^32-1 records since reset),
                                     or a caller buffer too small */
-    ZK_ERR_NOT_CLUSTERED = 7,    /* batch flags did not promise trace-clustered input */
+    ZK_ERR_NOT_CLUSTERED = 7,    /* ZK_BATCH_VERIFY_TRACES found a trace split into non-adjacent
+                                    runs, or over two accumulate calls since the last reset */
     ZK_ERR_NO_DEVICE = 8,        /* no HIP device / not gfx950 */
     ZK_ERR_SERVICE_RANGE = 9,    /* a record carries service_id >= num_services */
     ZK_ERR_UNSUPPORTED = 10,
@@ -91,10 +92,22 @@ typedef struct zk_span_cols {
     uint64_t        n;
 } zk_span_cols;
 
-/* batch flags for zk_deps_accumulate */
+/* batch flags for zk_deps_accumulate
+ *
+ * Fragments may come in ANY order, as the reference's shuffles allow (ZipkinAggregateJob.scala:21,
+ * 28-33): without ZK_BATCH_TRACE_CLUSTERED the batch first goes through a device clustering pass
+ * (a stable radix sort of the 64-bit traceIds, then one gather of the columns; ~3x the cost of the
+ * join itself). ZK_BATCH_TRACE_CLUSTERED is the caller's promise that the pass is unnecessary.
+ * ZK_BATCH_VERIFY_TRACES checks that promise, and the trace-complete-batch contract, exactly: every
+ * trace run's traceId is inserted into a device set of all traceIds accumulated since the last
+ * reset, and a traceId seen again (a trace split into non-adjacent runs, or spread over two
+ * accumulate calls -- either would be mis-joined) is counted in zk_stats.not_clustered and makes
+ * finalize return ZK_ERR_NOT_CLUSTERED. The set costs 16 B of HBM per record since reset and one
+ * extra read of the traceId column. */
 #define ZK_BATCH_DEVICE_PTRS     (1u << 0) /* column pointers are device (HBM) pointers; else host */
 #define ZK_BATCH_TRACE_CLUSTERED (1u << 1) /* all fragments of a trace are adjacent (Cassandra
                                               row-per-trace reads, StorageRecordReader.scala:49-54) */
+#define ZK_BATCH_VERIFY_TRACES   (1u << 2) /* check clustering and trace-completeness (see above) */
 
 typedef struct zk_config {
     uint32_t num_services;       /* S <= 4096: service ids are 0..S-1, link table is S x S */
@@ -106,8 +119,8 @@ typedef struct zk_config {
                                     CassieSpanStore.scala:50) */
     uint32_t timing;             /* 1: record per-kernel HIP events (zk_ctx_timing) */
     void*    table;              /* optional caller-owned device buffer for the exact accumulator
-                                    (zk_deps_partial layout, table_bytes >= S*S*128): lets the
-                                    host all-reduce it in place with its own RCCL communicator */
+                                    (zk_deps_partial layout, table_bytes >= ZK_TABLE_BYTES(S)): lets
+                                    the host all-reduce it in place with its own RCCL communicator */
     uint64_t table_bytes;
     uint32_t reserved[8];
 } zk_config;
@@ -130,7 +143,8 @@ typedef struct zk_stats {
     uint64_t duration_range;   /* links dropped for duration >= 2^40 us */
     uint64_t service_range;    /* records with service_id >= num_services */
     uint64_t trace_too_large;  /* traces longer than max_trace_records (not aggregated) */
-    uint64_t reserved[3];
+    uint64_t not_clustered;    /* trace runs whose traceId was already accumulated (VERIFY_TRACES) */
+    uint64_t reserved[2];
 } zk_stats;
 
 /* Device time of the last accumulate/finalize, from HIP events (config.timing = 1). */
@@ -179,10 +193,19 @@ zk_status zk_deps_reset(zk_ctx* ctx);
 zk_status zk_deps_accumulate(zk_ctx* ctx, const zk_span_cols* cols, uint32_t batch_flags);
 zk_status zk_deps_finalize(zk_ctx* ctx, const zk_link_table* out);
 
-/* Raw exact accumulator (device memory, S*S cells x 16 u64 limbs, 32-bit chunks per limb) for
-   an external SUM all-reduce (RCCL over xGMI) across traceId-hash shards. After the caller
-   reduced it in place, zk_deps_note_merged tells the ctx how many records the merged table
-   now covers (the headroom bound of ZK_ERR_CAPACITY). */
+/* Raw exact accumulator for an external SUM all-reduce (RCCL over xGMI) across traceId-hash
+   shards, replacing the cross-reducer .group.sum / .sum of ZipkinAggregateJob.scala:39-43.
+   Layout (ZK_TABLE_BYTES(S) bytes of device memory): S*S cells x 16 u64 limbs (32-bit chunks per
+   limb, carry-free), then a tail of 16 u64 = this ctx's zk_stats counters. zk_deps_partial enqueues
+   the fold of the counters into the tail on the ctx stream and returns the buffer; every field is
+   a plain sum, so ONE int64/uint64 SUM all-reduce of the whole buffer merges the exact power sums
+   and the job-wide counters. zk_deps_note_merged then tells the ctx that the buffer holds the
+   merged job: total_records bounds the ZK_ERR_CAPACITY headroom (0: read it from the merged
+   tail, which costs one stream synchronisation), and finalize / zk_ctx_stats read
+   the merged counters from the tail, so every rank reaches the same status (a strict-mode
+   ZK_ERR_NO_SERVICE on one shard fails all ranks alike instead of one rank leaving the others
+   blocked in the next collective). The next reset or accumulate leaves the merged state. */
+#define ZK_TABLE_BYTES(S) ((uint64_t)(S) * (uint64_t)(S) * 128u + 128u)
 zk_status zk_deps_partial(zk_ctx* ctx, void** dev_ptr, uint64_t* bytes);
 zk_status zk_deps_note_merged(zk_ctx* ctx, uint64_t total_records);
 

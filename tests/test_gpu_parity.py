@@ -19,11 +19,13 @@ SERVER = _abi.ZK_F_HAS_ANNOTATIONS | _abi.ZK_F_SVC_SERVER | (1 << _abi.ZK_F_SR_S
 CLIENT = _abi.ZK_F_HAS_ANNOTATIONS | _abi.ZK_F_SVC_CLIENT | (1 << _abi.ZK_F_CS_SHIFT) | (1 << _abi.ZK_F_CR_SHIFT)
 
 
-def run_gpu(cols, S, batches=None, device_cols=False, **kw):
+def run_gpu(cols, S, batches=None, device_cols=False, clustered=True, **kw):
+    """The clustered fast path (K1 straight on the input) with the exact clustering check on;
+    tests/test_gpu_order.py covers unclustered batches."""
     with DepsContext(S, **kw) as ctx:
         parts = batches or [cols]
         for p in parts:
-            ctx.accumulate(DeviceColumns.from_host(p) if device_cols else p)
+            ctx.accumulate(DeviceColumns.from_host(p) if device_cols else p, clustered=clustered)
         got = ctx.finalize()
         return got, ctx.stats()
 
@@ -213,10 +215,9 @@ def test_empty_single_and_unclustered(gpu):
     assert got.present.sum() == 0 and st["records"] == 0
     got, st = run_gpu(cols_from_rows([(1, 1, 0, 5, 9, 0, SERVER)]), 5)
     assert got.present.sum() == 0 and st["merged_spans"] == 1
-    with DepsContext(5) as ctx:
-        with pytest.raises(ZkError) as e:
-            ctx.accumulate(cols_from_rows([(1, 1, 0, 5, 9, 0, SERVER)]), clustered=False)
-        assert e.value.status == _abi.ZK_ERR_NOT_CLUSTERED
+    # without the clustered promise the batch goes through the device clustering pass
+    got, st = run_gpu(cols_from_rows([(1, 1, 0, 5, 9, 0, SERVER)]), 5, clustered=False)
+    assert got.present.sum() == 0 and st["merged_spans"] == 1
 
 
 M32 = 0xFFFFFFFF
@@ -291,3 +292,24 @@ def test_large_device_generated_batch(gpu):
     host = dev.to_host()
     assert len(host) == n and n > 9_000_000
     assert_parity(got, st, oracle.aggregate(host, S))
+
+
+def test_full_size_c2_batch(gpu):
+    """The bench's own C2 batch (BASELINE configs[1]: 1e8 records, 500 services, seed 2, maxDepth 6,
+    generated on the device exactly as bench.py does) against the oracle at full size."""
+    import os
+
+    S = 500
+    p = tracegen_params(2, int(1e8 / 15) + 1000, target_records=100_000_000, max_depth=6, num_services=S)
+    with DepsContext(S) as ctx:
+        dev = DeviceColumns(100_000_000)
+        n, ntr = ctx.tracegen_device(p, dev)
+        ctx.accumulate(dev, clustered=True, verify=True)
+        got = ctx.finalize()
+        st = ctx.stats()
+    host = dev.to_host()
+    del dev
+    assert n == len(host) and n > 99_000_000
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    assert_parity(got, st, oracle.aggregate(host, S, threads=threads))
+    assert st["not_clustered"] == 0

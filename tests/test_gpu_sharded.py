@@ -1,0 +1,131 @@
+"""The N>1 product path on one GPU: traceId-hash shards -> one DepsContext per shard over a
+caller-owned table -> zk_deps_partial (counters folded into the tail) -> SUM of the tables ->
+zk_deps_note_merged -> finalize.
+
+The SUM is a torch add of the int64 tables: exactly what RCCL's SUM all-reduce computes on every
+rank, so this is the merge of ZipkinAggregateJob.scala:39-43 (`.group.sum` and the final `.sum`
+across reducers) with the collective replaced by its arithmetic. Bar: m0..m4 and every counter
+bit-identical to the oracle over the union and to the 1-shard run; the device limb layout decodes
+(zipkin_amd/table.py) to the oracle's exact power sums."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+from tests.test_gpu_parity import SERVER, assert_parity, cols_from_rows
+from zipkin_amd import DepsContext, ZkError, _abi, table, tracegen_host
+from zipkin_amd.shards import split
+
+pytestmark = pytest.mark.gpu
+
+
+class Shard:
+    def __init__(self, S, **kw):
+        import torch
+
+        self.table = torch.zeros(_abi.table_words(S), dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        self.ctx = DepsContext(S, table_ptr=self.table.data_ptr(), table_bytes=self.table.numel() * 8, **kw)
+
+    def close(self):
+        self.ctx.close()
+
+
+def run_sharded(cols, S, world, **kw):
+    """-> (finalized table and stats of every rank, the summed int64 table)."""
+    import torch
+
+    parts = split(cols, world)
+    shards = [Shard(S, **kw) for _ in range(world)]
+    try:
+        for sh, p in zip(shards, parts):
+            sh.ctx.accumulate(p, clustered=True, verify=True)
+            ptr, nbytes = sh.ctx.partial()
+            assert ptr == sh.table.data_ptr() and nbytes == sh.table.numel() * 8
+        for sh in shards:
+            sh.ctx.sync()
+        total = torch.stack([sh.table for sh in shards]).sum(0)  # the all-reduce's SUM
+        outs = []
+        for sh in shards:  # every rank holds the same merged buffer after the all-reduce
+            sh.table.copy_(total)
+            torch.cuda.synchronize()
+            sh.ctx.note_merged(0)
+            try:
+                outs.append((sh.ctx.finalize(), sh.ctx.stats(), None))
+            except ZkError as e:
+                outs.append((None, sh.ctx.stats(), e.status))
+        return outs, total.cpu().numpy()
+    finally:
+        for sh in shards:
+            sh.close()
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_sharded_tables_sum_to_the_oracle(gpu, world):
+    S = 500
+    cols = tracegen_host(41, 60_000, max_depth=6, num_services=S)
+    ref = oracle.aggregate(cols, S)
+    outs, total = run_sharded(cols, S, world)
+    for got, st, status in outs:
+        assert status is None
+        assert_parity(got, st, ref)
+        assert st["records"] == len(cols) and st["not_clustered"] == 0
+    # the device layout decodes to the oracle's exact power sums (table.py is the host view)
+    dec = table.decode(total, S)
+    want = {}
+    for c in ref.present_cells():
+        want[(int(c) // S, int(c) % S)] = ref.power_sums(int(c))
+    assert dec == want
+    tail = table.tail_stats(total, S)
+    for k, v in ref.stats.items():
+        if k != "spilled_traces":
+            assert tail[k] == v, k
+
+
+def test_sharded_equals_one_shard_bit_for_bit(gpu):
+    S = 57
+    cols = tracegen_host(42, 30_000, max_depth=7, num_services=S)
+    one, t1 = run_sharded(cols, S, 1)
+    eight, t8 = run_sharded(cols, S, 8)
+    # limbs hold sums of 32-bit chunks, so their split depends on how links were grouped; the
+    # values they encode (the exact power sums) do not
+    assert table.decode(t1, S) == table.decode(t8, S)
+    for k in ("m0", "m1", "m2", "m3", "m4", "present"):
+        assert np.array_equal(getattr(one[0][0], k), getattr(eight[0][0], k)), k
+
+
+def test_strict_error_is_decided_from_the_merged_counters(gpu):
+    """A no-service pair on ONE shard fails finalize on EVERY rank (reference: the whole job fails
+    on None.get, ZipkinAggregateJob.scala:36-37), so no rank runs ahead into the next collective."""
+    S = 9
+    good = tracegen_host(43, 2000, max_depth=4, num_services=S)
+    bad = cols_from_rows([(7, 70, 0, 1, 9, 0, SERVER),
+                          (7, 71, 70, 2, 4, 0, _abi.ZK_F_HAS_ANNOTATIONS | 1 | (1 << 12) | (1 << 14))])
+    from zipkin_amd.columns import SpanColumns
+
+    cols = SpanColumns.concat([good, bad])
+    outs, _ = run_sharded(cols, S, 4, strict=True)
+    assert [s for _, _, s in outs] == [_abi.ZK_ERR_NO_SERVICE] * 4
+    assert all(st["no_service"] == 1 for _, st, _ in outs)
+    outs, _ = run_sharded(cols, S, 4, strict=False)
+    assert all(s is None for _, _, s in outs)
+    ref = oracle.aggregate(cols, S)
+    for got, st, _ in outs:
+        assert_parity(got, st, ref)
+
+
+def test_accumulate_after_merge_uses_local_counters_again(gpu):
+    S = 20
+    a = tracegen_host(44, 1000, max_depth=5, num_services=S)
+    sh = Shard(S)
+    try:
+        sh.ctx.accumulate(a)
+        sh.ctx.partial()
+        sh.ctx.sync()
+        sh.ctx.note_merged(0)
+        assert sh.ctx.stats()["records"] == len(a)
+        sh.ctx.reset()
+        sh.ctx.accumulate(a)
+        got = sh.ctx.finalize()
+        assert_parity(got, sh.ctx.stats(), oracle.aggregate(a, S))
+    finally:
+        sh.close()

@@ -39,8 +39,15 @@ ZK_F_SS_SHIFT = 14
 
 ZK_BATCH_DEVICE_PTRS = 1 << 0
 ZK_BATCH_TRACE_CLUSTERED = 1 << 1
+ZK_BATCH_VERIFY_TRACES = 1 << 2
 
 LIMBS_PER_CELL = 16
+TABLE_TAIL_WORDS = 16  # the folded zk_stats counters after the S*S cells (ZK_TABLE_BYTES)
+
+
+def table_words(num_services: int) -> int:
+    """u64 words of the exact accumulator + counter tail: ZK_TABLE_BYTES(S) / 8."""
+    return num_services * num_services * LIMBS_PER_CELL + TABLE_TAIL_WORDS
 
 
 class ZkLibraryError(RuntimeError):
@@ -98,8 +105,9 @@ class zk_stats(C.Structure):
             "duration_range",
             "service_range",
             "trace_too_large",
+            "not_clustered",
         )
-    ] + [("reserved", C.c_uint64 * 3)]
+    ] + [("reserved", C.c_uint64 * 2)]
 
     def as_dict(self) -> dict:
         return {k: int(getattr(self, k)) for k, _ in self._fields_ if k != "reserved"}

@@ -1,8 +1,9 @@
 """DepsContext: one device-resident zipkin-aggregate accumulator (a zk_ctx).
 
-Mirrors the compute half of ZipkinAggregateJob.scala:20-43: `accumulate` takes trace-clustered
-span fragment batches, `finalize` produces the dense (parent, child) -> Moments table that the
-job would turn into one Dependencies record.
+Mirrors the compute half of ZipkinAggregateJob.scala:20-43: `accumulate` takes span fragment
+batches (in any order, like the reference's shuffles; `clustered=True` skips the device clustering
+pass for batches whose traces are already contiguous), `finalize` produces the dense
+(parent, child) -> Moments table that the job would turn into one Dependencies record.
 """
 from __future__ import annotations
 
@@ -105,15 +106,25 @@ class DepsContext:
     def reset(self) -> None:
         self._check(self._L.zk_deps_reset(self._h))
 
-    def accumulate(self, cols, *, clustered: bool = True, n: int | None = None) -> None:
+    def accumulate(self, cols, *, clustered: bool = False, verify: bool = True, n: int | None = None) -> None:
+        """One batch of span fragments.
+
+        clustered: the caller promises that every trace's fragments are adjacent (Cassandra
+          row-per-trace reads); otherwise the device clusters the batch first (radix sort by traceId).
+        verify: check exactly, on the device, that no trace recurs after its run ended -- within the
+          batch or across accumulate calls since the last reset (a split trace would be mis-joined);
+          finalize then raises ZK_ERR_NOT_CLUSTERED. Costs one extra read of the traceId column.
+        """
         flags = _abi.ZK_BATCH_TRACE_CLUSTERED if clustered else 0
+        if verify:
+            flags |= _abi.ZK_BATCH_VERIFY_TRACES
         if isinstance(cols, DeviceColumns):
             ab = cols.abi(n)
             flags |= _abi.ZK_BATCH_DEVICE_PTRS
         elif isinstance(cols, SpanColumns):
             ab = cols.abi()
         else:
-            ab = cols  # a prepared zk_span_cols + caller sets flags through `clustered`
+            ab = cols  # a prepared zk_span_cols; flags from `clustered` / `verify`
         self._check(self._L.zk_deps_accumulate(self._h, C.byref(ab), flags))
 
     def finalize(self, out_device=None) -> LinkTable | None:
@@ -154,11 +165,14 @@ class DepsContext:
         self._check(self._L.zk_ctx_sync(self._h))
 
     def partial(self) -> tuple[int, int]:
+        """(device pointer, bytes) of the exact table + counter tail, counters folded in (enqueued
+        on the ctx stream): the buffer a SUM all-reduce merges across shards."""
         p, b = C.c_void_p(), C.c_uint64()
         self._check(self._L.zk_deps_partial(self._h, C.byref(p), C.byref(b)))
         return int(p.value or 0), int(b.value)
 
     def note_merged(self, total_records: int) -> None:
+        """The table now holds the merged job: finalize/stats use the merged counters."""
         self._check(self._L.zk_deps_note_merged(self._h, total_records))
 
     def tracegen_device(self, params: _abi.zk_tracegen_params, out: DeviceColumns) -> tuple[int, int]:

@@ -6,10 +6,12 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <new>
 #include <string>
 #include <utility>
 #include <vector>
 
+#include "zk_cluster.h"
 #include "zk_internal.h"
 #include "zk_rt_internal.h"
 
@@ -57,6 +59,17 @@ struct zk_ctx {
     // finalize staging for host outputs
     void* fin_stage = nullptr;
     uint64_t records_since_reset = 0;
+    bool merged = false;                  // the table holds the all-reduced job (zk_deps_note_merged)
+    // clustering pass for unclustered batches (zk_cluster.hip)
+    uint8_t* cl_cols = nullptr;           // 7 aligned columns of cl_cap records
+    uint64_t cl_cap = 0;
+    uint32_t* cl_idx = nullptr;
+    void* cl_temp = nullptr;
+    size_t cl_temp_bytes = 0;
+    // traceIds accumulated since reset (ZK_BATCH_VERIFY_TRACES): tset_slots + 1 u64
+    uint64_t* tset = nullptr;
+    uint64_t tset_slots = 0;
+    uint64_t tset_records = 0;
     std::string err;
     // bound realtime sketch (zk_rt_bind)
     zk_rt* rt = nullptr;
@@ -82,6 +95,19 @@ zk_status hip_fail(zk_ctx* c, hipError_t e, const char* where) {
         hipError_t _e = (call);                             \
         if (_e != hipSuccess) return hip_fail(ctx, _e, #call); \
     } while (0)
+
+// No C++ exception crosses the C ABI (zkagg.h: "never throws or aborts").
+#define ZK_TRY try {
+#define ZK_CATCH(ctx)                                                                      \
+    }                                                                                      \
+    catch (const std::bad_alloc&) {                                                        \
+        return fail(ctx, ZK_ERR_CAPACITY, "host allocation failed");                       \
+    }                                                                                      \
+    catch (...) {                                                                          \
+        return fail(ctx, ZK_ERR_INVALID_ARG, "unexpected host exception");                 \
+    }
+
+uint64_t table_bytes(uint32_t S) { return (uint64_t)S * S * kLimbs * 8 + kTableTailBytes; }
 
 EventPair take_pair(zk_ctx* c) {
     EventPair p;
@@ -149,7 +175,12 @@ zk_status stats_sum(zk_ctx* c, uint64_t out[ST_N]) {
     const size_t bytes = (size_t)kStatShards * ST_N * 8;
     if (!c->h_stats) ZK_HIP(c, hipHostMalloc((void**)&c->h_stats, bytes, hipHostMallocDefault));
     if (!c->ev_stats) ZK_HIP(c, hipEventCreateWithFlags(&c->ev_stats, hipEventDisableTiming));
-    ZK_HIP(c, hipMemcpyAsync(c->h_stats, c->stats, bytes, hipMemcpyDeviceToHost, c->stream));
+    const uint64_t cells = (uint64_t)c->S * c->S;
+    if (c->merged)  // the all-reduced job-wide counters in the table's tail
+        ZK_HIP(c, hipMemcpyAsync(c->h_stats, c->table + cells * kLimbs, kTableTailBytes, hipMemcpyDeviceToHost,
+                                 c->stream));
+    else
+        ZK_HIP(c, hipMemcpyAsync(c->h_stats, c->stats, bytes, hipMemcpyDeviceToHost, c->stream));
     ZK_HIP(c, hipEventRecord(c->ev_stats, c->stream));
     hipError_t q;
     while ((q = hipEventQuery(c->ev_stats)) == hipErrorNotReady) {
@@ -157,13 +188,87 @@ zk_status stats_sum(zk_ctx* c, uint64_t out[ST_N]) {
     if (q != hipSuccess) return fail(c, ZK_ERR_HIP, std::string("stats copy: ") + hipGetErrorString(q));
     const unsigned long long* h = c->h_stats;
     for (int s = 0; s < ST_N; ++s) out[s] = 0;
-    for (int sh = 0; sh < kStatShards; ++sh)
+    for (int sh = 0; sh < (c->merged ? 1 : kStatShards); ++sh)
         for (int s = 0; s < ST_N; ++s) out[s] += h[(size_t)sh * ST_N + s];
     return ZK_OK;
 }
 
 bool cols_ok(const zk_span_cols* c) {
     return c && c->trace_id && c->span_id && c->parent_id && c->first_ts && c->last_ts && c->service_id && c->flags;
+}
+
+// 7 columns of n records carved from one buffer, every column on a 256-byte boundary
+uint64_t carved_bytes(uint64_t n) { return 5 * ((n * 8 + 255) & ~255ull) + 2 * ((n * 4 + 255) & ~255ull); }
+SpanColsMut carve_cols(uint8_t* p, uint64_t n) {
+    auto take = [&](uint64_t bytes) {
+        uint8_t* q = p;
+        p += (bytes + 255) & ~255ull;
+        return q;
+    };
+    SpanColsMut m;
+    m.trace_id = (uint64_t*)take(n * 8);
+    m.span_id = (uint64_t*)take(n * 8);
+    m.parent_id = (uint64_t*)take(n * 8);
+    m.first_ts = (int64_t*)take(n * 8);
+    m.last_ts = (int64_t*)take(n * 8);
+    m.service_id = (uint32_t*)take(n * 4);
+    m.flags = (uint32_t*)take(n * 4);
+    return m;
+}
+
+// clustering pass: d (any order) -> ctx-owned trace-clustered columns
+zk_status cluster_batch(zk_ctx* c, SpanColsDev* d) {
+    const uint64_t n = d->n;
+    if (n > 0xFFFFFFFFull) return fail(c, ZK_ERR_CAPACITY, "an unclustered batch is limited to 2^32-1 records");
+    if (n > c->cl_cap) {
+        hipFree(c->cl_cols);
+        hipFree(c->cl_idx);
+        hipFree(c->cl_temp);
+        c->cl_cols = nullptr;
+        c->cl_idx = nullptr;
+        c->cl_temp = nullptr;
+        c->cl_cap = 0;
+        size_t tb = 0;
+        ZK_HIP(c, cluster_temp_bytes(n, &tb));
+        ZK_HIP(c, hipMalloc(&c->cl_cols, carved_bytes(n)));
+        ZK_HIP(c, hipMalloc(&c->cl_idx, n * sizeof(uint32_t)));
+        ZK_HIP(c, hipMalloc(&c->cl_temp, tb));
+        c->cl_temp_bytes = tb;
+        c->cl_cap = n;
+    }
+    const SpanColsMut m = carve_cols(c->cl_cols, n);
+    ZK_HIP(c, launch_cluster(*d, m, c->cl_idx, c->cl_temp, c->cl_temp_bytes, c->stream));
+    *d = SpanColsDev{m.trace_id, m.span_id, m.parent_id, m.first_ts, m.last_ts, m.service_id, m.flags, n};
+    return ZK_OK;
+}
+
+uint64_t pow2_at_least(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+// ZK_BATCH_VERIFY_TRACES: grow the traceId set (load <= 1/2 even if every record were its own
+// trace) and insert the batch's trace runs
+zk_status verify_batch(zk_ctx* c, const SpanColsDev& d) {
+    const uint64_t need = pow2_at_least(2 * (c->tset_records + d.n) > (1ull << 16) ? 2 * (c->tset_records + d.n)
+                                                                                   : (1ull << 16));
+    if (need > c->tset_slots) {
+        uint64_t* nt = nullptr;
+        ZK_HIP(c, hipMalloc(&nt, (need + 1) * 8));
+        ZK_HIP(c, hipMemsetAsync(nt, 0, (need + 1) * 8, c->stream));
+        if (c->tset) {
+            ZK_HIP(c, launch_trace_set_rehash(c->tset, c->tset_slots, nt, need, c->stream));
+            ZK_HIP(c, hipStreamSynchronize(c->stream));
+            hipFree(c->tset);
+        }
+        c->tset = nt;
+        c->tset_slots = need;
+    }
+    ZK_HIP(c, launch_trace_set_insert(d.trace_id, d.n, c->tset, c->tset_slots, &c->stats[ST_NOT_CLUSTERED],
+                                      c->stream));
+    c->tset_records += d.n;
+    return ZK_OK;
 }
 
 }  // namespace
@@ -193,6 +298,7 @@ const char* zk_status_str(zk_status s) {
 const char* zk_last_error(const zk_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
 zk_status zk_ctx_create(const zk_config* cfg, zk_ctx** out) {
+    ZK_TRY
     if (!cfg || !out) return ZK_ERR_INVALID_ARG;
     *out = nullptr;
     if (cfg->num_services == 0 || cfg->num_services > kMaxServices) return ZK_ERR_INVALID_ARG;
@@ -222,16 +328,15 @@ zk_status zk_ctx_create(const zk_config* cfg, zk_ctx** out) {
             c->own_stream = true;
         }
     }
-    const uint64_t cells = (uint64_t)c->S * c->S;
     if (cfg->table) {
-        if (cfg->table_bytes < cells * kLimbs * 8) {
-            delete c;
+        if (cfg->table_bytes < table_bytes(c->S)) {
+            zk_ctx_destroy(c);
             return ZK_ERR_INVALID_ARG;
         }
         c->table = (uint64_t*)cfg->table;
         c->own_table = false;
     } else if (e == hipSuccess) {
-        e = hipMalloc(&c->table, cells * kLimbs * 8);
+        e = hipMalloc(&c->table, table_bytes(c->S));
     }
     if (e == hipSuccess) e = hipMalloc(&c->stats, (size_t)kStatShards * ST_N * 8);
     if (e == hipSuccess) e = hipMalloc(&c->spill_count, 256);
@@ -244,6 +349,7 @@ zk_status zk_ctx_create(const zk_config* cfg, zk_ctx** out) {
     }
     *out = c;
     return ZK_OK;
+    ZK_CATCH(nullptr)
 }
 
 zk_status zk_ctx_destroy(zk_ctx* c) {
@@ -252,6 +358,7 @@ zk_status zk_ctx_destroy(zk_ctx* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->rt) rt_set_stream(c->rt, nullptr);
     if (c->own_table) hipFree(c->table);
+    c->table = nullptr;
     hipFree(c->stats);
     if (c->h_stats) hipHostFree(c->h_stats);
     if (c->ev_stats) hipEventDestroy(c->ev_stats);
@@ -266,6 +373,10 @@ zk_status zk_ctx_destroy(zk_ctx* c) {
     hipFree(c->sorted);
     hipFree(c->stage);
     hipFree(c->fin_stage);
+    hipFree(c->cl_cols);
+    hipFree(c->cl_idx);
+    hipFree(c->cl_temp);
+    hipFree(c->tset);
     for (auto* v : {&c->ev_free, &c->ev_join, &c->ev_reduce, &c->ev_spill, &c->ev_fin})
         for (auto& p : *v) {
             hipEventDestroy(p.a);
@@ -286,17 +397,21 @@ zk_status zk_ctx_sync(zk_ctx* c) {
 zk_status zk_deps_reset(zk_ctx* c) {
     if (!c) return ZK_ERR_INVALID_ARG;
     ZK_HIP(c, hipSetDevice(c->device));
-    ZK_HIP(c, hipMemsetAsync(c->table, 0, (size_t)c->S * c->S * kLimbs * 8, c->stream));
+    ZK_HIP(c, hipMemsetAsync(c->table, 0, table_bytes(c->S), c->stream));
     ZK_HIP(c, hipMemsetAsync(c->stats, 0, (size_t)kStatShards * ST_N * 8, c->stream));
+    if (c->tset && c->tset_records) ZK_HIP(c, hipMemsetAsync(c->tset, 0, (c->tset_slots + 1) * 8, c->stream));
+    c->tset_records = 0;
     c->records_since_reset = 0;
+    c->merged = false;
     return ZK_OK;
 }
 
 zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags) {
     if (!c) return ZK_ERR_INVALID_ARG;
+    ZK_TRY
     if (!cols) return fail(c, ZK_ERR_INVALID_ARG, "null columns");
-    if (!(flags & ZK_BATCH_TRACE_CLUSTERED))
-        return fail(c, ZK_ERR_NOT_CLUSTERED, "accumulate requires ZK_BATCH_TRACE_CLUSTERED batches");
+    if (flags & ~(ZK_BATCH_DEVICE_PTRS | ZK_BATCH_TRACE_CLUSTERED | ZK_BATCH_VERIFY_TRACES))
+        return fail(c, ZK_ERR_INVALID_ARG, "unknown batch flag");
     const uint64_t n = cols->n;
     if (n == 0) return ZK_OK;
     if (!cols_ok(cols)) return fail(c, ZK_ERR_INVALID_ARG, "null column pointer");
@@ -304,6 +419,10 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
     if (join && c->records_since_reset + n > kMaxRecordsSinceReset)
         return fail(c, ZK_ERR_CAPACITY, "more than 2^32-1 records since reset");
     ZK_HIP(c, hipSetDevice(c->device));
+    if (c->merged) {  // accumulating into a merged table: back to this ctx's own counters
+        ZK_HIP(c, hipMemsetAsync(c->stats, 0, (size_t)kStatShards * ST_N * 8, c->stream));
+        c->merged = false;
+    }
     SpanColsDev d{cols->trace_id, cols->span_id, cols->parent_id, cols->first_ts,
                   cols->last_ts,  cols->service_id, cols->flags,   n};
     if (!(flags & ZK_BATCH_DEVICE_PTRS)) {
@@ -336,12 +455,19 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
         ZK_HIP(c, hipMemcpyAsync(flg, cols->flags, n * 4, hipMemcpyHostToDevice, c->stream));
         d = SpanColsDev{tid, sid, pid, fts, lts, svc, flg, n};
     }
-    if (flags & ZK_BATCH_DEVICE_PTRS) {
+    if (!(flags & ZK_BATCH_TRACE_CLUSTERED)) {
+        const zk_status cs = cluster_batch(c, &d);
+        if (cs != ZK_OK) return cs;
+    } else if (flags & ZK_BATCH_DEVICE_PTRS) {
         // K1 reads two records per lane with one 16-byte (u64 columns) / 8-byte (u32) load
         if (!aligned(d.trace_id, 16) || !aligned(d.span_id, 16) || !aligned(d.parent_id, 16) ||
             !aligned(d.first_ts, 16) || !aligned(d.last_ts, 16) || !aligned(d.service_id, 8) ||
             !aligned(d.flags, 8))
             return fail(c, ZK_ERR_INVALID_ARG, "device columns must be 16-byte (u64) / 8-byte (u32) aligned");
+    }
+    if (flags & ZK_BATCH_VERIFY_TRACES) {
+        const zk_status vs = verify_batch(c, d);
+        if (vs != ZK_OK) return vs;
     }
     uint32_t grid = 0;
     uint64_t per_wg = 0, stride = 0;
@@ -424,10 +550,12 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
     }
     if (join) c->records_since_reset += n;
     return ZK_OK;
+    ZK_CATCH(c)
 }
 
 zk_status zk_deps_finalize(zk_ctx* c, const zk_link_table* out) {
     if (!c) return ZK_ERR_INVALID_ARG;
+    ZK_TRY
     if (!out || !out->m0 || !out->m1 || !out->m2 || !out->m3 || !out->m4 || !out->present)
         return fail(c, ZK_ERR_INVALID_ARG, "null output array");
     ZK_HIP(c, hipSetDevice(c->device));
@@ -467,11 +595,14 @@ zk_status zk_deps_finalize(zk_ctx* c, const zk_link_table* out) {
     if (s[ST_TOO_LARGE]) return fail(c, ZK_ERR_TRACE_TOO_LARGE, "trace longer than max_trace_records skipped");
     if (s[ST_SPILL_OVERFLOW])
         return fail(c, ZK_ERR_CAPACITY, "spill list overflow");
+    if (s[ST_NOT_CLUSTERED])
+        return fail(c, ZK_ERR_NOT_CLUSTERED, "a trace was split into non-adjacent runs or over two batches");
     if (s[ST_SVC_RANGE]) return fail(c, ZK_ERR_SERVICE_RANGE, "record with service_id >= num_services");
     if (s[ST_DUR_RANGE]) return fail(c, ZK_ERR_DURATION_RANGE, "link with duration >= 2^40 us dropped");
     if (c->strict && s[ST_NO_SERVICE])
         return fail(c, ZK_ERR_NO_SERVICE, "joined span without a service name (reference: None.get)");
     return ZK_OK;
+    ZK_CATCH(c)
 }
 
 zk_status zk_ctx_stats(zk_ctx* c, zk_stats* out) {
@@ -483,11 +614,13 @@ zk_status zk_ctx_stats(zk_ctx* c, zk_stats* out) {
     memset(out, 0, sizeof(*out));
     uint64_t* o = &out->records;
     for (int i = 0; i < ST_TOO_LARGE + 1; ++i) o[i] = s[i];
+    out->not_clustered = s[ST_NOT_CLUSTERED];
     return ZK_OK;
 }
 
 zk_status zk_ctx_timing(zk_ctx* c, zk_timing* out) {
     if (!c || !out) return ZK_ERR_INVALID_ARG;
+    ZK_TRY
     ZK_HIP(c, hipSetDevice(c->device));
     ZK_HIP(c, hipStreamSynchronize(c->stream));
     auto drain = [&](std::vector<EventPair>& v, double* last, double* total, uint64_t* calls) {
@@ -507,20 +640,34 @@ zk_status zk_ctx_timing(zk_ctx* c, zk_timing* out) {
     drain(c->ev_fin, &c->tm.finalize_ms, nullptr, nullptr);
     *out = c->tm;
     return ZK_OK;
+    ZK_CATCH(c)
 }
 
 zk_status zk_deps_partial(zk_ctx* c, void** dev_ptr, uint64_t* bytes) {
     if (!c || !dev_ptr || !bytes) return ZK_ERR_INVALID_ARG;
+    ZK_HIP(c, hipSetDevice(c->device));
+    if (!c->merged)  // a merged tail already holds the job-wide counters
+        ZK_HIP(c, launch_stats_fold(c->stats, (unsigned long long*)(c->table + (uint64_t)c->S * c->S * kLimbs),
+                                    c->stream));
     *dev_ptr = c->table;
-    *bytes = (uint64_t)c->S * c->S * kLimbs * 8;
+    *bytes = table_bytes(c->S);
     return ZK_OK;
 }
 
 zk_status zk_deps_note_merged(zk_ctx* c, uint64_t total_records) {
     if (!c) return ZK_ERR_INVALID_ARG;
+    if (total_records == 0) {  // take it from the all-reduced counter tail
+        ZK_HIP(c, hipSetDevice(c->device));
+        unsigned long long rec = 0;
+        ZK_HIP(c, hipMemcpyAsync(&rec, c->table + (uint64_t)c->S * c->S * kLimbs + ST_RECORDS, 8,
+                                 hipMemcpyDeviceToHost, c->stream));
+        ZK_HIP(c, hipStreamSynchronize(c->stream));
+        total_records = rec;
+    }
     if (total_records > kMaxRecordsSinceReset)
         return fail(c, ZK_ERR_CAPACITY, "merged table exceeds 2^32-1 records");
     c->records_since_reset = total_records;
+    c->merged = true;
     return ZK_OK;
 }
 

@@ -48,9 +48,14 @@ enum Stat : int {
     ST_TOO_LARGE,
     ST_RT_DUR_RANGE,     // sketch items dropped for a duration >= 2^40 us (not in zk_stats)
     ST_SPILL_OVERFLOW,   // spill-list pushes past its capacity (cannot happen: one per tile at most)
+    ST_NOT_CLUSTERED,    // trace segments whose traceId was already accumulated (ZK_BATCH_VERIFY_TRACES)
     ST_N = 16
 };
 constexpr int kStatShards = 256;  // stats buffer = kStatShards x ST_N u64
+// the exact table is followed by a tail of ST_N u64: the folded counters (zk_deps_partial), so one
+// SUM all-reduce of table + tail gives every rank the job-wide counters as well
+constexpr uint64_t kTableTailBytes = ST_N * 8;
+static_assert(ST_NOT_CLUSTERED < ST_N, "stat slots");
 
 struct SpanColsDev {
     const uint64_t* trace_id;

@@ -16,11 +16,21 @@ from . import _abi
 from .columns import SpanColumns
 
 
+def _mix64(z: np.ndarray) -> np.ndarray:
+    """splitmix64 finalizer, vectorised (zk_mix64 in zk_tracegen.h; uint64 wrap-around)."""
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
 def shard_of(trace_ids: np.ndarray, world: int) -> np.ndarray:
-    """Shard index of every traceId (the same hash the device tracegen and ingest use)."""
-    L = _abi.lib()
+    """Shard index of every traceId: zk_trace_shard = mix64(traceId) % world (the hash the device
+    tracegen and ingest use; tests/test_multirank.py checks it against the library)."""
     tids = np.asarray(trace_ids, dtype=np.uint64)
-    return np.fromiter((L.zk_trace_shard(int(t), world) for t in tids), dtype=np.uint32, count=len(tids))
+    if world <= 1:
+        return np.zeros(len(tids), np.uint32)
+    return (_mix64(tids) % np.uint64(world)).astype(np.uint32)
 
 
 def split(cols: SpanColumns, world: int) -> list[SpanColumns]:
@@ -72,8 +82,11 @@ def allreduce_stats(stats: dict, device="cpu", group=None) -> dict:
 class ShardedDeps:
     """One rank of the sharded job: a DepsContext over a caller-owned (all-reducible) table.
 
-    step(cols): reset -> accumulate this rank's shard -> SUM all-reduce -> finalize. With
-    world == 1 the all-reduce is skipped. Every rank ends with the same finalized table.
+    step(cols): reset -> accumulate this rank's shard -> fold the counters into the table's tail
+    (zk_deps_partial) -> ONE SUM all-reduce of limbs + counters -> note_merged -> finalize. With
+    world == 1 the all-reduce is skipped. Every rank ends with the same finalized table AND the
+    same status: finalize decides errors from the job-wide counters, so a strict-mode failure on
+    one shard fails every rank instead of leaving the others blocked in the next collective.
     """
 
     def __init__(self, num_services: int, *, device: int = 0, stream=None, timing: bool = False,
@@ -89,19 +102,21 @@ class ShardedDeps:
         dev = torch.device("cuda", device)
         # the library's kernels and the RCCL all-reduce must be ordered on ONE stream
         self.stream = torch.cuda.Stream(device=dev) if stream is None else stream
-        self.table = torch.zeros(num_services * num_services * 16, dtype=torch.int64, device=dev)
+        self.table = torch.zeros(_abi.table_words(num_services), dtype=torch.int64, device=dev)
         torch.cuda.current_stream(dev).synchronize()  # the zeroed table, before the library's stream
         self.ctx = DepsContext(num_services, device=device, stream=self.stream.cuda_stream, timing=timing,
                                table_ptr=self.table.data_ptr(), table_bytes=self.table.numel() * 8, ablate=ablate)
 
-    def step(self, cols, total_records: int | None = None, out_device=None):
+    def step(self, cols, total_records: int | None = None, out_device=None, *, clustered: bool = False,
+             verify: bool = True):
         import torch
 
         self.ctx.reset()
-        self.ctx.accumulate(cols)
+        self.ctx.accumulate(cols, clustered=clustered, verify=verify)
         if self.world > 1:
+            self.ctx.partial()  # counters -> table tail, on the ctx stream
             with torch.cuda.stream(self.stream):  # RCCL waits for the accumulate on this stream
                 allreduce_table(self.table, self.group)
-            if total_records is not None:
-                self.ctx.note_merged(total_records)
+            # 0: the library reads the merged record count from the all-reduced tail
+            self.ctx.note_merged(total_records or 0)
         return self.ctx.finalize(out_device=out_device)

@@ -28,9 +28,14 @@ def decode_cell(limbs) -> tuple[int, int, int, int, int]:
     return (v[0], *sums)
 
 
+TAIL = 16  # counter words after the cells (zk_deps_partial: the folded zk_stats, in field order)
+
+
 def decode(table: np.ndarray, num_services: int) -> dict:
-    """{(parent, child): (n, S1, S2, S3, S4)} for every cell with n > 0."""
-    t = np.asarray(table).reshape(num_services * num_services, LIMBS).view(np.uint64)
+    """{(parent, child): (n, S1, S2, S3, S4)} for every cell with n > 0 (the counter tail, if
+    present, is ignored: see `tail_stats`)."""
+    cells = num_services * num_services
+    t = np.asarray(table).reshape(-1)[: cells * LIMBS].reshape(cells, LIMBS).view(np.uint64)
     out = {}
     for c in np.flatnonzero(t[:, 0]):
         out[(int(c // num_services), int(c % num_services))] = decode_cell(t[c])
@@ -50,9 +55,30 @@ def encode_cell(n: int, s1: int, s2: int, s3: int, s4: int) -> np.ndarray:
     return out
 
 
-def encode(sums: dict, num_services: int) -> np.ndarray:
-    """Dense S*S*16 int64 table (the device dtype) from {(parent, child): (n, S1..S4)}."""
+def encode(sums: dict, num_services: int, stats: dict | None = None) -> np.ndarray:
+    """Dense int64 table in the device layout (S*S*16 limbs + the 16-word counter tail) from
+    {(parent, child): (n, S1..S4)} and optional zk_stats counters."""
     t = np.zeros((num_services * num_services, LIMBS), np.uint64)
     for (p, c), v in sums.items():
         t[p * num_services + c] = encode_cell(*v)
-    return t.reshape(-1).view(np.int64)
+    tail = np.zeros(TAIL, np.uint64)
+    if stats:
+        for i, k in enumerate(STAT_FIELDS):
+            tail[i] = stats.get(k, 0)
+    return np.concatenate([t.reshape(-1), tail]).view(np.int64)
+
+
+# zk_stats field order = the device counter slots (zk_internal.h Stat), as folded into the tail
+STAT_FIELDS = ("records", "merged_spans", "valid_spans", "invalid_spans", "child_spans", "joined_links",
+               "missing_parent", "no_service", "ambiguous", "spilled_traces", "duration_range", "service_range",
+               "trace_too_large")
+_NOT_CLUSTERED_SLOT = 15
+
+
+def tail_stats(table: np.ndarray, num_services: int) -> dict:
+    """zk_stats counters from the tail of a table returned by zk_deps_partial."""
+    cells = num_services * num_services
+    tail = np.asarray(table).reshape(-1)[cells * LIMBS : cells * LIMBS + TAIL].view(np.uint64)
+    out = {k: int(tail[i]) for i, k in enumerate(STAT_FIELDS)}
+    out["not_clustered"] = int(tail[_NOT_CLUSTERED_SLOT])
+    return out
