@@ -52,16 +52,32 @@ typedef struct zk_dep_link {
 #define ZK_TIME_TOP    INT64_MAX
 #define ZK_TIME_BOTTOM INT64_MIN
 
-/* getDependencies result shapes of the reference backends:
- *   ZK_STORE_ANORM   rows with start_ts >= start AND end_ts <= end, links concatenated newest
- *                    record first; result times = the query window (AnormAggregates.scala:52-76)
- *   ZK_STORE_SUMMED  the same containment window, records Monoid-summed: start = min, end = max,
- *                    links merged per (parent, child) with MomentsGroup.plus; no record ->
- *                    the monoid zero (CassandraAggregates.scala:54-74, HBaseAggregates.scala:39-53)
- * Defaults when a bound is absent (Option = None): start = now - 1 day, end = now
- * (AnormAggregates.scala:53-54; `now_us` is passed in so callers and tests control Time.now). */
-#define ZK_STORE_ANORM  0u
-#define ZK_STORE_SUMMED 1u
+/* Storage semantics of the reference backends (each mode reproduces one, quirks included):
+ *   ZK_STORE_ANORM      one row per stored record; getDependencies returns the links of the rows
+ *                       with start_ts >= start AND end_ts <= end, newest record first, times = the
+ *                       query window; absent bounds: start = now - 1 day, end = now
+ *                       (AnormAggregates.scala:52-76; `now_us` is passed in so callers and tests
+ *                       control Time.now)
+ *   ZK_STORE_CASSANDRA  row key = startTime floored to the day (us); a store CLOBBERS that row
+ *                       (CassandraAggregates.scala:111-116,122-136). getDependencies walks every
+ *                       row and drops a column only if its name -- the index 0, compared with the
+ *                       bounds in us (:58-61) -- exceeds a given bound, i.e. it returns every row
+ *                       unless a bound is negative; rows in row-key order, Monoid-summed
+ *   ZK_STORE_HBASE      row key = Long.MaxValue - startTime in ms, a store replaces a record of the
+ *                       same ms (HBaseAggregates.scala:55-60). getDependencies scans row keys
+ *                       [MaxValue - start ms, MaxValue - end ms) (:39-53): the records with
+ *                       end ms < record start ms <= start ms (no start: from key 0; no end: to the
+ *                       last row), newest first, Monoid-summed; start < end scans nothing
+ * Monoid-summed = Dependencies monoid left fold in scan order (start = min, end = max, links merged
+ * per (parent, child) with MomentsGroup.plus); no record -> the monoid zero (ZK_TIME_TOP,
+ * ZK_TIME_BOTTOM, no links). Top-annotation lists: Anorm's are stubs (store ignored, get empty,
+ * AnormAggregates.scala:111-137); Cassandra keeps one list per (service, kind), replaced by each
+ * store (CassandraAggregates.scala:79-108,119-136); HBase writes both kinds into one family, so its getTopKeyValueAnnotations
+ * is always empty and getTopAnnotations falls through to the next service id with a list
+ * (HBaseAggregates.scala:62-110). */
+#define ZK_STORE_ANORM     0u
+#define ZK_STORE_CASSANDRA 1u
+#define ZK_STORE_HBASE     2u
 
 /* top-annotation lists (CassandraAggregates.scala:79-108: row "<service>:annotation" / ":kv") */
 #define ZK_TOP_ANNOTATIONS    0u

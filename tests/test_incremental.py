@@ -71,7 +71,7 @@ def test_watermark_empty_then_max_end():
     assert agg.watermark() == 90
 
 
-@pytest.mark.parametrize("mode", ["anorm", "summed"])
+@pytest.mark.parametrize("mode", ["anorm", "cassandra"])
 def test_incremental_runs_aggregate_each_trace_once(mode):
     services = Dictionary(NAMES)
     agg = GpuAggregates(mode, services=services)
@@ -96,11 +96,14 @@ def test_incremental_runs_aggregate_each_trace_once(mode):
     assert inc.last_selected == len(b)
     new = trace_created(both, ts_both) > tc.max()
     assert _by_key(rec2) == _expect(both, new, services)
-    assert rec2.start_time == trace_created(b, ts_b).min() and agg.count() == 2
+    # Cassandra keys records by day and clobbers the row (CassandraAggregates.scala:111-116): both
+    # runs fall on day 0, so the second record replaces the first; Anorm keeps both rows
+    rows = 2 if mode == "anorm" else 1
+    assert rec2.start_time == trace_created(b, ts_b).min() and agg.count() == rows
 
     # run 3: nothing new -> nothing stored ("already up-to-date")
     assert inc.apply(both, ts_both, num_services=S) is None
-    assert agg.count() == 2 and job.runs == [len(a), len(b)]
+    assert agg.count() == rows and job.runs == [len(a), len(b)]
 
 
 def test_incremental_trace_straddling_the_watermark_is_new_as_a_whole():
@@ -119,7 +122,7 @@ def test_incremental_trace_straddling_the_watermark_is_new_as_a_whole():
 @pytest.mark.gpu
 def test_incremental_device_job_matches_oracle():
     services = Dictionary(NAMES)
-    agg = GpuAggregates("summed", services=services)
+    agg = GpuAggregates("cassandra", services=services)
     inc = IncrementalAggregator(agg)  # device ZipkinAggregateJob
     a = tracegen_host(seed=21, num_traces=2000, max_depth=6, num_services=S)
     ts_a = _created(a, 50_000)
@@ -133,3 +136,41 @@ def test_incremental_device_job_matches_oracle():
     new = trace_created(both, ts_both) > trace_created(a, ts_a).max()
     assert _by_key(rec2) == _expect(both, new, services)
     assert inc.apply(both, ts_both, num_services=S) is None
+
+
+def test_run_without_links_still_advances_the_watermark():
+    """AnormAggregator folds from Monoid.zero and stores whenever new spans exist (:41-56), so a
+    run whose new traces join nothing still moves the watermark and is not selected again."""
+    services = Dictionary(NAMES)
+    agg = GpuAggregates("anorm", services=services)
+    job = OracleJob(services)
+    inc = IncrementalAggregator(agg, job=job)
+    roots = tracegen_host(seed=13, num_traces=50, max_depth=1, num_services=S)  # root spans only
+    ts = _created(roots, 1000)
+    rec = inc.apply(roots, ts, num_services=S)
+    assert rec is not None and rec.links == () and agg.count() == 1
+    assert agg.watermark() == trace_created(roots, ts).max()
+    assert inc.apply(roots, ts, num_services=S) is None and job.runs == [len(roots)]
+
+
+def test_record_ends_at_the_last_step_boundary():
+    """More than 10000 new records: steps = count / 10000, the record ends on the last boundary of
+    Range.Long(min, max + 1, stepSize) and later traces wait for the next run (:35-39)."""
+    services = Dictionary(NAMES)
+    agg = GpuAggregates("anorm", services=services)
+    job = OracleJob(services)
+    inc = IncrementalAggregator(agg, job=job)
+    cols = tracegen_host(seed=14, num_traces=1500, max_depth=5, num_services=S)
+    starts = np.r_[True, cols.trace_id[1:] != cols.trace_id[:-1]]
+    k = np.cumsum(starts) - 1  # trace index per record
+    ts = (1000 + 7 * k).astype(np.int64)  # one created time per trace, 7 us apart
+    tc = trace_created(cols, ts)
+    rec = inc.apply(cols, ts, num_services=S)
+    lo, hi, count = int(tc.min()), int(tc.max()), len(cols)
+    steps = max(count // 10000, 1)
+    step = (hi - lo) // steps
+    end = lo + ((hi - lo) // step) * step
+    assert count > 10000 and (rec.start_time, rec.end_time) == (lo, end)
+    assert inc.last_selected == int((tc <= end).sum())
+    rest = inc.apply(cols, ts, num_services=S)  # the traces after the boundary, exactly once
+    assert rest is None or inc.last_selected == int((tc > end).sum())

@@ -235,6 +235,35 @@ def test_fuzzed_bytes_never_crash():
         assert len(cols) + rej == len(blobs)
 
 
+@pytest.mark.parametrize("header", [b"\xff\xff\xff\xff\x0f", b"\x80\x80\x80\x10", b"\x81\x80\x80\x08\x00"])
+def test_hostile_snappy_length_is_rejected_before_allocating(header):
+    """A header announcing gigabytes (or more than the format can expand the payload to) is
+    undecodable, without the decoder allocating it (zkingest.h ZK_INGEST_MAX_FRAGMENT)."""
+    from zipkin_amd.ingest import snappy_uncompress
+
+    blob = header + b"\x00a"
+    with pytest.raises(ZkError) as e:
+        snappy_uncompress(blob)
+    assert e.value.status == _abi.ZK_ERR_INVALID_SPAN
+    cols, rej = SpanDecoder().decode([blob, T.snappy(T.span(gen_traces(1, 1)[0]))], strict=False)
+    assert rej == 1 and len(cols) == 1
+    with pytest.raises(ZkError) as e:
+        SpanDecoder().decode([blob], strict=True)
+    assert e.value.status == _abi.ZK_ERR_INVALID_SPAN
+
+
+def test_snappy_expansion_bound_admits_real_maximum():
+    """The densest legal block (runs of 64-byte copies) still decodes under the expansion bound."""
+    data = b"z" * 200_000
+    assert snappy_roundtrip(data) == data
+
+
+def snappy_roundtrip(data):
+    from zipkin_amd.ingest import snappy_uncompress
+
+    return snappy_uncompress(T.snappy(data))
+
+
 def test_empty_batch_and_bad_arguments():
     cols, rej = SpanDecoder().decode([])
     assert len(cols) == 0 and rej == 0

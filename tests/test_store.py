@@ -145,21 +145,22 @@ def test_aggregates_sql_fixture_round_trips_exactly():
     links = tuple(link(l["parent"], l["child"], Moments(l["m0"], l["m1"], l["m2"], l["m3"], l["m4"]))
                   for l in fx["links"])
     assert len(links) == 150
-    for mode in ("anorm", "summed"):
+    for mode in ("anorm", "cassandra", "hbase"):
         agg = GpuAggregates(mode, clock=lambda: NOW)
         agg.storeDependencies(Dependencies(row["start_ts"], row["end_ts"], links))
-        got = agg.getDependencies(0, row["end_ts"])
+        # hbase: the scan starts at MaxValue - start ms and runs to the end without an end bound
+        got = agg.getDependencies(0, None if mode == "hbase" else row["end_ts"])
         assert got.start_time == (0 if mode == "anorm" else row["start_ts"])
         assert Counter(got.links) == Counter(links)
         assert all(_same_bits(a.duration_moments, b.duration_moments)
                    for a, b in zip(sorted(got.links, key=str), sorted(links, key=str)))
 
 
-def test_summed_mode_equals_monoid_fold_of_the_oracle():
-    rng = random.Random(3)
+def _random_records(seed, n, start_of):
+    rng = random.Random(seed)
     names = ["tfe", "mobileweb", "Gizmoduck", "tflock", "cassie"]
     records = []
-    for r in range(6):
+    for r in range(n):
         ls = {}
         for _ in range(rng.randrange(1, 6)):
             p, c = rng.sample(names, 2)
@@ -167,26 +168,82 @@ def test_summed_mode_equals_monoid_fold_of_the_oracle():
             for _ in range(rng.randrange(1, 5)):
                 m = m.plus(Moments.of(rng.randrange(1, 100_000)))
             ls[(p, c)] = m
-        records.append(Dependencies(r * 3600_000_000, (r + 1) * 3600_000_000,
+        records.append(Dependencies(start_of(r), start_of(r) + 3600_000_000,
                                     tuple(link(p, c, m) for (p, c), m in ls.items())))
-    agg = GpuAggregates("summed", clock=lambda: NOW)
-    for d in records:
-        agg.storeDependencies(d)
-    got = agg.getDependencies(0, 10 * 3600_000_000)
-    # the oracle's restatement of Dependencies.plus, reduceLeft over the rows
+    return records
+
+
+def _oracle_sum(records):
+    """The oracle's restatement of Dependencies.plus, reduceLeft over the records in order."""
     acc = None
     for d in records:
         od = ODeps(d.start_time, d.end_time,
                    tuple(OLink(l.parent.name, l.child.name, OMoments(*l.duration_moments)) for l in d.links))
         acc = od if acc is None else acc.plus(od)
+    return acc
+
+
+def _assert_sum(got, records):
+    acc = _oracle_sum(records)
     assert (got.start_time, got.end_time) == (acc.start_time, acc.end_time)
     exp = {(l.parent, l.child): l.moments for l in acc.links}
     assert len(got.links) == len(exp)
     for l in got.links:
         assert _same_bits(l.duration_moments, exp[(l.parent.name, l.child.name)])
-    # a window holding no row -> the monoid zero
-    z = agg.getDependencies(100 * 3600_000_000, 101 * 3600_000_000)
-    assert z == Dependencies.zero()
+
+
+DAY = 86_400_000_000
+
+
+def test_cassandra_rows_clobber_per_day_and_every_row_is_summed():
+    """CassandraAggregates.scala:111-136: row key = start floored to the day, store() = removeRow +
+    insert, so a second record of the same day replaces the first (CassandraAggregatesTest.scala
+    :101-112 only checks that the store does not throw). getDependencies keeps a column unless its
+    NAME -- the index 0 -- exceeds a bound in us (:58-61): any non-negative window returns every
+    row, Monoid-summed in row order."""
+    agg = GpuAggregates("cassandra", clock=lambda: NOW)
+    records = _random_records(3, 6, lambda r: r * DAY + 7)
+    for d in records:
+        agg.storeDependencies(d)
+    replaced = _random_records(4, 1, lambda r: 2 * DAY + 99)[0]  # same day as records[2]
+    agg.storeDependencies(replaced)
+    assert agg.count() == 6
+    kept = records[:2] + [replaced] + records[3:]
+    for window in ((0, 1), (5 * DAY, 6 * DAY), (None, None), (0, None), (10**15, 10**15 + 1)):
+        _assert_sum(agg.getDependencies(*window), kept)
+    assert agg.getDependencies(-1, None) == Dependencies.zero()  # 0 > -1: the column is filtered
+    assert agg.getDependencies(0, -5) == Dependencies.zero()
+    assert GpuAggregates("cassandra").getDependencies(0, 1) == Dependencies.zero()
+
+
+def test_hbase_reverse_ms_keys_and_reversed_scan():
+    """HBaseAggregates.scala:39-60: row key Long.MaxValue - start ms; getDependencies scans
+    [MaxValue - start ms, MaxValue - end ms), i.e. records with end ms < start <= start ms, newest
+    first. HBaseAggregatesSpec.scala:44-48: deps stored at 2 s come back from
+    getDependencies(Some(100 s)) unchanged."""
+    spec = Dependencies(2_000_000, 1_000_000_000, (link("HBase.Client", "HBase.RegionServer", Moments.of(1)),
+                                                     link("HBase.RegionServer", "HBase.Master", Moments.of(2))))
+    agg = GpuAggregates("hbase", clock=lambda: NOW)
+    agg.storeDependencies(spec)
+    assert agg.getDependencies(100_000_000) == spec
+    records = _random_records(5, 6, lambda r: (r + 1) * 3600_000_000)
+    agg = GpuAggregates("hbase", clock=lambda: NOW)
+    for d in records:
+        agg.storeDependencies(d)
+    h = 3600_000_000
+    # start bound 3.5 h, no end: records starting at <= 3.5 h, newest first
+    _assert_sum(agg.getDependencies(3 * h + h // 2), records[:3][::-1])
+    # start 5 h, end 2 h: (2 h, 5 h] -> records at 3, 4, 5 h, newest first
+    _assert_sum(agg.getDependencies(5 * h, 2 * h), records[2:5][::-1])
+    # the usual start < end window scans nothing
+    assert agg.getDependencies(0, 10 * h) == Dependencies.zero()
+    # no start: from key 0 = every record, newest first
+    _assert_sum(agg.getDependencies(None), records[::-1])
+    # a second record of the same millisecond replaces the first
+    again = _random_records(6, 1, lambda r: h + 250)[0]  # 1 h + 0.25 ms -> the same ms as records[0]
+    agg.storeDependencies(again)
+    assert agg.count() == 6
+    _assert_sum(agg.getDependencies(h), [again])
 
 
 def test_get_dependencies_capacity_error_is_reported():
@@ -229,7 +286,7 @@ def test_concurrent_stores_are_serialised():
 
 # ---- top annotations (CassandraAggregatesTest.scala:57-123) ----------------------------------
 def test_top_annotations_store_get_and_clobber():
-    agg = GpuAggregates("anorm")
+    agg = GpuAggregates("cassandra")
     assert agg.getTopAnnotations("mockingbird") == []
     agg.storeTopAnnotations("mockingbird", ["finagle.retry", "finagle.timeout", "annotation1"])
     agg.storeTopKeyValueAnnotations("mockingbird", ["hi", "there"])
@@ -351,3 +408,25 @@ def test_dependencies_thrift_edge_cases():
     assert cassandra_row_key(0) == 0
     assert cassandra_row_key(NOW) == NOW // day * day
     assert cassandra_row_key(3 * day - 1) == 2 * day
+
+
+def test_anorm_top_annotations_are_stubs():
+    """AnormAggregates.scala:111-137: store* do nothing, get* return Seq.empty."""
+    agg = GpuAggregates("anorm")
+    agg.storeTopAnnotations("mockingbird", ["a"])
+    agg.storeTopKeyValueAnnotations("mockingbird", ["k"])
+    assert agg.getTopAnnotations("mockingbird") == [] and agg.getTopKeyValueAnnotations("mockingbird") == []
+
+
+def test_hbase_top_annotations_one_family():
+    """HBaseAggregates.scala:62-110: both store* write the top-annotation family (the newest list
+    wins), getTopKeyValueAnnotations scans the key-value family and finds nothing, and
+    getTopAnnotations' open-ended scan falls through to the next service id holding a list."""
+    agg = GpuAggregates("hbase", services=Dictionary(["s0", "s1", "s2"]))
+    agg.storeTopAnnotations("s1", ["a", "b"])
+    assert agg.getTopAnnotations("s1") == ["a", "b"]
+    assert agg.getTopKeyValueAnnotations("s1") == []
+    agg.storeTopKeyValueAnnotations("s1", ["k1"])  # lands in the annotation family, newest
+    assert agg.getTopAnnotations("s1") == ["k1"]
+    assert agg.getTopAnnotations("s0") == ["k1"]  # no row for s0: the scan reaches s1's row
+    assert agg.getTopAnnotations("s2") == []

@@ -208,7 +208,8 @@ class zk_dep_link(C.Structure):
 
 
 ZK_STORE_ANORM = 0
-ZK_STORE_SUMMED = 1
+ZK_STORE_CASSANDRA = 1
+ZK_STORE_HBASE = 2
 ZK_TOP_ANNOTATIONS = 0
 ZK_TOP_KV_ANNOTATIONS = 1
 ZK_TIME_TOP = 2**63 - 1

@@ -209,15 +209,18 @@ class NullAggregates(Aggregates):
 
 
 class GpuAggregates(Aggregates):
-    """Aggregates over a zk_store: mode "anorm" (AnormAggregates window/row semantics) or
-    "summed" (Cassandra/HBase: contained rows Monoid-summed into one Dependencies).
+    """Aggregates over a zk_store with one reference backend's storage semantics (zkstore.h):
+    "anorm" (AnormAggregates: a row per record, containment window, top lists are stubs),
+    "cassandra" (CassandraAggregates: day-keyed rows clobbered per store, every row returned and
+    Monoid-summed, per-service top lists) or "hbase" (HBaseAggregates: reverse-ms row keys, the
+    reversed [start, end) scan, Monoid-summed).
 
     `clock` supplies Time.now in us (tests pin it)."""
 
     def __init__(self, mode: str = "anorm", services: Optional[Dictionary] = None,
                  annotations: Optional[Dictionary] = None, clock=now_us):
         self._L = _abi.lib()
-        m = {"anorm": _abi.ZK_STORE_ANORM, "summed": _abi.ZK_STORE_SUMMED}[mode]
+        m = {"anorm": _abi.ZK_STORE_ANORM, "cassandra": _abi.ZK_STORE_CASSANDRA, "hbase": _abi.ZK_STORE_HBASE}[mode]
         h = C.c_void_p()
         st = self._L.zk_store_create(m, C.byref(h))
         if st != _abi.ZK_OK:

@@ -10,6 +10,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "zk_guard.h"
 #include "zkingest.h"
 
 namespace {
@@ -30,9 +31,15 @@ bool snappy_len(const uint8_t* in, uint64_t n, uint64_t* len, uint64_t* hdr) {
     return false;
 }
 
+// the announced length is checked against the fragment cap and the format's expansion bound
+// before anything is allocated (the device decoder applies the same rule)
+bool snappy_len_ok(uint64_t len, uint64_t n, uint64_t hdr) {
+    return len <= ZK_INGEST_MAX_FRAGMENT && len <= (n - hdr) * (uint64_t)ZK_SNAPPY_MAX_EXPANSION;
+}
+
 bool snappy_uncompress(const uint8_t* in, uint64_t n, std::vector<uint8_t>* out) {
     uint64_t len, hdr;
-    if (!snappy_len(in, n, &len, &hdr)) return false;
+    if (!snappy_len(in, n, &len, &hdr) || !snappy_len_ok(len, n, hdr)) return false;
     out->resize(len);
     uint8_t* op = out->data();
     uint64_t o = 0;
@@ -391,9 +398,10 @@ uint64_t zk_hash_string(const char* s, uint64_t len) {
 }
 
 zk_status zk_snappy_uncompress(const uint8_t* in, uint64_t in_len, uint8_t* out, uint64_t cap, uint64_t* out_len) {
+    ZK_GUARD_BEGIN
     if (!in || !out_len) return ZK_ERR_INVALID_ARG;
     uint64_t len, hdr;
-    if (!snappy_len(in, in_len, &len, &hdr)) return ZK_ERR_INVALID_SPAN;
+    if (!snappy_len(in, in_len, &len, &hdr) || !snappy_len_ok(len, in_len, hdr)) return ZK_ERR_INVALID_SPAN;
     *out_len = len;
     if (!out) return ZK_OK;
     if (cap < len) return ZK_ERR_CAPACITY;
@@ -401,18 +409,23 @@ zk_status zk_snappy_uncompress(const uint8_t* in, uint64_t in_len, uint8_t* out,
     if (!snappy_uncompress(in, in_len, &tmp)) return ZK_ERR_INVALID_SPAN;
     memcpy(out, tmp.data(), len);
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_ingest_create(zk_ingest** out) {
+    ZK_GUARD_BEGIN
     if (!out) return ZK_ERR_INVALID_ARG;
     *out = new zk_ingest();
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_ingest_destroy(zk_ingest* g) {
+    ZK_GUARD_BEGIN
     if (!g) return ZK_ERR_INVALID_ARG;
     delete g;
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 const char* zk_ingest_last_error(const zk_ingest* g) { return g ? g->err.c_str() : "null decoder"; }
@@ -420,6 +433,7 @@ const char* zk_ingest_last_error(const zk_ingest* g) { return g ? g->err.c_str()
 zk_status zk_ingest_spans(zk_ingest* g, const uint8_t* buf, const uint64_t* offsets, uint64_t n, uint32_t codec,
                           uint32_t flags, const zk_span_cols* out, uint64_t* n_out, uint64_t* n_rejected,
                           zk_ingest_items* items) {
+    ZK_GUARD_BEGIN
     if (!g || !n_out || !n_rejected) return ZK_ERR_INVALID_ARG;
     *n_out = *n_rejected = 0;
     if (items) items->kv_n = items->ann_n = 0;
@@ -575,15 +589,19 @@ zk_status zk_ingest_spans(zk_ingest* g, const uint8_t* buf, const uint64_t* offs
         return ZK_ERR_CAPACITY;
     }
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_ingest_num_services(const zk_ingest* g, uint32_t* n) {
+    ZK_GUARD_BEGIN
     if (!g || !n) return ZK_ERR_INVALID_ARG;
     *n = (uint32_t)g->svc_names.size();
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_ingest_service_id(zk_ingest* g, const char* name, uint64_t len, uint32_t* id) {
+    ZK_GUARD_BEGIN
     if (!g || !id || (!name && len)) return ZK_ERR_INVALID_ARG;
     Host h;
     h.present = true;
@@ -591,9 +609,11 @@ zk_status zk_ingest_service_id(zk_ingest* g, const char* name, uint64_t len, uin
     h.svc_len = (uint32_t)len;
     *id = g->service(h);
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_ingest_service_name(const zk_ingest* g, uint32_t id, char* buf, uint64_t cap, uint64_t* len) {
+    ZK_GUARD_BEGIN
     if (!g || !len) return ZK_ERR_INVALID_ARG;
     if (id >= g->svc_names.size()) return ZK_ERR_SERVICE_RANGE;
     const std::string& s = g->svc_names[id];
@@ -602,12 +622,14 @@ zk_status zk_ingest_service_name(const zk_ingest* g, uint32_t id, char* buf, uin
     if (cap < s.size()) return ZK_ERR_CAPACITY;
     memcpy(buf, s.data(), s.size());
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 // ---- Dependencies wire format (zipkinDependencies.thrift:24-43, ScroogeThriftCodec) -------------
 zk_status zk_dependencies_encode(int64_t start_us, int64_t end_us, const zk_dep_link* links, uint64_t n_links,
                                  const char* const* names, const uint32_t* name_lens, uint32_t num_names,
                                  uint8_t* out, uint64_t cap, uint64_t* len) {
+    ZK_GUARD_BEGIN
     if (!len || (n_links && !links) || (num_names && (!names || !name_lens))) return ZK_ERR_INVALID_ARG;
     if (n_links > 0x7FFFFFFFull) return ZK_ERR_INVALID_ARG;
     for (uint64_t i = 0; i < n_links; ++i)
@@ -638,10 +660,12 @@ zk_status zk_dependencies_encode(int64_t start_us, int64_t end_us, const zk_dep_
     *len = w.len;
     if (out && w.len > cap) return ZK_ERR_CAPACITY;
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_dependencies_decode(zk_ingest* g, const uint8_t* buf, uint64_t len, int64_t* start_us,
                                  int64_t* end_us, zk_dep_link* out, uint64_t cap, uint64_t* n_links) {
+    ZK_GUARD_BEGIN
     if (!g || !buf || !start_us || !end_us || !n_links) return ZK_ERR_INVALID_ARG;
     Rd r{buf, buf + len};
     int64_t st = 0, en = 0;  // absent fields keep the thrift defaults
@@ -713,6 +737,7 @@ zk_status zk_dependencies_decode(zk_ingest* g, const uint8_t* buf, uint64_t len,
     *end_us = en;
     *n_links = k;
     return overflow ? ZK_ERR_CAPACITY : ZK_OK;
+    ZK_GUARD_END
 }
 
 int64_t zk_dependencies_row_key(int64_t start_us) {
@@ -722,6 +747,7 @@ int64_t zk_dependencies_row_key(int64_t start_us) {
 }
 
 zk_status zk_ingest_string(const zk_ingest* g, uint64_t hash, char* buf, uint64_t cap, uint64_t* len) {
+    ZK_GUARD_BEGIN
     if (!g || !len) return ZK_ERR_INVALID_ARG;
     auto it = g->strings.find(hash);
     if (it == g->strings.end()) return ZK_ERR_INVALID_ARG;
@@ -730,6 +756,7 @@ zk_status zk_ingest_string(const zk_ingest* g, uint64_t hash, char* buf, uint64_
     if (cap < it->second.size()) return ZK_ERR_CAPACITY;
     memcpy(buf, it->second.data(), it->second.size());
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 }  // extern "C"

@@ -23,13 +23,14 @@
 #include <string>
 #include <vector>
 
+#include "zk_guard.h"
 #include "zkingest.h"
 
 namespace zk {
 namespace {
 
 constexpr uint32_t kIngWG = 256;
-constexpr uint32_t kMaxRaw = 1u << 24;       // largest uncompressed fragment accepted (16 MiB)
+constexpr uint32_t kMaxRaw = ZK_INGEST_MAX_FRAGMENT;  // largest uncompressed fragment accepted (16 MiB)
 constexpr uint32_t kBadLen = 0xFFFFFFFFu;
 constexpr uint64_t kEmpty = 0ull;            // empty dictionary slot (hash 0 is stored as 1)
 constexpr uint32_t kNoId = 0xFFFFFFFFu;
@@ -342,7 +343,8 @@ __global__ __launch_bounds__(kIngWG) void k_ing_rawlen(IngArgs a) {
     uint64_t len = e >= b ? e - b : 0, hdr;
     if (e < b)
         len = kBadLen;
-    else if (a.snappy && !(snappy_hdr(a.buf + b, e - b, &len, &hdr) && len <= kMaxRaw))
+    else if (a.snappy && !(snappy_hdr(a.buf + b, e - b, &len, &hdr) && len <= kMaxRaw &&
+                           len <= (e - b - hdr) * (uint64_t)ZK_SNAPPY_MAX_EXPANSION))
         len = kBadLen;
     a.raw_len[i] = len == kBadLen ? 0 : len;
     a.status[i] = len == kBadLen ? kStUndecodable : kStOk;
@@ -884,6 +886,7 @@ uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
 extern "C" {
 
 zk_status zk_ingest_dev_create(int32_t device, void* stream, uint32_t max_services, zk_ingest_dev** out) {
+    ZK_GUARD_BEGIN
     if (!out || max_services == 0 || max_services > (1u << 20)) return ZK_ERR_INVALID_ARG;
     *out = nullptr;
     int ndev = 0;
@@ -925,9 +928,11 @@ zk_status zk_ingest_dev_create(int32_t device, void* stream, uint32_t max_servic
     }
     *out = g;
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_ingest_dev_destroy(zk_ingest_dev* g) {
+    ZK_GUARD_BEGIN
     if (!g) return ZK_ERR_INVALID_ARG;
     hipSetDevice(g->device);
     if (g->stream) hipStreamSynchronize(g->stream);
@@ -943,6 +948,7 @@ zk_status zk_ingest_dev_destroy(zk_ingest_dev* g) {
     if (g->own_stream && g->stream) hipStreamDestroy(g->stream);
     delete g;
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 const char* zk_ingest_dev_last_error(const zk_ingest_dev* g) { return g ? g->err.c_str() : "null decoder"; }
@@ -950,6 +956,7 @@ const char* zk_ingest_dev_last_error(const zk_ingest_dev* g) { return g ? g->err
 zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* offsets, uint64_t n,
                               uint32_t codec, uint32_t flags, const zk_span_cols* out, uint64_t* n_out,
                               uint64_t* n_rejected) {
+    ZK_GUARD_BEGIN
     if (!g || !n_out || !n_rejected) return ZK_ERR_INVALID_ARG;
     *n_out = *n_rejected = 0;
     if (n == 0) return ZK_OK;
@@ -1106,15 +1113,19 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     *n_out = kept;
     *n_rejected = bad;
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_ingest_dev_num_services(const zk_ingest_dev* g, uint32_t* n) {
+    ZK_GUARD_BEGIN
     if (!g || !n) return ZK_ERR_INVALID_ARG;
     *n = (uint32_t)g->names.size();
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_ingest_dev_service_name(const zk_ingest_dev* g, uint32_t id, char* buf, uint64_t cap, uint64_t* len) {
+    ZK_GUARD_BEGIN
     if (!g || !len) return ZK_ERR_INVALID_ARG;
     if (id >= g->names.size()) return ZK_ERR_SERVICE_RANGE;
     const std::string& s = g->names[id];
@@ -1123,6 +1134,7 @@ zk_status zk_ingest_dev_service_name(const zk_ingest_dev* g, uint32_t id, char* 
     if (cap < s.size()) return ZK_ERR_CAPACITY;
     memcpy(buf, s.data(), s.size());
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 }  // extern "C"

@@ -5,6 +5,7 @@
 #include <string>
 #include <vector>
 
+#include "zk_guard.h"
 #include "zk_sketch_internal.h"
 #include "zksketch.h"
 
@@ -72,6 +73,7 @@ zk_status check_state(zk_kv* kv, bool need_totals_ok) {
 extern "C" {
 
 zk_status zk_kv_create(const zk_kv_config* cfg, zk_kv** out) {
+    ZK_GUARD_BEGIN
     if (!cfg || !out) return ZK_ERR_INVALID_ARG;
     *out = nullptr;
     const uint32_t S = cfg->num_services;
@@ -125,9 +127,11 @@ zk_status zk_kv_create(const zk_kv_config* cfg, zk_kv** out) {
     }
     *out = k;
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_kv_destroy(zk_kv* k) {
+    ZK_GUARD_BEGIN
     if (!k) return ZK_ERR_INVALID_ARG;
     hipSetDevice(k->device);
     if (k->stream) hipStreamSynchronize(k->stream);
@@ -138,19 +142,23 @@ zk_status zk_kv_destroy(zk_kv* k) {
     if (k->own_stream && k->stream) hipStreamDestroy(k->stream);
     delete k;
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 const char* zk_kv_last_error(const zk_kv* k) { return k ? k->err.c_str() : "null handle"; }
 
 zk_status zk_kv_geometry(const zk_kv* k, uint32_t* width, uint32_t* depth, uint32_t* candidates) {
+    ZK_GUARD_BEGIN
     if (!k) return ZK_ERR_INVALID_ARG;
     if (width) *width = k->a.width;
     if (depth) *depth = k->a.depth;
     if (candidates) *candidates = k->a.cand;
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_kv_reset(zk_kv* k) {
+    ZK_GUARD_BEGIN
     if (!k) return ZK_ERR_INVALID_ARG;
     const KvArgs& a = k->a;
     KV_HIP(k, hipSetDevice(k->device));
@@ -160,9 +168,11 @@ zk_status zk_kv_reset(zk_kv* k) {
     KV_HIP(k, hipMemsetAsync(a.cand_est, 0, (uint64_t)a.S * a.cand * 4, k->stream));
     KV_HIP(k, hipMemsetAsync(k->dropped, 0, 8, k->stream));
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_kv_accumulate(zk_kv* k, const uint32_t* svc, const uint64_t* keys, uint64_t n, uint32_t flags) {
+    ZK_GUARD_BEGIN
     if (!k) return ZK_ERR_INVALID_ARG;
     if (n == 0) return ZK_OK;
     if (!svc || !keys) return kfail(k, ZK_ERR_INVALID_ARG, "null input");
@@ -233,9 +243,11 @@ zk_status zk_kv_accumulate(zk_kv* k, const uint32_t* svc, const uint64_t* keys, 
     KV_HIP(k, launch_kv_candidates(a, k->stream));
     KV_HIP(k, launch_kv_merge(a, k->stream));
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_kv_topk_all(zk_kv* k, uint32_t kk, uint64_t* keys, uint32_t* est, uint32_t* count) {
+    ZK_GUARD_BEGIN
     if (!k) return ZK_ERR_INVALID_ARG;
     if (kk == 0 || kk > k->a.cand || !keys || !est) return kfail(k, ZK_ERR_INVALID_ARG, "k must be in 1..candidates");
     const KvArgs& a = k->a;
@@ -253,9 +265,11 @@ zk_status zk_kv_topk_all(zk_kv* k, uint32_t kk, uint64_t* keys, uint32_t* est, u
             count[s] = c;
         }
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_kv_topk(zk_kv* k, uint32_t svc, uint32_t kk, uint64_t* keys, uint32_t* est, uint32_t* count) {
+    ZK_GUARD_BEGIN
     if (!k) return ZK_ERR_INVALID_ARG;
     if (svc >= k->a.S) return kfail(k, ZK_ERR_SERVICE_RANGE, "service >= S");
     if (kk == 0 || kk > k->a.cand || !keys || !est) return kfail(k, ZK_ERR_INVALID_ARG, "k must be in 1..candidates");
@@ -271,9 +285,11 @@ zk_status zk_kv_topk(zk_kv* k, uint32_t svc, uint32_t kk, uint64_t* keys, uint32
         *count = c;
     }
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_kv_estimate(zk_kv* k, uint32_t svc, const uint64_t* keys, uint64_t n, uint32_t* est) {
+    ZK_GUARD_BEGIN
     if (!k) return ZK_ERR_INVALID_ARG;
     if (svc >= k->a.S) return kfail(k, ZK_ERR_SERVICE_RANGE, "service >= S");
     if (n == 0) return ZK_OK;
@@ -293,35 +309,43 @@ zk_status zk_kv_estimate(zk_kv* k, uint32_t svc, const uint64_t* keys, uint64_t 
     KV_HIP(k, hipMemcpyAsync(est, k->qest, n * 4, hipMemcpyDeviceToHost, k->stream));
     KV_HIP(k, hipStreamSynchronize(k->stream));
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_kv_totals(zk_kv* k, uint64_t* totals) {
+    ZK_GUARD_BEGIN
     if (!k || !totals) return ZK_ERR_INVALID_ARG;
     KV_HIP(k, hipSetDevice(k->device));
     KV_HIP(k, hipMemcpyAsync(totals, k->a.totals, (uint64_t)k->a.S * 8, hipMemcpyDeviceToHost, k->stream));
     KV_HIP(k, hipStreamSynchronize(k->stream));
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_kv_partial(zk_kv* k, void** counters, uint64_t* cb, void** totals, uint64_t* tb) {
+    ZK_GUARD_BEGIN
     if (!k || !counters || !cb || !totals || !tb) return ZK_ERR_INVALID_ARG;
     *counters = k->a.cm;
     *cb = (uint64_t)k->a.S * k->a.depth * k->a.width * 4;
     *totals = k->a.totals;
     *tb = (uint64_t)k->a.S * 8;
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_kv_candidates(zk_kv* k, void** keys, void** est, uint64_t* bk, uint64_t* be) {
+    ZK_GUARD_BEGIN
     if (!k || !keys || !est || !bk || !be) return ZK_ERR_INVALID_ARG;
     *keys = k->a.cand_key;
     *est = k->a.cand_est;
     *bk = (uint64_t)k->a.S * k->a.cand * 8;
     *be = (uint64_t)k->a.S * k->a.cand * 4;
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_kv_merge_candidates(zk_kv* k, const uint64_t* keys, const uint32_t* est, uint32_t lists) {
+    ZK_GUARD_BEGIN
     if (!k) return ZK_ERR_INVALID_ARG;
     if (lists && (!keys || !est)) return kfail(k, ZK_ERR_INVALID_ARG, "null lists");
     KV_HIP(k, hipSetDevice(k->device));
@@ -332,6 +356,7 @@ zk_status zk_kv_merge_candidates(zk_kv* k, const uint64_t* keys, const uint32_t*
     a.extra_lists = lists;
     KV_HIP(k, launch_kv_merge(a, k->stream));
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 }  // extern "C"

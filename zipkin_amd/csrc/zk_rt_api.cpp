@@ -7,6 +7,7 @@
 #include <string>
 #include <vector>
 
+#include "zk_guard.h"
 #include "zk_internal.h"
 #include "zk_rt_internal.h"
 #include "zk_sketch_internal.h"
@@ -184,6 +185,7 @@ void rt_set_stream(zk_rt* r, hipStream_t s) { r->stream = s ? s : r->own; }
 extern "C" {
 
 zk_status zk_rt_create(const zk_rt_config* cfg, zk_rt** out) {
+    ZK_GUARD_BEGIN
     if (!cfg || !out) return ZK_ERR_INVALID_ARG;
     *out = nullptr;
     const uint32_t S = cfg->num_services;
@@ -224,9 +226,11 @@ zk_status zk_rt_create(const zk_rt_config* cfg, zk_rt** out) {
     }
     *out = r;
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_rt_destroy(zk_rt* r) {
+    ZK_GUARD_BEGIN
     if (!r) return ZK_ERR_INVALID_ARG;
     hipSetDevice(r->device);
     if (r->stream) hipStreamSynchronize(r->stream);
@@ -236,28 +240,34 @@ zk_status zk_rt_destroy(zk_rt* r) {
     // a caller-provided stream is not ours to destroy; a private one is
     delete r;
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 const char* zk_rt_last_error(const zk_rt* r) { return r ? r->err.c_str() : "null handle"; }
 
 zk_status zk_rt_geometry(const zk_rt* r, uint32_t* registers, uint32_t* bins) {
+    ZK_GUARD_BEGIN
     if (!r) return ZK_ERR_INVALID_ARG;
     if (registers) *registers = 1u << r->p;
     if (bins) *bins = r->nbins;
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_rt_reset(zk_rt* r) {
+    ZK_GUARD_BEGIN
     if (!r) return ZK_ERR_INVALID_ARG;
     RT_HIP(r, hipSetDevice(r->device));
     RT_HIP(r, hipMemsetAsync(r->regs, 0, (uint64_t)r->S << r->p, r->stream));
     RT_HIP(r, hipMemsetAsync(r->hist, 0, (uint64_t)r->S * r->nbins * 4, r->stream));
     RT_HIP(r, hipMemsetAsync(r->dropped, 0, 4 * 8, r->stream));
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_rt_accumulate_merged(zk_rt* r, const uint32_t* service_id, const uint64_t* trace_id,
                                   const int64_t* duration, uint64_t n, uint32_t flags) {
+    ZK_GUARD_BEGIN
     if (!r) return ZK_ERR_INVALID_ARG;
     if (n == 0) return ZK_OK;
     if (!service_id || !trace_id || !duration) return rfail(r, ZK_ERR_INVALID_ARG, "null input");
@@ -290,9 +300,11 @@ zk_status zk_rt_accumulate_merged(zk_rt* r, const uint32_t* service_id, const ui
                               r->stream));
     const PartitionPlan plan = partition_plan(n, r->S, r->cus);
     return sketch_items(r, plan, false, isvc, ipay, n, nullptr, n);
+    ZK_GUARD_END
 }
 
 zk_status zk_rt_read(zk_rt* r, uint8_t* registers, uint32_t* histogram) {
+    ZK_GUARD_BEGIN
     if (!r) return ZK_ERR_INVALID_ARG;
     RT_HIP(r, hipSetDevice(r->device));
     if (registers) RT_HIP(r, hipMemcpyAsync(registers, r->regs, (uint64_t)r->S << r->p, hipMemcpyDeviceToHost, r->stream));
@@ -300,19 +312,23 @@ zk_status zk_rt_read(zk_rt* r, uint8_t* registers, uint32_t* histogram) {
         RT_HIP(r, hipMemcpyAsync(histogram, r->hist, (uint64_t)r->S * r->nbins * 4, hipMemcpyDeviceToHost, r->stream));
     RT_HIP(r, hipStreamSynchronize(r->stream));
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_rt_distinct_traces(zk_rt* r, double* estimate) {
+    ZK_GUARD_BEGIN
     if (!r || !estimate) return ZK_ERR_INVALID_ARG;
     std::vector<uint8_t> regs((uint64_t)r->S << r->p);
     zk_status st = zk_rt_read(r, regs.data(), nullptr);
     if (st != ZK_OK) return st;
     for (uint32_t s = 0; s < r->S; ++s) estimate[s] = hll_estimate(regs.data() + ((uint64_t)s << r->p), r->p);
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_rt_quantiles(zk_rt* r, uint32_t service, const double* q, uint32_t nq, int64_t* lo, int64_t* hi,
                           uint64_t* count) {
+    ZK_GUARD_BEGIN
     if (!r) return ZK_ERR_INVALID_ARG;
     if (service >= r->S) return rfail(r, ZK_ERR_SERVICE_RANGE, "service >= S");
     if (nq && (!q || !lo || !hi)) return rfail(r, ZK_ERR_INVALID_ARG, "null array");
@@ -342,18 +358,22 @@ zk_status zk_rt_quantiles(zk_rt* r, uint32_t service, const double* q, uint32_t 
         }
     }
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_rt_partial(zk_rt* r, void** registers, uint64_t* rb, void** histogram, uint64_t* hb) {
+    ZK_GUARD_BEGIN
     if (!r || !registers || !rb || !histogram || !hb) return ZK_ERR_INVALID_ARG;
     *registers = r->regs;
     *rb = (uint64_t)r->S << r->p;
     *histogram = r->hist;
     *hb = (uint64_t)r->S * r->nbins * 4;
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_rt_dropped(zk_rt* r, uint64_t* service_range, uint64_t* duration_range) {
+    ZK_GUARD_BEGIN
     if (!r) return ZK_ERR_INVALID_ARG;
     unsigned long long d[4];
     RT_HIP(r, hipSetDevice(r->device));
@@ -362,6 +382,7 @@ zk_status zk_rt_dropped(zk_rt* r, uint64_t* service_range, uint64_t* duration_ra
     if (service_range) *service_range = d[0];
     if (duration_range) *duration_range = d[1];
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 }  // extern "C"

@@ -6,11 +6,24 @@
 //     stored Dependencies (start_ts, end_ts) plus its links; getDependencies returns the links of
 //     every row CONTAINED in [start, end] (start_ts >= start AND end_ts <= end), newest row first,
 //     as Dependencies(start, end, links) with the defaults start = now - 1 day, end = now.
-//   * Cassandra / HBase (CassandraAggregates.scala:54-74, HBaseAggregates.scala:39-53): the rows
-//     are Monoid-summed into one Dependencies (Dependencies.scala:65-82; links merged per
-//     (parent, child) by DependencyLink.sg = algebird MomentsGroup.plus, :38-43).
-//   * top annotation lists: a per-service list replaced wholesale by store* and read back in
-//     list order (CassandraAggregates.scala:79-108,119-136).
+//   * CassandraAggregates (zipkin-cassandra/.../storage/cassandra/CassandraAggregates.scala):
+//     storeDependencies writes row key startTime.floor(1.day) in us and store() clobbers the row
+//     (removeRow, then column index 0 -> the record, :111-116,122-136); getDependencies walks every
+//     row and keeps a column unless its NAME -- the index 0, not a time -- exceeds a given bound in
+//     us (:58-61), then Monoid-sums the records (:69-71).
+//   * HBaseAggregates (zipkin-hbase/.../storage/hbase/HBaseAggregates.scala): row key
+//     Long.MaxValue - startTime.inMilliseconds (:56-60, a later put of the same key replaces the
+//     record); getDependencies scans [MaxValue - start ms (0 without a start), MaxValue - end ms)
+//     in row-key byte order (:39-53) -- records with end < start ms <= start bound, newest first --
+//     and Monoid-sums them.
+//   Monoid.sum is reduceLeftOption(plus) over the rows in scan order (Dependencies.scala:65-82;
+//   links merged per (parent, child) by DependencyLink.sg = algebird MomentsGroup.plus, :38-43),
+//   the monoid zero when nothing matches.
+//   * top annotation lists (Anorm: stubs, AnormAggregates.scala:111-137): a per-service list replaced wholesale by store* and read back in
+//     list order (CassandraAggregates.scala:79-108,119-136). HBase (HBaseAggregates.scala:62-110)
+//     writes both kinds into the top-annotation family, so getTopKeyValueAnnotations finds nothing;
+//     getTopAnnotations returns the newest list stored under the first service id >= the asked one
+//     (its scan has a start row and no stop row).
 // Dictionary ids stand in for the strings (the host owns the dictionaries, as for zkagg.h).
 #include <math.h>
 #include <string.h>
@@ -22,6 +35,7 @@
 #include <utility>
 #include <vector>
 
+#include "zk_guard.h"
 #include "zkstore.h"
 
 namespace {
@@ -68,7 +82,8 @@ zk_moments moments_plus(const zk_moments& a, const zk_moments& b) {
 struct zk_store {
     std::mutex mu;
     uint32_t mode = ZK_STORE_ANORM;
-    std::vector<StoredDeps> rows;  // insertion order (Anorm's dlid)
+    std::vector<StoredDeps> rows;            // Anorm: insertion order (dlid)
+    std::map<uint64_t, StoredDeps> keyed;    // Cassandra / HBase: row key (unsigned = byte order)
     std::map<uint32_t, std::vector<uint64_t>> top[2];
     std::string err;
 };
@@ -80,30 +95,77 @@ zk_status sfail(zk_store* s, zk_status st, const char* msg) {
     return st;
 }
 
+// 8-byte big-endian row keys compare as unsigned integers (Cassandra row order under a byte-ordered
+// partitioner, HBase's lexicographic row order); Long arithmetic wraps like the JVM's
+uint64_t cassandra_key(int64_t start_us) { return (uint64_t)((start_us / kDayUs) * kDayUs); }  // Time.floor: Long division
+uint64_t hbase_key_ms(int64_t ms) { return (uint64_t)INT64_MAX - (uint64_t)ms; }
+
+// Monoid.sum over records in order: reduceLeftOption(Dependencies.plus), zero if none. A single
+// record comes back as stored; from two on, every operand goes through `links.map(k -> link).toMap`
+// (the last link of a duplicated key wins) and shared keys combine as sg.plus(r, l)
+// (Dependencies.scala:68-79). MomentsGroup.plus is bitwise symmetric, so only the left fold over
+// records fixes the rounding.
+void monoid_sum(const std::vector<const StoredDeps*>& hit, std::vector<zk_dep_link>* res, int64_t* rs,
+                int64_t* re) {
+    *rs = ZK_TIME_TOP;
+    *re = ZK_TIME_BOTTOM;
+    if (hit.size() == 1) {
+        *rs = hit[0]->start;
+        *re = hit[0]->end;
+        *res = hit[0]->links;
+        return;
+    }
+    std::map<std::pair<uint32_t, uint32_t>, zk_moments> acc;
+    for (size_t r = 0; r < hit.size(); ++r) {
+        const StoredDeps& d = *hit[r];
+        *rs = std::min(*rs, d.start);
+        *re = std::max(*re, d.end);
+        std::map<std::pair<uint32_t, uint32_t>, zk_moments> m;
+        for (const zk_dep_link& l : d.links) m[std::make_pair(l.parent, l.child)] = l.moments;
+        if (r == 0) {
+            acc = std::move(m);
+            continue;
+        }
+        for (const auto& kv : m) {
+            auto it = acc.find(kv.first);
+            if (it == acc.end())
+                acc.emplace(kv.first, kv.second);
+            else
+                it->second = moments_plus(kv.second, it->second);
+        }
+    }
+    for (const auto& kv : acc) res->push_back(zk_dep_link{kv.first.first, kv.first.second, kv.second});
+}
+
 }  // namespace
 
 extern "C" {
 
 zk_status zk_store_create(uint32_t mode, zk_store** out) {
+    ZK_GUARD_BEGIN
     if (!out) return ZK_ERR_INVALID_ARG;
     *out = nullptr;
-    if (mode != ZK_STORE_ANORM && mode != ZK_STORE_SUMMED) return ZK_ERR_INVALID_ARG;
+    if (mode != ZK_STORE_ANORM && mode != ZK_STORE_CASSANDRA && mode != ZK_STORE_HBASE) return ZK_ERR_INVALID_ARG;
     zk_store* s = new zk_store();
     s->mode = mode;
     *out = s;
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_store_destroy(zk_store* s) {
+    ZK_GUARD_BEGIN
     if (!s) return ZK_ERR_INVALID_ARG;
     delete s;
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 const char* zk_store_last_error(const zk_store* s) { return s ? s->err.c_str() : "null store"; }
 
 zk_status zk_store_put_dependencies(zk_store* s, int64_t start_us, int64_t end_us, const zk_dep_link* links,
                                     uint64_t n) {
+    ZK_GUARD_BEGIN
     if (!s) return ZK_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(s->mu);
     if (n && !links) return sfail(s, ZK_ERR_INVALID_ARG, "null links");
@@ -111,20 +173,47 @@ zk_status zk_store_put_dependencies(zk_store* s, int64_t start_us, int64_t end_u
     d.start = start_us;
     d.end = end_us;
     d.links.assign(links, links + n);
-    s->rows.push_back(std::move(d));
+    if (s->mode == ZK_STORE_CASSANDRA)
+        s->keyed[cassandra_key(start_us)] = std::move(d);  // removeRow + insert (:111-116,122-136)
+    else if (s->mode == ZK_STORE_HBASE)
+        s->keyed[hbase_key_ms(start_us / 1000)] = std::move(d);  // Put replaces the row's cell (:55-60)
+    else
+        s->rows.push_back(std::move(d));
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_store_get_dependencies(zk_store* s, const int64_t* start_us, const int64_t* end_us, int64_t now_us,
                                     zk_dep_link* out, uint64_t cap, uint64_t* n_links, int64_t* out_start,
                                     int64_t* out_end) {
+    ZK_GUARD_BEGIN
     if (!s || !n_links) return ZK_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(s->mu);
-    const int64_t lo = start_us ? *start_us : now_us - kDayUs;  // AnormAggregates.scala:53-54
-    const int64_t hi = end_us ? *end_us : now_us;
     std::vector<zk_dep_link> res;
     int64_t rs, re;
-    if (s->mode == ZK_STORE_ANORM) {
+    if (s->mode == ZK_STORE_CASSANDRA) {
+        // every row, column 0 kept unless a given bound is below 0 us (CassandraAggregates.scala:58-61)
+        std::vector<const StoredDeps*> hit;
+        const bool keep = !(end_us && 0 > *end_us) && !(start_us && 0 > *start_us);
+        if (keep)
+            for (const auto& kv : s->keyed) hit.push_back(&kv.second);
+        monoid_sum(hit, &res, &rs, &re);
+    } else if (s->mode == ZK_STORE_HBASE) {
+        // scan [startRow, stopRow) in row-key order (HBaseAggregates.scala:41-43); a start row at or
+        // past the stop row scans nothing
+        const uint64_t lo_key = hbase_key_ms(start_us ? *start_us / 1000 : INT64_MAX);
+        const bool has_stop = end_us != nullptr;
+        const uint64_t hi_key = has_stop ? hbase_key_ms(*end_us / 1000) : 0;
+        std::vector<const StoredDeps*> hit;
+        if (!has_stop || lo_key < hi_key)
+            for (auto it = s->keyed.lower_bound(lo_key); it != s->keyed.end(); ++it) {
+                if (has_stop && it->first >= hi_key) break;
+                hit.push_back(&it->second);
+            }
+        monoid_sum(hit, &res, &rs, &re);
+    } else {
+        const int64_t lo = start_us ? *start_us : now_us - kDayUs;  // AnormAggregates.scala:53-54
+        const int64_t hi = end_us ? *end_us : now_us;
         // WHERE start_ts >= {startTs} AND end_ts <= {endTs} ORDER BY dlid DESC (:56-64)
         for (size_t i = s->rows.size(); i-- > 0;) {
             const StoredDeps& d = s->rows[i];
@@ -132,43 +221,6 @@ zk_status zk_store_get_dependencies(zk_store* s, const int64_t* start_us, const 
         }
         rs = lo;
         re = hi;
-    } else {
-        // Monoid.sum over the contained rows in stored order = reduceLeftOption(plus), zero if
-        // none: a single row comes back as stored; from two rows on, every operand goes through
-        // `links.map(k -> link).toMap` (the last link of a duplicated key wins) and shared keys
-        // combine as sg.plus(r, l) (Dependencies.scala:68-79). MomentsGroup.plus is bitwise
-        // symmetric, so only the left fold over rows fixes the rounding.
-        std::vector<const StoredDeps*> hit;
-        for (const StoredDeps& d : s->rows)
-            if (d.start >= lo && d.end <= hi) hit.push_back(&d);
-        rs = ZK_TIME_TOP;
-        re = ZK_TIME_BOTTOM;
-        if (hit.size() == 1) {
-            rs = hit[0]->start;
-            re = hit[0]->end;
-            res = hit[0]->links;
-        } else if (hit.size() > 1) {
-            std::map<std::pair<uint32_t, uint32_t>, zk_moments> acc;
-            for (size_t r = 0; r < hit.size(); ++r) {
-                const StoredDeps& d = *hit[r];
-                rs = std::min(rs, d.start);
-                re = std::max(re, d.end);
-                std::map<std::pair<uint32_t, uint32_t>, zk_moments> m;
-                for (const zk_dep_link& l : d.links) m[std::make_pair(l.parent, l.child)] = l.moments;
-                if (r == 0) {
-                    acc = std::move(m);
-                    continue;
-                }
-                for (const auto& kv : m) {
-                    auto it = acc.find(kv.first);
-                    if (it == acc.end())
-                        acc.emplace(kv.first, kv.second);
-                    else
-                        it->second = moments_plus(kv.second, it->second);
-                }
-            }
-            for (const auto& kv : acc) res.push_back(zk_dep_link{kv.first.first, kv.first.second, kv.second});
-        }
     }
     *n_links = res.size();
     if (out_start) *out_start = rs;
@@ -177,16 +229,20 @@ zk_status zk_store_get_dependencies(zk_store* s, const int64_t* start_us, const 
     if (cap < res.size()) return sfail(s, ZK_ERR_CAPACITY, "output capacity smaller than the result");
     if (!res.empty()) memcpy(out, res.data(), res.size() * sizeof(zk_dep_link));
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_store_count(zk_store* s, uint64_t* records) {
+    ZK_GUARD_BEGIN
     if (!s || !records) return ZK_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(s->mu);
-    *records = s->rows.size();
+    *records = s->mode == ZK_STORE_ANORM ? s->rows.size() : s->keyed.size();
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_store_watermark(zk_store* s, int64_t* end_us) {
+    ZK_GUARD_BEGIN
     if (!s || !end_us) return ZK_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(s->mu);
     int64_t w = 0;
@@ -195,40 +251,67 @@ zk_status zk_store_watermark(zk_store* s, int64_t* end_us) {
         w = any ? std::max(w, d.end) : d.end;
         any = true;
     }
+    for (const auto& kv : s->keyed) {
+        w = any ? std::max(w, kv.second.end) : kv.second.end;
+        any = true;
+    }
     *end_us = any ? w : 0;
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_store_put_top(zk_store* s, uint32_t kind, uint32_t service, const uint64_t* ids, uint64_t n) {
+    ZK_GUARD_BEGIN
     if (!s) return ZK_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(s->mu);
     if (kind > ZK_TOP_KV_ANNOTATIONS) return sfail(s, ZK_ERR_INVALID_ARG, "unknown top-annotation kind");
     if (n && !ids) return sfail(s, ZK_ERR_INVALID_ARG, "null ids");
-    // store(): removeRow(key) then insert column i -> value i (CassandraAggregates.scala:122-136)
-    s->top[kind][service].assign(ids, ids + n);
+    // store(): removeRow(key) then insert column i -> value i (CassandraAggregates.scala:122-136).
+    // HBase puts both kinds into the top-annotation family, the newest put read first
+    // (HBaseAggregates.scala:104-110): one list per service, whichever kind stored it last.
+    // Anorm's top-annotation methods are stubs (AnormAggregates.scala:111-137): nothing is kept.
+    if (s->mode == ZK_STORE_ANORM) return ZK_OK;
+    s->top[s->mode == ZK_STORE_HBASE ? 0 : kind][service].assign(ids, ids + n);
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_store_get_top(zk_store* s, uint32_t kind, uint32_t service, uint64_t* ids, uint64_t cap, uint64_t* n) {
+    ZK_GUARD_BEGIN
     if (!s || !n) return ZK_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(s->mu);
     if (kind > ZK_TOP_KV_ANNOTATIONS) return sfail(s, ZK_ERR_INVALID_ARG, "unknown top-annotation kind");
     auto it = s->top[kind].find(service);
-    const uint64_t cnt = it == s->top[kind].end() ? 0 : it->second.size();
+    if (s->mode == ZK_STORE_HBASE) {
+        // the key-value family is never written; the annotation scan starts at (service id, 0) with
+        // no stop row and takes the first row, which belongs to the next stored service id when
+        // this one has none (HBaseAggregates.scala:70-94)
+        it = kind == ZK_TOP_KV_ANNOTATIONS ? s->top[0].end() : s->top[0].lower_bound(service);
+        if (kind == ZK_TOP_KV_ANNOTATIONS) {
+            *n = 0;
+            return ZK_OK;
+        }
+    }
+    const auto& tk = s->top[s->mode == ZK_STORE_HBASE ? 0 : kind];
+    const uint64_t cnt = it == tk.end() ? 0 : it->second.size();
     *n = cnt;
     if (!ids || cnt == 0) return ZK_OK;
     if (cap < cnt) return sfail(s, ZK_ERR_CAPACITY, "output capacity smaller than the list");
     memcpy(ids, it->second.data(), cnt * sizeof(uint64_t));
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_moments_plus(const zk_moments* a, const zk_moments* b, zk_moments* out) {
+    ZK_GUARD_BEGIN
     if (!a || !b || !out) return ZK_ERR_INVALID_ARG;
     *out = moments_plus(*a, *b);
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 zk_status zk_link_table_compact(const zk_link_table* t, uint32_t S, zk_dep_link* out, uint64_t cap, uint64_t* n) {
+    ZK_GUARD_BEGIN
     if (!t || !n || !t->m0 || !t->m1 || !t->m2 || !t->m3 || !t->m4 || !t->present || t->device_ptrs)
         return ZK_ERR_INVALID_ARG;
     const uint64_t cells = (uint64_t)S * S;
@@ -244,6 +327,7 @@ zk_status zk_link_table_compact(const zk_link_table* t, uint32_t S, zk_dep_link*
     }
     *n = k;
     return ZK_OK;
+    ZK_GUARD_END
 }
 
 }  // extern "C"

@@ -18,10 +18,17 @@ device) over the new part:
 * the unit is the trace, because the job needs trace-complete batches: a trace is new when its
   created time -- the latest `created_ts` of its fragments -- is after the watermark, and then
   all of its fragments are aggregated;
-* the stored record is Dependencies(start = earliest created time among the new traces,
-  end = latest, links of the new traces): the span of the reference's steps. One device job
-  over all new traces replaces the per-step Monoid sum; the two differ only in the rounding of
-  m1..m4 (the device's are exactly rounded; m0 is identical).
+* the record's time range follows the reference's steps: with min/max the earliest/latest created
+  time of the new traces and `count` their records, steps = max(count / 10000, 1) and
+  stepSize = (max - min) / steps (SpanSummary, :35-39); the steps run over
+  Range.Long(min, max + 1, stepSize), so the record is Dependencies(min, last boundary, links)
+  (:43-49, :102-120) and the traces created after the last boundary wait for the next run, as
+  the reference's spans do. (All new traces created at one instant make stepSize 0, where the
+  reference's Range throws; here the record then ends at that instant.)
+* the record is stored whenever new traces exist, with or without links: the reference folds
+  from Monoid.zero and always stores the result (:41-56), which is what advances the watermark;
+* one device job over the selected traces replaces the per-step Monoid sum; the two differ only
+  in the rounding of m1..m4 (the device's are exactly rounded; m0 is identical).
 
 The next run's watermark is that record's end, so a trace is aggregated exactly once as long as
 traces are complete when their created time passes the watermark (the reference assumes the same
@@ -71,17 +78,22 @@ class IncrementalAggregator:
         return self.aggregates.watermark()
 
     def apply(self, cols: SpanColumns, created_ts, num_services: Optional[int] = None) -> Optional[Dependencies]:
-        """Aggregate the traces created after the watermark and store their Dependencies; returns
-        the stored record, or None when nothing is new or the new traces have no link."""
+        """Aggregate the traces created after the watermark, up to the last step boundary, and
+        store their Dependencies; returns the stored record, or None when nothing is new."""
         wm = self.watermark()
         created = trace_created(cols, created_ts)
         new = created > wm
-        self.last_selected = int(new.sum())
-        if not self.last_selected:
+        count = int(new.sum())
+        if not count:
+            self.last_selected = 0
             return None  # "Aggregated span dependencies already up-to-date" (:52-55)
-        deps = self.job.run(cols.take(np.flatnonzero(new)), num_services=num_services)
-        if deps is None:
-            return None
-        rec = Dependencies(int(created[new].min()), int(created[new].max()), deps.links)
+        lo, hi = int(created[new].min()), int(created[new].max())
+        steps = max(count // 10000, 1)
+        step = (hi - lo) // steps
+        end = hi if step == 0 else lo + ((hi - lo) // step) * step
+        sel = new & (created <= end)
+        self.last_selected = int(sel.sum())
+        deps = self.job.run(cols.take(np.flatnonzero(sel)), num_services=num_services)
+        rec = Dependencies(lo, end, deps.links if deps is not None else ())
         self.aggregates.storeDependencies(rec)
         return rec
