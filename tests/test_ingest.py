@@ -349,7 +349,7 @@ def test_stored_span_job_end_to_end(gpu):
         by_trace.setdefault(sp.trace_id, []).append(sp)
     traces = list(by_trace.values())
     batches = [encode_all([sp for t in traces[i:i + 90] for sp in t]) for i in range(0, len(traces), 90)]
-    store = GpuAggregates("anorm")
+    store = GpuAggregates("cassandra")  # per-service top lists (Anorm's are stubs)
     job = StoredSpanJob(strict=False, aggregates=store, top_k=5, clock=lambda: 10**15)
     deps = job.run(batches)
     ref = aggregate_job(spans, strict=False)
