@@ -48,13 +48,13 @@ extern "C" {
 #define ZK_CODEC_THRIFT        0u  /* TBinaryProtocol-encoded Span */
 #define ZK_CODEC_SNAPPY_THRIFT 1u  /* raw Snappy block of the above (the stored Cassandra value) */
 
-#define ZK_INGEST_STRICT 1u
+#define ZK_INGEST_STRICT 1u        /* fail the batch on the first span the reference rejects */
 /* Both decoders (host zk_ingest_spans, device zk_ingest_dev_spans) reject a Snappy fragment whose
  * header announces more than ZK_INGEST_MAX_FRAGMENT bytes, or more than the format can expand its
  * payload to (a 3-byte copy emits at most 64 bytes: < ZK_SNAPPY_MAX_EXPANSION x), before any
  * allocation -- a 5-byte hostile header cannot make either decoder allocate gigabytes. */
 #define ZK_INGEST_MAX_FRAGMENT   (1u << 24)
-#define ZK_SNAPPY_MAX_EXPANSION  22u        /* fail the batch on the first span the reference rejects */
+#define ZK_SNAPPY_MAX_EXPANSION  22u
 
 typedef struct zk_ingest zk_ingest;
 
