@@ -61,3 +61,16 @@ def test_null_ctx_calls_are_errors():
     assert L.zk_deps_reset(None) == _abi.ZK_ERR_INVALID_ARG
     assert L.zk_ctx_destroy(None) == _abi.ZK_ERR_INVALID_ARG
     assert L.zk_deps_accumulate(None, None, 0) == _abi.ZK_ERR_INVALID_ARG
+
+
+def test_jni_sources_bind_only_declared_entry_points():
+    """jvm/src/main/c/zkagg_jni.c (uncompiled here: no JDK) calls only functions include/*.h
+    declares, and every ZkNative @native method has a JNI implementation."""
+    root = INCLUDE.parent
+    c = (root / "jvm" / "src" / "main" / "c" / "zkagg_jni.c").read_text()
+    calls = set(re.findall(r"\b(zk_[a-z0-9_]+)\s*\(", re.sub(r"/\*.*?\*/", "", c, flags=re.S)))
+    assert calls and calls <= set(declared_functions()), calls - set(declared_functions())
+    scala = (root / "jvm" / "src" / "main" / "scala" / "com" / "twitter" / "zipkin" / "gpu" / "ZkNative.scala").read_text()
+    natives = set(re.findall(r"@native def (\w+)", scala))
+    implemented = set(re.findall(r"JNICALL FN\((\w+)\)", c))
+    assert natives == implemented, natives ^ implemented
