@@ -41,7 +41,8 @@ def parse():
     ap.add_argument("--max-depth", type=int, default=6)
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--cpu-sample", type=int, default=20_000_000, help="records for the CPU baseline leg (0: skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0: every CPU this process may use, see usable_cpus)")
     ap.add_argument("--verify", type=int, default=0,
                     help="1: ZK_BATCH_VERIFY_TRACES on every step (exact device check of the clustering promise)")
     ap.add_argument("--ablate", type=int, default=0, help="diagnostic: 1 = K1 without link emission (not a valid result)")
@@ -49,12 +50,15 @@ def parse():
                     help="batches in flight behind the one being joined: 1 (default) = two table/stream "
                          "sets (batch k's join overlaps batch k-1's tail), 2 = three, 0 = one set, serial steps "
                          "(c2 takes any depth, c4/c5 use two sets when > 0)")
-    ap.add_argument("--workload", default="c2", choices=("c2", "c4", "c5", "ingest"),
-                    help="c2 (default, the headline): dependency path; c4: key-value top-K sketch over "
+    ap.add_argument("--workload", default="c2", choices=("c1", "c2", "c4", "c5", "ingest"),
+                    help="c2 (default, the headline): dependency path; c1: the reference's CPU config "
+                         "(10k tracegen traces, 20 services) on the GPU and the CPU baseline; "
+                         "c4: key-value top-K sketch over "
                          "binary annotations; c5: per-service HLL + duration histogram from span fragments; "
                          "ingest: device decode of stored Snappy+thrift fragments into columns")
     ap.add_argument("--fragments", type=int, default=20_000_000, help="ingest: stored fragments per step")
-    ap.add_argument("--items", type=int, default=250_000_000, help="c4: binary annotations per step")
+    ap.add_argument("--items", type=int, default=1_000_000_000,
+                    help="c4: binary annotations per step (BASELINE configs[3]: 1e9, 12 GB in HBM)")
     return ap.parse_args()
 
 
@@ -62,6 +66,8 @@ def main():
     a = parse()
     import torch
 
+    if a.workload == "c1":
+        return bench_c1(a)
     if a.workload == "c4":
         return bench_c4(a)
     if a.workload == "c5":
@@ -231,15 +237,18 @@ def main():
 
     cpu = parity = None
     if rank == 0 and world == 1 and a.cpu_sample > 0:
-        cpu, parity = cpu_baseline(cols, min(a.cpu_sample, n), S, a.cpu_threads, dev)
+        cpu, parity = cpu_baseline(cols, min(a.cpu_sample, n), S, a.cpu_threads or usable_cpus(), dev)
 
-    traffic = None
+    # PMC counters need their own rocprofv3 --pmc run (tools/pmc.sh), so the traffic figure is the
+    # builder's measurement of the same kernel on the same workload, labelled with its source
+    traffic = traffic_src = None
     pmc = ROOT / "profiles" / "pmc_latest.json"
     if pmc.exists():
         try:
             j = json.loads(pmc.read_text())
             if j.get("records") == n:
                 traffic = j.get("hbm_bytes_per_launch")
+                traffic_src = f"profiles/pmc_latest.json ({j.get('run', 'builder run')}, rocprofv3 --pmc, not this run)"
         except Exception:
             traffic = None
 
@@ -276,6 +285,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBS,
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": n * BYTES_PER_RECORD,
                 "avg_launch_ms": join_avg_ms,
                 # K1 alone (serial warmup steps): with the pipeline, the timed launches share the
@@ -301,13 +311,41 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(cols, sample, S, threads, dev):
-    """The oracle's multithreaded C restatement (kind "port") on the first `sample` records of the
-    same batch, on this box's host cores. A reported baseline only.
+def usable_cpus() -> int:
+    """CPUs this process may run on: its affinity mask, capped by a cgroup CPU quota and by the
+    thread budget the box exports (OMP_NUM_THREADS), whichever is smallest."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()
+        if q != "max":
+            n = min(n, max(1, int(q) // int(per)))
+    except Exception:
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit():
+        n = min(n, int(omp))
+    return max(1, n)
 
-    The same oracle run is the bench's parity check: the HIP path aggregates the same prefix of the
-    device batch, and m0..m4 and every counter must equal the oracle's bit for bit, or the bench
-    fails (the timed steps above process the full batch with the same kernels)."""
+
+def cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(cols, sample, S, threads, dev):
+    """The CPU baseline (kind "port"): oracle/zk_cpu_port.c -- the same job as one multithreaded
+    pass over trace-clustered input, the promise the GPU path runs under -- on the first `sample`
+    records of the same batch, on this box's host cores. A reported baseline only.
+
+    The literal oracle (oracle/zk_oracle.c) runs on the same prefix as the bench's parity check:
+    the HIP path aggregates that prefix of the device batch, and m0..m4 and every counter must equal
+    the oracle's bit for bit (and so must the port's), or the bench fails (the timed steps above
+    process the full batch with the same kernels)."""
     import numpy as np
 
     from oracle import oracle
@@ -320,8 +358,15 @@ def cpu_baseline(cols, sample, S, threads, dev):
     while cut < len(tid) and cut > 0 and tid[cut] == tid[cut - 1]:
         cut -= 1
     part = host.take(slice(0, cut))
-    oracle.aggregate(part.take(slice(0, min(cut, 100_000))), S, threads=threads)  # warm the library
+    oracle.aggregate_port(part.take(slice(0, min(cut, 100_000))), S, threads=threads)  # warm the library
+    times = []
+    for _ in range(3):
+        rp = oracle.aggregate_port(part, S, threads=threads, clustered=True)
+        times.append(rp.seconds)
+    port_s = sorted(times)[1]
     r = oracle.aggregate(part, S, threads=threads)
+    if not (np.array_equal(rp.cells, r.cells) and rp.stats == r.stats):
+        raise RuntimeError("the CPU port disagrees with the oracle")
     with DepsContext(S, device=dev.index or 0) as ctx:
         ctx.accumulate(cols, clustered=True, verify=True, n=cut)
         got = ctx.finalize()
@@ -333,12 +378,14 @@ def cpu_baseline(cols, sample, S, threads, dev):
     if bad:
         raise RuntimeError(f"parity failure on the {cut}-record prefix of the bench batch: {bad}")
     cpu = {
-        "value": cut / r.seconds,
+        "value": cut / port_s,
         "unit": "spans/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"first {cut} records (whole traces) of the benchmark batch; oracle/zk_oracle.c, "
-        f"{threads} threads, {r.seconds:.2f} s",
+        "cpu": cpu_model(),
+        "sample": f"first {cut} records (whole traces) of the benchmark batch; oracle/zk_cpu_port.c "
+        f"(trace-clustered single pass), {threads} threads, median of 3: {port_s:.3f} s; the literal "
+        f"oracle/zk_oracle.c took {r.seconds:.2f} s",
     }
     parity = {"result": "exact", "records": cut, "links": int(got.present.sum()),
               "checked": "m0..m4 bit-identical + all counters, HIP path vs oracle/zk_oracle.c, same prefix"}
@@ -557,6 +604,68 @@ def bench_c5(a):
     }), flush=True)
 
 
+def bench_c1(a):
+    """BASELINE configs[0], "C1": the reference's own CPU-runnable case -- the dependency job on 10k
+    zipkin-tracegen traces (maxDepth 7, 20 services, seed 1; ~0.3M records). The GPU path runs it
+    from HBM (reset + accumulate + finalize per step, like C2); the CPU baseline is the port on all
+    usable cores, median of 10 runs, as BASELINE.md asks; both are checked against the oracle."""
+    import numpy as np
+    import torch
+
+    from oracle import oracle
+    from zipkin_amd import DepsContext, DeviceColumns, tracegen_host
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
+    S, T = 20, 10_000
+    host = tracegen_host(1, T, max_depth=7, num_services=S)
+    n = len(host)
+    cols = DeviceColumns.from_host(host, device="cuda:0")
+    ctx = DepsContext(S, device=0, stream=stream.cuda_stream, timing=True)
+    out = {k: torch.empty(S * S, dtype=dt, device=dev) for k, dt in
+           (("m0", torch.int64), ("m1", torch.float64), ("m2", torch.float64), ("m3", torch.float64),
+            ("m4", torch.float64), ("present", torch.uint8))}
+
+    def step():
+        ctx.reset()
+        ctx.accumulate(cols, clustered=True, verify=False)
+        ctx.finalize(out_device=out)
+
+    wall, ev_ms = _timed(step, a.steps, a.warmup, stream)
+    got = ctx.finalize()
+    st = ctx.stats()
+    ref = oracle.aggregate(host, S)
+    m0, ms = ref.dense()
+    if not (np.array_equal(got.m0, m0) and all(np.array_equal(x, y) for x, y in zip((got.m1, got.m2, got.m3, got.m4), ms))
+            and all(st[k] == v for k, v in ref.stats.items() if k != "spilled_traces")):
+        raise RuntimeError("C1: GPU result differs from the oracle")
+    threads = a.cpu_threads or usable_cpus()
+    times = []
+    for _ in range(11):  # one warm-up + 10 timed
+        rp = oracle.aggregate_port(host, S, threads=threads, clustered=True)
+        times.append(rp.seconds)
+    cpu_s = float(np.median(times[1:]))
+    if not (np.array_equal(rp.cells, ref.cells) and rp.stats == ref.stats):
+        raise RuntimeError("C1: CPU port differs from the oracle")
+    ctx.close()
+    print(json.dumps({
+        "metric": "spans/sec into DependencyLinks (BASELINE configs[0]: 10k tracegen traces, 20 services)",
+        "value": n * a.steps / wall, "unit": "spans/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": wall * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u64", "data": "synthetic (zipkin-tracegen-shaped, seed 1)",
+        "config": {"workload": "C1: 10k tracegen traces, maxDepth 7, 20 services", "records": n, "traces": T,
+                   "services": S, "step": "reset + span_join + spill + finalize(m0..m4) + status check"},
+        "parity": {"result": "exact", "records": n, "links": int(got.present.sum()),
+                   "checked": "GPU and CPU port vs oracle/zk_oracle.c: m0..m4 bit-identical + counters"},
+        "cpu_baseline": {"value": n / cpu_s, "unit": "spans/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
+                         "sample": f"the whole C1 batch ({n} records), oracle/zk_cpu_port.c, median of 10: "
+                                   f"{cpu_s * 1e3:.2f} ms"},
+        "detail": {"event_ms_per_step": ev_ms / a.steps, "note": "a 14 MB batch: launch- and latency-bound on the GPU"},
+    }), flush=True)
+
+
 def bench_c4(a):
     """BASELINE configs[3] (one GPU slice): getTopKeyValueAnnotations via count-min + top-K over
     binary annotations (service u32, key hash u64 = 12 B/item), Zipf(1.1) keys over 1e6 ids,
@@ -596,7 +705,7 @@ def bench_c4(a):
         z = (z ^ shr(z, 27)) * s64(0x94D049BB133111EB)
         keys[b:e] = z ^ shr(z, 31)
     del M
-    kv = KvSketch(S, stream=stream.cuda_stream, seed=4)
+    kv = KvSketch(S, stream=stream.cuda_stream, seed=4, timing=True)
 
     def step():
         kv.reset()
@@ -628,6 +737,18 @@ def bench_c4(a):
         if not (np.array_equal(kk, kk2) and np.array_equal(est, est2) and np.array_equal(cnt, cnt2)):
             raise RuntimeError("pipelined C4 step: the two sketch sets differ")
         kv2.close()
+    # per-phase device time of isolated (serial) steps, HIP events inside zk_kv_accumulate
+    ph = []
+    for _ in range(3):
+        kv.reset()
+        kv.accumulate(svc, keys)
+        ph.append(kv.phase_ms())
+    phase = {k: float(np.median([p[k] for p in ph])) for k in ph[0]}
+    # algorithmic bytes per item: the partition reads the item (12 B) and writes its key in service
+    # order (8 B); the sketch and candidate passes each read the sorted key (8 B)
+    per_item = {"partition": 20, "sketch": 8, "candidates": 8}
+    kernels = {k: {"ms": phase[k], "bytes": n * b, "achieved_GBs": n * b / (phase[k] * 1e-3) / 1e9,
+                   "frac": n * b / (phase[k] * 1e-3) / 1e9 / PEAK_HBM_GBS} for k, b in per_item.items()}
     value = n * a.steps / wall
     achieved = n * 12 / (ev_ms / a.steps * 1e-3) / 1e9  # HIP events on the step's stream
     print(json.dumps({
@@ -635,13 +756,18 @@ def bench_c4(a):
         "value": value, "unit": "annotations/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": wall * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u32", "data": "synthetic (Zipf(1.1) keys over 1e6 ids, 500 services, generated on device)",
-        "config": {"workload": f"C4: {n:.3g} binary annotations per step, count-min 4 x 2048 per service, K=64 kept",
+        "config": {"workload": f"C4: {n:.3g} binary annotations per step, count-min 4 x {kv.width} per service, K=64 kept",
                    "items": n, "services": S,
+                   "count_min": f"depth {kv.depth} x width {kv.width} per service = {kv.depth * kv.width * S / 2**20:.2f} Mi "
+                                "u32 counters, the memory of SURVEY 8d's d=4, w=2^20; per-service error e/w x N_s "
+                                f"= {2.718281828 / kv.width / S:.3g} N with N_s = N/S, the same absolute bound as one "
+                                "global 4 x 2^20 sketch (e/2^20 N = 2.59e-6 N), delta = e^-4",
                    "step": "reset + partition + sketch + candidates + merge"
                            + (" (two sets: batch k overlaps batch k-1)" if a.pipeline else "")},
         "roofline": {"bound": "hbm", "kernel": "whole step (partition + sketch + candidates + merge)",
                      "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                      "algorithmic_bytes_per_step": n * 12},
+        "kernels": kernels,
         "detail": {"event_ms_per_step": ev_ms / a.steps, "topk_query_ms": query_ms,
                    "service0_top3": [(int(k), int(e)) for k, e in zip(kk[0][:3], est[0][:3])]},
     }), flush=True)

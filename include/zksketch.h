@@ -77,6 +77,12 @@ zk_status   zk_kv_partial(zk_kv* kv, void** counters, uint64_t* counter_bytes, v
                           uint64_t* totals_bytes);
 zk_status   zk_kv_candidates(zk_kv* kv, void** keys, void** est, uint64_t* bytes_keys, uint64_t* bytes_est);
 zk_status   zk_kv_merge_candidates(zk_kv* kv, const uint64_t* keys, const uint32_t* est, uint32_t lists);
+/* Device time (ms, HIP events on the handle's stream) of the last zk_kv_accumulate's phases:
+ * [0] service partition (histogram + scan + line scatter), [1] count-min sketch, [2] candidate
+ * pass, [3] merge. Recorded only when zk_kv_config.reserved[0] has bit 0 set (ZK_KV_TIMING);
+ * syncs the stream. */
+#define ZK_KV_TIMING 1u
+zk_status   zk_kv_phase_ms(zk_kv* kv, double out[4]);
 
 /* ------------------------------------------------------------------------------------------
  * Realtime span sketches per service: distinct traces (HyperLogLog) and duration quantiles.

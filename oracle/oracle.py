@@ -55,6 +55,9 @@ def lib():
         L = C.CDLL(str(LIB))
         L.zko_aggregate.restype = C.c_int
         L.zko_aggregate.argtypes = [C.c_void_p] * 7 + [C.c_uint64, C.c_uint32, C.c_int, C.c_void_p, C.c_void_p]
+        L.zkp_aggregate.restype = C.c_int
+        L.zkp_aggregate.argtypes = [C.c_void_p] * 7 + [C.c_uint64, C.c_uint32, C.c_int, C.c_int, C.c_void_p,
+                                                       C.c_void_p]
         _lib = L
     return _lib
 
@@ -98,6 +101,16 @@ class OracleResult:
 
 def aggregate(cols, num_services: int, threads: int | None = None) -> OracleResult:
     """Run the restatement on a zipkin_amd.SpanColumns-like object (numpy columns)."""
+    return _run(cols, num_services, threads, None)
+
+
+def aggregate_port(cols, num_services: int, threads: int | None = None, clustered: bool = True) -> OracleResult:
+    """The CPU baseline (zk_cpu_port.c): the same job in one pass, trace at a time for clustered
+    input or hash-partitioned for any order. Output identical to `aggregate`."""
+    return _run(cols, num_services, threads, clustered)
+
+
+def _run(cols, num_services, threads, port_clustered) -> OracleResult:
     if threads is None:
         threads = min(8, os.cpu_count() or 1)
     L = lib()
@@ -115,7 +128,11 @@ def aggregate(cols, num_services: int, threads: int | None = None) -> OracleResu
     ]
     n = int(arrs[0].shape[0])
     t0 = time.perf_counter()
-    rc = L.zko_aggregate(*[a.ctypes.data for a in arrs], n, S, threads, cells.ctypes.data, stats.ctypes.data)
+    if port_clustered is None:
+        rc = L.zko_aggregate(*[a.ctypes.data for a in arrs], n, S, threads, cells.ctypes.data, stats.ctypes.data)
+    else:
+        rc = L.zkp_aggregate(*[a.ctypes.data for a in arrs], n, S, threads, 1 if port_clustered else 0,
+                             cells.ctypes.data, stats.ctypes.data)
     dt = time.perf_counter() - t0
     if rc != 0:
         raise MemoryError("oracle allocation failed")

@@ -21,6 +21,10 @@ for s in $STEPS; do
     bench)
       timeout -k 10 250 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
       ok_or_stop $? bench; tail -2 gpurun_out/bench.log ;;
+    bench_c1|bench_c4|bench_c5|bench_ingest)
+      w=${s#bench_}
+      timeout -k 10 250 python bench.py --workload $w > gpurun_out/bench_$w.log 2>&1
+      ok_or_stop $? $s; tail -1 gpurun_out/bench_$w.log | cut -c1-400 ;;
     prof)
       timeout -k 10 250 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --cpu-sample 0 ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
       ok_or_stop $? prof; find gpurun_out/prof -name '*stats*' | head ;;

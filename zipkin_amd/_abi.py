@@ -259,6 +259,7 @@ _SIGNATURES = [
     ("zk_kv_partial", C.c_int, [_P, C.POINTER(_P), _U64P, C.POINTER(_P), _U64P]),
     ("zk_kv_candidates", C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), _U64P, _U64P]),
     ("zk_kv_merge_candidates", C.c_int, [_P, _P, _P, C.c_uint32]),
+    ("zk_kv_phase_ms", C.c_int, [_P, C.POINTER(C.c_double)]),
     # include/zksketch.h: realtime span sketches (HyperLogLog + duration histogram)
     ("zk_rt_create", C.c_int, [C.POINTER(zk_rt_config), C.POINTER(_P)]),
     ("zk_rt_destroy", C.c_int, [_P]),

@@ -33,6 +33,9 @@ struct zk_kv {
     uint64_t* qkeys = nullptr;  // estimate staging
     uint32_t* qest = nullptr;
     uint64_t qcap = 0;
+    bool timing = false;
+    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    bool ev_recorded = false;
     std::string err;
 };
 
@@ -104,7 +107,9 @@ zk_status zk_kv_create(const zk_kv_config* cfg, zk_kv** out) {
     a.cand = cand;
     for (uint32_t r = 0; r < kKvMaxDepth; ++r) a.seeds[r] = sk_mix64(cfg->seed + 0x9E3779B97F4A7C15ull * (r + 1));
     a.unit_items = kKvUnitItems;
+    k->timing = (cfg->reserved[0] & ZK_KV_TIMING) != 0;
     hipError_t e = hipSetDevice(k->device);
+    for (int i = 0; i < 5 && k->timing && e == hipSuccess; ++i) e = hipEventCreate(&k->ev[i]);
     if (e == hipSuccess) {
         if (cfg->stream) {
             k->stream = (hipStream_t)cfg->stream;
@@ -139,6 +144,8 @@ zk_status zk_kv_destroy(zk_kv* k) {
                     (void*)k->sorted, (void*)k->seg, (void*)k->unit_base, k->part, (void*)k->unit_key,
                     (void*)k->unit_est, k->stage, (void*)k->qkeys, (void*)k->qest})
         if (p) hipFree(p);
+    for (hipEvent_t ev : k->ev)
+        if (ev) hipEventDestroy(ev);
     if (k->own_stream && k->stream) hipStreamDestroy(k->stream);
     delete k;
     return ZK_OK;
@@ -228,8 +235,10 @@ zk_status zk_kv_accumulate(zk_kv* k, const uint32_t* svc, const uint64_t* keys, 
         KV_HIP(k, hipMalloc(&k->unit_est, max_units * a.cand * 4));
         k->unit_cap = (uint32_t)max_units;
     }
+    if (k->timing) KV_HIP(k, hipEventRecord(k->ev[0], k->stream));
     KV_HIP(k, launch_partition(plan, svc, keys, n, k->sorted, k->seg, k->dropped, k->part, k->stream));
     KV_HIP(k, launch_unit_plan(k->seg, a.S, a.unit_items, k->unit_base, k->stream));
+    if (k->timing) KV_HIP(k, hipEventRecord(k->ev[1], k->stream));
     a.keys = k->sorted;
     a.seg = k->seg;
     a.unit_base = k->unit_base;
@@ -240,8 +249,29 @@ zk_status zk_kv_accumulate(zk_kv* k, const uint32_t* svc, const uint64_t* keys, 
     a.extra_est = nullptr;
     a.extra_lists = 0;
     KV_HIP(k, launch_kv_sketch(a, k->stream));
+    if (k->timing) KV_HIP(k, hipEventRecord(k->ev[2], k->stream));
     KV_HIP(k, launch_kv_candidates(a, k->stream));
+    if (k->timing) KV_HIP(k, hipEventRecord(k->ev[3], k->stream));
     KV_HIP(k, launch_kv_merge(a, k->stream));
+    if (k->timing) {
+        KV_HIP(k, hipEventRecord(k->ev[4], k->stream));
+        k->ev_recorded = true;
+    }
+    return ZK_OK;
+    ZK_GUARD_END
+}
+
+zk_status zk_kv_phase_ms(zk_kv* k, double out[4]) {
+    ZK_GUARD_BEGIN
+    if (!k || !out) return ZK_ERR_INVALID_ARG;
+    if (!k->timing || !k->ev_recorded) return kfail(k, ZK_ERR_UNSUPPORTED, "create the sketch with ZK_KV_TIMING");
+    KV_HIP(k, hipSetDevice(k->device));
+    KV_HIP(k, hipEventSynchronize(k->ev[4]));
+    for (int i = 0; i < 4; ++i) {
+        float ms = 0.f;
+        KV_HIP(k, hipEventElapsedTime(&ms, k->ev[i], k->ev[i + 1]));
+        out[i] = ms;
+    }
     return ZK_OK;
     ZK_GUARD_END
 }

@@ -21,9 +21,10 @@ def _ptr(a) -> int:
 
 class KvSketch:
     def __init__(self, num_services: int, *, device: int = 0, stream: int | None = None, width: int = 0,
-                 depth: int = 0, candidates: int = 0, seed: int = 0):
+                 depth: int = 0, candidates: int = 0, seed: int = 0, timing: bool = False):
         self._L = _abi.lib()
         cfg = _abi.zk_kv_config()
+        cfg.reserved[0] = 1 if timing else 0  # ZK_KV_TIMING
         cfg.num_services = num_services
         cfg.device = device
         cfg.stream = stream
@@ -45,6 +46,12 @@ class KvSketch:
     def _check(self, st: int) -> None:
         if st != _abi.ZK_OK:
             raise _abi.ZkError(st, self._L.zk_kv_last_error(self._h).decode() or _abi.status_str(st))
+
+    def phase_ms(self) -> dict:
+        """Device ms of the last accumulate's phases (needs timing=True)."""
+        out = (C.c_double * 4)()
+        self._check(self._L.zk_kv_phase_ms(self._h, out))
+        return dict(zip(("partition", "sketch", "candidates", "merge"), list(out)))
 
     def close(self) -> None:
         if getattr(self, "_h", None):
