@@ -299,6 +299,7 @@ def main():
             "detail": {
                 "event_ms_per_step": ev_ms / a.steps,
                 "finalize_ms_last": tm1["finalize_ms"],
+                "reduce_avg_ms": (tm1["reduce_ms_total"] - tm0["reduce_ms_total"]) / max(1, join_calls),
                 "spill_ms_last": tm1["spill_ms"],
                 "joined_links_per_step": int(st["joined_links"]),  # stats cover the last step (reset per step)
                 "merged_spans_per_step": int(st["merged_spans"]),

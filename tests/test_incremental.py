@@ -121,21 +121,30 @@ def test_incremental_trace_straddling_the_watermark_is_new_as_a_whole():
 
 @pytest.mark.gpu
 def test_incremental_device_job_matches_oracle():
+    """Runs until up to date: every record covers exactly the traces created in (previous
+    watermark, its end] (the step boundary rule), with the device job's links equal to the
+    oracle's, and every trace is aggregated exactly once."""
     services = Dictionary(NAMES)
-    agg = GpuAggregates("cassandra", services=services)
+    agg = GpuAggregates("anorm", services=services)
     inc = IncrementalAggregator(agg)  # device ZipkinAggregateJob
     a = tracegen_host(seed=21, num_traces=2000, max_depth=6, num_services=S)
     ts_a = _created(a, 50_000)
-    rec1 = inc.apply(a, ts_a, num_services=S)
-    assert _by_key(rec1) == _expect(a, np.ones(len(a), bool), services)
     b = tracegen_host(seed=22, num_traces=1500, max_depth=6, num_services=S)
     ts_b = _created(b, int(trace_created(a, ts_a).max()) + 1)
-    both = type(a).concat([a, b])
-    ts_both = np.concatenate([ts_a, ts_b])
-    rec2 = inc.apply(both, ts_both, num_services=S)
-    new = trace_created(both, ts_both) > trace_created(a, ts_a).max()
-    assert _by_key(rec2) == _expect(both, new, services)
-    assert inc.apply(both, ts_both, num_services=S) is None
+    seen = np.zeros(len(a) + len(b), np.int64)
+    for cols, ts in ((a, ts_a), (type(a).concat([a, b]), np.concatenate([ts_a, ts_b]))):
+        tc = trace_created(cols, ts)
+        while True:
+            wm = agg.watermark()
+            rec = inc.apply(cols, ts, num_services=S)
+            if rec is None:
+                break
+            sel = (tc > wm) & (tc <= rec.end_time)
+            assert inc.last_selected == int(sel.sum()) and rec.start_time == int(tc[tc > wm].min())
+            assert _by_key(rec) == _expect(cols, sel, services)
+            seen[: len(cols)] += sel
+        assert agg.watermark() == tc.max()
+    assert (seen == 1).all()
 
 
 def test_run_without_links_still_advances_the_watermark():

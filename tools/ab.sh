@@ -11,7 +11,9 @@ for r in 1 2 3; do
 import json, sys
 v = sys.argv[1]
 j = json.loads(open(f"gpurun_out/ab_{v}.log").read().strip().splitlines()[-1])
-print(f"{v:10s} step {j['ms_per_step']:.4f} ms  K1 {j['roofline']['avg_launch_ms']:.4f} ms  frac {j['roofline']['frac']:.3f}")
+d = j.get("detail", {})
+print(f"{v:10s} step {j['ms_per_step']:.4f} ms  K1 {j['roofline']['avg_launch_ms']:.4f} ms  frac {j['roofline']['frac']:.3f}"
+      f"  K1-isolated {j['roofline'].get('isolated_avg_launch_ms') or 0:.4f}  reduce {d.get('reduce_avg_ms', 0):.4f}")
 PY
   done
 done

@@ -391,11 +391,16 @@ __global__ __launch_bounds__(1 << CB_SHIFT) void k_bucket_reduce(ReduceArgs r, u
 
 }  // namespace
 
+#ifndef ZK_CB_MIN_SHIFT
+#define ZK_CB_MIN_SHIFT 9  // smallest cell bucket: 2^9 cells (2^8: 977 buckets at S = 500, measured
+                           // 0.46 -> 0.53 ms for K2 + K3: K2's per-bucket LDS carry doubles)
+#endif
+
 void bucket_geometry(uint32_t S, uint32_t* nb, uint32_t* cb_shift) {
     const uint64_t cells = (uint64_t)S * S;
     *nb = 0;
     *cb_shift = 0;
-    for (uint32_t sh = 9; sh <= 10; ++sh) {
+    for (uint32_t sh = ZK_CB_MIN_SHIFT; sh <= 10; ++sh) {
         const uint64_t n = (cells + (1ull << sh) - 1) >> sh;
         if (n <= kMaxBuckets) {
             *nb = (uint32_t)n;
@@ -412,7 +417,9 @@ hipError_t launch_partitioned_reduce(const ReduceArgs& r, hipStream_t s) {
     hipLaunchKernelGGL((k_link_scatter<ZK_K2_U, ZK_K2_WG>), dim3(r.lists), dim3(ZK_K2_WG), (size_t)r.nb * kScatterLine * 8, s, r);
     const uint32_t splits = r.nb >= 256 ? 1u : (512u + r.nb - 1) / r.nb;
     // CB = 512: 512 threads, 4096-link chunks (36 KB LDS); CB = 1024: 1024 threads, 4096-link chunks
-    if (r.cb_shift == 9)
+    if (r.cb_shift == 8)
+        hipLaunchKernelGGL((k_bucket_reduce<8, 16>), dim3(r.nb * splits), dim3(256), 0, s, r, splits);
+    else if (r.cb_shift == 9)
         hipLaunchKernelGGL((k_bucket_reduce<9, 8>), dim3(r.nb * splits), dim3(512), 0, s, r, splits);
     else
         hipLaunchKernelGGL((k_bucket_reduce<10, 4>), dim3(r.nb * splits), dim3(1024), 0, s, r, splits);
