@@ -124,10 +124,17 @@ __device__ __forceinline__ void emit_link(uint64_t* __restrict__ table, uint32_t
     add_chunk(c + kLimbS4 + 4, w2);
 }
 
-// packed per-thread stat counters: 4 x 16-bit fields per u64 (a tile never exceeds 2^16)
+// packed per-thread stat counters of K1: 4 x 16-bit fields per u64 (a thread adds <= 2 per stat per
+// window; folded every kFoldWindows windows, so a wave sum of 64 lanes stays below 2^16)
 struct StatPack {
     uint64_t w[4] = {0, 0, 0, 0};
     __device__ __forceinline__ void inc(int s, uint32_t v = 1) { w[s >> 2] += (uint64_t)v << (16 * (s & 3)); }
+};
+// the spill kernel's counters: one u64 per stat (a spilled trace can hold up to 2^20 records, more
+// than 16-bit wave sums can count)
+struct StatWide {
+    uint64_t w[ST_N] = {};
+    __device__ __forceinline__ void inc(int s, uint32_t v = 1) { w[s] += v; }
 };
 
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
@@ -136,27 +143,21 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
     return v;
 }
 
-// Per-thread packed counts -> per-wave sums (16-bit fields cannot overflow: a wave covers at most
-// 64 x 512 records) -> u32 LDS totals -> one add per stat into a sharded global slot (the stats
-// array holds kStatShards copies, summed by the host, so 1e5 tiles never hammer one address).
-__device__ __forceinline__ void flush_stats(StatPack& sp, uint32_t* s_stat, unsigned long long* g_stats) {
+// spill kernel: per-thread counts -> per-wave sums -> u64 LDS totals -> one add per stat into a
+// sharded global slot (the stats array holds kStatShards copies, summed by the host, so 1e5 tiles
+// never hammer one address)
+__device__ __forceinline__ void flush_stats(StatWide& sp, unsigned long long* s_stat, unsigned long long* g_stats) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < ST_N; ++i) {
         const uint64_t v = wave_sum_u64(sp.w[i]);
-        if (lane == 0 && v) {
-#pragma unroll
-            for (int f = 0; f < 4; ++f) {
-                const uint32_t x = (uint32_t)((v >> (16 * f)) & 0xFFFFull);
-                if (x) atomicAdd(&s_stat[i * 4 + f], x);
-            }
-        }
+        if (lane == 0 && v) atomicAdd(&s_stat[i], (unsigned long long)v);
     }
     __syncthreads();
     if (threadIdx.x < ST_N) {
-        const uint32_t v = s_stat[threadIdx.x];
+        const unsigned long long v = s_stat[threadIdx.x];
         unsigned long long* slot = g_stats + (uint64_t)(blockIdx.x % kStatShards) * ST_N;
-        if (v) atomicAdd(&slot[threadIdx.x], (unsigned long long)v);
+        if (v) atomicAdd(&slot[threadIdx.x], v);
     }
 }
 
@@ -340,7 +341,24 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     }
     const uint64_t R1 = (R0 + a.per_wg < n) ? R0 + a.per_wg : n;
     uint64_t* __restrict__ out = a.links + (uint64_t)blockIdx.x * a.link_stride;
+#ifndef ZK_K1_TRASH_SPREAD
+#define ZK_K1_TRASH_SPREAD 0
+#endif
+#ifndef ZK_K1_OOB_STORE
+#define ZK_K1_OOB_STORE 0
+#endif
+#if ZK_K1_TRASH_SPREAD
+    // absent links go to a per-thread trash slot at the end of the list (join_geometry reserves TILE)
+    const uint64_t trash = a.link_stride - TILE + 2 * tid;
+#else
     const uint64_t trash = a.link_stride - 1;  // never a real link slot (join_geometry)
+#endif
+#if ZK_K1_OOB_STORE
+    // the link list as a buffer: an absent link is stored at an offset past num_records, which the
+    // hardware drops -- still exactly two stores per thread per window, no trash traffic
+    const __amdgpu_buffer_rsrc_t out_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)out, (short)0, (int)((a.link_stride - 1) * 8), 0x00020000);
+#endif
     uint64_t* __restrict__ it_pay = a.rt_pay + (uint64_t)blockIdx.x * a.link_stride;
     uint32_t* __restrict__ it_svc = a.rt_svc + (uint64_t)blockIdx.x * a.link_stride;
     uint32_t nitem = 0;       // sketch items written by this workgroup (uniform)
@@ -664,7 +682,13 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const bool v = r_link[e] != ~0ull;
-                out[v ? (uint64_t)pos : trash] = r_link[e];
+#if ZK_K1_OOB_STORE
+                typedef unsigned int v2u_t __attribute__((ext_vector_type(2)));
+                const v2u_t lv = {(unsigned int)r_link[e], (unsigned int)(r_link[e] >> 32)};
+                __builtin_amdgcn_raw_buffer_store_b64(lv, out_rsrc, v ? pos * 8u : 0x7FFFFFF8u, 0, 0);
+#else
+                out[v ? (uint64_t)pos : trash + (ZK_K1_TRASH_SPREAD ? e : 0)] = r_link[e];
+#endif
                 pos += v ? 1u : 0u;
             }
             nout += total & 0xFFFFu;
@@ -785,12 +809,12 @@ __device__ __forceinline__ bool spill_valid(uint64_t A, uint64_t B) {
 
 __global__ __launch_bounds__(kSpillWG) void k_span_join_spill(JoinArgs a) {
     __shared__ unsigned long long s_end;
-    __shared__ uint32_t s_stat[ST_N];
+    __shared__ unsigned long long s_stat[ST_N];
     const uint32_t total = min(*a.spill_count, (unsigned int)a.spill_cap);
     const uint64_t n = a.c.n;
     const uint64_t* __restrict__ tr = a.c.trace_id;
     uint8_t* base = a.spill_scratch + (uint64_t)blockIdx.x * a.spill_scratch_stride;
-    StatPack st;
+    StatWide st;
     if (threadIdx.x < ST_N) s_stat[threadIdx.x] = 0u;
     for (uint32_t e = blockIdx.x; e < total; e += gridDim.x) {
         const uint64_t s = a.spill_list[e];
@@ -952,9 +976,9 @@ __global__ __launch_bounds__(kSpillWG) void k_span_join_spill(JoinArgs a) {
         if (threadIdx.x == 0) atomicAdd(&a.stats[ST_RECORDS], (unsigned long long)L);
         // flush per trace so the per-thread 16-bit fields never overflow
         flush_stats(st, s_stat, a.stats);
-        st = StatPack();
+        st = StatWide();
         __syncthreads();
-        if (threadIdx.x < ST_N) s_stat[threadIdx.x] = 0u;
+        if (threadIdx.x < ST_N) s_stat[threadIdx.x] = 0ull;
         __syncthreads();
     }
 }
@@ -1017,8 +1041,12 @@ void join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, u
     const uint64_t per = ((n + g - 1) / g + kTile - 1) / kTile * kTile;
     *grid = (uint32_t)g;
     *per_wg = per ? per : kTile;
-    // a workgroup's last trace may overhang its range by < TILE; +1: the trash slot of K1's stores
+    // a workgroup's last trace may overhang its range by < TILE; then the trash slot(s) of K1's stores
+#if ZK_K1_TRASH_SPREAD
+    *link_stride = *per_wg + 2 * kTile;
+#else
     *link_stride = *per_wg + kTile + 1;
+#endif
 }
 
 }  // namespace zk

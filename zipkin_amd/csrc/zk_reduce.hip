@@ -389,7 +389,88 @@ __global__ __launch_bounds__(1 << CB_SHIFT) void k_bucket_reduce(ReduceArgs r, u
     }
 }
 
+// K3, LDS-atomic form: one bucket per workgroup. Every link adds its 32-bit-chunk contributions to
+// the bucket's limb table in LDS with non-returning 64-bit LDS atomics -- no counting sort, no
+// per-chunk barriers and no run-length imbalance (every thread handles the same number of links).
+// Limb-major table [15][CB]: lanes with random cells spread over the banks. d < 2^32 (durations
+// under 71 minutes) touches 11 limbs; a longer d touches all 15.
+template <int CB_SHIFT, int WG, int U>
+__global__ __launch_bounds__(WG) void k_bucket_lds_reduce(ReduceArgs r, uint32_t splits) {
+    constexpr int CB = 1 << CB_SHIFT;
+    __shared__ unsigned long long s_t[15 * CB];
+    const int tid = threadIdx.x;
+    const uint32_t b = blockIdx.x / splits, part = blockIdx.x % splits;
+    for (int x = tid; x < 15 * CB; x += WG) s_t[x] = 0ull;
+    const uint64_t lo = r.bucket_base[b], hi = r.bucket_base[b + 1];
+    const uint64_t per = (hi - lo + splits - 1) / splits;
+    const uint64_t s0 = lo + per * part;
+    const uint64_t s1 = (s0 + per < hi) ? s0 + per : hi;
+    const uint64_t cell0 = (uint64_t)b << CB_SHIFT;
+    __syncthreads();
+    constexpr uint64_t M = 0xFFFFFFFFull;
+    for (uint64_t base = s0; base < s1; base += (uint64_t)WG * U) {
+        uint64_t v[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const uint64_t i = base + tid + (uint64_t)k * WG;
+            v[k] = i < s1 ? r.sorted[i] : ~0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            if (v[k] == ~0ull) continue;
+            const uint32_t c = (uint32_t)((v[k] >> 40) - cell0);
+            const uint64_t d = v[k] & (kMaxDuration - 1);
+            unsigned long long* t = s_t + c;
+            atomicAdd(&t[kLimbM0 * CB], 1ull);
+            if ((d >> 32) == 0) {
+                const uint64_t d2 = d * d;                                   // < 2^64
+                const unsigned __int128 d3 = (unsigned __int128)d2 * d;       // < 2^96
+                const unsigned __int128 d4 = (unsigned __int128)d2 * d2;      // < 2^128
+                const uint64_t d3lo = (uint64_t)d3, d4lo = (uint64_t)d4, d4hi = (uint64_t)(d4 >> 64);
+                atomicAdd(&t[kLimbS1 * CB], (unsigned long long)d);
+                atomicAdd(&t[(kLimbS2 + 0) * CB], (unsigned long long)(d2 & M));
+                atomicAdd(&t[(kLimbS2 + 1) * CB], (unsigned long long)(d2 >> 32));
+                atomicAdd(&t[(kLimbS3 + 0) * CB], (unsigned long long)(d3lo & M));
+                atomicAdd(&t[(kLimbS3 + 1) * CB], (unsigned long long)(d3lo >> 32));
+                atomicAdd(&t[(kLimbS3 + 2) * CB], (unsigned long long)(uint64_t)(d3 >> 64));
+                atomicAdd(&t[(kLimbS4 + 0) * CB], (unsigned long long)(d4lo & M));
+                atomicAdd(&t[(kLimbS4 + 1) * CB], (unsigned long long)(d4lo >> 32));
+                atomicAdd(&t[(kLimbS4 + 2) * CB], (unsigned long long)(d4hi & M));
+                atomicAdd(&t[(kLimbS4 + 3) * CB], (unsigned long long)(d4hi >> 32));
+            } else {
+#pragma unroll
+                for (int q = 1; q < 15; ++q) {
+                    const uint64_t x = limb_value(q, d);
+                    if (x) atomicAdd(&t[q * CB], (unsigned long long)x);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (int c = tid; c < CB; c += WG) {
+        const uint64_t cell = cell0 + c;
+        if (cell >= r.cells) continue;
+        uint64_t* dst = r.table + cell * kLimbs;
+#pragma unroll
+        for (int q = 0; q < 15; ++q) {
+            const uint64_t x = s_t[q * CB + c];
+            if (!x) continue;
+            if (splits == 1)
+                dst[q] += x;  // this workgroup owns the cell
+            else
+                atomicAdd((unsigned long long*)&dst[q], (unsigned long long)x);
+        }
+    }
+}
+
 }  // namespace
+
+#ifndef ZK_K3_LDS
+// 1 (default): K3 as LDS atomics (k_bucket_lds_reduce); 0: counting sort + owner sums
+// (k_bucket_reduce). Same box, interleaved (profiles/r02/ab_k3lds.txt): serial steps equal
+// (K2 + K3 0.45 ms either way), pipelined steps 1.63 -> 1.57 ms.
+#define ZK_K3_LDS 1
+#endif
 
 #ifndef ZK_CB_MIN_SHIFT
 #define ZK_CB_MIN_SHIFT 9  // smallest cell bucket: 2^9 cells (2^8: 977 buckets at S = 500, measured
@@ -416,6 +497,16 @@ hipError_t launch_partitioned_reduce(const ReduceArgs& r, hipStream_t s) {
     hipLaunchKernelGGL(k_bucket_base, dim3(1), dim3(1024), 0, s, r.bucket_base, r.nb);
     hipLaunchKernelGGL((k_link_scatter<ZK_K2_U, ZK_K2_WG>), dim3(r.lists), dim3(ZK_K2_WG), (size_t)r.nb * kScatterLine * 8, s, r);
     const uint32_t splits = r.nb >= 256 ? 1u : (512u + r.nb - 1) / r.nb;
+#if ZK_K3_LDS
+    if (r.cb_shift == 8) {
+        hipLaunchKernelGGL((k_bucket_lds_reduce<8, 256, 4>), dim3(r.nb * splits), dim3(256), 0, s, r, splits);
+        return hipGetLastError();
+    }
+    if (r.cb_shift == 9) {
+        hipLaunchKernelGGL((k_bucket_lds_reduce<9, 512, 4>), dim3(r.nb * splits), dim3(512), 0, s, r, splits);
+        return hipGetLastError();
+    }
+#endif
     // CB = 512: 512 threads, 4096-link chunks (36 KB LDS); CB = 1024: 1024 threads, 4096-link chunks
     if (r.cb_shift == 8)
         hipLaunchKernelGGL((k_bucket_reduce<8, 16>), dim3(r.nb * splits), dim3(256), 0, s, r, splits);
