@@ -25,6 +25,13 @@
 #ifndef ZK_K1_WGS_PER_CU
 #define ZK_K1_WGS_PER_CU 4  // resident K1 workgroups per CU (one wave per SIMD each)
 #endif
+// A/B variant of the north star's sorted-segment design (not the product): instead of the LDS hash,
+// every record ranks itself inside its trace segment by (spanId, index) -- a rank sort, so the
+// segment's records land in s_perm in sorted order and the first of equal spanIds is the merge
+// leader -- and a child finds its parent by binary search over the sorted segment.
+#ifndef ZK_K1_SORTJOIN
+#define ZK_K1_SORTJOIN 0
+#endif
 
 namespace zk {
 namespace {
@@ -313,7 +320,7 @@ constexpr int kModeEmit = 2;
 template <int TILE, int WG, int ABL, int MODE>
 // launch bounds: minimum waves per SIMD = resident workgroups per CU x waves per workgroup / 4 SIMDs
 __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_stream(JoinArgs a) {
-    constexpr int H = ZK_HASH_FACTOR * TILE;  // load <= 1/16 (distinct spans / slots): short probe chains, since a wave waits for its longest
+    constexpr int H = ZK_K1_SORTJOIN ? 64 : ZK_HASH_FACTOR * TILE;  // load <= 1/16 (distinct spans / slots): short probe chains, since a wave waits for its longest
     constexpr int NWORD = TILE / 64;
     static_assert(TILE == 2 * WG && TILE <= 2047, "two records per thread");
     __shared__ __align__(16) uint64_t s_sid[TILE];
@@ -323,6 +330,10 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     __shared__ __align__(16) uint32_t s_svck[TILE];
     __shared__ __align__(16) uint16_t s_seg[TILE];
     __shared__ __align__(16) uint32_t s_ht[H];
+#if ZK_K1_SORTJOIN
+    __shared__ __align__(16) uint32_t s_bits[TILE];  // merged seen-once/twice + parent bits per leader
+    __shared__ __align__(16) uint16_t s_perm[TILE];  // segment records in (spanId, index) order
+#endif
     __shared__ __align__(16) uint64_t s_mask[NWORD];
     __shared__ uint32_t s_stat[ST_N];
     __shared__ uint32_t s_wsum[WG / 64];
@@ -398,6 +409,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         // lane w < NW holds wave w's masks: the first boundary >= lo_j (start), the first >= r1_j
         // (stop), the last of the window (last_b) and the last before this wave's records (prev_b)
         int start = -1, stop = -1, last_b = -1, prev_b = -1;  // wave-uniform (SGPRs)
+        int next_after = wn;
         {
             constexpr int NW = WG / 64;
             uint64_t ev = 0ull, od = 0ull;
@@ -428,6 +440,17 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 const int w = 63 - (int)__clzll((long long)bp);
                 prev_b = 128 * w + __builtin_amdgcn_readlane(lb, w);
             }
+#if ZK_K1_SORTJOIN
+            {  // the first boundary after this wave's records (a segment's end), else the window end
+                const int fb = lane < NW ? first_ge(ev, od, 0) : -1;
+                const uint64_t bf = __ballot(fb >= 0) & ~((2ull << wave) - 1ull);
+                next_after = wn;
+                if (bf) {
+                    const int w = __ffsll((unsigned long long)bf) - 1;
+                    next_after = 128 * w + __builtin_amdgcn_readlane(fb, w);
+                }
+            }
+#endif
         }
         const bool at_end = ws + (uint64_t)wn >= n;
         int m;                  // records [start, m) are processed in this window
@@ -477,6 +500,9 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         int r_seg[2];
         uint32_t r_svck[2];
         bool r_rerr[2];
+#if ZK_K1_SORTJOIN
+        int r_end[2];  // end of the record's trace segment in the window
+#endif
         {
             const int j0 = 2 * tid;
             // last boundary <= j0 among this wave's records, else the one before the wave (it exists
@@ -504,6 +530,16 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             *reinterpret_cast<ulonglong2*>(&s_pid[j0]) = make_ulonglong2(v_pid[0], v_pid[1]);
             *reinterpret_cast<uint2*>(&s_svck[j0]) = make_uint2(r_svck[0], r_svck[1]);
             *reinterpret_cast<uint32_t*>(&s_seg[j0]) = ((uint32_t)r_seg[0] & 0xFFFFu) | ((uint32_t)r_seg[1] << 16);
+#if ZK_K1_SORTJOIN
+            {
+                const int p0 = first_ge(m_ev, m_od, 2 * lane + 1), p1 = first_ge(m_ev, m_od, 2 * lane + 2);
+                r_end[0] = p0 >= 0 ? 128 * wave + p0 : next_after;
+                r_end[1] = p1 >= 0 ? 128 * wave + p1 : next_after;
+                uint32_t once;
+                *reinterpret_cast<uint2*>(&s_bits[j0]) =
+                    make_uint2(frag_bits(cur.flags[0], &once), frag_bits(cur.flags[1], &once));
+            }
+#endif
         }
         __syncthreads();  // (the hash table is empty here: cleared once, then by its leaders)
         ZK_STAMP(2);
@@ -512,6 +548,25 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         // Both records of the thread probe together (one LDS round trip per step for the pair).
         int r_leader[2];
         uint32_t r_slot[2];
+#if ZK_K1_SORTJOIN
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            r_leader[e] = -1;
+            r_slot[e] = 0u;
+            if (r_seg[e] < 0) continue;
+            const int j = 2 * tid + e;
+            const uint64_t sid = cur.sid[e];
+            int rank = 0, L = j;
+            for (int k = r_seg[e]; k < r_end[e]; ++k) {
+                const uint64_t x = s_sid[k];
+                rank += (x < sid || (x == sid && k < j)) ? 1 : 0;
+                L = (x == sid && k < L) ? k : L;
+            }
+            r_leader[e] = L;
+            s_perm[r_seg[e] + rank] = (uint16_t)j;
+        }
+        if (false)
+#endif
         {
             bool act[2];
             uint32_t word[2];
@@ -575,9 +630,14 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 if (f & ZK_F_HAS_PARENT) atomicMin((unsigned long long*)&s_pid[L], (unsigned long long)cur.pid[e]);
                 uint32_t once;
                 const uint32_t bits = frag_bits(f, &once);
-                const uint32_t old = atomicOr(&s_ht[r_slot[e]], bits);
+#if ZK_K1_SORTJOIN
+                uint32_t* const wp = &s_bits[L];
+#else
+                uint32_t* const wp = &s_ht[r_slot[e]];
+#endif
+                const uint32_t old = atomicOr(wp, bits);
                 const uint32_t promote = once & (old >> kSlotA) & 0xFu;  // second occurrence
-                if (promote) atomicOr(&s_ht[r_slot[e]], promote << kSlotB);
+                if (promote) atomicOr(wp, promote << kSlotB);
             }
         }
         __syncthreads();
@@ -596,7 +656,11 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             if (L < 0) continue;
             const int j = 2 * tid + e;
             const uint32_t f = cur.flags[e];
+#if ZK_K1_SORTJOIN
+            const uint32_t w = s_bits[L];
+#else
             const uint32_t w = s_ht[r_slot[e]];
+#endif
             const uint32_t sL = s_svck[L];
             const uint64_t pL = s_pid[L];
             bool amb = (f & ZK_F_HAS_PARENT) ? (cur.pid[e] != pL) : ((w & kSlotP1) != 0u);
@@ -624,6 +688,35 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             if constexpr (!JOIN) continue;
             if (!(valid && (w & kSlotP1))) continue;
             st.inc(ST_CHILD);
+#if ZK_K1_SORTJOIN
+            // binary search of the parent's spanId in the sorted segment: the first of equal spanIds
+            // is the parent span's leader
+            int P = -1;
+            uint32_t pw = 0;
+            {
+                int lo = r_seg[e], hi = r_end[e];
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (s_sid[s_perm[mid]] < pL)
+                        lo = mid + 1;
+                    else
+                        hi = mid;
+                }
+                if (lo < r_end[e]) {
+                    const int q = s_perm[lo];
+                    if (s_sid[q] == pL) {
+                        P = q;
+                        pw = s_bits[q];
+                    }
+                }
+            }
+            if (P < 0 || !slot_valid(pw)) {
+                st.inc(ST_MISSING_PARENT);
+                continue;
+            }
+            st.inc(ST_JOINED);
+            const uint32_t sp = s_svck[P];
+#else
             const uint16_t seg = (uint16_t)r_seg[e];
             uint32_t slot = slot_hash(pL, seg) & (H - 1);
             uint32_t pw = 0;
@@ -643,6 +736,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             }
             st.inc(ST_JOINED);
             const uint32_t sp = s_svck[(pw & kSlotIdx) - 1];
+#endif
             if (sp == kSvcNone || sL == kSvcNone) {
                 st.inc(ST_NO_SERVICE);
                 continue;
@@ -709,7 +803,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         // the next window inserts only after its phase-1 and phase-3 barriers)
 #pragma unroll
         for (int e = 0; e < 2; ++e)
-            if (r_leader[e] == 2 * tid + e) s_ht[r_slot[e]] = 0u;
+            if (!ZK_K1_SORTJOIN && r_leader[e] == 2 * tid + e) s_ht[r_slot[e]] = 0u;
         ZK_STAMP(6);
         }  // ablate != 2
         if (--fold_in == 0) {
