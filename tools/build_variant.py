@@ -50,8 +50,8 @@ def main():
         with ThreadPoolExecutor(max_workers=8) as ex:
             objs = list(ex.map(cc, srcs))
         out = ROOT / "zipkin_amd" / f"libzkagg_{a.name}.so"
-        subprocess.run([zb._hipcc(), f"--offload-arch={zb.ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(out)],
-                       check=True)
+        subprocess.run([zb._hipcc(), f"--offload-arch={zb.ARCH}", "-shared", "-fPIC", *map(str, objs), "-L/opt/rocm/lib",
+                        "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib", "-o", str(out)], check=True)
         print(out)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)

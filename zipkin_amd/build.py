@@ -78,7 +78,8 @@ def build(force: bool = False, verbose: bool = False, variant: str = "", defines
 
     with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
         objs = list(ex.map(compile_one, SOURCES))
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *[str(o) for o in objs], "-o", str(lib) + ".tmp"]
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *[str(o) for o in objs], "-L/opt/rocm/lib",
+           "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib", "-o", str(lib) + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -218,6 +218,7 @@ SpanColsMut carve_cols(uint8_t* p, uint64_t n) {
 
 // clustering pass: d (any order) -> ctx-owned trace-clustered columns
 zk_status cluster_batch(zk_ctx* c, SpanColsDev* d) {
+    RoctxRange rr("zk_cluster_batch");
     const uint64_t n = d->n;
     if (n > 0xFFFFFFFFull) return fail(c, ZK_ERR_CAPACITY, "an unclustered batch is limited to 2^32-1 records");
     if (n > c->cl_cap) {
@@ -251,6 +252,7 @@ uint64_t pow2_at_least(uint64_t x) {
 // ZK_BATCH_VERIFY_TRACES: grow the traceId set (load <= 1/2 even if every record were its own
 // trace) and insert the batch's trace runs
 zk_status verify_batch(zk_ctx* c, const SpanColsDev& d) {
+    RoctxRange rr("zk_verify_traces");
     const uint64_t need = pow2_at_least(2 * (c->tset_records + d.n) > (1ull << 16) ? 2 * (c->tset_records + d.n)
                                                                                    : (1ull << 16));
     if (need > c->tset_slots) {
@@ -409,6 +411,7 @@ zk_status zk_deps_reset(zk_ctx* c) {
 zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags) {
     if (!c) return ZK_ERR_INVALID_ARG;
     ZK_TRY
+    RoctxRange rr("zk_deps_accumulate");
     if (!cols) return fail(c, ZK_ERR_INVALID_ARG, "null columns");
     if (flags & ~(ZK_BATCH_DEVICE_PTRS | ZK_BATCH_TRACE_CLUSTERED | ZK_BATCH_VERIFY_TRACES))
         return fail(c, ZK_ERR_INVALID_ARG, "unknown batch flag");
@@ -556,6 +559,7 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
 zk_status zk_deps_finalize(zk_ctx* c, const zk_link_table* out) {
     if (!c) return ZK_ERR_INVALID_ARG;
     ZK_TRY
+    RoctxRange rr("zk_deps_finalize");
     if (!out || !out->m0 || !out->m1 || !out->m2 || !out->m3 || !out->m4 || !out->present)
         return fail(c, ZK_ERR_INVALID_ARG, "null output array");
     ZK_HIP(c, hipSetDevice(c->device));

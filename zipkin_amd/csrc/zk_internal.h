@@ -7,6 +7,18 @@
 
 #include "../../include/zkagg.h"
 
+// roctx ranges around the library's host calls (rocprofv3 --marker-trace shows them next to the
+// kernels they enqueue); a scope object so every return path pops
+#include <rocprofiler-sdk-roctx/roctx.h>
+namespace zk {
+struct RoctxRange {
+    explicit RoctxRange(const char* name) { roctxRangePushA(name); }
+    ~RoctxRange() { roctxRangePop(); }
+    RoctxRange(const RoctxRange&) = delete;
+    RoctxRange& operator=(const RoctxRange&) = delete;
+};
+}  // namespace zk
+
 namespace zk {
 
 // ---- exact accumulator layout ----------------------------------------------------------------

@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "zk_guard.h"
+#include "zk_internal.h"
 #include "zk_sketch_internal.h"
 #include "zksketch.h"
 
@@ -184,6 +185,7 @@ zk_status zk_kv_accumulate(zk_kv* k, const uint32_t* svc, const uint64_t* keys, 
     if (n == 0) return ZK_OK;
     if (!svc || !keys) return kfail(k, ZK_ERR_INVALID_ARG, "null input");
     if (n >= (1ull << 32)) return kfail(k, ZK_ERR_INVALID_ARG, "batch of >= 2^32 items");
+    RoctxRange rr("zk_kv_accumulate");
     KV_HIP(k, hipSetDevice(k->device));
     if (!(flags & ZK_BATCH_DEVICE_PTRS)) {
         if (n > k->stage_cap) {
