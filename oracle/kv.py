@@ -105,6 +105,27 @@ class KvOracle:
             o = np.lexsort((allk, -est.astype(np.int64)))[: self.cand]
             self.lists[s] = [(int(allk[i]), int(est[i])) for i in o]
 
+    @classmethod
+    def merged(cls, shards: list["KvOracle"]) -> "KvOracle":
+        """The job-wide sketch of disjoint item shards (include/zksketch.h, zk_kv_merge_candidates):
+        counters and totals are summed (count-min is linear, so they equal one sketch over all
+        items); every shard's list is offered, deduplicated, re-estimated against the summed
+        counters and the best `candidates` kept, ordered (estimate desc, key asc)."""
+        a = shards[0]
+        out = cls(a.S, width=a.width, depth=a.depth, candidates=a.cand)
+        out.seeds = list(a.seeds)
+        out.cm = np.sum([o.cm for o in shards], axis=0, dtype=np.uint64)
+        out.totals = np.sum([o.totals for o in shards], axis=0, dtype=np.uint64)
+        out.dropped = sum(o.dropped for o in shards)
+        for s in range(a.S):
+            allk = np.unique(np.array([k for o in shards for k, _ in o.lists[s]], dtype=np.uint64))
+            if len(allk) == 0:
+                continue
+            est = out.estimate(s, allk)
+            o = np.lexsort((allk, -est.astype(np.int64)))[: out.cand]
+            out.lists[s] = [(int(allk[i]), int(est[i])) for i in o]
+        return out
+
     def topk(self, service: int, k: int) -> list[tuple[int, int]]:
         return self.lists[service][:k]
 

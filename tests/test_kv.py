@@ -58,6 +58,26 @@ def test_oracle_topk_finds_heavy_hitters_across_batches():
             assert k in got
 
 
+def test_oracle_shard_merge_equals_one_sketch_on_heavy_hitters():
+    """KvOracle.merged (the restatement of the N>1 merge): summed counters equal one sketch over
+    all items bit for bit, and the clear heavy hitters come out with the same estimates."""
+    S = 5
+    svc, keys = zipf_items(90_000, S, num_keys=4000, s=1.3, seed=6)
+    one = KvOracle(S, width=1024, depth=4, candidates=32, seed=3)
+    one.accumulate(svc, keys)
+    parts = []
+    for a, b in ((0, 20_000), (20_000, 20_000), (20_000, 90_000)):
+        o = KvOracle(S, width=1024, depth=4, candidates=32, seed=3)
+        o.accumulate(svc[a:b], keys[a:b])
+        parts.append(o)
+    m = KvOracle.merged(parts)
+    assert np.array_equal(m.cm, one.cm) and np.array_equal(m.totals, one.totals)
+    for s in range(S):
+        assert m.topk(s, 5) == one.topk(s, 5)
+        for k, e in m.topk(s, 32):  # every merged estimate is the one-sketch estimate
+            assert int(one.estimate(s, [k])[0]) == e
+
+
 def test_oracle_drops_out_of_range_services():
     o = KvOracle(3, width=64, depth=2, candidates=4)
     o.accumulate(np.array([0, 1, 3, 7], np.uint32), np.array([5, 5, 5, 5], np.uint64))

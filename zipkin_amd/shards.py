@@ -68,6 +68,84 @@ def allreduce_kv_counters(counters, totals, group=None) -> None:
     dist.all_reduce(totals, op=dist.ReduceOp.SUM, group=group)
 
 
+_TYPESTR = {"uint8": "|u1", "int32": "<i4", "int64": "<i8"}
+
+
+class _DeviceBuffer:
+    """__cuda_array_interface__ (v3) of a library-owned device buffer, for torch.as_tensor."""
+
+    def __init__(self, ptr: int, nbytes: int, dtype):
+        name = str(dtype).replace("torch.", "")
+        size = {"uint8": 1, "int32": 4, "int64": 8}[name]
+        if nbytes % size:
+            raise ValueError(f"{nbytes} bytes is not a whole number of {name}")
+        self.__cuda_array_interface__ = {"shape": (nbytes // size,), "typestr": _TYPESTR[name],
+                                         "data": (int(ptr), False), "version": 3, "strides": None}
+
+
+def device_view(ptr: int, nbytes: int, dtype, device: int = 0):
+    """Zero-copy torch tensor over a buffer the library owns (zk_rt_partial / zk_kv_partial /
+    zk_kv_candidates), so that RCCL reduces the sketch state in place. The view does not keep
+    the handle alive: use it only while the sketch is open."""
+    import torch
+
+    return torch.as_tensor(_DeviceBuffer(ptr, nbytes, dtype), device=torch.device("cuda", device))
+
+
+def rt_views(rt, device: int = 0):
+    """(registers uint8[S*2^p], histogram int32[S*bins]) device views of an RtSketch."""
+    import torch
+
+    rp, rb, hp, hb = rt.partial()
+    return device_view(rp, rb, torch.uint8, device), device_view(hp, hb, torch.int32, device)
+
+
+def kv_views(kv, device: int = 0):
+    """(counters int32[S*depth*width], totals int64[S], candidate keys int64[S, C], candidate
+    estimates int32[S, C]) device views of a KvSketch."""
+    import torch
+
+    cp, cb, tp, tb = kv.partial()
+    kp, ep, kb, eb = kv.candidate_buffers()
+    S, C = kv.num_services, kv.candidates
+    return (device_view(cp, cb, torch.int32, device), device_view(tp, tb, torch.int64, device),
+            device_view(kp, kb, torch.int64, device).view(S, C), device_view(ep, eb, torch.int32, device).view(S, C))
+
+
+def merge_rt(rt, group=None, device: int = 0) -> None:
+    """Job-wide realtime sketch on every rank: MAX/SUM all-reduce of this rank's RtSketch state
+    (each rank fed a disjoint traceId shard). Call after the rank's accumulates; the library's
+    stream is drained first, the collective runs on torch's current stream and is complete on
+    return, so the sketch's queries read the merged state."""
+    import torch
+
+    torch.cuda.synchronize(device)
+    regs, hist = rt_views(rt, device)
+    allreduce_sketch(regs, hist, group)
+    torch.cuda.current_stream(device).synchronize()
+
+
+def merge_kv(kv, group=None, device: int = 0) -> None:
+    """Job-wide key-value top-K on every rank (any item sharding): SUM all-reduce of the count-min
+    counters and totals, all-gather of every rank's candidate lists, then zk_kv_merge_candidates
+    re-estimates them against the merged counters, so every rank holds the same lists."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    torch.cuda.synchronize(device)
+    counters, totals, keys, est = kv_views(kv, device)
+    # the candidate lists are gathered before anything changes them: the merge overwrites them
+    all_keys = torch.empty((world,) + tuple(keys.shape), dtype=keys.dtype, device=keys.device)
+    all_est = torch.empty((world,) + tuple(est.shape), dtype=est.dtype, device=est.device)
+    dist.all_gather_into_tensor(all_keys, keys.contiguous(), group=group)
+    dist.all_gather_into_tensor(all_est, est.contiguous(), group=group)
+    allreduce_kv_counters(counters, totals, group)
+    torch.cuda.current_stream(device).synchronize()
+    kv.merge_candidates(all_keys, all_est, world)
+    torch.cuda.synchronize(device)
+
+
 def allreduce_stats(stats: dict, device="cpu", group=None) -> dict:
     """Job-wide zk_stats: every counter is a sum over ranks."""
     import torch
