@@ -15,6 +15,17 @@
 #ifndef ZK_K2_WG
 #define ZK_K2_WG 1024  // K2 workgroup: 8192-link chunks (512 threads: 0.236 -> 0.199 ms on C2)
 #endif
+#ifndef ZK_K3_GUARD
+#define ZK_K3_GUARD 1  // K3: skip zero chunk updates
+#endif
+#ifndef ZK_K3_PACK
+#define ZK_K3_PACK 1   // K3: m0 and S1 of a short link in one packed LDS add
+#endif
+// GUARD + PACK, same box, interleaved, serial steps (profiles/r02/ab_k3pack_serial.txt): K2 + K3
+// 0.454 -> 0.405 ms, step 1.815 -> 1.766 ms
+#ifndef ZK_K3_U
+#define ZK_K3_U 4      // links per thread per K3 iteration
+#endif
 
 namespace zk {
 namespace {
@@ -397,15 +408,19 @@ __global__ __launch_bounds__(1 << CB_SHIFT) void k_bucket_reduce(ReduceArgs r, u
 template <int CB_SHIFT, int WG, int U>
 __global__ __launch_bounds__(WG) void k_bucket_lds_reduce(ReduceArgs r, uint32_t splits) {
     constexpr int CB = 1 << CB_SHIFT;
-    __shared__ unsigned long long s_t[15 * CB];
+    constexpr int ROWS = ZK_K3_PACK ? 16 : 15;
+    __shared__ unsigned long long s_t[ROWS * CB];
     const int tid = threadIdx.x;
     const uint32_t b = blockIdx.x / splits, part = blockIdx.x % splits;
-    for (int x = tid; x < 15 * CB; x += WG) s_t[x] = 0ull;
+    for (int x = tid; x < ROWS * CB; x += WG) s_t[x] = 0ull;
     const uint64_t lo = r.bucket_base[b], hi = r.bucket_base[b + 1];
     const uint64_t per = (hi - lo + splits - 1) / splits;
     const uint64_t s0 = lo + per * part;
     const uint64_t s1 = (s0 + per < hi) ? s0 + per : hi;
     const uint64_t cell0 = (uint64_t)b << CB_SHIFT;
+    // packed row (ZK_K3_PACK): a link with d < 2^21 adds 2^42 + d to row 15 instead of 1 to m0 and d
+    // to S1; with < 2^20 links in the part the row holds m0 in bits 42.. and S1 below (< 2^41)
+    const bool packable = ZK_K3_PACK && (s1 - s0) < (1ull << 20);
     __syncthreads();
     constexpr uint64_t M = 0xFFFFFFFFull;
     for (uint64_t base = s0; base < s1; base += (uint64_t)WG * U) {
@@ -421,23 +436,41 @@ __global__ __launch_bounds__(WG) void k_bucket_lds_reduce(ReduceArgs r, uint32_t
             const uint32_t c = (uint32_t)((v[k] >> 40) - cell0);
             const uint64_t d = v[k] & (kMaxDuration - 1);
             unsigned long long* t = s_t + c;
-            atomicAdd(&t[kLimbM0 * CB], 1ull);
             if ((d >> 32) == 0) {
                 const uint64_t d2 = d * d;                                   // < 2^64
                 const unsigned __int128 d3 = (unsigned __int128)d2 * d;       // < 2^96
                 const unsigned __int128 d4 = (unsigned __int128)d2 * d2;      // < 2^128
                 const uint64_t d3lo = (uint64_t)d3, d4lo = (uint64_t)d4, d4hi = (uint64_t)(d4 >> 64);
-                atomicAdd(&t[kLimbS1 * CB], (unsigned long long)d);
-                atomicAdd(&t[(kLimbS2 + 0) * CB], (unsigned long long)(d2 & M));
-                atomicAdd(&t[(kLimbS2 + 1) * CB], (unsigned long long)(d2 >> 32));
-                atomicAdd(&t[(kLimbS3 + 0) * CB], (unsigned long long)(d3lo & M));
-                atomicAdd(&t[(kLimbS3 + 1) * CB], (unsigned long long)(d3lo >> 32));
-                atomicAdd(&t[(kLimbS3 + 2) * CB], (unsigned long long)(uint64_t)(d3 >> 64));
-                atomicAdd(&t[(kLimbS4 + 0) * CB], (unsigned long long)(d4lo & M));
-                atomicAdd(&t[(kLimbS4 + 1) * CB], (unsigned long long)(d4lo >> 32));
-                atomicAdd(&t[(kLimbS4 + 2) * CB], (unsigned long long)(d4hi & M));
-                atomicAdd(&t[(kLimbS4 + 3) * CB], (unsigned long long)(d4hi >> 32));
+#if ZK_K3_GUARD
+                // the high chunks are zero for short durations (d < 2^16: d^2 >> 32, d^4 >> 64; d <
+                // 2^21: d^3 >> 64, d^4 >> 96): masked lanes skip the LDS update, an all-zero wave
+                // skips the instruction
+#define ZK_K3_ADD(q, x)                                             \
+    do {                                                            \
+        const uint64_t x_ = (x);                                    \
+        if (x_) atomicAdd(&t[(q) * CB], (unsigned long long)x_);    \
+    } while (0)
+#else
+#define ZK_K3_ADD(q, x) atomicAdd(&t[(q) * CB], (unsigned long long)(x))
+#endif
+                if (packable && d < (1ull << 21)) {
+                    atomicAdd(&t[15 * CB], (1ull << 42) | d);
+                } else {
+                    atomicAdd(&t[kLimbM0 * CB], 1ull);
+                    ZK_K3_ADD(kLimbS1, d);
+                }
+                ZK_K3_ADD(kLimbS2 + 0, d2 & M);
+                ZK_K3_ADD(kLimbS2 + 1, d2 >> 32);
+                ZK_K3_ADD(kLimbS3 + 0, d3lo & M);
+                ZK_K3_ADD(kLimbS3 + 1, d3lo >> 32);
+                ZK_K3_ADD(kLimbS3 + 2, (uint64_t)(d3 >> 64));
+                ZK_K3_ADD(kLimbS4 + 0, d4lo & M);
+                ZK_K3_ADD(kLimbS4 + 1, d4lo >> 32);
+                ZK_K3_ADD(kLimbS4 + 2, d4hi & M);
+                ZK_K3_ADD(kLimbS4 + 3, d4hi >> 32);
+#undef ZK_K3_ADD
             } else {
+                atomicAdd(&t[kLimbM0 * CB], 1ull);
 #pragma unroll
                 for (int q = 1; q < 15; ++q) {
                     const uint64_t x = limb_value(q, d);
@@ -451,9 +484,13 @@ __global__ __launch_bounds__(WG) void k_bucket_lds_reduce(ReduceArgs r, uint32_t
         const uint64_t cell = cell0 + c;
         if (cell >= r.cells) continue;
         uint64_t* dst = r.table + cell * kLimbs;
+        uint64_t x15 = 0;
+        if constexpr (ZK_K3_PACK) x15 = s_t[15 * CB + c];
 #pragma unroll
         for (int q = 0; q < 15; ++q) {
-            const uint64_t x = s_t[q * CB + c];
+            uint64_t x = s_t[q * CB + c];
+            if (q == kLimbM0) x += x15 >> 42;
+            if (q == kLimbS1) x += x15 & ((1ull << 42) - 1);  // S1's low limb may exceed 32 bits: value-exact
             if (!x) continue;
             if (splits == 1)
                 dst[q] += x;  // this workgroup owns the cell
@@ -499,11 +536,11 @@ hipError_t launch_partitioned_reduce(const ReduceArgs& r, hipStream_t s) {
     const uint32_t splits = r.nb >= 256 ? 1u : (512u + r.nb - 1) / r.nb;
 #if ZK_K3_LDS
     if (r.cb_shift == 8) {
-        hipLaunchKernelGGL((k_bucket_lds_reduce<8, 256, 4>), dim3(r.nb * splits), dim3(256), 0, s, r, splits);
+        hipLaunchKernelGGL((k_bucket_lds_reduce<8, 256, ZK_K3_U>), dim3(r.nb * splits), dim3(256), 0, s, r, splits);
         return hipGetLastError();
     }
     if (r.cb_shift == 9) {
-        hipLaunchKernelGGL((k_bucket_lds_reduce<9, 512, 4>), dim3(r.nb * splits), dim3(512), 0, s, r, splits);
+        hipLaunchKernelGGL((k_bucket_lds_reduce<9, 512, ZK_K3_U>), dim3(r.nb * splits), dim3(512), 0, s, r, splits);
         return hipGetLastError();
     }
 #endif
