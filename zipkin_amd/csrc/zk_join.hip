@@ -298,6 +298,36 @@ __device__ __forceinline__ void load_window(const JoinArgs& a, uint64_t ws, Wind
     w.prev = a.c.trace_id[(i > 0 && i - 1 < n) ? i - 1 : 0];
 }
 
+// ZK_K1_LATE (default): only the traceIds (what the boundary phase needs) are prefetched a window
+// ahead; the other five columns of a window are loaded at the top of its own iteration and arrive
+// during the boundary phases (26 -> 6 registers of prefetch, 120 -> 100 VGPRs). Same box,
+// interleaved, serial steps (profiles/r02/ab_late.txt): K1 1.251 -> 1.227 ms; with the freed
+// registers spent on a fifth workgroup per CU (hash factor 4 to fit the LDS): 1.233 ms.
+#ifndef ZK_K1_LATE
+#define ZK_K1_LATE 1
+#endif
+__device__ __forceinline__ void load_tid(const JoinArgs& a, uint64_t ws, Window& w) {
+    const uint64_t n = a.c.n;
+    const uint64_t i = ws + 2 * threadIdx.x;
+    ld2_u64(a.c.trace_id, i, n, w.tid);
+    w.prev = a.c.trace_id[(i > 0 && i - 1 < n) ? i - 1 : 0];
+}
+template <bool JOIN>
+__device__ __forceinline__ void load_rest(const JoinArgs& a, uint64_t ws, Window& w) {
+    const uint64_t n = a.c.n;
+    const uint64_t i = ws + 2 * threadIdx.x;
+    ld2_u64(a.c.span_id, i, n, w.sid);
+    if constexpr (JOIN) {
+        ld2_u64(a.c.parent_id, i, n, w.pid);
+    } else {
+        w.pid[0] = w.pid[1] = 0ull;
+    }
+    ld2_u64((const uint64_t*)a.c.first_ts, i, n, w.first);
+    ld2_u64((const uint64_t*)a.c.last_ts, i, n, w.last);
+    ld2_u32(a.c.service_id, i, n, w.svc);
+    ld2_u32(a.c.flags, i, n, w.flags);
+}
+
 // =============================================================================================
 // K1: persistent streaming span_join
 //
@@ -384,11 +414,18 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     uint64_t seek = R0;       // first record that may start one of our traces
     Window cur, nxt;
     constexpr bool JOIN = (MODE & kModeJoin) != 0, EMIT = (MODE & kModeEmit) != 0;
+#if ZK_K1_LATE
+    load_tid(a, ws, cur);
+#else
     load_window<JOIN>(a, ws, cur);
+#endif
 #pragma unroll
     for (int x = tid; x < H / 4; x += WG) reinterpret_cast<uint4*>(s_ht)[x] = make_uint4(0u, 0u, 0u, 0u);
     ZK_STAMP_DECL
     for (;;) {
+#if ZK_K1_LATE
+        load_rest<JOIN>(a, ws, cur);
+#endif
         const int wn = (int)((n - ws) < (uint64_t)TILE ? (n - ws) : (uint64_t)TILE);
         // ---- 1. trace boundaries of the window -------------------------------------------------
         uint64_t m_ev, m_od;  // this wave's boundary ballots (uniform; phase 3 reuses them)
@@ -488,7 +525,11 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         }
         if (!done && next_seek >= R1) done = true;
         const uint64_t next_ws = next_seek & ~1ull;
+#if ZK_K1_LATE
+        load_tid(a, done ? ws : next_ws, nxt);
+#else
         load_window<JOIN>(a, done ? ws : next_ws, nxt);  // in flight during the LDS phases below (unconditional: see ld2)
+#endif
         ZK_STAMP(1);
         nrec += (uint64_t)(m - start);
         if constexpr (ABL != 2) {  // diagnostic build: 2 = stream windows only
@@ -813,7 +854,13 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         if (done) break;
         ws = next_ws;
         seek = next_seek;
+#if ZK_K1_LATE
+        cur.tid[0] = nxt.tid[0];
+        cur.tid[1] = nxt.tid[1];
+        cur.prev = nxt.prev;
+#else
         cur = nxt;
+#endif
         // no loop-end barrier: the next window's phase-1 barrier already separates this window's
         // last LDS reads (phase 6-7) from its writes (phase 3 on), and phase 1's s_mask writes
         // from this window's reads (phases 2-3, before the barrier that ends phase 3)
