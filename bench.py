@@ -50,6 +50,12 @@ def parse():
                     help="batches in flight behind the one being joined: 1 (default) = two table/stream "
                          "sets (batch k's join overlaps batch k-1's tail), 2 = three, 0 = one set, serial steps "
                          "(c2 takes any depth, c4/c5 use two sets when > 0)")
+    ap.add_argument("--overlap", default="full", choices=("tail", "full"),
+                    help="c2 pipelined steps: full (default) = no ordering between the table sets: batch k's "
+                         "join shares the GPU with batch k-1's K2/K3 (faster steps; K1's launch events then also "
+                         "cover the K2/K3 work it shares the chip with, see roofline.isolated_*); tail = batch k's "
+                         "join starts once batch k-1's reduce is done, so only spill, [all-reduce,] finalize, "
+                         "status check and reset overlap the next join and every K1 launch runs alone")
     ap.add_argument("--workload", default="c2", choices=("c1", "c2", "c4", "c5", "ingest"),
                     help="c2 (default, the headline): dependency path; c1: the reference's CPU config "
                          "(10k tracegen traces, 20 services) on the GPU and the CPU baseline; "
@@ -164,7 +170,13 @@ def main():
             state["k"] += 1
             torch.cuda.set_stream(s)
             c.reset()
+            if a.overlap == "tail" and state.get("reduced") is not None:
+                s.wait_event(state["reduced"])  # K1 after the previous batch's K2/K3
             c.accumulate(cols, clustered=True, verify=a.verify)
+            if a.overlap == "tail":
+                ev = torch.cuda.Event()
+                ev.record(s)
+                state["reduced"] = ev
             if dist is not None:
                 c.partial()
                 allreduce_table(t)  # ordered on s; the host does not wait for it
@@ -180,16 +192,18 @@ def main():
 
     # warmup: serial steps first (their K1 launches give the isolated K1 duration), then two
     # pipelined steps so that the second set's buffers exist before the timed region
+    # (at least ISOLATED + 1 serial steps: untimed, outside the timed region, so that the isolated K1
+    # figure averages several warm launches whatever --warmup is)
+    ISOLATED = 4
     tmf = None
-    for i in range(a.warmup):
+    for i in range(max(a.warmup, ISOLATED + 1)):
         step_serial()
         if i == 0:  # the first launch is cold: the isolated figure averages the later ones
             tmf = dict(ctx.timing())
     torch.cuda.synchronize()
     tmw = ctx.timing()
-    k1_isolated_ms = None
-    if a.warmup >= 2:
-        k1_isolated_ms = (tmw["join_ms_total"] - tmf["join_ms_total"]) / (tmw["join_calls"] - tmf["join_calls"])
+    k1_isolated_ms = (tmw["join_ms_total"] - tmf["join_ms_total"]) / (tmw["join_calls"] - tmf["join_calls"])
+    isolated_launches = tmw["join_calls"] - tmf["join_calls"]
     if pipeline:
         for _ in range(len(sets)):
             step()
@@ -274,8 +288,10 @@ def main():
                 "max_depth": a.max_depth,
                 "parallelism": f"traceId-hash shards x{world}" + (", RCCL all-reduce of the link table" if world > 1 else ""),
                 "step": "reset + span_join + spill + [all-reduce] + finalize(m0..m4) + status check"
-                        + (f" ({a.pipeline + 1} table sets: batch k's join overlaps earlier batches' reduce, [all-reduce,] finalize)"
-                           if pipeline else ""),
+                        + ((f" ({a.pipeline + 1} table sets: batch k's join follows batch k-1's reduce and overlaps "
+                            "its [all-reduce,] finalize, status check and reset)") if pipeline and a.overlap == "tail" else
+                           (f" ({a.pipeline + 1} table sets: batch k's join overlaps earlier batches' reduce, [all-reduce,] "
+                            "finalize)") if pipeline else ""),
             },
             "roofline": {
                 "bound": "hbm",
@@ -293,6 +309,9 @@ def main():
                 "isolated_avg_launch_ms": k1_isolated_ms,
                 "isolated_frac": (n * BYTES_PER_RECORD / (k1_isolated_ms * 1e-3) / 1e9 / PEAK_HBM_GBS
                                   if k1_isolated_ms else None),
+                "isolated_launches": isolated_launches,
+                # the whole step's algorithmic bytes (K1's input) over the step time
+                "step_frac": n * BYTES_PER_RECORD / (elapsed / a.steps) / 1e9 / PEAK_HBM_GBS,
             },
             "cpu_baseline": cpu,
             "parity": parity,

@@ -1177,7 +1177,15 @@ extern "C" int zk_debug_stamps(unsigned long long* out, int reset) {
 
 void join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, uint64_t* link_stride) {
     const uint64_t windows = (n + kTile - 1) / kTile;
-    uint64_t g = (uint64_t)cus * ZK_K1_WGS_PER_CU;  // all resident at once (<= 128 VGPRs, <= 40 KB LDS)
+#ifndef ZK_K1_GRID_MULT
+// workgroups per resident slot (1: persistent, every workgroup resident at once). 4: a quarter of
+// the range per workgroup, so the last workgroups' imbalance is smaller and a K1 launch shares the
+// chip gracefully with the other table set's K2/K3 (same box, interleaved, profiles/r02/
+// ab_grid_mult_overlap.txt: serial K1 1.226 -> 1.187 ms, two-set step with full overlap 1.63-1.68 ->
+// 1.56-1.57 ms; 8: slower). K2 walks 4 lists per workgroup, so its grid stays 1024.
+#define ZK_K1_GRID_MULT 4
+#endif
+    uint64_t g = (uint64_t)cus * ZK_K1_WGS_PER_CU * ZK_K1_GRID_MULT;  // <= 128 VGPRs, <= 40 KB LDS per WG
     if (g > windows) g = windows ? windows : 1;
     const uint64_t per = ((n + g - 1) / g + kTile - 1) / kTile * kTile;
     *grid = (uint32_t)g;

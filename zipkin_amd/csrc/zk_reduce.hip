@@ -110,9 +110,14 @@ __global__ __launch_bounds__(1024) void k_bucket_base(uint64_t* __restrict__ bas
 // store instruction, at ~2.3x write amplification in WRITE_SIZE).
 constexpr int kScatterLine = 8;  // links per 64-byte line (128-byte lines: WRITE_SIZE 571 -> 396 MB, but
                                  // their LDS carry halves the resident workgroups: 1.4x slower)
+// One workgroup walks LPW consecutive K1 lists as one stream: within every bucket, list w+1's range
+// follows list w's (col_off is an exclusive scan over lists), so the per-bucket cursors and line
+// carries run on across the list boundaries and K2's grid stays ~1024 workgroups whatever K1's grid.
+constexpr int kScatterMaxLPW = 8;
 template <int U, int WG>
-__global__ __launch_bounds__(WG) void k_link_scatter(ReduceArgs r) {
+__global__ __launch_bounds__(WG) void k_link_scatter(ReduceArgs r, uint32_t lpw) {
     constexpr int C = WG * U;
+    __shared__ uint32_t s_pre[kScatterMaxLPW + 1];  // exclusive prefix of the group's list counts
     __shared__ uint32_t s_cur[kMaxBuckets];   // output position of each bucket's first pending link
     __shared__ uint32_t s_hist[kMaxBuckets];  // links of the chunk per bucket
     __shared__ uint32_t s_off[kMaxBuckets];   // exclusive offsets in the sorted chunk
@@ -120,7 +125,8 @@ __global__ __launch_bounds__(WG) void k_link_scatter(ReduceArgs r) {
     __shared__ uint64_t s_sorted[C];
     __shared__ uint32_t s_tmp[32];
     extern __shared__ __attribute__((aligned(16))) uint64_t s_carry[];  // [nb][kScatterLine]
-    const uint32_t w = blockIdx.x;
+    const uint32_t w = blockIdx.x * lpw;  // first list of the group
+    const uint32_t nl = (r.lists - w) < lpw ? (r.lists - w) : lpw;
     const int tid = threadIdx.x;
     constexpr int BPT = (kMaxBuckets + WG - 1) / WG;  // buckets per thread in the scan
     for (uint32_t b = tid; b < r.nb; b += WG) {
@@ -128,15 +134,33 @@ __global__ __launch_bounds__(WG) void k_link_scatter(ReduceArgs r) {
         s_hist[b] = 0u;
         s_cc[b] = 0u;
     }
-    const uint32_t c = r.counts[w];
-    const uint64_t* __restrict__ L = r.links + (uint64_t)w * r.stride;
+    if (tid == 0) {
+        uint32_t acc = 0;
+        for (uint32_t q = 0; q < nl; ++q) {
+            s_pre[q] = acc;
+            acc += r.counts[w + q];
+        }
+        s_pre[nl] = acc;
+    }
+    __syncthreads();
+    const uint32_t c = s_pre[nl];  // links of the group
+    uint32_t pre[kScatterMaxLPW + 1];
+#pragma unroll
+    for (int q = 0; q <= kScatterMaxLPW; ++q) pre[q] = q <= (int)nl ? s_pre[q] : 0xFFFFFFFFu;
+    // element i of the group's stream (i < c): list q with pre[q] <= i < pre[q + 1]
+    auto at = [&](uint32_t i) -> const uint64_t* {
+        uint32_t q = 0;
+#pragma unroll
+        for (int k = 1; k < kScatterMaxLPW; ++k) q += (i >= pre[k]) ? 1u : 0u;
+        q = q < nl - 1 ? q : nl - 1;  // an empty group (c == 0) reads element 0 of its last list
+        return r.links + (uint64_t)(w + q) * r.stride + (i - pre[q]);
+    };
     uint64_t nxt[U];
 #pragma unroll
     for (int k = 0; k < U; ++k) {
         const uint32_t i = tid + WG * k;
-        nxt[k] = L[i < c ? i : 0];
+        nxt[k] = *at(i < c ? i : 0);
     }
-    __syncthreads();
     for (uint32_t base = 0; base < c; base += C) {
         const uint32_t cnt = (c - base) < (uint32_t)C ? (c - base) : (uint32_t)C;
         const bool last = base + C >= c;
@@ -146,7 +170,7 @@ __global__ __launch_bounds__(WG) void k_link_scatter(ReduceArgs r) {
         for (int k = 0; k < U; ++k) {
             v[k] = nxt[k];
             const uint32_t i = base + C + tid + WG * k;
-            nxt[k] = L[i < c ? i : 0];  // next chunk in flight
+            nxt[k] = *at(i < c ? i : 0);  // next chunk in flight
         }
 #pragma unroll
         for (int k = 0; k < U; ++k) {
@@ -532,7 +556,12 @@ hipError_t launch_partitioned_reduce(const ReduceArgs& r, hipStream_t s) {
     if (!r.nb || !r.lists) return hipSuccess;
     hipLaunchKernelGGL(k_bucket_colscan, dim3(r.nb), dim3(1024), 0, s, r.hist, r.lists, r.col_off, r.bucket_base);
     hipLaunchKernelGGL(k_bucket_base, dim3(1), dim3(1024), 0, s, r.bucket_base, r.nb);
-    hipLaunchKernelGGL((k_link_scatter<ZK_K2_U, ZK_K2_WG>), dim3(r.lists), dim3(ZK_K2_WG), (size_t)r.nb * kScatterLine * 8, s, r);
+    // ~1024 K2 workgroups: a K1 grid larger than that is walked LPW lists per workgroup
+    uint32_t lpw = (r.lists + 1023) / 1024;
+    if (lpw > (uint32_t)kScatterMaxLPW) lpw = kScatterMaxLPW;
+    const uint32_t k2_grid = (r.lists + lpw - 1) / lpw;
+    hipLaunchKernelGGL((k_link_scatter<ZK_K2_U, ZK_K2_WG>), dim3(k2_grid), dim3(ZK_K2_WG), (size_t)r.nb * kScatterLine * 8, s, r,
+                       lpw);
     const uint32_t splits = r.nb >= 256 ? 1u : (512u + r.nb - 1) / r.nb;
 #if ZK_K3_LDS
     if (r.cb_shift == 8) {
