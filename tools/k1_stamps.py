@@ -21,8 +21,8 @@ import torch  # noqa: E402
 from zipkin_amd import DepsContext, DeviceColumns, tracegen_params  # noqa: E402
 from zipkin_amd import _abi  # noqa: E402
 
-PHASES = ["boundaries+sync", "scan+issue loads", "stage+clear+sync", "hash insert+sync", "merge+sync",
-          "validate/join/emit", "prefix+write links", "loop-end sync"]
+PHASES = ["boundaries", "scan+issue loads", "stage", "hash insert", "merge", "validate/join/emit",
+          "prefix+write links", "loop end", "barrier waits"]
 
 
 def main():
@@ -38,16 +38,16 @@ def main():
     buf = (C.c_ulonglong * 16)()
     for it in range(3):
         ctx.reset()
-        ctx.accumulate(cols)
+        ctx.accumulate(cols, clustered=True, verify=False)
         ctx.sync()
         if it == 0:
             dbg(buf, 1)  # warm-up: discard
     dbg(buf, 1)
     tm = ctx.timing()
-    tot = sum(buf[i] for i in range(8))
+    tot = sum(buf[i] for i in range(9))
     out = {"records": nrec, "join_ms_last": tm["join_ms"],
-           "shares": {PHASES[i]: round(buf[i] / tot, 4) for i in range(8)},
-           "raw": [int(buf[i]) for i in range(8)]}
+           "shares": {PHASES[i]: round(buf[i] / tot, 4) for i in range(9)},
+           "raw": [int(buf[i]) for i in range(9)]}
     print(json.dumps(out, indent=1))
 
 

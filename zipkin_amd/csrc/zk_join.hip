@@ -50,7 +50,7 @@ __device__ __forceinline__ unsigned long long zk_memtime() {
 }
 #define ZK_STAMP_DECL                                 \
     unsigned long long zk_t_prev = zk_memtime();      \
-    unsigned long long zk_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long zk_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 #define ZK_STAMP(k)                                   \
     do {                                              \
         const unsigned long long zk_t = zk_memtime(); \
@@ -60,13 +60,20 @@ __device__ __forceinline__ unsigned long long zk_memtime() {
 #define ZK_STAMP_FLUSH()                                                              \
     do {                                                                              \
         if ((threadIdx.x & 63) == 0)                                                  \
-            for (int q = 0; q < 8; ++q) atomicAdd(&g_zk_stamps[q], zk_acc[q]);        \
+            for (int q = 0; q < 9; ++q) atomicAdd(&g_zk_stamps[q], zk_acc[q]);        \
     } while (0)
 #else
 #define ZK_STAMP_DECL
 #define ZK_STAMP(k)
 #define ZK_STAMP_FLUSH()
 #endif
+// a workgroup barrier that ends phase k: the stamps build books the wait itself to slot 8
+#define ZK_PHASE_SYNC(k) \
+    do {                 \
+        ZK_STAMP(k);     \
+        __syncthreads(); \
+        ZK_STAMP(8);     \
+    } while (0)
 
 __device__ __forceinline__ uint32_t slot_hash(uint64_t sid, uint32_t seg) {
     uint64_t x = sid ^ ((uint64_t)(seg + 1) * 0x9E3779B97F4A7C15ull);
@@ -203,13 +210,19 @@ __device__ __forceinline__ bool slot_valid(uint32_t w) { return ((w >> kSlotB) &
 // which serialises the column loads and defeats the prefetch. Index i < lim reads the aligned pair
 // at i (columns are 16-B / 8-B aligned, so the pair never crosses a page even when i + 1 == lim);
 // i >= lim reads pair 0.
+// ZK_K1_HOTREAD (diagnostic builds only, results wrong): every column load is redirected into the
+// first 2^16 records, which stay in L2 -- K1's time without HBM, to split compute from streaming
+#ifndef ZK_K1_HOTREAD
+#define ZK_K1_HOTREAD 0
+#endif
+__device__ __forceinline__ uint64_t hot_index(uint64_t i) { return ZK_K1_HOTREAD ? (i & 0xFFFEull) : i; }
 __device__ __forceinline__ void ld2_u64(const uint64_t* __restrict__ p, uint64_t i, uint64_t lim, uint64_t v[2]) {
-    const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(p + (i < lim ? i : 0));
+    const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(p + hot_index(i < lim ? i : 0));
     v[0] = x.x;
     v[1] = x.y;
 }
 __device__ __forceinline__ void ld2_u32(const uint32_t* __restrict__ p, uint64_t i, uint64_t lim, uint32_t v[2]) {
-    const uint2 x = *reinterpret_cast<const uint2*>(p + (i < lim ? i : 0));
+    const uint2 x = *reinterpret_cast<const uint2*>(p + hot_index(i < lim ? i : 0));
     v[0] = x.x;
     v[1] = x.y;
 }
@@ -310,7 +323,7 @@ __device__ __forceinline__ void load_tid(const JoinArgs& a, uint64_t ws, Window&
     const uint64_t n = a.c.n;
     const uint64_t i = ws + 2 * threadIdx.x;
     ld2_u64(a.c.trace_id, i, n, w.tid);
-    w.prev = a.c.trace_id[(i > 0 && i - 1 < n) ? i - 1 : 0];
+    w.prev = a.c.trace_id[hot_index((i > 0 && i - 1 < n) ? i - 1 : 0)];
 }
 template <bool JOIN>
 __device__ __forceinline__ void load_rest(const JoinArgs& a, uint64_t ws, Window& w) {
@@ -438,8 +451,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             m_od = __ballot(b1);
             if (lane == 0) *reinterpret_cast<ulonglong2*>(&s_mask[2 * wave]) = make_ulonglong2(m_ev, m_od);
         }
-        __syncthreads();
-        ZK_STAMP(0);
+        ZK_PHASE_SYNC(0);
         // ---- 2. which records are ours, where the next window starts (uniform) ----------------
         const int lo_j = (int)(seek - ws);
         const int r1_j = (R1 - ws < (uint64_t)wn) ? (int)(R1 - ws) : wn;
@@ -582,8 +594,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             }
 #endif
         }
-        __syncthreads();  // (the hash table is empty here: cleared once, then by its leaders)
-        ZK_STAMP(2);
+        ZK_PHASE_SYNC(2);  // (the hash table is empty here: cleared once, then by its leaders)
 
         // ---- 4. groupBy((id, traceId)): the first fragment to claim a slot leads --------------
         // Both records of the thread probe together (one LDS round trip per step for the pair).
@@ -681,8 +692,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 if (promote) atomicOr(wp, promote << kSlotB);
             }
         }
-        __syncthreads();
-        ZK_STAMP(4);
+        ZK_PHASE_SYNC(4);
 
         // ---- 6. filter(isValid), join on (parentId, traceId), (cell, duration) links ----------
         uint64_t r_link[2], r_item[2];
@@ -801,7 +811,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         const uint32_t below = (lanes_below(l1) + lanes_below(l2)) | ((lanes_below(i1) + lanes_below(i2)) << 16);
         if (lane == 0)
             s_wsum[wave] = (uint32_t)(__popcll(l1) + __popcll(l2)) | ((uint32_t)(__popcll(i1) + __popcll(i2)) << 16);
-        __syncthreads();
+        ZK_PHASE_SYNC(6);
         uint32_t base = 0, total = 0;
 #pragma unroll
         for (int w2 = 0; w2 < WG / 64; ++w2) {

@@ -26,6 +26,9 @@
 #ifndef ZK_K3_U
 #define ZK_K3_U 4      // links per thread per K3 iteration
 #endif
+#ifndef ZK_K3_PREFETCH
+#define ZK_K3_PREFETCH 1  // K3: load the next iteration's links before this one's atomics
+#endif
 
 namespace zk {
 namespace {
@@ -433,10 +436,13 @@ template <int CB_SHIFT, int WG, int U>
 __global__ __launch_bounds__(WG) void k_bucket_lds_reduce(ReduceArgs r, uint32_t splits) {
     constexpr int CB = 1 << CB_SHIFT;
     constexpr int ROWS = ZK_K3_PACK ? 16 : 15;
-    __shared__ unsigned long long s_t[ROWS * CB];
+    // row stride CB + 1: the 16 limbs of one cell fall in distinct banks, so the flush below can read
+    // a cell's limbs with 16 adjacent lanes and write the 128-byte cell whole
+    constexpr int RS = CB + 1;
+    __shared__ unsigned long long s_t[ROWS * RS];
     const int tid = threadIdx.x;
     const uint32_t b = blockIdx.x / splits, part = blockIdx.x % splits;
-    for (int x = tid; x < ROWS * CB; x += WG) s_t[x] = 0ull;
+    for (int x = tid; x < ROWS * RS; x += WG) s_t[x] = 0ull;
     const uint64_t lo = r.bucket_base[b], hi = r.bucket_base[b + 1];
     const uint64_t per = (hi - lo + splits - 1) / splits;
     const uint64_t s0 = lo + per * part;
@@ -445,15 +451,34 @@ __global__ __launch_bounds__(WG) void k_bucket_lds_reduce(ReduceArgs r, uint32_t
     // packed row (ZK_K3_PACK): a link with d < 2^21 adds 2^42 + d to row 15 instead of 1 to m0 and d
     // to S1; with < 2^20 links in the part the row holds m0 in bits 42.. and S1 below (< 2^41)
     const bool packable = ZK_K3_PACK && (s1 - s0) < (1ull << 20);
-    __syncthreads();
     constexpr uint64_t M = 0xFFFFFFFFull;
+#if ZK_K3_PREFETCH
+    // the next iteration's links are in flight while this one's LDS atomics run (one K3 wave of
+    // ~2 workgroups per CU cannot hide an HBM round trip per iteration otherwise)
+    uint64_t nxt[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        const uint64_t i = s0 + tid + (uint64_t)k * WG;
+        nxt[k] = i < s1 ? r.sorted[i] : ~0ull;
+    }
+#endif
+    __syncthreads();
     for (uint64_t base = s0; base < s1; base += (uint64_t)WG * U) {
         uint64_t v[U];
+#if ZK_K3_PREFETCH
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            v[k] = nxt[k];
+            const uint64_t i = base + (uint64_t)WG * U + tid + (uint64_t)k * WG;
+            nxt[k] = i < s1 ? r.sorted[i] : ~0ull;
+        }
+#else
 #pragma unroll
         for (int k = 0; k < U; ++k) {
             const uint64_t i = base + tid + (uint64_t)k * WG;
             v[k] = i < s1 ? r.sorted[i] : ~0ull;
         }
+#endif
 #pragma unroll
         for (int k = 0; k < U; ++k) {
             if (v[k] == ~0ull) continue;
@@ -472,15 +497,15 @@ __global__ __launch_bounds__(WG) void k_bucket_lds_reduce(ReduceArgs r, uint32_t
 #define ZK_K3_ADD(q, x)                                             \
     do {                                                            \
         const uint64_t x_ = (x);                                    \
-        if (x_) atomicAdd(&t[(q) * CB], (unsigned long long)x_);    \
+        if (x_) atomicAdd(&t[(q) * RS], (unsigned long long)x_);    \
     } while (0)
 #else
-#define ZK_K3_ADD(q, x) atomicAdd(&t[(q) * CB], (unsigned long long)(x))
+#define ZK_K3_ADD(q, x) atomicAdd(&t[(q) * RS], (unsigned long long)(x))
 #endif
                 if (packable && d < (1ull << 21)) {
-                    atomicAdd(&t[15 * CB], (1ull << 42) | d);
+                    atomicAdd(&t[15 * RS], (1ull << 42) | d);
                 } else {
-                    atomicAdd(&t[kLimbM0 * CB], 1ull);
+                    atomicAdd(&t[kLimbM0 * RS], 1ull);
                     ZK_K3_ADD(kLimbS1, d);
                 }
                 ZK_K3_ADD(kLimbS2 + 0, d2 & M);
@@ -494,33 +519,35 @@ __global__ __launch_bounds__(WG) void k_bucket_lds_reduce(ReduceArgs r, uint32_t
                 ZK_K3_ADD(kLimbS4 + 3, d4hi >> 32);
 #undef ZK_K3_ADD
             } else {
-                atomicAdd(&t[kLimbM0 * CB], 1ull);
+                atomicAdd(&t[kLimbM0 * RS], 1ull);
 #pragma unroll
                 for (int q = 1; q < 15; ++q) {
                     const uint64_t x = limb_value(q, d);
-                    if (x) atomicAdd(&t[q * CB], (unsigned long long)x);
+                    if (x) atomicAdd(&t[q * RS], (unsigned long long)x);
                 }
             }
         }
     }
     __syncthreads();
-    for (int c = tid; c < CB; c += WG) {
+    // flush: lane group of 16 = one cell, lane q = limb q, so a wave reads and writes 4 whole 128-byte
+    // cells (one thread per cell wrote 64 lines 8 bytes at a time: 3.6x WRITE_SIZE over the table)
+    static_assert(kLimbs == 16, "a cell is 16 limbs");
+    for (int x = tid; x < CB * kLimbs; x += WG) {
+        const int c = x >> 4, q = x & 15;
         const uint64_t cell = cell0 + c;
-        if (cell >= r.cells) continue;
-        uint64_t* dst = r.table + cell * kLimbs;
-        uint64_t x15 = 0;
-        if constexpr (ZK_K3_PACK) x15 = s_t[15 * CB + c];
-#pragma unroll
-        for (int q = 0; q < 15; ++q) {
-            uint64_t x = s_t[q * CB + c];
-            if (q == kLimbM0) x += x15 >> 42;
-            if (q == kLimbS1) x += x15 & ((1ull << 42) - 1);  // S1's low limb may exceed 32 bits: value-exact
-            if (!x) continue;
-            if (splits == 1)
-                dst[q] += x;  // this workgroup owns the cell
-            else
-                atomicAdd((unsigned long long*)&dst[q], (unsigned long long)x);
+        if (cell >= r.cells || q == 15) continue;
+        uint64_t v = s_t[q * RS + c];
+        if constexpr (ZK_K3_PACK) {
+            const uint64_t x15 = (q <= kLimbS1) ? s_t[15 * RS + c] : 0ull;
+            if (q == kLimbM0) v += x15 >> 42;
+            if (q == kLimbS1) v += x15 & ((1ull << 42) - 1);  // S1's low limb may exceed 32 bits: value-exact
         }
+        if (!v) continue;
+        uint64_t* dst = r.table + cell * kLimbs + q;
+        if (splits == 1)
+            *dst += v;  // this workgroup owns the cell
+        else
+            atomicAdd((unsigned long long*)dst, (unsigned long long)v);
     }
 }
 
