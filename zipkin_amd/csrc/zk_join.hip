@@ -286,6 +286,19 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {  // set bits of m 
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// boundary ballots of a window starting at ws with wn records: ev bit t = record 2t starts a trace,
+// od bit t = record 2t+1 does (this wave's lanes)
+template <class Win>
+__device__ __forceinline__ void window_ballots(const Win& w, uint64_t ws, int wn, uint64_t* ev, uint64_t* od) {
+    const int t = threadIdx.x, lane = t & 63;
+    uint64_t prev = lane_shr1(w.tid[1]);
+    if (lane == 0) prev = (ws + 2 * t > 0) ? w.prev : ~w.tid[0];
+    const bool b0 = (2 * t < wn) && w.tid[0] != prev;
+    const bool b1 = (2 * t + 1 < wn) && w.tid[1] != w.tid[0];
+    *ev = __ballot(b0);
+    *od = __ballot(b1);
+}
+
 struct Window {  // two consecutive records per thread
     uint64_t tid[2], sid[2], pid[2], first[2], last[2];
     uint32_t svc[2], flags[2];
@@ -318,6 +331,32 @@ __device__ __forceinline__ void load_window(const JoinArgs& a, uint64_t ws, Wind
 // registers spent on a fifth workgroup per CU (hash factor 4 to fit the LDS): 1.233 ms.
 #ifndef ZK_K1_LATE
 #define ZK_K1_LATE 1
+#endif
+// ZK_K1_REST_AFTER_BOUNDARIES: issue a window's five late columns after its boundary ballots, so the
+// boundary phase's wait for the prefetched traceIds is not also a wait for the link stores that the
+// previous window issued after that prefetch (vmcnt counts loads and stores in one in-order queue)
+#ifndef ZK_K1_REST_AFTER_BOUNDARIES
+#define ZK_K1_REST_AFTER_BOUNDARIES 0
+#endif
+// ZK_K1_EARLY_BALLOT: take the next window's boundary ballots at the end of this window, before its
+// link stores (see the loop)
+#ifndef ZK_K1_EARLY_BALLOT
+#define ZK_K1_EARLY_BALLOT 1
+#endif
+// ZK_K1_ATOMIC_APPEND: waves claim their slice of the link list with an LDS atomic, so the window
+// needs no link-append barrier (3 barriers per window instead of 4); hash slots are emptied one
+// window later
+#ifndef ZK_K1_ATOMIC_APPEND
+#define ZK_K1_ATOMIC_APPEND 1
+#endif
+// ZK_K1_FAST_SCAN: skip the search for the window's first own trace start and for the range end
+// when the window before already found them (see phase 2)
+#ifndef ZK_K1_FAST_SCAN
+#define ZK_K1_FAST_SCAN 1
+#endif
+// ZK_K1_TOUCH: L2 prefetch of the next window's late columns from phase 3 (see there)
+#ifndef ZK_K1_TOUCH
+#define ZK_K1_TOUCH 0
 #endif
 __device__ __forceinline__ void load_tid(const JoinArgs& a, uint64_t ws, Window& w) {
     const uint64_t n = a.c.n;
@@ -380,6 +419,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     __shared__ __align__(16) uint64_t s_mask[NWORD];
     __shared__ uint32_t s_stat[ST_N];
     __shared__ uint32_t s_wsum[WG / 64];
+    __shared__ uint64_t s_cursor;  // ZK_K1_ATOMIC_APPEND: links (low 32) and items (high 32) appended
     __shared__ uint32_t s_hist[kMaxBuckets];  // links per cell bucket (K2's scatter offsets)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -421,10 +461,19 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     StatPack st;
     int fold_in = kFoldWindows;  // windows until the next stat fold (uniform)
     if (tid < ST_N) s_stat[tid] = 0u;
+    if (tid == 0) s_cursor = 0ull;
     for (uint32_t x = tid; x < a.nb; x += WG) s_hist[x] = 0u;
+    constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+#if ZK_K1_TOUCH
+    constexpr int kTouchLines = 160;  // 4 x 32 lines of 8-byte columns + 2 x 16 of 4-byte ones per window
+    static_assert(TILE == 512 && WG >= kTouchLines, "touch geometry");
+    uint32_t touch = 0u;
+#endif
+    uint32_t r_clear[2] = {kNoSlot, kNoSlot};  // hash slots this thread's leaders of the last window hold
 
     uint64_t ws = R0;         // window start (even)
     uint64_t seek = R0;       // first record that may start one of our traces
+    bool seek_start = false;  // seek is known to be a trace start (uniform)
     Window cur, nxt;
     constexpr bool JOIN = (MODE & kModeJoin) != 0, EMIT = (MODE & kModeEmit) != 0;
 #if ZK_K1_LATE
@@ -434,23 +483,27 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
 #endif
 #pragma unroll
     for (int x = tid; x < H / 4; x += WG) reinterpret_cast<uint4*>(s_ht)[x] = make_uint4(0u, 0u, 0u, 0u);
+    uint64_t m_ev, m_od;  // this wave's boundary ballots of the current window (uniform; phase 3 reuses them)
+    constexpr bool EB = ZK_K1_EARLY_BALLOT && ABL != 2;  // (the stream-only diagnostic has no phase 7)
+    if constexpr (EB) {
+        // the first window's ballots; later windows' are taken at the end of the window before (below)
+        window_ballots(cur, ws, (int)((n - ws) < (uint64_t)TILE ? (n - ws) : (uint64_t)TILE), &m_ev, &m_od);
+        if (lane == 0) *reinterpret_cast<ulonglong2*>(&s_mask[2 * wave]) = make_ulonglong2(m_ev, m_od);
+    }
     ZK_STAMP_DECL
     for (;;) {
-#if ZK_K1_LATE
+#if ZK_K1_LATE && !ZK_K1_REST_AFTER_BOUNDARIES
         load_rest<JOIN>(a, ws, cur);
 #endif
         const int wn = (int)((n - ws) < (uint64_t)TILE ? (n - ws) : (uint64_t)TILE);
         // ---- 1. trace boundaries of the window -------------------------------------------------
-        uint64_t m_ev, m_od;  // this wave's boundary ballots (uniform; phase 3 reuses them)
-        {
-            uint64_t prev = lane_shr1(cur.tid[1]);
-            if (lane == 0) prev = (ws + 2 * tid > 0) ? cur.prev : ~cur.tid[0];
-            const bool b0 = (2 * tid < wn) && cur.tid[0] != prev;
-            const bool b1 = (2 * tid + 1 < wn) && cur.tid[1] != cur.tid[0];
-            m_ev = __ballot(b0);
-            m_od = __ballot(b1);
+        if constexpr (!EB) {
+            window_ballots(cur, ws, wn, &m_ev, &m_od);
             if (lane == 0) *reinterpret_cast<ulonglong2*>(&s_mask[2 * wave]) = make_ulonglong2(m_ev, m_od);
         }
+#if ZK_K1_LATE && ZK_K1_REST_AFTER_BOUNDARIES
+        load_rest<JOIN>(a, ws, cur);
+#endif
         ZK_PHASE_SYNC(0);
         // ---- 2. which records are ours, where the next window starts (uniform) ----------------
         const int lo_j = (int)(seek - ws);
@@ -468,18 +521,27 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 od = x.y;
             }
             const int base = 128 * lane;
-            const int fs = lane < NW ? first_ge(ev, od, lo_j - base) : -1;
-            const int ft = lane < NW ? first_ge(ev, od, r1_j - base) : -1;
+            // steady state (ZK_K1_FAST_SCAN): the window starts at the trace start `seek` that the
+            // window before found, and the range end R1 is beyond it -- start = lo_j, stop = none,
+            // with no search (the search would return exactly these: bit lo_j is set in the masks)
+            const bool fast = ZK_K1_FAST_SCAN && !ZK_K1_SORTJOIN && seek_start && lo_j < wn && R1 - ws >= (uint64_t)wn;
+            if (fast) {
+                start = lo_j;
+            } else {
+                const int fs = lane < NW ? first_ge(ev, od, lo_j - base) : -1;
+                const int ft = lane < NW ? first_ge(ev, od, r1_j - base) : -1;
+                const uint64_t bs = __ballot(fs >= 0), bt = __ballot(ft >= 0);
+                if (bs) {
+                    const int w = __ffsll((unsigned long long)bs) - 1;
+                    start = 128 * w + __builtin_amdgcn_readlane(fs, w);
+                }
+                if (bt) {
+                    const int w = __ffsll((unsigned long long)bt) - 1;
+                    stop = 128 * w + __builtin_amdgcn_readlane(ft, w);
+                }
+            }
             const int lb = last_of(ev, od);
-            const uint64_t bs = __ballot(fs >= 0), bt = __ballot(ft >= 0), bl = __ballot(lb >= 0);
-            if (bs) {
-                const int w = __ffsll((unsigned long long)bs) - 1;
-                start = 128 * w + __builtin_amdgcn_readlane(fs, w);
-            }
-            if (bt) {
-                const int w = __ffsll((unsigned long long)bt) - 1;
-                stop = 128 * w + __builtin_amdgcn_readlane(ft, w);
-            }
+            const uint64_t bl = __ballot(lb >= 0);
             if (bl) {
                 const int w = 63 - (int)__clzll((long long)bl);
                 last_b = 128 * w + __builtin_amdgcn_readlane(lb, w);
@@ -505,6 +567,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         int m;                  // records [start, m) are processed in this window
         bool done = false;
         uint64_t next_seek = 0;
+        bool next_seek_start = false;  // next_seek is a trace start (uniform)
         if (start < 0 || (stop >= 0 && stop <= start)) {
             // no trace of ours starts in the rest of this window
             done = (start >= 0) || at_end || ws + (uint64_t)TILE >= R1;
@@ -519,9 +582,11 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         } else if (last_b > start) {
             m = last_b;  // the last trace may continue past the window: it starts the next one
             next_seek = ws + (uint64_t)last_b;
+            next_seek_start = true;
         } else if (start > 1) {
             m = start;  // a single long trace starts mid-window: give it a window of its own
             next_seek = ws + (uint64_t)start;
+            next_seek_start = true;
         } else {
             // the trace at `start` is longer than a window: spill it, then seek past it
             if (tid == 0) {
@@ -544,8 +609,15 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
 #endif
         ZK_STAMP(1);
         nrec += (uint64_t)(m - start);
+        uint64_t n_ev = 0, n_od = 0;  // the next window's ballots (EB)
         if constexpr (ABL != 2) {  // diagnostic build: 2 = stream windows only
 
+#if ZK_K1_ATOMIC_APPEND
+        // the last window's leaders empty their hash slots (see phase 7)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+            if (r_clear[e] != kNoSlot) s_ht[r_clear[e]] = 0u;
+#endif
         // ---- 3. segment ids and LDS staging ----------------------------------------------------
         // seg = index of the trace's first record in the window (the last boundary <= j), from the
         // wave's own ballots: record 2t+1 is its own segment start or shares 2t's. Staging stores
@@ -594,6 +666,33 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             }
 #endif
         }
+#if ZK_K1_TOUCH
+        // pull the next window's five late columns into L2 now (one 4-byte load per 128-byte line,
+        // right after this window's own late columns were waited for): the next window's late
+        // loads then hit L2, and the HBM round trip runs during phases 3-6 instead of stalling
+        // the next window's staging; the value is consumed after the phase-7 wait (below)
+        if (!done && tid < kTouchLines) {
+            const uint64_t nws = next_ws;
+            const int t = tid;
+            const uint8_t* p;
+            uint64_t off, lim;
+            if (t < 128) {
+                const int c = t >> 5;  // span_id, parent_id, first_ts, last_ts
+                p = (const uint8_t*)(c == 0 ? (const void*)a.c.span_id
+                                     : c == 1 ? (const void*)a.c.parent_id
+                                     : c == 2 ? (const void*)a.c.first_ts
+                                              : (const void*)a.c.last_ts);
+                off = nws * 8 + (uint64_t)(t & 31) * 128;
+                lim = n * 8;
+            } else {
+                const int c = (t - 128) >> 4;  // service_id, flags
+                p = (const uint8_t*)(c == 0 ? (const void*)a.c.service_id : (const void*)a.c.flags);
+                off = nws * 4 + (uint64_t)((t - 128) & 15) * 128;
+                lim = n * 4;
+            }
+            if (off + 4 <= lim) touch ^= *reinterpret_cast<const uint32_t*>(p + (off & ~3ull));
+        }
+#endif
         ZK_PHASE_SYNC(2);  // (the hash table is empty here: cleared once, then by its leaders)
 
         // ---- 4. groupBy((id, traceId)): the first fragment to claim a slot leads --------------
@@ -808,6 +907,22 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         // per-wave counts and lane offsets from ballots (nl, ni are 0..2: two bits each)
         const uint64_t l1 = __ballot(nl >= 1u), l2 = __ballot(nl >= 2u);
         const uint64_t i1 = EMIT ? __ballot(ni >= 1u) : 0ull, i2 = EMIT ? __ballot(ni >= 2u) : 0ull;
+#if ZK_K1_ATOMIC_APPEND
+        // no barrier: each wave claims its slice of the workgroup's lists with ONE LDS atomic on a
+        // cursor (links in the low 32 bits, sketch items in the high 32). The waves' order inside a
+        // list is whatever the atomics give -- the reduce adds exact integers, so it is free.
+        uint32_t lbase = 0, ibase = 0;
+        {
+            const uint64_t wtot = (uint64_t)(__popcll(l1) + __popcll(l2)) | ((uint64_t)(__popcll(i1) + __popcll(i2)) << 32);
+            uint64_t old = 0;
+            if (lane == 0 && wtot) old = atomicAdd((unsigned long long*)&s_cursor, (unsigned long long)wtot);
+            old = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(old >> 32), 0) << 32) | (uint32_t)__shfl((int)(uint32_t)old, 0);
+            lbase = (uint32_t)old + lanes_below(l1) + lanes_below(l2);
+            ibase = (uint32_t)(old >> 32) + lanes_below(i1) + lanes_below(i2);
+        }
+#else
+        // one exclusive scan for both counts: links in bits 0..15, items in 16..31 (<= 512 each)
+        // per-wave counts and lane offsets from ballots (nl, ni are 0..2: two bits each)
         const uint32_t below = (lanes_below(l1) + lanes_below(l2)) | ((lanes_below(i1) + lanes_below(i2)) << 16);
         if (lane == 0)
             s_wsum[wave] = (uint32_t)(__popcll(l1) + __popcll(l2)) | ((uint32_t)(__popcll(i1) + __popcll(i2)) << 16);
@@ -820,10 +935,26 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             total += v;
         }
         const uint32_t excl = base + below;
+        const uint32_t lbase = nout + (excl & 0xFFFFu), ibase = nitem + (excl >> 16);
+#endif
+        // the next window's ballots, BEFORE this window's link stores: the prefetched traceIds are
+        // then waited for while only they are in flight, not behind the stores (vmcnt is one queue
+        // for loads and stores, and the first use of a prefetched value waits for everything older
+        // in the compiler's model). s_mask is free: every wave read it in phase 2, before the
+        // phase-3 barrier; the next window's phase-1 barrier publishes the new masks.
+        if (EB && !done) {
+            const uint64_t nws = next_ws;
+            window_ballots(nxt, nws, (int)((n - nws) < (uint64_t)TILE ? (n - nws) : (uint64_t)TILE), &n_ev, &n_od);
+            if (lane == 0) *reinterpret_cast<ulonglong2*>(&s_mask[2 * wave]) = make_ulonglong2(n_ev, n_od);
+        }
+#if ZK_K1_TOUCH
+        asm volatile("" ::"v"(touch));  // the touch loads are waited for here, with the traceIds
+        touch = 0u;
+#endif
         if constexpr (ABL == 0 && JOIN) {
             // exactly two stores per thread on every path (absent links go to the list's trash
             // slot), so the loop-end wait for the prefetched window can count them: vmcnt(2)
-            uint32_t pos = nout + (excl & 0xFFFFu);
+            uint32_t pos = lbase;
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const bool v = r_link[e] != ~0ull;
@@ -836,10 +967,12 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
 #endif
                 pos += v ? 1u : 0u;
             }
+#if !ZK_K1_ATOMIC_APPEND
             nout += total & 0xFFFFu;
+#endif
         }
         if constexpr (ABL == 0 && EMIT) {
-            uint32_t pos = nitem + (excl >> 16);
+            uint32_t pos = ibase;
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const bool v = r_item[e] != ~0ull;
@@ -848,13 +981,23 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 it_svc[at] = r_isvc[e];
                 pos += v ? 1u : 0u;
             }
+#if !ZK_K1_ATOMIC_APPEND
             nitem += total >> 16;
+#endif
         }
+#if ZK_K1_ATOMIC_APPEND
+        // every leader empties its own slot in the NEXT window, after its phase-1 barrier (which
+        // every wave reaches only when done probing this window) and before its phase-3 barrier
+        // (after which that window inserts)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) r_clear[e] = (!ZK_K1_SORTJOIN && r_leader[e] == 2 * tid + e) ? r_slot[e] : kNoSlot;
+#else
         // every leader empties its own slot (phase 7's barrier is past all probes of this window;
         // the next window inserts only after its phase-1 and phase-3 barriers)
 #pragma unroll
         for (int e = 0; e < 2; ++e)
             if (!ZK_K1_SORTJOIN && r_leader[e] == 2 * tid + e) s_ht[r_slot[e]] = 0u;
+#endif
         ZK_STAMP(6);
         }  // ablate != 2
         if (--fold_in == 0) {
@@ -864,6 +1007,11 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         if (done) break;
         ws = next_ws;
         seek = next_seek;
+        seek_start = next_seek_start;
+        if constexpr (EB) {
+            m_ev = n_ev;
+            m_od = n_od;
+        }
 #if ZK_K1_LATE
         cur.tid[0] = nxt.tid[0];
         cur.tid[1] = nxt.tid[1];
@@ -877,6 +1025,11 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         ZK_STAMP(7);
     }
     ZK_STAMP_FLUSH();
+#if ZK_K1_ATOMIC_APPEND
+    __syncthreads();  // every wave's last append is in the cursor
+    nout = (uint32_t)s_cursor;
+    nitem = (uint32_t)(s_cursor >> 32);
+#endif
     if (tid == 0) {
         a.link_count[blockIdx.x] = nout;
         if constexpr (EMIT) a.rt_count[blockIdx.x] = nitem;
