@@ -56,10 +56,45 @@ __device__ __forceinline__ uint64_t d_hash(const uint8_t* s, uint32_t n) {  // =
     return h ? h : 1ull;
 }
 
-// bounds-checked big-endian reader over [p, e)
-struct DRd {
-    const uint8_t* p;
-    const uint8_t* e;
+// unaligned big-endian loads (one 2/4/8-byte access: gfx950 reads unaligned LDS and global words)
+template <class P>
+__device__ __forceinline__ uint16_t ld_be16(P p) {
+    uint16_t v;
+    __builtin_memcpy(&v, p, 2);
+    return __builtin_bswap16(v);
+}
+template <class P>
+__device__ __forceinline__ uint32_t ld_be32(P p) {
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);
+    return __builtin_bswap32(v);
+}
+template <class P>
+__device__ __forceinline__ uint64_t ld_be64(P p) {
+    uint64_t v;
+    __builtin_memcpy(&v, p, 8);
+    return __builtin_bswap64(v);
+}
+// copy 8 / 4 bytes through a register (source read before the destination is written)
+template <class D, class S>
+__device__ __forceinline__ void cp8(D d, S s) {
+    uint64_t v;
+    __builtin_memcpy(&v, s, 8);
+    __builtin_memcpy(d, &v, 8);
+}
+template <class D, class S>
+__device__ __forceinline__ void cp4(D d, S s) {
+    uint32_t v;
+    __builtin_memcpy(&v, s, 4);
+    __builtin_memcpy(d, &v, 4);
+}
+
+// bounds-checked big-endian reader over [p, e); P is a generic pointer, or an LDS one (the LDS
+// decoder: its reads are then ds_read_* instead of flat loads through the aperture)
+template <class P>
+struct DRdT {
+    P p;
+    P e;
     bool ok;
     __device__ bool need(uint64_t k) {
         if (!ok || (uint64_t)(e - p) < k) ok = false;
@@ -68,24 +103,44 @@ struct DRd {
     __device__ uint8_t u8() { return need(1) ? *p++ : 0; }
     __device__ int16_t i16() {
         if (!need(2)) return 0;
-        const int16_t v = (int16_t)((p[0] << 8) | p[1]);
+        const int16_t v = (int16_t)ld_be16(p);
         p += 2;
         return v;
     }
     __device__ int32_t i32() {
         if (!need(4)) return 0;
-        const uint32_t v = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+        const uint32_t v = ld_be32(p);
         p += 4;
         return (int32_t)v;
     }
+    // a struct field header: its type, and its id unless the type is STOP (returns false then, or
+    // on a short read). One 4-byte load when 4 bytes remain (the LDS decoder reads its fragment
+    // with 32-bit loads instead of three byte loads per field).
+    __device__ bool field(uint8_t* t, int16_t* id) {
+        if (!ok) return false;
+        if (e - p >= 4) {
+            const uint32_t v = ld_be32(p);
+            *t = (uint8_t)(v >> 24);
+            if (*t == T_STOP) {
+                p += 1;
+                return false;
+            }
+            *id = (int16_t)(v >> 8);
+            p += 3;
+            return true;
+        }
+        *t = u8();
+        if (!ok || *t == T_STOP) return false;
+        *id = i16();
+        return ok;
+    }
     __device__ int64_t i64() {
         if (!need(8)) return 0;
-        uint64_t v = 0;
-        for (int k = 0; k < 8; ++k) v = (v << 8) | p[k];
+        const uint64_t v = ld_be64(p);
         p += 8;
         return (int64_t)v;
     }
-    __device__ bool str(const uint8_t** s, uint32_t* len) {
+    __device__ bool str(P* s, uint32_t* len) {
         const int32_t l = i32();
         if (!ok || l < 0 || !need((uint64_t)l)) return ok = false;
         *s = p;
@@ -110,7 +165,7 @@ struct DRd {
                 case T_DOUBLE:
                 case T_I64: i64(); break;
                 case T_STRING: {
-                    const uint8_t* s;
+                    P s;
                     uint32_t l;
                     str(&s, &l);
                     break;
@@ -173,15 +228,20 @@ struct DRd {
     }
 };
 
+using DRd = DRdT<const uint8_t*>;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+
 // The generic skip out of line (nested containers are rare in stored spans): keeps its stack and
 // switch out of the decoders' register budget. DRd travels by value, so nothing goes to scratch.
-__device__ __noinline__ DRd skip_call(DRd r, uint8_t t) {
+template <class P>
+__device__ __noinline__ DRdT<P> skip_call(DRdT<P> r, uint8_t t) {
     r.skip(t);
     return r;
 }
 
 // skip one value: fixed-width fields and strings inline, anything else through skip_call
-__device__ __forceinline__ void skip_flat(DRd& r, uint8_t t) {
+template <class P>
+__device__ __forceinline__ void skip_flat(DRdT<P>& r, uint8_t t) {
     uint32_t w = 0;
     switch (t) {
         case T_BOOL:
@@ -205,26 +265,38 @@ __device__ __forceinline__ void skip_flat(DRd& r, uint8_t t) {
 }
 
 // skip a struct whose fields are flat or flat structs (BinaryAnnotation with its Endpoint host)
-__device__ __forceinline__ void skip_struct2(DRd& r) {
+template <class P>
+__device__ __forceinline__ void skip_struct2(DRdT<P>& r) {
     for (;;) {
-        const uint8_t t = r.u8();
-        if (!r.ok || t == T_STOP) return;
-        r.i16();
+        uint8_t t;
+        int16_t fid;
+        if (!r.field(&t, &fid)) return;
         if (t != T_STRUCT) {
             skip_flat(r, t);
             continue;
         }
-        for (;;) {
-            const uint8_t u = r.u8();
-            if (!r.ok || u == T_STOP) break;
-            r.i16();
-            skip_flat(r, u);
-        }
+        uint8_t u;
+        int16_t uid;
+        while (r.field(&u, &uid)) skip_flat(r, u);
         if (!r.ok) return;
     }
 }
 
-__device__ __forceinline__ bool snappy_hdr(const uint8_t* in, uint64_t n, uint64_t* len, uint64_t* hdr) {
+// Snappy copy of l bytes from off back: an 8-byte (off >= 8) or 4-byte (off >= 4) step never reads
+// what it writes; the overlapping rest goes bytewise
+template <class P>
+__device__ __forceinline__ void backref_copy(P out, uint64_t o, uint64_t off, uint64_t l) {
+    uint64_t k = 0;
+    if (off >= 8) {
+        for (; k + 8 <= l; k += 8) cp8(out + o + k, out + o - off + k);
+    } else if (off >= 4) {
+        for (; k + 4 <= l; k += 4) cp4(out + o + k, out + o - off + k);
+    }
+    for (; k < l; ++k) out[o + k] = out[o - off + k];
+}
+
+template <class P>
+__device__ __forceinline__ bool snappy_hdr(P in, uint64_t n, uint64_t* len, uint64_t* hdr) {
     uint64_t v = 0;
     for (uint64_t i = 0; i < n && i < 5; ++i) {
         v |= (uint64_t)(in[i] & 0x7F) << (7 * i);
@@ -257,13 +329,7 @@ __device__ __forceinline__ bool snappy_block(const uint8_t* in, uint64_t n, uint
             l += 1;
             if (i + l > n || o + l > len) return false;
             uint64_t k = 0;
-            for (; k + 4 <= l; k += 4) {
-                const uint8_t x0 = in[i + k], x1 = in[i + k + 1], x2 = in[i + k + 2], x3 = in[i + k + 3];
-                out[o + k] = x0;
-                out[o + k + 1] = x1;
-                out[o + k + 2] = x2;
-                out[o + k + 3] = x3;
-            }
+            for (; k + 8 <= l; k += 8) cp8(out + o + k, in + i + k);
             for (; k < l; ++k) out[o + k] = in[i + k];
             i += l;
             o += l;
@@ -287,18 +353,7 @@ __device__ __forceinline__ bool snappy_block(const uint8_t* in, uint64_t n, uint
             i += 4;
         }
         if (off == 0 || off > o || o + l > len) return false;
-        uint64_t k = 0;
-        if (off >= 4) {  // a 4-byte step never reads what it writes
-            for (; k + 4 <= l; k += 4) {
-                const uint8_t* q = out + o - off + k;
-                const uint8_t x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
-                out[o + k] = x0;
-                out[o + k + 1] = x1;
-                out[o + k + 2] = x2;
-                out[o + k + 3] = x3;
-            }
-        }
-        for (; k < l; ++k) out[o + k] = out[o - off + k];  // overlapping tail: bytewise
+        backref_copy(out, o, off, l);
         o += l;
     }
     return o == len;
@@ -350,7 +405,8 @@ __global__ __launch_bounds__(kIngWG) void k_ing_rawlen(IngArgs a) {
     a.status[i] = len == kBadLen ? kStUndecodable : kStOk;
 }
 
-__device__ __forceinline__ bool is_core(const uint8_t* v, uint32_t l, int* c) {
+template <class P>
+__device__ __forceinline__ bool is_core(P v, uint32_t l, int* c) {
     if (!v || l != 2) return false;
     if (v[0] == 'c' && (v[1] == 's' || v[1] == 'r')) {
         *c = v[1] == 's' ? 0 : 1;
@@ -364,13 +420,14 @@ __device__ __forceinline__ bool is_core(const uint8_t* v, uint32_t l, int* c) {
 }
 
 // the service name of an endpoint struct: field 3 (string); absent or "" -> kUnknown
-__device__ __forceinline__ void read_endpoint(DRd& r, const uint8_t** name, uint32_t* nlen) {
+template <class P>
+__device__ __forceinline__ void read_endpoint(DRdT<P>& r, P* name, uint32_t* nlen) {
     *name = nullptr;
     *nlen = 0;
     for (;;) {
-        const uint8_t t = r.u8();
-        if (!r.ok || t == T_STOP) return;
-        const int16_t id = r.i16();
+        uint8_t t;
+        int16_t id;
+        if (!r.field(&t, &id)) return;
         if (id == 3 && t == T_STRING)
             r.str(name, nlen);
         else
@@ -380,25 +437,26 @@ __device__ __forceinline__ void read_endpoint(DRd& r, const uint8_t** name, uint
 
 // The thrift walk of one decompressed Span at [src, src + len): validation (status on failure,
 // -1), the record columns, and the service name (1: *nm/*nl set; 0: the span has no service).
-__device__ __forceinline__ int parse_record(const IngArgs& a, uint64_t i, const uint8_t* src, uint64_t len,
+template <class P>
+__device__ __forceinline__ int parse_record(const IngArgs& a, uint64_t i, P src, uint64_t len,
                                             const uint8_t** nm_out, uint32_t* nl_out) {
-    DRd r{src, src + len, true};
+    DRdT<P> r{src, src + len, true};
     int64_t trace = 0, id = 0, parent = 0;
     bool has_parent = false, has_name = false, invalid = false;
     int64_t first = 0, last = 0;
     uint32_t nann = 0, cnt[4] = {0, 0, 0, 0};
-    const uint8_t* srv = nullptr;  // first sr/ss host's name (srv_set: a host was seen)
-    const uint8_t* cli = nullptr;
+    P srv = nullptr;  // first sr/ss host's name (srv_set: a host was seen)
+    P cli = nullptr;
     uint32_t srv_len = 0, cli_len = 0;
     bool srv_set = false, cli_set = false;
     for (;;) {
-        const uint8_t t = r.u8();
-        if (!r.ok || t == T_STOP) break;
-        const int16_t fid = r.i16();
+        uint8_t t;
+        int16_t fid;
+        if (!r.field(&t, &fid)) break;
         if (fid == 1 && t == T_I64) {
             trace = r.i64();
         } else if (fid == 3 && t == T_STRING) {
-            const uint8_t* s;
+            P s;
             uint32_t l;
             has_name = r.str(&s, &l);
         } else if (fid == 4 && t == T_I64) {
@@ -420,15 +478,15 @@ __device__ __forceinline__ int parse_record(const IngArgs& a, uint64_t i, const 
             for (int32_t q = 0; r.ok && q < cntl; ++q) {
                 // Annotation {1: i64 timestamp, 2: string value, 3: optional Endpoint host}
                 int64_t ts = 0;
-                const uint8_t* v = nullptr;
+                P v = nullptr;
                 uint32_t vl = 0;
                 bool host = false;
-                const uint8_t* hn = nullptr;
+                P hn = nullptr;
                 uint32_t hl = 0;
                 for (;;) {
-                    const uint8_t at = r.u8();
-                    if (!r.ok || at == T_STOP) break;
-                    const int16_t aid = r.i16();
+                    uint8_t at;
+                    int16_t aid;
+                    if (!r.field(&at, &aid)) break;
                     if (aid == 1 && at == T_I64)
                         ts = r.i64();
                     else if (aid == 2 && at == T_STRING)
@@ -491,11 +549,11 @@ __device__ __forceinline__ int parse_record(const IngArgs& a, uint64_t i, const 
     uint32_t nl = 0;
     if (srv_set) {
         f |= ZK_F_SVC_SERVER;
-        nm = srv;
+        nm = (const uint8_t*)srv;
         nl = srv_len;
     } else if (cli_set) {
         f |= ZK_F_SVC_CLIENT;
-        nm = cli;
+        nm = (const uint8_t*)cli;
         nl = cli_len;
     }
     if ((srv_set || cli_set) && (!nm || nl == 0)) {
@@ -591,8 +649,8 @@ constexpr uint32_t kLdsSlack = 64;  // region bytes beyond max(raw, compressed):
 
 // Snappy block from in = out + D (the same region), in place: false with *unsafe set when a step
 // would write over input bytes not yet read.
-__device__ __forceinline__ bool snappy_inplace(uint8_t* out, uint64_t D, uint64_t n, uint64_t len, bool* unsafe) {
-    const uint8_t* in = out + D;
+__device__ __forceinline__ bool snappy_inplace(lds_u8* out, uint64_t D, uint64_t n, uint64_t len, bool* unsafe) {
+    const lds_u8* in = out + D;
     uint64_t dl, hdr;
     if (!snappy_hdr(in, n, &dl, &hdr) || dl != len) return false;
     uint64_t o = 0, i = hdr;
@@ -611,18 +669,14 @@ __device__ __forceinline__ bool snappy_inplace(uint8_t* out, uint64_t D, uint64_
             }
             l += 1;
             if (i + l > n || o + l > len) return false;
-            if (o > D + i) {  // output byte o + k is written after input byte i + k + 3 is read
+            // an 8-byte step writes output [o + k, o + k + 8) after reading input [i + k, i + k + 8):
+            // it never reaches unread input while o <= D + i
+            if (o > D + i) {
                 *unsafe = true;
                 return false;
             }
             uint64_t k = 0;
-            for (; k + 4 <= l; k += 4) {
-                const uint8_t x0 = in[i + k], x1 = in[i + k + 1], x2 = in[i + k + 2], x3 = in[i + k + 3];
-                out[o + k] = x0;
-                out[o + k + 1] = x1;
-                out[o + k + 2] = x2;
-                out[o + k + 3] = x3;
-            }
+            for (; k + 8 <= l; k += 8) cp8(out + o + k, in + i + k);
             for (; k < l; ++k) out[o + k] = in[i + k];
             i += l;
             o += l;
@@ -650,18 +704,7 @@ __device__ __forceinline__ bool snappy_inplace(uint8_t* out, uint64_t D, uint64_
             *unsafe = true;
             return false;
         }
-        uint64_t k = 0;
-        if (off >= 4) {  // a 4-byte step never reads what it writes
-            for (; k + 4 <= l; k += 4) {
-                const uint8_t* q = out + o - off + k;
-                const uint8_t x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
-                out[o + k] = x0;
-                out[o + k + 1] = x1;
-                out[o + k + 2] = x2;
-                out[o + k + 3] = x3;
-            }
-        }
-        for (; k < l; ++k) out[o + k] = out[o - off + k];  // overlapping tail: bytewise
+        backref_copy(out, o, off, l);
         o += l;
     }
     return o == len;
@@ -711,16 +754,21 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                 // [D - mis, D + clen + 15] inside [0, R) since R >= clen + kLdsSlack
                 const uint32_t D = ((R - 16u - (uint32_t)clen - mis) & ~15u) + mis;
                 uint8_t* reg = s_buf + R0;
-                const uint4* g = reinterpret_cast<const uint4*>((uintptr_t)(a.buf + b) & ~(uintptr_t)15);
+                // 16-B blocks through a global-space pointer (global_load, not a flat load)
+                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                typedef const __attribute__((address_space(1))) u32x4 g_u32x4;
+                g_u32x4* g = (g_u32x4*)((uintptr_t)(a.buf + b) & ~(uintptr_t)15);
                 const uint32_t nblk = (uint32_t)((clen + mis + 15) >> 4);
-                uint4* dst = reinterpret_cast<uint4*>(reg + D - mis);
+                u32x4* dst = reinterpret_cast<u32x4*>(reg + D - mis);
                 for (uint32_t c = 0; c < nblk; ++c) dst[c] = g[c];
-                const uint8_t* src = reg + D;
+                // the region as an LDS pointer: the decoder's byte and word reads become ds_read_*
+                lds_u8* const lreg = (lds_u8*)reg;
+                const lds_u8* src = lreg + D;
                 uint64_t len = clen;
                 bool ok = true, unsafe = false;
                 if (a.snappy) {
-                    ok = snappy_inplace(reg, D, clen, raw, &unsafe);
-                    src = reg;
+                    ok = snappy_inplace(lreg, D, clen, raw, &unsafe);
+                    src = lreg;
                     len = raw;
                 }
                 if (!ok) {
@@ -732,7 +780,7 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                     if (r >= 0) {
                         if (r && !try_resolve(a, i, nm, nl, d_hash(nm, nl))) {
                             if (nm != a.unknown) {  // the name lies in this lane's own bytes
-                                const uint64_t off = (uint64_t)((uintptr_t)nm - (uintptr_t)src);
+                                const uint64_t off = (uint64_t)(nm - (const uint8_t*)src);
                                 if (a.snappy) {
                                     uint8_t* gd = a.scratch + a.raw_off[i] + off;  // copy out to the scratch
                                     for (uint32_t q = 0; q < nl; ++q) gd[q] = nm[q];

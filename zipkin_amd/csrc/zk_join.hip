@@ -216,15 +216,32 @@ __device__ __forceinline__ bool slot_valid(uint32_t w) { return ((w >> kSlotB) &
 #define ZK_K1_HOTREAD 0
 #endif
 __device__ __forceinline__ uint64_t hot_index(uint64_t i) { return ZK_K1_HOTREAD ? (i & 0xFFFEull) : i; }
+// ZK_K1_NT_LOADS: the column loads carry the non-temporal hint (streamed once; only the re-read
+// tail of a window would hit L2 again)
+#ifndef ZK_K1_NT_LOADS
+#define ZK_K1_NT_LOADS 0
+#endif
 __device__ __forceinline__ void ld2_u64(const uint64_t* __restrict__ p, uint64_t i, uint64_t lim, uint64_t v[2]) {
-    const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(p + hot_index(i < lim ? i : 0));
+    const ulonglong2* q = reinterpret_cast<const ulonglong2*>(p + hot_index(i < lim ? i : 0));
+#if ZK_K1_NT_LOADS
+    v[0] = __builtin_nontemporal_load(&q->x);
+    v[1] = __builtin_nontemporal_load(&q->y);
+#else
+    const ulonglong2 x = *q;
     v[0] = x.x;
     v[1] = x.y;
+#endif
 }
 __device__ __forceinline__ void ld2_u32(const uint32_t* __restrict__ p, uint64_t i, uint64_t lim, uint32_t v[2]) {
-    const uint2 x = *reinterpret_cast<const uint2*>(p + hot_index(i < lim ? i : 0));
+    const uint2* q = reinterpret_cast<const uint2*>(p + hot_index(i < lim ? i : 0));
+#if ZK_K1_NT_LOADS
+    v[0] = __builtin_nontemporal_load(&q->x);
+    v[1] = __builtin_nontemporal_load(&q->y);
+#else
+    const uint2 x = *q;
     v[0] = x.x;
     v[1] = x.y;
+#endif
 }
 
 // K1 stat counters: the per-thread 16-bit pack (StatPack) is folded into the workgroup's u32 LDS
@@ -357,6 +374,10 @@ __device__ __forceinline__ void load_window(const JoinArgs& a, uint64_t ws, Wind
 // ZK_K1_TOUCH: L2 prefetch of the next window's late columns from phase 3 (see there)
 #ifndef ZK_K1_TOUCH
 #define ZK_K1_TOUCH 0
+#endif
+// ZK_K1_NT_STORES: link stores with the non-temporal hint
+#ifndef ZK_K1_NT_STORES
+#define ZK_K1_NT_STORES 0
 #endif
 __device__ __forceinline__ void load_tid(const JoinArgs& a, uint64_t ws, Window& w) {
     const uint64_t n = a.c.n;
@@ -963,7 +984,11 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 const v2u_t lv = {(unsigned int)r_link[e], (unsigned int)(r_link[e] >> 32)};
                 __builtin_amdgcn_raw_buffer_store_b64(lv, out_rsrc, v ? pos * 8u : 0x7FFFFFF8u, 0, 0);
 #else
+#if ZK_K1_NT_STORES
+                __builtin_nontemporal_store(r_link[e], &out[v ? (uint64_t)pos : trash + (ZK_K1_TRASH_SPREAD ? e : 0)]);
+#else
                 out[v ? (uint64_t)pos : trash + (ZK_K1_TRASH_SPREAD ? e : 0)] = r_link[e];
+#endif
 #endif
                 pos += v ? 1u : 0u;
             }
