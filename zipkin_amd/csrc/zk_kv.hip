@@ -42,8 +42,15 @@ __device__ __forceinline__ bool beats(uint32_t e1, uint64_t k1, uint32_t e2, uin
 struct RowHash {
     uint32_t x, h2, sh, set;  // set: the key's first slot in a workgroup's candidate hash set
     RowHash() = default;
-    __device__ __forceinline__ RowHash(uint64_t key, uint64_t seed, uint32_t wbits) {
-        const uint64_t h = sk_mix64(key ^ seed);
+    __device__ __forceinline__ RowHash(uint64_t key, uint64_t seed, uint32_t wbits) { init(sk_mix64(key ^ seed), wbits); }
+    // from the key's hash h = sk_mix64(key ^ seed): the partition writes h, so the sketch and
+    // candidate passes skip the 64-bit mix
+    __device__ static __forceinline__ RowHash from_hash(uint64_t h, uint32_t wbits) {
+        RowHash r;
+        r.init(h, wbits);
+        return r;
+    }
+    __device__ __forceinline__ void init(uint64_t h, uint32_t wbits) {
         set = (uint32_t)(h >> 53);  // top 11 bits (kSetCap = 2^11)
         x = (uint32_t)h;
         h2 = (uint32_t)(h >> 32) | 1u;
@@ -65,7 +72,13 @@ __device__ __forceinline__ uint32_t estimate(const uint32_t* cm, const KvArgs& a
     return estimate_rh(cm, a, RowHash(key, a.seeds[0], a.wbits));
 }
 
-// Distinct (key, estimate) set keeping the best `keep` entries (estimate desc, key asc).
+// a key's count-min hash and back (sk_mix64 is a bijection)
+__device__ __forceinline__ uint64_t kv_hash(uint64_t key, uint64_t seed) { return sk_mix64(key ^ seed); }
+__device__ __forceinline__ uint64_t kv_key(uint64_t h, uint64_t seed) { return sk_unmix64(h) ^ seed; }
+
+// Distinct (key, estimate) set keeping the best `keep` entries (estimate desc, key asc). The hash set
+// hk holds the keys' HASHES (kv_hash: distinct keys, distinct hashes); the sort buffer sk and the
+// threshold hold the keys themselves, so ties order by key as the oracle does.
 struct TopSet {
     uint64_t hk[kSetCap];
     uint32_t he[kSetCap];
@@ -75,7 +88,7 @@ struct TopSet {
     uint32_t pending[2];  // survivors of the current block (candidates kernel), by block parity
     uint32_t has_thr, thr_est;
     uint64_t thr_key;
-    uint32_t special, special_est;  // the key equal to the empty sentinel
+    uint32_t special, special_est;  // the key whose hash equals the empty sentinel
 };
 
 __device__ void ts_init(TopSet& t) {
@@ -88,7 +101,7 @@ __device__ void ts_init(TopSet& t) {
     __syncthreads();
 }
 
-__device__ __forceinline__ void ts_insert(TopSet& t, uint64_t key, uint32_t est, uint32_t slot) {
+__device__ __forceinline__ void ts_insert(TopSet& t, uint64_t key, uint32_t est, uint32_t slot) {  // key: a hash
     if (key == kEmptyKey) {
         if (atomicCAS(&t.special, 0u, 1u) == 0u) {
             t.special_est = est;
@@ -128,23 +141,23 @@ __device__ __forceinline__ bool ts_contains(TopSet& t, uint64_t key, uint32_t sl
     }
 }
 
-__device__ __forceinline__ uint32_t set_slot(uint64_t key, uint64_t seed) { return (uint32_t)(sk_mix64(key ^ seed) >> 53); }
-
-__device__ __forceinline__ void ts_offer(TopSet& t, uint64_t key, uint32_t est, uint32_t slot) {
+// offer a key (threshold test on the key itself) whose hash is h
+__device__ __forceinline__ void ts_offer(TopSet& t, uint64_t key, uint64_t h, uint32_t est) {
     if (est == 0u) return;
     if (t.has_thr && !beats(est, key, t.thr_est, t.thr_key)) return;
-    ts_insert(t, key, est, slot);
+    ts_insert(t, h, est, (uint32_t)(h >> 53));
 }
 
-// gather + sort (best first) into sk/se; returns the number of entries. Clears the set.
-__device__ uint32_t ts_sort(TopSet& t) {
+// gather + sort (best first) into sk/se, hashes turned back into keys; returns the number of
+// entries. Clears the set.
+__device__ uint32_t ts_sort(TopSet& t, uint64_t seed) {
     if (threadIdx.x == 0) t.gcount = 0;
     __syncthreads();
     for (uint32_t x = threadIdx.x; x < kSetCap; x += kKvWG) {
         const uint64_t k = t.hk[x];
         if (k != kEmptyKey) {
             const uint32_t p = atomicAdd(&t.gcount, 1u);
-            t.sk[p] = k;
+            t.sk[p] = kv_key(k, seed);
             t.se[p] = t.he[x];
         }
         t.hk[x] = kEmptyKey;
@@ -152,7 +165,7 @@ __device__ uint32_t ts_sort(TopSet& t) {
     __syncthreads();
     if (threadIdx.x == 0 && t.special) {
         const uint32_t p = t.gcount++;
-        t.sk[p] = kEmptyKey;
+        t.sk[p] = kv_key(kEmptyKey, seed);
         t.se[p] = t.special_est;
     }
     __syncthreads();
@@ -192,14 +205,17 @@ __device__ uint32_t ts_sort(TopSet& t) {
 
 // keep the best `keep`, raise the threshold when the kept set is full
 __device__ void ts_compact(TopSet& t, uint32_t keep, uint64_t seed) {
-    const uint32_t n = ts_sort(t);
+    const uint32_t n = ts_sort(t, seed);
     const uint32_t m = n < keep ? n : keep;
     if (threadIdx.x == 0 && m == keep && keep > 0) {
         t.has_thr = 1;
         t.thr_est = t.se[m - 1];
         t.thr_key = t.sk[m - 1];
     }
-    for (uint32_t x = threadIdx.x; x < m; x += kKvWG) ts_insert(t, t.sk[x], t.se[x], set_slot(t.sk[x], seed));
+    for (uint32_t x = threadIdx.x; x < m; x += kKvWG) {
+        const uint64_t h = kv_hash(t.sk[x], seed);
+        ts_insert(t, h, t.se[x], (uint32_t)(h >> 53));
+    }
     __syncthreads();
 }
 
@@ -247,7 +263,7 @@ __global__ __launch_bounds__(kKvWG) void k_kv_sketch(KvArgs a) {
         // row hashes unconditionally, so the loads are not sunk into the conditional (see candidates)
         RowHash rh[U];
 #pragma unroll
-        for (int e = 0; e < U; ++e) rh[e] = RowHash(k[e], a.seeds[0], a.wbits);
+        for (int e = 0; e < U; ++e) rh[e] = RowHash::from_hash(k[e], a.wbits);  // keys arrive hashed
 #pragma unroll
         for (int e = 0; e < U; ++e) {
             if (b + (uint64_t)e * kKvWG + threadIdx.x < hi)
@@ -303,7 +319,7 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
         uint32_t est[J], slot[J];
 #pragma unroll
         for (int j = 0; j < J; ++j) {
-            const RowHash rh(kq[j], a.seeds[0], a.wbits);
+            const RowHash rh = RowHash::from_hash(kq[j], a.wbits);  // kq: the keys' hashes
             est[j] = estimate_rh(cm, a, rh);
             slot[j] = rh.set;
         }
@@ -312,8 +328,10 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
         uint32_t need = 0;
 #pragma unroll
         for (int j = 0; j < J; ++j) {
+            // a tie with the threshold estimate is decided on the key itself (unhashed only then)
             const bool live = b + (uint64_t)j * kKvWG + threadIdx.x < hi && est[j] != 0u &&
-                              (!has_thr || beats(est[j], kq[j], thr_est, thr_key));
+                              (!has_thr || est[j] > thr_est ||
+                               (est[j] == thr_est && kv_key(kq[j], a.seeds[0]) < thr_key));
             if (live && !ts_contains(t, kq[j], slot[j])) need |= 1u << j;
         }
         if (need) atomicAdd(&t.pending[parity], (uint32_t)__popc(need));
@@ -336,7 +354,7 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
         }
         parity ^= 1u;
     }
-    const uint32_t n = ts_sort(t);
+    const uint32_t n = ts_sort(t, a.seeds[0]);
     uint64_t* ok = a.unit_key + (uint64_t)u * a.cand;
     uint32_t* oe = a.unit_est + (uint64_t)u * a.cand;
     for (uint32_t x = threadIdx.x; x < a.cand; x += kKvWG) {
@@ -377,14 +395,14 @@ __global__ __launch_bounds__(kKvWG) void k_kv_merge(KvArgs a, uint32_t use_units
                 old = a.extra_est[(l * a.S + s) * C + x];
             }
             if (old) {
-                const RowHash rh(key, a.seeds[0], a.wbits);
-                ts_offer(t, key, estimate_rh(cm, a, rh), rh.set);
+                const uint64_t h = kv_hash(key, a.seeds[0]);
+                ts_offer(t, key, h, estimate_rh(cm, a, RowHash::from_hash(h, a.wbits)));
             }
         }
         __syncthreads();
         if (t.count > kSortCap - kRound) ts_compact(t, C, a.seeds[0]);
     }
-    const uint32_t n = ts_sort(t);
+    const uint32_t n = ts_sort(t, a.seeds[0]);
     for (uint32_t x = threadIdx.x; x < C; x += kKvWG) {
         a.cand_key[(uint64_t)s * C + x] = x < n ? t.sk[x] : 0ull;
         a.cand_est[(uint64_t)s * C + x] = x < n ? t.se[x] : 0u;

@@ -238,7 +238,9 @@ zk_status zk_kv_accumulate(zk_kv* k, const uint32_t* svc, const uint64_t* keys, 
         k->unit_cap = (uint32_t)max_units;
     }
     if (k->timing) KV_HIP(k, hipEventRecord(k->ev[0], k->stream));
-    KV_HIP(k, launch_partition(plan, svc, keys, n, k->sorted, k->seg, k->dropped, k->part, k->stream));
+    // the partition writes each key's count-min hash sk_mix64(key ^ seeds[0]), not the key itself
+    KV_HIP(k, launch_partition(plan, svc, keys, n, k->sorted, k->seg, k->dropped, k->part, k->stream, true,
+                               a.seeds[0]));
     KV_HIP(k, launch_unit_plan(k->seg, a.S, a.unit_items, k->unit_base, k->stream));
     if (k->timing) KV_HIP(k, hipEventRecord(k->ev[1], k->stream));
     a.keys = k->sorted;

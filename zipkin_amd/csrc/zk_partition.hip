@@ -65,7 +65,7 @@ __global__ __launch_bounds__(kPartWG) void k_part_scatter(const uint32_t* __rest
                                                            uint64_t per, const uint32_t* __restrict__ counts,
                                                            uint32_t S, uint32_t grid,
                                                            const uint32_t* __restrict__ offs,
-                                                           uint64_t* __restrict__ out) {
+                                                           uint64_t* __restrict__ out, bool hash, uint64_t hash_seed) {
     extern __shared__ uint32_t cur[];  // absolute output cursor per service
     for (uint32_t i = threadIdx.x; i < S; i += kPartWG) cur[i] = offs[(uint64_t)i * grid + blockIdx.x];
     __syncthreads();
@@ -80,6 +80,7 @@ __global__ __launch_bounds__(kPartWG) void k_part_scatter(const uint32_t* __rest
             const bool in = i < hi;
             v[e] = in ? svc[i] : 0xFFFFFFFFu;
             p[e] = in ? payload[i] : 0ull;
+            if (hash) p[e] = sk_mix64(p[e] ^ hash_seed);
         }
 #pragma unroll
         for (int e = 0; e < kPartU; ++e)
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(WG) void k_part_scatter_lines(const uint32_t* __res
                                                             uint64_t per, const uint32_t* __restrict__ counts,
                                                             uint32_t S, uint32_t grid,
                                                             const uint32_t* __restrict__ offs,
-                                                            uint64_t* __restrict__ out) {
+                                                            uint64_t* __restrict__ out, bool hash, uint64_t hash_seed) {
     constexpr int C = WG * U;
     constexpr int BPT = (kLineMaxS + WG - 1) / WG;  // services per thread in the scan
     __shared__ uint32_t s_cur[kLineMaxS];  // output position of each service's first pending item
@@ -143,7 +144,7 @@ __global__ __launch_bounds__(WG) void k_part_scatter_lines(const uint32_t* __res
         uint32_t bk[U], rank[U];
 #pragma unroll
         for (int k = 0; k < U; ++k) {
-            v[k] = nv[k];
+            v[k] = hash ? sk_mix64(nv[k] ^ hash_seed) : nv[k];
             bk[k] = (base + tid + (uint64_t)WG * k < hi) ? ns[k] : 0xFFFFFFFFu;
             const uint64_t i = base + C + tid + (uint64_t)WG * k;  // next chunk in flight
             ns[k] = svc[i < hi ? i : lo0];
@@ -293,7 +294,7 @@ uint64_t partition_scratch_bytes(const PartitionPlan& p) {
 namespace {
 hipError_t partition_impl(const PartitionPlan& p, const uint32_t* svc, const uint64_t* payload, uint64_t n,
                           const uint32_t* counts, uint64_t* out, uint64_t* seg, unsigned long long* dropped,
-                          void* scratch, hipStream_t s) {
+                          void* scratch, hipStream_t s, bool hash, uint64_t hash_seed) {
     const uint64_t m = (uint64_t)p.S * p.grid;
     const uint64_t a = (m * 4 + 255) & ~255ull;
     uint32_t* hist = (uint32_t*)scratch;
@@ -310,10 +311,10 @@ hipError_t partition_impl(const PartitionPlan& p, const uint32_t* svc, const uin
     if (p.S <= kLineMaxS)
         hipLaunchKernelGGL((k_part_scatter_lines<ZK_PART_U, ZK_PART_WG>), dim3(p.grid), dim3(ZK_PART_WG),
                            (size_t)p.S * kLineItems * 8, s,
-                           svc, payload, n, p.per_wg, counts, p.S, p.grid, offs, out);
+                           svc, payload, n, p.per_wg, counts, p.S, p.grid, offs, out, hash, hash_seed);
     else
         hipLaunchKernelGGL(k_part_scatter, dim3(p.grid), dim3(kPartWG), lds, s, svc, payload, n, p.per_wg, counts,
-                           p.S, p.grid, offs, out);
+                           p.S, p.grid, offs, out, hash, hash_seed);
     hipLaunchKernelGGL(k_part_seg, dim3((p.S + 256) / 256), dim3(256), 0, s, offs, hist, p.S, p.grid, seg);
     return hipGetLastError();
 }
@@ -321,8 +322,8 @@ hipError_t partition_impl(const PartitionPlan& p, const uint32_t* svc, const uin
 
 hipError_t launch_partition(const PartitionPlan& p, const uint32_t* svc, const uint64_t* payload, uint64_t n,
                             uint64_t* out, uint64_t* seg, unsigned long long* dropped, void* scratch,
-                            hipStream_t s) {
-    return partition_impl(p, svc, payload, n, nullptr, out, seg, dropped, scratch, s);
+                            hipStream_t s, bool hash, uint64_t hash_seed) {
+    return partition_impl(p, svc, payload, n, nullptr, out, seg, dropped, scratch, s, hash, hash_seed);
 }
 
 PartitionPlan partition_plan_lists(uint32_t lists, uint32_t S) {
@@ -338,7 +339,7 @@ hipError_t launch_partition_lists(const PartitionPlan& p0, const uint32_t* svc, 
                                   unsigned long long* dropped, void* scratch, hipStream_t s) {
     PartitionPlan p = p0;
     p.per_wg = stride;
-    return partition_impl(p, svc, payload, 0, counts, out, seg, dropped, scratch, s);
+    return partition_impl(p, svc, payload, 0, counts, out, seg, dropped, scratch, s, false, 0);
 }
 
 hipError_t launch_unit_plan(const uint64_t* seg, uint32_t S, uint64_t unit_items, uint32_t* unit_base,

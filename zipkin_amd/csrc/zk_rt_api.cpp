@@ -178,7 +178,16 @@ zk_status rt_consume_lists(zk_rt* r, uint32_t grid, uint64_t stride, uint64_t n)
 
 const char* rt_error(const zk_rt* r) { return r->err.c_str(); }
 int rt_device(const zk_rt* r) { return r->device; }
-void rt_set_stream(zk_rt* r, hipStream_t s) { r->stream = s ? s : r->own; }
+// Moving the sketch to another stream (zk_rt_bind) first drains the one it was on: work queued
+// there (the zeroing of zk_rt_create/zk_rt_reset on the private stream) would otherwise race with
+// the first kernels on the new one -- a zeroing that lands after the first sketch pass wipes it.
+void rt_set_stream(zk_rt* r, hipStream_t s) {
+    hipStream_t ns = s ? s : r->own;
+    if (ns != r->stream) {
+        if (r->stream) (void)hipStreamSynchronize(r->stream);
+        r->stream = ns;
+    }
+}
 
 }  // namespace zk
 

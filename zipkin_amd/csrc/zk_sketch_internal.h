@@ -19,6 +19,15 @@ __host__ __device__ inline uint64_t sk_mix64(uint64_t z) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
+// the inverse of sk_mix64 (the splitmix64 finalizer is a bijection of 64-bit words)
+__host__ __device__ inline uint64_t sk_unmix64(uint64_t z) {
+    z = z ^ (z >> 31) ^ (z >> 62);
+    z *= 0x319642B2D24D8EC3ull;
+    z = z ^ (z >> 27) ^ (z >> 54);
+    z *= 0x96DE1B173F119089ull;
+    z = z ^ (z >> 30) ^ (z >> 60);
+    return z;
+}
 
 // Partition of (service, payload) items into service-contiguous order.
 struct PartitionPlan {
@@ -36,9 +45,11 @@ uint64_t partition_scratch_bytes(const PartitionPlan& p);
 // svc/payload: device arrays of n items. out: device array of n payloads (service-contiguous).
 // seg: device u64[S+1], seg[s]..seg[s+1] is service s's run in `out`. dropped: device u64 counter
 // (items with svc >= S are dropped and counted). scratch: partition_scratch_bytes.
+// hash: every payload is written as sk_mix64(payload ^ hash_seed) (the count-min's key hash,
+// computed once here instead of in both sketch passes; sk_unmix64 recovers the key)
 hipError_t launch_partition(const PartitionPlan& p, const uint32_t* svc, const uint64_t* payload, uint64_t n,
                             uint64_t* out, uint64_t* seg, unsigned long long* dropped, void* scratch,
-                            hipStream_t s);
+                            hipStream_t s, bool hash = false, uint64_t hash_seed = 0);
 // lists form: counts[w] items at offset w * stride (plan from partition_plan_lists)
 hipError_t launch_partition_lists(const PartitionPlan& p, const uint32_t* svc, const uint64_t* payload,
                                   uint64_t stride, const uint32_t* counts, uint64_t* out, uint64_t* seg,
@@ -62,7 +73,7 @@ struct KvArgs {
     uint32_t S, width, depth, wbits, cand;
     uint64_t seeds[kKvMaxDepth];
     uint32_t* cm;            // [S][depth][width] u32, accumulated across batches
-    const uint64_t* keys;    // service-contiguous batch keys
+    const uint64_t* keys;    // service-contiguous batch keys, hashed: sk_mix64(key ^ seeds[0])
     const uint64_t* seg;     // [S+1]
     const uint32_t* unit_base;  // [S+1]
     uint64_t unit_items;
