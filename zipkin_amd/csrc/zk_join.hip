@@ -375,6 +375,10 @@ __device__ __forceinline__ void load_window(const JoinArgs& a, uint64_t ws, Wind
 #ifndef ZK_K1_TOUCH
 #define ZK_K1_TOUCH 0
 #endif
+// ZK_K1_EARLY_COLS: four of the six late columns loaded a phase earlier (see load_early)
+#ifndef ZK_K1_EARLY_COLS
+#define ZK_K1_EARLY_COLS 1
+#endif
 // ZK_K1_NT_STORES: link stores with the non-temporal hint
 #ifndef ZK_K1_NT_STORES
 #define ZK_K1_NT_STORES 0
@@ -384,6 +388,29 @@ __device__ __forceinline__ void load_tid(const JoinArgs& a, uint64_t ws, Window&
     const uint64_t i = ws + 2 * threadIdx.x;
     ld2_u64(a.c.trace_id, i, n, w.tid);
     w.prev = a.c.trace_id[hot_index((i > 0 && i - 1 < n) ? i - 1 : 0)];
+}
+// ZK_K1_EARLY_COLS: the columns phase 6 no longer reads (spanId, first, last, service) are loaded
+// for the next window right after this window's merge barrier, into the same registers; only
+// parentId and flags stay at the top of the next iteration
+template <bool JOIN>
+__device__ __forceinline__ void load_early(const JoinArgs& a, uint64_t ws, Window& w) {
+    const uint64_t n = a.c.n;
+    const uint64_t i = ws + 2 * threadIdx.x;
+    ld2_u64(a.c.span_id, i, n, w.sid);
+    ld2_u64((const uint64_t*)a.c.first_ts, i, n, w.first);
+    ld2_u64((const uint64_t*)a.c.last_ts, i, n, w.last);
+    ld2_u32(a.c.service_id, i, n, w.svc);
+}
+template <bool JOIN>
+__device__ __forceinline__ void load_late(const JoinArgs& a, uint64_t ws, Window& w) {
+    const uint64_t n = a.c.n;
+    const uint64_t i = ws + 2 * threadIdx.x;
+    if constexpr (JOIN) {
+        ld2_u64(a.c.parent_id, i, n, w.pid);
+    } else {
+        w.pid[0] = w.pid[1] = 0ull;
+    }
+    ld2_u32(a.c.flags, i, n, w.flags);
 }
 template <bool JOIN>
 __device__ __forceinline__ void load_rest(const JoinArgs& a, uint64_t ws, Window& w) {
@@ -497,8 +524,11 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     bool seek_start = false;  // seek is known to be a trace start (uniform)
     Window cur, nxt;
     constexpr bool JOIN = (MODE & kModeJoin) != 0, EMIT = (MODE & kModeEmit) != 0;
+    constexpr bool EC = ZK_K1_EARLY_COLS && ZK_K1_LATE && ABL != 2;  // (the stream-only diagnostic has no phase 5)
 #if ZK_K1_LATE
     load_tid(a, ws, cur);
+    if constexpr (EC) load_early<JOIN>(a, ws, cur);
+    if constexpr (EC && ZK_K1_EARLY_COLS >= 2) load_late<JOIN>(a, ws, cur);
 #else
     load_window<JOIN>(a, ws, cur);
 #endif
@@ -514,7 +544,11 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     ZK_STAMP_DECL
     for (;;) {
 #if ZK_K1_LATE && !ZK_K1_REST_AFTER_BOUNDARIES
-        load_rest<JOIN>(a, ws, cur);
+        if constexpr (EC) {
+            if constexpr (ZK_K1_EARLY_COLS < 2) load_late<JOIN>(a, ws, cur);
+        } else {
+            load_rest<JOIN>(a, ws, cur);
+        }
 #endif
         const int wn = (int)((n - ws) < (uint64_t)TILE ? (n - ws) : (uint64_t)TILE);
         // ---- 1. trace boundaries of the window -------------------------------------------------
@@ -813,6 +847,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             }
         }
         ZK_PHASE_SYNC(4);
+        if constexpr (EC) load_early<JOIN>(a, done ? ws : next_ws, cur);  // see load_early
 
         // ---- 6. filter(isValid), join on (parentId, traceId), (cell, duration) links ----------
         uint64_t r_link[2], r_item[2];
@@ -923,6 +958,8 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             ++nl;
         }
         ZK_STAMP(5);
+        // ZK_K1_EARLY_COLS >= 2: parentId and flags of the next window, now that phase 6 is done with them
+        if constexpr (EC && ZK_K1_EARLY_COLS >= 2) load_late<JOIN>(a, done ? ws : next_ws, cur);
         // ---- 7. append the window's links (and sketch items) to this workgroup's lists ----------
         // one exclusive scan for both counts: links in bits 0..15, items in 16..31 (<= 512 each)
         // per-wave counts and lane offsets from ballots (nl, ni are 0..2: two bits each)
