@@ -216,32 +216,15 @@ __device__ __forceinline__ bool slot_valid(uint32_t w) { return ((w >> kSlotB) &
 #define ZK_K1_HOTREAD 0
 #endif
 __device__ __forceinline__ uint64_t hot_index(uint64_t i) { return ZK_K1_HOTREAD ? (i & 0xFFFEull) : i; }
-// ZK_K1_NT_LOADS: the column loads carry the non-temporal hint (streamed once; only the re-read
-// tail of a window would hit L2 again)
-#ifndef ZK_K1_NT_LOADS
-#define ZK_K1_NT_LOADS 0
-#endif
 __device__ __forceinline__ void ld2_u64(const uint64_t* __restrict__ p, uint64_t i, uint64_t lim, uint64_t v[2]) {
-    const ulonglong2* q = reinterpret_cast<const ulonglong2*>(p + hot_index(i < lim ? i : 0));
-#if ZK_K1_NT_LOADS
-    v[0] = __builtin_nontemporal_load(&q->x);
-    v[1] = __builtin_nontemporal_load(&q->y);
-#else
-    const ulonglong2 x = *q;
+    const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(p + hot_index(i < lim ? i : 0));
     v[0] = x.x;
     v[1] = x.y;
-#endif
 }
 __device__ __forceinline__ void ld2_u32(const uint32_t* __restrict__ p, uint64_t i, uint64_t lim, uint32_t v[2]) {
-    const uint2* q = reinterpret_cast<const uint2*>(p + hot_index(i < lim ? i : 0));
-#if ZK_K1_NT_LOADS
-    v[0] = __builtin_nontemporal_load(&q->x);
-    v[1] = __builtin_nontemporal_load(&q->y);
-#else
-    const uint2 x = *q;
+    const uint2 x = *reinterpret_cast<const uint2*>(p + hot_index(i < lim ? i : 0));
     v[0] = x.x;
     v[1] = x.y;
-#endif
 }
 
 // K1 stat counters: the per-thread 16-bit pack (StatPack) is folded into the workgroup's u32 LDS
@@ -349,12 +332,6 @@ __device__ __forceinline__ void load_window(const JoinArgs& a, uint64_t ws, Wind
 #ifndef ZK_K1_LATE
 #define ZK_K1_LATE 1
 #endif
-// ZK_K1_REST_AFTER_BOUNDARIES: issue a window's five late columns after its boundary ballots, so the
-// boundary phase's wait for the prefetched traceIds is not also a wait for the link stores that the
-// previous window issued after that prefetch (vmcnt counts loads and stores in one in-order queue)
-#ifndef ZK_K1_REST_AFTER_BOUNDARIES
-#define ZK_K1_REST_AFTER_BOUNDARIES 0
-#endif
 // ZK_K1_EARLY_BALLOT: take the next window's boundary ballots at the end of this window, before its
 // link stores (see the loop)
 #ifndef ZK_K1_EARLY_BALLOT
@@ -371,17 +348,9 @@ __device__ __forceinline__ void load_window(const JoinArgs& a, uint64_t ws, Wind
 #ifndef ZK_K1_FAST_SCAN
 #define ZK_K1_FAST_SCAN 1
 #endif
-// ZK_K1_TOUCH: L2 prefetch of the next window's late columns from phase 3 (see there)
-#ifndef ZK_K1_TOUCH
-#define ZK_K1_TOUCH 0
-#endif
 // ZK_K1_EARLY_COLS: four of the six late columns loaded a phase earlier (see load_early)
 #ifndef ZK_K1_EARLY_COLS
 #define ZK_K1_EARLY_COLS 1
-#endif
-// ZK_K1_NT_STORES: link stores with the non-temporal hint
-#ifndef ZK_K1_NT_STORES
-#define ZK_K1_NT_STORES 0
 #endif
 __device__ __forceinline__ void load_tid(const JoinArgs& a, uint64_t ws, Window& w) {
     const uint64_t n = a.c.n;
@@ -512,11 +481,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     if (tid == 0) s_cursor = 0ull;
     for (uint32_t x = tid; x < a.nb; x += WG) s_hist[x] = 0u;
     constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
-#if ZK_K1_TOUCH
-    constexpr int kTouchLines = 160;  // 4 x 32 lines of 8-byte columns + 2 x 16 of 4-byte ones per window
-    static_assert(TILE == 512 && WG >= kTouchLines, "touch geometry");
-    uint32_t touch = 0u;
-#endif
     uint32_t r_clear[2] = {kNoSlot, kNoSlot};  // hash slots this thread's leaders of the last window hold
 
     uint64_t ws = R0;         // window start (even)
@@ -543,7 +507,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     }
     ZK_STAMP_DECL
     for (;;) {
-#if ZK_K1_LATE && !ZK_K1_REST_AFTER_BOUNDARIES
+#if ZK_K1_LATE
         if constexpr (EC) {
             if constexpr (ZK_K1_EARLY_COLS < 2) load_late<JOIN>(a, ws, cur);
         } else {
@@ -556,9 +520,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             window_ballots(cur, ws, wn, &m_ev, &m_od);
             if (lane == 0) *reinterpret_cast<ulonglong2*>(&s_mask[2 * wave]) = make_ulonglong2(m_ev, m_od);
         }
-#if ZK_K1_LATE && ZK_K1_REST_AFTER_BOUNDARIES
-        load_rest<JOIN>(a, ws, cur);
-#endif
         ZK_PHASE_SYNC(0);
         // ---- 2. which records are ours, where the next window starts (uniform) ----------------
         const int lo_j = (int)(seek - ws);
@@ -721,33 +682,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             }
 #endif
         }
-#if ZK_K1_TOUCH
-        // pull the next window's five late columns into L2 now (one 4-byte load per 128-byte line,
-        // right after this window's own late columns were waited for): the next window's late
-        // loads then hit L2, and the HBM round trip runs during phases 3-6 instead of stalling
-        // the next window's staging; the value is consumed after the phase-7 wait (below)
-        if (!done && tid < kTouchLines) {
-            const uint64_t nws = next_ws;
-            const int t = tid;
-            const uint8_t* p;
-            uint64_t off, lim;
-            if (t < 128) {
-                const int c = t >> 5;  // span_id, parent_id, first_ts, last_ts
-                p = (const uint8_t*)(c == 0 ? (const void*)a.c.span_id
-                                     : c == 1 ? (const void*)a.c.parent_id
-                                     : c == 2 ? (const void*)a.c.first_ts
-                                              : (const void*)a.c.last_ts);
-                off = nws * 8 + (uint64_t)(t & 31) * 128;
-                lim = n * 8;
-            } else {
-                const int c = (t - 128) >> 4;  // service_id, flags
-                p = (const uint8_t*)(c == 0 ? (const void*)a.c.service_id : (const void*)a.c.flags);
-                off = nws * 4 + (uint64_t)((t - 128) & 15) * 128;
-                lim = n * 4;
-            }
-            if (off + 4 <= lim) touch ^= *reinterpret_cast<const uint32_t*>(p + (off & ~3ull));
-        }
-#endif
         ZK_PHASE_SYNC(2);  // (the hash table is empty here: cleared once, then by its leaders)
 
         // ---- 4. groupBy((id, traceId)): the first fragment to claim a slot leads --------------
@@ -1005,10 +939,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             window_ballots(nxt, nws, (int)((n - nws) < (uint64_t)TILE ? (n - nws) : (uint64_t)TILE), &n_ev, &n_od);
             if (lane == 0) *reinterpret_cast<ulonglong2*>(&s_mask[2 * wave]) = make_ulonglong2(n_ev, n_od);
         }
-#if ZK_K1_TOUCH
-        asm volatile("" ::"v"(touch));  // the touch loads are waited for here, with the traceIds
-        touch = 0u;
-#endif
         if constexpr (ABL == 0 && JOIN) {
             // exactly two stores per thread on every path (absent links go to the list's trash
             // slot), so the loop-end wait for the prefetched window can count them: vmcnt(2)
@@ -1021,11 +951,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 const v2u_t lv = {(unsigned int)r_link[e], (unsigned int)(r_link[e] >> 32)};
                 __builtin_amdgcn_raw_buffer_store_b64(lv, out_rsrc, v ? pos * 8u : 0x7FFFFFF8u, 0, 0);
 #else
-#if ZK_K1_NT_STORES
-                __builtin_nontemporal_store(r_link[e], &out[v ? (uint64_t)pos : trash + (ZK_K1_TRASH_SPREAD ? e : 0)]);
-#else
                 out[v ? (uint64_t)pos : trash + (ZK_K1_TRASH_SPREAD ? e : 0)] = r_link[e];
-#endif
 #endif
                 pos += v ? 1u : 0u;
             }
