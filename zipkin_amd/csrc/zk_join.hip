@@ -188,6 +188,13 @@ constexpr int kSlotA = 12;
 constexpr int kSlotB = 16;
 constexpr uint32_t kSlotP1 = 1u << 20;
 constexpr uint32_t kSlotP0 = 1u << 21;
+// ZK_K1_SEG_IN_SLOT: bits 22..30 of the slot word hold the leader's trace segment (< 512), so a probe
+// compares the segment from the word it already read and loads the occupant's spanId only on a
+// segment match (no s_seg array: one LDS round trip less per parent probe)
+#ifndef ZK_K1_SEG_IN_SLOT
+#define ZK_K1_SEG_IN_SLOT 1
+#endif
+constexpr int kSlotSegShift = 22;
 
 // own bits of a fragment and the "seen exactly once" core annotations it may promote to ">= 2"
 __device__ __forceinline__ uint32_t frag_bits(uint32_t f, uint32_t* once) {
@@ -427,7 +434,10 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     __shared__ __align__(16) long long s_last[TILE];
     __shared__ __align__(16) uint64_t s_pid[TILE];
     __shared__ __align__(16) uint32_t s_svck[TILE];
+#if ZK_K1_SORTJOIN || !ZK_K1_SEG_IN_SLOT
     __shared__ __align__(16) uint16_t s_seg[TILE];
+#endif
+    static_assert(!ZK_K1_SEG_IN_SLOT || TILE <= 512, "the segment field of the slot word is 9 bits");
     __shared__ __align__(16) uint32_t s_ht[H];
 #if ZK_K1_SORTJOIN
     __shared__ __align__(16) uint32_t s_bits[TILE];  // merged seen-once/twice + parent bits per leader
@@ -670,7 +680,9 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             *reinterpret_cast<ulonglong2*>(&s_last[j0]) = make_ulonglong2(v_last[0], v_last[1]);
             *reinterpret_cast<ulonglong2*>(&s_pid[j0]) = make_ulonglong2(v_pid[0], v_pid[1]);
             *reinterpret_cast<uint2*>(&s_svck[j0]) = make_uint2(r_svck[0], r_svck[1]);
+#if ZK_K1_SORTJOIN || !ZK_K1_SEG_IN_SLOT
             *reinterpret_cast<uint32_t*>(&s_seg[j0]) = ((uint32_t)r_seg[0] & 0xFFFFu) | ((uint32_t)r_seg[1] << 16);
+#endif
 #if ZK_K1_SORTJOIN
             {
                 const int p0 = first_ge(m_ev, m_od, 2 * lane + 1), p1 = first_ge(m_ev, m_od, 2 * lane + 2);
@@ -717,6 +729,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 r_slot[e] = slot_hash(cur.sid[e], (uint32_t)(r_seg[e] & 0xFFFF)) & (H - 1);
                 uint32_t once;
                 word[e] = (uint32_t)(2 * tid + e + 1) | frag_bits(cur.flags[e], &once);
+                if (ZK_K1_SEG_IN_SLOT) word[e] |= ((uint32_t)r_seg[e] & 0x1FFu) << kSlotSegShift;
             }
             while (act[0] || act[1]) {
                 uint32_t old[2];
@@ -735,8 +748,13 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 uint16_t oseg[2];
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
+#if ZK_K1_SEG_IN_SLOT
+                    oseg[e] = (uint16_t)((old[e] >> kSlotSegShift) & 0x1FFu);
+                    osid[e] = (act[e] && oseg[e] == (uint16_t)r_seg[e]) ? s_sid[o[e]] : ~cur.sid[e];
+#else
                     osid[e] = act[e] ? s_sid[o[e]] : 0ull;
                     oseg[e] = act[e] ? s_seg[o[e]] : (uint16_t)0;
+#endif
                 }
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
@@ -864,7 +882,11 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 const uint32_t o = s_ht[slot];
                 if (o == 0u) break;
                 const int oi = (int)(o & kSlotIdx) - 1;
+#if ZK_K1_SEG_IN_SLOT
+                if (((o >> kSlotSegShift) & 0x1FFu) == seg && s_sid[oi] == pL) {
+#else
                 if (s_sid[oi] == pL && s_seg[oi] == seg) {
+#endif
                     pw = o;
                     break;
                 }
