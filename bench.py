@@ -46,10 +46,12 @@ def parse():
     ap.add_argument("--verify", type=int, default=0,
                     help="1: ZK_BATCH_VERIFY_TRACES on every step (exact device check of the clustering promise)")
     ap.add_argument("--ablate", type=int, default=0, help="diagnostic: 1 = K1 without link emission (not a valid result)")
-    ap.add_argument("--pipeline", type=int, default=1,
-                    help="batches in flight behind the one being joined: 1 (default) = two table/stream "
+    ap.add_argument("--pipeline", type=int, default=None,
+                    help="batches in flight behind the one being joined: 1 = two table/stream "
                          "sets (batch k's join overlaps batch k-1's tail), 2 = three, 0 = one set, serial steps "
-                         "(c2 takes any depth, c4/c5 use two sets when > 0)")
+                         "(c2 takes any depth, c4/c5 use two sets when > 0). Default: 1 for c2/c5, 0 for c4, whose "
+                         "partition scatter and candidate pass each fill the LDS of a CU, so two overlapped sets only "
+                         "contend (12.06 ms serial vs 14.13 ms pipelined, profiles/r02/ab_c4_pipeline.txt)")
     ap.add_argument("--overlap", default="full", choices=("tail", "full"),
                     help="c2 pipelined steps: full (default) = no ordering between the table sets: batch k's "
                          "join shares the GPU with batch k-1's K2/K3 (faster steps; K1's launch events then also "
@@ -65,7 +67,10 @@ def parse():
     ap.add_argument("--fragments", type=int, default=20_000_000, help="ingest: stored fragments per step")
     ap.add_argument("--items", type=int, default=1_000_000_000,
                     help="c4: binary annotations per step (BASELINE configs[3]: 1e9, 12 GB in HBM)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.pipeline is None:
+        a.pipeline = 0 if a.workload == "c4" else 1
+    return a
 
 
 def main():
