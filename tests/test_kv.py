@@ -125,6 +125,8 @@ def _assert_same(k, o, kk):
     (3, 1000, 64, 2, 8),
     (57, 50_000, 0, 4, 64),
     (500, 300_000, 0, 4, 16),
+    (1022, 200_000, 0, 2, 32),  # largest S whose line-scatter carry fits the LDS
+    (1024, 200_000, 0, 2, 32),  # one past it: item-by-item scatter (the line kernel would not launch)
     (2000, 200_000, 0, 3, 256),
 ])
 def test_gpu_topk_bit_exact_vs_oracle(gpu, S, n, width, depth, cand):

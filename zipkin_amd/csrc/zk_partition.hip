@@ -100,7 +100,12 @@ constexpr uint32_t kLineMaxS = 1024;
 #ifndef ZK_PART_WG
 #define ZK_PART_WG 1024  // line-scatter workgroup (512 threads x 4 items: 2.38 -> 1.76 ms on C4)
 #endif
-constexpr int kLineItems = 8;  // items per 64-byte line
+// Items per output line: 8 = 64 bytes. 128-byte lines (7168-item chunks, so that the S x 128 B carry
+// fits) measured 8.99-9.03 ms against 6.93-7.00 ms for the C4 partition (profiles/r02/ab_part_lines.txt).
+constexpr int kLineItems = 8;
+constexpr uint64_t kLdsBytes = 160 * 1024;
+// LDS of one line-scatter workgroup: the fixed arrays below plus the [S][kLineItems] carry
+constexpr uint64_t part_lines_static(int U, int WG) { return 4ull * kLineMaxS * 4 + (uint64_t)WG * U * 10 + 32 * 4; }
 template <int U, int WG>
 __global__ __launch_bounds__(WG) void k_part_scatter_lines(const uint32_t* __restrict__ svc,
                                                             const uint64_t* __restrict__ payload, uint64_t n,
@@ -308,7 +313,9 @@ hipError_t partition_impl(const PartitionPlan& p, const uint32_t* svc, const uin
     if (e != hipSuccess) return e;
     e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, hist, offs, (int)m, s);
     if (e != hipSuccess) return e;
-    if (p.S <= kLineMaxS)
+    // whole lines while the carry fits the LDS (S <= 1022 at 8192-item chunks; S = 1024 faulted
+    // before this check), else item by item
+    if (p.S <= kLineMaxS && part_lines_static(ZK_PART_U, ZK_PART_WG) + (uint64_t)p.S * kLineItems * 8 <= kLdsBytes)
         hipLaunchKernelGGL((k_part_scatter_lines<ZK_PART_U, ZK_PART_WG>), dim3(p.grid), dim3(ZK_PART_WG),
                            (size_t)p.S * kLineItems * 8, s,
                            svc, payload, n, p.per_wg, counts, p.S, p.grid, offs, out, hash, hash_seed);
