@@ -2,7 +2,7 @@
 """Build an A/B variant of libzkagg: the sources of a git revision (default: the working tree) with
 optional -D defines, into zipkin_amd/libzkagg_<name>.so (run with ZKAGG_LIB=... or tools/ab.sh).
 
-  python tools/build_variant.py NAME [--rev REV] [-D DEFINE ...]
+  python tools/build_variant.py NAME [--rev REV] [-D DEFINE ...] [--flag=COMPILER_FLAG ...]
 """
 import argparse
 import shutil
@@ -22,6 +22,7 @@ def main():
     ap.add_argument("name")
     ap.add_argument("--rev", default=None)
     ap.add_argument("-D", action="append", default=[])
+    ap.add_argument("--flag", action="append", default=[], help="extra compiler flag (e.g. --flag=-mllvm=-x)")
     a = ap.parse_args()
     tmp = Path(tempfile.mkdtemp(prefix="zkvar_"))
     try:
@@ -40,7 +41,8 @@ def main():
         csrc = tmp / "zipkin_amd" / "csrc"
         srcs = [s for s in zb.SOURCES if (csrc / s).exists()]
         flags = [f"--offload-arch={zb.ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result",
-                 "-Wno-unused-value", f"-I{tmp / 'include'}"] + [f"-D{d}" for d in a.D]
+                 "-Wno-unused-value", f"-I{tmp / 'include'}"] + [f"-D{d}" for d in a.D] + [
+                     x for f in a.flag for x in (f.split("=", 1) if f.startswith("-mllvm=") else [f])]
 
         def cc(src):
             obj = tmp / (src + ".o")
