@@ -28,7 +28,15 @@ constexpr int kKvWG = ZK_KV_WG;
 constexpr uint32_t kSetCap = 2048;  // 2^11: RowHash.set is 11 bits  // LDS hash-set slots (load <= 0.5)
 constexpr uint32_t kSortCap = 1024; // compaction sort buffer
 constexpr uint32_t kRound = 512;  // merge: entries offered between compaction checks (<= kSortCap / 2)
-constexpr int kPrefetch = 8;        // candidate rounds of keys in flight per thread
+#ifndef ZK_KV_PREFETCH
+#define ZK_KV_PREFETCH 4  // 8 without ZK_KV_CAND_PIPE (two 16-key buffers: 179 VGPRs, 5.6 ms on C4)
+#endif
+constexpr int kPrefetch = ZK_KV_PREFETCH;  // candidate rounds of keys in flight per thread
+#ifndef ZK_KV_CAND_PIPE
+// candidates: the next block's keys load while this block is estimated and inserted (C4: 3.46 ->
+// 3.22-3.26 ms, profiles/r02/ab_kv_cand_pipe.txt)
+#define ZK_KV_CAND_PIPE 1
+#endif
 constexpr uint64_t kEmptyKey = ~0ull;
 
 __device__ __forceinline__ bool beats(uint32_t e1, uint64_t k1, uint32_t e2, uint64_t k2) {
@@ -295,25 +303,28 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
     unit_range(a, s, u, &lo, &hi);
     load_cm(cm, a, s);
     ts_init(t);  // contains the barrier that publishes cm
-    // Blocks of J = 16 keys per thread (4096 per workgroup). All of a block's loads are issued
-    // together and nothing is carried across the loop's back edge (a register ring of prefetched
-    // keys makes the compiler copy it at the loop head, waiting for every load in flight). Per
-    // block: every key is estimated and filtered against the current threshold and the set
-    // (read-only probes: under a skewed key distribution most survivors are already in the set);
+    // Blocks of J = 8 keys per thread (4096 per workgroup), in two alternating key buffers: one
+    // block's loads are in flight while the other is processed (a register ring carried across the
+    // back edge instead makes the compiler copy it at the loop head, waiting for every load in
+    // flight). Per block: every key is estimated and filtered against the current threshold and the
+    // set (read-only probes: under a skewed key distribution most survivors are already in the set);
     // the survivors are counted (B1) and, when they fit the sort buffer, inserted at once (B2) --
-    // two barriers per 4096 keys instead of one per 512. A block with too many survivors (the
-    // start of a unit) is inserted 256 at a time with a compaction check in between.
+    // two barriers per block instead of one per workgroup of keys. A block with too many survivors
+    // (the start of a unit) is inserted one workgroup of keys at a time with a compaction check in
+    // between.
     constexpr int J = 2 * kPrefetch;
+    constexpr uint64_t BS = (uint64_t)kKvWG * J;  // keys per block
     uint32_t parity = 0;
     if (threadIdx.x == 0) t.pending[0] = t.pending[1] = 0u;
     __syncthreads();
-    for (uint64_t b = lo; b < hi; b += (uint64_t)kKvWG * J) {
-        uint64_t kq[J];
+    auto load_block = [&](uint64_t (&kq)[J], uint64_t b) {
 #pragma unroll
         for (int j = 0; j < J; ++j) {
             const uint64_t i = b + (uint64_t)j * kKvWG + threadIdx.x;
             kq[j] = a.keys[i < hi ? i : lo];
         }
+    };
+    auto run_block = [&](const uint64_t (&kq)[J], uint64_t b) {
         // estimates unconditionally (clamped keys past the end are harmless): a load whose only
         // uses sit in a conditional block is sunk into it, and then every key waits for HBM
         uint32_t est[J], slot[J];
@@ -353,7 +364,26 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
             }
         }
         parity ^= 1u;
+    };
+#if ZK_KV_CAND_PIPE
+    // two key buffers, alternating: the next block's loads are in flight while this one is
+    // estimated and inserted (each buffer is loaded and consumed in fixed places, so nothing is
+    // copied across the back edge)
+    uint64_t ka[J], kb[J];
+    load_block(ka, lo);
+    for (uint64_t b = lo; b < hi; b += 2 * BS) {
+        load_block(kb, b + BS);
+        run_block(ka, b);
+        load_block(ka, b + 2 * BS);
+        if (b + BS < hi) run_block(kb, b + BS);
     }
+#else
+    for (uint64_t b = lo; b < hi; b += BS) {
+        uint64_t kq[J];
+        load_block(kq, b);
+        run_block(kq, b);
+    }
+#endif
     const uint32_t n = ts_sort(t, a.seeds[0]);
     uint64_t* ok = a.unit_key + (uint64_t)u * a.cand;
     uint32_t* oe = a.unit_est + (uint64_t)u * a.cand;
