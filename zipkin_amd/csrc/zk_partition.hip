@@ -17,6 +17,10 @@ namespace {
 
 constexpr int kPartWG = 256;
 constexpr int kPartU = 4;  // items per thread per iteration (loads issued before the LDS atomics)
+#ifndef ZK_PART_HIST_PIPE
+// histogram: two alternating load buffers (C4 partition 6.95 -> 6.77 ms, profiles/r02/ab_part_hist_pipe.txt)
+#define ZK_PART_HIST_PIPE 1
+#endif
 
 // range of workgroup w: a slice of one flat array (counts == nullptr) or list w of the lists form
 __device__ __forceinline__ void part_range(uint64_t n, uint64_t per, const uint32_t* counts, uint64_t* lo,
@@ -39,13 +43,15 @@ __global__ __launch_bounds__(kPartWG) void k_part_hist(const uint32_t* __restric
     uint64_t lo, hi;
     part_range(n, per, counts, &lo, &hi);
     uint32_t bad = 0;
-    for (uint64_t b = lo; b < hi; b += (uint64_t)kPartWG * kPartU) {
-        uint32_t v[kPartU];
+    constexpr uint64_t BS = (uint64_t)kPartWG * kPartU;
+    auto load = [&](uint32_t (&v)[kPartU], uint64_t b) {
 #pragma unroll
         for (int e = 0; e < kPartU; ++e) {
             const uint64_t i = b + (uint64_t)e * kPartWG + threadIdx.x;
             v[e] = i < hi ? svc[i] : 0xFFFFFFFFu;
         }
+    };
+    auto count = [&](const uint32_t (&v)[kPartU], uint64_t b) {
 #pragma unroll
         for (int e = 0; e < kPartU; ++e) {
             const uint64_t i = b + (uint64_t)e * kPartWG + threadIdx.x;
@@ -54,7 +60,24 @@ __global__ __launch_bounds__(kPartWG) void k_part_hist(const uint32_t* __restric
             else if (i < hi)
                 ++bad;
         }
+    };
+#if ZK_PART_HIST_PIPE
+    // two alternating buffers: one block's loads are in flight while the other is counted
+    uint32_t va[kPartU], vb[kPartU];
+    load(va, lo);
+    for (uint64_t b = lo; b < hi; b += 2 * BS) {
+        load(vb, b + BS);
+        count(va, b);
+        load(va, b + 2 * BS);
+        count(vb, b + BS);  // past hi: every entry is the 0xFFFFFFFF sentinel and i >= hi
     }
+#else
+    for (uint64_t b = lo; b < hi; b += BS) {
+        uint32_t v[kPartU];
+        load(v, b);
+        count(v, b);
+    }
+#endif
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < S; i += kPartWG) hist[(uint64_t)i * grid + blockIdx.x] = h[i];
     if (bad) atomicAdd(dropped, (unsigned long long)bad);
