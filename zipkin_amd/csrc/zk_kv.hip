@@ -32,6 +32,11 @@ constexpr uint32_t kRound = 512;  // merge: entries offered between compaction c
 #define ZK_KV_PREFETCH 4  // 8 without ZK_KV_CAND_PIPE (two 16-key buffers: 179 VGPRs, 5.6 ms on C4)
 #endif
 constexpr int kPrefetch = ZK_KV_PREFETCH;  // candidate rounds of keys in flight per thread
+#ifndef ZK_KV_SKETCH_PIPE
+// sketch: two alternating 4-key buffers (C4 sketch 2.00 -> 1.96-1.97 ms; the pass is LDS-atomic-bound,
+// profiles/r02/ab_kv_sketch_pipe.txt)
+#define ZK_KV_SKETCH_PIPE 1
+#endif
 #ifndef ZK_KV_CAND_PIPE
 // candidates: the next block's keys load while this block is estimated and inserted (C4: 3.46 ->
 // 3.22-3.26 ms, profiles/r02/ab_kv_cand_pipe.txt)
@@ -260,14 +265,20 @@ __global__ __launch_bounds__(kKvWG) void k_kv_sketch(KvArgs a) {
     const uint32_t cells = a.depth * a.width;
     for (uint32_t x = threadIdx.x; x < cells; x += kKvWG) cm[x] = 0u;
     __syncthreads();
+#if ZK_KV_SKETCH_PIPE
+    constexpr int U = 4;  // keys per thread per buffer; two buffers alternate
+#else
     constexpr int U = 8;  // keys per thread in flight
-    for (uint64_t b = lo; b < hi; b += (uint64_t)kKvWG * U) {
-        uint64_t k[U];
+#endif
+    constexpr uint64_t BS = (uint64_t)kKvWG * U;
+    auto load = [&](uint64_t (&k)[U], uint64_t b) {
 #pragma unroll
         for (int e = 0; e < U; ++e) {
             const uint64_t i = b + (uint64_t)e * kKvWG + threadIdx.x;
             k[e] = a.keys[i < hi ? i : lo];
         }
+    };
+    auto add = [&](const uint64_t (&k)[U], uint64_t b) {
         // row hashes unconditionally, so the loads are not sunk into the conditional (see candidates)
         RowHash rh[U];
 #pragma unroll
@@ -277,7 +288,23 @@ __global__ __launch_bounds__(kKvWG) void k_kv_sketch(KvArgs a) {
             if (b + (uint64_t)e * kKvWG + threadIdx.x < hi)
                 for (uint32_t r = 0; r < a.depth; ++r) atomicAdd(&cm[r * a.width + rh[e].next()], 1u);
         }
+    };
+#if ZK_KV_SKETCH_PIPE
+    uint64_t ka[U], kb[U];
+    load(ka, lo);
+    for (uint64_t b = lo; b < hi; b += 2 * BS) {
+        load(kb, b + BS);
+        add(ka, b);
+        load(ka, b + 2 * BS);
+        add(kb, b + BS);  // past hi: every key is masked
     }
+#else
+    for (uint64_t b = lo; b < hi; b += BS) {
+        uint64_t k[U];
+        load(k, b);
+        add(k, b);
+    }
+#endif
     __syncthreads();
     uint32_t* g = a.cm + (uint64_t)s * cells;
     for (uint32_t x = threadIdx.x; x < cells; x += kKvWG) {
