@@ -49,6 +49,11 @@ __device__ __forceinline__ uint32_t bytewise_max(uint32_t a, uint32_t b) {
     return r;
 }
 
+// ZK_RT_SKETCH_PIPE: two alternating load buffers, as in the KV passes. C5 step within noise
+// (pipelined 1.43-1.46 vs 1.44-1.47 ms, serial equal: profiles/r02/ab_rt_sketch_pipe.txt), so off.
+#ifndef ZK_RT_SKETCH_PIPE
+#define ZK_RT_SKETCH_PIPE 0
+#endif
 __global__ __launch_bounds__(kRtWG) void k_rt_sketch(RtArgs a) {
     extern __shared__ uint32_t lds[];
     const uint32_t R = 1u << a.p;        // registers per service
@@ -64,13 +69,15 @@ __global__ __launch_bounds__(kRtWG) void k_rt_sketch(RtArgs a) {
     for (uint32_t x = threadIdx.x; x < a.nbins; x += kRtWG) s_bin[x] = 0u;
     __syncthreads();
     constexpr int U = 4;
-    for (uint64_t b = lo; b < hi; b += (uint64_t)kRtWG * U) {
-        uint64_t v[U];
+    constexpr uint64_t BS = (uint64_t)kRtWG * U;
+    auto load = [&](uint64_t (&v)[U], uint64_t b) {
 #pragma unroll
         for (int e = 0; e < U; ++e) {
             const uint64_t i = b + (uint64_t)e * kRtWG + threadIdx.x;
             v[e] = a.items[i < hi ? i : lo];
         }
+    };
+    auto add = [&](const uint64_t (&v)[U], uint64_t b) {
 #pragma unroll
         for (int e = 0; e < U; ++e) {
             if (b + (uint64_t)e * kRtWG + threadIdx.x >= hi) continue;
@@ -80,7 +87,24 @@ __global__ __launch_bounds__(kRtWG) void k_rt_sketch(RtArgs a) {
             max_byte(&s_reg[idx >> 2], 8u * (idx & 3u), rho);
             atomicAdd(&s_bin[rt_bin(d, a.m)], 1u);
         }
+    };
+#if ZK_RT_SKETCH_PIPE
+    // two alternating buffers: one block's loads are in flight while the other is added
+    uint64_t va[U], vb[U];
+    load(va, lo);
+    for (uint64_t b = lo; b < hi; b += 2 * BS) {
+        load(vb, b + BS);
+        add(va, b);
+        load(va, b + 2 * BS);
+        add(vb, b + BS);  // past hi: every item is masked
     }
+#else
+    for (uint64_t b = lo; b < hi; b += BS) {
+        uint64_t v[U];
+        load(v, b);
+        add(v, b);
+    }
+#endif
     __syncthreads();
     uint32_t* g_reg = (uint32_t*)(a.regs + (uint64_t)s * R);
     for (uint32_t x = threadIdx.x; x < (R >> 2); x += kRtWG) {
