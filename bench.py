@@ -58,6 +58,11 @@ def parse():
                          "cover the K2/K3 work it shares the chip with, see roofline.isolated_*); tail = batch k's "
                          "join starts once batch k-1's reduce is done, so only spill, [all-reduce,] finalize, "
                          "status check and reset overlap the next join and every K1 launch runs alone")
+    ap.add_argument("--order", default="clustered", choices=("clustered", "shuffled"),
+                    help="c2: clustered (default) = the batch as TraceGen emits it, trace-clustered like "
+                         "Cassandra row-per-trace reads, accumulated with ZK_BATCH_TRACE_CLUSTERED; shuffled = "
+                         "the same records in a random permutation (the reference's shuffles accept any order, "
+                         "ZipkinAggregateJob.scala:21-22,28-33): every step runs the device clustering pass first")
     ap.add_argument("--workload", default="c2", choices=("c1", "c2", "c4", "c5", "ingest"),
                     help="c2 (default, the headline): dependency path; c1: the reference's CPU config "
                          "(10k tracegen traces, 20 services) on the GPU and the CPU baseline; "
@@ -126,6 +131,18 @@ def main():
                         rank=rank, world=world)
     cols = DeviceColumns(a.records, device=f"cuda:{local}")
     n, ntr = ctx.tracegen_device(p, cols)
+    shuffled = a.order == "shuffled"
+    clustered_cols = cols
+    if shuffled:
+        # the same records in a random order, permuted once before the timed region
+        g = torch.Generator(device=dev)
+        g.manual_seed(a.seed + 1000 * rank)
+        perm = torch.randperm(n, device=dev, generator=g)
+        sc = DeviceColumns(n, device=f"cuda:{local}")
+        for k in ("trace_id", "span_id", "parent_id", "first_ts", "last_ts", "service_id", "flags"):
+            torch.index_select(getattr(cols, k)[:n], 0, perm, out=getattr(sc, k))
+        del perm
+        cols = sc
     out = {
         "m0": torch.empty(cells, dtype=torch.int64, device=dev),
         "m1": torch.empty(cells, dtype=torch.float64, device=dev),
@@ -138,7 +155,7 @@ def main():
     def step_serial():
         ctx.reset()
         # device-generated batches are trace-clustered by construction (zk_tracegen_device)
-        ctx.accumulate(cols, clustered=True, verify=a.verify)
+        ctx.accumulate(cols, clustered=not shuffled, verify=a.verify)
         if dist is not None:
             ctx.partial()  # fold the counters into the table tail (same stream)
             allreduce_table(table)  # exact u64-limb + counter SUM over xGMI (RCCL): shards are disjoint traces
@@ -177,7 +194,7 @@ def main():
             c.reset()
             if a.overlap == "tail" and state.get("reduced") is not None:
                 s.wait_event(state["reduced"])  # K1 after the previous batch's K2/K3
-            c.accumulate(cols, clustered=True, verify=a.verify)
+            c.accumulate(cols, clustered=not shuffled, verify=a.verify)
             if a.overlap == "tail":
                 ev = torch.cuda.Event()
                 ev.record(s)
@@ -199,7 +216,7 @@ def main():
     # pipelined steps so that the second set's buffers exist before the timed region
     # (at least ISOLATED + 1 serial steps: untimed, outside the timed region, so that the isolated K1
     # figure averages several warm launches whatever --warmup is)
-    ISOLATED = 4
+    ISOLATED = 8
     tmf = None
     for i in range(max(a.warmup, ISOLATED + 1)):
         step_serial()
@@ -241,10 +258,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     total_records = n * world
+    if dist is not None:  # the records every rank actually aggregated (shards differ in size)
+        t = torch.tensor([n], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        total_records = int(t.item())
     value = total_records * a.steps / elapsed
     join_calls = tm1["join_calls"] - tm0["join_calls"]
     join_avg_ms = (tm1["join_ms_total"] - tm0["join_ms_total"]) / max(1, join_calls)
-    achieved = n * BYTES_PER_RECORD / (join_avg_ms * 1e-3) / 1e9
     st = ctx.stats()
     if pipeline:
         # both pipeline sets finalized the same batch: their outputs must agree bit for bit
@@ -255,8 +275,23 @@ def main():
             c2.close()
 
     cpu = parity = None
+    shuffled_parity = None
+    if shuffled:
+        # the whole shuffled batch must give the clustered batch's result bit for bit (every cell's
+        # m0..m4 and every counter): permutation invariance at full size
+        ref_out = {k: torch.empty_like(v) for k, v in out.items()}
+        with DepsContext(S, device=local, stream=stream.cuda_stream) as cref:
+            cref.accumulate(clustered_cols, clustered=True, verify=False, n=n)
+            cref.finalize(out_device=ref_out)
+            stc = cref.stats()
+        bad = [k for k in out if not torch.equal(out[k], ref_out[k])]
+        bad += [k for k, v in stc.items() if k != "spilled_traces" and st[k] != v]
+        if bad:
+            raise RuntimeError(f"shuffled batch differs from the clustered batch: {bad}")
+        shuffled_parity = {"result": "exact", "records": n,
+                           "checked": "m0..m4, present and all counters of the shuffled full batch == the clustered batch"}
     if rank == 0 and world == 1 and a.cpu_sample > 0:
-        cpu, parity = cpu_baseline(cols, min(a.cpu_sample, n), S, a.cpu_threads or usable_cpus(), dev)
+        cpu, parity = cpu_baseline(clustered_cols, min(a.cpu_sample, n), S, a.cpu_threads or usable_cpus(), dev)
 
     # PMC counters need their own rocprofv3 --pmc run (tools/pmc.sh), so the traffic figure is the
     # builder's measurement of the same kernel on the same workload, labelled with its source
@@ -286,9 +321,14 @@ def main():
             "dtype": "u64",
             "data": "synthetic (zipkin-tracegen-shaped, generated on device)",
             "config": {
-                "workload": "C2: 1e8 span records/GPU, 500 services, dependency link table + Moments",
+                "workload": "C2: 1e8 span records/GPU, 500 services, dependency link table + Moments"
+                            + (" (records in random order: device clustering pass in every step)" if shuffled else ""),
                 "records_per_gpu": n,
                 "traces_per_gpu": ntr,
+                "records_per_trace": round(n / max(1, ntr), 2),
+                "vs_configs_1": "BASELINE configs[1] names 100M spans / 5M traces (20 records per trace); TraceGen "
+                                "with integer maxDepth gives 15.2 (depth 5) or 24.1 (depth 6) records per trace, so "
+                                f"the batch holds {n:.3g} records in {ntr:.3g} whole traces (maxDepth {a.max_depth})",
                 "services": S,
                 "max_depth": a.max_depth,
                 "parallelism": f"traceId-hash shards x{world}" + (", RCCL all-reduce of the link table" if world > 1 else ""),
@@ -298,30 +338,39 @@ def main():
                            (f" ({a.pipeline + 1} table sets: batch k's join overlaps earlier batches' reduce, [all-reduce,] "
                             "finalize)") if pipeline else ""),
             },
+            # K1 (the dominant kernel) timed ALONE: HIP events on the ctx stream around each K1 launch
+            # of the serial steps (nothing else on the chip: no overlap with the other table set's
+            # K2/K3), averaged over `launches` warm launches -- the figure rocprofv3's serial kernel
+            # stats reproduce. The pipelined launches of the timed steps share the chip with the other
+            # set's reduce, so their event spans are not a kernel duration: detail.pipelined_k1_*.
             "roofline": {
                 "bound": "hbm",
                 "kernel": "k_span_join_stream",
-                "achieved": achieved,
+                "achieved": n * BYTES_PER_RECORD / (k1_isolated_ms * 1e-3) / 1e9,
                 "peak": PEAK_HBM_GBS,
                 "unit": "GB/s",
-                "frac": achieved / PEAK_HBM_GBS,
+                "frac": n * BYTES_PER_RECORD / (k1_isolated_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": n * BYTES_PER_RECORD,
-                "avg_launch_ms": join_avg_ms,
-                # K1 alone (serial warmup steps): with the pipeline, the timed launches share the
-                # chip with the other set's K2/K3/finalize, so avg_launch_ms above is longer
-                "isolated_avg_launch_ms": k1_isolated_ms,
-                "isolated_frac": (n * BYTES_PER_RECORD / (k1_isolated_ms * 1e-3) / 1e9 / PEAK_HBM_GBS
-                                  if k1_isolated_ms else None),
-                "isolated_launches": isolated_launches,
+                "bytes_per_record": BYTES_PER_RECORD,
+                "avg_launch_ms": k1_isolated_ms,
+                "launches": isolated_launches,
+                "timing": "HIP events on the ctx stream around each K1 launch of serial (non-overlapped) steps",
                 # the whole step's algorithmic bytes (K1's input) over the step time
                 "step_frac": n * BYTES_PER_RECORD / (elapsed / a.steps) / 1e9 / PEAK_HBM_GBS,
             },
             "cpu_baseline": cpu,
-            "parity": parity,
+            "parity": parity if not shuffled else {"prefix_vs_oracle": parity, "shuffled_vs_clustered": shuffled_parity},
             "detail": {
                 "event_ms_per_step": ev_ms / a.steps,
+                # K1 event spans inside the timed (pipelined) steps: they also cover the other table
+                # set's K2/K3 that share the chip with K1, so they are longer than the kernel
+                "pipelined_k1_event_ms": join_avg_ms,
+                "pipelined_k1_launches": join_calls,
+                "order": a.order,
+                "cluster_ms_avg": ((tm1["cluster_ms_total"] - tm0["cluster_ms_total"]) / max(1, join_calls)
+                                   if shuffled else 0.0),
                 "finalize_ms_last": tm1["finalize_ms"],
                 "reduce_avg_ms": (tm1["reduce_ms_total"] - tm0["reduce_ms_total"]) / max(1, join_calls),
                 "spill_ms_last": tm1["spill_ms"],
@@ -608,7 +657,7 @@ def bench_c5(a):
     est = rt.distinct_traces()
     q = [rt.quantiles(s, (0.5, 0.99)) for s in range(S)]
     query_ms = (time.perf_counter() - t0) * 1e3
-    achieved = n * 40 / (join_ms * 1e-3) / 1e9
+    achieved = n * 40 / (k1_isolated_ms * 1e-3) / 1e9  # K1 alone (serial launches), as in the c2 line
     print(json.dumps({
         "metric": "spans/sec into per-service HLL distinct traceIds + duration p50/p99 (BASELINE configs[4], 1 GPU)",
         "value": n * a.steps / wall, "unit": "spans/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
@@ -620,10 +669,10 @@ def bench_c5(a):
                            + (" (two sets: batch k's K1 overlaps batch k-1's partition + sketch)" if a.pipeline else "")},
         "roofline": {"bound": "hbm", "kernel": "k_span_join_stream<..., kModeEmit>", "achieved": achieved,
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
-                     "algorithmic_bytes_per_launch": n * 40, "avg_launch_ms": join_ms,
-                     "isolated_avg_launch_ms": k1_isolated_ms,
-                     "isolated_frac": n * 40 / (k1_isolated_ms * 1e-3) / 1e9 / PEAK_HBM_GBS},
+                     "algorithmic_bytes_per_launch": n * 40, "avg_launch_ms": k1_isolated_ms, "launches": 3,
+                     "timing": "HIP events on the ctx stream around each K1 launch of serial (non-overlapped) steps"},
         "detail": {"event_ms_per_step": ev_ms / a.steps, "query_ms_all_services": query_ms,
+                   "pipelined_k1_event_ms": join_ms,
                    "median_distinct_estimate": float(sorted(est)[S // 2]),
                    "p50_p99_bins_service0": q[0][0]},
     }), flush=True)

@@ -102,8 +102,9 @@ typedef struct zk_span_cols {
  * trace run's traceId is inserted into a device set of all traceIds accumulated since the last
  * reset, and a traceId seen again (a trace split into non-adjacent runs, or spread over two
  * accumulate calls -- either would be mis-joined) is counted in zk_stats.not_clustered and makes
- * finalize return ZK_ERR_NOT_CLUSTERED. The set costs 16 B of HBM per record since reset and one
- * extra read of the traceId column. */
+ * finalize return ZK_ERR_NOT_CLUSTERED. The set costs 16 B of HBM per record since reset (about
+ * 24 B per record while it is rehashed into a larger set: both are live) and one extra read of the
+ * traceId column; when that memory cannot be allocated accumulate returns ZK_ERR_CAPACITY. */
 #define ZK_BATCH_DEVICE_PTRS     (1u << 0) /* column pointers are device (HBM) pointers; else host */
 #define ZK_BATCH_TRACE_CLUSTERED (1u << 1) /* all fragments of a trace are adjacent (Cassandra
                                               row-per-trace reads, StorageRecordReader.scala:49-54) */
@@ -156,7 +157,9 @@ typedef struct zk_timing {
     uint64_t join_calls;   /* cumulative number of timed K1 launches */
     double join_ms_total;  /* cumulative K1 time */
     double reduce_ms_total;
-    double reserved[4];
+    double cluster_ms;        /* clustering pass of the last unclustered batch (0 when none) */
+    double cluster_ms_total;  /* cumulative clustering-pass time */
+    double reserved[2];
 } zk_timing;
 
 /* Dense S x S output table of DependencyLink(parent=i, child=j, Moments) for cell i*S+j

@@ -129,3 +129,48 @@ def test_accumulate_after_merge_uses_local_counters_again(gpu):
         assert_parity(got, sh.ctx.stats(), oracle.aggregate(a, S))
     finally:
         sh.close()
+
+
+def test_note_merged_requires_partial(gpu):
+    """zk_deps_note_merged trusts the table's counter tail, which only zk_deps_partial fills: without
+    it (or after a later accumulate) the call is refused instead of dropping every error counter."""
+    S = 20
+    a = tracegen_host(45, 500, max_depth=5, num_services=S)
+    sh = Shard(S)
+    try:
+        sh.ctx.accumulate(a)
+        with pytest.raises(ZkError) as e:
+            sh.ctx.note_merged(0)
+        assert e.value.status == _abi.ZK_ERR_INVALID_ARG
+        sh.ctx.partial()
+        sh.ctx.accumulate(a.take(np.arange(0)))  # an empty batch changes nothing
+        sh.ctx.note_merged(0)
+        sh.ctx.reset()  # reset forgets the fold
+        sh.ctx.accumulate(a)
+        with pytest.raises(ZkError):
+            sh.ctx.note_merged(len(a))
+    finally:
+        sh.close()
+
+
+def test_accumulate_into_merged_table_keeps_the_job_counters(gpu):
+    """A batch accumulated into a merged table: finalize reports the merged job plus the batch, and
+    the table's values are the union's (the ctx's counters restart from the merged tail)."""
+    S = 20
+    a = tracegen_host(46, 800, max_depth=5, num_services=S)
+    b = tracegen_host(47, 600, max_depth=5, num_services=S)
+    from zipkin_amd.columns import SpanColumns
+
+    sh = Shard(S)
+    try:
+        sh.ctx.accumulate(a)
+        sh.ctx.partial()
+        sh.ctx.sync()
+        sh.ctx.note_merged(0)
+        sh.ctx.accumulate(b)
+        got = sh.ctx.finalize()
+        st = sh.ctx.stats()
+        assert st["records"] == len(a) + len(b)
+        assert_parity(got, st, oracle.aggregate(SpanColumns.concat([a, b]), S))
+    finally:
+        sh.close()

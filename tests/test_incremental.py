@@ -84,7 +84,8 @@ def test_incremental_runs_aggregate_each_trace_once(mode):
     rec1 = inc.apply(a, ts_a, num_services=S)
     tc = trace_created(a, ts_a)
     assert rec1.start_time == tc.min() and rec1.end_time == tc.max()
-    assert _by_key(rec1) == _expect(a, np.ones(len(a), bool), services)
+    # the first step is created_ts > minTime (AnormAggregator.scala:46-47,79): the earliest trace is skipped
+    assert _by_key(rec1) == _expect(a, tc > tc.min(), services)
     assert agg.watermark() == tc.max() and agg.count() == 1
 
     # run 2: the same traces again plus newer ones: only the newer ones are aggregated
@@ -93,8 +94,9 @@ def test_incremental_runs_aggregate_each_trace_once(mode):
     both = type(a).concat([a, b])
     ts_both = np.concatenate([ts_a, ts_b])
     rec2 = inc.apply(both, ts_both, num_services=S)
-    assert inc.last_selected == len(b)
-    new = trace_created(both, ts_both) > tc.max()
+    tcb = trace_created(both, ts_both)
+    new = (tcb > tc.max()) & (tcb > trace_created(b, ts_b).min())
+    assert inc.last_selected == int(new.sum()) and 0 < int(new.sum()) < len(b)
     assert _by_key(rec2) == _expect(both, new, services)
     # Cassandra keys records by day and clobbers the row (CassandraAggregates.scala:111-116): both
     # runs fall on day 0, so the second record replaces the first; Anorm keeps both rows
@@ -103,7 +105,7 @@ def test_incremental_runs_aggregate_each_trace_once(mode):
 
     # run 3: nothing new -> nothing stored ("already up-to-date")
     assert inc.apply(both, ts_both, num_services=S) is None
-    assert agg.count() == rows and job.runs == [len(a), len(b)]
+    assert agg.count() == rows and job.runs == [int((tc > tc.min()).sum()), int(new.sum())]
 
 
 def test_incremental_trace_straddling_the_watermark_is_new_as_a_whole():
@@ -132,6 +134,7 @@ def test_incremental_device_job_matches_oracle():
     b = tracegen_host(seed=22, num_traces=1500, max_depth=6, num_services=S)
     ts_b = _created(b, int(trace_created(a, ts_a).max()) + 1)
     seen = np.zeros(len(a) + len(b), np.int64)
+    skipped = np.zeros(len(a) + len(b), bool)
     for cols, ts in ((a, ts_a), (type(a).concat([a, b]), np.concatenate([ts_a, ts_b]))):
         tc = trace_created(cols, ts)
         while True:
@@ -139,12 +142,16 @@ def test_incremental_device_job_matches_oracle():
             rec = inc.apply(cols, ts, num_services=S)
             if rec is None:
                 break
-            sel = (tc > wm) & (tc <= rec.end_time)
-            assert inc.last_selected == int(sel.sum()) and rec.start_time == int(tc[tc > wm].min())
+            lo = int(tc[tc > wm].min())
+            sel = (tc > wm) & (tc <= rec.end_time) & (tc > lo)  # first step: created_ts > minTime
+            assert inc.last_selected == int(sel.sum()) and rec.start_time == lo
             assert _by_key(rec) == _expect(cols, sel, services)
             seen[: len(cols)] += sel
+            skipped[: len(cols)] |= tc == lo
         assert agg.watermark() == tc.max()
-    assert (seen == 1).all()
+    # every trace exactly once, except those created exactly at a run's minTime, which the
+    # reference never aggregates
+    assert (seen[~skipped] == 1).all() and (seen[skipped] == 0).all() and skipped.any()
 
 
 def test_run_without_links_still_advances_the_watermark():
@@ -159,7 +166,7 @@ def test_run_without_links_still_advances_the_watermark():
     rec = inc.apply(roots, ts, num_services=S)
     assert rec is not None and rec.links == () and agg.count() == 1
     assert agg.watermark() == trace_created(roots, ts).max()
-    assert inc.apply(roots, ts, num_services=S) is None and job.runs == [len(roots)]
+    assert inc.apply(roots, ts, num_services=S) is None and job.runs == [len(roots) - 1]  # all but the first
 
 
 def test_record_ends_at_the_last_step_boundary():
@@ -180,6 +187,10 @@ def test_record_ends_at_the_last_step_boundary():
     step = (hi - lo) // steps
     end = lo + ((hi - lo) // step) * step
     assert count > 10000 and (rec.start_time, rec.end_time) == (lo, end)
-    assert inc.last_selected == int((tc <= end).sum())
-    rest = inc.apply(cols, ts, num_services=S)  # the traces after the boundary, exactly once
-    assert rest is None or inc.last_selected == int((tc > end).sum())
+    assert inc.last_selected == int(((tc <= end) & (tc > lo)).sum())
+    rest = inc.apply(cols, ts, num_services=S)  # the traces after the boundary (but its first)
+    after = tc > end
+    lo2 = tc[after].min()
+    # one created instant left: stepSize 0 (the reference's Range throws), those traces are kept
+    expect = after if (tc[after] == lo2).all() else after & (tc > lo2)
+    assert rest is None or inc.last_selected == int(expect.sum())

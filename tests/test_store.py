@@ -237,6 +237,10 @@ def test_hbase_reverse_ms_keys_and_reversed_scan():
     _assert_sum(agg.getDependencies(5 * h, 2 * h), records[2:5][::-1])
     # the usual start < end window scans nothing
     assert agg.getDependencies(0, 10 * h) == Dependencies.zero()
+    # start and end in the same millisecond: startRow == stopRow is HBase's get-scan (inclusive
+    # stop row): exactly the record stored at that key, and nothing when no record is there
+    _assert_sum(agg.getDependencies(4 * h, 4 * h + 999), [records[3]])
+    assert agg.getDependencies(4 * h + 1000, 4 * h + 1000) == Dependencies.zero()
     # no start: from key 0 = every record, newest first
     _assert_sum(agg.getDependencies(None), records[::-1])
     # a second record of the same millisecond replaces the first

@@ -25,6 +25,15 @@ for s in $STEPS; do
       w=${s#bench_}
       timeout -k 10 250 python bench.py --workload $w > gpurun_out/bench_$w.log 2>&1
       ok_or_stop $? $s; tail -1 gpurun_out/bench_$w.log | cut -c1-400 ;;
+    bench_shuffled)
+      timeout -k 10 300 python bench.py --order shuffled --cpu-sample 0 ${BENCH_ARGS:-} > gpurun_out/bench_shuffled.log 2>&1
+      ok_or_stop $? bench_shuffled; tail -1 gpurun_out/bench_shuffled.log | cut -c1-600 ;;
+    prof_serial)
+      timeout -k 10 250 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_serial -o run --output-format csv -- python3 bench.py --steps 10 --warmup 1 --pipeline 0 --cpu-sample 0 ${BENCH_ARGS:-} > gpurun_out/prof_serial.log 2>&1
+      ok_or_stop $? prof_serial; find gpurun_out/prof_serial -name '*stats*' | head ;;
+    prof_shuffled)
+      timeout -k 10 250 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_shuffled -o run --output-format csv -- python3 bench.py --order shuffled --steps 5 --warmup 1 --pipeline 0 --cpu-sample 0 ${BENCH_ARGS:-} > gpurun_out/prof_shuffled.log 2>&1
+      ok_or_stop $? prof_shuffled; find gpurun_out/prof_shuffled -name '*stats*' | head ;;
     prof)
       timeout -k 10 250 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --cpu-sample 0 ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
       ok_or_stop $? prof; find gpurun_out/prof -name '*stats*' | head ;;

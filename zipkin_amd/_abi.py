@@ -122,7 +122,9 @@ class zk_timing(C.Structure):
         ("join_calls", C.c_uint64),
         ("join_ms_total", C.c_double),
         ("reduce_ms_total", C.c_double),
-        ("reserved", C.c_double * 4),
+        ("cluster_ms", C.c_double),
+        ("cluster_ms_total", C.c_double),
+        ("reserved", C.c_double * 2),
     ]
 
 

@@ -60,6 +60,8 @@ struct zk_ctx {
     void* fin_stage = nullptr;
     uint64_t records_since_reset = 0;
     bool merged = false;                  // the table holds the all-reduced job (zk_deps_note_merged)
+    bool folded = false;                  // zk_deps_partial folded this ctx's counters into the table tail
+                                          // since the last reset / accumulate (note_merged requires it)
     // clustering pass for unclustered batches (zk_cluster.hip)
     uint8_t* cl_cols = nullptr;           // 7 aligned columns of cl_cap records
     uint64_t cl_cap = 0;
@@ -75,7 +77,7 @@ struct zk_ctx {
     zk_rt* rt = nullptr;
     uint32_t rt_mode = ZK_RT_WITH_DEPS;
     // timing
-    std::vector<EventPair> ev_free, ev_join, ev_reduce, ev_spill, ev_fin;
+    std::vector<EventPair> ev_free, ev_join, ev_reduce, ev_spill, ev_fin, ev_cluster;
     zk_timing tm{};
 };
 
@@ -257,13 +259,22 @@ zk_status verify_batch(zk_ctx* c, const SpanColsDev& d) {
                                                                                    : (1ull << 16));
     if (need > c->tset_slots) {
         uint64_t* nt = nullptr;
-        ZK_HIP(c, hipMalloc(&nt, (need + 1) * 8));
-        ZK_HIP(c, hipMemsetAsync(nt, 0, (need + 1) * 8, c->stream));
-        if (c->tset) {
-            ZK_HIP(c, launch_trace_set_rehash(c->tset, c->tset_slots, nt, need, c->stream));
-            ZK_HIP(c, hipStreamSynchronize(c->stream));
-            hipFree(c->tset);
+        if (hipMalloc(&nt, (need + 1) * 8) != hipSuccess) {
+            (void)hipGetLastError();  // clear the sticky allocation error
+            return fail(c, ZK_ERR_CAPACITY,
+                        "ZK_BATCH_VERIFY_TRACES: no device memory for the traceId set (" +
+                            std::to_string((need + 1) * 8) + " B; 16 B per record since reset, ~24 B during a rehash)");
         }
+        hipError_t e = hipMemsetAsync(nt, 0, (need + 1) * 8, c->stream);
+        if (e == hipSuccess && c->tset) {
+            e = launch_trace_set_rehash(c->tset, c->tset_slots, nt, need, c->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        }
+        if (e != hipSuccess) {
+            hipFree(nt);
+            return hip_fail(c, e, "traceId set rehash");
+        }
+        if (c->tset) hipFree(c->tset);
         c->tset = nt;
         c->tset_slots = need;
     }
@@ -379,7 +390,7 @@ zk_status zk_ctx_destroy(zk_ctx* c) {
     hipFree(c->cl_idx);
     hipFree(c->cl_temp);
     hipFree(c->tset);
-    for (auto* v : {&c->ev_free, &c->ev_join, &c->ev_reduce, &c->ev_spill, &c->ev_fin})
+    for (auto* v : {&c->ev_free, &c->ev_join, &c->ev_reduce, &c->ev_spill, &c->ev_fin, &c->ev_cluster})
         for (auto& p : *v) {
             hipEventDestroy(p.a);
             hipEventDestroy(p.b);
@@ -405,6 +416,7 @@ zk_status zk_deps_reset(zk_ctx* c) {
     c->tset_records = 0;
     c->records_since_reset = 0;
     c->merged = false;
+    c->folded = false;
     return ZK_OK;
 }
 
@@ -422,10 +434,16 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
     if (join && c->records_since_reset + n > kMaxRecordsSinceReset)
         return fail(c, ZK_ERR_CAPACITY, "more than 2^32-1 records since reset");
     ZK_HIP(c, hipSetDevice(c->device));
-    if (c->merged) {  // accumulating into a merged table: back to this ctx's own counters
+    if (c->merged) {
+        // accumulating into a merged table: the table holds the whole job, so the ctx's own counters
+        // restart from the merged (job-wide) ones in the tail -- shard 0 takes the tail, the other
+        // shards are zeroed -- and finalize then reports the job plus this batch
         ZK_HIP(c, hipMemsetAsync(c->stats, 0, (size_t)kStatShards * ST_N * 8, c->stream));
+        ZK_HIP(c, hipMemcpyAsync(c->stats, c->table + (uint64_t)c->S * c->S * kLimbs, kTableTailBytes,
+                                 hipMemcpyDeviceToDevice, c->stream));
         c->merged = false;
     }
+    c->folded = false;  // the tail no longer holds this ctx's counters once the batch lands
     SpanColsDev d{cols->trace_id, cols->span_id, cols->parent_id, cols->first_ts,
                   cols->last_ts,  cols->service_id, cols->flags,   n};
     if (!(flags & ZK_BATCH_DEVICE_PTRS)) {
@@ -459,8 +477,20 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
         d = SpanColsDev{tid, sid, pid, fts, lts, svc, flg, n};
     }
     if (!(flags & ZK_BATCH_TRACE_CLUSTERED)) {
+        EventPair ec;
+        if (c->timing) {
+            ec = take_pair(c);
+            ZK_HIP(c, hipEventRecord(ec.a, c->stream));
+        }
         const zk_status cs = cluster_batch(c, &d);
-        if (cs != ZK_OK) return cs;
+        if (cs != ZK_OK) {
+            if (c->timing) c->ev_free.push_back(ec);
+            return cs;
+        }
+        if (c->timing) {
+            ZK_HIP(c, hipEventRecord(ec.b, c->stream));
+            c->ev_cluster.push_back(ec);
+        }
     } else if (flags & ZK_BATCH_DEVICE_PTRS) {
         // K1 reads two records per lane with one 16-byte (u64 columns) / 8-byte (u32) load
         if (!aligned(d.trace_id, 16) || !aligned(d.span_id, 16) || !aligned(d.parent_id, 16) ||
@@ -642,6 +672,7 @@ zk_status zk_ctx_timing(zk_ctx* c, zk_timing* out) {
     drain(c->ev_reduce, &c->tm.reduce_ms, &c->tm.reduce_ms_total, nullptr);
     drain(c->ev_spill, &c->tm.spill_ms, nullptr, nullptr);
     drain(c->ev_fin, &c->tm.finalize_ms, nullptr, nullptr);
+    drain(c->ev_cluster, &c->tm.cluster_ms, &c->tm.cluster_ms_total, nullptr);
     *out = c->tm;
     return ZK_OK;
     ZK_CATCH(c)
@@ -653,6 +684,7 @@ zk_status zk_deps_partial(zk_ctx* c, void** dev_ptr, uint64_t* bytes) {
     if (!c->merged)  // a merged tail already holds the job-wide counters
         ZK_HIP(c, launch_stats_fold(c->stats, (unsigned long long*)(c->table + (uint64_t)c->S * c->S * kLimbs),
                                     c->stream));
+    c->folded = true;
     *dev_ptr = c->table;
     *bytes = table_bytes(c->S);
     return ZK_OK;
@@ -660,6 +692,10 @@ zk_status zk_deps_partial(zk_ctx* c, void** dev_ptr, uint64_t* bytes) {
 
 zk_status zk_deps_note_merged(zk_ctx* c, uint64_t total_records) {
     if (!c) return ZK_ERR_INVALID_ARG;
+    // the tail is only meaningful after zk_deps_partial folded this ctx's counters into it (an
+    // all-reduce of a stale or zeroed tail would silently drop every error counter on every rank)
+    if (!c->folded)
+        return fail(c, ZK_ERR_INVALID_ARG, "zk_deps_note_merged without zk_deps_partial since the last reset/accumulate");
     if (total_records == 0) {  // take it from the all-reduced counter tail
         ZK_HIP(c, hipSetDevice(c->device));
         unsigned long long rec = 0;

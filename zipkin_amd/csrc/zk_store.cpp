@@ -199,17 +199,22 @@ zk_status zk_store_get_dependencies(zk_store* s, const int64_t* start_us, const 
             for (const auto& kv : s->keyed) hit.push_back(&kv.second);
         monoid_sum(hit, &res, &rs, &re);
     } else if (s->mode == ZK_STORE_HBASE) {
-        // scan [startRow, stopRow) in row-key order (HBaseAggregates.scala:41-43); a start row at or
-        // past the stop row scans nothing
+        // scan [startRow, stopRow) in row-key order (HBaseAggregates.scala:41-43); a start row past
+        // the stop row scans nothing; startRow == stopRow is a get-scan (HBase's Scan.isGetScan:
+        // the stop row is inclusive), which returns the record stored under that one key
         const uint64_t lo_key = hbase_key_ms(start_us ? *start_us / 1000 : INT64_MAX);
         const bool has_stop = end_us != nullptr;
         const uint64_t hi_key = has_stop ? hbase_key_ms(*end_us / 1000) : 0;
         std::vector<const StoredDeps*> hit;
-        if (!has_stop || lo_key < hi_key)
+        if (has_stop && lo_key == hi_key) {
+            const auto it = s->keyed.find(lo_key);
+            if (it != s->keyed.end()) hit.push_back(&it->second);
+        } else if (!has_stop || lo_key < hi_key) {
             for (auto it = s->keyed.lower_bound(lo_key); it != s->keyed.end(); ++it) {
                 if (has_stop && it->first >= hi_key) break;
                 hit.push_back(&it->second);
             }
+        }
         monoid_sum(hit, &res, &rs, &re);
     } else {
         const int64_t lo = start_us ? *start_us : now_us - kDayUs;  // AnormAggregates.scala:53-54

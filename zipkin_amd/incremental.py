@@ -23,8 +23,11 @@ device) over the new part:
   stepSize = (max - min) / steps (SpanSummary, :35-39); the steps run over
   Range.Long(min, max + 1, stepSize), so the record is Dependencies(min, last boundary, links)
   (:43-49, :102-120) and the traces created after the last boundary wait for the next run, as
-  the reference's spans do. (All new traces created at one instant make stepSize 0, where the
-  reference's Range throws; here the record then ends at that instant.)
+  the reference's spans do. The first step is the half-open (min, boundary] of the reference's
+  `created_ts > start` with start = min (:46-47, :79), so the traces created exactly at min are
+  skipped for good, as the reference skips those spans. (All new traces created at one instant
+  make stepSize 0, where the reference's Range throws; here they are aggregated and the record
+  ends at that instant.)
 * the record is stored whenever new traces exist, with or without links: the reference folds
   from Monoid.zero and always stores the result (:41-56), which is what advances the watermark;
 * one device job over the selected traces replaces the per-step Monoid sum; the two differ only
@@ -91,7 +94,13 @@ class IncrementalAggregator:
         steps = max(count // 10000, 1)
         step = (hi - lo) // steps
         end = hi if step == 0 else lo + ((hi - lo) // step) * step
+        # the reference's first step queries created_ts > minTime with start = minTime
+        # (AnormAggregator.scala:46-47,79): spans created exactly at minTime are never aggregated,
+        # and the stored record's end moves the watermark past them. (stepSize 0 -- every new trace
+        # created at one instant -- makes the reference's Range throw; here those traces are kept.)
         sel = new & (created <= end)
+        if step != 0:
+            sel &= created > lo
         self.last_selected = int(sel.sum())
         deps = self.job.run(cols.take(np.flatnonzero(sel)), num_services=num_services)
         rec = Dependencies(lo, end, deps.links if deps is not None else ())
