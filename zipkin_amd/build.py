@@ -24,8 +24,9 @@ SOURCES = [
     "zk_ingest.cpp",
     "zk_ingest_dev.hip",
     "zk_cluster.hip",
+    "zk_launch.cpp",
 ]
-HEADERS = ["zk_internal.h", "zk_cluster.h", "zk_tracegen.h", "zk_sketch_internal.h", "zk_rt_internal.h", "zk_block.h"]
+HEADERS = ["zk_internal.h", "zk_cluster.h", "zk_tracegen.h", "zk_sketch_internal.h", "zk_rt_internal.h", "zk_block.h", "zk_launch.h"]
 PUBLIC_HEADERS = ["zkagg.h", "zksketch.h", "zkstore.h", "zkingest.h"]
 LIB = PKG / "libzkagg.so"
 ARCH = os.environ.get("ZK_OFFLOAD_ARCH", "gfx950")

@@ -13,6 +13,7 @@
 
 #include "zk_cluster.h"
 #include "zk_internal.h"
+#include "zk_launch.h"
 #include "zk_rt_internal.h"
 
 using namespace zk;
@@ -89,6 +90,8 @@ zk_status fail(zk_ctx* c, zk_status s, const std::string& msg) {
 }
 
 zk_status hip_fail(zk_ctx* c, hipError_t e, const char* where) {
+    if (e == hipErrorLaunchOutOfResources && *launch_refusal())  // launch_checked refused a launch
+        return fail(c, ZK_ERR_CAPACITY, std::string(where) + ": " + launch_refusal());
     return fail(c, ZK_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
 }
 

@@ -18,6 +18,7 @@
 #include <rocprim/iterator/counting_iterator.hpp>
 
 #include "zk_cluster.h"
+#include "zk_launch.h"
 #include "zk_tracegen.h"
 
 namespace zk {
@@ -123,28 +124,24 @@ hipError_t launch_cluster(const SpanColsDev& in, const SpanColsMut& out, uint32_
     hipError_t e = rocprim::radix_sort_pairs(temp, b, in.trace_id, out.trace_id, rocprim::counting_iterator<uint32_t>(0u),
                                              idx, (uint32_t)in.n, 0u, 64u, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_gather_cols, dim3(grid_for(in.n)), dim3(256), 0, s, in, idx, out);
-    return hipGetLastError();
+    return launch_checked("k_gather_cols", k_gather_cols, dim3(grid_for(in.n)), dim3(256), 0, s, in, idx, out);
 }
 
 hipError_t launch_trace_set_insert(const uint64_t* trace_id, uint64_t n, uint64_t* set, uint64_t slots,
                                    unsigned long long* dup, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_trace_set_insert, dim3(grid_for(n)), dim3(256), 0, s, trace_id, n,
-                       (unsigned long long*)set, slots, dup);
-    return hipGetLastError();
+    return launch_checked("k_trace_set_insert", k_trace_set_insert, dim3(grid_for(n)), dim3(256), 0, s, trace_id, n,
+                          (unsigned long long*)set, slots, dup);
 }
 
 hipError_t launch_trace_set_rehash(const uint64_t* old, uint64_t old_slots, uint64_t* set, uint64_t slots,
                                    hipStream_t s) {
-    hipLaunchKernelGGL(k_trace_set_rehash, dim3(grid_for(old_slots + 1)), dim3(256), 0, s,
-                       (const unsigned long long*)old, old_slots, (unsigned long long*)set, slots);
-    return hipGetLastError();
+    return launch_checked("k_trace_set_rehash", k_trace_set_rehash, dim3(grid_for(old_slots + 1)), dim3(256), 0, s,
+                          (const unsigned long long*)old, old_slots, (unsigned long long*)set, slots);
 }
 
 hipError_t launch_stats_fold(const unsigned long long* shards, unsigned long long* out, hipStream_t s) {
-    hipLaunchKernelGGL(k_stats_fold, dim3(1), dim3(256), 0, s, shards, kStatShards, out);
-    return hipGetLastError();
+    return launch_checked("k_stats_fold", k_stats_fold, dim3(1), dim3(256), 0, s, shards, (int)kStatShards, out);
 }
 
 }  // namespace zk

@@ -13,6 +13,7 @@
 // are evaluated in 384-bit integers and divided with one round-to-nearest-even: the result is the
 // correctly rounded value of the exact moments, independent of order, GPU count and batching.
 #include "zk_internal.h"
+#include "zk_launch.h"
 
 namespace zk {
 namespace {
@@ -293,9 +294,8 @@ __global__ __launch_bounds__(256) void k_finalize(const uint64_t* __restrict__ t
 hipError_t launch_finalize(const uint64_t* table, uint32_t S, const zk_link_table* out, hipStream_t s) {
     const uint64_t cells = (uint64_t)S * S;
     if (!cells) return hipSuccess;
-    hipLaunchKernelGGL(k_finalize, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, table, cells,
-                       out->m0, out->m1, out->m2, out->m3, out->m4, out->present);
-    return hipGetLastError();
+    return launch_checked("k_finalize", k_finalize, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, table, cells,
+                          out->m0, out->m1, out->m2, out->m3, out->m4, out->present);
 }
 
 }  // namespace zk

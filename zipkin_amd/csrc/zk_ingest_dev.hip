@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "zk_guard.h"
+#include "zk_launch.h"
 #include "zkingest.h"
 
 namespace zk {
@@ -924,7 +925,9 @@ zk_status dfail(zk_ingest_dev* g, zk_status s, const std::string& m) {
 #define ING_HIP(g, call)                                                                                \
     do {                                                                                                \
         hipError_t _e = (call);                                                                         \
-        if (_e != hipSuccess) return dfail(g, ZK_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(_e)); \
+        if (_e != hipSuccess)                                                                          \
+            return dfail(g, is_refusal(_e) ? ZK_ERR_CAPACITY : ZK_ERR_HIP,                          \
+                        std::string(#call) + ": " + launch_error_str(_e));                             \
     } while (0)
 
 uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
@@ -1060,8 +1063,7 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     const dim3 grid((unsigned)((n + kIngWG - 1) / kIngWG)), blk(kIngWG);
     hipStream_t s = g->stream;
     // D1 + scan: scratch offsets
-    hipLaunchKernelGGL(k_ing_rawlen, grid, blk, 0, s, a);
-    ING_HIP(g, hipGetLastError());
+    ING_HIP(g, launch_checked("k_ing_rawlen", k_ing_rawlen, grid, blk, 0, s, a));
     size_t need = 0, need2 = 0;
     ING_HIP(g, hipcub::DeviceScan::ExclusiveSum(nullptr, need, a.raw_len, a.raw_off, (int)n1, s));
     ING_HIP(g, hipcub::DeviceScan::ExclusiveSum(nullptr, need2, a.keep, a.pos, (int)n1, s));
@@ -1087,10 +1089,10 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     }
     a.scratch = g->scratch;
     // D2, D3
-    hipLaunchKernelGGL(k_ing_decode_lds, dim3((unsigned)((n + kLdsBlock - 1) / kLdsBlock)), dim3(kLdsWG), 0, s, a);
-    hipLaunchKernelGGL(k_ing_decode, grid, blk, 0, s, a, 1u);  // the deferred waves
-    hipLaunchKernelGGL(k_ing_dict_insert, grid, blk, 0, s, a);
-    ING_HIP(g, hipGetLastError());
+    ING_HIP(g, launch_checked("k_ing_decode_lds", k_ing_decode_lds, dim3((unsigned)((n + kLdsBlock - 1) / kLdsBlock)),
+                              dim3(kLdsWG), 0, s, a));
+    ING_HIP(g, launch_checked("k_ing_decode", k_ing_decode, grid, blk, 0, s, a, 1u));  // the deferred waves
+    ING_HIP(g, launch_checked("k_ing_dict_insert", k_ing_dict_insert, grid, blk, 0, s, a));
     // ids for new slots, in slot order; their names into the device arena
     std::vector<uint64_t> key(g->table), ptr(g->table);
     std::vector<uint32_t> len(g->table);
@@ -1130,14 +1132,13 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
         ING_HIP(g, hipMemcpyAsync(g->d_ptr, ptr.data(), ptr.size() * 8, hipMemcpyHostToDevice, s));
     }
     // D4, scan, D5
-    hipLaunchKernelGGL(k_ing_lookup, grid, blk, 0, s, a);
+    ING_HIP(g, launch_checked("k_ing_lookup", k_ing_lookup, grid, blk, 0, s, a));
     ING_HIP(g, hipMemsetAsync(a.keep + n, 0, 4, s));
     ING_HIP(g, hipcub::DeviceScan::ExclusiveSum(g->cub, need, a.keep, a.pos, (int)n1, s));
     ING_HIP(g, hipMemsetAsync(g->counts, 0, 8 * 8, s));
     ING_HIP(g, hipMemsetAsync(g->counts + 8, 0xFF, 8, s));
-    hipLaunchKernelGGL(k_ing_count, grid, blk, 0, s, (const uint8_t*)a.status, n, g->counts,
-                       (unsigned int*)(g->counts + 8));
-    ING_HIP(g, hipGetLastError());
+    ING_HIP(g, launch_checked("k_ing_count", k_ing_count, grid, blk, 0, s, (const uint8_t*)a.status, n, g->counts,
+                              (unsigned int*)(g->counts + 8)));
     unsigned long long c[9];
     uint32_t kept = 0;
     ING_HIP(g, hipMemcpyAsync(c, g->counts, 9 * 8, hipMemcpyDeviceToHost, s));
@@ -1155,8 +1156,7 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     if (strict && bad)
         return dfail(g, ZK_ERR_INVALID_SPAN, "span " + std::to_string(first_bad) + ": " +
                                                  (c[kStUndecodable] ? "undecodable or invalid span" : "invalid span"));
-    hipLaunchKernelGGL(k_ing_compact, grid, blk, 0, s, a, *out);
-    ING_HIP(g, hipGetLastError());
+    ING_HIP(g, launch_checked("k_ing_compact", k_ing_compact, grid, blk, 0, s, a, *out));
     ING_HIP(g, hipStreamSynchronize(s));
     *n_out = kept;
     *n_rejected = bad;

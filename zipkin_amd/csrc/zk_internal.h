@@ -142,6 +142,7 @@ struct ReduceArgs {
 hipError_t launch_partitioned_reduce(const ReduceArgs& r, hipStream_t s);
 // bucket geometry for S services (nb = 0: use the atomic reduce)
 void bucket_geometry(uint32_t S, uint32_t* nb, uint32_t* cb_shift);
+uint64_t reduce_scatter_dyn_lds(uint32_t S);  // K2's dynamic LDS for S services (0: atomic reduce)
 hipError_t launch_spill(const JoinArgs& a, uint32_t spill_wgs, hipStream_t s);
 uint64_t spill_scratch_bytes_per_wg(uint32_t max_trace);
 hipError_t launch_finalize(const uint64_t* table, uint32_t S, const zk_link_table* out,

@@ -17,6 +17,7 @@
 // leave LDS. Traces longer than the tile capacity are deferred to k_span_join_spill (global
 // scratch, one trace per workgroup at a time).
 #include "zk_internal.h"
+#include "zk_launch.h"
 #include "zk_sketch_internal.h"
 
 #ifndef ZK_HASH_FACTOR
@@ -1317,22 +1318,20 @@ hipError_t launch_join(const JoinArgs& a, hipStream_t s) {
     const dim3 g((unsigned)a.grid), b(kTileWG);
     const bool emit = a.rt_pay != nullptr, join = a.join != 0;
     if (a.ablate == 1)
-        hipLaunchKernelGGL((k_span_join_stream<kTile, kTileWG, 1, kModeJoin>), g, b, 0, s, a);
-    else if (a.ablate == 2)
-        hipLaunchKernelGGL((k_span_join_stream<kTile, kTileWG, 2, kModeJoin>), g, b, 0, s, a);
-    else if (emit && join)
-        hipLaunchKernelGGL((k_span_join_stream<kTile, kTileWG, 0, kModeJoin | kModeEmit>), g, b, 0, s, a);
-    else if (emit)
-        hipLaunchKernelGGL((k_span_join_stream<kTile, kTileWG, 0, kModeEmit>), g, b, 0, s, a);
-    else
-        hipLaunchKernelGGL((k_span_join_stream<kTile, kTileWG, 0, kModeJoin>), g, b, 0, s, a);
-    return hipGetLastError();
+        return launch_checked("k_span_join_stream<ablate 1>", k_span_join_stream<kTile, kTileWG, 1, kModeJoin>, g, b, 0, s, a);
+    if (a.ablate == 2)
+        return launch_checked("k_span_join_stream<ablate 2>", k_span_join_stream<kTile, kTileWG, 2, kModeJoin>, g, b, 0, s, a);
+    if (emit && join)
+        return launch_checked("k_span_join_stream<join|emit>", k_span_join_stream<kTile, kTileWG, 0, kModeJoin | kModeEmit>,
+                              g, b, 0, s, a);
+    if (emit)
+        return launch_checked("k_span_join_stream<emit>", k_span_join_stream<kTile, kTileWG, 0, kModeEmit>, g, b, 0, s, a);
+    return launch_checked("k_span_join_stream<join>", k_span_join_stream<kTile, kTileWG, 0, kModeJoin>, g, b, 0, s, a);
 }
 
 hipError_t launch_spill(const JoinArgs& a, uint32_t spill_wgs, hipStream_t s) {
     if (a.c.n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_span_join_spill, dim3(spill_wgs), dim3(kSpillWG), 0, s, a);
-    return hipGetLastError();
+    return launch_checked("k_span_join_spill", k_span_join_spill, dim3(spill_wgs), dim3(kSpillWG), 0, s, a);
 }
 
 uint64_t join_tile_records() { return kTile; }

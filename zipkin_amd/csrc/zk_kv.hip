@@ -17,6 +17,7 @@
 // The result is deterministic: it equals "top `cand` by current estimate among (previous
 // candidates U this batch's distinct keys)", which oracle/kv.py restates.
 #include "zk_sketch_internal.h"
+#include "zk_launch.h"
 
 namespace zk {
 namespace {
@@ -478,27 +479,25 @@ __global__ void k_kv_estimate(KvArgs a, uint32_t s, const uint64_t* __restrict__
 
 hipError_t launch_kv_sketch(const KvArgs& a, hipStream_t s) {
     if (!a.max_units) return hipSuccess;
-    hipLaunchKernelGGL(k_kv_sketch, dim3(a.max_units), dim3(kKvWG), (size_t)a.depth * a.width * 4, s, a);
-    return hipGetLastError();
+    return launch_checked("k_kv_sketch", k_kv_sketch, dim3(a.max_units), dim3(kKvWG), (size_t)a.depth * a.width * 4, s, a);
 }
 
 hipError_t launch_kv_candidates(const KvArgs& a, hipStream_t s) {
     if (!a.max_units) return hipSuccess;
-    hipLaunchKernelGGL(k_kv_candidates, dim3(a.max_units), dim3(kKvWG), (size_t)a.depth * a.width * 4, s, a);
-    return hipGetLastError();
+    return launch_checked("k_kv_candidates", k_kv_candidates, dim3(a.max_units), dim3(kKvWG),
+                          (size_t)a.depth * a.width * 4, s, a);
 }
 
 hipError_t launch_kv_merge(const KvArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_kv_merge, dim3(a.S), dim3(kKvWG), (size_t)a.depth * a.width * 4, s, a,
-                       a.max_units ? 1u : 0u);
-    return hipGetLastError();
+    return launch_checked("k_kv_merge", k_kv_merge, dim3(a.S), dim3(kKvWG), (size_t)a.depth * a.width * 4, s, a,
+                          a.max_units ? 1u : 0u);
 }
 
 hipError_t launch_kv_estimate(const KvArgs& a, uint32_t svc, const uint64_t* keys, uint64_t n, uint32_t* est,
                               hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_kv_estimate, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, svc, keys, n, est);
-    return hipGetLastError();
+    return launch_checked("k_kv_estimate", k_kv_estimate, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, svc,
+                          keys, n, est);
 }
 
 }  // namespace zk

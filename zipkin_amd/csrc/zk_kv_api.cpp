@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "zk_guard.h"
+#include "zk_launch.h"
 #include "zk_internal.h"
 #include "zk_sketch_internal.h"
 #include "zksketch.h"
@@ -50,7 +51,9 @@ zk_status kfail(zk_kv* k, zk_status s, const std::string& m) {
 #define KV_HIP(kv, call)                                                                         \
     do {                                                                                         \
         hipError_t _e = (call);                                                                  \
-        if (_e != hipSuccess) return kfail(kv, ZK_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(_e)); \
+        if (_e != hipSuccess)                                                                          \
+            return kfail(kv, is_refusal(_e) ? ZK_ERR_CAPACITY : ZK_ERR_HIP,                          \
+                        std::string(#call) + ": " + launch_error_str(_e));                             \
     } while (0)
 
 uint32_t ilog2(uint32_t x) {

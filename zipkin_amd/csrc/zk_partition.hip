@@ -11,6 +11,7 @@
 
 #include "zk_block.h"
 #include "zk_sketch_internal.h"
+#include "zk_launch.h"
 
 namespace zk {
 namespace {
@@ -126,9 +127,6 @@ constexpr uint32_t kLineMaxS = 1024;
 // Items per output line: 8 = 64 bytes. 128-byte lines (7168-item chunks, so that the S x 128 B carry
 // fits) measured 8.99-9.03 ms against 6.93-7.00 ms for the C4 partition (profiles/r02/ab_part_lines.txt).
 constexpr int kLineItems = 8;
-constexpr uint64_t kLdsBytes = 160 * 1024;
-// LDS of one line-scatter workgroup: the fixed arrays below plus the [S][kLineItems] carry
-constexpr uint64_t part_lines_static(int U, int WG) { return 4ull * kLineMaxS * 4 + (uint64_t)WG * U * 10 + 32 * 4; }
 template <int U, int WG>
 __global__ __launch_bounds__(WG) void k_part_scatter_lines(const uint32_t* __restrict__ svc,
                                                             const uint64_t* __restrict__ payload, uint64_t n,
@@ -299,6 +297,16 @@ uint64_t scan_temp_bytes(uint64_t m) {
 
 }  // namespace
 
+int partition_scatter_choice(uint32_t S, uint64_t static_lines, uint64_t static_items, uint64_t* dyn) {
+    const uint64_t carry = (uint64_t)S * kLineItems * 8;  // the line kernel's [S][8] u64 carry
+    if (S <= kLineMaxS && lds_fits(static_lines, carry)) {
+        *dyn = carry;
+        return kScatterLines;
+    }
+    *dyn = (uint64_t)S * 4;  // the item kernel's per-service cursor
+    return lds_fits(static_items, *dyn) ? kScatterItems : kScatterNone;
+}
+
 PartitionPlan partition_plan(uint64_t n, uint32_t S, uint32_t cus) {
     PartitionPlan p;
     p.S = S;
@@ -330,23 +338,30 @@ hipError_t partition_impl(const PartitionPlan& p, const uint32_t* svc, const uin
     void* temp = (uint8_t*)scratch + 2 * a;
     size_t temp_bytes = scan_temp_bytes(m);
     const size_t lds = (size_t)p.S * 4;
-    hipLaunchKernelGGL(k_part_hist, dim3(p.grid), dim3(kPartWG), lds, s, svc, n, p.per_wg, counts, p.S, p.grid, hist,
-                       dropped);
-    hipError_t e = hipGetLastError();
+    hipError_t e = launch_checked("k_part_hist", k_part_hist, dim3(p.grid), dim3(kPartWG), lds, s, svc, n, p.per_wg,
+                                  counts, p.S, p.grid, hist, dropped);
     if (e != hipSuccess) return e;
     e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, hist, offs, (int)m, s);
     if (e != hipSuccess) return e;
-    // whole lines while the carry fits the LDS (S <= 1022 at 8192-item chunks; S = 1024 faulted
-    // before this check), else item by item
-    if (p.S <= kLineMaxS && part_lines_static(ZK_PART_U, ZK_PART_WG) + (uint64_t)p.S * kLineItems * 8 <= kLdsBytes)
-        hipLaunchKernelGGL((k_part_scatter_lines<ZK_PART_U, ZK_PART_WG>), dim3(p.grid), dim3(ZK_PART_WG),
-                           (size_t)p.S * kLineItems * 8, s,
-                           svc, payload, n, p.per_wg, counts, p.S, p.grid, offs, out, hash, hash_seed);
+    // whole lines while the line kernel's static LDS (read from its code object) plus the [S][8]
+    // carry fit one CU (S <= 1022 at 8192-item chunks; S = 1024 faulted in round 2, before any
+    // check), else item by item
+    uint32_t st_lines = 0, st_items = 0, mt = 0;
+    e = kernel_attrs((const void*)k_part_scatter_lines<ZK_PART_U, ZK_PART_WG>, &st_lines, &mt);
+    if (e == hipSuccess) e = kernel_attrs((const void*)k_part_scatter, &st_items, &mt);
+    if (e != hipSuccess) return e;
+    uint64_t dyn = 0;
+    const int choice = partition_scatter_choice(p.S, st_lines, st_items, &dyn);
+    if (choice == kScatterLines)
+        e = launch_checked("k_part_scatter_lines", k_part_scatter_lines<ZK_PART_U, ZK_PART_WG>, dim3(p.grid),
+                           dim3(ZK_PART_WG), dyn, s, svc, payload, n, p.per_wg, counts, p.S, p.grid, offs, out, hash,
+                           hash_seed);
     else
-        hipLaunchKernelGGL(k_part_scatter, dim3(p.grid), dim3(kPartWG), lds, s, svc, payload, n, p.per_wg, counts,
-                           p.S, p.grid, offs, out, hash, hash_seed);
-    hipLaunchKernelGGL(k_part_seg, dim3((p.S + 256) / 256), dim3(256), 0, s, offs, hist, p.S, p.grid, seg);
-    return hipGetLastError();
+        e = launch_checked("k_part_scatter", k_part_scatter, dim3(p.grid), dim3(kPartWG), dyn, s, svc, payload, n,
+                           p.per_wg, counts, p.S, p.grid, offs, out, hash, hash_seed);
+    if (e != hipSuccess) return e;
+    return launch_checked("k_part_seg", k_part_seg, dim3((p.S + 256) / 256), dim3(256), 0, s, offs, hist, p.S, p.grid,
+                          seg);
 }
 }  // namespace
 
@@ -374,8 +389,12 @@ hipError_t launch_partition_lists(const PartitionPlan& p0, const uint32_t* svc, 
 
 hipError_t launch_unit_plan(const uint64_t* seg, uint32_t S, uint64_t unit_items, uint32_t* unit_base,
                             hipStream_t s) {
-    hipLaunchKernelGGL(k_unit_plan, dim3(1), dim3(1024), 0, s, seg, S, unit_items, unit_base);
-    return hipGetLastError();
+    return launch_checked("k_unit_plan", k_unit_plan, dim3(1), dim3(1024), 0, s, seg, S, unit_items, unit_base);
 }
 
 }  // namespace zk
+
+// internal (not in include/): the partition's scatter choice for a CPU test of the LDS planner
+extern "C" int zk_internal_partition_choice(uint32_t S, uint64_t static_lines, uint64_t static_items, uint64_t* dyn) {
+    return zk::partition_scatter_choice(S, static_lines, static_items, dyn);
+}

@@ -8,6 +8,7 @@
 // profiles/r01_atomics_microbench.txt).
 #include "zk_block.h"
 #include "zk_internal.h"
+#include "zk_launch.h"
 
 #ifndef ZK_K2_U
 #define ZK_K2_U 8      // links per thread per K2 chunk
@@ -579,43 +580,49 @@ void bucket_geometry(uint32_t S, uint32_t* nb, uint32_t* cb_shift) {
     }
 }
 
+uint64_t reduce_scatter_dyn_lds(uint32_t S) {
+    uint32_t nb = 0, sh = 0;
+    bucket_geometry(S, &nb, &sh);
+    return (uint64_t)nb * kScatterLine * 8;  // K2's per-bucket line carry
+}
+
 hipError_t launch_partitioned_reduce(const ReduceArgs& r, hipStream_t s) {
     if (!r.nb || !r.lists) return hipSuccess;
-    hipLaunchKernelGGL(k_bucket_colscan, dim3(r.nb), dim3(1024), 0, s, r.hist, r.lists, r.col_off, r.bucket_base);
-    hipLaunchKernelGGL(k_bucket_base, dim3(1), dim3(1024), 0, s, r.bucket_base, r.nb);
+    hipError_t e = launch_checked("k_bucket_colscan", k_bucket_colscan, dim3(r.nb), dim3(1024), 0, s, r.hist, r.lists,
+                                  r.col_off, r.bucket_base);
+    if (e != hipSuccess) return e;
+    e = launch_checked("k_bucket_base", k_bucket_base, dim3(1), dim3(1024), 0, s, r.bucket_base, r.nb);
+    if (e != hipSuccess) return e;
     // ~1024 K2 workgroups: a K1 grid larger than that is walked LPW lists per workgroup
     uint32_t lpw = (r.lists + 1023) / 1024;
     if (lpw > (uint32_t)kScatterMaxLPW) lpw = kScatterMaxLPW;
     const uint32_t k2_grid = (r.lists + lpw - 1) / lpw;
-    hipLaunchKernelGGL((k_link_scatter<ZK_K2_U, ZK_K2_WG>), dim3(k2_grid), dim3(ZK_K2_WG), (size_t)r.nb * kScatterLine * 8, s, r,
-                       lpw);
+    e = launch_checked("k_link_scatter", k_link_scatter<ZK_K2_U, ZK_K2_WG>, dim3(k2_grid), dim3(ZK_K2_WG),
+                       (size_t)r.nb * kScatterLine * 8, s, r, lpw);
+    if (e != hipSuccess) return e;
     const uint32_t splits = r.nb >= 256 ? 1u : (512u + r.nb - 1) / r.nb;
 #if ZK_K3_LDS
-    if (r.cb_shift == 8) {
-        hipLaunchKernelGGL((k_bucket_lds_reduce<8, 256, ZK_K3_U>), dim3(r.nb * splits), dim3(256), 0, s, r, splits);
-        return hipGetLastError();
-    }
-    if (r.cb_shift == 9) {
-        hipLaunchKernelGGL((k_bucket_lds_reduce<9, 512, ZK_K3_U>), dim3(r.nb * splits), dim3(512), 0, s, r, splits);
-        return hipGetLastError();
-    }
+    if (r.cb_shift == 8)
+        return launch_checked("k_bucket_lds_reduce<8>", k_bucket_lds_reduce<8, 256, ZK_K3_U>, dim3(r.nb * splits),
+                              dim3(256), 0, s, r, splits);
+    if (r.cb_shift == 9)
+        return launch_checked("k_bucket_lds_reduce<9>", k_bucket_lds_reduce<9, 512, ZK_K3_U>, dim3(r.nb * splits),
+                              dim3(512), 0, s, r, splits);
 #endif
     // CB = 512: 512 threads, 4096-link chunks (36 KB LDS); CB = 1024: 1024 threads, 4096-link chunks
     if (r.cb_shift == 8)
-        hipLaunchKernelGGL((k_bucket_reduce<8, 16>), dim3(r.nb * splits), dim3(256), 0, s, r, splits);
-    else if (r.cb_shift == 9)
-        hipLaunchKernelGGL((k_bucket_reduce<9, 8>), dim3(r.nb * splits), dim3(512), 0, s, r, splits);
-    else
-        hipLaunchKernelGGL((k_bucket_reduce<10, 4>), dim3(r.nb * splits), dim3(1024), 0, s, r, splits);
-    return hipGetLastError();
+        return launch_checked("k_bucket_reduce<8>", k_bucket_reduce<8, 16>, dim3(r.nb * splits), dim3(256), 0, s, r, splits);
+    if (r.cb_shift == 9)
+        return launch_checked("k_bucket_reduce<9>", k_bucket_reduce<9, 8>, dim3(r.nb * splits), dim3(512), 0, s, r, splits);
+    return launch_checked("k_bucket_reduce<10>", k_bucket_reduce<10, 4>, dim3(r.nb * splits), dim3(1024), 0, s, r, splits);
 }
 
 hipError_t launch_link_reduce(const uint64_t* links, const uint32_t* counts, uint64_t stride, uint64_t tiles,
                               uint64_t* table, hipStream_t s) {
     if (!tiles) return hipSuccess;
     const uint64_t grid = tiles < 4096 ? tiles : 4096;
-    hipLaunchKernelGGL(k_link_reduce_atomic, dim3((unsigned)grid), dim3(256), 0, s, links, counts, stride, tiles, table);
-    return hipGetLastError();
+    return launch_checked("k_link_reduce_atomic", k_link_reduce_atomic, dim3((unsigned)grid), dim3(256), 0, s, links,
+                          counts, stride, tiles, table);
 }
 
 }  // namespace zk

@@ -9,6 +9,7 @@
 // them into the global sketch once: byte-wise MAX for registers, SUM for bins. Both merges are
 // order-independent, so the sketch state is bit-identical for any batching or GPU count.
 #include "zk_sketch_internal.h"
+#include "zk_launch.h"
 
 namespace zk {
 namespace {
@@ -152,24 +153,15 @@ __global__ void k_rt_items(const uint32_t* __restrict__ svc, const uint64_t* __r
 hipError_t launch_rt_sketch(const RtArgs& a, hipStream_t s) {
     if (!a.max_units) return hipSuccess;
     const size_t lds = (size_t)((1u << a.p) / 4 + a.nbins) * 4;
-    if (lds > 65536) {
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void*)k_rt_sketch, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-            attr = true;
-        }
-    }
-    hipLaunchKernelGGL(k_rt_sketch, dim3(a.max_units), dim3(kRtWG), lds, s, a);
-    return hipGetLastError();
+    return launch_checked("k_rt_sketch", k_rt_sketch, dim3(a.max_units), dim3(kRtWG), lds, s, a);
 }
 
 hipError_t launch_rt_items(const uint32_t* svc, const uint64_t* trace_id, const int64_t* dur, uint64_t n, uint32_t S,
                            uint32_t p, uint64_t seed, uint32_t* out_svc, uint64_t* out_pay,
                            unsigned long long* dropped, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_rt_items, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, svc, trace_id, dur, n, S, p,
-                       seed, out_svc, out_pay, dropped);
-    return hipGetLastError();
+    return launch_checked("k_rt_items", k_rt_items, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, svc, trace_id,
+                          dur, n, S, p, seed, out_svc, out_pay, dropped);
 }
 
 }  // namespace zk

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "zk_guard.h"
+#include "zk_launch.h"
 #include "zk_internal.h"
 #include "zk_rt_internal.h"
 #include "zk_sketch_internal.h"
@@ -54,7 +55,9 @@ zk_status rfail(zk_rt* r, zk_status s, const std::string& m) {
 #define RT_HIP(rt, call)                                                                                  \
     do {                                                                                                  \
         hipError_t _e = (call);                                                                           \
-        if (_e != hipSuccess) return rfail(rt, ZK_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(_e)); \
+        if (_e != hipSuccess)                                                                          \
+            return rfail(rt, is_refusal(_e) ? ZK_ERR_CAPACITY : ZK_ERR_HIP,                          \
+                        std::string(#call) + ": " + launch_error_str(_e));                             \
     } while (0)
 
 template <class T>

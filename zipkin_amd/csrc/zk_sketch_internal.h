@@ -37,6 +37,10 @@ struct PartitionPlan {
 };
 
 PartitionPlan partition_plan(uint64_t n, uint32_t S, uint32_t cus);
+// which scatter kernel a partition of S services launches: the line scatter when its static LDS plus
+// the [S][8] carry fit one CU, else the item scatter, else none (a refusal); *dyn = its dynamic LDS
+enum { kScatterNone = -1, kScatterItems = 0, kScatterLines = 1 };
+int partition_scatter_choice(uint32_t S, uint64_t static_lines, uint64_t static_items, uint64_t* dyn);
 // Partition of per-workgroup lists instead of one flat range: list w is [w*stride, w*stride +
 // counts[w]) of svc/payload (the item lists K1 writes), one partition workgroup per list.
 PartitionPlan partition_plan_lists(uint32_t lists, uint32_t S);

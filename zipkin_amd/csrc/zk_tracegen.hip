@@ -5,6 +5,7 @@
 
 #include "zk_internal.h"
 #include "zk_tracegen.h"
+#include "zk_launch.h"
 
 namespace zk {
 namespace {
@@ -81,14 +82,12 @@ hipError_t launch_tracegen(const zk_tracegen_params* p, const zk_span_cols* out,
     if (e == hipSuccess) e = hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, counts, incl, (int)T, s);
     if (e == hipSuccess) e = hipMalloc(&tmp, tmp_bytes);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_tg_count, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, s, *p, counts);
-        e = hipGetLastError();
+        e = launch_checked("k_tg_count", k_tg_count, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, s, *p, counts);
     }
     if (e == hipSuccess) e = hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, counts, incl, (int)T, s);
     const uint64_t target = p->target_records ? (p->target_records < cap ? p->target_records : cap) : cap;
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_tg_cut, dim3(1), dim3(1), 0, s, incl, T, target, cut);
-        e = hipGetLastError();
+        e = launch_checked("k_tg_cut", k_tg_cut, dim3(1), dim3(1), 0, s, incl, T, target, cut);
     }
     uint64_t hc[2] = {0, 0};
     if (e == hipSuccess) e = hipMemcpyAsync(hc, cut, 16, hipMemcpyDeviceToHost, s);
@@ -96,9 +95,8 @@ hipError_t launch_tracegen(const zk_tracegen_params* p, const zk_span_cols* out,
     if (e == hipSuccess && hc[0] > 0) {
         ColEmit c{(uint64_t*)out->trace_id, (uint64_t*)out->span_id, (uint64_t*)out->parent_id, (int64_t*)out->first_ts,
                   (int64_t*)out->last_ts,   (uint32_t*)out->service_id, (uint32_t*)out->flags, 0};
-        hipLaunchKernelGGL(k_tg_write, dim3((unsigned)((hc[0] + 255) / 256)), dim3(256), 0, s, *p, hc[0], incl,
-                           counts, c);
-        e = hipGetLastError();
+        e = launch_checked("k_tg_write", k_tg_write, dim3((unsigned)((hc[0] + 255) / 256)), dim3(256), 0, s, *p, hc[0],
+                           incl, counts, c);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
     }
     hipFree(counts);
