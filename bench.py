@@ -141,6 +141,9 @@ def main():
         sc = DeviceColumns(n, device=f"cuda:{local}")
         for k in ("trace_id", "span_id", "parent_id", "first_ts", "last_ts", "service_id", "flags"):
             torch.index_select(getattr(cols, k)[:n], 0, perm, out=getattr(sc, k))
+        # the gathers run on `stream`; the second table set's context later writes memory torch may
+        # recycle from `perm` on ANOTHER stream, so the gathers must be done before perm is released
+        torch.cuda.synchronize()
         del perm
         cols = sc
     out = {
@@ -212,6 +215,14 @@ def main():
                 finalize_oldest()
             torch.cuda.set_stream(stream)
 
+    debug = os.environ.get("ZK_BENCH_DEBUG") == "1"
+
+    def csum(c):
+        return [int(getattr(c, k)[:n].to(torch.int64).sum().item()) for k in
+                ("trace_id", "span_id", "parent_id", "first_ts", "last_ts", "service_id", "flags")]
+
+    if debug:
+        sums0 = (csum(cols), csum(clustered_cols))
     # warmup: serial steps first (their K1 launches give the isolated K1 duration), then two
     # pipelined steps so that the second set's buffers exist before the timed region
     # (at least ISOLATED + 1 serial steps: untimed, outside the timed region, so that the isolated K1
@@ -274,6 +285,9 @@ def main():
                     raise RuntimeError(f"pipelined step: output '{k}' differs between the table sets")
             c2.close()
 
+    if debug:
+        sums1 = (csum(cols), csum(clustered_cols))
+        print(f"[debug] column sums before/after: {sums0 == sums1} {sums0} {sums1}", file=sys.stderr, flush=True)
     cpu = parity = None
     shuffled_parity = None
     if shuffled:
@@ -287,7 +301,9 @@ def main():
         bad = [k for k in out if not torch.equal(out[k], ref_out[k])]
         bad += [k for k, v in stc.items() if k != "spilled_traces" and st[k] != v]
         if bad:
-            raise RuntimeError(f"shuffled batch differs from the clustered batch: {bad}")
+            ncell = int((out["m0"] != ref_out["m0"]).sum())
+            raise RuntimeError(f"shuffled batch differs from the clustered batch: {bad}; {ncell} cells differ in m0; "
+                               f"shuffled stats {st}, clustered stats {stc}")
         shuffled_parity = {"result": "exact", "records": n,
                            "checked": "m0..m4, present and all counters of the shuffled full batch == the clustered batch"}
     if rank == 0 and world == 1 and a.cpu_sample > 0:

@@ -123,3 +123,114 @@ def test_verify_set_grows_over_many_batches(gpu):
 def test_empty_batches(gpu):
     got, st = run([SpanColumns.empty(0), SpanColumns.empty(0)], 5)
     assert got.present.sum() == 0 and st["records"] == 0
+
+
+# ---- the hand-written clustering pass (zk_cluster.hip): every plan shape and its edge cases ----
+M64 = (1 << 64) - 1
+PART_SALT = 0xC2B2AE3D27D4EB4F  # zk_cluster.hip kPartSalt
+
+
+def unmix64(z):
+    """Inverse of zk_mix64 (zk_tracegen.h): lets a test pick a traceId's partition hash."""
+    z = (z ^ (z >> 31) ^ (z >> 62)) & M64
+    z = (z * 0x319642B2D24D8EC3) & M64
+    z = (z ^ (z >> 27) ^ (z >> 54)) & M64
+    z = (z * 0x96DE1B173F119089) & M64
+    return (z ^ (z >> 30) ^ (z >> 60)) & M64
+
+
+@pytest.mark.parametrize("traces,depth", [(1_500, 5), (6_000, 5), (40_000, 6)])
+def test_plan_shapes(gpu, traces, depth):
+    """P3 alone (<= 65536 records), P1 + P3, and P1 + P2 + P3, host and device pointers."""
+    S = 97
+    cols = tracegen_host(55 + traces, traces, max_depth=depth, num_services=S)
+    ref = oracle.aggregate(cols, S)
+    perm = np.random.default_rng(traces).permutation(len(cols))
+    for batch in (cols.take(perm), DeviceColumns.from_host(cols.take(perm))):
+        got, st = run([batch], S)
+        assert_parity(got, st, ref)
+        assert st["not_clustered"] == 0
+
+
+def test_giant_trace_in_a_shuffled_batch(gpu):
+    """One trace of 60k records among ordinary ones: its sub-bucket is done in rounds, and K1's
+    spill kernel then joins it (longer than a window)."""
+    S = 7
+    rows = star_trace(777, 30_000, nsvc=S)
+    for t in range(2_000):
+        rows += star_trace(10_000 + t, 1 + t % 9, svc_root=t % S, nsvc=S)
+    cols = cols_from_rows(rows)
+    ref = oracle.aggregate(cols, S)
+    got, st = run([cols.take(np.random.default_rng(5).permutation(len(cols)))], S)
+    assert_parity(got, st, ref)
+    assert st["spilled_traces"] >= 1
+
+
+def test_singleton_traces_and_extreme_trace_ids(gpu):
+    """300k single-span traces (as many distinct traceIds as records), plus traces 0 and 2^64-1
+    (the trace table's empty-key marker takes its own slot) with many records."""
+    S = 11
+    rng = np.random.default_rng(8)
+    n = 300_000
+    c = SpanColumns.empty(n)
+    c.trace_id[:] = rng.integers(2, 2**64 - 2, n, dtype=np.uint64)
+    c.span_id[:] = rng.integers(1, 2**63, n, dtype=np.uint64)
+    c.first_ts[:] = 1_000
+    c.last_ts[:] = 1_000 + rng.integers(0, 5000, n)
+    c.service_id[:] = rng.integers(0, S, n, dtype=np.uint32)
+    from tests.test_gpu_parity import SERVER
+
+    c.flags[:] = SERVER
+    extra = cols_from_rows(star_trace(0, 3000, nsvc=S) + star_trace(M64, 2500, nsvc=S))
+    cols = SpanColumns.concat([c, extra])
+    ref = oracle.aggregate(cols, S)
+    got, st = run([cols.take(rng.permutation(len(cols)))], S)
+    assert_parity(got, st, ref)
+
+
+def test_every_trace_in_one_sub_bucket(gpu):
+    """Adversarial traceIds: all share the top 24 bits of the partition hash, so every first- and
+    second-level digit is the same and one sub-bucket holds the whole batch (many rounds of the
+    trace table, with restarts when a round's hash range overfills it)."""
+    S = 13
+    rows = []
+    for t in range(12_000):
+        tid = unmix64(((0xABCDEF << 40) | (t * 2654435761 & ((1 << 40) - 1))) & M64) ^ PART_SALT
+        rows += star_trace(tid, 1 + t % 5, svc_root=t % S, nsvc=S)
+    cols = cols_from_rows(rows)
+    assert len(cols) > 65_536  # the partition runs (P1 + P2), not P3 alone
+    ref = oracle.aggregate(cols, S)
+    got, st = run([cols.take(np.random.default_rng(9).permutation(len(cols)))], S)
+    assert_parity(got, st, ref)
+
+
+def test_shuffled_c2_shape_at_scale(gpu):
+    """2e7 device-generated TraceGen records (the bench's shape), shuffled on the device: the result
+    equals the clustered batch's bit for bit (m0..m4 and every counter)."""
+    import torch
+
+    from zipkin_amd import tracegen_params
+
+    S, N = 500, 20_000_000
+    with DepsContext(S) as g:
+        cols = DeviceColumns(N)
+        n, _ = g.tracegen_device(tracegen_params(2, N // 15 + 1000, target_records=N, max_depth=6, num_services=S),
+                                 cols)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(11)
+    perm = torch.randperm(n, device="cuda", generator=gen)
+    sc = DeviceColumns(n)
+    for k in ("trace_id", "span_id", "parent_id", "first_ts", "last_ts", "service_id", "flags"):
+        torch.index_select(getattr(cols, k)[:n], 0, perm, out=getattr(sc, k))
+    torch.cuda.synchronize()  # the contexts below run on their own streams
+    with DepsContext(S) as a:
+        a.accumulate(cols, clustered=True, verify=True, n=n)
+        ra, sa = a.finalize(), a.stats()
+    with DepsContext(S) as b:
+        b.accumulate(sc, clustered=False, verify=True)
+        rb, sb = b.finalize(), b.stats()
+    for k in ("m0", "m1", "m2", "m3", "m4", "present"):
+        assert np.array_equal(getattr(ra, k), getattr(rb, k)), k
+    for k in sa:
+        if k != "spilled_traces":
+            assert sa[k] == sb[k], k

@@ -64,10 +64,9 @@ struct zk_ctx {
     bool folded = false;                  // zk_deps_partial folded this ctx's counters into the table tail
                                           // since the last reset / accumulate (note_merged requires it)
     // clustering pass for unclustered batches (zk_cluster.hip)
-    uint8_t* cl_cols = nullptr;           // 7 aligned columns of cl_cap records
+    uint8_t* cl_cols = nullptr;           // 2 x 7 aligned columns of cl_cap records (the passes ping-pong)
     uint64_t cl_cap = 0;
-    uint32_t* cl_idx = nullptr;
-    void* cl_temp = nullptr;
+    void* cl_temp = nullptr;              // partition histograms, offsets, bucket bounds, scan scratch
     size_t cl_temp_bytes = 0;
     // traceIds accumulated since reset (ZK_BATCH_VERIFY_TRACES): tset_slots + 1 u64
     uint64_t* tset = nullptr;
@@ -226,24 +225,30 @@ zk_status cluster_batch(zk_ctx* c, SpanColsDev* d) {
     RoctxRange rr("zk_cluster_batch");
     const uint64_t n = d->n;
     if (n > 0xFFFFFFFFull) return fail(c, ZK_ERR_CAPACITY, "an unclustered batch is limited to 2^32-1 records");
+    const ClusterPlan plan = cluster_plan(n, c->cus);
+    const uint64_t tb = cluster_scratch_bytes(plan);
     if (n > c->cl_cap) {
         hipFree(c->cl_cols);
-        hipFree(c->cl_idx);
-        hipFree(c->cl_temp);
         c->cl_cols = nullptr;
-        c->cl_idx = nullptr;
-        c->cl_temp = nullptr;
         c->cl_cap = 0;
-        size_t tb = 0;
-        ZK_HIP(c, cluster_temp_bytes(n, &tb));
-        ZK_HIP(c, hipMalloc(&c->cl_cols, carved_bytes(n)));
-        ZK_HIP(c, hipMalloc(&c->cl_idx, n * sizeof(uint32_t)));
-        ZK_HIP(c, hipMalloc(&c->cl_temp, tb));
-        c->cl_temp_bytes = tb;
+        if (hipMalloc(&c->cl_cols, 2 * carved_bytes(n)) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(c, ZK_ERR_CAPACITY, "no device memory for the clustering pass (96 B per record)");
+        }
         c->cl_cap = n;
     }
-    const SpanColsMut m = carve_cols(c->cl_cols, n);
-    ZK_HIP(c, launch_cluster(*d, m, c->cl_idx, c->cl_temp, c->cl_temp_bytes, c->stream));
+    if (tb > c->cl_temp_bytes) {
+        hipFree(c->cl_temp);
+        c->cl_temp = nullptr;
+        c->cl_temp_bytes = 0;
+        ZK_HIP(c, hipMalloc(&c->cl_temp, tb));
+        c->cl_temp_bytes = tb;
+    }
+    const SpanColsMut A = carve_cols(c->cl_cols, n);
+    const SpanColsMut B = carve_cols(c->cl_cols + carved_bytes(n), n);
+    int res = 0;
+    ZK_HIP(c, launch_cluster(plan, *d, A, B, c->cl_temp, c->cus, c->stream, &res));
+    const SpanColsMut& m = res ? B : A;
     *d = SpanColsDev{m.trace_id, m.span_id, m.parent_id, m.first_ts, m.last_ts, m.service_id, m.flags, n};
     return ZK_OK;
 }
@@ -390,7 +395,6 @@ zk_status zk_ctx_destroy(zk_ctx* c) {
     hipFree(c->stage);
     hipFree(c->fin_stage);
     hipFree(c->cl_cols);
-    hipFree(c->cl_idx);
     hipFree(c->cl_temp);
     hipFree(c->tset);
     for (auto* v : {&c->ev_free, &c->ev_join, &c->ev_reduce, &c->ev_spill, &c->ev_fin, &c->ev_cluster})

@@ -14,11 +14,20 @@ struct SpanColsMut {
     uint32_t* flags;
 };
 
-// rocprim scratch for clustering n records
-hipError_t cluster_temp_bytes(uint64_t n, size_t* bytes);
-// in (any order) -> out (trace-clustered: stable sort by traceId); idx: n u32 scratch
-hipError_t launch_cluster(const SpanColsDev& in, const SpanColsMut& out, uint32_t* idx, void* temp, size_t temp_bytes,
-                          hipStream_t s);
+// clustering pass (zk_cluster.hip): b1 + b2 digit bits of the traceId hash (first level P1 global,
+// second level P2 per bucket), then P3 per sub-bucket; b1 = 0: P3 alone over the whole batch
+constexpr uint64_t kClusterSmall = 65536;
+struct ClusterPlan {
+    uint64_t n;
+    uint32_t b1, b2, nb1, nb2;
+    uint32_t grid;  // P0 / P1 workgroups
+    uint64_t per;   // records per P0 / P1 workgroup (whole 8192-record chunks)
+};
+ClusterPlan cluster_plan(uint64_t n, uint32_t cus);
+uint64_t cluster_scratch_bytes(const ClusterPlan& p);
+// in (any order) -> trace-clustered columns in A (*result = 0) or B (*result = 1); both hold n records
+hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const SpanColsMut& A, const SpanColsMut& B,
+                          void* scratch, uint32_t cus, hipStream_t s, int* result);
 // insert the traceId of every segment start into `set` (slots: power of two; slot `slots` counts
 // traceId 0); *dup += segments whose traceId was already present
 hipError_t launch_trace_set_insert(const uint64_t* trace_id, uint64_t n, uint64_t* set, uint64_t slots,

@@ -1,22 +1,43 @@
-// zk_cluster.hip — order-agnostic input and the trace-clustering check.
+// zk_cluster.hip — order-agnostic input: a hand-written traceId-hash partition, and the
+// trace-clustering check.
 //
 // The reference job accepts span fragments in any order: Scalding shuffles them by key before
 // every reduce (groupBy((id, traceId)) at ZipkinAggregateJob.scala:21-22, the (parentId, traceId)
-// join key at :28-33). K1 instead merges and joins inside a trace segment, so it needs every
-// fragment of a trace to be adjacent. Two device pieces bridge that:
+// join key at :28-33). K1 merges and joins inside a trace segment, so it needs every fragment of a
+// trace adjacent. The clustering pass makes a batch in any order trace-clustered, MSD-radix style
+// on the digits of a hash of the traceId -- the traceId is in the shuffle key of both reference
+// joins, so a trace never straddles two buckets:
 //
-//  * clustering pass (batches without ZK_BATCH_TRACE_CLUSTERED): a radix sort of the 64-bit
-//    traceIds carrying the record index (rocprim, stable), then one gather of the seven columns
-//    into ctx-owned, 16-byte-aligned scratch columns. The full 64-bit key is sorted: clustering
-//    on any narrower hash would interleave two traces whose hashes collide.
-//  * trace set (ZK_BATCH_VERIFY_TRACES): every trace segment start inserts its traceId into an
-//    open-addressing set of all traceIds accumulated since the last reset. A traceId found again
-//    means a trace split into two non-adjacent runs, or spread over two accumulate calls -- both
-//    would be mis-joined silently -- and is counted in ST_NOT_CLUSTERED (finalize then returns
-//    ZK_ERR_NOT_CLUSTERED). Exact: the set stores whole traceIds, so it has no false positives.
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
+//   P0 k_cl_hist     per-workgroup LDS histogram of the first digit (top hash bits) of a contiguous
+//                    input range; one exclusive scan (hipcub) of the digit-major matrix gives every
+//                    (digit, workgroup) pair a disjoint output range
+//   P1 k_cl_scatter  each workgroup re-reads its range in chunks of 8192 records: digits ranked in
+//      <global>      LDS (atomic counting sort), then column by column the chunk is loaded
+//                    coalesced, staged in LDS in digit order and written as per-digit runs at the
+//                    ranges' cursors
+//   P2 k_cl_scatter  one workgroup per first-level bucket: an LDS histogram of the second digit over
+//      <local>       the bucket, its scan (the sub-bucket bounds), then the same chunked scatter
+//                    inside the bucket
+//   P3 k_cl_traces   one workgroup per sub-bucket (~1k records): an LDS hash table of the
+//                    sub-bucket's distinct traceIds counts each trace's records, a scan places the
+//                    traces, and a second sweep writes every record to its trace's run -- the
+//                    output is exactly trace-clustered (a sub-bucket larger than 2048 records is
+//                    done in several rounds, each taking a hash range of its traceIds)
+//
+// Small batches run P3 alone over the whole batch. Traffic per record: 8 B (P0) + 104 B (P1:
+// traceIds twice, every column once, written once) + 112 B (P2, plus its histogram sweep) + 104 B
+// (P3). Round 2 used rocprim's radix_sort_pairs over the 64-bit traceIds and a gather of the
+// columns by the sorted index (random 8-byte reads): 21 ms per 1e8 records on MI355X against
+// 1.2 ms for K1 (profiles/r03/).
+//
+// The trace set (ZK_BATCH_VERIFY_TRACES): every trace segment start inserts its traceId into an
+// open-addressing set of all traceIds accumulated since the last reset. A traceId found again
+// means a trace split into two non-adjacent runs, or spread over two accumulate calls -- both
+// would be mis-joined silently -- and is counted in ST_NOT_CLUSTERED (finalize then returns
+// ZK_ERR_NOT_CLUSTERED). Exact: the set stores whole traceIds, so it has no false positives.
+#include <hipcub/hipcub.hpp>
 
+#include "zk_block.h"
 #include "zk_cluster.h"
 #include "zk_launch.h"
 #include "zk_tracegen.h"
@@ -25,6 +46,15 @@ namespace zk {
 namespace {
 
 constexpr uint64_t kSetSalt = 0x6A09E667F3BCC909ull;
+// the partition hash: independent of the shard function mix64(traceId) % world (zk_trace_shard)
+// and of TraceGen's traceId construction (traceId = mix64^-1(k * world + rank))
+constexpr uint64_t kPartSalt = 0xC2B2AE3D27D4EB4Full;
+constexpr uint64_t kTraceSalt = 0x165667B19E3779F9ull;
+
+__device__ __forceinline__ uint64_t part_hash(uint64_t tid) { return zk_mix64(tid ^ kPartSalt); }
+__device__ __forceinline__ uint32_t digit_of(uint64_t h, uint32_t shift, uint32_t mask) {
+    return (uint32_t)(h >> shift) & mask;
+}
 
 __device__ __forceinline__ uint64_t set_slot(uint64_t tid, uint64_t mask) { return zk_mix64(tid ^ kSetSalt) & mask; }
 
@@ -39,22 +69,348 @@ __device__ __forceinline__ bool set_insert(unsigned long long* set, uint64_t mas
     }
 }
 
-__global__ __launch_bounds__(256) void k_gather_cols(SpanColsDev in, const uint32_t* __restrict__ idx,
-                                                     SpanColsMut out) {
-    const uint64_t n = in.n;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t j = idx[i];
-        out.span_id[i] = in.span_id[j];
-        out.parent_id[i] = in.parent_id[j];
-        out.first_ts[i] = in.first_ts[j];
-        out.last_ts[i] = in.last_ts[j];
-        out.service_id[i] = in.service_id[j];
-        out.flags[i] = in.flags[j];
+// ---- P0: per-workgroup digit histogram -----------------------------------------------------------
+constexpr int kHistWG = 256;
+constexpr int kHistU = 8;
+
+__global__ __launch_bounds__(kHistWG) void k_cl_hist(const uint64_t* __restrict__ tid, uint64_t n, uint64_t per,
+                                                      uint32_t shift, uint32_t nd, uint32_t grid,
+                                                      uint32_t* __restrict__ hist) {
+    extern __shared__ uint32_t h[];
+    for (uint32_t i = threadIdx.x; i < nd; i += kHistWG) h[i] = 0u;
+    __syncthreads();
+    const uint64_t lo = (uint64_t)blockIdx.x * per;
+    const uint64_t hi = lo + per < n ? lo + per : n;
+    const uint32_t mask = nd - 1;
+    for (uint64_t b = lo; b < hi; b += (uint64_t)kHistWG * kHistU) {
+        uint64_t v[kHistU];
+#pragma unroll
+        for (int e = 0; e < kHistU; ++e) {
+            const uint64_t i = b + (uint64_t)e * kHistWG + threadIdx.x;
+            v[e] = tid[i < hi ? i : lo];
+        }
+#pragma unroll
+        for (int e = 0; e < kHistU; ++e) {
+            const uint64_t i = b + (uint64_t)e * kHistWG + threadIdx.x;
+            if (i < hi) atomicAdd(&h[digit_of(part_hash(v[e]), shift, mask)], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < nd; d += kHistWG) hist[(uint64_t)d * grid + blockIdx.x] = h[d];
+}
+
+// bucket bounds from the scanned matrix: base[d] = offs[d * grid] (the first workgroup's range of
+// digit d), base[nd] = n
+__global__ void k_cl_bounds(const uint32_t* __restrict__ offs, uint32_t nd, uint32_t grid, uint64_t n,
+                            uint32_t* __restrict__ base) {
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d < nd) base[d] = offs[(uint64_t)d * grid];
+    if (d == nd) base[nd] = (uint32_t)n;
+}
+
+// ---- P1 / P2: chunked LDS-staged scatter ---------------------------------------------------------
+constexpr int kScWG = 1024;
+constexpr int kScU = 8;
+constexpr int kScChunk = kScWG * kScU;  // 8192 records per chunk
+constexpr uint32_t kMaxDigits = 2048;   // <= 11 bits per level
+
+struct ScatterArgs {
+    SpanColsDev in;  // in.n = records of the whole batch
+    SpanColsMut out;
+    // global (P1): workgroup w owns [w * per, ...) and its digit cursors start at offs[d * grid + w]
+    uint64_t per;
+    uint32_t grid;
+    const uint32_t* offs;
+    // local (P2): workgroup b owns bucket [bucket[b], bucket[b + 1]) and writes its sub-bucket
+    // bounds to sub[b * nd + d] (and sub[nbuckets * nd] = n)
+    const uint32_t* bucket;
+    uint32_t nbuckets;
+    uint32_t* sub;
+    uint32_t shift, nd;  // digit = (hash >> shift) & (nd - 1)
+};
+
+// one column of a chunk: coalesced loads, LDS stage in digit order, coalesced per-digit runs out
+template <class T>
+__device__ __forceinline__ void scatter_column(const T* __restrict__ src, T* __restrict__ dst, uint64_t base,
+                                               uint32_t cnt, const uint32_t (&pos)[kScU],
+                                               const uint32_t (&dest)[kScU], T* stage) {
+    const int t = threadIdx.x;
+    T v[kScU];
+#pragma unroll
+    for (int k = 0; k < kScU; ++k) {
+        const uint32_t j = t + k * kScWG;
+        v[k] = src[base + (j < cnt ? j : 0)];
+    }
+#pragma unroll
+    for (int k = 0; k < kScU; ++k)
+        if (t + k * kScWG < cnt) stage[pos[k]] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kScU; ++k) {
+        const uint32_t i = t + k * kScWG;
+        if (i < cnt) dst[dest[k]] = stage[i];
+    }
+    __syncthreads();
+}
+
+// exclusive scan of s_cnt[0..nd) into out[d] = add + offset (one pass of the whole workgroup)
+template <int WG>
+__device__ __forceinline__ void scan_digits(const uint32_t* s_cnt, uint32_t nd, uint32_t add, uint32_t* out,
+                                            uint32_t* s_tmp) {
+    constexpr int DPT = (kMaxDigits + WG - 1) / WG;
+    const int t = threadIdx.x;
+    uint32_t h[DPT], sum = 0;
+#pragma unroll
+    for (int q = 0; q < DPT; ++q) {
+        const uint32_t d = t * DPT + q;
+        h[q] = d < nd ? s_cnt[d] : 0u;
+        sum += h[q];
+    }
+    uint32_t tot;
+    uint32_t ex = block_excl_scan<WG / 64>(sum, s_tmp, &tot);
+#pragma unroll
+    for (int q = 0; q < DPT; ++q) {
+        const uint32_t d = t * DPT + q;
+        if (d < nd) out[d] = add + ex;
+        ex += h[q];
     }
 }
 
-// One lane per record: a record whose traceId differs from its predecessor's starts a segment.
-// set[slots] counts segments of the traceId 0 (the empty-slot marker cannot be stored).
+template <bool LOCAL>
+__global__ __launch_bounds__(kScWG) void k_cl_scatter(ScatterArgs a) {
+    __shared__ uint32_t s_cur[kMaxDigits];  // output position of each digit's next record
+    __shared__ uint32_t s_cnt[kMaxDigits];  // records of the chunk per digit
+    __shared__ uint32_t s_off[kMaxDigits];  // exclusive offsets of the digits inside the sorted chunk
+    __shared__ uint16_t s_dig[kScChunk];    // digit of the sorted chunk's record i
+    __shared__ __align__(16) uint64_t s_stage[kScChunk];
+    __shared__ uint32_t s_tmp[32];
+    const int t = threadIdx.x;
+    const uint32_t nd = a.nd, mask = nd - 1;
+    uint64_t lo, hi;
+    if constexpr (LOCAL) {
+        lo = a.bucket[blockIdx.x];
+        hi = a.bucket[blockIdx.x + 1];
+        // sweep 1: the bucket's histogram of the second digit, then the sub-bucket bounds
+        for (uint32_t d = t; d < nd; d += kScWG) s_cnt[d] = 0u;
+        __syncthreads();
+        for (uint64_t b = lo; b < hi; b += (uint64_t)kScChunk) {
+            uint64_t v[kScU];
+#pragma unroll
+            for (int k = 0; k < kScU; ++k) {
+                const uint64_t i = b + t + (uint64_t)k * kScWG;
+                v[k] = a.in.trace_id[i < hi ? i : lo];
+            }
+#pragma unroll
+            for (int k = 0; k < kScU; ++k)
+                if (b + t + (uint64_t)k * kScWG < hi) atomicAdd(&s_cnt[digit_of(part_hash(v[k]), a.shift, mask)], 1u);
+        }
+        __syncthreads();
+        scan_digits<kScWG>(s_cnt, nd, (uint32_t)lo, s_cur, s_tmp);
+        __syncthreads();
+        for (uint32_t d = t; d < nd; d += kScWG) a.sub[(uint64_t)blockIdx.x * nd + d] = s_cur[d];
+        if (blockIdx.x == a.nbuckets - 1 && t == 0) a.sub[(uint64_t)a.nbuckets * nd] = (uint32_t)a.in.n;
+    } else {
+        lo = (uint64_t)blockIdx.x * a.per;
+        hi = lo + a.per < a.in.n ? lo + a.per : a.in.n;
+        for (uint32_t d = t; d < nd; d += kScWG) s_cur[d] = a.offs[(uint64_t)d * a.grid + blockIdx.x];
+    }
+    for (uint32_t d = t; d < nd; d += kScWG) s_cnt[d] = 0u;
+    __syncthreads();
+    for (uint64_t base = lo; base < hi; base += kScChunk) {
+        const uint32_t cnt = (uint32_t)(hi - base < (uint64_t)kScChunk ? hi - base : (uint64_t)kScChunk);
+        // 1. digits and ranks (LDS atomic counting sort: the order inside a digit is free)
+        uint32_t dg[kScU], rank[kScU];
+        {
+            uint64_t v[kScU];
+#pragma unroll
+            for (int k = 0; k < kScU; ++k) {
+                const uint32_t j = t + k * kScWG;
+                v[k] = a.in.trace_id[base + (j < cnt ? j : 0)];
+            }
+#pragma unroll
+            for (int k = 0; k < kScU; ++k) {
+                dg[k] = digit_of(part_hash(v[k]), a.shift, mask);
+                rank[k] = (t + k * kScWG < cnt) ? atomicAdd(&s_cnt[dg[k]], 1u) : 0u;
+            }
+        }
+        __syncthreads();
+        // 2. digit offsets inside the chunk
+        scan_digits<kScWG>(s_cnt, nd, 0u, s_off, s_tmp);
+        __syncthreads();
+        // 3. sorted position of each loaded record; digit of each sorted slot
+        uint32_t pos[kScU], dest[kScU];
+#pragma unroll
+        for (int k = 0; k < kScU; ++k) {
+            pos[k] = s_off[dg[k]] + rank[k];
+            if (t + k * kScWG < cnt) s_dig[pos[k]] = (uint16_t)dg[k];
+        }
+        __syncthreads();
+        // 4. output position of each sorted slot this thread writes
+#pragma unroll
+        for (int k = 0; k < kScU; ++k) {
+            const uint32_t i = t + k * kScWG;
+            const uint32_t d = i < cnt ? s_dig[i] : 0u;
+            dest[k] = i < cnt ? s_cur[d] + (i - s_off[d]) : 0u;
+        }
+        // 5. the columns, one at a time through the LDS stage
+        scatter_column<uint64_t>(a.in.trace_id, a.out.trace_id, base, cnt, pos, dest, s_stage);
+        scatter_column<uint64_t>(a.in.span_id, a.out.span_id, base, cnt, pos, dest, s_stage);
+        scatter_column<uint64_t>(a.in.parent_id, a.out.parent_id, base, cnt, pos, dest, s_stage);
+        scatter_column<uint64_t>((const uint64_t*)a.in.first_ts, (uint64_t*)a.out.first_ts, base, cnt, pos, dest,
+                                 s_stage);
+        scatter_column<uint64_t>((const uint64_t*)a.in.last_ts, (uint64_t*)a.out.last_ts, base, cnt, pos, dest,
+                                 s_stage);
+        scatter_column<uint32_t>(a.in.service_id, a.out.service_id, base, cnt, pos, dest, (uint32_t*)s_stage);
+        scatter_column<uint32_t>(a.in.flags, a.out.flags, base, cnt, pos, dest, (uint32_t*)s_stage);
+        // 6. advance the cursors and clear the counts (scatter_column's last barrier orders every
+        //    read of s_cur / s_off / s_cnt above before these writes)
+        for (uint32_t d = t; d < nd; d += kScWG) {
+            s_cur[d] += s_cnt[d];
+            s_cnt[d] = 0u;
+        }
+        __syncthreads();
+    }
+}
+
+// ---- P3: trace runs inside each sub-bucket --------------------------------------------------------
+constexpr int kTrWG = 512;
+constexpr uint32_t kTrSlots = 4096;    // LDS trace table: load <= 1/2 at <= 2048 records per round
+constexpr uint64_t kEmptyKey = ~0ull;  // a traceId equal to it takes the extra slot kTrSlots
+
+struct TraceArgs {
+    SpanColsDev in;
+    SpanColsMut out;
+    const uint32_t* sub;  // nsub + 1 sub-bucket bounds
+    uint32_t nsub;
+    unsigned int* next;   // work counter: sub-buckets are handed out one at a time
+};
+
+__device__ __forceinline__ uint64_t trace_hash(uint64_t tid) { return zk_mix64(tid ^ kTraceSalt); }
+
+__global__ __launch_bounds__(kTrWG) void k_cl_traces(TraceArgs a) {
+    __shared__ unsigned long long s_key[kTrSlots];
+    __shared__ uint32_t s_cnt[kTrSlots + 1];  // records per trace, then the trace's run start (scan)
+    __shared__ uint32_t s_cur[kTrSlots + 1];  // records placed per trace
+    __shared__ uint32_t s_work;
+    __shared__ uint32_t s_fail;
+    __shared__ uint32_t s_tmp[32];
+    const int t = threadIdx.x;
+    constexpr int SPT = (kTrSlots + 1 + kTrWG - 1) / kTrWG;
+    for (;;) {
+        __syncthreads();  // every thread is past the previous sub-bucket's reads of s_work and the table
+        if (t == 0) s_work = atomicAdd(a.next, 1u);
+        __syncthreads();
+        const uint32_t w = s_work;
+        if (w >= a.nsub) break;
+        const uint64_t lo = a.sub[w], hi = a.sub[w + 1];
+        const uint64_t len = hi - lo;
+        // rounds of <= 2048 records expected (a hash range of the traceIds each), and a table of a
+        // power of two >= 2 x the round's records: the load stays <= 1/2 whatever the trace sizes
+        // (a round's distinct traceIds are at most its records)
+        uint32_t rounds = 1;
+        while (len / rounds > kTrSlots / 2) rounds <<= 1;
+        uint32_t slots = 64;
+        while (slots < 2 * (len / rounds + 1) && slots < kTrSlots) slots <<= 1;
+        uint32_t smask = slots - 1;
+        uint64_t placed = lo;  // output position of this round's first record
+        for (uint32_t r = 0; r < rounds; ++r) {
+            for (uint32_t s = t; s < slots; s += kTrWG) {
+                s_key[s] = kEmptyKey;
+                s_cnt[s] = 0u;
+                s_cur[s] = 0u;
+            }
+            if (t == 0) {
+                s_cnt[kTrSlots] = 0u;
+                s_cur[kTrSlots] = 0u;
+                s_fail = 0u;
+            }
+            __syncthreads();
+            // sweep 1: count each trace's records of this round
+            for (uint64_t i = lo + t; i < hi; i += kTrWG) {
+                const uint64_t tid = a.in.trace_id[i];
+                const uint64_t th = trace_hash(tid);
+                if (rounds > 1 && (uint32_t)(th >> 40) % rounds != r) continue;
+                uint32_t slot = kTrSlots;
+                if (tid != kEmptyKey) {
+                    slot = (uint32_t)th & smask;
+                    uint32_t probes = 0;
+                    for (;;) {
+                        const unsigned long long k = s_key[slot];
+                        if (k == tid) break;
+                        if (k == kEmptyKey) {
+                            const unsigned long long old = atomicCAS(&s_key[slot], kEmptyKey, (unsigned long long)tid);
+                            if (old == kEmptyKey || old == tid) break;
+                        }
+                        slot = (slot + 1) & smask;
+                        if (++probes >= slots) {  // full: a hash range far above its share of traces
+                            s_fail = 1u;
+                            slot = kTrSlots + 1;
+                            break;
+                        }
+                    }
+                }
+                if (slot <= kTrSlots) atomicAdd(&s_cnt[slot], 1u);
+            }
+            __syncthreads();
+            if (s_fail) {
+                // start the sub-bucket over with twice the rounds (every output position of the
+                // sub-bucket is rewritten by the new layout)
+                rounds <<= 1;
+                slots = 64;
+                while (slots < 2 * (len / rounds + 1) && slots < kTrSlots) slots <<= 1;
+                smask = slots - 1;
+                placed = lo;
+                r = ~0u;  // the loop's ++r makes it round 0
+                __syncthreads();  // every thread read s_fail before the next round clears it
+                continue;
+            }
+            // scan: the run start of each trace of the round (slot order, the extra slot last)
+            {
+                uint32_t h[SPT], sum = 0;
+#pragma unroll
+                for (int q = 0; q < SPT; ++q) {
+                    const uint32_t s = t * SPT + q;
+                    h[q] = (s < slots || s == kTrSlots) ? s_cnt[s] : 0u;
+                    sum += h[q];
+                }
+                uint32_t tot;
+                uint32_t ex = block_excl_scan<kTrWG / 64>(sum, s_tmp, &tot);
+                __syncthreads();  // every thread read its counts before any is overwritten
+#pragma unroll
+                for (int q = 0; q < SPT; ++q) {
+                    const uint32_t s = t * SPT + q;
+                    if (s < slots || s == kTrSlots) s_cnt[s] = ex;
+                    ex += h[q];
+                }
+                if (t == 0) s_tmp[31] = tot;
+            }
+            __syncthreads();
+            const uint32_t round_records = s_tmp[31];
+            // sweep 2: every record of the round to its trace's run
+            for (uint64_t i = lo + t; i < hi; i += kTrWG) {
+                const uint64_t tid = a.in.trace_id[i];
+                const uint64_t th = trace_hash(tid);
+                if (rounds > 1 && (uint32_t)(th >> 40) % rounds != r) continue;
+                uint32_t slot = kTrSlots;
+                if (tid != kEmptyKey) {
+                    slot = (uint32_t)th & smask;
+                    while (s_key[slot] != tid) slot = (slot + 1) & smask;
+                }
+                const uint64_t j = placed + s_cnt[slot] + atomicAdd(&s_cur[slot], 1u);
+                a.out.trace_id[j] = tid;
+                a.out.span_id[j] = a.in.span_id[i];
+                a.out.parent_id[j] = a.in.parent_id[i];
+                a.out.first_ts[j] = a.in.first_ts[i];
+                a.out.last_ts[j] = a.in.last_ts[i];
+                a.out.service_id[j] = a.in.service_id[i];
+                a.out.flags[j] = a.in.flags[i];
+            }
+            placed += round_records;
+            __syncthreads();  // the round's placement reads are done before the next round clears
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_trace_set_insert(const uint64_t* __restrict__ tid, uint64_t n,
                                                           unsigned long long* __restrict__ set, uint64_t slots,
                                                           unsigned long long* __restrict__ dup) {
@@ -105,26 +461,130 @@ unsigned grid_for(uint64_t n) {
     return (unsigned)(g < 8192 ? (g ? g : 1) : 8192);
 }
 
-}  // namespace
+uint64_t align256(uint64_t b) { return (b + 255) & ~255ull; }
 
-hipError_t cluster_temp_bytes(uint64_t n, size_t* bytes) {
+size_t scan_bytes(uint64_t m) {
     size_t b = 0;
-    const hipError_t e = rocprim::radix_sort_pairs(nullptr, b, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                                   rocprim::counting_iterator<uint32_t>(0u), (uint32_t*)nullptr,
-                                                   (uint32_t)n, 0u, 64u, (hipStream_t)0);
-    *bytes = b;
-    return e;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)m);
+    return b;
 }
 
-hipError_t launch_cluster(const SpanColsDev& in, const SpanColsMut& out, uint32_t* idx, void* temp, size_t temp_bytes,
-                          hipStream_t s) {
-    if (in.n == 0) return hipSuccess;
-    size_t b = temp_bytes;
-    // sorted traceIds land directly in the output traceId column
-    hipError_t e = rocprim::radix_sort_pairs(temp, b, in.trace_id, out.trace_id, rocprim::counting_iterator<uint32_t>(0u),
-                                             idx, (uint32_t)in.n, 0u, 64u, s);
+}  // namespace
+
+ClusterPlan cluster_plan(uint64_t n, uint32_t cus) {
+    ClusterPlan p{};
+    p.n = n;
+    // digit bits in all: sub-buckets of ~1k records (one P3 round unless a bucket holds > 2048)
+    uint32_t bits = 0;
+    while (bits < 22 && (n >> bits) > 1024) ++bits;
+    if (n <= kClusterSmall) bits = 0;  // P3 alone: one workgroup over the whole batch
+    if (bits <= 8) {
+        p.b1 = bits;
+        p.b2 = 0;
+    } else {
+        p.b1 = 8;
+        p.b2 = bits - 8;
+        if (p.b2 > 11) {  // > 2^29 records: widen the first level
+            p.b1 = bits - 11;
+            p.b2 = 11;
+        }
+    }
+    p.nb1 = 1u << p.b1;
+    p.nb2 = 1u << p.b2;
+    // P0/P1 geometry: about one resident 1024-thread workgroup per CU, whole chunks each
+    uint64_t g = cus ? cus : 256;
+    const uint64_t chunks = (n + kScChunk - 1) / kScChunk;
+    if (g > chunks) g = chunks ? chunks : 1;
+    p.grid = (uint32_t)g;
+    p.per = ((n + g - 1) / g + kScChunk - 1) / kScChunk * kScChunk;
+    if (!p.per) p.per = kScChunk;
+    return p;
+}
+
+uint64_t cluster_scratch_bytes(const ClusterPlan& p) {
+    const uint64_t m = (uint64_t)p.nb1 * p.grid;
+    return 2 * align256(m * 4) + align256(((uint64_t)p.nb1 + 1) * 4) + align256(((uint64_t)p.nb1 * p.nb2 + 1) * 4) +
+           256 + align256(scan_bytes(m));
+}
+
+hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const SpanColsMut& A, const SpanColsMut& B,
+                          void* scratch, uint32_t cus, hipStream_t s, int* result) {
+    const uint64_t n = in.n;
+    *result = 0;
+    if (n == 0) return hipSuccess;
+    const uint64_t m = (uint64_t)p.nb1 * p.grid;
+    uint8_t* sp = (uint8_t*)scratch;
+    uint32_t* hist = (uint32_t*)sp;
+    uint32_t* offs = (uint32_t*)(sp + align256(m * 4));
+    uint32_t* bucket = (uint32_t*)(sp + 2 * align256(m * 4));
+    uint32_t* sub = (uint32_t*)((uint8_t*)bucket + align256(((uint64_t)p.nb1 + 1) * 4));
+    unsigned int* next = (unsigned int*)((uint8_t*)sub + align256(((uint64_t)p.nb1 * p.nb2 + 1) * 4));
+    void* temp = (uint8_t*)next + 256;
+    hipError_t e = hipMemsetAsync(next, 0, 4, s);
     if (e != hipSuccess) return e;
-    return launch_checked("k_gather_cols", k_gather_cols, dim3(grid_for(in.n)), dim3(256), 0, s, in, idx, out);
+    auto dev = [n](const SpanColsMut& c) {
+        return SpanColsDev{c.trace_id, c.span_id, c.parent_id, c.first_ts, c.last_ts, c.service_id, c.flags, n};
+    };
+    TraceArgs ta{};
+    ta.next = next;
+    if (!p.b1) {  // P3 alone: in -> A
+        const uint32_t h_sub[2] = {0u, (uint32_t)n};
+        e = hipMemcpyAsync(sub, h_sub, 8, hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) return e;
+        ta.in = in;
+        ta.out = A;
+        ta.sub = sub;
+        ta.nsub = 1;
+        *result = 0;
+        return launch_checked("k_cl_traces", k_cl_traces, dim3(1), dim3(kTrWG), 0, s, ta);
+    }
+    // P0 + scan + first-level bucket bounds
+    const uint32_t sh1 = 64 - p.b1;
+    e = launch_checked("k_cl_hist", k_cl_hist, dim3(p.grid), dim3(kHistWG), (size_t)p.nb1 * 4, s, in.trace_id, n, p.per,
+                       sh1, p.nb1, p.grid, hist);
+    if (e != hipSuccess) return e;
+    size_t temp_bytes = scan_bytes(m);
+    e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, hist, offs, (int)m, s);
+    if (e != hipSuccess) return e;
+    e = launch_checked("k_cl_bounds", k_cl_bounds, dim3((p.nb1 + 256) / 256), dim3(256), 0, s, offs, p.nb1, p.grid, n,
+                       bucket);
+    if (e != hipSuccess) return e;
+    // P1: in -> A (first-level buckets)
+    ScatterArgs a{};
+    a.in = in;
+    a.out = A;
+    a.per = p.per;
+    a.grid = p.grid;
+    a.offs = offs;
+    a.shift = sh1;
+    a.nd = p.nb1;
+    e = launch_checked("k_cl_scatter<global>", k_cl_scatter<false>, dim3(p.grid), dim3(kScWG), 0, s, a);
+    if (e != hipSuccess) return e;
+    if (!p.b2) {  // P3: A -> B
+        ta.in = dev(A);
+        ta.out = B;
+        ta.sub = bucket;
+        ta.nsub = p.nb1;
+        *result = 1;
+    } else {  // P2: A -> B (sub-buckets), P3: B -> A
+        ScatterArgs b{};
+        b.in = dev(A);
+        b.out = B;
+        b.bucket = bucket;
+        b.nbuckets = p.nb1;
+        b.sub = sub;
+        b.shift = sh1 - p.b2;
+        b.nd = p.nb2;
+        e = launch_checked("k_cl_scatter<local>", k_cl_scatter<true>, dim3(p.nb1), dim3(kScWG), 0, s, b);
+        if (e != hipSuccess) return e;
+        ta.in = dev(B);
+        ta.out = A;
+        ta.sub = sub;
+        ta.nsub = p.nb1 * p.nb2;
+        *result = 0;
+    }
+    const uint32_t g3 = ta.nsub < 2 * cus ? ta.nsub : 2 * cus;
+    return launch_checked("k_cl_traces", k_cl_traces, dim3(g3), dim3(kTrWG), 0, s, ta);
 }
 
 hipError_t launch_trace_set_insert(const uint64_t* trace_id, uint64_t n, uint64_t* set, uint64_t slots,
