@@ -129,28 +129,56 @@ struct ScatterArgs {
     uint32_t shift, nd;  // digit = (hash >> shift) & (nd - 1)
 };
 
-// one column of a chunk: coalesced loads, LDS stage in digit order, coalesced per-digit runs out
-template <class T>
-__device__ __forceinline__ void scatter_column(const T* __restrict__ src, T* __restrict__ dst, uint64_t base,
-                                               uint32_t cnt, const uint32_t (&pos)[kScU],
-                                               const uint32_t (&dest)[kScU], T* stage) {
+// column C (0..6) of a batch: the u64 columns first, then service_id and flags (u32)
+template <int C>
+__device__ __forceinline__ uint64_t col_load(const SpanColsDev& c, uint64_t i) {
+    if constexpr (C == 0) return c.trace_id[i];
+    if constexpr (C == 1) return c.span_id[i];
+    if constexpr (C == 2) return c.parent_id[i];
+    if constexpr (C == 3) return (uint64_t)c.first_ts[i];
+    if constexpr (C == 4) return (uint64_t)c.last_ts[i];
+    if constexpr (C == 5) return c.service_id[i];
+    return c.flags[i];
+}
+template <int C>
+__device__ __forceinline__ void col_store(const SpanColsMut& c, uint64_t i, uint64_t v) {
+    if constexpr (C == 0) c.trace_id[i] = v;
+    if constexpr (C == 1) c.span_id[i] = v;
+    if constexpr (C == 2) c.parent_id[i] = v;
+    if constexpr (C == 3) c.first_ts[i] = (int64_t)v;
+    if constexpr (C == 4) c.last_ts[i] = (int64_t)v;
+    if constexpr (C == 5) c.service_id[i] = (uint32_t)v;
+    if constexpr (C == 6) c.flags[i] = (uint32_t)v;
+}
+
+// Move the seven columns of rows base + t + k*WG (k < U, those < cnt) through the LDS stage: row
+// (t, k) goes to stage slot pos[k], and the thread writes stage slot t + k*WG to out row dest[k].
+// v holds column 0 (the traceIds) of the thread's rows on entry.
+// Coalesced loads and coalesced per-run stores; column C + 1's loads are issued before column C's
+// stores, so a column's HBM latency hides behind the previous column's LDS round trip.
+template <int U, int WG, int C = 0>
+__device__ __forceinline__ void move_columns(const SpanColsDev& in, const SpanColsMut& out, uint64_t base,
+                                             uint32_t cnt, const uint32_t (&pos)[U], const uint64_t (&dest)[U],
+                                             uint64_t* stage, uint64_t (&v)[U]) {
     const int t = threadIdx.x;
-    T v[kScU];
 #pragma unroll
-    for (int k = 0; k < kScU; ++k) {
-        const uint32_t j = t + k * kScWG;
-        v[k] = src[base + (j < cnt ? j : 0)];
+    for (int k = 0; k < U; ++k)
+        if (t + k * WG < cnt) stage[pos[k]] = v[k];
+    __syncthreads();
+    if constexpr (C < 6) {
+#pragma unroll
+        for (int k = 0; k < U; ++k) {  // the next column, in flight during this column's stores
+            const uint32_t j = t + k * WG;
+            v[k] = col_load<C + 1>(in, base + (j < cnt ? j : 0));
+        }
     }
 #pragma unroll
-    for (int k = 0; k < kScU; ++k)
-        if (t + k * kScWG < cnt) stage[pos[k]] = v[k];
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kScU; ++k) {
-        const uint32_t i = t + k * kScWG;
-        if (i < cnt) dst[dest[k]] = stage[i];
+    for (int k = 0; k < U; ++k) {
+        const uint32_t i = t + k * WG;
+        if (i < cnt) col_store<C>(out, dest[k], stage[i]);
     }
     __syncthreads();
+    if constexpr (C < 6) move_columns<U, WG, C + 1>(in, out, base, cnt, pos, dest, stage, v);
 }
 
 // exclusive scan of s_cnt[0..nd) into out[d] = add + offset (one pass of the whole workgroup)
@@ -220,25 +248,24 @@ __global__ __launch_bounds__(kScWG) void k_cl_scatter(ScatterArgs a) {
         const uint32_t cnt = (uint32_t)(hi - base < (uint64_t)kScChunk ? hi - base : (uint64_t)kScChunk);
         // 1. digits and ranks (LDS atomic counting sort: the order inside a digit is free)
         uint32_t dg[kScU], rank[kScU];
-        {
-            uint64_t v[kScU];
+        uint64_t tids[kScU];
 #pragma unroll
-            for (int k = 0; k < kScU; ++k) {
-                const uint32_t j = t + k * kScWG;
-                v[k] = a.in.trace_id[base + (j < cnt ? j : 0)];
-            }
+        for (int k = 0; k < kScU; ++k) {
+            const uint32_t j = t + k * kScWG;
+            tids[k] = a.in.trace_id[base + (j < cnt ? j : 0)];
+        }
 #pragma unroll
-            for (int k = 0; k < kScU; ++k) {
-                dg[k] = digit_of(part_hash(v[k]), a.shift, mask);
-                rank[k] = (t + k * kScWG < cnt) ? atomicAdd(&s_cnt[dg[k]], 1u) : 0u;
-            }
+        for (int k = 0; k < kScU; ++k) {
+            dg[k] = digit_of(part_hash(tids[k]), a.shift, mask);
+            rank[k] = (t + k * kScWG < cnt) ? atomicAdd(&s_cnt[dg[k]], 1u) : 0u;
         }
         __syncthreads();
         // 2. digit offsets inside the chunk
         scan_digits<kScWG>(s_cnt, nd, 0u, s_off, s_tmp);
         __syncthreads();
         // 3. sorted position of each loaded record; digit of each sorted slot
-        uint32_t pos[kScU], dest[kScU];
+        uint32_t pos[kScU];
+        uint64_t dest[kScU];
 #pragma unroll
         for (int k = 0; k < kScU; ++k) {
             pos[k] = s_off[dg[k]] + rank[k];
@@ -250,19 +277,16 @@ __global__ __launch_bounds__(kScWG) void k_cl_scatter(ScatterArgs a) {
         for (int k = 0; k < kScU; ++k) {
             const uint32_t i = t + k * kScWG;
             const uint32_t d = i < cnt ? s_dig[i] : 0u;
-            dest[k] = i < cnt ? s_cur[d] + (i - s_off[d]) : 0u;
+            dest[k] = i < cnt ? (uint64_t)s_cur[d] + (i - s_off[d]) : 0ull;
         }
-        // 5. the columns, one at a time through the LDS stage
-        scatter_column<uint64_t>(a.in.trace_id, a.out.trace_id, base, cnt, pos, dest, s_stage);
-        scatter_column<uint64_t>(a.in.span_id, a.out.span_id, base, cnt, pos, dest, s_stage);
-        scatter_column<uint64_t>(a.in.parent_id, a.out.parent_id, base, cnt, pos, dest, s_stage);
-        scatter_column<uint64_t>((const uint64_t*)a.in.first_ts, (uint64_t*)a.out.first_ts, base, cnt, pos, dest,
-                                 s_stage);
-        scatter_column<uint64_t>((const uint64_t*)a.in.last_ts, (uint64_t*)a.out.last_ts, base, cnt, pos, dest,
-                                 s_stage);
-        scatter_column<uint32_t>(a.in.service_id, a.out.service_id, base, cnt, pos, dest, (uint32_t*)s_stage);
-        scatter_column<uint32_t>(a.in.flags, a.out.flags, base, cnt, pos, dest, (uint32_t*)s_stage);
-        // 6. advance the cursors and clear the counts (scatter_column's last barrier orders every
+        // 5. the columns through the LDS stage (the traceIds are in registers already)
+        {
+            uint64_t v[kScU];
+#pragma unroll
+            for (int k = 0; k < kScU; ++k) v[k] = tids[k];
+            move_columns<kScU, kScWG, 0>(a.in, a.out, base, cnt, pos, dest, s_stage, v);
+        }
+        // 6. advance the cursors and clear the counts (move_columns' last barrier orders every
         //    read of s_cur / s_off / s_cnt above before these writes)
         for (uint32_t d = t; d < nd; d += kScWG) {
             s_cur[d] += s_cnt[d];
@@ -276,6 +300,8 @@ __global__ __launch_bounds__(kScWG) void k_cl_scatter(ScatterArgs a) {
 constexpr int kTrWG = 512;
 constexpr uint32_t kTrSlots = 4096;    // LDS trace table: load <= 1/2 at <= 2048 records per round
 constexpr uint64_t kEmptyKey = ~0ull;  // a traceId equal to it takes the extra slot kTrSlots
+constexpr int kTrFast = 2048;          // sub-buckets up to this many records: the LDS-staged path
+static_assert(kTrFast * 8 <= (kTrSlots + 4) * 4, "the fast path's stage aliases s_cur");
 
 struct TraceArgs {
     SpanColsDev in;
@@ -290,7 +316,8 @@ __device__ __forceinline__ uint64_t trace_hash(uint64_t tid) { return zk_mix64(t
 __global__ __launch_bounds__(kTrWG) void k_cl_traces(TraceArgs a) {
     __shared__ unsigned long long s_key[kTrSlots];
     __shared__ uint32_t s_cnt[kTrSlots + 1];  // records per trace, then the trace's run start (scan)
-    __shared__ uint32_t s_cur[kTrSlots + 1];  // records placed per trace
+    // records placed per trace (large sub-buckets); the fast path's u64 column stage (2048 rows)
+    __shared__ __align__(16) uint32_t s_cur[kTrSlots + 4];
     __shared__ uint32_t s_work;
     __shared__ uint32_t s_fail;
     __shared__ uint32_t s_tmp[32];
@@ -304,6 +331,79 @@ __global__ __launch_bounds__(kTrWG) void k_cl_traces(TraceArgs a) {
         if (w >= a.nsub) break;
         const uint64_t lo = a.sub[w], hi = a.sub[w + 1];
         const uint64_t len = hi - lo;
+        if (len <= (uint64_t)kTrFast) {
+            // fast path (nearly every sub-bucket): the traceIds stay in registers, each record's
+            // rank inside its trace comes back from the count's atomic, and the columns move through
+            // an LDS stage with coalesced loads and stores (move_columns)
+            constexpr int U = kTrFast / kTrWG;
+            uint32_t slots = 64;
+            while (slots < 2 * len) slots <<= 1;
+            const uint32_t smask = slots - 1;
+            uint64_t tids[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const uint32_t j = t + k * kTrWG;
+                tids[k] = a.in.trace_id[lo + (j < len ? j : 0)];
+            }
+            for (uint32_t s = t; s < slots; s += kTrWG) {
+                s_key[s] = kEmptyKey;
+                s_cnt[s] = 0u;
+            }
+            if (t == 0) s_cnt[kTrSlots] = 0u;
+            __syncthreads();
+            uint32_t slot[U], rank[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                slot[k] = kTrSlots;
+                rank[k] = 0u;
+                if (t + k * kTrWG >= len) continue;
+                const uint64_t tid = tids[k];
+                if (tid != kEmptyKey) {
+                    // distinct traceIds <= len <= slots / 2: a free slot always exists
+                    uint32_t sl = (uint32_t)trace_hash(tid) & smask;
+                    for (;;) {
+                        const unsigned long long kk = s_key[sl];
+                        if (kk == tid) break;
+                        if (kk == kEmptyKey) {
+                            const unsigned long long old = atomicCAS(&s_key[sl], kEmptyKey, (unsigned long long)tid);
+                            if (old == kEmptyKey || old == tid) break;
+                        }
+                        sl = (sl + 1) & smask;
+                    }
+                    slot[k] = sl;
+                }
+                rank[k] = atomicAdd(&s_cnt[slot[k]], 1u);
+            }
+            __syncthreads();
+            {
+                uint32_t h[SPT], sum = 0;
+#pragma unroll
+                for (int q = 0; q < SPT; ++q) {
+                    const uint32_t sx = t * SPT + q;
+                    h[q] = (sx < slots || sx == kTrSlots) ? s_cnt[sx] : 0u;
+                    sum += h[q];
+                }
+                uint32_t tot;
+                uint32_t ex = block_excl_scan<kTrWG / 64>(sum, s_tmp, &tot);
+#pragma unroll
+                for (int q = 0; q < SPT; ++q) {
+                    const uint32_t sx = t * SPT + q;
+                    if (sx < slots || sx == kTrSlots) s_cnt[sx] = ex;
+                    ex += h[q];
+                }
+            }
+            __syncthreads();
+            uint32_t pos[U];
+            uint64_t dest[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                pos[k] = s_cnt[slot[k]] + rank[k];
+                dest[k] = lo + t + k * kTrWG;
+            }
+            move_columns<U, kTrWG, 0>(a.in, a.out, lo, (uint32_t)len, pos, dest,
+                                      reinterpret_cast<uint64_t*>(s_cur), tids);
+            continue;
+        }
         // rounds of <= 2048 records expected (a hash range of the traceIds each), and a table of a
         // power of two >= 2 x the round's records: the load stays <= 1/2 whatever the trace sizes
         // (a round's distinct traceIds are at most its records)

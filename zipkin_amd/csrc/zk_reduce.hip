@@ -27,6 +27,9 @@
 #ifndef ZK_K3_U
 #define ZK_K3_U 4      // links per thread per K3 iteration
 #endif
+#ifndef ZK_K3_WIDE
+#define ZK_K3_WIDE 1   // K3: 42-bit pieces, 6 LDS atomics per short link (k_bucket_lds_reduce_wide)
+#endif
 #ifndef ZK_K3_PREFETCH
 #define ZK_K3_PREFETCH 1  // K3: load the next iteration's links before this one's atomics
 #endif
@@ -552,6 +555,160 @@ __global__ __launch_bounds__(WG) void k_bucket_lds_reduce(ReduceArgs r, uint32_t
     }
 }
 
+// K3, wide rows (ZK_K3_WIDE): the same LDS-atomic reduce with fewer atomics per link. Each power
+// sum is kept as 42-bit pieces instead of 32-bit chunks -- S1 one piece, S2 two, S3 three, S4 four,
+// each row summing < 2^42 per link over a sub-part of < 2^20 links (< 2^62) -- and a link with d <
+// 2^21 adds m0 and S1 as one packed word (2^42 + d): 6 LDS atomics for such a link (d^2 < 2^42 is one
+// piece; d^3 < 2^63 and d^4 < 2^84 two each) against 8 with 32-bit chunks. At the flush every
+// thread rebuilds its cell's exact S1..S4 from the pieces and cuts them into the table's 32-bit
+// limbs with carries: all but the top limb of a sum receive < 2^32 per flush, and a flush holds at
+// least one link, so with < 2^32 links since reset those limbs stay < 2^64; the top limb receives
+// floor(S / 2^(32 top)) <= sum over the flush's links of (floor(d^k / 2^(32 top)) + 1) <= 2^32 per
+// link (tests/test_reduce_bounds.py checks these bounds against the limb layout at d = 2^40 - 1).
+template <int CB_SHIFT, int WG>
+__global__ __launch_bounds__(WG) void k_bucket_lds_reduce_wide(ReduceArgs r, uint32_t splits) {
+    constexpr int CB = 1 << CB_SHIFT;
+    static_assert(CB == WG, "one thread per cell at the flush");
+    constexpr int ROWS = 12;  // 0 m0, 1 S1, 2-3 S2, 4-6 S3, 7-10 S4, 11 packed m0|S1
+    constexpr int RS = CB + 1;
+    constexpr int CS = 17;  // staging stride of a cell's 15 limbs (odd: conflict-free both ways)
+    constexpr int WORDS = (ROWS * RS > CB * CS) ? ROWS * RS : CB * CS;
+    constexpr uint64_t P42 = (1ull << 42) - 1;
+    constexpr uint64_t M = 0xFFFFFFFFull;
+    constexpr uint64_t kSub = 1ull << 20;  // links per sub-part (row sums < 2^62)
+    __shared__ unsigned long long s_t[WORDS];
+    const int tid = threadIdx.x;
+    const uint32_t b = blockIdx.x / splits, part = blockIdx.x % splits;
+    const uint64_t lo = r.bucket_base[b], hi = r.bucket_base[b + 1];
+    const uint64_t per = (hi - lo + splits - 1) / splits;
+    const uint64_t p0 = lo + per * part;
+    const uint64_t p1 = (p0 + per < hi) ? p0 + per : hi;
+    const uint64_t cell0 = (uint64_t)b << CB_SHIFT;
+    for (uint64_t s0 = p0; s0 < p1 || s0 == p0; s0 += kSub) {
+        const uint64_t s1 = (s0 + kSub < p1) ? s0 + kSub : p1;
+        for (int x = tid; x < ROWS * RS; x += WG) s_t[x] = 0ull;
+        uint64_t nxt[ZK_K3_U];
+#pragma unroll
+        for (int k = 0; k < ZK_K3_U; ++k) {
+            const uint64_t i = s0 + tid + (uint64_t)k * WG;
+            nxt[k] = i < s1 ? r.sorted[i] : ~0ull;
+        }
+        __syncthreads();
+        for (uint64_t base = s0; base < s1; base += (uint64_t)WG * ZK_K3_U) {
+            uint64_t v[ZK_K3_U];
+#pragma unroll
+            for (int k = 0; k < ZK_K3_U; ++k) {
+                v[k] = nxt[k];
+                const uint64_t i = base + (uint64_t)WG * ZK_K3_U + tid + (uint64_t)k * WG;
+                nxt[k] = i < s1 ? r.sorted[i] : ~0ull;
+            }
+#pragma unroll
+            for (int k = 0; k < ZK_K3_U; ++k) {
+                if (v[k] == ~0ull) continue;
+                const uint32_t c = (uint32_t)((v[k] >> 40) - cell0);
+                const uint64_t d = v[k] & (kMaxDuration - 1);
+                unsigned long long* t = s_t + c;
+#define ZK_K3W_ADD(q, x)                                            \
+    do {                                                            \
+        const uint64_t x_ = (x);                                    \
+        if (x_) atomicAdd(&t[(q) * RS], (unsigned long long)x_);    \
+    } while (0)
+                if (d < (1ull << 21)) {
+                    const uint64_t d2 = d * d;                           // < 2^42
+                    const uint64_t d3 = d2 * d;                          // < 2^63
+                    const unsigned __int128 d4 = (unsigned __int128)d2 * d2;  // < 2^84
+                    atomicAdd(&t[11 * RS], (1ull << 42) | d);
+                    ZK_K3W_ADD(2, d2);
+                    ZK_K3W_ADD(4, d3 & P42);
+                    ZK_K3W_ADD(5, d3 >> 42);
+                    ZK_K3W_ADD(7, (uint64_t)d4 & P42);
+                    ZK_K3W_ADD(8, (uint64_t)(d4 >> 42));
+                } else {
+                    // d < 2^40: d^2 < 2^80, d^3 < 2^120, d^4 < 2^160 as 64-bit words
+                    const unsigned __int128 d2 = (unsigned __int128)d * d;
+                    const unsigned __int128 d3 = d2 * d;
+                    const uint64_t d3lo = (uint64_t)d3, d3hi = (uint64_t)(d3 >> 64);
+                    const unsigned __int128 q0 = (unsigned __int128)d3lo * d;
+                    const unsigned __int128 q1 = (unsigned __int128)d3hi * d + (uint64_t)(q0 >> 64);
+                    const uint64_t w0 = (uint64_t)q0, w1 = (uint64_t)q1, w2 = (uint64_t)(q1 >> 64);  // d^4
+                    atomicAdd(&t[0 * RS], 1ull);
+                    ZK_K3W_ADD(1, d);
+                    ZK_K3W_ADD(2, (uint64_t)d2 & P42);
+                    ZK_K3W_ADD(3, (uint64_t)(d2 >> 42));
+                    ZK_K3W_ADD(4, d3lo & P42);
+                    ZK_K3W_ADD(5, (uint64_t)(d3 >> 42) & P42);
+                    ZK_K3W_ADD(6, (uint64_t)(d3 >> 84));
+                    ZK_K3W_ADD(7, w0 & P42);
+                    ZK_K3W_ADD(8, ((w0 >> 42) | (w1 << 22)) & P42);
+                    ZK_K3W_ADD(9, ((w1 >> 20) | (w2 << 44)) & P42);
+                    ZK_K3W_ADD(10, (w1 >> 62) | (w2 << 2));
+                }
+#undef ZK_K3W_ADD
+            }
+        }
+        __syncthreads();
+        // rebuild the cell's exact sums from the pieces and cut them into 32-bit limbs
+        uint64_t limb[15];
+        {
+            const int c = tid;
+            uint64_t rv[ROWS];
+#pragma unroll
+            for (int q = 0; q < ROWS; ++q) rv[q] = s_t[q * RS + c];
+            const uint64_t m0 = rv[0] + (rv[11] >> 42);
+            const uint64_t S1 = rv[1] + (rv[11] & P42);  // < 2^63
+            // S2 = rv2 + rv3 * 2^42 (< 2^104)
+            const unsigned __int128 S2 = (unsigned __int128)rv[2] + ((unsigned __int128)rv[3] << 42);
+            // S3 = rv4 + rv5 * 2^42 + rv6 * 2^84 (< 2^147): as lo128 + hi
+            unsigned __int128 a3 = (unsigned __int128)rv[4] + ((unsigned __int128)rv[5] << 42);
+            const unsigned __int128 t6 = (unsigned __int128)rv[6] << 20;  // rv6 * 2^84 = (rv6 << 20) * 2^64
+            unsigned __int128 s3lo = a3 + ((unsigned __int128)(uint64_t)t6 << 64);
+            uint64_t s3hi = (uint64_t)(t6 >> 64) + (s3lo < a3 ? 1u : 0u);
+            // S4 = rv7 + rv8 * 2^42 + rv9 * 2^84 + rv10 * 2^126 (< 2^189): as 3 words
+            const unsigned __int128 a4 = (unsigned __int128)rv[7] + ((unsigned __int128)rv[8] << 42);  // < 2^105
+            const unsigned __int128 b4 = (unsigned __int128)rv[9] << 20;   // rv9 * 2^84 in units of 2^64
+            const unsigned __int128 c4 = (unsigned __int128)rv[10] << 62;  // rv10 * 2^126 in units of 2^64
+            // word 0 and the carry into word 1
+            const uint64_t s4w0 = (uint64_t)a4;
+            const unsigned __int128 hi = (a4 >> 64) + b4 + c4;  // the sum in units of 2^64 (< 2^125)
+            const uint64_t s4w1 = (uint64_t)hi, s4w2 = (uint64_t)(hi >> 64);
+            limb[0] = m0;
+            limb[1] = S1 & M;
+            limb[2] = S1 >> 32;
+            limb[3] = (uint64_t)S2 & M;
+            limb[4] = ((uint64_t)S2) >> 32;
+            limb[5] = (uint64_t)(S2 >> 64);
+            limb[6] = (uint64_t)s3lo & M;
+            limb[7] = ((uint64_t)s3lo) >> 32;
+            limb[8] = (uint64_t)(s3lo >> 64) & M;
+            limb[9] = ((uint64_t)(s3lo >> 96)) | (s3hi << 32);
+            limb[10] = s4w0 & M;
+            limb[11] = s4w0 >> 32;
+            limb[12] = s4w1 & M;
+            limb[13] = s4w1 >> 32;
+            limb[14] = s4w2;
+        }
+        __syncthreads();  // every row read before the staging overwrites them
+#pragma unroll
+        for (int q = 0; q < 15; ++q) s_t[tid * CS + q] = limb[q];
+        __syncthreads();
+        // 16 lanes per 128-byte cell: whole lines read-modify-written
+        for (int x = tid; x < CB * kLimbs; x += WG) {
+            const int c = x >> 4, q = x & 15;
+            const uint64_t cell = cell0 + c;
+            if (cell >= r.cells || q == 15) continue;
+            const uint64_t v = s_t[c * CS + q];
+            if (!v) continue;
+            uint64_t* dst = r.table + cell * kLimbs + q;
+            if (splits == 1)
+                *dst += v;  // this workgroup owns the cell
+            else
+                atomicAdd((unsigned long long*)dst, (unsigned long long)v);
+        }
+        __syncthreads();  // the staging is read before the next sub-part clears the rows
+        if (s1 >= p1) break;
+    }
+}
+
 }  // namespace
 
 #ifndef ZK_K3_LDS
@@ -605,9 +762,13 @@ hipError_t launch_partitioned_reduce(const ReduceArgs& r, hipStream_t s) {
     if (r.cb_shift == 8)
         return launch_checked("k_bucket_lds_reduce<8>", k_bucket_lds_reduce<8, 256, ZK_K3_U>, dim3(r.nb * splits),
                               dim3(256), 0, s, r, splits);
-    if (r.cb_shift == 9)
+    if (r.cb_shift == 9) {
+        if (ZK_K3_WIDE)
+            return launch_checked("k_bucket_lds_reduce_wide<9>", k_bucket_lds_reduce_wide<9, 512>,
+                                  dim3(r.nb * splits), dim3(512), 0, s, r, splits);
         return launch_checked("k_bucket_lds_reduce<9>", k_bucket_lds_reduce<9, 512, ZK_K3_U>, dim3(r.nb * splits),
                               dim3(512), 0, s, r, splits);
+    }
 #endif
     // CB = 512: 512 threads, 4096-link chunks (36 KB LDS); CB = 1024: 1024 threads, 4096-link chunks
     if (r.cb_shift == 8)
