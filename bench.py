@@ -113,7 +113,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from zipkin_amd import DepsContext, DeviceColumns, tracegen_params
-    from zipkin_amd.shards import allreduce_table
+    from zipkin_amd.shards import allreduce_table, device_view
 
     S = a.services
     cells = S * S
@@ -131,6 +131,11 @@ def main():
                         rank=rank, world=world)
     cols = DeviceColumns(a.records, device=f"cuda:{local}")
     n, ntr = ctx.tracegen_device(p, cols)
+    total_hint = n * world  # records of the whole job per step (exact below, before the timed steps)
+    if dist is not None:
+        tt = torch.tensor([n], dtype=torch.int64, device=dev)
+        dist.all_reduce(tt)
+        total_hint = int(tt.item())
     shuffled = a.order == "shuffled"
     clustered_cols = cols
     if shuffled:
@@ -160,9 +165,11 @@ def main():
         # device-generated batches are trace-clustered by construction (zk_tracegen_device)
         ctx.accumulate(cols, clustered=not shuffled, verify=a.verify)
         if dist is not None:
-            ctx.partial()  # fold the counters into the table tail (same stream)
-            allreduce_table(table)  # exact u64-limb + counter SUM over xGMI (RCCL): shards are disjoint traces
-            ctx.note_merged(n * world)
+            # counters folded into the table tail, the table packed into 56-bit limbs (same stream)
+            xp, xb = ctx.partial()
+            # exact limb + counter SUM over xGMI (RCCL): shards are disjoint traces
+            allreduce_table(device_view(xp, xb, torch.int64, local))
+            ctx.note_merged(total_hint)
         ctx.finalize(out_device=out)
 
     step = step_serial
@@ -203,9 +210,9 @@ def main():
                 ev.record(s)
                 state["reduced"] = ev
             if dist is not None:
-                c.partial()
-                allreduce_table(t)  # ordered on s; the host does not wait for it
-                c.note_merged(n * world)
+                xp, xb = c.partial()
+                allreduce_table(device_view(xp, xb, torch.int64, local))  # ordered on s; the host does not wait
+                c.note_merged(total_hint)
             state["pending"].append((c, t, s, o))
             if len(state["pending"]) > a.pipeline:
                 finalize_oldest()
@@ -268,11 +275,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    total_records = n * world
-    if dist is not None:  # the records every rank actually aggregated (shards differ in size)
-        t = torch.tensor([n], dtype=torch.int64, device=dev)
-        dist.all_reduce(t)
-        total_records = int(t.item())
+    total_records = total_hint  # the records every rank actually aggregated (shards differ in size)
     value = total_records * a.steps / elapsed
     join_calls = tm1["join_calls"] - tm0["join_calls"]
     join_avg_ms = (tm1["join_ms_total"] - tm0["join_ms_total"]) / max(1, join_calls)

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define ZK_ABI_VERSION 2
+#define ZK_ABI_VERSION 3
 
 typedef enum zk_status {
     ZK_OK = 0,
@@ -196,19 +196,26 @@ zk_status zk_deps_reset(zk_ctx* ctx);
 zk_status zk_deps_accumulate(zk_ctx* ctx, const zk_span_cols* cols, uint32_t batch_flags);
 zk_status zk_deps_finalize(zk_ctx* ctx, const zk_link_table* out);
 
-/* Raw exact accumulator for an external SUM all-reduce (RCCL over xGMI) across traceId-hash
+/* Exact accumulator exchange for an external SUM all-reduce (RCCL over xGMI) across traceId-hash
    shards, replacing the cross-reducer .group.sum / .sum of ZipkinAggregateJob.scala:39-43.
-   Layout (ZK_TABLE_BYTES(S) bytes of device memory): S*S cells x 16 u64 limbs (32-bit chunks per
-   limb, carry-free), then a tail of 16 u64 = this ctx's zk_stats counters. zk_deps_partial enqueues
-   the fold of the counters into the tail on the ctx stream and returns the buffer; every field is
-   a plain sum, so ONE int64/uint64 SUM all-reduce of the whole buffer merges the exact power sums
-   and the job-wide counters. zk_deps_note_merged then tells the ctx that the buffer holds the
-   merged job: total_records bounds the ZK_ERR_CAPACITY headroom (0: read it from the merged
-   tail, which costs one stream synchronisation), and finalize / zk_ctx_stats read
-   the merged counters from the tail, so every rank reaches the same status (a strict-mode
-   ZK_ERR_NO_SERVICE on one shard fails all ranks alike instead of one rank leaving the others
-   blocked in the next collective). The next reset or accumulate leaves the merged state. */
+   The accumulator (zk_config.table, ZK_TABLE_BYTES(S) bytes) is S*S cells x 16 u64 limbs of
+   32-bit chunks, carry-free, then a tail of 16 u64 = this ctx's zk_stats counters.
+   zk_deps_partial enqueues on the ctx stream the fold of the counters into the tail and the
+   carry-normalisation of every cell into the ctx-owned EXCHANGE buffer it returns
+   (ZK_XCHG_BYTES(S): S*S cells x 12 u64 limbs of 56 bits -- m0 one, S1 two, S2 two, S3 three, S4
+   four, a sum's top limb holding its remaining bits -- then the counter tail): 25 % fewer bytes to
+   move than the accumulator, and every field is a plain sum that cannot carry out of its u64
+   for up to 256 ranks, so ONE int64/uint64 SUM all-reduce of the returned buffer merges the exact
+   power sums and the job-wide counters. zk_deps_note_merged (after the all-reduce, on the same
+   stream) rebuilds the merged exact sums into the accumulator and tells the ctx that it holds the
+   merged job: total_records bounds the ZK_ERR_CAPACITY headroom (0: read it from the merged tail,
+   which costs one stream synchronisation), and finalize / zk_ctx_stats read the merged counters,
+   so every rank reaches the same status (a strict-mode ZK_ERR_NO_SERVICE on one shard fails all
+   ranks alike instead of one rank leaving the others blocked in the next collective).
+   note_merged without a partial since the last reset/accumulate returns ZK_ERR_INVALID_ARG. The
+   next reset leaves the merged state; an accumulate into a merged table continues the job. */
 #define ZK_TABLE_BYTES(S) ((uint64_t)(S) * (uint64_t)(S) * 128u + 128u)
+#define ZK_XCHG_BYTES(S) ((uint64_t)(S) * (uint64_t)(S) * 96u + 128u)
 zk_status zk_deps_partial(zk_ctx* ctx, void** dev_ptr, uint64_t* bytes);
 zk_status zk_deps_note_merged(zk_ctx* ctx, uint64_t total_records);
 

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     raw = C.CDLL(str(_abi.LIB_PATH))
     for name in declared_functions():
         assert hasattr(raw, name), name
-    assert L.zk_abi_version() == 2
+    assert L.zk_abi_version() == 3
 
 
 def test_status_strings():

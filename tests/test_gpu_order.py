@@ -139,9 +139,10 @@ def unmix64(z):
     return (z ^ (z >> 30) ^ (z >> 60)) & M64
 
 
-@pytest.mark.parametrize("traces,depth", [(1_500, 5), (6_000, 5), (40_000, 6)])
+@pytest.mark.parametrize("traces,depth", [(150, 4), (1_500, 5), (6_000, 5), (40_000, 6)])
 def test_plan_shapes(gpu, traces, depth):
-    """P3 alone (<= 65536 records), P1 + P3, and P1 + P2 + P3, host and device pointers."""
+    """P3 alone (<= 4096 records), P1 + P3 (<= 2048 x 256 records), and P1 + P2 + P3, host and
+    device pointers."""
     S = 97
     cols = tracegen_host(55 + traces, traces, max_depth=depth, num_services=S)
     ref = oracle.aggregate(cols, S)

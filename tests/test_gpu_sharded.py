@@ -13,7 +13,7 @@ import pytest
 from oracle import oracle
 from tests.test_gpu_parity import SERVER, assert_parity, cols_from_rows
 from zipkin_amd import DepsContext, ZkError, _abi, table, tracegen_host
-from zipkin_amd.shards import split
+from zipkin_amd.shards import device_view, split
 
 pytestmark = pytest.mark.gpu
 
@@ -37,23 +37,30 @@ def run_sharded(cols, S, world, **kw):
     parts = split(cols, world)
     shards = [Shard(S, **kw) for _ in range(world)]
     try:
+        views = []
         for sh, p in zip(shards, parts):
             sh.ctx.accumulate(p, clustered=True, verify=True)
-            ptr, nbytes = sh.ctx.partial()
-            assert ptr == sh.table.data_ptr() and nbytes == sh.table.numel() * 8
+            ptr, nbytes = sh.ctx.partial()  # the exchange form: 12 limbs of 56 bits per cell + tail
+            assert nbytes == _abi.xchg_words(S) * 8
+            views.append(device_view(ptr, nbytes, torch.int64))
         for sh in shards:
             sh.ctx.sync()
-        total = torch.stack([sh.table for sh in shards]).sum(0)  # the all-reduce's SUM
+        # the exchange form packs the accumulator exactly (zipkin_amd/table.py pack is the host view)
+        assert np.array_equal(views[0].cpu().numpy(), table.pack(shards[0].table.cpu().numpy(), S))
+        total = torch.stack(views).sum(0)  # the all-reduce's SUM
         outs = []
-        for sh in shards:  # every rank holds the same merged buffer after the all-reduce
-            sh.table.copy_(total)
+        for sh, v in zip(shards, views):  # every rank holds the same merged buffer after the all-reduce
+            v.copy_(total)
             torch.cuda.synchronize()
             sh.ctx.note_merged(0)
             try:
                 outs.append((sh.ctx.finalize(), sh.ctx.stats(), None))
             except ZkError as e:
                 outs.append((None, sh.ctx.stats(), e.status))
-        return outs, total.cpu().numpy()
+        # the merged accumulator (unpacked on every rank) is the host unpack of the summed exchange form
+        merged = shards[0].table.cpu().numpy()
+        assert np.array_equal(merged, table.unpack(total.cpu().numpy(), S))
+        return outs, merged
     finally:
         for sh in shards:
             sh.close()

@@ -55,9 +55,11 @@ def _worker(rank, world, port, mode):
         assert (shard_of(np.unique(mine.trace_id), world) == rank).all()
 
         sums, stats = _oracle_sums(mine)
-        t = torch.from_numpy(table.encode(sums, S))
+        # the exchange form zk_deps_partial hands to the all-reduce (56-bit limbs), as the host packs it
+        t = torch.from_numpy(table.pack(table.encode(sums, S), S))
         allreduce_table(t)
-        got = table.decode(t.numpy(), S)
+        got = table.decode(table.unpack(t.numpy(), S), S)
+        assert got == table.decode_exchange(t.numpy(), S)
         gstats = allreduce_stats(stats)
 
         want, wstats = _oracle_sums(SpanColumns.concat(shards))
@@ -143,3 +145,25 @@ def test_split_partitions_whole_traces():
         # trace-clustered order survives the split
         change = np.flatnonzero(np.diff(p.trace_id.view(np.int64)) != 0)
         assert len(change) + 1 == len(u)
+
+
+def test_exchange_form_bounds_and_linearity():
+    """56-bit limbs: pack/unpack round trip at the largest sums the accumulator can hold (2^32 - 1
+    records of d = 2^40 - 1), and the limb-wise SUM of 256 ranks' exchange buffers decodes to the sum
+    of their sums without any limb passing 2^64."""
+    n, d = (1 << 32) - 1, (1 << 40) - 1
+    big = (n, n * d, n * d ** 2, n * d ** 3, n * d ** 4)
+    x = table.encode_exchange({(0, 1): big}, 2)
+    assert table.decode_exchange(x, 2) == {(0, 1): big}
+    assert np.array_equal(table.unpack(table.pack(table.encode({(0, 1): big}, 2), 2), 2), table.encode({(0, 1): big}, 2))
+    # 256 ranks each holding 1/256 of the job: every limb of the sum stays below 2^64
+    share = tuple(v // 256 for v in big)
+    cell = table.encode_exchange_cell(*share).astype(object)
+    assert all(int(v) * 256 < 1 << 64 for v in cell)
+    rng = np.random.default_rng(3)
+    parts = []
+    for _ in range(4):
+        ds = [int(v) for v in rng.integers(0, 1 << 40, 50, dtype=np.uint64)]
+        parts.append((len(ds), sum(ds), sum(v * v for v in ds), sum(v ** 3 for v in ds), sum(v ** 4 for v in ds)))
+    tot = sum(table.encode_exchange({(1, 0): p}, 2).view(np.uint64) for p in parts).view(np.int64)
+    assert table.decode_exchange(tot, 2) == {(1, 0): tuple(sum(p[i] for p in parts) for i in range(5))}

@@ -50,6 +50,11 @@ def table_words(num_services: int) -> int:
     return num_services * num_services * LIMBS_PER_CELL + TABLE_TAIL_WORDS
 
 
+def xchg_words(num_services: int) -> int:
+    """int64 words of the exchange buffer zk_deps_partial returns (ZK_XCHG_BYTES(S) / 8)."""
+    return num_services * num_services * 12 + 16
+
+
 class ZkLibraryError(RuntimeError):
     pass
 

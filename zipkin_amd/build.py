@@ -25,6 +25,7 @@ SOURCES = [
     "zk_ingest_dev.hip",
     "zk_cluster.hip",
     "zk_launch.cpp",
+    "zk_exchange.hip",
 ]
 HEADERS = ["zk_internal.h", "zk_cluster.h", "zk_tracegen.h", "zk_sketch_internal.h", "zk_rt_internal.h", "zk_block.h", "zk_launch.h"]
 PUBLIC_HEADERS = ["zkagg.h", "zksketch.h", "zkstore.h", "zkingest.h"]

@@ -61,6 +61,7 @@ struct zk_ctx {
     void* fin_stage = nullptr;
     uint64_t records_since_reset = 0;
     bool merged = false;                  // the table holds the all-reduced job (zk_deps_note_merged)
+    uint64_t* xchg = nullptr;             // packed exchange form of the table (zk_deps_partial)
     bool folded = false;                  // zk_deps_partial folded this ctx's counters into the table tail
                                           // since the last reset / accumulate (note_merged requires it)
     // clustering pass for unclustered batches (zk_cluster.hip)
@@ -397,6 +398,7 @@ zk_status zk_ctx_destroy(zk_ctx* c) {
     hipFree(c->cl_cols);
     hipFree(c->cl_temp);
     hipFree(c->tset);
+    hipFree(c->xchg);
     for (auto* v : {&c->ev_free, &c->ev_join, &c->ev_reduce, &c->ev_spill, &c->ev_fin, &c->ev_cluster})
         for (auto& p : *v) {
             hipEventDestroy(p.a);
@@ -691,9 +693,15 @@ zk_status zk_deps_partial(zk_ctx* c, void** dev_ptr, uint64_t* bytes) {
     if (!c->merged)  // a merged tail already holds the job-wide counters
         ZK_HIP(c, launch_stats_fold(c->stats, (unsigned long long*)(c->table + (uint64_t)c->S * c->S * kLimbs),
                                     c->stream));
+    if (!c->xchg && hipMalloc(&c->xchg, exchange_bytes(c->S)) != hipSuccess) {
+        (void)hipGetLastError();
+        c->xchg = nullptr;
+        return fail(c, ZK_ERR_CAPACITY, "no device memory for the exchange buffer");
+    }
+    ZK_HIP(c, launch_table_pack(c->table, c->S, c->xchg, c->stream));  // 56-bit limbs + the counter tail
     c->folded = true;
-    *dev_ptr = c->table;
-    *bytes = table_bytes(c->S);
+    *dev_ptr = c->xchg;
+    *bytes = exchange_bytes(c->S);
     return ZK_OK;
 }
 
@@ -703,8 +711,10 @@ zk_status zk_deps_note_merged(zk_ctx* c, uint64_t total_records) {
     // all-reduce of a stale or zeroed tail would silently drop every error counter on every rank)
     if (!c->folded)
         return fail(c, ZK_ERR_INVALID_ARG, "zk_deps_note_merged without zk_deps_partial since the last reset/accumulate");
+    ZK_HIP(c, hipSetDevice(c->device));
+    // the all-reduced exchange buffer back into the accumulator's own layout (exact sums, counters)
+    ZK_HIP(c, launch_table_unpack(c->xchg, c->S, c->table, c->stream));
     if (total_records == 0) {  // take it from the all-reduced counter tail
-        ZK_HIP(c, hipSetDevice(c->device));
         unsigned long long rec = 0;
         ZK_HIP(c, hipMemcpyAsync(&rec, c->table + (uint64_t)c->S * c->S * kLimbs + ST_RECORDS, 8,
                                  hipMemcpyDeviceToHost, c->stream));

@@ -16,7 +16,7 @@ struct SpanColsMut {
 
 // clustering pass (zk_cluster.hip): b1 + b2 digit bits of the traceId hash (first level P1 global,
 // second level P2 per bucket), then P3 per sub-bucket; b1 = 0: P3 alone over the whole batch
-constexpr uint64_t kClusterSmall = 65536;
+constexpr uint64_t kClusterSmall = 4096;
 struct ClusterPlan {
     uint64_t n;
     uint32_t b1, b2, nb1, nb2;

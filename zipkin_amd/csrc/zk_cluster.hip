@@ -35,6 +35,8 @@
 // means a trace split into two non-adjacent runs, or spread over two accumulate calls -- both
 // would be mis-joined silently -- and is counted in ST_NOT_CLUSTERED (finalize then returns
 // ZK_ERR_NOT_CLUSTERED). Exact: the set stores whole traceIds, so it has no false positives.
+#include <stdlib.h>
+
 #include <hipcub/hipcub.hpp>
 
 #include "zk_block.h"
@@ -300,8 +302,9 @@ __global__ __launch_bounds__(kScWG) void k_cl_scatter(ScatterArgs a) {
 constexpr int kTrWG = 512;
 constexpr uint32_t kTrSlots = 4096;    // LDS trace table: load <= 1/2 at <= 2048 records per round
 constexpr uint64_t kEmptyKey = ~0ull;  // a traceId equal to it takes the extra slot kTrSlots
-constexpr int kTrFast = 2048;          // sub-buckets up to this many records: the LDS-staged path
-static_assert(kTrFast * 8 <= (kTrSlots + 4) * 4, "the fast path's stage aliases s_cur");
+constexpr int kTrFast = 4096;          // sub-buckets up to this many records: the LDS-staged path
+constexpr int kTrStage = 2 * kTrFast;  // s_cur words: the fast path's u64 column stage aliases it
+static_assert(kTrStage >= kTrSlots + 1, "s_cur also counts placements per slot");
 
 struct TraceArgs {
     SpanColsDev in;
@@ -317,7 +320,7 @@ __global__ __launch_bounds__(kTrWG) void k_cl_traces(TraceArgs a) {
     __shared__ unsigned long long s_key[kTrSlots];
     __shared__ uint32_t s_cnt[kTrSlots + 1];  // records per trace, then the trace's run start (scan)
     // records placed per trace (large sub-buckets); the fast path's u64 column stage (2048 rows)
-    __shared__ __align__(16) uint32_t s_cur[kTrSlots + 4];
+    __shared__ __align__(16) uint32_t s_cur[kTrStage];
     __shared__ uint32_t s_work;
     __shared__ uint32_t s_fail;
     __shared__ uint32_t s_tmp[32];
@@ -331,13 +334,15 @@ __global__ __launch_bounds__(kTrWG) void k_cl_traces(TraceArgs a) {
         if (w >= a.nsub) break;
         const uint64_t lo = a.sub[w], hi = a.sub[w + 1];
         const uint64_t len = hi - lo;
+        // fast path (nearly every sub-bucket): the traceIds stay in registers, each record's rank
+        // inside its trace comes back from the count's atomic, and the columns move through an LDS
+        // stage with coalesced loads and stores (move_columns). The table holds up to kTrSlots / 2
+        // distinct traces; a sub-bucket with more (or more records than kTrFast) takes the rounds
+        // path below.
         if (len <= (uint64_t)kTrFast) {
-            // fast path (nearly every sub-bucket): the traceIds stay in registers, each record's
-            // rank inside its trace comes back from the count's atomic, and the columns move through
-            // an LDS stage with coalesced loads and stores (move_columns)
             constexpr int U = kTrFast / kTrWG;
             uint32_t slots = 64;
-            while (slots < 2 * len) slots <<= 1;
+            while (slots < 2 * len && slots < kTrSlots) slots <<= 1;
             const uint32_t smask = slots - 1;
             uint64_t tids[U];
 #pragma unroll
@@ -349,7 +354,10 @@ __global__ __launch_bounds__(kTrWG) void k_cl_traces(TraceArgs a) {
                 s_key[s] = kEmptyKey;
                 s_cnt[s] = 0u;
             }
-            if (t == 0) s_cnt[kTrSlots] = 0u;
+            if (t == 0) {
+                s_cnt[kTrSlots] = 0u;
+                s_fail = 0u;
+            }
             __syncthreads();
             uint32_t slot[U], rank[U];
 #pragma unroll
@@ -359,8 +367,7 @@ __global__ __launch_bounds__(kTrWG) void k_cl_traces(TraceArgs a) {
                 if (t + k * kTrWG >= len) continue;
                 const uint64_t tid = tids[k];
                 if (tid != kEmptyKey) {
-                    // distinct traceIds <= len <= slots / 2: a free slot always exists
-                    uint32_t sl = (uint32_t)trace_hash(tid) & smask;
+                    uint32_t sl = (uint32_t)trace_hash(tid) & smask, probes = 0;
                     for (;;) {
                         const unsigned long long kk = s_key[sl];
                         if (kk == tid) break;
@@ -369,13 +376,18 @@ __global__ __launch_bounds__(kTrWG) void k_cl_traces(TraceArgs a) {
                             if (old == kEmptyKey || old == tid) break;
                         }
                         sl = (sl + 1) & smask;
+                        if (++probes >= slots) {  // more distinct traces than the table holds
+                            s_fail = 1u;
+                            sl = kTrSlots + 1;
+                            break;
+                        }
                     }
                     slot[k] = sl;
                 }
-                rank[k] = atomicAdd(&s_cnt[slot[k]], 1u);
+                if (slot[k] <= kTrSlots) rank[k] = atomicAdd(&s_cnt[slot[k]], 1u);
             }
             __syncthreads();
-            {
+            if (s_fail == 0u) {
                 uint32_t h[SPT], sum = 0;
 #pragma unroll
                 for (int q = 0; q < SPT; ++q) {
@@ -391,18 +403,19 @@ __global__ __launch_bounds__(kTrWG) void k_cl_traces(TraceArgs a) {
                     if (sx < slots || sx == kTrSlots) s_cnt[sx] = ex;
                     ex += h[q];
                 }
-            }
-            __syncthreads();
-            uint32_t pos[U];
-            uint64_t dest[U];
+                __syncthreads();
+                uint32_t pos[U];
+                uint64_t dest[U];
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
-                pos[k] = s_cnt[slot[k]] + rank[k];
-                dest[k] = lo + t + k * kTrWG;
+                for (int k = 0; k < U; ++k) {
+                    pos[k] = s_cnt[slot[k]] + rank[k];
+                    dest[k] = lo + t + k * kTrWG;
+                }
+                move_columns<U, kTrWG, 0>(a.in, a.out, lo, (uint32_t)len, pos, dest,
+                                          reinterpret_cast<uint64_t*>(s_cur), tids);
+                continue;
             }
-            move_columns<U, kTrWG, 0>(a.in, a.out, lo, (uint32_t)len, pos, dest,
-                                      reinterpret_cast<uint64_t*>(s_cur), tids);
-            continue;
+            __syncthreads();  // every thread read s_fail before the rounds path clears it
         }
         // rounds of <= 2048 records expected (a hash range of the traceIds each), and a table of a
         // power of two >= 2 x the round's records: the load stays <= 1/2 whatever the trace sizes
@@ -574,9 +587,9 @@ size_t scan_bytes(uint64_t m) {
 ClusterPlan cluster_plan(uint64_t n, uint32_t cus) {
     ClusterPlan p{};
     p.n = n;
-    // digit bits in all: sub-buckets of ~1k records (one P3 round unless a bucket holds > 2048)
+    // digit bits in all: sub-buckets of 1-2k records on average (P3's fast path takes up to 4096)
     uint32_t bits = 0;
-    while (bits < 22 && (n >> bits) > 1024) ++bits;
+    while (bits < 22 && (n >> bits) > 2048) ++bits;
     if (n <= kClusterSmall) bits = 0;  // P3 alone: one workgroup over the whole batch
     if (bits <= 8) {
         p.b1 = bits;
@@ -587,6 +600,14 @@ ClusterPlan cluster_plan(uint64_t n, uint32_t cus) {
         if (p.b2 > 11) {  // > 2^29 records: widen the first level
             p.b1 = bits - 11;
             p.b2 = 11;
+        }
+    }
+    // diagnostic A/B override of the digit split (never set by the product)
+    if (const char* e1 = getenv("ZK_CL_B1")) {
+        const uint32_t b1 = (uint32_t)atoi(e1);
+        if (b1 <= bits && b1 <= 11 && bits - b1 <= 11 && (b1 > 0 || bits == 0)) {
+            p.b1 = b1;
+            p.b2 = bits - b1;
         }
     }
     p.nb1 = 1u << p.b1;

@@ -67,6 +67,7 @@ constexpr int kStatShards = 256;  // stats buffer = kStatShards x ST_N u64
 // the exact table is followed by a tail of ST_N u64: the folded counters (zk_deps_partial), so one
 // SUM all-reduce of table + tail gives every rank the job-wide counters as well
 constexpr uint64_t kTableTailBytes = ST_N * 8;
+constexpr uint64_t kStatTailWords = ST_N;
 static_assert(ST_NOT_CLUSTERED < ST_N, "stat slots");
 
 struct SpanColsDev {
@@ -147,6 +148,10 @@ hipError_t launch_spill(const JoinArgs& a, uint32_t spill_wgs, hipStream_t s);
 uint64_t spill_scratch_bytes_per_wg(uint32_t max_trace);
 hipError_t launch_finalize(const uint64_t* table, uint32_t S, const zk_link_table* out,
                            hipStream_t s);
+// packed exchange form of the table (zk_exchange.hip): S*S cells x 12 u64 (56-bit limbs) + the tail
+uint64_t exchange_bytes(uint32_t S);
+hipError_t launch_table_pack(const uint64_t* table, uint32_t S, uint64_t* xchg, hipStream_t s);
+hipError_t launch_table_unpack(const uint64_t* xchg, uint32_t S, uint64_t* table, hipStream_t s);
 hipError_t launch_tracegen(const zk_tracegen_params* p, const zk_span_cols* out, uint64_t cap,
                            uint64_t* n_records, uint64_t* n_traces, hipStream_t s);
 

@@ -40,7 +40,8 @@ def split(cols: SpanColumns, world: int) -> list[SpanColumns]:
 
 
 def allreduce_table(table, group=None) -> None:
-    """In-place SUM of the exact accumulator (int64 tensor, device or host) across ranks.
+    """In-place SUM of the exact accumulator's exchange form (int64 tensor, device or host: the
+    buffer zk_deps_partial returns) across ranks.
 
     int64 two's-complement addition is bit-identical to the u64 limb addition the layout needs.
     """
@@ -160,8 +161,9 @@ def allreduce_stats(stats: dict, device="cpu", group=None) -> dict:
 class ShardedDeps:
     """One rank of the sharded job: a DepsContext over a caller-owned (all-reducible) table.
 
-    step(cols): reset -> accumulate this rank's shard -> fold the counters into the table's tail
-    (zk_deps_partial) -> ONE SUM all-reduce of limbs + counters -> note_merged -> finalize. With
+    step(cols): reset -> accumulate this rank's shard -> zk_deps_partial (counters folded into the
+    table's tail, the table packed into 56-bit limbs) -> ONE SUM all-reduce of that exchange buffer
+    -> note_merged (unpacked into the table) -> finalize. With
     world == 1 the all-reduce is skipped. Every rank ends with the same finalized table AND the
     same status: finalize decides errors from the job-wide counters, so a strict-mode failure on
     one shard fails every rank instead of leaving the others blocked in the next collective.
@@ -176,6 +178,7 @@ class ShardedDeps:
 
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.group = group
+        self.device = device
         self.num_services = num_services
         dev = torch.device("cuda", device)
         # the library's kernels and the RCCL all-reduce must be ordered on ONE stream
@@ -192,9 +195,10 @@ class ShardedDeps:
         self.ctx.reset()
         self.ctx.accumulate(cols, clustered=clustered, verify=verify)
         if self.world > 1:
-            self.ctx.partial()  # counters -> table tail, on the ctx stream
-            with torch.cuda.stream(self.stream):  # RCCL waits for the accumulate on this stream
-                allreduce_table(self.table, self.group)
+            # counters -> table tail, then the table's 56-bit-limb exchange form, on the ctx stream
+            ptr, nbytes = self.ctx.partial()
+            with torch.cuda.stream(self.stream):  # RCCL waits for the pack on this stream
+                allreduce_table(device_view(ptr, nbytes, torch.int64, self.device), self.group)
             # 0: the library reads the merged record count from the all-reduced tail
             self.ctx.note_merged(total_records or 0)
         return self.ctx.finalize(out_device=out_device)

@@ -8,6 +8,10 @@ RCCL SUM all-reduce of the multi-GPU step does) and decode to the exact power su
 
 These helpers decode a table to exact integers on the host (for inspection, persistence of
 incremental runs and the multi-process tests) and encode exact sums back into limbs.
+
+The exchange form (zk_deps_partial, zipkin_amd/csrc/zk_exchange.hip) is what ranks all-reduce: 12
+limbs of 56 bits per cell -- m0, S1 in two, S2 in two, S3 in three, S4 in four, each sum's top limb
+holding its remaining bits -- so that a SUM over up to 256 ranks cannot carry out of a u64.
 """
 from __future__ import annotations
 
@@ -75,10 +79,77 @@ STAT_FIELDS = ("records", "merged_spans", "valid_spans", "invalid_spans", "child
 _NOT_CLUSTERED_SLOT = 15
 
 
-def tail_stats(table: np.ndarray, num_services: int) -> dict:
-    """zk_stats counters from the tail of a table returned by zk_deps_partial."""
+def tail_stats(table: np.ndarray, num_services: int, limbs: int = LIMBS) -> dict:
+    """zk_stats counters from the tail of an accumulator (limbs = 16) or of the exchange buffer
+    zk_deps_partial returns (limbs = XLIMBS)."""
     cells = num_services * num_services
-    tail = np.asarray(table).reshape(-1)[cells * LIMBS : cells * LIMBS + TAIL].view(np.uint64)
+    tail = np.asarray(table).reshape(-1)[cells * limbs : cells * limbs + TAIL].view(np.uint64)
     out = {k: int(tail[i]) for i, k in enumerate(STAT_FIELDS)}
     out["not_clustered"] = int(tail[_NOT_CLUSTERED_SLOT])
     return out
+
+
+# ---- exchange form (zk_exchange.hip): 12 limbs of 56 bits per cell ---------------------------------
+XLIMBS = 12
+# (offset, limbs) of S1..S4 in the exchange cell (m0 is limb 0)
+XPOWER_LIMBS = ((1, 2), (3, 2), (5, 3), (8, 4))
+_M56 = (1 << 56) - 1
+
+
+def encode_exchange_cell(n: int, s1: int, s2: int, s3: int, s4: int) -> np.ndarray:
+    out = np.zeros(XLIMBS, np.uint64)
+    out[0] = n
+    for (off, k), s in zip(XPOWER_LIMBS, (s1, s2, s3, s4)):
+        for i in range(k):
+            x = (s >> (56 * i)) if i == k - 1 else ((s >> (56 * i)) & _M56)
+            if x >= 1 << 64:
+                raise OverflowError("power sum exceeds the exchange form's range")
+            out[off + i] = x
+    return out
+
+
+def decode_exchange_cell(limbs) -> tuple[int, int, int, int, int]:
+    v = [int(x) & ((1 << 64) - 1) for x in limbs]
+    return (v[0], *(sum(v[off + i] << (56 * i) for i in range(k)) for off, k in XPOWER_LIMBS))
+
+
+def encode_exchange(sums: dict, num_services: int, stats: dict | None = None) -> np.ndarray:
+    """Dense int64 exchange buffer (S*S*12 limbs + the counter tail) from exact sums."""
+    t = np.zeros((num_services * num_services, XLIMBS), np.uint64)
+    for (p, c), v in sums.items():
+        t[p * num_services + c] = encode_exchange_cell(*v)
+    tail = np.zeros(TAIL, np.uint64)
+    if stats:
+        for i, k in enumerate(STAT_FIELDS):
+            tail[i] = stats.get(k, 0)
+    return np.concatenate([t.reshape(-1), tail]).view(np.int64)
+
+
+def decode_exchange(x: np.ndarray, num_services: int) -> dict:
+    cells = num_services * num_services
+    t = np.asarray(x).reshape(-1)[: cells * XLIMBS].reshape(cells, XLIMBS).view(np.uint64)
+    return {(int(c // num_services), int(c % num_services)): decode_exchange_cell(t[c]) for c in np.flatnonzero(t[:, 0])}
+
+
+def pack(table: np.ndarray, num_services: int) -> np.ndarray:
+    """Host restatement of k_table_pack: accumulator layout -> exchange form (tail copied)."""
+    cells = num_services * num_services
+    flat = np.asarray(table).reshape(-1)
+    t = flat[: cells * LIMBS].reshape(cells, LIMBS).view(np.uint64)
+    out = np.zeros((cells, XLIMBS), np.uint64)
+    for c in range(cells):
+        if t[c].any():
+            out[c] = encode_exchange_cell(*decode_cell(t[c]))
+    return np.concatenate([out.reshape(-1), flat[cells * LIMBS: cells * LIMBS + TAIL].view(np.uint64)]).view(np.int64)
+
+
+def unpack(x: np.ndarray, num_services: int) -> np.ndarray:
+    """Host restatement of k_table_unpack: exchange form -> accumulator layout (tail copied)."""
+    cells = num_services * num_services
+    flat = np.asarray(x).reshape(-1)
+    t = flat[: cells * XLIMBS].reshape(cells, XLIMBS).view(np.uint64)
+    out = np.zeros((cells, LIMBS), np.uint64)
+    for c in range(cells):
+        if t[c].any():
+            out[c] = encode_cell(*decode_exchange_cell(t[c]))
+    return np.concatenate([out.reshape(-1), flat[cells * XLIMBS: cells * XLIMBS + TAIL].view(np.uint64)]).view(np.int64)
