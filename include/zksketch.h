@@ -143,6 +143,17 @@ zk_status   zk_rt_distinct_traces(zk_rt* rt, double* estimate);
  * N. With N = 0 all outputs are 0. */
 zk_status   zk_rt_quantiles(zk_rt* rt, uint32_t service, const double* q, uint32_t nq, int64_t* lo, int64_t* hi,
                             uint64_t* count);
+/* Duration t-digest of one service (BASELINE configs[4]: "duration t-digest p50/p99"): a merging
+ * t-digest with the k1 scale function at the given compression (delta, e.g. 200), built from the
+ * service's exact histogram -- bins in ascending order, each its midpoint weighted by its count,
+ * merged while a centroid's quantile span stays within one unit of k(q) = delta/(2 pi) asin(2q-1).
+ * Because the histogram is merged exactly across shards (SUM), the digest is the same on every
+ * rank and for every world size and batch order (a digest merged centroid-by-centroid is not).
+ * Outputs: the centroids (mean, weight: host double[cap], NULL to size with *n), the t-digest
+ * estimate of each quantile q[i] (host double[nq]; interpolation between centroid centres), and
+ * the item count. */
+zk_status   zk_rt_tdigest(zk_rt* rt, uint32_t service, double compression, double* mean, double* weight,
+                          uint32_t cap, uint32_t* n, const double* q, uint32_t nq, double* value, uint64_t* count);
 /* Raw state for tests and multi-GPU merging: registers u8[S][2^p] (MAX all-reduce) and histogram
  * u32[S][bins] (SUM all-reduce), device pointers; and host copies. */
 zk_status   zk_rt_partial(zk_rt* rt, void** registers, uint64_t* register_bytes, void** histogram,

@@ -205,3 +205,65 @@ def exact_distinct(service_id, trace_id, num_services: int) -> np.ndarray:
 def exact_quantile(durations: np.ndarray, q: float) -> int:
     d = np.sort(np.asarray(durations, dtype=np.int64))
     return int(d[nearest_rank(q, len(d)) - 1])
+
+
+# ---- t-digest over the histogram (zk_rt_tdigest, zipkin_amd/csrc/zk_rt_api.cpp) --------------------
+# Restates the library's build: Dunning's merging t-digest with the k1 scale function
+# k(q) = delta / (2 pi) asin(2q - 1) (T. Dunning, O. Ertl, "Computing extremely accurate quantiles
+# using t-digests", 2019; the published algorithm, no library source), fed with the histogram's
+# nonzero bins in ascending order as (midpoint, count) points; a bin is never split.
+def tdigest(hist_row, m: int, delta: float):
+    h = np.asarray(hist_row, dtype=np.uint64)
+    N = int(h.sum())
+    if N == 0:
+        return [], 0, 0, 0
+    def k_of(q):
+        return delta / (2 * math.pi) * math.asin(2 * q - 1)
+    def q_of(k):
+        x = 2 * math.pi * k / delta
+        return 1.0 if x >= math.pi / 2 else (math.sin(x) + 1) / 2
+    cent = []
+    first = True
+    before = cw = cs = qlim = 0.0
+    vmin = vmax = 0
+    for b in np.flatnonzero(h):
+        lo, hi = bin_bounds(int(b), m)
+        if first:
+            vmin = lo
+        vmax = hi
+        w, x = float(h[b]), 0.5 * (float(lo) + float(hi))
+        if not first and (before + cw + w) / N <= qlim:
+            cw += w
+            cs += w * x
+            continue
+        if not first:
+            cent.append((cs / cw, cw))
+            before += cw
+        first = False
+        cw, cs = w, w * x
+        qlim = q_of(k_of(before / N) + 1.0)
+    cent.append((cs / cw, cw))
+    return cent, vmin, vmax, N
+
+
+def tdigest_quantile(cent, vmin: int, vmax: int, N: int, q: float) -> float:
+    if not cent or N == 0:
+        return 0.0
+    if len(cent) == 1:
+        return cent[0][0]
+    idx = q * N
+    if idx <= cent[0][1] / 2:
+        t = idx / (cent[0][1] / 2) if cent[0][1] > 0 else 0.0
+        return vmin + t * (cent[0][0] - vmin)
+    cum = 0.0
+    for i in range(len(cent) - 1):
+        a = cum + cent[i][1] / 2
+        b = cum + cent[i][1] + cent[i + 1][1] / 2
+        if idx <= b:
+            t = (idx - a) / (b - a) if b > a else 0.0
+            return cent[i][0] + t * (cent[i + 1][0] - cent[i][0])
+        cum += cent[i][1]
+    mean, w = cent[-1]
+    a = N - w / 2
+    t = (idx - a) / (w / 2) if w > 0 else 0.0
+    return mean + min(t, 1.0) * (vmax - mean)

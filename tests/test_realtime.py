@@ -276,3 +276,53 @@ def test_gpu_c5_shape_error_bounds(gpu):
         for q, (lo, hi) in ((0.5, b50), (0.99, b99)):
             x = exact_quantile(ds, q)
             assert lo <= x <= hi
+
+
+
+def test_tdigest_over_histogram_bounds():
+    """The t-digest (delta = 200) of a log-normal duration sample: p50 and p99 within the t-digest's
+    rank bound of the exact distribution, weights summing to N, centroid count O(delta)."""
+    from oracle.realtime import tdigest, tdigest_quantile
+
+    rng = np.random.default_rng(5)
+    for n in (50, 5_000, 400_000):
+        d = rng.lognormal(9, 1.5, n).astype(np.int64)
+        o = RtOracle(1, p=4, m=7)
+        o.accumulate_merged(np.zeros(n, np.uint32), np.arange(n, dtype=np.uint64), d)
+        cent, vmin, vmax, N = tdigest(o.hist[0], 7, 200.0)
+        assert N == n and abs(sum(w for _, w in cent) - n) < 1e-6
+        assert len(cent) <= 400
+        ds = np.sort(d)
+        for q in (0.5, 0.99):
+            est = tdigest_quantile(cent, vmin, vmax, N, q)
+            assert d.min() <= est <= d.max()
+            # the t-digest's accuracy is a rank bound: the estimate's rank is within the quantile
+            # span of a k1 centroid there (pi sqrt(q (1 - q)) / delta, doubled) plus the histogram
+            # bin (2^-7 relative: a few ranks), plus 2 / n
+            rank = np.searchsorted(ds, est, side="right") / n
+            assert abs(rank - q) <= 2 * math.pi * math.sqrt(q * (1 - q)) / 200 + 2 / n + 0.002, (n, q, rank)
+
+
+@pytest.mark.gpu
+def test_gpu_tdigest_equals_oracle(gpu):
+    """zk_rt_tdigest on the device sketch == the oracle's digest of the same histogram (centroids
+    and estimates bit for bit), and within the t-digest's rank bound at C5 shape."""
+    from oracle.realtime import tdigest, tdigest_quantile
+    from zipkin_amd import tracegen_host
+
+    S = 500
+    cols = tracegen_host(9, 200_000, max_depth=6, num_services=S)
+    rt, *_ = _bound_run(cols, S, True)
+    _, hist = rt.read()
+    svc, tid, dur, _ = merged_span_items(cols, S)
+    for s in range(0, S, 50):
+        mean, weight, est, n = rt.tdigest(s, 200.0, (0.5, 0.99))
+        cent, vmin, vmax, N = tdigest(hist[s], rt.m, 200.0)
+        assert n == N and len(cent) == len(mean)
+        assert np.array_equal(mean, np.array([c[0] for c in cent])) and np.array_equal(weight, np.array([c[1] for c in cent]))
+        for q, e in zip((0.5, 0.99), est):
+            assert e == tdigest_quantile(cent, vmin, vmax, N, q)
+            ds = np.sort(dur[svc == s])
+            if len(ds) >= 1000:
+                rank = np.searchsorted(ds, e, side="right") / len(ds)
+                assert abs(rank - q) <= 2 * math.pi * math.sqrt(q * (1 - q)) / 200 + 2 / len(ds) + 0.002, (s, q, rank)

@@ -277,6 +277,7 @@ _SIGNATURES = [
     ("zk_rt_accumulate_merged", C.c_int, [_P, _P, _P, _P, C.c_uint64, C.c_uint32]),
     ("zk_rt_distinct_traces", C.c_int, [_P, _P]),
     ("zk_rt_quantiles", C.c_int, [_P, C.c_uint32, _P, C.c_uint32, _P, _P, _U64P]),
+    ("zk_rt_tdigest", C.c_int, [_P, C.c_uint32, C.c_double, _P, _P, C.c_uint32, C.POINTER(C.c_uint32), _P, C.c_uint32, _P, C.POINTER(C.c_uint64)]),
     ("zk_rt_partial", C.c_int, [_P, C.POINTER(_P), _U64P, C.POINTER(_P), _U64P]),
     ("zk_rt_read", C.c_int, [_P, _P, _P]),
     ("zk_rt_dropped", C.c_int, [_P, _U64P, _U64P]),

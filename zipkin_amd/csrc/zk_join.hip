@@ -197,15 +197,19 @@ constexpr uint32_t kSlotP0 = 1u << 21;
 #endif
 constexpr int kSlotSegShift = 22;
 
-// own bits of a fragment and the "seen exactly once" core annotations it may promote to ">= 2"
+// own bits of a fragment and the "seen exactly once" core annotations it may promote to ">= 2":
+// the four 2-bit counts of cs|cr|sr|ss (bits 8..15) give ">= 1" (either bit) and ">= 2" (the high
+// bit) per field, compressed from every other bit to four contiguous bits -- ten bit operations
+// instead of a compare and select per field and threshold
 __device__ __forceinline__ uint32_t frag_bits(uint32_t f, uint32_t* once) {
-    uint32_t A = 0, B = 0;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const uint32_t k = (f >> (ZK_F_CS_SHIFT + 2 * c)) & 3u;
-        A |= (k >= 1 ? 1u : 0u) << c;
-        B |= (k >= 2 ? 1u : 0u) << c;
-    }
+    static_assert(ZK_F_SR_SHIFT == ZK_F_CS_SHIFT + 4 && ZK_F_CR_SHIFT == ZK_F_CS_SHIFT + 2 &&
+                      ZK_F_SS_SHIFT == ZK_F_CS_SHIFT + 6, "cs, cr, sr, ss counts in consecutive 2-bit fields");
+    const uint32_t f8 = (f >> ZK_F_CS_SHIFT) & 0xFFu;
+    const uint32_t hi = (f8 >> 1) & 0x55u;
+    uint32_t y = (f8 & 0x55u) | hi | (hi << 8);  // ">= 1" spread in the low byte, ">= 2" in the high byte
+    y = (y | (y >> 1)) & 0x3333u;
+    y = (y | (y >> 2)) & 0x0F0Fu;
+    const uint32_t A = y & 0xFu, B = y >> 8;
     *once = A & ~B;
     return (A << kSlotA) | (B << kSlotB) | ((f & ZK_F_HAS_PARENT) ? kSlotP1 : kSlotP0);
 }

@@ -141,6 +141,81 @@ void bin_bounds(uint32_t b, uint32_t m, int64_t* lo, int64_t* hi) {
     *hi = (int64_t)(l + (1ull << (e - m)) - 1ull);
 }
 
+struct Centroid {
+    double mean, weight;
+};
+
+// A merging t-digest (Dunning's k1 scale function, compression delta) over one service's histogram:
+// the nonzero bins in ascending order, each a point at its midpoint with its count as weight, are
+// merged into a centroid while the centroid's quantile span stays within one unit of
+// k(q) = delta / (2 pi) * asin(2q - 1). A bin is never split (its values lie in [lo, hi]), so a bin
+// heavier than the bound is a centroid of its own. The input is the exact (all-reduced) histogram,
+// so the digest is identical on every rank and for every world size and batch order.
+void build_tdigest(const std::vector<uint32_t>& h, uint32_t m, double delta, std::vector<Centroid>* out,
+                   int64_t* vmin, int64_t* vmax, uint64_t* total) {
+    out->clear();
+    uint64_t N = 0;
+    for (uint32_t c : h) N += c;
+    *total = N;
+    *vmin = *vmax = 0;
+    if (!N) return;
+    const double pi = 3.14159265358979323846;
+    auto k_of = [&](double q) { return delta / (2.0 * pi) * asin(2.0 * q - 1.0); };
+    auto q_of = [&](double k) {
+        const double x = 2.0 * pi * k / delta;
+        return x >= pi / 2 ? 1.0 : (sin(x) + 1.0) / 2.0;
+    };
+    bool first = true;
+    double before = 0.0, cw = 0.0, cs = 0.0, qlim = 0.0;
+    for (uint32_t b = 0; b < (uint32_t)h.size(); ++b) {
+        if (!h[b]) continue;
+        int64_t lo, hi;
+        bin_bounds(b, m, &lo, &hi);
+        if (first) *vmin = lo;
+        *vmax = hi;
+        const double w = (double)h[b], x = 0.5 * ((double)lo + (double)hi);
+        if (!first && (before + cw + w) / (double)N <= qlim) {
+            cw += w;
+            cs += w * x;
+            continue;
+        }
+        if (!first) {
+            out->push_back({cs / cw, cw});
+            before += cw;
+        }
+        first = false;
+        cw = w;
+        cs = w * x;
+        qlim = q_of(k_of(before / (double)N) + 1.0);
+    }
+    out->push_back({cs / cw, cw});
+}
+
+// t-digest quantile (nearest centroids' centers, linearly interpolated; the ends interpolate to
+// the smallest / largest bin bound)
+double tdigest_quantile(const std::vector<Centroid>& c, int64_t vmin, int64_t vmax, uint64_t N, double q) {
+    if (c.empty() || !N) return 0.0;
+    if (c.size() == 1) return c[0].mean;
+    const double idx = q * (double)N;
+    if (idx <= c[0].weight / 2) {
+        const double t = c[0].weight > 0 ? idx / (c[0].weight / 2) : 0.0;
+        return (double)vmin + t * (c[0].mean - (double)vmin);
+    }
+    double cum = 0.0;
+    for (size_t i = 0; i + 1 < c.size(); ++i) {
+        const double a = cum + c[i].weight / 2, b = cum + c[i].weight + c[i + 1].weight / 2;
+        if (idx <= b) {
+            const double t = b > a ? (idx - a) / (b - a) : 0.0;
+            return c[i].mean + t * (c[i + 1].mean - c[i].mean);
+        }
+        cum += c[i].weight;
+    }
+    const Centroid& l = c.back();
+    const double a = (double)N - l.weight / 2;
+    const double t = l.weight > 0 ? (idx - a) / (l.weight / 2) : 0.0;
+    return l.mean + (t > 1.0 ? 1.0 : t) * ((double)vmax - l.mean);
+}
+
 }  // namespace
 
 namespace zk {
@@ -369,6 +444,38 @@ zk_status zk_rt_quantiles(zk_rt* r, uint32_t service, const double* q, uint32_t 
             }
         }
     }
+    return ZK_OK;
+    ZK_GUARD_END
+}
+
+zk_status zk_rt_tdigest(zk_rt* r, uint32_t service, double compression, double* mean, double* weight, uint32_t cap,
+                        uint32_t* n, const double* q, uint32_t nq, double* value, uint64_t* count) {
+    ZK_GUARD_BEGIN
+    if (!r || !n) return ZK_ERR_INVALID_ARG;
+    if (service >= r->S) return rfail(r, ZK_ERR_SERVICE_RANGE, "service >= S");
+    if (!(compression >= 10.0 && compression <= 10000.0)) return rfail(r, ZK_ERR_INVALID_ARG, "compression outside [10, 10000]");
+    if (nq && (!q || !value)) return rfail(r, ZK_ERR_INVALID_ARG, "null array");
+    for (uint32_t i = 0; i < nq; ++i)
+        if (!(q[i] >= 0.0 && q[i] <= 1.0)) return rfail(r, ZK_ERR_INVALID_ARG, "quantile outside [0, 1]");
+    RT_HIP(r, hipSetDevice(r->device));
+    std::vector<uint32_t> h(r->nbins);
+    RT_HIP(r, hipMemcpyAsync(h.data(), r->hist + (uint64_t)service * r->nbins, (uint64_t)r->nbins * 4,
+                             hipMemcpyDeviceToHost, r->stream));
+    RT_HIP(r, hipStreamSynchronize(r->stream));
+    std::vector<Centroid> c;
+    int64_t vmin, vmax;
+    uint64_t N;
+    build_tdigest(h, r->m, compression, &c, &vmin, &vmax, &N);
+    if (count) *count = N;
+    *n = (uint32_t)c.size();
+    if (mean || weight) {
+        if (cap < c.size()) return rfail(r, ZK_ERR_CAPACITY, "centroid capacity smaller than the digest");
+        for (size_t i = 0; i < c.size(); ++i) {
+            if (mean) mean[i] = c[i].mean;
+            if (weight) weight[i] = c[i].weight;
+        }
+    }
+    for (uint32_t i = 0; i < nq; ++i) value[i] = tdigest_quantile(c, vmin, vmax, N, q[i]);
     return ZK_OK;
     ZK_GUARD_END
 }

@@ -113,6 +113,20 @@ class RtSketch:
                                             C.byref(cnt)))
         return [(int(a), int(b)) for a, b in zip(lo, hi)], int(cnt.value)
 
+    def tdigest(self, service: int, compression: float = 200.0, qs=(0.5, 0.99)):
+        """(centroid means, centroid weights, t-digest estimates of qs, count) of one service's
+        duration digest (zk_rt_tdigest: a merging t-digest over the exact histogram)."""
+        q = np.ascontiguousarray(qs, dtype=np.float64)
+        val = np.zeros(len(q), np.float64)
+        n, cnt = C.c_uint32(), C.c_uint64()
+        self._check(self._L.zk_rt_tdigest(self._h, service, compression, None, None, 0, C.byref(n), None, 0, None,
+                                          None))
+        mean = np.zeros(n.value, np.float64)
+        weight = np.zeros(n.value, np.float64)
+        self._check(self._L.zk_rt_tdigest(self._h, service, compression, mean.ctypes.data, weight.ctypes.data, n.value,
+                                          C.byref(n), q.ctypes.data, len(q), val.ctypes.data, C.byref(cnt)))
+        return mean, weight, val, int(cnt.value)
+
     def read(self):
         """(registers uint8[S, 2^p], histogram uint32[S, bins]) host copies."""
         regs = np.zeros((self.num_services, self.registers), np.uint8)
