@@ -646,7 +646,11 @@ __device__ __forceinline__ bool try_resolve(const IngArgs& a, uint64_t i, const 
 constexpr uint32_t kLdsWG = 64;
 constexpr uint32_t kLdsBudget = 20480;
 constexpr uint32_t kLdsBlock = 1024;
-constexpr uint32_t kLdsSlack = 64;  // region bytes beyond max(raw, compressed): in-place headroom + alignment
+constexpr uint32_t kLdsSlack = 80;  // region bytes beyond max(raw, compressed): in-place headroom + alignment
+                                    // + the lane's bank skew
+#ifndef ZK_ING_SKEW
+#define ZK_ING_SKEW 1  // decompressed span starts 4 * (lane % 4) bytes into its region (see below)
+#endif
 
 // Snappy block from in = out + D (the same region), in place: false with *unsafe set when a step
 // would write over input bytes not yet read.
@@ -762,14 +766,18 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                 const uint32_t nblk = (uint32_t)((clen + mis + 15) >> 4);
                 u32x4* dst = reinterpret_cast<u32x4*>(reg + D - mis);
                 for (uint32_t c = 0; c < nblk; ++c) dst[c] = g[c];
-                // the region as an LDS pointer: the decoder's byte and word reads become ds_read_*
+                // the region as an LDS pointer: the decoder's byte and word reads become ds_read_*.
+                // Regions start on 16-byte boundaries, i.e. on one of 8 bank offsets of a 32-bank
+                // group; lanes parsing the same field at the same offset then collide. The
+                // decompressed span starts 4 * (lane % 4) bytes in, spreading the lanes over all 32.
                 lds_u8* const lreg = (lds_u8*)reg;
+                const uint32_t skew = ZK_ING_SKEW ? 4u * (lane & 3u) : 0u;
                 const lds_u8* src = lreg + D;
                 uint64_t len = clen;
                 bool ok = true, unsafe = false;
                 if (a.snappy) {
-                    ok = snappy_inplace(lreg, D, clen, raw, &unsafe);
-                    src = lreg;
+                    ok = snappy_inplace(lreg + skew, D - skew, clen, raw, &unsafe);
+                    src = lreg + skew;
                     len = raw;
                 }
                 if (!ok) {

@@ -360,6 +360,13 @@ __device__ __forceinline__ void load_window(const JoinArgs& a, uint64_t ws, Wind
 #ifndef ZK_K1_FAST_SCAN
 #define ZK_K1_FAST_SCAN 1
 #endif
+// ZK_K1_SLOT16: 16-byte hash slots {spanId, slot word, merged service key}: a parent probe reads
+// the parent's spanId, validity bits and service in ONE ds_read_b128 (the slot word alone needed two
+// more dependent reads: the occupant's spanId and its service). 2 x TILE slots (16 KB, the LDS of the
+// 8 x TILE u32 table); the service key array goes.
+#ifndef ZK_K1_SLOT16
+#define ZK_K1_SLOT16 0
+#endif
 // ZK_K1_EARLY_COLS: four of the six late columns loaded a phase earlier (see load_early)
 #ifndef ZK_K1_EARLY_COLS
 #define ZK_K1_EARLY_COLS 1
@@ -431,19 +438,29 @@ constexpr int kModeEmit = 2;
 template <int TILE, int WG, int ABL, int MODE>
 // launch bounds: minimum waves per SIMD = resident workgroups per CU x waves per workgroup / 4 SIMDs
 __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_stream(JoinArgs a) {
-    constexpr int H = ZK_K1_SORTJOIN ? 64 : ZK_HASH_FACTOR * TILE;  // load <= 1/16 (distinct spans / slots): short probe chains, since a wave waits for its longest
+    constexpr int H = ZK_K1_SORTJOIN ? 64 : ZK_K1_SLOT16 ? 2 * TILE : ZK_HASH_FACTOR * TILE;  // load <= 1/16 (distinct spans / slots): short probe chains, since a wave waits for its longest
     constexpr int NWORD = TILE / 64;
     static_assert(TILE == 2 * WG && TILE <= 2047, "two records per thread");
     __shared__ __align__(16) uint64_t s_sid[TILE];
     __shared__ __align__(16) long long s_first[TILE];
     __shared__ __align__(16) long long s_last[TILE];
     __shared__ __align__(16) uint64_t s_pid[TILE];
+#if !ZK_K1_SLOT16
     __shared__ __align__(16) uint32_t s_svck[TILE];
+#endif
 #if ZK_K1_SORTJOIN || !ZK_K1_SEG_IN_SLOT
     __shared__ __align__(16) uint16_t s_seg[TILE];
 #endif
     static_assert(!ZK_K1_SEG_IN_SLOT || TILE <= 512, "the segment field of the slot word is 9 bits");
+#if ZK_K1_SLOT16
+    __shared__ __align__(16) uint4 s_h16[H];  // {spanId lo, spanId hi, slot word, service key}
+#define ZK_HMETA(x) (&s_h16[x].z)
+#define ZK_HSVC(L, x) (&s_h16[x].w)
+#else
     __shared__ __align__(16) uint32_t s_ht[H];
+#define ZK_HMETA(x) (&s_ht[x])
+#define ZK_HSVC(L, x) (&s_svck[L])
+#endif
 #if ZK_K1_SORTJOIN
     __shared__ __align__(16) uint32_t s_bits[TILE];  // merged seen-once/twice + parent bits per leader
     __shared__ __align__(16) uint16_t s_perm[TILE];  // segment records in (spanId, index) order
@@ -512,7 +529,11 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     load_window<JOIN>(a, ws, cur);
 #endif
 #pragma unroll
+#if ZK_K1_SLOT16
+    for (int x = tid; x < H; x += WG) s_h16[x] = make_uint4(0u, 0u, 0u, kSvcNone);
+#else
     for (int x = tid; x < H / 4; x += WG) reinterpret_cast<uint4*>(s_ht)[x] = make_uint4(0u, 0u, 0u, 0u);
+#endif
     uint64_t m_ev, m_od;  // this wave's boundary ballots of the current window (uniform; phase 3 reuses them)
     constexpr bool EB = ZK_K1_EARLY_BALLOT && ABL != 2;  // (the stream-only diagnostic has no phase 7)
     if constexpr (EB) {
@@ -647,7 +668,11 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         // the last window's leaders empty their hash slots (see phase 7)
 #pragma unroll
         for (int e = 0; e < 2; ++e)
+#if ZK_K1_SLOT16
+            if (r_clear[e] != kNoSlot) s_h16[r_clear[e]] = make_uint4(0u, 0u, 0u, kSvcNone);
+#else
             if (r_clear[e] != kNoSlot) s_ht[r_clear[e]] = 0u;
+#endif
 #endif
         // ---- 3. segment ids and LDS staging ----------------------------------------------------
         // seg = index of the trace's first record in the window (the last boundary <= j), from the
@@ -656,6 +681,9 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         int r_seg[2];
         uint32_t r_svck[2];
         bool r_rerr[2];
+#if ZK_K1_SLOT16
+        uint32_t r_lsvc[2];
+#endif
 #if ZK_K1_SORTJOIN
         int r_end[2];  // end of the record's trace segment in the window
 #endif
@@ -680,11 +708,17 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 v_last[e] = ha ? cur.last[e] : (uint64_t)LLONG_MIN;
                 v_pid[e] = (f & ZK_F_HAS_PARENT) ? cur.pid[e] : ~0ull;
             }
+            uint32_t c_svck[2] = {r_svck[0], r_svck[1]};
             *reinterpret_cast<ulonglong2*>(&s_sid[j0]) = make_ulonglong2(cur.sid[0], cur.sid[1]);
             *reinterpret_cast<ulonglong2*>(&s_first[j0]) = make_ulonglong2(v_first[0], v_first[1]);
             *reinterpret_cast<ulonglong2*>(&s_last[j0]) = make_ulonglong2(v_last[0], v_last[1]);
             *reinterpret_cast<ulonglong2*>(&s_pid[j0]) = make_ulonglong2(v_pid[0], v_pid[1]);
-            *reinterpret_cast<uint2*>(&s_svck[j0]) = make_uint2(r_svck[0], r_svck[1]);
+#if !ZK_K1_SLOT16
+            *reinterpret_cast<uint2*>(&s_svck[j0]) = make_uint2(c_svck[0], c_svck[1]);
+#else
+            r_lsvc[0] = c_svck[0];  // a leader enters its (carrier) service into its slot
+            r_lsvc[1] = c_svck[1];
+#endif
 #if ZK_K1_SORTJOIN || !ZK_K1_SEG_IN_SLOT
             *reinterpret_cast<uint32_t*>(&s_seg[j0]) = ((uint32_t)r_seg[0] & 0xFFFFu) | ((uint32_t)r_seg[1] << 16);
 #endif
@@ -739,7 +773,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             while (act[0] || act[1]) {
                 uint32_t old[2];
 #pragma unroll
-                for (int e = 0; e < 2; ++e) old[e] = act[e] ? atomicCAS(&s_ht[r_slot[e]], 0u, word[e]) : 0u;
+                for (int e = 0; e < 2; ++e) old[e] = act[e] ? atomicCAS(ZK_HMETA(r_slot[e]), 0u, word[e]) : 0u;
                 int o[2];
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
@@ -747,6 +781,12 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                     if (act[e] && old[e] == 0u) {
                         r_leader[e] = 2 * tid + e;
                         act[e] = false;
+#if ZK_K1_SLOT16
+                        // the slot's spanId copy (read by the phase-6 probes, after two barriers) and
+                        // the leader's service (fragments that found it meanwhile min in theirs)
+                        *reinterpret_cast<uint64_t*>(&s_h16[r_slot[e]].x) = cur.sid[e];
+                        if (r_lsvc[e] != kSvcNone) atomicMin(&s_h16[r_slot[e]].w, r_lsvc[e]);
+#endif
                     }
                 }
                 uint64_t osid[2];
@@ -789,14 +829,14 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                     atomicMin(&s_first[L], (long long)cur.first[e]);
                     atomicMax(&s_last[L], (long long)cur.last[e]);
                 }
-                if (r_svck[e] != kSvcNone) atomicMin(&s_svck[L], r_svck[e]);
+                if (r_svck[e] != kSvcNone) atomicMin(ZK_HSVC(L, r_slot[e]), r_svck[e]);
                 if (f & ZK_F_HAS_PARENT) atomicMin((unsigned long long*)&s_pid[L], (unsigned long long)cur.pid[e]);
                 uint32_t once;
                 const uint32_t bits = frag_bits(f, &once);
 #if ZK_K1_SORTJOIN
                 uint32_t* const wp = &s_bits[L];
 #else
-                uint32_t* const wp = &s_ht[r_slot[e]];
+                uint32_t* const wp = ZK_HMETA(r_slot[e]);
 #endif
                 const uint32_t old = atomicOr(wp, bits);
                 const uint32_t promote = once & (old >> kSlotA) & 0xFu;  // second occurrence
@@ -821,10 +861,14 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             const uint32_t f = cur.flags[e];
 #if ZK_K1_SORTJOIN
             const uint32_t w = s_bits[L];
+            const uint32_t sL = s_svck[L];
+#elif ZK_K1_SLOT16
+            const uint4 q = s_h16[r_slot[e]];
+            const uint32_t w = q.z, sL = q.w;
 #else
             const uint32_t w = s_ht[r_slot[e]];
-#endif
             const uint32_t sL = s_svck[L];
+#endif
             const uint64_t pL = s_pid[L];
             bool amb = (f & ZK_F_HAS_PARENT) ? (cur.pid[e] != pL) : ((w & kSlotP1) != 0u);
             const uint32_t sk = r_svck[e];
@@ -883,6 +927,24 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             const uint16_t seg = (uint16_t)r_seg[e];
             uint32_t slot = slot_hash(pL, seg) & (H - 1);
             uint32_t pw = 0;
+#if ZK_K1_SLOT16
+            uint32_t sp = kSvcNone;
+            for (;;) {
+                const uint4 q = s_h16[slot];  // spanId, slot word and service in one read
+                if (q.z == 0u) break;
+                if (((q.z >> kSlotSegShift) & 0x1FFu) == seg && (((uint64_t)q.y << 32) | q.x) == pL) {
+                    pw = q.z;
+                    sp = q.w;
+                    break;
+                }
+                slot = (slot + 1) & (H - 1);
+            }
+            if (pw == 0u || !slot_valid(pw)) {
+                st.inc(ST_MISSING_PARENT);
+                continue;
+            }
+            st.inc(ST_JOINED);
+#else
             for (;;) {
                 const uint32_t o = s_ht[slot];
                 if (o == 0u) break;
@@ -903,6 +965,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             }
             st.inc(ST_JOINED);
             const uint32_t sp = s_svck[(pw & kSlotIdx) - 1];
+#endif
 #endif
             if (sp == kSvcNone || sL == kSvcNone) {
                 st.inc(ST_NO_SERVICE);
@@ -1011,7 +1074,11 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         // the next window inserts only after its phase-1 and phase-3 barriers)
 #pragma unroll
         for (int e = 0; e < 2; ++e)
+#if ZK_K1_SLOT16
+            if (r_leader[e] == 2 * tid + e) s_h16[r_slot[e]] = make_uint4(0u, 0u, 0u, kSvcNone);
+#else
             if (!ZK_K1_SORTJOIN && r_leader[e] == 2 * tid + e) s_ht[r_slot[e]] = 0u;
+#endif
 #endif
         ZK_STAMP(6);
         }  // ablate != 2
