@@ -37,6 +37,8 @@
 // ZK_ERR_NOT_CLUSTERED). Exact: the set stores whole traceIds, so it has no false positives.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include <hipcub/hipcub.hpp>
 
 #include "zk_block.h"
@@ -112,9 +114,23 @@ __global__ void k_cl_bounds(const uint32_t* __restrict__ offs, uint32_t nd, uint
 
 // ---- P1 / P2: chunked LDS-staged scatter ---------------------------------------------------------
 constexpr int kScWG = 1024;
-constexpr int kScU = 8;
+#ifndef ZK_CL_SCU
+#define ZK_CL_SCU 8
+#endif
+#ifndef ZK_CL_SC_GRID
+#define ZK_CL_SC_GRID 1  // P0/P1 workgroups per CU
+#endif
+constexpr int kScU = ZK_CL_SCU;
 constexpr int kScChunk = kScWG * kScU;  // 8192 records per chunk
 constexpr uint32_t kMaxDigits = 2048;   // <= 11 bits per level
+// levels of <= 256 digits (8 bits: every level up to 2^24 records) run a variant with byte digit
+// tags and 3 KB of digit arrays (75 KB of LDS instead of 104 KB). Two such workgroups per CU need
+// <= 64 VGPRs, which spills (52 B/lane): 9.07 ms for the clustering pass at 1e8 against 8.65 ms at
+// one workgroup per CU (profiles/r03/ab_cluster.txt)
+constexpr uint32_t kSmallDigits = 256;
+#ifndef ZK_CL_SMALL_GRID
+#define ZK_CL_SMALL_GRID 1  // P0/P1 workgroups per CU when the first level has <= 256 digits (2: 64 VGPRs, spills)
+#endif
 
 struct ScatterArgs {
     SpanColsDev in;  // in.n = records of the whole batch
@@ -160,7 +176,7 @@ __device__ __forceinline__ void col_store(const SpanColsMut& c, uint64_t i, uint
 // stores, so a column's HBM latency hides behind the previous column's LDS round trip.
 template <int U, int WG, int C = 0>
 __device__ __forceinline__ void move_columns(const SpanColsDev& in, const SpanColsMut& out, uint64_t base,
-                                             uint32_t cnt, const uint32_t (&pos)[U], const uint64_t (&dest)[U],
+                                             uint32_t cnt, const uint32_t (&pos)[U], const uint32_t (&dest)[U],
                                              uint64_t* stage, uint64_t (&v)[U]) {
     const int t = threadIdx.x;
 #pragma unroll
@@ -184,10 +200,10 @@ __device__ __forceinline__ void move_columns(const SpanColsDev& in, const SpanCo
 }
 
 // exclusive scan of s_cnt[0..nd) into out[d] = add + offset (one pass of the whole workgroup)
-template <int WG>
+template <int WG, uint32_t MAXD>
 __device__ __forceinline__ void scan_digits(const uint32_t* s_cnt, uint32_t nd, uint32_t add, uint32_t* out,
                                             uint32_t* s_tmp) {
-    constexpr int DPT = (kMaxDigits + WG - 1) / WG;
+    constexpr int DPT = (MAXD + WG - 1) / WG;
     const int t = threadIdx.x;
     uint32_t h[DPT], sum = 0;
 #pragma unroll
@@ -206,12 +222,13 @@ __device__ __forceinline__ void scan_digits(const uint32_t* s_cnt, uint32_t nd, 
     }
 }
 
-template <bool LOCAL>
-__global__ __launch_bounds__(kScWG) void k_cl_scatter(ScatterArgs a) {
-    __shared__ uint32_t s_cur[kMaxDigits];  // output position of each digit's next record
-    __shared__ uint32_t s_cnt[kMaxDigits];  // records of the chunk per digit
-    __shared__ uint32_t s_off[kMaxDigits];  // exclusive offsets of the digits inside the sorted chunk
-    __shared__ uint16_t s_dig[kScChunk];    // digit of the sorted chunk's record i
+template <bool LOCAL, uint32_t MAXD>
+__global__ __launch_bounds__(kScWG, (MAXD <= 256 ? 4 * ZK_CL_SMALL_GRID : 4)) void k_cl_scatter(ScatterArgs a) {
+    using DigT = typename std::conditional<(MAXD <= 256), uint8_t, uint16_t>::type;
+    __shared__ uint32_t s_cur[MAXD];  // output position of each digit's next record
+    __shared__ uint32_t s_cnt[MAXD];  // records of the chunk per digit
+    __shared__ uint32_t s_off[MAXD];  // exclusive offsets of the digits inside the sorted chunk
+    __shared__ DigT s_dig[kScChunk];  // digit of the sorted chunk's record i
     __shared__ __align__(16) uint64_t s_stage[kScChunk];
     __shared__ uint32_t s_tmp[32];
     const int t = threadIdx.x;
@@ -235,7 +252,7 @@ __global__ __launch_bounds__(kScWG) void k_cl_scatter(ScatterArgs a) {
                 if (b + t + (uint64_t)k * kScWG < hi) atomicAdd(&s_cnt[digit_of(part_hash(v[k]), a.shift, mask)], 1u);
         }
         __syncthreads();
-        scan_digits<kScWG>(s_cnt, nd, (uint32_t)lo, s_cur, s_tmp);
+        scan_digits<kScWG, MAXD>(s_cnt, nd, (uint32_t)lo, s_cur, s_tmp);
         __syncthreads();
         for (uint32_t d = t; d < nd; d += kScWG) a.sub[(uint64_t)blockIdx.x * nd + d] = s_cur[d];
         if (blockIdx.x == a.nbuckets - 1 && t == 0) a.sub[(uint64_t)a.nbuckets * nd] = (uint32_t)a.in.n;
@@ -263,15 +280,15 @@ __global__ __launch_bounds__(kScWG) void k_cl_scatter(ScatterArgs a) {
         }
         __syncthreads();
         // 2. digit offsets inside the chunk
-        scan_digits<kScWG>(s_cnt, nd, 0u, s_off, s_tmp);
+        scan_digits<kScWG, MAXD>(s_cnt, nd, 0u, s_off, s_tmp);
         __syncthreads();
         // 3. sorted position of each loaded record; digit of each sorted slot
         uint32_t pos[kScU];
-        uint64_t dest[kScU];
+        uint32_t dest[kScU];  // (record positions fit 32 bits: the bounds are u32)
 #pragma unroll
         for (int k = 0; k < kScU; ++k) {
             pos[k] = s_off[dg[k]] + rank[k];
-            if (t + k * kScWG < cnt) s_dig[pos[k]] = (uint16_t)dg[k];
+            if (t + k * kScWG < cnt) s_dig[pos[k]] = (DigT)dg[k];
         }
         __syncthreads();
         // 4. output position of each sorted slot this thread writes
@@ -279,7 +296,7 @@ __global__ __launch_bounds__(kScWG) void k_cl_scatter(ScatterArgs a) {
         for (int k = 0; k < kScU; ++k) {
             const uint32_t i = t + k * kScWG;
             const uint32_t d = i < cnt ? s_dig[i] : 0u;
-            dest[k] = i < cnt ? (uint64_t)s_cur[d] + (i - s_off[d]) : 0ull;
+            dest[k] = i < cnt ? s_cur[d] + (i - s_off[d]) : 0u;
         }
         // 5. the columns through the LDS stage (the traceIds are in registers already)
         {
@@ -300,7 +317,13 @@ __global__ __launch_bounds__(kScWG) void k_cl_scatter(ScatterArgs a) {
 
 // ---- P3: trace runs inside each sub-bucket --------------------------------------------------------
 constexpr int kTrWG = 512;
-constexpr uint32_t kTrSlots = 4096;    // LDS trace table: load <= 1/2 at <= 2048 records per round
+#ifndef ZK_CL_TR_SLOTS
+#define ZK_CL_TR_SLOTS 2048
+#endif
+#ifndef ZK_CL_TR_GRID
+#define ZK_CL_TR_GRID 2  // P3 workgroups per CU
+#endif
+constexpr uint32_t kTrSlots = ZK_CL_TR_SLOTS;  // LDS trace table: load <= 1/2 at <= kTrSlots / 2 records per round
 constexpr uint64_t kEmptyKey = ~0ull;  // a traceId equal to it takes the extra slot kTrSlots
 constexpr int kTrFast = 4096;          // sub-buckets up to this many records: the LDS-staged path
 constexpr int kTrStage = 2 * kTrFast;  // s_cur words: the fast path's u64 column stage aliases it
@@ -405,11 +428,11 @@ __global__ __launch_bounds__(kTrWG) void k_cl_traces(TraceArgs a) {
                 }
                 __syncthreads();
                 uint32_t pos[U];
-                uint64_t dest[U];
+                uint32_t dest[U];
 #pragma unroll
                 for (int k = 0; k < U; ++k) {
                     pos[k] = s_cnt[slot[k]] + rank[k];
-                    dest[k] = lo + t + k * kTrWG;
+                    dest[k] = (uint32_t)lo + t + k * kTrWG;
                 }
                 move_columns<U, kTrWG, 0>(a.in, a.out, lo, (uint32_t)len, pos, dest,
                                           reinterpret_cast<uint64_t*>(s_cur), tids);
@@ -613,7 +636,7 @@ ClusterPlan cluster_plan(uint64_t n, uint32_t cus) {
     p.nb1 = 1u << p.b1;
     p.nb2 = 1u << p.b2;
     // P0/P1 geometry: about one resident 1024-thread workgroup per CU, whole chunks each
-    uint64_t g = cus ? cus : 256;
+    uint64_t g = (uint64_t)(cus ? cus : 256) * (p.nb1 <= kSmallDigits ? ZK_CL_SMALL_GRID : ZK_CL_SC_GRID);
     const uint64_t chunks = (n + kScChunk - 1) / kScChunk;
     if (g > chunks) g = chunks ? chunks : 1;
     p.grid = (uint32_t)g;
@@ -679,7 +702,10 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
     a.offs = offs;
     a.shift = sh1;
     a.nd = p.nb1;
-    e = launch_checked("k_cl_scatter<global>", k_cl_scatter<false>, dim3(p.grid), dim3(kScWG), 0, s, a);
+    e = p.nb1 <= kSmallDigits
+            ? launch_checked("k_cl_scatter<global,256>", k_cl_scatter<false, kSmallDigits>, dim3(p.grid), dim3(kScWG), 0,
+                             s, a)
+            : launch_checked("k_cl_scatter<global>", k_cl_scatter<false, kMaxDigits>, dim3(p.grid), dim3(kScWG), 0, s, a);
     if (e != hipSuccess) return e;
     if (!p.b2) {  // P3: A -> B
         ta.in = dev(A);
@@ -696,7 +722,11 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
         b.sub = sub;
         b.shift = sh1 - p.b2;
         b.nd = p.nb2;
-        e = launch_checked("k_cl_scatter<local>", k_cl_scatter<true>, dim3(p.nb1), dim3(kScWG), 0, s, b);
+        e = p.nb2 <= kSmallDigits
+                ? launch_checked("k_cl_scatter<local,256>", k_cl_scatter<true, kSmallDigits>, dim3(p.nb1), dim3(kScWG),
+                                 0, s, b)
+                : launch_checked("k_cl_scatter<local>", k_cl_scatter<true, kMaxDigits>, dim3(p.nb1), dim3(kScWG), 0, s,
+                                 b);
         if (e != hipSuccess) return e;
         ta.in = dev(B);
         ta.out = A;
@@ -704,7 +734,7 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
         ta.nsub = p.nb1 * p.nb2;
         *result = 0;
     }
-    const uint32_t g3 = ta.nsub < 2 * cus ? ta.nsub : 2 * cus;
+    const uint32_t g3 = ta.nsub < ZK_CL_TR_GRID * cus ? ta.nsub : ZK_CL_TR_GRID * cus;
     return launch_checked("k_cl_traces", k_cl_traces, dim3(g3), dim3(kTrWG), 0, s, ta);
 }
 
