@@ -113,9 +113,17 @@ __global__ void k_cl_bounds(const uint32_t* __restrict__ offs, uint32_t nd, uint
 }
 
 // ---- P1 / P2: chunked LDS-staged scatter ---------------------------------------------------------
-constexpr int kScWG = 1024;
+#ifndef ZK_CL_SCWG
+#define ZK_CL_SCWG 1024
+#endif
+constexpr int kScWG = ZK_CL_SCWG;
 #ifndef ZK_CL_SCU
 #define ZK_CL_SCU 8
+#endif
+// diagnostic builds only (results wrong): 1 = every chunk written contiguously at its own input
+// position (the scatter's structure without its scattered stores), 2 = no column stores
+#ifndef ZK_CL_DIAG
+#define ZK_CL_DIAG 0
 #endif
 #ifndef ZK_CL_SC_GRID
 #define ZK_CL_SC_GRID 1  // P0/P1 workgroups per CU
@@ -193,7 +201,7 @@ __device__ __forceinline__ void move_columns(const SpanColsDev& in, const SpanCo
 #pragma unroll
     for (int k = 0; k < U; ++k) {
         const uint32_t i = t + k * WG;
-        if (i < cnt) col_store<C>(out, dest[k], stage[i]);
+        if (ZK_CL_DIAG != 2 && i < cnt) col_store<C>(out, dest[k], stage[i]);
     }
     __syncthreads();
     if constexpr (C < 6) move_columns<U, WG, C + 1>(in, out, base, cnt, pos, dest, stage, v);
@@ -223,7 +231,7 @@ __device__ __forceinline__ void scan_digits(const uint32_t* s_cnt, uint32_t nd, 
 }
 
 template <bool LOCAL, uint32_t MAXD>
-__global__ __launch_bounds__(kScWG, (MAXD <= 256 ? 4 * ZK_CL_SMALL_GRID : 4)) void k_cl_scatter(ScatterArgs a) {
+__global__ __launch_bounds__(kScWG, (MAXD <= 256 ? ZK_CL_SMALL_GRID : ZK_CL_SC_GRID) * kScWG / 256) void k_cl_scatter(ScatterArgs a) {
     using DigT = typename std::conditional<(MAXD <= 256), uint8_t, uint16_t>::type;
     __shared__ uint32_t s_cur[MAXD];  // output position of each digit's next record
     __shared__ uint32_t s_cnt[MAXD];  // records of the chunk per digit
@@ -297,6 +305,7 @@ __global__ __launch_bounds__(kScWG, (MAXD <= 256 ? 4 * ZK_CL_SMALL_GRID : 4)) vo
             const uint32_t i = t + k * kScWG;
             const uint32_t d = i < cnt ? s_dig[i] : 0u;
             dest[k] = i < cnt ? s_cur[d] + (i - s_off[d]) : 0u;
+            if (ZK_CL_DIAG == 1) dest[k] = (uint32_t)base + i;
         }
         // 5. the columns through the LDS stage (the traceIds are in registers already)
         {

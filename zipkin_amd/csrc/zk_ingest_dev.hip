@@ -420,11 +420,11 @@ __device__ __forceinline__ bool is_core(P v, uint32_t l, int* c) {
     return false;
 }
 
-// the service name of an endpoint struct: field 3 (string); absent or "" -> kUnknown
+// the service name of an endpoint struct: field 3 (string); absent or "" -> kUnknown. Like the
+// host's read_endpoint, a second host field of the same annotation keeps the first one's name
+// unless it has its own (the caller resets the name per annotation).
 template <class P>
 __device__ __forceinline__ void read_endpoint(DRdT<P>& r, P* name, uint32_t* nlen) {
-    *name = nullptr;
-    *nlen = 0;
     for (;;) {
         uint8_t t;
         int16_t id;
@@ -571,6 +571,212 @@ __device__ __forceinline__ int parse_record(const IngArgs& a, uint64_t i, P src,
     a.svc[i] = 0u;
     *nm_out = nm;
     *nl_out = nl;
+    return (srv_set || cli_set) ? 1 : 0;
+}
+
+// ---- the flat thrift walk (LDS decoder) -------------------------------------------------------
+// parse_record's nested loops and switches compile to exec-mask bookkeeping (~250 saveexec/branch
+// pairs and 210 SGPR spills in k_ing_decode_lds), and every lane pays for every path. The flat walk
+// consumes ONE token per iteration -- a struct field header and its value, a list/set/map element,
+// or a container end -- with the same straight-line code for every lane: one 16-byte LDS window at
+// the cursor, the value's width and the semantic capture as selects, and a container push/pop on
+// a 4-level register stack (span -> annotation list -> annotation -> endpoint; a span nested any
+// deeper goes to the global-memory decoder, like an oversized one). Accept/reject and every captured value follow
+// the host decoder (zk_ingest.cpp read_span / read_annotation / read_endpoint): last field wins,
+// an annotation's host name is reset per annotation only.
+// ZK_ING_FLAT (A/B, off): the LDS decoder walks with parse_record_flat instead of parse_record.
+// Measured on the bench's ingest workload (profiles/r03/ingest_flat_walk.txt): 15.6-15.9 ms per
+// 1.98e7 fragments against 14.1-14.3 ms -- the flat step costs ~350 instructions per token, half of
+// them scalar lane-mask logic, and the bench's spans all share one layout, so the branchy walk's
+// lanes hardly diverge. Kept as the starting point for a table-driven walk.
+#ifndef ZK_ING_FLAT
+#define ZK_ING_FLAT 0
+#endif
+namespace tw {
+constexpr uint32_t kStruct = 0, kList = 1, kMap = 2;
+// per thrift type (0..15): bytes of a value past its start (a string adds its length), as nibbles;
+// the valid value types; the container types
+constexpr uint64_t tw_width(int t) {
+    return t == T_BOOL || t == T_BYTE ? 1 : t == T_I16 ? 2 : t == T_I32 || t == T_STRING ? 4
+         : t == T_DOUBLE || t == T_I64 ? 8 : t == T_SET || t == T_LIST ? 5 : t == T_MAP ? 6 : 0;
+}
+constexpr uint64_t tw_widths() {
+    uint64_t w = 0;
+    for (int t = 0; t < 16; ++t) w |= tw_width(t) << (4 * t);
+    return w;
+}
+constexpr uint64_t kTypeWidth = tw_widths();
+constexpr uint32_t kKnownTypes = (1u << T_BOOL) | (1u << T_BYTE) | (1u << T_DOUBLE) | (1u << T_I16) | (1u << T_I32) |
+                                 (1u << T_I64) | (1u << T_STRING) | (1u << T_STRUCT) | (1u << T_MAP) | (1u << T_SET) |
+                                 (1u << T_LIST);
+constexpr uint32_t kContainerTypes = (1u << T_STRUCT) | (1u << T_MAP) | (1u << T_SET) | (1u << T_LIST);
+constexpr uint32_t kSkip = 0, kSpan = 1, kAnnList = 2, kAnn = 3, kEp = 4;
+// level word: kind (bits 0-1), semantic context (2-4), list element / map key type (8-15), map
+// value type (16-23); the level's remaining element count travels beside it
+__device__ __forceinline__ uint32_t lvl(uint32_t kind, uint32_t sem, uint32_t et, uint32_t vt) {
+    return kind | (sem << 2) | (et << 8) | (vt << 16);
+}
+}  // namespace tw
+
+// lane flags of the flat walk (one VGPR instead of a dozen lane masks)
+constexpr uint32_t F_DONE = 1u << 0, F_BAD = 1u << 1, F_DEEP = 1u << 2, F_PAR = 1u << 3, F_NAME = 1u << 4,
+                   F_INVALID = 1u << 5, F_VSET = 1u << 6, F_HOST = 1u << 7, F_HNSET = 1u << 8, F_SRV = 1u << 9,
+                   F_CLI = 1u << 10, F_SRVN = 1u << 11, F_CLIN = 1u << 12;
+
+// The record and the service name (an LDS byte offset into `base`) of the Span at [p0, p0 + len).
+// Returns like parse_record: -1 (status set), 0 (no service), 1 (*nm_off / *nl set; *nm_off = ~0u:
+// "Unknown service name"); -2: nested deeper than the register stack (nothing written: defer).
+// Every per-token decision is a select: the loop's exit is the only branch.
+__device__ __forceinline__ int parse_record_flat(const IngArgs& a, uint64_t i, const lds_u8* base, uint32_t p0,
+                                                 uint32_t len, uint32_t* nm_off, uint32_t* nl_out) {
+    using namespace tw;
+    uint32_t p = p0;
+    const uint32_t e = p0 + len;
+    uint32_t fl = 0;
+    uint32_t d = 0;
+    uint32_t mt = lvl(kStruct, kSpan, 0, 0);  // the open container (top of the stack)
+    uint32_t nt = 0;
+    uint32_t sm0 = 0, sm1 = 0, sm2 = 0, sn0 = 0, sn1 = 0, sn2 = 0;  // saved levels 0..2
+    uint64_t trace = 0, id = 0, parent = 0;
+    int64_t first = 0, last = 0;
+    uint32_t nann = 0, cnt = 0;  // cnt: 2-bit counts of cs | cr << 2 | sr << 4 | ss << 6
+    int64_t ts = 0;              // the annotation being read
+    uint32_t vl = 0, vc = 0, hn = 0, hl = 0;
+    uint32_t srv = 0, srv_len = 0, cli = 0, cli_len = 0;  // first server / client core annotation with a host
+    while (!(fl & F_DONE)) {
+        uint64_t lo, hi;
+        __builtin_memcpy(&lo, base + p, 8);
+        __builtin_memcpy(&hi, base + p + 8, 8);
+        const uint32_t kind = mt & 3u, sem = (mt >> 2) & 7u;
+        const uint32_t avail = e - p;
+        const bool in_struct = kind == kStruct;
+        // the token: a struct field header, or the next element of a list / map (keys and values alternate)
+        const uint32_t et = (kind == kList || (nt & 1u) == 0u) ? (mt >> 8) & 0xFFu : (mt >> 16) & 0xFFu;
+        const uint32_t t = in_struct ? (uint32_t)(lo & 0xFFu) : et;
+        const int32_t fid = in_struct ? (int32_t)(int16_t)__builtin_bswap16((uint16_t)(lo >> 8)) : -1;
+        const bool end = in_struct ? t == T_STOP : nt == 0u;
+        // ---- the value of type t at q = p + vofs
+        const uint32_t vofs = in_struct ? 3u : 0u;
+        const uint64_t vlo = in_struct ? ((lo >> 24) | (hi << 40)) : lo;
+        const uint32_t w32 = __builtin_bswap32((uint32_t)vlo);  // i32 / string length at q
+        const uint64_t w64 = __builtin_bswap64(vlo);            // i64 at q
+        // width / validity of type t from packed tables (compare chains compile to a branch tree):
+        // the value's bytes past q (a string's length word, a list's or map's header), 0 for a struct
+        const uint32_t t4 = t & 15u;
+        const bool known = t < 16u && ((kKnownTypes >> t4) & 1u);
+        const bool is_str = t == T_STRING, is_list = (t | 1u) == T_LIST, is_map = t == T_MAP;
+        const bool container = ((kContainerTypes >> t4) & 1u) & (t < 16u);
+        const int32_t lcnt = (int32_t)__builtin_bswap32((uint32_t)(vlo >> 8));
+        const int32_t mcnt = (int32_t)__builtin_bswap32((uint32_t)(vlo >> 16));
+        const uint64_t w = ((kTypeWidth >> (4u * t4)) & 15u) + (is_str ? (uint64_t)(int64_t)(int32_t)w32 : 0ull);
+        // a map's entries alternate key and value; > 2^29 entries cannot fit a 16 MiB fragment
+        const int64_t ncnt = is_list ? (int64_t)lcnt : is_map ? (mcnt > (1 << 29) ? -1ll : 2ll * mcnt) : 0ll;
+        const bool vbad = !known | (is_str & ((int32_t)w32 < 0)) | (ncnt < 0) | ((uint64_t)avail < vofs + w);
+        const bool bad = end ? (in_struct && avail < 1u) : vbad;
+        const bool val = !end && !bad;  // a value was read
+        const bool deep = val && container && d == 3u;
+        const bool push = val && container && d < 3u;
+        const bool pop = end && !bad;
+        const uint32_t q = p + vofs;
+        p += bad ? 0u : end ? (in_struct ? 1u : 0u) : vofs + (uint32_t)w;
+        // ---- semantic capture (the host's read_span / read_annotation / read_endpoint)
+        const bool sspan = val && sem == kSpan, sann = val && sem == kAnn, sep = val && sem == kEp;
+        trace = (sspan && fid == 1 && t == T_I64) ? w64 : trace;
+        id = (sspan && fid == 4 && t == T_I64) ? w64 : id;
+        const bool gpar = sspan && fid == 5 && t == T_I64;
+        parent = gpar ? w64 : parent;
+        fl |= (gpar ? F_PAR : 0u) | ((sspan && fid == 3 && is_str) ? F_NAME : 0u);
+        ts = (sann && fid == 1 && t == T_I64) ? (int64_t)w64 : ts;
+        const bool gval = sann && fid == 2 && is_str;
+        vl = gval ? w32 : vl;
+        vc = gval ? (uint32_t)((vlo >> 32) & 0xFFFFu) : vc;
+        const bool ghn = sep && fid == 3 && is_str;
+        hn = ghn ? q + 4u : hn;
+        hl = ghn ? w32 : hl;
+        fl |= (gval ? F_VSET : 0u) | ((sann && fid == 3 && t == T_STRUCT) ? F_HOST : 0u) | (ghn ? F_HNSET : 0u);
+        // ---- an annotation ends: thrift.scala:66-71 validation, Span.scala:213-240 first/last/core
+        const bool commit = pop && sem == kAnn;
+        const bool vset = (fl & F_VSET) != 0u;
+        fl |= (commit && (ts <= 0 || (vset && vl == 0u))) ? F_INVALID : 0u;
+        first = (commit && (nann == 0u || ts < first)) ? ts : first;
+        last = (commit && (nann == 0u || ts > last)) ? ts : last;
+        nann += commit ? 1u : 0u;
+        const uint32_t c0 = vc & 0xFFu, c1 = vc >> 8;
+        const bool core = commit && vset && vl == 2u &&
+                          ((c0 == 'c' && (c1 == 's' || c1 == 'r')) || (c0 == 's' && (c1 == 'r' || c1 == 's')));
+        const uint32_t c = c0 == 'c' ? (c1 == 's' ? 0u : 1u) : (c1 == 'r' ? 2u : 3u);
+        cnt += (core && ((cnt >> (2 * c)) & 3u) < 2u) ? (1u << (2 * c)) : 0u;
+        const bool hst = core && (fl & F_HOST) != 0u, named = (fl & F_HNSET) != 0u;
+        const bool tsrv = hst && c >= 2u && !(fl & F_SRV), tcli = hst && c < 2u && !(fl & F_CLI);
+        srv = tsrv ? hn : srv;
+        srv_len = tsrv ? hl : srv_len;
+        cli = tcli ? hn : cli;
+        cli_len = tcli ? hl : cli_len;
+        fl |= (tsrv ? F_SRV | (named ? F_SRVN : 0u) : 0u) | (tcli ? F_CLI | (named ? F_CLIN : 0u) : 0u);
+        // ---- push / pop on the register stack
+        uint32_t nsem = kSkip;
+        nsem = (t == T_STRUCT && sem == kAnnList) ? kAnn : nsem;
+        nsem = (t == T_STRUCT && sem == kAnn && fid == 3) ? kEp : nsem;
+        nsem = (is_list && sem == kSpan && fid == 6 && (vlo & 0xFFu) == T_STRUCT) ? kAnnList : nsem;
+        const bool nann_start = push && nsem == kAnn;  // a new annotation: reset its fields
+        ts = nann_start ? 0 : ts;
+        vl = nann_start ? 0u : vl;
+        vc = nann_start ? 0u : vc;
+        hn = nann_start ? 0u : hn;
+        hl = nann_start ? 0u : hl;
+        fl &= nann_start ? ~(F_VSET | F_HOST | F_HNSET) : ~0u;
+        nt -= (val && !in_struct) ? 1u : 0u;
+        sm0 = (push && d == 0u) ? mt : sm0;
+        sn0 = (push && d == 0u) ? nt : sn0;
+        sm1 = (push && d == 1u) ? mt : sm1;
+        sn1 = (push && d == 1u) ? nt : sn1;
+        sm2 = (push && d == 2u) ? mt : sm2;
+        sn2 = (push && d == 2u) ? nt : sn2;
+        const uint32_t nkind = is_list ? kList : is_map ? kMap : kStruct;
+        const uint32_t pm = d == 1u ? sm0 : d == 2u ? sm1 : sm2, pn = d == 1u ? sn0 : d == 2u ? sn1 : sn2;
+        mt = push ? lvl(nkind, nsem, (is_list || is_map) ? (uint32_t)(vlo & 0xFFu) : 0u,
+                        is_map ? (uint32_t)((vlo >> 8) & 0xFFu) : 0u)
+                  : (pop && d > 0u) ? pm : mt;
+        nt = push ? (uint32_t)ncnt : (pop && d > 0u) ? pn : nt;
+        fl |= (bad ? F_BAD | F_DONE : 0u) | (deep ? F_DEEP | F_DONE : 0u) | ((pop && d == 0u) ? F_DONE : 0u);
+        d = push ? d + 1u : (pop && d > 0u) ? d - 1u : d;
+    }
+    if (fl & F_DEEP) return -2;
+    if (fl & F_BAD) {
+        a.status[i] = kStUndecodable;
+        return -1;
+    }
+    if (!(fl & F_NAME) || (fl & F_INVALID)) {  // IncompleteTraceDataException / IllegalArgumentException
+        a.status[i] = kStInvalid;
+        return -1;
+    }
+    const bool has_parent = (fl & F_PAR) != 0u, srv_set = (fl & F_SRV) != 0u, cli_set = (fl & F_CLI) != 0u;
+    uint32_t f = has_parent ? ZK_F_HAS_PARENT : 0u;
+    if (nann) f |= ZK_F_HAS_ANNOTATIONS;
+    *nm_off = ~0u;
+    *nl_out = 0u;
+    if (srv_set) {
+        f |= ZK_F_SVC_SERVER;
+        if ((fl & F_SRVN) && srv_len) {
+            *nm_off = srv;
+            *nl_out = srv_len;
+        }
+    } else if (cli_set) {
+        f |= ZK_F_SVC_CLIENT;
+        if ((fl & F_CLIN) && cli_len) {
+            *nm_off = cli;
+            *nl_out = cli_len;
+        }
+    }
+    f |= ((cnt & 3u) << ZK_F_CS_SHIFT) | (((cnt >> 2) & 3u) << ZK_F_CR_SHIFT) | (((cnt >> 4) & 3u) << ZK_F_SR_SHIFT) |
+         (((cnt >> 6) & 3u) << ZK_F_SS_SHIFT);
+    a.tid[i] = trace;
+    a.sid[i] = id;
+    a.pid[i] = has_parent ? parent : 0ull;
+    a.first[i] = nann ? first : 0;
+    a.last[i] = nann ? last : 0;
+    a.flags[i] = f;
+    a.svc[i] = 0u;
     return (srv_set || cli_set) ? 1 : 0;
 }
 
@@ -724,11 +930,42 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
+// ---- diagnostic phase stamps (separate build with -DZK_ING_STAMPS; never in the product .so) --
+#ifdef ZK_ING_STAMPS
+__device__ unsigned long long g_ing_stamps[8];
+__device__ __forceinline__ unsigned long long ing_memtime() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define ING_STAMP_DECL                            \
+    unsigned long long ing_prev = ing_memtime();  \
+    unsigned long long ing_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define ING_STAMP(k)                                      \
+    do {                                                  \
+        const unsigned long long ing_t = ing_memtime();   \
+        ing_acc[k] += ing_t - ing_prev;                   \
+        ing_prev = ing_t;                                 \
+    } while (0)
+#define ING_STAMP_FLUSH()                                                          \
+    do {                                                                           \
+        if (threadIdx.x == 0)                                                      \
+            for (int q = 0; q < 8; ++q) atomicAdd(&g_ing_stamps[q], ing_acc[q]);  \
+    } while (0)
+#else
+#define ING_STAMP_DECL
+#define ING_STAMP(k)
+#define ING_STAMP_FLUSH()
+#endif
+
 __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
     __shared__ __align__(16) uint8_t s_buf[kLdsBudget];
     const uint32_t lane = threadIdx.x;
     const uint64_t blk0 = (uint64_t)blockIdx.x * kLdsBlock;
     const uint64_t blk1 = blk0 + kLdsBlock < a.n ? blk0 + kLdsBlock : a.n;
+    ING_STAMP_DECL
     for (uint64_t f0 = blk0; f0 < blk1;) {  // uniform
         const uint64_t i = f0 + lane;
         const bool have = i < blk1;
@@ -747,6 +984,7 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
         // this round: the longest prefix of lanes that fits (at least lane 0, to make progress)
         uint32_t k = (uint32_t)__popcll(__ballot(have && incl <= kLdsBudget));
         if (k == 0) k = 1;  // lane 0 alone does not fit: deferred below
+        ING_STAMP(0);
         if (lane < k && have) {
             a.keep[i] = 0u;
             a.svc_hash[i] = 0ull;
@@ -766,6 +1004,7 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                 const uint32_t nblk = (uint32_t)((clen + mis + 15) >> 4);
                 u32x4* dst = reinterpret_cast<u32x4*>(reg + D - mis);
                 for (uint32_t c = 0; c < nblk; ++c) dst[c] = g[c];
+                ING_STAMP(1);
                 // the region as an LDS pointer: the decoder's byte and word reads become ds_read_*.
                 // Regions start on 16-byte boundaries, i.e. on one of 8 bank offsets of a 32-bank
                 // group; lanes parsing the same field at the same offset then collide. The
@@ -780,16 +1019,32 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                     src = lreg + skew;
                     len = raw;
                 }
+                ING_STAMP(2);
                 if (!ok) {
                     a.status[i] = unsafe ? kStDefer : kStUndecodable;
                 } else {
-                    const uint8_t* nm;
-                    uint32_t nl;
-                    const int r = parse_record(a, i, src, len, &nm, &nl);
+                    const lds_u8* const lbase = (const lds_u8*)s_buf;
+                    const uint32_t p0 = (uint32_t)(src - lbase);
+                    uint32_t nmo, nl;
+#if ZK_ING_FLAT
+                    int r = parse_record_flat(a, i, lbase, p0, (uint32_t)len, &nmo, &nl);
+                    if (r == -2) {
+                        a.status[i] = kStDefer;
+                        r = -1;
+                    }
+#else
+                    const uint8_t* gnm = nullptr;
+                    const int r = parse_record(a, i, src, len, &gnm, &nl);
+                    nmo = (r == 1 && gnm != (const uint8_t*)a.unknown) ? (uint32_t)(gnm - (const uint8_t*)lbase) : ~0u;
+#endif
+                    const bool unknown = nmo == ~0u;
+                    const uint8_t* nm = unknown ? a.unknown : (const uint8_t*)(lbase + nmo);
+                    if (unknown) nl = sizeof(kUnknown) - 1;
+                    ING_STAMP(3);
                     if (r >= 0) {
                         if (r && !try_resolve(a, i, nm, nl, d_hash(nm, nl))) {
-                            if (nm != a.unknown) {  // the name lies in this lane's own bytes
-                                const uint64_t off = (uint64_t)(nm - (const uint8_t*)src);
+                            if (!unknown) {  // the name lies in this lane's own bytes
+                                const uint64_t off = nmo - p0;
                                 if (a.snappy) {
                                     uint8_t* gd = a.scratch + a.raw_off[i] + off;  // copy out to the scratch
                                     for (uint32_t q = 0; q < nl; ++q) gd[q] = nm[q];
@@ -805,9 +1060,12 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                 }
             }
         }
+        ING_STAMP(4);
         f0 += k;
         __syncthreads();  // one wave: this round's LDS accesses complete before the next round's copies
+        ING_STAMP(5);
     }
+    ING_STAMP_FLUSH();
 }
 
 __global__ __launch_bounds__(kIngWG) void k_ing_dict_insert(IngArgs a) {
@@ -1011,6 +1269,17 @@ zk_status zk_ingest_dev_destroy(zk_ingest_dev* g) {
 }
 
 const char* zk_ingest_dev_last_error(const zk_ingest_dev* g) { return g ? g->err.c_str() : "null decoder"; }
+
+#ifdef ZK_ING_STAMPS
+int zk_debug_ing_stamps(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ing_stamps), 8 * 8) != hipSuccess) return 1;
+    if (reset) {
+        unsigned long long z[8] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_ing_stamps), z, sizeof(z)) != hipSuccess) return 1;
+    }
+    return 0;
+}
+#endif
 
 zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* offsets, uint64_t n,
                               uint32_t codec, uint32_t flags, const zk_span_cols* out, uint64_t* n_out,
