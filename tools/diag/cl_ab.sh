@@ -12,10 +12,11 @@ for v in "$@"; do
     -- python3 tools/diag/cl_time.py ${CL_ARGS:-} > gpurun_out/clab_$v.log 2>&1 || { echo "$v failed"; tail -5 gpurun_out/clab_$v.log; exit 1; }
   grep "cluster" gpurun_out/clab_$v.log | tail -1
   python3 - gpurun_out/clab_$v/run_kernel_stats.csv <<'PY'
-import csv, sys
+import csv, re, sys
 for r in csv.DictReader(open(sys.argv[1])):
     n = r["Name"]
     if any(k in n for k in ("k_cl_", "k_span_join_stream", "k_link_scatter", "k_bucket_lds")):
-        print(f"    {n.split('(')[0][-48:]:48s} {int(r['Calls']):4d} x {float(r['AverageNs']) / 1e6:8.4f} ms")
+        m = re.search(r"(k_\w+(?:<[^>]*>)?)", n)
+        print(f"    {(m.group(1) if m else n)[:48]:48s} {int(r['Calls']):4d} x {float(r['AverageNs']) / 1e6:8.4f} ms")
 PY
 done
