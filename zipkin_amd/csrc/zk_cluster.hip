@@ -324,6 +324,205 @@ __global__ __launch_bounds__(kScWG, (MAXD <= 256 ? ZK_CL_SMALL_GRID : ZK_CL_SC_G
     }
 }
 
+// ---- P1 / P2 with write-combining carries (levels of <= 256 digits) -------------------------------
+// k_cl_scatter writes each chunk's per-digit runs as they fall: at 32 records per digit per chunk
+// both ends of every run are partial 64-B segments, and the 256 x 7 open tails of a workgroup are
+// evicted from L2 before the next chunk completes them (1.1 ms of a 3.0 ms pass,
+// profiles/r03/ab_cluster_writes.txt). Here every (digit, column) keeps the records of its last
+// incomplete 64-B segment in LDS: a chunk writes a digit's run only up to the last segment boundary
+// (plus the carried head of the segment it completes, in the same phase), and the rest becomes the
+// new carry. The head of a digit's range (not segment-aligned) and the tails at the end are the
+// only partial segments. 152 KB of LDS: one 1024-thread workgroup per CU, chunks of 4096 records.
+#ifndef ZK_CL_WC
+#define ZK_CL_WC 1  // 0: the round-2/3 scatter (runs written as they fall)
+#endif
+constexpr int kWcWG = 1024;
+constexpr int kWcU = 4;
+constexpr int kWcChunk = kWcWG * kWcU;
+constexpr uint32_t kWcDigits = 256;
+
+struct WcLds {
+    uint64_t stage[kWcChunk];        // the chunk's current column in digit order
+    uint64_t c64[5][kWcDigits][8];   // carries of the u64 columns (8 per 64-B segment)
+    uint32_t c32[2][kWcDigits][16];  // carries of the u32 columns (16 per segment)
+    uint32_t cur[kWcDigits];         // output position of each digit's next record
+    uint32_t cnt[kWcDigits];         // records of the chunk per digit
+    uint32_t off[kWcDigits];         // exclusive offsets of the digits inside the sorted chunk
+    uint32_t rs[kWcDigits];          // start of each digit's output range (not segment-aligned)
+    uint8_t dig[kWcChunk];           // digit of the sorted chunk's record i
+    uint32_t tmp[32];
+};
+
+template <int C>
+__device__ __forceinline__ void carry_put(WcLds& L, uint32_t d, uint32_t s, uint64_t v) {
+    if constexpr (C < 5)
+        L.c64[C][d][s] = v;
+    else
+        L.c32[C - 5][d][s] = (uint32_t)v;
+}
+template <int C>
+__device__ __forceinline__ uint64_t carry_get(const WcLds& L, uint32_t d, uint32_t s) {
+    if constexpr (C < 5)
+        return L.c64[C][d][s];
+    else
+        return L.c32[C - 5][d][s];
+}
+
+// the carried records of column C whose segment is complete (final: every carried record) go out
+template <int C, bool FINAL>
+__device__ __forceinline__ void carry_flush(const WcLds& L, const SpanColsMut& out, uint32_t nd) {
+    constexpr uint32_t E = C < 5 ? 8u : 16u;
+    for (uint32_t q = threadIdx.x; q < nd * E; q += kWcWG) {
+        const uint32_t d = q / E, s = q % E;
+        const uint32_t c = L.cur[d], seg = c & ~(E - 1u);
+        const uint32_t A = L.rs[d] > seg ? L.rs[d] : seg;
+        const uint32_t x = seg + s;
+        const uint32_t Z = FINAL ? c : (c + L.cnt[d]) & ~(E - 1u);
+        if (x >= A && x < c && x < Z) col_store<C>(out, x, carry_get<C>(L, d, s));
+    }
+}
+
+template <int C>
+__device__ __forceinline__ void move_columns_wc(const SpanColsDev& in, const SpanColsMut& out, uint64_t base,
+                                                uint32_t cnt, uint32_t nd, const uint32_t (&pos)[kWcU],
+                                                const uint32_t (&dest)[kWcU], const uint32_t (&dd)[kWcU], WcLds& L,
+                                                uint64_t (&v)[kWcU]) {
+    constexpr uint32_t E = C < 5 ? 8u : 16u;
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < kWcU; ++k)
+        if (t + k * kWcWG < cnt) L.stage[pos[k]] = v[k];
+    __syncthreads();
+    if constexpr (C < 6) {
+#pragma unroll
+        for (int k = 0; k < kWcU; ++k) {  // the next column, in flight during this column's stores
+            const uint32_t j = t + k * kWcWG;
+            v[k] = col_load<C + 1>(in, base + (j < cnt ? j : 0));
+        }
+    }
+    uint64_t cv[kWcU];
+    uint32_t cs[kWcU];
+    bool hc[kWcU];
+#pragma unroll
+    for (int k = 0; k < kWcU; ++k) {
+        const uint32_t i = t + k * kWcWG;
+        hc[k] = false;
+        cv[k] = 0;
+        cs[k] = 0;
+        if (i < cnt) {
+            const uint32_t d = dd[k];
+            const uint32_t Z = (L.cur[d] + L.cnt[d]) & ~(E - 1u);
+            const uint64_t val = L.stage[i];
+            if (dest[k] < Z) {
+                col_store<C>(out, dest[k], val);
+            } else {
+                hc[k] = true;
+                cv[k] = val;
+                cs[k] = dest[k] & (E - 1u);
+            }
+        }
+    }
+    carry_flush<C, false>(L, out, nd);
+    __syncthreads();  // the old carries are read before the new ones overwrite their slots
+#pragma unroll
+    for (int k = 0; k < kWcU; ++k)
+        if (hc[k]) carry_put<C>(L, dd[k], cs[k], cv[k]);
+    if constexpr (C < 6) move_columns_wc<C + 1>(in, out, base, cnt, nd, pos, dest, dd, L, v);
+}
+
+template <int C>
+__device__ __forceinline__ void carry_flush_all(const WcLds& L, const SpanColsMut& out, uint32_t nd) {
+    carry_flush<C, true>(L, out, nd);
+    if constexpr (C < 6) carry_flush_all<C + 1>(L, out, nd);
+}
+
+template <bool LOCAL>
+__global__ __launch_bounds__(kWcWG, kWcWG / 256) void k_cl_scatter_wc(ScatterArgs a) {
+    __shared__ WcLds L;
+    const int t = threadIdx.x;
+    const uint32_t nd = a.nd, mask = nd - 1;
+    uint64_t lo, hi;
+    if constexpr (LOCAL) {
+        lo = a.bucket[blockIdx.x];
+        hi = a.bucket[blockIdx.x + 1];
+        // sweep 1: the bucket's histogram of the second digit, then the sub-bucket bounds
+        for (uint32_t d = t; d < nd; d += kWcWG) L.cnt[d] = 0u;
+        __syncthreads();
+        for (uint64_t b = lo; b < hi; b += (uint64_t)kWcChunk) {
+            uint64_t v[kWcU];
+#pragma unroll
+            for (int k = 0; k < kWcU; ++k) {
+                const uint64_t i = b + t + (uint64_t)k * kWcWG;
+                v[k] = a.in.trace_id[i < hi ? i : lo];
+            }
+#pragma unroll
+            for (int k = 0; k < kWcU; ++k)
+                if (b + t + (uint64_t)k * kWcWG < hi) atomicAdd(&L.cnt[digit_of(part_hash(v[k]), a.shift, mask)], 1u);
+        }
+        __syncthreads();
+        scan_digits<kWcWG, kWcDigits>(L.cnt, nd, (uint32_t)lo, L.cur, L.tmp);
+        __syncthreads();
+        for (uint32_t d = t; d < nd; d += kWcWG) a.sub[(uint64_t)blockIdx.x * nd + d] = L.cur[d];
+        if (blockIdx.x == a.nbuckets - 1 && t == 0) a.sub[(uint64_t)a.nbuckets * nd] = (uint32_t)a.in.n;
+    } else {
+        lo = (uint64_t)blockIdx.x * a.per;
+        hi = lo + a.per < a.in.n ? lo + a.per : a.in.n;
+        for (uint32_t d = t; d < nd; d += kWcWG) L.cur[d] = a.offs[(uint64_t)d * a.grid + blockIdx.x];
+    }
+    for (uint32_t d = t; d < nd; d += kWcWG) {
+        L.cnt[d] = 0u;
+        L.rs[d] = L.cur[d];
+    }
+    __syncthreads();
+    for (uint64_t base = lo; base < hi; base += kWcChunk) {
+        const uint32_t cnt = (uint32_t)(hi - base < (uint64_t)kWcChunk ? hi - base : (uint64_t)kWcChunk);
+        // 1. digits and ranks (LDS atomic counting sort: the order inside a digit is free)
+        uint32_t dg[kWcU], rank[kWcU];
+        uint64_t v[kWcU];
+#pragma unroll
+        for (int k = 0; k < kWcU; ++k) {
+            const uint32_t j = t + k * kWcWG;
+            v[k] = a.in.trace_id[base + (j < cnt ? j : 0)];
+        }
+#pragma unroll
+        for (int k = 0; k < kWcU; ++k) {
+            dg[k] = digit_of(part_hash(v[k]), a.shift, mask);
+            rank[k] = (t + k * kWcWG < cnt) ? atomicAdd(&L.cnt[dg[k]], 1u) : 0u;
+        }
+        __syncthreads();
+        // 2. digit offsets inside the chunk
+        scan_digits<kWcWG, kWcDigits>(L.cnt, nd, 0u, L.off, L.tmp);
+        __syncthreads();
+        // 3. sorted position of each loaded record; digit of each sorted slot
+        uint32_t pos[kWcU];
+#pragma unroll
+        for (int k = 0; k < kWcU; ++k) {
+            pos[k] = L.off[dg[k]] + rank[k];
+            if (t + k * kWcWG < cnt) L.dig[pos[k]] = (uint8_t)dg[k];
+        }
+        __syncthreads();
+        // 4. digit and output position of each sorted slot this thread writes
+        uint32_t dest[kWcU], dd[kWcU];
+#pragma unroll
+        for (int k = 0; k < kWcU; ++k) {
+            const uint32_t i = t + k * kWcWG;
+            dd[k] = i < cnt ? L.dig[i] : 0u;
+            dest[k] = i < cnt ? L.cur[dd[k]] + (i - L.off[dd[k]]) : 0u;
+        }
+        // 5. the columns through the LDS stage and the carries (the traceIds are in registers)
+        move_columns_wc<0>(a.in, a.out, base, cnt, nd, pos, dest, dd, L, v);
+        __syncthreads();  // every carry of this chunk is in place before the cursors move
+        // 6. advance the cursors and clear the counts
+        for (uint32_t d = t; d < nd; d += kWcWG) {
+            L.cur[d] += L.cnt[d];
+            L.cnt[d] = 0u;
+        }
+        __syncthreads();
+    }
+    // the tail of every digit's range
+    carry_flush_all<0>(L, a.out, nd);
+}
+
 // ---- P3: trace runs inside each sub-bucket --------------------------------------------------------
 constexpr int kTrWG = 512;
 #ifndef ZK_CL_TR_SLOTS
@@ -711,7 +910,9 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
     a.offs = offs;
     a.shift = sh1;
     a.nd = p.nb1;
-    e = p.nb1 <= kSmallDigits
+    e = (ZK_CL_WC && p.nb1 <= kWcDigits)
+            ? launch_checked("k_cl_scatter_wc<global>", k_cl_scatter_wc<false>, dim3(p.grid), dim3(kWcWG), 0, s, a)
+        : p.nb1 <= kSmallDigits
             ? launch_checked("k_cl_scatter<global,256>", k_cl_scatter<false, kSmallDigits>, dim3(p.grid), dim3(kScWG), 0,
                              s, a)
             : launch_checked("k_cl_scatter<global>", k_cl_scatter<false, kMaxDigits>, dim3(p.grid), dim3(kScWG), 0, s, a);
@@ -731,7 +932,9 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
         b.sub = sub;
         b.shift = sh1 - p.b2;
         b.nd = p.nb2;
-        e = p.nb2 <= kSmallDigits
+        e = (ZK_CL_WC && p.nb2 <= kWcDigits)
+                ? launch_checked("k_cl_scatter_wc<local>", k_cl_scatter_wc<true>, dim3(p.nb1), dim3(kWcWG), 0, s, b)
+            : p.nb2 <= kSmallDigits
                 ? launch_checked("k_cl_scatter<local,256>", k_cl_scatter<true, kSmallDigits>, dim3(p.nb1), dim3(kScWG),
                                  0, s, b)
                 : launch_checked("k_cl_scatter<local>", k_cl_scatter<true, kMaxDigits>, dim3(p.nb1), dim3(kScWG), 0, s,
