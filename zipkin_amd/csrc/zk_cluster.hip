@@ -523,173 +523,6 @@ __global__ __launch_bounds__(kWcWG, kWcWG / 256) void k_cl_scatter_wc(ScatterArg
     carry_flush_all<0>(L, a.out, nd);
 }
 
-// ---- P1 / P2 as tile-interleaved passes (levels of <= 256 digits) --------------------------------
-// In k_cl_scatter(_wc) a workgroup owns a contiguous range per digit, so at any moment the 256
-// workgroups write every digit's output ~12 KB apart (one stream per workgroup), and the runs'
-// partial segments wait for the same workgroup's next chunk. Here the unit is the TILE (8192
-// records inside one segment: the whole batch for P1, a first-level bucket for P2): a histogram
-// pass counts every tile's digits, one exclusive scan of the (segment, digit, tile)-ordered counts
-// gives every (tile, digit) run its output position, and the scatter runs one workgroup per tile in
-// tile order. Tiles in flight at the same time are neighbours, so their runs of a digit are
-// adjacent in the output: the writes of concurrently running workgroups fill the same lines and
-// DRAM pages (contiguous per-chunk writes ran the pass in 2.0 ms against 3.0,
-// profiles/r03/ab_cluster_writes.txt). Counts: nd x tiles u32 (n / 32 bytes at 256 digits).
-#ifndef ZK_CL_TILES
-#define ZK_CL_TILES 1  // 0: the per-workgroup-range scatter for every level
-#endif
-constexpr int kTlWG = 1024;
-constexpr int kTlU = 8;
-constexpr uint32_t kTile = kTlWG * kTlU;  // records per tile
-constexpr int kThWG = 256;                // tile histogram workgroup
-constexpr uint32_t kTlDigits = 256;
-
-struct TileArgs {
-    SpanColsDev in;              // in.n = records of the whole batch
-    SpanColsMut out;
-    const uint32_t* seg;         // nseg + 1 segment bounds
-    const uint32_t* tiles_before;  // nseg + 1: tiles of the segments before segment s
-    uint32_t nseg;
-    uint32_t shift, nd;          // digit = (hash >> shift) & (nd - 1)
-    uint32_t* hist;              // counts of (segment s, digit d, tile j) at nd * tiles_before[s] + d * T_s + j
-    const uint32_t* offs;        // their exclusive scan (the output position of every tile's run of a digit)
-};
-
-// tile k -> its segment s (the last with tiles_before[s] <= k), tile j inside it, and its records
-__device__ __forceinline__ bool tile_of(const TileArgs& a, uint32_t k, uint32_t* s, uint32_t* j, uint32_t* ts,
-                                        uint64_t* lo, uint64_t* hi) {
-    if (k >= a.tiles_before[a.nseg]) return false;
-    uint32_t l = 0, r = a.nseg;  // tiles_before[l] <= k < tiles_before[r]
-    while (r - l > 1) {
-        const uint32_t m = (l + r) >> 1;
-        if (a.tiles_before[m] <= k)
-            l = m;
-        else
-            r = m;
-    }
-    *s = l;
-    *j = k - a.tiles_before[l];
-    *ts = a.tiles_before[l + 1] - a.tiles_before[l];
-    *lo = (uint64_t)a.seg[l] + (uint64_t)*j * kTile;
-    const uint64_t e = a.seg[l + 1];
-    *hi = *lo + kTile < e ? *lo + kTile : e;
-    return true;
-}
-
-// tiles per segment (one workgroup, nseg <= 1024)
-__global__ __launch_bounds__(1024) void k_cl_tiles(const uint32_t* __restrict__ seg, uint32_t nseg,
-                                                   uint32_t* __restrict__ tiles_before) {
-    __shared__ uint32_t s_tmp[32];
-    const uint32_t t = threadIdx.x;
-    const uint32_t v = t < nseg ? (seg[t + 1] - seg[t] + kTile - 1) / kTile : 0u;
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan<1024 / 64>(v, s_tmp, &tot);
-    if (t < nseg) tiles_before[t] = ex;
-    if (t == 0) tiles_before[nseg] = tot;
-}
-
-// P1's single segment: the whole batch
-__global__ void k_cl_seg1(uint32_t n, uint32_t* __restrict__ seg, uint32_t* __restrict__ tiles_before) {
-    if (threadIdx.x == 0) {
-        seg[0] = 0u;
-        seg[1] = n;
-        tiles_before[0] = 0u;
-        tiles_before[1] = (uint32_t)(((uint64_t)n + kTile - 1) / kTile);
-    }
-}
-
-__global__ __launch_bounds__(kThWG) void k_cl_thist(TileArgs a) {
-    __shared__ uint32_t h[kTlDigits];
-    uint32_t s, j, ts;
-    uint64_t lo, hi;
-    if (!tile_of(a, blockIdx.x, &s, &j, &ts, &lo, &hi)) return;
-    const uint32_t mask = a.nd - 1;
-    for (uint32_t d = threadIdx.x; d < a.nd; d += kThWG) h[d] = 0u;
-    __syncthreads();
-    constexpr int U = kTile / kThWG;
-    uint64_t v[U];
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-        const uint64_t i = lo + threadIdx.x + (uint64_t)k * kThWG;
-        v[k] = a.in.trace_id[i < hi ? i : lo];
-    }
-#pragma unroll
-    for (int k = 0; k < U; ++k)
-        if (lo + threadIdx.x + (uint64_t)k * kThWG < hi) atomicAdd(&h[digit_of(part_hash(v[k]), a.shift, mask)], 1u);
-    __syncthreads();
-    uint32_t* out = a.hist + (uint64_t)a.nd * a.tiles_before[s] + j;
-    for (uint32_t d = threadIdx.x; d < a.nd; d += kThWG) out[(uint64_t)d * ts] = h[d];
-}
-
-// sub-bucket bounds: out[s * nd + d] = the output position of segment s's first tile's run of
-// digit d (an empty segment's entries fall on the next segment's start), out[nseg * nd] = n
-__global__ void k_cl_tbounds(TileArgs a, uint64_t n, uint32_t* __restrict__ out) {
-    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t m = (uint64_t)a.nseg * a.nd;
-    if (q < m) {
-        const uint32_t s = (uint32_t)(q / a.nd), d = (uint32_t)(q % a.nd);
-        const uint32_t ts = a.tiles_before[s + 1] - a.tiles_before[s];
-        out[q] = a.offs[(uint64_t)a.nd * a.tiles_before[s] + (uint64_t)d * ts];
-    }
-    if (q == m) out[m] = (uint32_t)n;
-}
-
-__global__ __launch_bounds__(kTlWG, kTlWG / 256) void k_cl_tscatter(TileArgs a) {
-    __shared__ uint32_t s_cur[kTlDigits];  // output position of each digit's run
-    __shared__ uint32_t s_cnt[kTlDigits];  // records of the tile per digit
-    __shared__ uint32_t s_off[kTlDigits];  // exclusive offsets of the digits inside the sorted tile
-    __shared__ uint8_t s_dig[kTile];       // digit of the sorted tile's record i
-    __shared__ __align__(16) uint64_t s_stage[kTile];
-    __shared__ uint32_t s_tmp[32];
-    uint32_t s, j, ts;
-    uint64_t lo, hi;
-    if (!tile_of(a, blockIdx.x, &s, &j, &ts, &lo, &hi)) return;
-    const int t = threadIdx.x;
-    const uint32_t nd = a.nd, mask = nd - 1;
-    const uint32_t cnt = (uint32_t)(hi - lo);
-    {
-        const uint32_t* o = a.offs + (uint64_t)nd * a.tiles_before[s] + j;
-        for (uint32_t d = t; d < nd; d += kTlWG) {
-            s_cur[d] = o[(uint64_t)d * ts];
-            s_cnt[d] = 0u;
-        }
-    }
-    // 1. digits and ranks (LDS atomic counting sort: the order inside a digit is free)
-    uint32_t dg[kTlU], rank[kTlU];
-    uint64_t v[kTlU];
-#pragma unroll
-    for (int k = 0; k < kTlU; ++k) {
-        const uint32_t i = t + k * kTlWG;
-        v[k] = a.in.trace_id[lo + (i < cnt ? i : 0)];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kTlU; ++k) {
-        dg[k] = digit_of(part_hash(v[k]), a.shift, mask);
-        rank[k] = (t + k * kTlWG < cnt) ? atomicAdd(&s_cnt[dg[k]], 1u) : 0u;
-    }
-    __syncthreads();
-    // 2. digit offsets inside the tile
-    scan_digits<kTlWG, kTlDigits>(s_cnt, nd, 0u, s_off, s_tmp);
-    __syncthreads();
-    // 3. sorted position of each loaded record; digit of each sorted slot
-    uint32_t pos[kTlU], dest[kTlU];
-#pragma unroll
-    for (int k = 0; k < kTlU; ++k) {
-        pos[k] = s_off[dg[k]] + rank[k];
-        if (t + k * kTlWG < cnt) s_dig[pos[k]] = (uint8_t)dg[k];
-    }
-    __syncthreads();
-    // 4. output position of each sorted slot this thread writes
-#pragma unroll
-    for (int k = 0; k < kTlU; ++k) {
-        const uint32_t i = t + k * kTlWG;
-        const uint32_t d = i < cnt ? s_dig[i] : 0u;
-        dest[k] = i < cnt ? s_cur[d] + (i - s_off[d]) : 0u;
-    }
-    // 5. the columns through the LDS stage (the traceIds are in registers already)
-    move_columns<kTlU, kTlWG, 0>(a.in, a.out, lo, cnt, pos, dest, s_stage, v);
-}
-
 // ---- P3: trace runs inside each sub-bucket --------------------------------------------------------
 constexpr int kTrWG = 512;
 #ifndef ZK_CL_TR_SLOTS
@@ -1020,18 +853,10 @@ ClusterPlan cluster_plan(uint64_t n, uint32_t cus) {
     return p;
 }
 
-// the tile path (both levels <= 256 digits) or the per-workgroup-range scatter
-bool tile_path(const ClusterPlan& p) { return ZK_CL_TILES && p.nb1 <= kTlDigits && p.nb2 <= kTlDigits; }
-uint64_t tile_hist_words(const ClusterPlan& p) {
-    const uint64_t tmax = (p.n + kTile - 1) / kTile + p.nb1 + 1;
-    return (uint64_t)kTlDigits * tmax + 1;
-}
-uint64_t range_hist_words(const ClusterPlan& p) { return (uint64_t)p.nb1 * p.grid; }
-
 uint64_t cluster_scratch_bytes(const ClusterPlan& p) {
-    const uint64_t m = tile_path(p) ? tile_hist_words(p) : range_hist_words(p);
+    const uint64_t m = (uint64_t)p.nb1 * p.grid;
     return 2 * align256(m * 4) + align256(((uint64_t)p.nb1 + 1) * 4) + align256(((uint64_t)p.nb1 * p.nb2 + 1) * 4) +
-           256 + 3 * align256(((uint64_t)p.nb1 + 2) * 4) + align256(scan_bytes(m));
+           256 + align256(scan_bytes(m));
 }
 
 hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const SpanColsMut& A, const SpanColsMut& B,
@@ -1039,13 +864,14 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
     const uint64_t n = in.n;
     *result = 0;
     if (n == 0) return hipSuccess;
-    const uint64_t m = tile_path(p) ? tile_hist_words(p) : range_hist_words(p);
+    const uint64_t m = (uint64_t)p.nb1 * p.grid;
     uint8_t* sp = (uint8_t*)scratch;
     uint32_t* hist = (uint32_t*)sp;
     uint32_t* offs = (uint32_t*)(sp + align256(m * 4));
     uint32_t* bucket = (uint32_t*)(sp + 2 * align256(m * 4));
     uint32_t* sub = (uint32_t*)((uint8_t*)bucket + align256(((uint64_t)p.nb1 + 1) * 4));
     unsigned int* next = (unsigned int*)((uint8_t*)sub + align256(((uint64_t)p.nb1 * p.nb2 + 1) * 4));
+    void* temp = (uint8_t*)next + 256;
     hipError_t e = hipMemsetAsync(next, 0, 4, s);
     if (e != hipSuccess) return e;
     auto dev = [n](const SpanColsMut& c) {
@@ -1064,127 +890,61 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
         *result = 0;
         return launch_checked("k_cl_traces", k_cl_traces, dim3(1), dim3(kTrWG), 0, s, ta);
     }
+    // P0 + scan + first-level bucket bounds
     const uint32_t sh1 = 64 - p.b1;
-    uint32_t* seg1 = (uint32_t*)((uint8_t*)next + 256);
-    uint32_t* tb1 = (uint32_t*)((uint8_t*)seg1 + align256(((uint64_t)p.nb1 + 2) * 4));
-    uint32_t* tb2 = (uint32_t*)((uint8_t*)tb1 + align256(((uint64_t)p.nb1 + 2) * 4));
-    void* temp = (uint8_t*)tb2 + align256(((uint64_t)p.nb1 + 2) * 4);
-    if (tile_path(p)) {
-        // P1: tile histograms, one scan, bucket bounds, tile scatter in -> A
-        const uint64_t hw = tile_hist_words(p);
-        size_t temp_bytes = scan_bytes(hw);
-        const uint32_t t1 = (uint32_t)((n + kTile - 1) / kTile);
-        TileArgs ta1{};
-        ta1.in = in;
-        ta1.out = A;
-        ta1.seg = seg1;
-        ta1.tiles_before = tb1;
-        ta1.nseg = 1;
-        ta1.shift = sh1;
-        ta1.nd = p.nb1;
-        ta1.hist = hist;
-        ta1.offs = offs;
-        e = launch_checked("k_cl_seg1", k_cl_seg1, dim3(1), dim3(64), 0, s, (uint32_t)n, seg1, tb1);
-        if (e == hipSuccess) e = hipMemsetAsync(hist + (uint64_t)p.nb1 * t1, 0, 4, s);
-        if (e == hipSuccess) e = launch_checked("k_cl_thist<1>", k_cl_thist, dim3(t1), dim3(kThWG), 0, s, ta1);
-        if (e == hipSuccess)
-            e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, hist, offs, (int)((uint64_t)p.nb1 * t1 + 1), s);
-        if (e == hipSuccess)
-            e = launch_checked("k_cl_tbounds<1>", k_cl_tbounds, dim3((p.nb1 + 256) / 256), dim3(256), 0, s, ta1, n, bucket);
-        if (e == hipSuccess) e = launch_checked("k_cl_tscatter<1>", k_cl_tscatter, dim3(t1), dim3(kTlWG), 0, s, ta1);
+    e = launch_checked("k_cl_hist", k_cl_hist, dim3(p.grid), dim3(kHistWG), (size_t)p.nb1 * 4, s, in.trace_id, n, p.per,
+                       sh1, p.nb1, p.grid, hist);
+    if (e != hipSuccess) return e;
+    size_t temp_bytes = scan_bytes(m);
+    e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, hist, offs, (int)m, s);
+    if (e != hipSuccess) return e;
+    e = launch_checked("k_cl_bounds", k_cl_bounds, dim3((p.nb1 + 256) / 256), dim3(256), 0, s, offs, p.nb1, p.grid, n,
+                       bucket);
+    if (e != hipSuccess) return e;
+    // P1: in -> A (first-level buckets)
+    ScatterArgs a{};
+    a.in = in;
+    a.out = A;
+    a.per = p.per;
+    a.grid = p.grid;
+    a.offs = offs;
+    a.shift = sh1;
+    a.nd = p.nb1;
+    e = (ZK_CL_WC && p.nb1 <= kWcDigits)
+            ? launch_checked("k_cl_scatter_wc<global>", k_cl_scatter_wc<false>, dim3(p.grid), dim3(kWcWG), 0, s, a)
+        : p.nb1 <= kSmallDigits
+            ? launch_checked("k_cl_scatter<global,256>", k_cl_scatter<false, kSmallDigits>, dim3(p.grid), dim3(kScWG), 0,
+                             s, a)
+            : launch_checked("k_cl_scatter<global>", k_cl_scatter<false, kMaxDigits>, dim3(p.grid), dim3(kScWG), 0, s, a);
+    if (e != hipSuccess) return e;
+    if (!p.b2) {  // P3: A -> B
+        ta.in = dev(A);
+        ta.out = B;
+        ta.sub = bucket;
+        ta.nsub = p.nb1;
+        *result = 1;
+    } else {  // P2: A -> B (sub-buckets), P3: B -> A
+        ScatterArgs b{};
+        b.in = dev(A);
+        b.out = B;
+        b.bucket = bucket;
+        b.nbuckets = p.nb1;
+        b.sub = sub;
+        b.shift = sh1 - p.b2;
+        b.nd = p.nb2;
+        e = (ZK_CL_WC && p.nb2 <= kWcDigits)
+                ? launch_checked("k_cl_scatter_wc<local>", k_cl_scatter_wc<true>, dim3(p.nb1), dim3(kWcWG), 0, s, b)
+            : p.nb2 <= kSmallDigits
+                ? launch_checked("k_cl_scatter<local,256>", k_cl_scatter<true, kSmallDigits>, dim3(p.nb1), dim3(kScWG),
+                                 0, s, b)
+                : launch_checked("k_cl_scatter<local>", k_cl_scatter<true, kMaxDigits>, dim3(p.nb1), dim3(kScWG), 0, s,
+                                 b);
         if (e != hipSuccess) return e;
-        if (!p.b2) {  // P3: A -> B
-            ta.in = dev(A);
-            ta.out = B;
-            ta.sub = bucket;
-            ta.nsub = p.nb1;
-            *result = 1;
-        } else {
-            // P2: the same over the first-level buckets (segments), A -> B; the bounds are the sub-buckets
-            const uint32_t t2 = (uint32_t)((n + kTile - 1) / kTile + p.nb1);
-            TileArgs ta2{};
-            ta2.in = dev(A);
-            ta2.out = B;
-            ta2.seg = bucket;
-            ta2.tiles_before = tb2;
-            ta2.nseg = p.nb1;
-            ta2.shift = sh1 - p.b2;
-            ta2.nd = p.nb2;
-            ta2.hist = hist;
-            ta2.offs = offs;
-            e = launch_checked("k_cl_tiles", k_cl_tiles, dim3(1), dim3(1024), 0, s, (const uint32_t*)bucket, p.nb1, tb2);
-            if (e == hipSuccess) e = hipMemsetAsync(hist, 0, hw * 4, s);
-            if (e == hipSuccess) e = launch_checked("k_cl_thist<2>", k_cl_thist, dim3(t2), dim3(kThWG), 0, s, ta2);
-            if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, hist, offs, (int)hw, s);
-            if (e == hipSuccess) {
-                const uint64_t m2 = (uint64_t)p.nb1 * p.nb2 + 1;
-                e = launch_checked("k_cl_tbounds<2>", k_cl_tbounds, dim3((unsigned)((m2 + 255) / 256)), dim3(256), 0, s,
-                                   ta2, n, sub);
-            }
-            if (e == hipSuccess) e = launch_checked("k_cl_tscatter<2>", k_cl_tscatter, dim3(t2), dim3(kTlWG), 0, s, ta2);
-            if (e != hipSuccess) return e;
-            ta.in = dev(B);
-            ta.out = A;
-            ta.sub = sub;
-            ta.nsub = p.nb1 * p.nb2;
-            *result = 0;
-        }
-    } else {
-        // P0 + scan + first-level bucket bounds
-        e = launch_checked("k_cl_hist", k_cl_hist, dim3(p.grid), dim3(kHistWG), (size_t)p.nb1 * 4, s, in.trace_id, n, p.per,
-                           sh1, p.nb1, p.grid, hist);
-        if (e != hipSuccess) return e;
-        size_t temp_bytes = scan_bytes(m);
-        e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, hist, offs, (int)m, s);
-        if (e != hipSuccess) return e;
-        e = launch_checked("k_cl_bounds", k_cl_bounds, dim3((p.nb1 + 256) / 256), dim3(256), 0, s, offs, p.nb1, p.grid, n,
-                           bucket);
-        if (e != hipSuccess) return e;
-        // P1: in -> A (first-level buckets)
-        ScatterArgs a{};
-        a.in = in;
-        a.out = A;
-        a.per = p.per;
-        a.grid = p.grid;
-        a.offs = offs;
-        a.shift = sh1;
-        a.nd = p.nb1;
-        e = (ZK_CL_WC && p.nb1 <= kWcDigits)
-                ? launch_checked("k_cl_scatter_wc<global>", k_cl_scatter_wc<false>, dim3(p.grid), dim3(kWcWG), 0, s, a)
-            : p.nb1 <= kSmallDigits
-                ? launch_checked("k_cl_scatter<global,256>", k_cl_scatter<false, kSmallDigits>, dim3(p.grid), dim3(kScWG), 0,
-                                 s, a)
-                : launch_checked("k_cl_scatter<global>", k_cl_scatter<false, kMaxDigits>, dim3(p.grid), dim3(kScWG), 0, s, a);
-        if (e != hipSuccess) return e;
-        if (!p.b2) {  // P3: A -> B
-            ta.in = dev(A);
-            ta.out = B;
-            ta.sub = bucket;
-            ta.nsub = p.nb1;
-            *result = 1;
-        } else {  // P2: A -> B (sub-buckets), P3: B -> A
-            ScatterArgs b{};
-            b.in = dev(A);
-            b.out = B;
-            b.bucket = bucket;
-            b.nbuckets = p.nb1;
-            b.sub = sub;
-            b.shift = sh1 - p.b2;
-            b.nd = p.nb2;
-            e = (ZK_CL_WC && p.nb2 <= kWcDigits)
-                    ? launch_checked("k_cl_scatter_wc<local>", k_cl_scatter_wc<true>, dim3(p.nb1), dim3(kWcWG), 0, s, b)
-                : p.nb2 <= kSmallDigits
-                    ? launch_checked("k_cl_scatter<local,256>", k_cl_scatter<true, kSmallDigits>, dim3(p.nb1), dim3(kScWG),
-                                     0, s, b)
-                    : launch_checked("k_cl_scatter<local>", k_cl_scatter<true, kMaxDigits>, dim3(p.nb1), dim3(kScWG), 0, s,
-                                     b);
-            if (e != hipSuccess) return e;
-            ta.in = dev(B);
-            ta.out = A;
-            ta.sub = sub;
-            ta.nsub = p.nb1 * p.nb2;
-            *result = 0;
-        }
+        ta.in = dev(B);
+        ta.out = A;
+        ta.sub = sub;
+        ta.nsub = p.nb1 * p.nb2;
+        *result = 0;
     }
     const uint32_t g3 = ta.nsub < ZK_CL_TR_GRID * cus ? ta.nsub : ZK_CL_TR_GRID * cus;
     return launch_checked("k_cl_traces", k_cl_traces, dim3(g3), dim3(kTrWG), 0, s, ta);
