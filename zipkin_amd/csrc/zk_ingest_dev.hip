@@ -57,36 +57,74 @@ __device__ __forceinline__ uint64_t d_hash(const uint8_t* s, uint32_t n) {  // =
     return h ? h : 1ull;
 }
 
-// unaligned big-endian loads (one 2/4/8-byte access: gfx950 reads unaligned LDS and global words)
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// Multi-byte reads at any byte offset. Global / generic pointers: one unaligned access. LDS: an
+// access off its natural alignment is replayed on gfx950 (cdna_hip_programming.md Guideline 17;
+// SQ_LDS_UNALIGNED_STALL was 23 % of the LDS decoder's cycles, and splitting the 8-byte reads into
+// unaligned 4-byte ones made it worse, profiles/r03/ingest_pmc.txt), so LDS bytes are read as
+// ALIGNED dwords and shifted into place with v_alignbyte_b32.
+template <class P>
+__device__ __forceinline__ uint32_t ld_u32(P p) {
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);
+    return v;
+}
+__device__ __forceinline__ uint32_t ld_u32(const lds_u8* p) {
+    const uint32_t a = (uint32_t)(uintptr_t)p;
+    const lds_u32* w = (const lds_u32*)(uintptr_t)(a & ~3u);
+    return __builtin_amdgcn_alignbyte(w[1], w[0], a & 3u);
+}
+template <class P>
+__device__ __forceinline__ uint64_t ld_u64(P p) {
+    uint64_t v;
+    __builtin_memcpy(&v, p, 8);
+    return v;
+}
+__device__ __forceinline__ uint64_t ld_u64(const lds_u8* p) {
+    const uint32_t a = (uint32_t)(uintptr_t)p;
+    const lds_u32* w = (const lds_u32*)(uintptr_t)(a & ~3u);
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], s = a & 3u;
+    return ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, s) << 32) | __builtin_amdgcn_alignbyte(w1, w0, s);
+}
+__device__ __forceinline__ uint32_t ld_u32(lds_u8* p) { return ld_u32((const lds_u8*)p); }
+__device__ __forceinline__ uint64_t ld_u64(lds_u8* p) { return ld_u64((const lds_u8*)p); }
 template <class P>
 __device__ __forceinline__ uint16_t ld_be16(P p) {
-    uint16_t v;
-    __builtin_memcpy(&v, p, 2);
-    return __builtin_bswap16(v);
+    return __builtin_bswap16((uint16_t)ld_u32(p));
 }
 template <class P>
 __device__ __forceinline__ uint32_t ld_be32(P p) {
-    uint32_t v;
-    __builtin_memcpy(&v, p, 4);
-    return __builtin_bswap32(v);
+    return __builtin_bswap32(ld_u32(p));
 }
 template <class P>
 __device__ __forceinline__ uint64_t ld_be64(P p) {
-    uint64_t v;
-    __builtin_memcpy(&v, p, 8);
-    return __builtin_bswap64(v);
+    return __builtin_bswap64(ld_u64(p));
 }
 // copy 8 / 4 bytes through a register (source read before the destination is written)
+#ifndef ZK_ING_BYTEWR
+#define ZK_ING_BYTEWR 1  // LDS destinations written byte by byte (never off alignment): 14.00 vs 14.03-14.21 ms
+#endif
 template <class D, class S>
 __device__ __forceinline__ void cp8(D d, S s) {
-    uint64_t v;
-    __builtin_memcpy(&v, s, 8);
+    const uint64_t v = ld_u64(s);
     __builtin_memcpy(d, &v, 8);
+}
+template <class S>
+__device__ __forceinline__ void cp8(lds_u8* d, S s) {
+    const uint64_t v = ld_u64(s);
+    if (ZK_ING_BYTEWR) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d[k] = (uint8_t)(v >> (8 * k));
+    } else {
+        typedef __attribute__((address_space(3), aligned(1))) uint64_t lds_u64u;
+        *(lds_u64u*)d = v;
+    }
 }
 template <class D, class S>
 __device__ __forceinline__ void cp4(D d, S s) {
-    uint32_t v;
-    __builtin_memcpy(&v, s, 4);
+    const uint32_t v = ld_u32(s);
     __builtin_memcpy(d, &v, 4);
 }
 
@@ -230,7 +268,6 @@ struct DRdT {
 };
 
 using DRd = DRdT<const uint8_t*>;
-typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
 // The generic skip out of line (nested containers are rare in stored spans): keeps its stack and
 // switch out of the decoders' register budget. DRd travels by value, so nothing goes to scratch.
@@ -293,6 +330,7 @@ __device__ __forceinline__ void backref_copy(P out, uint64_t o, uint64_t off, ui
     } else if (off >= 4) {
         for (; k + 4 <= l; k += 4) cp4(out + o + k, out + o - off + k);
     }
+    #pragma clang loop vectorize(disable)  // (a vectorised byte loop reads LDS with unaligned ds_read_b128)
     for (; k < l; ++k) out[o + k] = out[o - off + k];
 }
 
@@ -331,6 +369,7 @@ __device__ __forceinline__ bool snappy_block(const uint8_t* in, uint64_t n, uint
             if (i + l > n || o + l > len) return false;
             uint64_t k = 0;
             for (; k + 8 <= l; k += 8) cp8(out + o + k, in + i + k);
+            #pragma clang loop vectorize(disable)  // (a vectorised byte loop reads LDS with unaligned ds_read_b128)
             for (; k < l; ++k) out[o + k] = in[i + k];
             i += l;
             o += l;
@@ -644,9 +683,7 @@ __device__ __forceinline__ int parse_record_flat(const IngArgs& a, uint64_t i, c
     uint32_t vl = 0, vc = 0, hn = 0, hl = 0;
     uint32_t srv = 0, srv_len = 0, cli = 0, cli_len = 0;  // first server / client core annotation with a host
     while (!(fl & F_DONE)) {
-        uint64_t lo, hi;
-        __builtin_memcpy(&lo, base + p, 8);
-        __builtin_memcpy(&hi, base + p + 8, 8);
+        const uint64_t lo = ld_u64(base + p), hi = ld_u64(base + p + 8);  // aligned dword reads
         const uint32_t kind = mt & 3u, sem = (mt >> 2) & 7u;
         const uint32_t avail = e - p;
         const bool in_struct = kind == kStruct;
@@ -888,6 +925,7 @@ __device__ __forceinline__ bool snappy_inplace(lds_u8* out, uint64_t D, uint64_t
             }
             uint64_t k = 0;
             for (; k + 8 <= l; k += 8) cp8(out + o + k, in + i + k);
+            #pragma clang loop vectorize(disable)  // (a vectorised byte loop reads LDS with unaligned ds_read_b128)
             for (; k < l; ++k) out[o + k] = in[i + k];
             i += l;
             o += l;
@@ -1047,6 +1085,7 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                                 const uint64_t off = nmo - p0;
                                 if (a.snappy) {
                                     uint8_t* gd = a.scratch + a.raw_off[i] + off;  // copy out to the scratch
+#pragma clang loop vectorize(disable)
                                     for (uint32_t q = 0; q < nl; ++q) gd[q] = nm[q];
                                     nm = gd;
                                 } else {
