@@ -519,8 +519,8 @@ def _thrift_fragments(cols, S):
     def st(b):
         return struct.pack(">i", len(b)) + b
 
-    def ep(name):
-        return fh(12, 3) + fh(8, 1) + struct.pack(">i", 0x7F000001) + fh(6, 2) + struct.pack(">h", 9410) + fh(11, 3) + st(name) + b"\0"
+    def ep(name, fid=3):  # Annotation.host is field 3, BinaryAnnotation.host field 4
+        return fh(12, fid) + fh(8, 1) + struct.pack(">i", 0x7F000001) + fh(6, 2) + struct.pack(">h", 9410) + fh(11, 3) + st(name) + b"\0"
 
     def ann(ts, v, name):
         return fh(10, 1) + struct.pack(">q", ts) + fh(11, 2) + st(v) + (ep(name) if name else b"") + b"\0"
@@ -538,7 +538,7 @@ def _thrift_fragments(cols, S):
             body += fh(10, 5) + struct.pack(">Q", int(cols.parent_id[i]))
         body += fh(15, 6) + struct.pack(">bi", 12, len(anns)) + b"".join(anns)
         body += fh(15, 8) + struct.pack(">bi", 12, 1) + fh(11, 1) + st(b"http.uri") + fh(11, 2) + st(b"/api/v1")
-        body += fh(8, 3) + struct.pack(">i", 6) + ep(name) + b"\0"
+        body += fh(8, 3) + struct.pack(">i", 6) + ep(name, 4) + b"\0"
         body += fh(2, 9) + b"\0" + b"\0"
         out.append(snappy.compress(body, asbytes=True))
     return out

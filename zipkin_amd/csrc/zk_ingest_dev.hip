@@ -817,6 +817,224 @@ __device__ __forceinline__ int parse_record_flat(const IngArgs& a, uint64_t i, c
     return (srv_set || cli_set) ? 1 : 0;
 }
 
+// ---- fast path: the canonical layout of a stored zipkin Span (LDS decoder) ----------------------
+// Scrooge writes a Span's fields in id order (zipkinCore.thrift:27-58): 1 trace_id, 3 name, 4 id,
+// 5 parent_id (optional), 6 annotations {1 timestamp, 2 value, 3 host (optional) {1 ipv4, 2 port,
+// 3 service_name}}, 8 binary_annotations (optional) {1 key, 2 value, 3 annotation_type, 4 host
+// (optional)}, 9 debug (optional). The branchy walk reads that as ~47 dependent tokens (a header
+// byte, then the value, then the next header); here each group of fixed-layout fields is ONE
+// window of aligned LDS dwords, checked byte for byte, so a span costs ~13 dependent steps (2 per
+// annotation). Anything else -- another field, another order, a missing endpoint field, a length
+// past the end -- returns -3 before anything is written, and the lane runs the generic walk: the
+// fast path accepts only byte strings on which parse_record yields exactly the same record.
+#ifndef ZK_ING_FAST
+#define ZK_ING_FAST 1  // 0: every span through the generic walk (A/B)
+#endif
+template <int W>
+struct LWin {  // W + 1 aligned dwords from the dword holding byte x; byte x + j is at compile-time j
+    uint32_t d[W + 1];
+    uint32_t s;
+    __device__ __forceinline__ void load(const lds_u8* base, uint32_t x) {
+        const uint32_t adr = (uint32_t)(uintptr_t)(base + x);
+        const lds_u32* w = (const lds_u32*)(uintptr_t)(adr & ~3u);
+        s = adr & 3u;
+#pragma unroll
+        for (int k = 0; k <= W; ++k) d[k] = w[k];
+    }
+    template <int K>
+    __device__ __forceinline__ uint32_t dw() const {  // bytes x + 4K .. x + 4K + 3
+        static_assert(K + 1 <= W, "window too short");
+        return __builtin_amdgcn_alignbyte(d[K + 1], d[K], s);
+    }
+    template <int J>
+    __device__ __forceinline__ uint32_t raw32() const {  // bytes x + J .. x + J + 3, little-endian
+        if constexpr ((J & 3) == 0)
+            return dw<(J >> 2)>();
+        else
+            return (dw<(J >> 2)>() >> (8 * (J & 3))) | (dw<(J >> 2) + 1>() << (32 - 8 * (J & 3)));
+    }
+    template <int J>
+    __device__ __forceinline__ uint32_t u8() const { return raw32<J>() & 0xFFu; }
+    template <int J>
+    __device__ __forceinline__ uint32_t be32() const { return __builtin_bswap32(raw32<J>()); }
+    template <int J>
+    __device__ __forceinline__ uint64_t be64() const { return ((uint64_t)be32<J>() << 32) | be32<J + 4>(); }
+    template <int J>
+    __device__ __forceinline__ uint32_t hdr() const { return be32<J>() >> 8; }  // type << 16 | field id
+};
+constexpr uint32_t fh(uint32_t type, uint32_t id) { return (type << 16) | id; }
+
+// a length-prefixed value of `len` bytes after `at` header bytes fits the remaining `avail`
+__device__ __forceinline__ bool fits(uint32_t avail, uint32_t at, int32_t len) {
+    return len >= 0 && (uint64_t)avail >= (uint64_t)at + (uint32_t)len;
+}
+
+__device__ __forceinline__ int parse_record_fast(const IngArgs& a, uint64_t i, const lds_u8* base, uint32_t p0,
+                                                 uint32_t len, uint32_t* nm_off, uint32_t* nl_out) {
+    constexpr int kNo = -3;
+    const uint32_t e = p0 + len;
+    uint32_t p = p0;
+    // [0A 0001] trace_id [0B 0003] name
+    LWin<5> w1;
+    w1.load(base, p);
+    if (e - p < 18u || w1.hdr<0>() != fh(T_I64, 1) || w1.hdr<11>() != fh(T_STRING, 3)) return kNo;
+    const uint64_t trace = w1.be64<3>();
+    const int32_t nlen = (int32_t)w1.be32<14>();
+    if (!fits(e - p, 18u, nlen)) return kNo;
+    p += 18u + (uint32_t)nlen;
+    // [0A 0004] id, [0A 0005] parent_id (optional), [0F 0006] [0C] count
+    LWin<8> w2;
+    w2.load(base, p);
+    if (e - p < 11u || w2.hdr<0>() != fh(T_I64, 4)) return kNo;
+    const uint64_t id = w2.be64<3>();
+    const bool has_parent = w2.hdr<11>() == fh(T_I64, 5);
+    const uint64_t parent = w2.be64<14>();
+    const uint32_t lh = has_parent ? w2.hdr<22>() : w2.hdr<11>();
+    const uint32_t let = has_parent ? w2.u8<25>() : w2.u8<14>();
+    const int32_t na = (int32_t)(has_parent ? w2.be32<26>() : w2.be32<15>());
+    const uint32_t q2 = has_parent ? 30u : 19u;
+    if (e - p < q2 || lh != fh(T_LIST, 6) || let != T_STRUCT || na < 0) return kNo;
+    p += q2;
+    int64_t first = 0, last = 0;
+    uint32_t nann = 0, cnt = 0;
+    bool invalid = false, srv_set = false, cli_set = false;
+    uint32_t srv = 0, srv_len = 0, cli = 0, cli_len = 0;
+    for (int32_t k = 0; k < na; ++k) {
+        // [0A 0001] timestamp [0B 0002] value
+        LWin<6> c;
+        c.load(base, p);
+        if (e - p < 18u || c.hdr<0>() != fh(T_I64, 1) || c.hdr<11>() != fh(T_STRING, 2)) return kNo;
+        const int64_t ts = (int64_t)c.be64<3>();
+        const int32_t vl = (int32_t)c.be32<14>();
+        if (!fits(e - p, 18u, vl)) return kNo;
+        const uint32_t vc = c.raw32<18>() & 0xFFFFu;  // the value's first two bytes (used when vl == 2)
+        p += 18u + (uint32_t)vl;
+        // STOP, or [0C 0003] {[08 0001] ipv4 [06 0002] port [0B 0003] service_name} STOP STOP
+        LWin<6> h;
+        h.load(base, p);
+        if (e - p < 1u) return kNo;
+        bool host = false;
+        uint32_t hn = 0, hl = 0;
+        if (h.u8<0>() == T_STOP) {
+            p += 1u;
+        } else {
+            if (e - p < 22u || h.hdr<0>() != fh(T_STRUCT, 3) || h.hdr<3>() != fh(T_I32, 1) ||
+                h.hdr<10>() != fh(T_I16, 2) || h.hdr<15>() != fh(T_STRING, 3))
+                return kNo;
+            const int32_t L = (int32_t)h.be32<18>();
+            if (!fits(e - p, 24u, L)) return kNo;  // + the two STOPs
+            hn = p + 22u;
+            hl = (uint32_t)L;
+            host = true;
+            p += 22u + (uint32_t)L;
+            LWin<1> z;
+            z.load(base, p);
+            if ((z.raw32<0>() & 0xFFFFu) != 0u) return kNo;
+            p += 2u;
+        }
+        // read_annotation returned: thrift.scala:66-71, Span.scala:213-240 (as parse_record)
+        if (ts <= 0 || vl == 0) invalid = true;
+        if (nann == 0u || ts < first) first = ts;
+        if (nann == 0u || ts > last) last = ts;
+        ++nann;
+        const uint32_t c0 = vc & 0xFFu, c1 = vc >> 8;
+        if (vl == 2 && ((c0 == 'c' && (c1 == 's' || c1 == 'r')) || (c0 == 's' && (c1 == 'r' || c1 == 's')))) {
+            const uint32_t cc = c0 == 'c' ? (c1 == 's' ? 0u : 1u) : (c1 == 'r' ? 2u : 3u);
+            if (((cnt >> (2 * cc)) & 3u) < 2u) cnt += 1u << (2 * cc);
+            if (host && cc >= 2u && !srv_set) {
+                srv_set = true;
+                srv = hn;
+                srv_len = hl;
+            }
+            if (host && cc < 2u && !cli_set) {
+                cli_set = true;
+                cli = hn;
+                cli_len = hl;
+            }
+        }
+    }
+    // [0F 0008] [0C] count (optional)
+    LWin<3> d;
+    d.load(base, p);
+    int32_t nb = 0;
+    if (e - p >= 8u && d.hdr<0>() == fh(T_LIST, 8)) {
+        nb = (int32_t)d.be32<4>();
+        if (d.u8<3>() != T_STRUCT || nb < 0) return kNo;
+        p += 8u;
+    }
+    for (int32_t k = 0; k < nb; ++k) {
+        // [0B 0001] key [0B 0002] value [08 0003] annotation_type, then STOP or [0C 0004] endpoint STOP STOP
+        LWin<2> k1;
+        k1.load(base, p);
+        if (e - p < 7u || k1.hdr<0>() != fh(T_STRING, 1)) return kNo;
+        const int32_t kl = (int32_t)k1.be32<3>();
+        if (!fits(e - p, 7u, kl)) return kNo;
+        p += 7u + (uint32_t)kl;
+        LWin<2> k2;
+        k2.load(base, p);
+        if (e - p < 7u || k2.hdr<0>() != fh(T_STRING, 2)) return kNo;
+        const int32_t bl = (int32_t)k2.be32<3>();
+        if (!fits(e - p, 7u, bl)) return kNo;
+        p += 7u + (uint32_t)bl;
+        LWin<8> k3;
+        k3.load(base, p);
+        if (e - p < 8u || k3.hdr<0>() != fh(T_I32, 3)) return kNo;
+        if (k3.u8<7>() == T_STOP) {
+            p += 8u;
+        } else {
+            if (e - p < 29u || k3.hdr<7>() != fh(T_STRUCT, 4) || k3.hdr<10>() != fh(T_I32, 1) ||
+                k3.hdr<17>() != fh(T_I16, 2) || k3.hdr<22>() != fh(T_STRING, 3))
+                return kNo;
+            const int32_t L = (int32_t)k3.be32<25>();
+            if (!fits(e - p, 31u, L)) return kNo;
+            p += 29u + (uint32_t)L;
+            LWin<1> z;
+            z.load(base, p);
+            if ((z.raw32<0>() & 0xFFFFu) != 0u) return kNo;
+            p += 2u;
+        }
+    }
+    // [02 0009] debug (optional), then the Span's STOP
+    LWin<2> f;
+    f.load(base, p);
+    if (e - p < 1u) return kNo;
+    if (f.u8<0>() != T_STOP) {
+        if (e - p < 5u || f.hdr<0>() != fh(T_BOOL, 9) || f.u8<4>() != T_STOP) return kNo;
+    }
+    // the record (as parse_record: the name is present, so only the annotations can invalidate)
+    if (invalid) {
+        a.status[i] = kStInvalid;
+        return -1;
+    }
+    uint32_t fl = has_parent ? ZK_F_HAS_PARENT : 0u;
+    if (nann) fl |= ZK_F_HAS_ANNOTATIONS;
+    *nm_off = ~0u;
+    *nl_out = 0u;
+    if (srv_set) {
+        fl |= ZK_F_SVC_SERVER;
+        if (srv_len) {
+            *nm_off = srv;
+            *nl_out = srv_len;
+        }
+    } else if (cli_set) {
+        fl |= ZK_F_SVC_CLIENT;
+        if (cli_len) {
+            *nm_off = cli;
+            *nl_out = cli_len;
+        }
+    }
+    fl |= ((cnt & 3u) << ZK_F_CS_SHIFT) | (((cnt >> 2) & 3u) << ZK_F_CR_SHIFT) | (((cnt >> 4) & 3u) << ZK_F_SR_SHIFT) |
+          (((cnt >> 6) & 3u) << ZK_F_SS_SHIFT);
+    a.tid[i] = trace;
+    a.sid[i] = id;
+    a.pid[i] = has_parent ? parent : 0ull;
+    a.first[i] = nann ? first : 0;
+    a.last[i] = nann ? last : 0;
+    a.flags[i] = fl;
+    a.svc[i] = 0u;
+    return (srv_set || cli_set) ? 1 : 0;
+}
+
 __device__ __forceinline__ void publish_name(const IngArgs& a, uint64_t i, const uint8_t* nm, uint32_t nl) {
     a.svc_hash[i] = d_hash(nm, nl);
     a.name_ptr[i] = (uint64_t)(uintptr_t)nm;
@@ -1064,17 +1282,21 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                     const lds_u8* const lbase = (const lds_u8*)s_buf;
                     const uint32_t p0 = (uint32_t)(src - lbase);
                     uint32_t nmo, nl;
+                    int r = ZK_ING_FAST ? parse_record_fast(a, i, lbase, p0, (uint32_t)len, &nmo, &nl) : -3;
+                    if (r == -3) {  // not the canonical layout: the generic walk
 #if ZK_ING_FLAT
-                    int r = parse_record_flat(a, i, lbase, p0, (uint32_t)len, &nmo, &nl);
-                    if (r == -2) {
-                        a.status[i] = kStDefer;
-                        r = -1;
-                    }
+                        r = parse_record_flat(a, i, lbase, p0, (uint32_t)len, &nmo, &nl);
+                        if (r == -2) {
+                            a.status[i] = kStDefer;
+                            r = -1;
+                        }
 #else
-                    const uint8_t* gnm = nullptr;
-                    const int r = parse_record(a, i, src, len, &gnm, &nl);
-                    nmo = (r == 1 && gnm != (const uint8_t*)a.unknown) ? (uint32_t)(gnm - (const uint8_t*)lbase) : ~0u;
+                        const uint8_t* gnm = nullptr;
+                        r = parse_record(a, i, src, len, &gnm, &nl);
+                        nmo = (r == 1 && gnm != (const uint8_t*)a.unknown) ? (uint32_t)(gnm - (const uint8_t*)lbase)
+                                                                           : ~0u;
 #endif
+                    }
                     const bool unknown = nmo == ~0u;
                     const uint8_t* nm = unknown ? a.unknown : (const uint8_t*)(lbase + nmo);
                     if (unknown) nl = sizeof(kUnknown) - 1;
