@@ -1109,6 +1109,10 @@ constexpr uint32_t kLdsBudget = 20480;
 constexpr uint32_t kLdsBlock = 1024;
 constexpr uint32_t kLdsSlack = 80;  // region bytes beyond max(raw, compressed): in-place headroom + alignment
                                     // + the lane's bank skew
+#ifndef ZK_ING_UNIFORM
+#define ZK_ING_UNIFORM 1  // equal-size regions per round, placed for distinct banks (see the round setup)
+#endif
+constexpr uint32_t kLdsUniformCap = 640;  // largest region (bytes) of a uniform round
 #ifndef ZK_ING_SKEW
 #define ZK_ING_SKEW 1  // decompressed span starts 4 * (lane % 4) bytes into its region (see below)
 #endif
@@ -1236,18 +1240,42 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
             const uint64_t r = ((raw > clen ? raw : clen) + kLdsSlack + 15) & ~15ull;
             need = st == kStOk ? (r > kLdsBudget ? kLdsBudget + 1 : (uint32_t)r) : 0u;
         }
-        const uint32_t incl = wave_incl_scan(need);
-        // this round: the longest prefix of lanes that fits (at least lane 0, to make progress)
-        uint32_t k = (uint32_t)__popcll(__ballot(have && incl <= kLdsBudget));
-        if (k == 0) k = 1;  // lane 0 alone does not fit: deferred below
+        // Uniform layout (every region of the round has the size R of the largest, R / 16 odd, lane
+        // L at L * R with a skew of 4 * (L / 16) bytes): lanes parsing the same field offset then
+        // hit 64 different banks, where regions packed back to back at sizes that are multiples of
+        // 16 B put several lanes on one bank. Used while no region of the next 64 exceeds
+        // kLdsUniformCap; else regions are packed.
+        uint32_t mx = need;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t y = (uint32_t)__shfl_xor((int)mx, o);
+            mx = y > mx ? y : mx;
+        }
+        const bool uniform = ZK_ING_UNIFORM && mx <= kLdsUniformCap;
+        uint32_t R = need, R0, k;
+        bool fits;
+        if (uniform) {
+            R = mx < 16u ? 16u : mx;
+            if (((R >> 4) & 1u) == 0u) R += 16u;
+            k = kLdsBudget / R;
+            if (k > 64u) k = 64u;
+            R0 = lane * R;
+            fits = true;
+        } else {
+            const uint32_t incl = wave_incl_scan(need);
+            // this round: the longest prefix of lanes that fits (at least lane 0, to make progress)
+            k = (uint32_t)__popcll(__ballot(have && incl <= kLdsBudget));
+            if (k == 0) k = 1;  // lane 0 alone does not fit: deferred below
+            R0 = incl - need;
+            fits = incl <= kLdsBudget;
+        }
         ING_STAMP(0);
         if (lane < k && have) {
             a.keep[i] = 0u;
             a.svc_hash[i] = 0ull;
-            if (st == kStOk && incl > kLdsBudget) {
+            if (st == kStOk && !fits) {
                 a.status[i] = kStDefer;
             } else if (st == kStOk) {
-                const uint32_t R = need, R0 = incl - need;
                 const uint32_t mis = (uint32_t)((uintptr_t)(a.buf + b) & 15u);
                 // input at offset D of the region (D = mis mod 16): its aligned 16-B blocks cover
                 // [D - mis, D + clen + 15] inside [0, R) since R >= clen + kLdsSlack
@@ -1266,7 +1294,7 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                 // group; lanes parsing the same field at the same offset then collide. The
                 // decompressed span starts 4 * (lane % 4) bytes in, spreading the lanes over all 32.
                 lds_u8* const lreg = (lds_u8*)reg;
-                const uint32_t skew = ZK_ING_SKEW ? 4u * (lane & 3u) : 0u;
+                const uint32_t skew = ZK_ING_SKEW ? 4u * (uniform ? (lane >> 4) & 3u : lane & 3u) : 0u;
                 const lds_u8* src = lreg + D;
                 uint64_t len = clen;
                 bool ok = true, unsafe = false;
