@@ -523,6 +523,233 @@ __global__ __launch_bounds__(kWcWG, kWcWG / 256) void k_cl_scatter_wc(ScatterArg
     carry_flush_all<0>(L, a.out, nd);
 }
 
+// ---- P1 / P2 with streams shared per XCD (ZK_CL_XCD) ---------------------------------------------
+// In k_cl_scatter(_wc) every workgroup owns one output range per digit: 256 workgroups x 256
+// digits x 7 columns of write streams ~12 KB apart, and a run's partial tail line waits for the
+// same workgroup's next chunk. Here the input is cut into P <= 8 portions, and a digit's output
+// range is cut into P sub-ranges, one per portion; a chunk of portion p claims its runs at the
+// portion's shared cursors (one global atomic per digit of the chunk). Workgroups start on the
+// portion of their XCD (HW_REG_XCC_ID) and take chunks in order, so at any moment the ~32
+// workgroups of an XCD append to the same 256 x 7 streams: neighbouring runs are written through
+// the same L2, and the open lines of an XCD are 256 x 7 instead of 32 x 256 x 7. Placement only
+// changes speed: a workgroup whose portion is drained takes chunks of the others, and every
+// portion's cursors belong to the portion, not to an XCD.
+//   P1: portion p = the P0 ranges [p g / P, (p + 1) g / P); its cursors start at the scanned P0
+//       offsets of its first range.
+//   P2: portion p = the first-level buckets b = p, p + P, ...; a chunk lies inside one bucket and
+//       claims its runs at the bucket's sub-bucket cursors (the scanned (bucket, digit) histogram
+//       of P2h, which also gives the sub-bucket bounds).
+#ifndef ZK_CL_XCD
+#define ZK_CL_XCD 1  // 0: the per-workgroup-range scatter (k_cl_scatter_wc)
+#endif
+constexpr uint32_t kParts = 8;
+constexpr int kXsWG = 1024;
+constexpr int kXsU = 8;
+constexpr uint32_t kXsChunk = kXsWG * kXsU;
+
+struct XArgs {
+    SpanColsDev in;
+    SpanColsMut out;
+    uint32_t shift, nd;
+    uint32_t parts;                    // P
+    const uint32_t* part_tiles;        // P + 1: chunks of the portions before p
+    unsigned int* next;                // P chunk counters
+    unsigned int* cursor;              // global: [P][nd]; local: [nb1][nd] (absolute output positions)
+    // global: portion p = records [part_lo[p], part_lo[p + 1])
+    const uint32_t* part_lo;
+    // local: portion p's buckets b = p + P m; bucket_tiles[p * (nbp + 1) + m] = chunks of its first m buckets
+    const uint32_t* bucket;            // nb1 + 1 bucket bounds
+    const uint32_t* bucket_tiles;
+    uint32_t nb1, nbp;
+    uint32_t* hist;                    // P2h: [nb1][nd] counts
+};
+
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    return x;
+}
+
+// chunk j of portion p -> its records [lo, hi) and (local) its bucket
+template <bool LOCAL>
+__device__ __forceinline__ void xchunk(const XArgs& a, uint32_t p, uint32_t j, uint64_t* lo, uint64_t* hi,
+                                       uint32_t* b) {
+    if constexpr (!LOCAL) {
+        *b = 0;
+        *lo = (uint64_t)a.part_lo[p] + (uint64_t)j * kXsChunk;
+        const uint64_t e = a.part_lo[p + 1];
+        *hi = *lo + kXsChunk < e ? *lo + kXsChunk : e;
+    } else {
+        const uint32_t* bt = a.bucket_tiles + (uint64_t)p * (a.nbp + 1);
+        uint32_t l = 0, r = a.nbp;  // bt[l] <= j < bt[r]
+        while (r - l > 1) {
+            const uint32_t m = (l + r) >> 1;
+            if (bt[m] <= j)
+                l = m;
+            else
+                r = m;
+        }
+        const uint32_t bk = p + a.parts * l;
+        *b = bk;
+        *lo = (uint64_t)a.bucket[bk] + (uint64_t)(j - bt[l]) * kXsChunk;
+        const uint64_t e = a.bucket[bk + 1];
+        *hi = *lo + kXsChunk < e ? *lo + kXsChunk : e;
+    }
+}
+
+// P1 cursors: cursor[p][d] = offs[d * grid + first P0 range of p]; portion bounds and chunk counts
+__global__ void k_cl_xprep1(const uint32_t* __restrict__ offs, uint32_t nd, uint32_t grid, uint32_t parts,
+                            uint64_t per, uint64_t n, unsigned int* __restrict__ cursor, uint32_t* __restrict__ part_lo,
+                            uint32_t* __restrict__ part_tiles, unsigned int* __restrict__ next) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < parts * nd) {
+        const uint32_t p = q / nd, d = q % nd;
+        cursor[q] = offs[(uint64_t)d * grid + (uint64_t)p * grid / parts];
+    }
+    if (q == 0) {
+        uint32_t t = 0;
+        for (uint32_t p = 0; p <= parts; ++p) {
+            const uint64_t lo = (uint64_t)p * grid / parts * per;
+            part_lo[p] = (uint32_t)(lo < n ? lo : n);
+        }
+        for (uint32_t p = 0; p < parts; ++p) {
+            part_tiles[p] = t;
+            t += (part_lo[p + 1] - part_lo[p] + kXsChunk - 1) / kXsChunk;
+            next[p] = 0u;
+        }
+        part_tiles[parts] = t;
+    }
+}
+
+// P2 work lists: the chunks of each portion's buckets (one thread per portion)
+__global__ void k_cl_xprep2(const uint32_t* __restrict__ bucket, uint32_t nb1, uint32_t parts, uint32_t nbp,
+                            uint32_t* __restrict__ bucket_tiles, uint32_t* __restrict__ part_tiles,
+                            unsigned int* __restrict__ next) {
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t p = 0; p < parts; ++p) {
+            part_tiles[p] = t;
+            uint32_t c = 0;
+            uint32_t* bt = bucket_tiles + (uint64_t)p * (nbp + 1);
+            for (uint32_t m = 0; m < nbp; ++m) {
+                bt[m] = c;
+                const uint32_t bk = p + parts * m;
+                if (bk < nb1) c += (bucket[bk + 1] - bucket[bk] + kXsChunk - 1) / kXsChunk;
+            }
+            bt[nbp] = c;
+            t += c;
+            next[p] = 0u;
+        }
+        part_tiles[parts] = t;
+    }
+}
+
+// P2h: (bucket, second digit) counts; one workgroup per chunk of any portion
+__global__ __launch_bounds__(256) void k_cl_xhist2(XArgs a) {
+    __shared__ uint32_t h[kMaxDigits];
+    const uint32_t k = blockIdx.x;
+    if (k >= a.part_tiles[a.parts]) return;
+    uint32_t p = 0;
+    while (p + 1 < a.parts && a.part_tiles[p + 1] <= k) ++p;
+    uint64_t lo, hi;
+    uint32_t b;
+    xchunk<true>(a, p, k - a.part_tiles[p], &lo, &hi, &b);
+    const uint32_t mask = a.nd - 1;
+    for (uint32_t d = threadIdx.x; d < a.nd; d += 256) h[d] = 0u;
+    __syncthreads();
+    constexpr int U = kXsChunk / 256;
+    uint64_t v[U];
+#pragma unroll
+    for (int e = 0; e < U; ++e) {
+        const uint64_t i = lo + threadIdx.x + (uint64_t)e * 256;
+        v[e] = a.in.trace_id[i < hi ? i : lo];
+    }
+#pragma unroll
+    for (int e = 0; e < U; ++e)
+        if (lo + threadIdx.x + (uint64_t)e * 256 < hi) atomicAdd(&h[digit_of(part_hash(v[e]), a.shift, mask)], 1u);
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < a.nd; d += 256)
+        if (h[d]) atomicAdd(&a.hist[(uint64_t)b * a.nd + d], h[d]);
+}
+
+// sub-bucket bounds from the scanned (bucket, digit) counts (the scan itself is the P2 cursors)
+__global__ void k_cl_xsub(const uint32_t* __restrict__ scanned, uint64_t m, uint64_t n, uint32_t* __restrict__ sub) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < m) sub[q] = scanned[q];
+    if (q == m) sub[m] = (uint32_t)n;
+}
+
+template <bool LOCAL, uint32_t MAXD>
+__global__ __launch_bounds__(kXsWG, kXsWG / 256) void k_cl_xscatter(XArgs a) {
+    using DigT = typename std::conditional<(MAXD <= 256), uint8_t, uint16_t>::type;
+    __shared__ uint32_t s_cur[MAXD];  // output position of the chunk's run of each digit
+    __shared__ uint32_t s_cnt[MAXD];  // records of the chunk per digit
+    __shared__ uint32_t s_off[MAXD];  // exclusive offsets of the digits inside the sorted chunk
+    __shared__ DigT s_dig[kXsChunk];  // digit of the sorted chunk's record i
+    __shared__ __align__(16) uint64_t s_stage[kXsChunk];
+    __shared__ uint32_t s_tmp[32];
+    __shared__ uint32_t s_job;
+    const int t = threadIdx.x;
+    const uint32_t nd = a.nd, mask = nd - 1;
+    const uint32_t p0 = xcc_id() % a.parts;
+    for (uint32_t d = t; d < nd; d += kXsWG) s_cnt[d] = 0u;
+    for (uint32_t step = 0; step < a.parts;) {
+        const uint32_t p = (p0 + step) % a.parts;
+        __syncthreads();  // the previous chunk is done with s_job and the counts
+        if (t == 0) s_job = atomicAdd(&a.next[p], 1u);
+        __syncthreads();
+        const uint32_t j = s_job;
+        if (j >= a.part_tiles[p + 1] - a.part_tiles[p]) {  // this portion is drained: the next one
+            ++step;
+            continue;
+        }
+        uint64_t lo, hi;
+        uint32_t bk;
+        xchunk<LOCAL>(a, p, j, &lo, &hi, &bk);
+        const uint32_t cnt = (uint32_t)(hi - lo);
+        unsigned int* const cur = a.cursor + (uint64_t)(LOCAL ? bk : p) * nd;
+        // 1. digits and ranks (LDS atomic counting sort: the order inside a digit is free)
+        uint32_t dg[kXsU], rank[kXsU];
+        uint64_t tids[kXsU];
+#pragma unroll
+        for (int k = 0; k < kXsU; ++k) {
+            const uint32_t i = t + k * kXsWG;
+            tids[k] = a.in.trace_id[lo + (i < cnt ? i : 0)];
+        }
+#pragma unroll
+        for (int k = 0; k < kXsU; ++k) {
+            dg[k] = digit_of(part_hash(tids[k]), a.shift, mask);
+            rank[k] = (t + k * kXsWG < cnt) ? atomicAdd(&s_cnt[dg[k]], 1u) : 0u;
+        }
+        __syncthreads();
+        // 2. digit offsets inside the chunk; the chunk's runs claimed at the shared cursors
+        scan_digits<kXsWG, MAXD>(s_cnt, nd, 0u, s_off, s_tmp);
+        for (uint32_t d = t; d < nd; d += kXsWG) {
+            const uint32_t c = s_cnt[d];
+            s_cur[d] = c ? atomicAdd(&cur[d], c) : 0u;
+        }
+        __syncthreads();
+        // 3. sorted position of each loaded record; digit of each sorted slot
+        uint32_t pos[kXsU], dest[kXsU];
+#pragma unroll
+        for (int k = 0; k < kXsU; ++k) {
+            pos[k] = s_off[dg[k]] + rank[k];
+            if (t + k * kXsWG < cnt) s_dig[pos[k]] = (DigT)dg[k];
+        }
+        __syncthreads();
+        // 4. output position of each sorted slot this thread writes
+#pragma unroll
+        for (int k = 0; k < kXsU; ++k) {
+            const uint32_t i = t + k * kXsWG;
+            const uint32_t d = i < cnt ? s_dig[i] : 0u;
+            dest[k] = i < cnt ? s_cur[d] + (i - s_off[d]) : 0u;
+        }
+        // 5. the columns through the LDS stage (the traceIds are in registers already)
+        move_columns<kXsU, kXsWG, 0>(a.in, a.out, lo, cnt, pos, dest, s_stage, tids);
+        for (uint32_t d = t; d < nd; d += kXsWG) s_cnt[d] = 0u;  // (move_columns ended on a barrier)
+    }
+}
+
 // ---- P3: trace runs inside each sub-bucket --------------------------------------------------------
 constexpr int kTrWG = 512;
 #ifndef ZK_CL_TR_SLOTS
@@ -853,10 +1080,28 @@ ClusterPlan cluster_plan(uint64_t n, uint32_t cus) {
     return p;
 }
 
+// the XCD-shared-stream path's extra scratch: P1 cursors, portion tables, P2 chunk lists, the
+// (bucket, digit) counts and the P2 cursors
+struct XLayout {
+    uint64_t cur1, part, btiles, m2, total;
+};
+XLayout x_layout(const ClusterPlan& p) {
+    XLayout l{};
+    const uint64_t nbp = (p.nb1 + kParts - 1) / kParts;
+    l.m2 = (uint64_t)p.nb1 * p.nb2 + 1;
+    l.cur1 = align256((uint64_t)kParts * p.nb1 * 4);
+    l.part = align256((kParts + 1) * 4);
+    l.btiles = align256(kParts * (nbp + 1) * 4);
+    l.total = l.cur1 + 3 * l.part + l.btiles + 2 * align256(l.m2 * 4);
+    return l;
+}
+
 uint64_t cluster_scratch_bytes(const ClusterPlan& p) {
     const uint64_t m = (uint64_t)p.nb1 * p.grid;
+    const XLayout xl = x_layout(p);
+    const uint64_t sm = m > xl.m2 ? m : xl.m2;
     return 2 * align256(m * 4) + align256(((uint64_t)p.nb1 + 1) * 4) + align256(((uint64_t)p.nb1 * p.nb2 + 1) * 4) +
-           256 + align256(scan_bytes(m));
+           256 + xl.total + align256(scan_bytes(sm));
 }
 
 hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const SpanColsMut& A, const SpanColsMut& B,
@@ -871,7 +1116,16 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
     uint32_t* bucket = (uint32_t*)(sp + 2 * align256(m * 4));
     uint32_t* sub = (uint32_t*)((uint8_t*)bucket + align256(((uint64_t)p.nb1 + 1) * 4));
     unsigned int* next = (unsigned int*)((uint8_t*)sub + align256(((uint64_t)p.nb1 * p.nb2 + 1) * 4));
-    void* temp = (uint8_t*)next + 256;
+    const XLayout xl = x_layout(p);
+    uint8_t* xp = (uint8_t*)next + 256;
+    unsigned int* cursor1 = (unsigned int*)xp;
+    uint32_t* part_lo = (uint32_t*)(xp + xl.cur1);
+    uint32_t* part_tiles = (uint32_t*)(xp + xl.cur1 + xl.part);
+    unsigned int* xnext = (unsigned int*)(xp + xl.cur1 + 2 * xl.part);
+    uint32_t* bucket_tiles = (uint32_t*)(xp + xl.cur1 + 3 * xl.part);
+    uint32_t* hist2 = (uint32_t*)(xp + xl.cur1 + 3 * xl.part + xl.btiles);
+    unsigned int* cursor2 = (unsigned int*)((uint8_t*)hist2 + align256(xl.m2 * 4));
+    void* temp = xp + xl.total;
     hipError_t e = hipMemsetAsync(next, 0, 4, s);
     if (e != hipSuccess) return e;
     auto dev = [n](const SpanColsMut& c) {
@@ -910,7 +1164,29 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
     a.offs = offs;
     a.shift = sh1;
     a.nd = p.nb1;
-    e = (ZK_CL_WC && p.nb1 <= kWcDigits)
+    const uint32_t parts1 = p.grid < kParts ? p.grid : kParts;
+    XArgs x1{};
+    if (ZK_CL_XCD) {
+        x1.in = in;
+        x1.out = A;
+        x1.shift = sh1;
+        x1.nd = p.nb1;
+        x1.parts = parts1;
+        x1.part_tiles = part_tiles;
+        x1.next = xnext;
+        x1.cursor = cursor1;
+        x1.part_lo = part_lo;
+        e = launch_checked("k_cl_xprep1", k_cl_xprep1, dim3((parts1 * p.nb1 + 255) / 256), dim3(256), 0, s,
+                           (const uint32_t*)offs, p.nb1, p.grid, parts1, p.per, n, cursor1, part_lo, part_tiles, xnext);
+        if (e != hipSuccess) return e;
+    }
+    const uint32_t gx = cus ? cus : 256;
+    e = ZK_CL_XCD ? (p.nb1 <= kSmallDigits
+                         ? launch_checked("k_cl_xscatter<global,256>", k_cl_xscatter<false, kSmallDigits>, dim3(gx),
+                                          dim3(kXsWG), 0, s, x1)
+                         : launch_checked("k_cl_xscatter<global>", k_cl_xscatter<false, kMaxDigits>, dim3(gx),
+                                          dim3(kXsWG), 0, s, x1))
+        : (ZK_CL_WC && p.nb1 <= kWcDigits)
             ? launch_checked("k_cl_scatter_wc<global>", k_cl_scatter_wc<false>, dim3(p.grid), dim3(kWcWG), 0, s, a)
         : p.nb1 <= kSmallDigits
             ? launch_checked("k_cl_scatter<global,256>", k_cl_scatter<false, kSmallDigits>, dim3(p.grid), dim3(kScWG), 0,
@@ -932,7 +1208,41 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
         b.sub = sub;
         b.shift = sh1 - p.b2;
         b.nd = p.nb2;
-        e = (ZK_CL_WC && p.nb2 <= kWcDigits)
+        const uint32_t parts2 = p.nb1 < kParts ? p.nb1 : kParts;
+        const uint32_t nbp = (p.nb1 + parts2 - 1) / parts2;
+        XArgs x2{};
+        if (ZK_CL_XCD) {
+            x2.in = dev(A);
+            x2.out = B;
+            x2.shift = sh1 - p.b2;
+            x2.nd = p.nb2;
+            x2.parts = parts2;
+            x2.part_tiles = part_tiles;
+            x2.next = xnext;
+            x2.cursor = cursor2;
+            x2.bucket = bucket;
+            x2.bucket_tiles = bucket_tiles;
+            x2.nb1 = p.nb1;
+            x2.nbp = nbp;
+            x2.hist = hist2;
+            const uint32_t maxchunks = (uint32_t)((n + kXsChunk - 1) / kXsChunk + p.nb1);
+            size_t tb2 = scan_bytes(xl.m2);
+            e = launch_checked("k_cl_xprep2", k_cl_xprep2, dim3(1), dim3(64), 0, s, (const uint32_t*)bucket, p.nb1,
+                               parts2, nbp, bucket_tiles, part_tiles, xnext);
+            if (e == hipSuccess) e = hipMemsetAsync(hist2, 0, xl.m2 * 4, s);
+            if (e == hipSuccess) e = launch_checked("k_cl_xhist2", k_cl_xhist2, dim3(maxchunks), dim3(256), 0, s, x2);
+            if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(temp, tb2, hist2, cursor2, (int)xl.m2, s);
+            if (e == hipSuccess)
+                e = launch_checked("k_cl_xsub", k_cl_xsub, dim3((unsigned)((xl.m2 + 255) / 256)), dim3(256), 0, s,
+                                   (const uint32_t*)cursor2, xl.m2 - 1, n, sub);
+            if (e != hipSuccess) return e;
+        }
+        e = ZK_CL_XCD ? (p.nb2 <= kSmallDigits
+                             ? launch_checked("k_cl_xscatter<local,256>", k_cl_xscatter<true, kSmallDigits>, dim3(gx),
+                                              dim3(kXsWG), 0, s, x2)
+                             : launch_checked("k_cl_xscatter<local>", k_cl_xscatter<true, kMaxDigits>, dim3(gx),
+                                              dim3(kXsWG), 0, s, x2))
+            : (ZK_CL_WC && p.nb2 <= kWcDigits)
                 ? launch_checked("k_cl_scatter_wc<local>", k_cl_scatter_wc<true>, dim3(p.nb1), dim3(kWcWG), 0, s, b)
             : p.nb2 <= kSmallDigits
                 ? launch_checked("k_cl_scatter<local,256>", k_cl_scatter<true, kSmallDigits>, dim3(p.nb1), dim3(kScWG),
