@@ -6,6 +6,14 @@
 
 namespace zk {
 
+// the XCD this wave runs on (0..7): a placement hint for speed only (MI355X_MICROARCH.md,
+// "Workgroup dispatch, XCD placement")
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    return x;
+}
+
 // Exclusive prefix sum over the workgroup (one value per thread) and the workgroup total.
 // NW = waves per block (blockDim.x == 64 * NW, NW <= 16); s_tmp: 32 u32 of LDS. Two barriers.
 template <int NW>

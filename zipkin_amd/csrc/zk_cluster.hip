@@ -564,12 +564,6 @@ struct XArgs {
     uint32_t* hist;                    // P2h: [nb1][nd] counts
 };
 
-__device__ __forceinline__ uint32_t xcc_id() {
-    uint32_t x;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
-    return x;
-}
-
 // chunk j of portion p -> its records [lo, hi) and (local) its bucket
 template <bool LOCAL>
 __device__ __forceinline__ void xchunk(const XArgs& a, uint32_t p, uint32_t j, uint64_t* lo, uint64_t* hi,

@@ -248,6 +248,138 @@ __global__ __launch_bounds__(WG) void k_part_scatter_lines(const uint32_t* __res
     }
 }
 
+// The scatter with write streams shared per XCD (flat input, S <= kLineMaxS; ZK_PART_XCD): the
+// input is cut into P <= 8 portions (groups of the histogram's workgroup ranges) and every
+// service's output range into P sub-ranges, one per portion. Workgroups start on their XCD's
+// portion (HW_REG_XCC_ID), take chunks of 8192 items in order, counting-sort a chunk by service
+// in LDS and claim its runs at the portion's shared per-service cursors (one global atomic per
+// service of the chunk): the ~32 workgroups of an XCD append to the same S streams, so adjacent
+// runs fill their lines through one L2 (the per-workgroup ranges of k_part_scatter_lines keep
+// grid x S streams apart and need LDS carries for whole lines). A workgroup whose portion is
+// drained takes chunks of the others: placement changes only speed. Same pattern as the
+// clustering pass (zk_cluster.hip k_cl_xscatter, profiles/r03/ab_cluster_writes.txt).
+#ifndef ZK_PART_XCD
+#define ZK_PART_XCD 1
+#endif
+constexpr uint32_t kPartParts = 8;
+constexpr int kPxWG = 1024;
+constexpr int kPxU = 8;
+constexpr uint32_t kPxChunk = kPxWG * kPxU;
+
+struct PartX {
+    const uint32_t* svc;
+    const uint64_t* payload;
+    uint64_t* out;
+    uint32_t S, parts;
+    unsigned int* cursor;        // [P][S]
+    const uint64_t* part_lo;     // P + 1 portion bounds (items)
+    const uint32_t* part_tiles;  // P + 1: chunks of the portions before p
+    unsigned int* next;          // P chunk counters
+    bool hash;
+    uint64_t hash_seed;
+};
+
+__global__ void k_part_xprep(const uint32_t* __restrict__ offs, uint32_t S, uint32_t grid, uint32_t parts,
+                             uint64_t per, uint64_t n, unsigned int* __restrict__ cursor, uint64_t* __restrict__ part_lo,
+                             uint32_t* __restrict__ part_tiles, unsigned int* __restrict__ next) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < parts * S) {
+        const uint32_t p = q / S, b = q % S;
+        cursor[q] = offs[(uint64_t)b * grid + (uint64_t)p * grid / parts];
+    }
+    if (q == 0) {
+        uint32_t t = 0;
+        for (uint32_t p = 0; p <= parts; ++p) {
+            const uint64_t lo = (uint64_t)p * grid / parts * per;
+            part_lo[p] = lo < n ? lo : n;
+        }
+        for (uint32_t p = 0; p < parts; ++p) {
+            part_tiles[p] = t;
+            t += (uint32_t)((part_lo[p + 1] - part_lo[p] + kPxChunk - 1) / kPxChunk);
+            next[p] = 0u;
+        }
+        part_tiles[parts] = t;
+    }
+}
+
+__global__ __launch_bounds__(kPxWG, kPxWG / 256) void k_part_xscatter(PartX a) {
+    constexpr int BPT = (kLineMaxS + kPxWG - 1) / kPxWG;  // services per thread in the scan
+    __shared__ uint32_t s_cnt[kLineMaxS];  // items of the chunk per service
+    __shared__ uint32_t s_off[kLineMaxS];  // exclusive offsets in the sorted chunk
+    __shared__ uint32_t s_cur[kLineMaxS];  // output position of the chunk's run of each service
+    __shared__ uint64_t s_sorted[kPxChunk];
+    __shared__ uint16_t s_svc[kPxChunk];
+    __shared__ uint32_t s_tmp[32];
+    __shared__ uint32_t s_job;
+    const int t = threadIdx.x;
+    const uint32_t S = a.S;
+    const uint32_t p0 = xcc_id() % a.parts;
+    for (uint32_t b = t; b < S; b += kPxWG) s_cnt[b] = 0u;
+    for (uint32_t step = 0; step < a.parts;) {
+        const uint32_t p = (p0 + step) % a.parts;
+        __syncthreads();  // the previous chunk is done with s_job and the counts
+        if (t == 0) s_job = atomicAdd(&a.next[p], 1u);
+        __syncthreads();
+        const uint32_t j = s_job;
+        if (j >= a.part_tiles[p + 1] - a.part_tiles[p]) {  // drained: the next portion
+            ++step;
+            continue;
+        }
+        const uint64_t lo = a.part_lo[p] + (uint64_t)j * kPxChunk;
+        const uint64_t e = a.part_lo[p + 1];
+        const uint64_t hi = lo + kPxChunk < e ? lo + kPxChunk : e;
+        uint64_t v[kPxU];
+        uint32_t bk[kPxU], rank[kPxU];
+#pragma unroll
+        for (int k = 0; k < kPxU; ++k) {
+            const uint64_t i = lo + t + (uint64_t)kPxWG * k;
+            bk[k] = a.svc[i < hi ? i : lo];
+            v[k] = a.payload[i < hi ? i : lo];
+        }
+#pragma unroll
+        for (int k = 0; k < kPxU; ++k) {
+            if (lo + t + (uint64_t)kPxWG * k >= hi) bk[k] = 0xFFFFFFFFu;
+            if (a.hash) v[k] = sk_mix64(v[k] ^ a.hash_seed);
+            rank[k] = bk[k] < S ? atomicAdd(&s_cnt[bk[k]], 1u) : 0u;
+        }
+        __syncthreads();
+        uint32_t cnt;
+        {
+            uint32_t h[BPT], sum = 0;
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) {
+                const uint32_t bin = t * BPT + q;
+                h[q] = bin < S ? s_cnt[bin] : 0u;
+                sum += h[q];
+            }
+            uint32_t ex = block_excl_scan<kPxWG / 64>(sum, s_tmp, &cnt);
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) {
+                const uint32_t bin = t * BPT + q;
+                if (bin < S) {
+                    s_off[bin] = ex;
+                    s_cur[bin] = h[q] ? atomicAdd(&a.cursor[(uint64_t)p * S + bin], h[q]) : 0u;
+                }
+                ex += h[q];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kPxU; ++k)
+            if (bk[k] < S) {
+                const uint32_t q = s_off[bk[k]] + rank[k];
+                s_sorted[q] = v[k];
+                s_svc[q] = (uint16_t)bk[k];
+            }
+        __syncthreads();
+        for (uint32_t i = t; i < cnt; i += kPxWG) {
+            const uint32_t b = s_svc[i];
+            a.out[s_cur[b] + (i - s_off[b])] = s_sorted[i];
+        }
+        for (uint32_t b = t; b < S; b += kPxWG) s_cnt[b] = 0u;  // read by this thread only after the barrier above
+    }
+}
+
 // seg[s] = offs[s * grid], seg[S] = number of partitioned items
 __global__ void k_part_seg(const uint32_t* __restrict__ offs, const uint32_t* __restrict__ hist, uint32_t S,
                            uint32_t grid, uint64_t* __restrict__ seg) {
@@ -321,10 +453,15 @@ PartitionPlan partition_plan(uint64_t n, uint32_t S, uint32_t cus) {
     return p;
 }
 
+// the XCD-stream scatter's cursors [8][S] and portion tables, after the scan temp
+uint64_t part_x_bytes(uint32_t S) {
+    return (((uint64_t)kPartParts * S * 4 + 255) & ~255ull) + 3 * 256;
+}
+
 uint64_t partition_scratch_bytes(const PartitionPlan& p) {
     const uint64_t m = (uint64_t)p.S * p.grid;
     const uint64_t a = (m * 4 + 255) & ~255ull;
-    return 2 * a + scan_temp_bytes(m);
+    return 2 * a + scan_temp_bytes(m) + part_x_bytes(p.S);
 }
 
 namespace {
@@ -352,7 +489,32 @@ hipError_t partition_impl(const PartitionPlan& p, const uint32_t* svc, const uin
     if (e != hipSuccess) return e;
     uint64_t dyn = 0;
     const int choice = partition_scatter_choice(p.S, st_lines, st_items, &dyn);
-    if (choice == kScatterLines)
+    if (ZK_PART_XCD && !counts && p.S <= kLineMaxS && n > 0) {
+        uint8_t* xp = (uint8_t*)temp + temp_bytes;
+        PartX x{};
+        x.svc = svc;
+        x.payload = payload;
+        x.out = out;
+        x.S = p.S;
+        x.parts = p.grid < kPartParts ? p.grid : kPartParts;
+        x.cursor = (unsigned int*)xp;
+        xp += ((uint64_t)kPartParts * p.S * 4 + 255) & ~255ull;
+        uint64_t* part_lo = (uint64_t*)xp;
+        uint32_t* part_tiles = (uint32_t*)(xp + 256);
+        unsigned int* next = (unsigned int*)(xp + 512);
+        x.part_lo = part_lo;
+        x.part_tiles = part_tiles;
+        x.next = next;
+        x.hash = hash;
+        x.hash_seed = hash_seed;
+        e = launch_checked("k_part_xprep", k_part_xprep, dim3((x.parts * p.S + 255) / 256), dim3(256), 0, s,
+                           (const uint32_t*)offs, p.S, p.grid, x.parts, p.per_wg, n, x.cursor, part_lo, part_tiles, next);
+        if (e == hipSuccess) {
+            int dev = 0, cus = 256;
+            if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            e = launch_checked("k_part_xscatter", k_part_xscatter, dim3(cus > 0 ? cus : 256), dim3(kPxWG), 0, s, x);
+        }
+    } else if (choice == kScatterLines)
         e = launch_checked("k_part_scatter_lines", k_part_scatter_lines<ZK_PART_U, ZK_PART_WG>, dim3(p.grid),
                            dim3(ZK_PART_WG), dyn, s, svc, payload, n, p.per_wg, counts, p.S, p.grid, offs, out, hash,
                            hash_seed);
