@@ -16,6 +16,11 @@
 #ifndef ZK_K2_WG
 #define ZK_K2_WG 1024  // K2 workgroup: 8192-link chunks (512 threads: 0.236 -> 0.199 ms on C2)
 #endif
+#ifndef ZK_K2_REMAP
+// K2: list groups in XCD-major order. Same box, clustered C2 kernels (profiles/r03/ab_k2_xcd.txt):
+// K2 0.221 -> 0.217 ms, K3 0.149 -> 0.143 ms
+#define ZK_K2_REMAP 1
+#endif
 #ifndef ZK_K3_GUARD
 #define ZK_K3_GUARD 1  // K3: skip zero chunk updates
 #endif
@@ -132,7 +137,15 @@ __global__ __launch_bounds__(WG) void k_link_scatter(ReduceArgs r, uint32_t lpw)
     __shared__ uint64_t s_sorted[C];
     __shared__ uint32_t s_tmp[32];
     extern __shared__ __attribute__((aligned(16))) uint64_t s_carry[];  // [nb][kScatterLine]
+#if ZK_K2_REMAP
+    // XCD-aware order (dispatch puts block i on XCD i % 8): the blocks of one XCD take consecutive
+    // list groups, so the per-bucket ranges of neighbouring lists (which share their boundary
+    // lines) are written through one L2
+    const uint32_t gx = gridDim.x / 8, gr = gridDim.x % 8, xi = blockIdx.x % 8;
+    const uint32_t w = (xi * gx + (xi < gr ? xi : gr) + blockIdx.x / 8) * lpw;  // first list of the group
+#else
     const uint32_t w = blockIdx.x * lpw;  // first list of the group
+#endif
     const uint32_t nl = (r.lists - w) < lpw ? (r.lists - w) : lpw;
     const int tid = threadIdx.x;
     constexpr int BPT = (kMaxBuckets + WG - 1) / WG;  // buckets per thread in the scan
