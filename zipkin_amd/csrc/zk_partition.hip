@@ -380,6 +380,97 @@ __global__ __launch_bounds__(kPxWG, kPxWG / 256) void k_part_xscatter(PartX a) {
     }
 }
 
+// ZK_PART_XSTATIC: the same scatter with portion p's chunks taken in a static stride by the blocks
+// dispatched to XCD p (block i runs on XCD i % 8), so no chunk claim is needed, and the next chunk's
+// services and payloads loaded while this chunk is placed and stored: per chunk, the claim and the
+// load round trips left the critical path (only the cursor claims' round trip stays on it).
+#ifndef ZK_PART_XSTATIC
+#define ZK_PART_XSTATIC 1
+#endif
+__global__ __launch_bounds__(kPxWG, kPxWG / 256) void k_part_xscatter_static(PartX a) {
+    constexpr int BPT = (kLineMaxS + kPxWG - 1) / kPxWG;  // services per thread in the scan
+    __shared__ uint32_t s_cnt[kLineMaxS];  // items of the chunk per service
+    __shared__ uint32_t s_off[kLineMaxS];  // exclusive offsets in the sorted chunk
+    __shared__ uint32_t s_cur[kLineMaxS];  // output position of the chunk's run of each service
+    __shared__ uint64_t s_sorted[kPxChunk];
+    __shared__ uint16_t s_svc[kPxChunk];
+    __shared__ uint32_t s_tmp[32];
+    const int t = threadIdx.x;
+    const uint32_t S = a.S;
+    const uint32_t p = blockIdx.x % a.parts, xb = blockIdx.x / a.parts;
+    const uint32_t nx = gridDim.x / a.parts + (p < gridDim.x % a.parts ? 1u : 0u);
+    const uint32_t nj = a.part_tiles[p + 1] - a.part_tiles[p];
+    const uint64_t plo = a.part_lo[p], phi = a.part_lo[p + 1];
+    unsigned int* const cur = a.cursor + (uint64_t)p * S;
+    for (uint32_t b = t; b < S; b += kPxWG) s_cnt[b] = 0u;
+    uint64_t nv[kPxU];
+    uint32_t nbk[kPxU];
+    auto load = [&](uint32_t j) {
+        const uint64_t lo = plo + (uint64_t)j * kPxChunk;
+        const uint64_t hi = lo + kPxChunk < phi ? lo + kPxChunk : phi;
+#pragma unroll
+        for (int k = 0; k < kPxU; ++k) {
+            const uint64_t i = lo + t + (uint64_t)kPxWG * k;
+            nbk[k] = a.svc[i < hi ? i : lo];
+            nv[k] = a.payload[i < hi ? i : lo];
+        }
+    };
+    if (xb < nj) load(xb);
+    for (uint32_t j = xb; j < nj; j += nx) {
+        const uint64_t lo = plo + (uint64_t)j * kPxChunk;
+        const uint64_t hi = lo + kPxChunk < phi ? lo + kPxChunk : phi;
+        uint64_t v[kPxU];
+        uint32_t bk[kPxU], rank[kPxU];
+#pragma unroll
+        for (int k = 0; k < kPxU; ++k) {
+            v[k] = nv[k];
+            bk[k] = nbk[k];
+            if (lo + t + (uint64_t)kPxWG * k >= hi) bk[k] = 0xFFFFFFFFu;
+            if (a.hash) v[k] = sk_mix64(v[k] ^ a.hash_seed);
+            rank[k] = bk[k] < S ? atomicAdd(&s_cnt[bk[k]], 1u) : 0u;
+        }
+        __syncthreads();
+        uint32_t cnt;
+        {
+            uint32_t h[BPT], sum = 0;
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) {
+                const uint32_t bin = t * BPT + q;
+                h[q] = bin < S ? s_cnt[bin] : 0u;
+                sum += h[q];
+            }
+            uint32_t ex = block_excl_scan<kPxWG / 64>(sum, s_tmp, &cnt);
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) {
+                const uint32_t bin = t * BPT + q;
+                if (bin < S) {
+                    s_off[bin] = ex;
+                    s_cur[bin] = h[q] ? atomicAdd(&cur[bin], h[q]) : 0u;
+                    s_cnt[bin] = 0u;  // every rank is taken: ready for the next chunk
+                }
+                ex += h[q];
+            }
+        }
+        __syncthreads();
+        // the next chunk's loads in flight while this one is placed and stored (issued after the
+        // cursor claims, whose returns would otherwise wait for them)
+        if (j + nx < nj) load(j + nx);
+#pragma unroll
+        for (int k = 0; k < kPxU; ++k)
+            if (bk[k] < S) {
+                const uint32_t q = s_off[bk[k]] + rank[k];
+                s_sorted[q] = v[k];
+                s_svc[q] = (uint16_t)bk[k];
+            }
+        __syncthreads();
+        for (uint32_t i = t; i < cnt; i += kPxWG) {
+            const uint32_t b = s_svc[i];
+            a.out[s_cur[b] + (i - s_off[b])] = s_sorted[i];
+        }
+        __syncthreads();  // s_sorted, s_svc, s_cur and s_off are read before the next chunk rewrites them
+    }
+}
+
 // seg[s] = offs[s * grid], seg[S] = number of partitioned items
 __global__ void k_part_seg(const uint32_t* __restrict__ offs, const uint32_t* __restrict__ hist, uint32_t S,
                            uint32_t grid, uint64_t* __restrict__ seg) {
@@ -512,7 +603,10 @@ hipError_t partition_impl(const PartitionPlan& p, const uint32_t* svc, const uin
         if (e == hipSuccess) {
             int dev = 0, cus = 256;
             if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            e = launch_checked("k_part_xscatter", k_part_xscatter, dim3(cus > 0 ? cus : 256), dim3(kPxWG), 0, s, x);
+            e = ZK_PART_XSTATIC ? launch_checked("k_part_xscatter_static", k_part_xscatter_static,
+                                                 dim3(cus > 0 ? cus : 256), dim3(kPxWG), 0, s, x)
+                                : launch_checked("k_part_xscatter", k_part_xscatter, dim3(cus > 0 ? cus : 256),
+                                                 dim3(kPxWG), 0, s, x);
         }
     } else if (choice == kScatterLines)
         e = launch_checked("k_part_scatter_lines", k_part_scatter_lines<ZK_PART_U, ZK_PART_WG>, dim3(p.grid),
