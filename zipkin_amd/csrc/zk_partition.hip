@@ -262,7 +262,13 @@ __global__ __launch_bounds__(WG) void k_part_scatter_lines(const uint32_t* __res
 #define ZK_PART_XCD 1
 #endif
 constexpr uint32_t kPartParts = 8;
-constexpr int kPxWG = 1024;
+#ifndef ZK_PX_WG
+#define ZK_PX_WG 1024  // XCD scatter workgroup (chunks of 8 items per thread)
+#endif
+#ifndef ZK_PX_GRID
+#define ZK_PX_GRID 1   // XCD scatter workgroups per CU
+#endif
+constexpr int kPxWG = ZK_PX_WG;
 constexpr int kPxU = 8;
 constexpr uint32_t kPxChunk = kPxWG * kPxU;
 
@@ -387,7 +393,7 @@ __global__ __launch_bounds__(kPxWG, kPxWG / 256) void k_part_xscatter(PartX a) {
 #ifndef ZK_PART_XSTATIC
 #define ZK_PART_XSTATIC 1
 #endif
-__global__ __launch_bounds__(kPxWG, kPxWG / 256) void k_part_xscatter_static(PartX a) {
+__global__ __launch_bounds__(kPxWG, ZK_PX_GRID * kPxWG / 256) void k_part_xscatter_static(PartX a) {
     constexpr int BPT = (kLineMaxS + kPxWG - 1) / kPxWG;  // services per thread in the scan
     __shared__ uint32_t s_cnt[kLineMaxS];  // items of the chunk per service
     __shared__ uint32_t s_off[kLineMaxS];  // exclusive offsets in the sorted chunk
@@ -604,7 +610,7 @@ hipError_t partition_impl(const PartitionPlan& p, const uint32_t* svc, const uin
             int dev = 0, cus = 256;
             if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
             e = ZK_PART_XSTATIC ? launch_checked("k_part_xscatter_static", k_part_xscatter_static,
-                                                 dim3(cus > 0 ? cus : 256), dim3(kPxWG), 0, s, x)
+                                                 dim3((cus > 0 ? cus : 256) * ZK_PX_GRID), dim3(kPxWG), 0, s, x)
                                 : launch_checked("k_part_xscatter", k_part_xscatter, dim3(cus > 0 ? cus : 256),
                                                  dim3(kPxWG), 0, s, x);
         }
