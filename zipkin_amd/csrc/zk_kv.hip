@@ -43,6 +43,12 @@ constexpr int kPrefetch = ZK_KV_PREFETCH;  // candidate rounds of keys in flight
 // 3.22-3.26 ms, profiles/r02/ab_kv_cand_pipe.txt)
 #define ZK_KV_CAND_PIPE 1
 #endif
+#ifndef ZK_KV_PROBE1
+#define ZK_KV_PROBE1 1  // candidates: every key's first set slot read before any probe chain
+#endif
+#ifndef ZK_KV_DIAG
+#define ZK_KV_DIAG 0  // A/B diagnostics of the candidate pass (results wrong): 1 no set probes/inserts, 2 + no estimates
+#endif
 constexpr uint64_t kEmptyKey = ~0ull;
 
 __device__ __forceinline__ bool beats(uint32_t e1, uint64_t k1, uint32_t e2, uint64_t k2) {
@@ -359,19 +365,43 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
 #pragma unroll
         for (int j = 0; j < J; ++j) {
             const RowHash rh = RowHash::from_hash(kq[j], a.wbits);  // kq: the keys' hashes
-            est[j] = estimate_rh(cm, a, rh);
+            est[j] = ZK_KV_DIAG == 2 ? (uint32_t)kq[j] | 1u : estimate_rh(cm, a, rh);
             slot[j] = rh.set;
         }
         const uint32_t has_thr = t.has_thr, thr_est = t.thr_est;
         const uint64_t thr_key = t.thr_key;
         uint32_t need = 0;
+#if ZK_KV_PROBE1
+        // the first slot of every key read at once (J independent LDS reads instead of J dependent
+        // probe chains): under a skewed distribution most live keys sit in their first slot; only
+        // a collision walks on. No insert runs between here and B1, so plain reads are final.
+        uint64_t h0[J];
+#pragma unroll
+        for (int j = 0; j < J; ++j) h0[j] = t.hk[slot[j]];
+#endif
 #pragma unroll
         for (int j = 0; j < J; ++j) {
             // a tie with the threshold estimate is decided on the key itself (unhashed only then)
             const bool live = b + (uint64_t)j * kKvWG + threadIdx.x < hi && est[j] != 0u &&
                               (!has_thr || est[j] > thr_est ||
                                (est[j] == thr_est && kv_key(kq[j], a.seeds[0]) < thr_key));
-            if (live && !ts_contains(t, kq[j], slot[j])) need |= 1u << j;
+#if ZK_KV_PROBE1
+            if (ZK_KV_DIAG == 0 && live) {
+                bool in;
+                if (kq[j] == kEmptyKey)
+                    in = ts_contains(t, kq[j], slot[j]);
+                else if (h0[j] == kq[j])
+                    in = true;
+                else if (h0[j] == kEmptyKey)
+                    in = false;
+                else
+                    in = ts_contains(t, kq[j], (slot[j] + 1) & (kSetCap - 1));
+                if (!in) need |= 1u << j;
+            }
+#else
+            if (ZK_KV_DIAG == 0 && live && !ts_contains(t, kq[j], slot[j])) need |= 1u << j;
+#endif
+            if (ZK_KV_DIAG != 0 && live) need |= (est[j] == 0xFFFFFFFFu) << j;  // (never: keeps est live)
         }
         if (need) atomicAdd(&t.pending[parity], (uint32_t)__popc(need));
         __syncthreads();  // B1: survivors counted
