@@ -543,8 +543,14 @@ __global__ __launch_bounds__(kWcWG, kWcWG / 256) void k_cl_scatter_wc(ScatterArg
 #define ZK_CL_XCD 1  // 0: the per-workgroup-range scatter (k_cl_scatter_wc)
 #endif
 constexpr uint32_t kParts = 8;
+#ifndef ZK_CL_XS_U
+#define ZK_CL_XS_U 8     // records per thread per P1/P2 chunk
+#endif
+#ifndef ZK_CL_XS_GRID
+#define ZK_CL_XS_GRID 1  // P1/P2 workgroups per CU
+#endif
 constexpr int kXsWG = 1024;
-constexpr int kXsU = 8;
+constexpr int kXsU = ZK_CL_XS_U;
 constexpr uint32_t kXsChunk = kXsWG * kXsU;
 
 struct XArgs {
@@ -674,7 +680,7 @@ __global__ void k_cl_xsub(const uint32_t* __restrict__ scanned, uint64_t m, uint
 }
 
 template <bool LOCAL, uint32_t MAXD>
-__global__ __launch_bounds__(kXsWG, kXsWG / 256) void k_cl_xscatter(XArgs a) {
+__global__ __launch_bounds__(kXsWG, ZK_CL_XS_GRID * kXsWG / 256) void k_cl_xscatter(XArgs a) {
     using DigT = typename std::conditional<(MAXD <= 256), uint8_t, uint16_t>::type;
     __shared__ uint32_t s_cur[MAXD];  // output position of the chunk's run of each digit
     __shared__ uint32_t s_cnt[MAXD];  // records of the chunk per digit
@@ -1174,7 +1180,7 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
                            (const uint32_t*)offs, p.nb1, p.grid, parts1, p.per, n, cursor1, part_lo, part_tiles, xnext);
         if (e != hipSuccess) return e;
     }
-    const uint32_t gx = cus ? cus : 256;
+    const uint32_t gx = (cus ? cus : 256) * ZK_CL_XS_GRID;
     e = ZK_CL_XCD ? (p.nb1 <= kSmallDigits
                          ? launch_checked("k_cl_xscatter<global,256>", k_cl_xscatter<false, kSmallDigits>, dim3(gx),
                                           dim3(kXsWG), 0, s, x1)
