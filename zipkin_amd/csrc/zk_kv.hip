@@ -44,7 +44,7 @@ constexpr int kPrefetch = ZK_KV_PREFETCH;  // candidate rounds of keys in flight
 #define ZK_KV_CAND_PIPE 1
 #endif
 #ifndef ZK_KV_PROBE1
-#define ZK_KV_PROBE1 1  // candidates: every key's first set slot read before any probe chain
+#define ZK_KV_PROBE1 2  // candidates: 1 every key's first set slot read before any probe chain; 2 + two slots, mask decisions
 #endif
 #ifndef ZK_KV_DIAG
 #define ZK_KV_DIAG 0  // A/B diagnostics of the candidate pass (results wrong): 1 no set probes/inserts, 2 + no estimates
@@ -379,6 +379,45 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
 #pragma unroll
         for (int j = 0; j < J; ++j) h0[j] = t.hk[slot[j]];
 #endif
+#if ZK_KV_PROBE1 == 2
+        // Decisions as bit masks (no short-circuit branches: every divergent branch costs the scalar
+        // unit exec-mask bookkeeping, and the pass was bound by scalar issue, profiles/r03/
+        // ab_kv_candidates.txt). The first two probe slots of every key are read at once; only a
+        // threshold tie (decided on the unhashed key), the sentinel key and a key whose two slots hold
+        // other keys take a branch.
+        uint64_t h1[J];
+#pragma unroll
+        for (int j = 0; j < J; ++j) h1[j] = t.hk[(slot[j] + 1) & (kSetCap - 1)];
+        uint32_t live_m = 0, tie_m = 0;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const bool valid = (b + (uint64_t)j * kKvWG + threadIdx.x < hi) & (est[j] != 0u);
+            live_m |= (uint32_t)(valid & ((has_thr == 0u) | (est[j] > thr_est))) << j;
+            tie_m |= (uint32_t)(valid & (has_thr != 0u) & (est[j] == thr_est)) << j;
+        }
+        if (tie_m) {
+#pragma unroll
+            for (int j = 0; j < J; ++j)
+                if ((tie_m >> j) & 1u) live_m |= (uint32_t)(kv_key(kq[j], a.seeds[0]) < thr_key) << j;
+        }
+        uint32_t slow_m = 0;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const bool special = kq[j] == kEmptyKey;
+            const bool hit = (h0[j] == kq[j]) | ((h0[j] != kEmptyKey) & (h1[j] == kq[j]));
+            const bool absent = (h0[j] == kEmptyKey) | ((h0[j] != kq[j]) & (h1[j] == kEmptyKey));
+            const uint32_t lv = (live_m >> j) & 1u;
+            need |= (lv & (uint32_t)(!special & absent & !hit)) << j;
+            slow_m |= (lv & (uint32_t)(special | (!hit & !absent))) << j;
+        }
+        if (ZK_KV_DIAG != 0) need = live_m & (uint32_t)(est[0] == 0xFFFFFFFFu);  // (never: keeps est live)
+        if (ZK_KV_DIAG == 0 && slow_m) {
+#pragma unroll
+            for (int j = 0; j < J; ++j)
+                if (((slow_m >> j) & 1u) && !ts_contains(t, kq[j], kq[j] == kEmptyKey ? slot[j] : (slot[j] + 2) & (kSetCap - 1)))
+                    need |= 1u << j;
+        }
+#else
 #pragma unroll
         for (int j = 0; j < J; ++j) {
             // a tie with the threshold estimate is decided on the key itself (unhashed only then)
@@ -403,6 +442,7 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
 #endif
             if (ZK_KV_DIAG != 0 && live) need |= (est[j] == 0xFFFFFFFFu) << j;  // (never: keeps est live)
         }
+#endif
         if (need) atomicAdd(&t.pending[parity], (uint32_t)__popc(need));
         __syncthreads();  // B1: survivors counted
         if (threadIdx.x == 0) t.pending[parity ^ 1u] = 0u;  // the previous block's count: read by all before B1
