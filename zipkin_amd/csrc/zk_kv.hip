@@ -46,6 +46,9 @@ constexpr int kPrefetch = ZK_KV_PREFETCH;  // candidate rounds of keys in flight
 #ifndef ZK_KV_PROBE1
 #define ZK_KV_PROBE1 2  // candidates: 1 every key's first set slot read before any probe chain; 2 + two slots, mask decisions
 #endif
+#ifndef ZK_KV_ROWS_OUTER
+#define ZK_KV_ROWS_OUTER 1  // candidates: count-min rows as the outer loop over a thread's keys
+#endif
 #ifndef ZK_KV_DIAG
 #define ZK_KV_DIAG 0  // A/B diagnostics of the candidate pass (results wrong): 1 no set probes/inserts, 2 + no estimates
 #endif
@@ -362,12 +365,32 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
         // estimates unconditionally (clamped keys past the end are harmless): a load whose only
         // uses sit in a conditional block is sunk into it, and then every key waits for HBM
         uint32_t est[J], slot[J];
+#if ZK_KV_ROWS_OUTER
+        {  // rows outer, keys inner: one loop step per row for all J keys
+            RowHash rh[J];
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                rh[j] = RowHash::from_hash(kq[j], a.wbits);  // kq: the keys' hashes
+                est[j] = 0xFFFFFFFFu;
+                slot[j] = rh[j].set;
+            }
+            for (uint32_t r = 0; r < a.depth; ++r) {
+                const uint32_t* row = cm + r * a.width;
+#pragma unroll
+                for (int j = 0; j < J; ++j) est[j] = min(est[j], row[rh[j].next()]);
+            }
+            if (ZK_KV_DIAG == 2)
+#pragma unroll
+                for (int j = 0; j < J; ++j) est[j] = (uint32_t)kq[j] | 1u;
+        }
+#else
 #pragma unroll
         for (int j = 0; j < J; ++j) {
             const RowHash rh = RowHash::from_hash(kq[j], a.wbits);  // kq: the keys' hashes
             est[j] = ZK_KV_DIAG == 2 ? (uint32_t)kq[j] | 1u : estimate_rh(cm, a, rh);
             slot[j] = rh.set;
         }
+#endif
         const uint32_t has_thr = t.has_thr, thr_est = t.thr_est;
         const uint64_t thr_key = t.thr_key;
         uint32_t need = 0;
