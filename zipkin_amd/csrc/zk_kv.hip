@@ -46,6 +46,9 @@ constexpr int kPrefetch = ZK_KV_PREFETCH;  // candidate rounds of keys in flight
 #ifndef ZK_KV_PROBE1
 #define ZK_KV_PROBE1 2  // candidates: 1 every key's first set slot read before any probe chain; 2 + two slots, mask decisions
 #endif
+#ifndef ZK_KV_HOT
+#define ZK_KV_HOT 1  // sketch: one learned hot key per wave, its lanes' adds combined
+#endif
 #ifndef ZK_KV_ROWS_OUTER
 #define ZK_KV_ROWS_OUTER 1  // candidates: count-min rows as the outer loop over a thread's keys
 #endif
@@ -288,6 +291,16 @@ __global__ __launch_bounds__(kKvWG) void k_kv_sketch(KvArgs a) {
             k[e] = a.keys[i < hi ? i : lo];
         }
     };
+#if ZK_KV_HOT
+    // Under a skewed key distribution several lanes of one atomic instruction hold the same hot key and
+    // their adds to the same counters serialise in LDS. Each wave tracks one hot key (wave-uniform):
+    // the lanes holding it are counted by a ballot and their first lane adds the count. The hot key
+    // is learned on the fly: every instruction also tests the key of a rotating lane and adopts it
+    // when more lanes hold it. (Only which lane adds what changes: every counter gets the same total.)
+    const int lane = threadIdx.x & 63;
+    uint64_t hot = ~0ull;
+    int probe = 0;
+#endif
     auto add = [&](const uint64_t (&k)[U], uint64_t b) {
         // row hashes unconditionally, so the loads are not sunk into the conditional (see candidates)
         RowHash rh[U];
@@ -295,8 +308,26 @@ __global__ __launch_bounds__(kKvWG) void k_kv_sketch(KvArgs a) {
         for (int e = 0; e < U; ++e) rh[e] = RowHash::from_hash(k[e], a.wbits);  // keys arrive hashed
 #pragma unroll
         for (int e = 0; e < U; ++e) {
-            if (b + (uint64_t)e * kKvWG + threadIdx.x < hi)
+            const bool valid = b + (uint64_t)e * kKvWG + threadIdx.x < hi;
+#if ZK_KV_HOT
+            const uint64_t cand = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(k[e] >> 32), probe) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readlane((uint32_t)k[e], probe);
+            probe = (probe + 1) & 63;
+            uint64_t mh = __ballot(valid && k[e] == hot);
+            const uint64_t mc = __ballot(valid && k[e] == cand);
+            if (__popcll(mc) > __popcll(mh)) {
+                hot = cand;
+                mh = mc;
+            }
+            const bool in = (mh >> lane) & 1ull;
+            const uint32_t inc = in ? (lane == __ffsll((unsigned long long)mh) - 1 ? (uint32_t)__popcll(mh) : 0u)
+                                    : (valid ? 1u : 0u);
+            if (inc)
+                for (uint32_t r = 0; r < a.depth; ++r) atomicAdd(&cm[r * a.width + rh[e].next()], inc);
+#else
+            if (valid)
                 for (uint32_t r = 0; r < a.depth; ++r) atomicAdd(&cm[r * a.width + rh[e].next()], 1u);
+#endif
         }
     };
 #if ZK_KV_SKETCH_PIPE
