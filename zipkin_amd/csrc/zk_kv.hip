@@ -503,9 +503,11 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
         const uint32_t pend = t.pending[parity];
         if (t.count + pend > kSortCap && t.count > a.cand) ts_compact(t, a.cand, a.seeds[0]);
         if (t.count + pend <= kSortCap) {
+            if (need) {  // (most threads insert nothing: one branch instead of J)
 #pragma unroll
-            for (int j = 0; j < J; ++j)
-                if (need & (1u << j)) ts_insert(t, kq[j], est[j], slot[j]);
+                for (int j = 0; j < J; ++j)
+                    if (need & (1u << j)) ts_insert(t, kq[j], est[j], slot[j]);
+            }
             __syncthreads();  // B2: the set and count are complete for the next block's filter
         } else {
 #pragma unroll
