@@ -1105,7 +1105,10 @@ __device__ __forceinline__ bool try_resolve(const IngArgs& a, uint64_t i, const 
 // or an unsafe in-place step) go to the global-memory kernel. Service names are copied out to the
 // global scratch (the dictionary kernels read them after this kernel).
 constexpr uint32_t kLdsWG = 64;
-constexpr uint32_t kLdsBudget = 20480;
+#ifndef ZK_ING_BUDGET
+#define ZK_ING_BUDGET 20480  // LDS bytes per wave (8 waves per CU)
+#endif
+constexpr uint32_t kLdsBudget = ZK_ING_BUDGET;
 constexpr uint32_t kLdsBlock = 1024;
 constexpr uint32_t kLdsSlack = 80;  // region bytes beyond max(raw, compressed): in-place headroom + alignment
                                     // + the lane's bank skew
