@@ -7,10 +7,14 @@ all-reduce of the accumulator across traceId-hash shards], finalize into device-
 (parent, child) -> Moments arrays (K5), including the status check the reference's fail-fast
 semantics need.
 
-Workload (BASELINE.json configs[1], "C2"): 1e8 span records per GPU, zipkin-tracegen shape
-(maxDepth 6, ~24 records / ~12 logical spans per trace, ~4.15e6 traces), 500 services, generated
-on device (synthetic). N > 1: every rank owns its own traceId-hash shard of the same size
-(weak scaling; at N = 8 that is 8e8 records, the scale of configs[2]).
+Workloads (synthetic, zipkin-tracegen shape: maxDepth 6, ~24 records / ~12 logical spans per trace,
+500 services, generated on device):
+  C2 (default at N = 1, BASELINE.json configs[1]): 1e8 span records on one GPU.
+  C3 (default at N > 1, configs[2]): ONE global set of 1e9 span records whose traceIds do not depend
+     on N, sharded by mix64(traceId) % N -- rank r generates exactly the set's traces of its shard --
+     with one RCCL SUM all-reduce of the exact table per step (strong scaling: the same 1e9 records
+     at every N). Every rank hashes the finalized table (SHA-256 of m0..m4 + present); the digests
+     must agree across ranks and with the G = 1 digest in tests/golden/c3_digest.json.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -36,16 +40,17 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--records", type=int, default=100_000_000, help="span records per GPU")
+    ap.add_argument("--records", type=int, default=None,
+                    help="c2: span records per GPU (default 1e8); c3: records of the whole global set (default 1e9)")
     ap.add_argument("--services", type=int, default=500)
     ap.add_argument("--max-depth", type=int, default=6)
     ap.add_argument("--seed", type=int, default=2)
-    ap.add_argument("--cpu-sample", type=int, default=20_000_000, help="records for the CPU baseline leg (0: skip)")
+    ap.add_argument("--cpu-sample", type=int, default=100_000_000,
+                    help="records for the CPU baseline and oracle parity leg (0: skip; default: the whole C2 batch)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (0: every CPU this process may use, see usable_cpus)")
     ap.add_argument("--verify", type=int, default=0,
                     help="1: ZK_BATCH_VERIFY_TRACES on every step (exact device check of the clustering promise)")
-    ap.add_argument("--ablate", type=int, default=0, help="diagnostic: 1 = K1 without link emission (not a valid result)")
     ap.add_argument("--pipeline", type=int, default=None,
                     help="batches in flight behind the one being joined: 1 = two table/stream "
                          "sets (batch k's join overlaps batch k-1's tail), 2 = three, 0 = one set, serial steps "
@@ -63,8 +68,10 @@ def parse():
                          "Cassandra row-per-trace reads, accumulated with ZK_BATCH_TRACE_CLUSTERED; shuffled = "
                          "the same records in a random permutation (the reference's shuffles accept any order, "
                          "ZipkinAggregateJob.scala:21-22,28-33): every step runs the device clustering pass first")
-    ap.add_argument("--workload", default="c2", choices=("c1", "c2", "c4", "c5", "ingest"),
-                    help="c2 (default, the headline): dependency path; c1: the reference's CPU config "
+    ap.add_argument("--workload", default=None, choices=("c1", "c2", "c3", "c4", "c5", "ingest"),
+                    help="default: c2 at N = 1, c3 at N > 1. c2 (the N = 1 headline): dependency path on 1e8 "
+                         "records; c3: the same path on one global 1e9-record set sharded across the N ranks "
+                         "(configs[2]); c1: the reference's CPU config "
                          "(10k tracegen traces, 20 services) on the GPU and the CPU baseline; "
                          "c4: key-value top-K sketch over "
                          "binary annotations; c5: per-service HLL + duration histogram from span fragments; "
@@ -73,6 +80,10 @@ def parse():
     ap.add_argument("--items", type=int, default=1_000_000_000,
                     help="c4: binary annotations per step (BASELINE configs[3]: 1e9, 12 GB in HBM)")
     a = ap.parse_args()
+    if a.workload is None:
+        a.workload = "c3" if int(os.environ.get("WORLD_SIZE", "1")) > 1 else "c2"
+    if a.records is None:
+        a.records = 1_000_000_000 if a.workload == "c3" else 100_000_000
     if a.pipeline is None:
         a.pipeline = 0 if a.workload == "c4" else 1
     return a
@@ -115,21 +126,25 @@ def main():
     from zipkin_amd import DepsContext, DeviceColumns, tracegen_params
     from zipkin_amd.shards import allreduce_table, device_view
 
+    c3 = a.workload == "c3"
     S = a.services
     cells = S * S
     # one dedicated stream orders the library's kernels, torch's allocations and RCCL (a handle of
     # 0 -- torch's legacy default stream -- would make the library create an unordered private one)
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
-    from zipkin_amd._abi import table_words
-
-    table = torch.zeros(table_words(S), dtype=torch.int64, device=dev)
-    ctx = DepsContext(S, device=local, stream=stream.cuda_stream, timing=True,
-                      table_ptr=table.data_ptr(), table_bytes=table.numel() * 8, ablate=a.ablate)
+    ctx = DepsContext(S, device=local, stream=stream.cuda_stream, timing=True)
     traces_cap = int(a.records / 15) + 1000
-    p = tracegen_params(a.seed, traces_cap, target_records=a.records, max_depth=a.max_depth, num_services=S,
-                        rank=rank, world=world)
-    cols = DeviceColumns(a.records, device=f"cuda:{local}")
+    if c3:
+        # one global set of a.records records: this rank generates the set's traces of its shard
+        p = tracegen_params(a.seed, traces_cap, target_records=a.records, max_depth=a.max_depth, num_services=S,
+                            rank=rank, world=world, global_ids=True)
+        cap = int(a.records / world * 1.02) + 1_000_000  # shards are hash-balanced (+-0.1 % at 4e7 traces)
+    else:
+        p = tracegen_params(a.seed, traces_cap, target_records=a.records, max_depth=a.max_depth, num_services=S,
+                            rank=rank, world=world)
+        cap = a.records
+    cols = DeviceColumns(cap, device=f"cuda:{local}")
     n, ntr = ctx.tracegen_device(p, cols)
     total_hint = n * world  # records of the whole job per step (exact below, before the timed steps)
     if dist is not None:
@@ -183,13 +198,11 @@ def main():
         # k-1's tail (K2/K3, at N > 1 the all-reduce over RCCL, finalize and status check) completes
         # on the other; every batch is still joined, reduced and finalized inside the timed region
         # (drain() finalizes the last one).
-        sets = [(ctx, table, stream, out)]
+        sets = [(ctx, None, stream, out)]
         for _ in range(a.pipeline):  # a.pipeline batches in flight behind the one being joined
             s2 = torch.cuda.Stream(device=dev)
-            t2 = torch.zeros_like(table)
-            c2 = DepsContext(S, device=local, stream=s2.cuda_stream, timing=False,
-                             table_ptr=t2.data_ptr(), table_bytes=t2.numel() * 8, ablate=a.ablate)
-            sets.append((c2, t2, s2, {k: torch.empty_like(v) for k, v in out.items()}))
+            c2 = DepsContext(S, device=local, stream=s2.cuda_stream, timing=False)
+            sets.append((c2, None, s2, {k: torch.empty_like(v) for k, v in out.items()}))
         state = {"k": 0, "pending": []}
 
         def finalize_oldest():
@@ -288,6 +301,26 @@ def main():
                     raise RuntimeError(f"pipelined step: output '{k}' differs between the table sets")
             c2.close()
 
+    # the finalized table's digest on every rank (all ranks hold the merged job): C3 checks it
+    # against the other ranks and against the G = 1 digest of the same global set
+    digest = table_digest(out)
+    digest_check = None
+    if c3:
+        digests = [digest]
+        if dist is not None:
+            digests = [None] * world
+            dist.all_gather_object(digests, digest)
+        if len(set(digests)) != 1:
+            raise RuntimeError(f"C3: the ranks' finalized tables differ: {digests}")
+        key = f"seed{a.seed}_records{a.records}_S{S}_depth{a.max_depth}"
+        golden = ROOT / "tests" / "golden" / "c3_digest.json"
+        gd = json.loads(golden.read_text()) if golden.exists() else {}
+        want = gd.get(key, {}).get("sha256")
+        if want is not None and want != digest:
+            raise RuntimeError(f"C3 at N = {world}: table digest {digest} != the G = 1 digest {want} ({golden})")
+        digest_check = {"sha256": digest, "ranks_agree": True,
+                        "vs_g1": ("exact" if want == digest else "no G = 1 digest recorded for this set"),
+                        "golden": f"tests/golden/c3_digest.json[{key}]"}
     if debug:
         sums1 = (csum(cols), csum(clustered_cols))
         print(f"[debug] column sums before/after: {sums0 == sums1} {sums0} {sums1}", file=sys.stderr, flush=True)
@@ -311,6 +344,8 @@ def main():
                            "checked": "m0..m4, present and all counters of the shuffled full batch == the clustered batch"}
     if rank == 0 and world == 1 and a.cpu_sample > 0:
         cpu, parity = cpu_baseline(clustered_cols, min(a.cpu_sample, n), S, a.cpu_threads or usable_cpus(), dev)
+    if c3:
+        parity = {"digest": digest_check, "prefix_vs_oracle": parity}
 
     # PMC counters need their own rocprofv3 --pmc run (tools/pmc.sh), so the traffic figure is the
     # builder's measurement of the same kernel on the same workload, labelled with its source
@@ -335,13 +370,17 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": elapsed * 1e3 / a.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if c3 else "weak",
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (zipkin-tracegen-shaped, generated on device)",
             "config": {
-                "workload": "C2: 1e8 span records/GPU, 500 services, dependency link table + Moments"
+                "workload": (f"C3: one global set of {a.records:.3g} span records (BASELINE configs[2]) sharded by "
+                             f"mix64(traceId) % {world} across {world} GPU(s), {S} services, dependency link table + "
+                             "Moments, RCCL SUM all-reduce of the exact table" if c3 else
+                             "C2: 1e8 span records/GPU, 500 services, dependency link table + Moments")
                             + (" (records in random order: device clustering pass in every step)" if shuffled else ""),
+                "total_records": total_records,
                 "records_per_gpu": n,
                 "traces_per_gpu": ntr,
                 "records_per_trace": round(n / max(1, ntr), 2),
@@ -404,6 +443,16 @@ def main():
         dist.destroy_process_group()
 
 
+def table_digest(out) -> str:
+    """SHA-256 of a finalized table (m0 u64, m1..m4 f64, present u8, in that order, cell-major)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for k in ("m0", "m1", "m2", "m3", "m4", "present"):
+        h.update(out[k].cpu().numpy().tobytes())
+    return h.hexdigest()
+
+
 def usable_cpus() -> int:
     """CPUs this process may run on: its affinity mask, capped by a cgroup CPU quota and by the
     thread budget the box exports (OMP_NUM_THREADS), whichever is smallest."""
@@ -444,7 +493,7 @@ def cpu_baseline(cols, sample, S, threads, dev):
     from oracle import oracle
     from zipkin_amd import DepsContext
 
-    host = cols.to_host()
+    host = cols.to_host(sample + 100_000)
     # cut at a trace boundary so the sample is trace-complete
     tid = host.trace_id
     cut = sample

@@ -120,8 +120,11 @@ typedef struct zk_config {
                                     CassieSpanStore.scala:50) */
     uint32_t timing;             /* 1: record per-kernel HIP events (zk_ctx_timing) */
     void*    table;              /* optional caller-owned device buffer for the exact accumulator
-                                    (zk_deps_partial layout, table_bytes >= ZK_TABLE_BYTES(S)): lets
-                                    the host all-reduce it in place with its own RCCL communicator */
+                                    (table_bytes >= ZK_TABLE_BYTES(S)), e.g. to place it in a pool the
+                                    caller manages. It is NOT the exchange buffer: only the buffer
+                                    zk_deps_partial returns may be all-reduced, and
+                                    zk_deps_note_merged overwrites this table from that buffer (an
+                                    all-reduce of the table itself would be lost) */
     uint64_t table_bytes;
     uint32_t reserved[8];
 } zk_config;
@@ -213,7 +216,10 @@ zk_status zk_deps_finalize(zk_ctx* ctx, const zk_link_table* out);
    so every rank reaches the same status (a strict-mode ZK_ERR_NO_SERVICE on one shard fails all
    ranks alike instead of one rank leaving the others blocked in the next collective).
    note_merged without a partial since the last reset/accumulate returns ZK_ERR_INVALID_ARG. The
-   next reset leaves the merged state; an accumulate into a merged table continues the job. */
+   next reset leaves the merged state. An accumulate into a merged table continues the job on THIS
+   rank (finalize then reports the merged job plus the batch), but such a ctx holds the whole job, so
+   zk_deps_partial refuses it (ZK_ERR_INVALID_ARG) until the next reset: exchanging it again would
+   add the job once per rank. */
 #define ZK_TABLE_BYTES(S) ((uint64_t)(S) * (uint64_t)(S) * 128u + 128u)
 #define ZK_XCHG_BYTES(S) ((uint64_t)(S) * (uint64_t)(S) * 96u + 128u)
 zk_status zk_deps_partial(zk_ctx* ctx, void** dev_ptr, uint64_t* bytes);
@@ -222,7 +228,8 @@ zk_status zk_deps_note_merged(zk_ctx* ctx, uint64_t total_records);
 /* ---- synthetic zipkin-tracegen workload (TraceGen.scala:50-143) ------------------------------
  * Counter-based, so host and device produce bit-identical records for the same parameters.
  * Traces are emitted trace-clustered, in TraceGen's own post-order. Sharding: trace k of shard
- * (rank, world) gets a unique traceId whose zk_trace_shard(traceId, world) == rank. */
+ * (rank, world) gets a unique traceId whose zk_trace_shard(traceId, world) == rank (each shard its
+ * own traces), or with global_ids the shards split ONE set of traces by that hash. */
 typedef struct zk_tracegen_params {
     uint64_t seed;
     uint64_t num_traces;      /* traces to generate (upper bound when target_records > 0) */
@@ -232,7 +239,12 @@ typedef struct zk_tracegen_params {
     int64_t  base_ts;         /* "now" in us; traces start 1..8 hours before it */
     uint32_t rank;
     uint32_t world;
-    uint32_t reserved[4];
+    uint32_t global_ids;      /* 1: ONE trace set for every world size (configs[2]): trace k has a
+                                 traceId independent of world, and shard (rank, world) generates only
+                                 the traces of that set with zk_trace_shard(traceId, world) == rank;
+                                 num_traces / target_records then describe the WHOLE set (the cut is
+                                 the same on every rank) and n_records / n_traces the shard's part */
+    uint32_t reserved[3];
 } zk_tracegen_params;
 
 uint32_t  zk_trace_shard(uint64_t trace_id, uint32_t world);

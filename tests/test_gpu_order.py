@@ -205,6 +205,34 @@ def test_every_trace_in_one_sub_bucket(gpu):
     assert_parity(got, st, ref)
 
 
+TRACE_SALT = 0x165667B19E3779F9  # zk_cluster.hip kTraceSalt
+
+
+def test_trace_hash_collisions_fail_with_capacity(gpu):
+    """Crafted traceIds whose trace hash shares bits 40..63 (the bits the trace pass splits its
+    rounds on) overfill the LDS table at every doubling: the pass gives the sub-bucket up after a
+    bounded number of restarts and finalize reports ZK_ERR_CAPACITY, instead of sweeping 2^24 rounds.
+    Honest traceIds of the same batch shape are exact."""
+    S = 5
+    n = 4096  # P3 alone: one sub-bucket of 4096 singleton traces, more than the table's 2048 slots
+    c = SpanColumns.empty(n)
+    c.trace_id[:] = [unmix64(t + 1) ^ TRACE_SALT for t in range(n)]  # trace hash = t + 1 < 2^40
+    c.span_id[:] = np.arange(1, n + 1, dtype=np.uint64)
+    c.first_ts[:] = 1_000
+    c.last_ts[:] = 2_000
+    from tests.test_gpu_parity import SERVER
+
+    c.flags[:] = SERVER
+    with DepsContext(S) as ctx:
+        ctx.accumulate(c.take(np.random.default_rng(3).permutation(n)), verify=False)
+        with pytest.raises(ZkError) as e:
+            ctx.finalize()
+        assert e.value.status == _abi.ZK_ERR_CAPACITY
+    c.trace_id[:] = np.random.default_rng(4).integers(1, 2**63, n, dtype=np.uint64)
+    got, st = run([c], S)
+    assert_parity(got, st, oracle.aggregate(c, S))
+
+
 def test_shuffled_c2_shape_at_scale(gpu):
     """2e7 device-generated TraceGen records (the bench's shape), shuffled on the device: the result
     equals the clustered batch's bit for bit (m0..m4 and every counter)."""

@@ -179,5 +179,12 @@ def test_accumulate_into_merged_table_keeps_the_job_counters(gpu):
         st = sh.ctx.stats()
         assert st["records"] == len(a) + len(b)
         assert_parity(got, st, oracle.aggregate(SpanColumns.concat([a, b]), S))
+        # this ctx now holds the whole job: a second exchange would add it once per rank
+        with pytest.raises(ZkError) as e:
+            sh.ctx.partial()
+        assert e.value.status == _abi.ZK_ERR_INVALID_ARG
+        sh.ctx.reset()  # a reset starts a fresh shard that may be exchanged again
+        sh.ctx.accumulate(b)
+        sh.ctx.partial()
     finally:
         sh.close()

@@ -156,6 +156,13 @@ def test_exchange_form_bounds_and_linearity():
     x = table.encode_exchange({(0, 1): big}, 2)
     assert table.decode_exchange(x, 2) == {(0, 1): big}
     assert np.array_equal(table.unpack(table.pack(table.encode({(0, 1): big}, 2), 2), 2), table.encode({(0, 1): big}, 2))
+    # the tightest limb is S2's top one (bits 56..111 of a value below 2^112: up to 2^56 - 1): 256
+    # copies of the largest cell still sum without a carry out of any u64 limb, and decode exactly
+    xc = table.encode_exchange_cell(*big)
+    assert int(xc[4]) < 1 << 56 and int(xc[4]) > (1 << 55)  # S2's top limb really is near 2^56
+    summed = [sum(int(v) for _ in range(256)) for v in xc]
+    assert max(summed) < 1 << 64
+    assert table.decode_exchange_cell(summed) == tuple(256 * v for v in big)
     # 256 ranks each holding 1/256 of the job: every limb of the sum stays below 2^64
     share = tuple(v // 256 for v in big)
     cell = table.encode_exchange_cell(*share).astype(object)

@@ -48,3 +48,32 @@ def test_shards_are_disjoint_and_owned():
         ids.append(u)
     allids = np.concatenate(ids)
     assert len(np.unique(allids)) == len(allids)
+
+
+def _rows(c):
+    return np.stack([c.trace_id, c.span_id, c.parent_id, c.first_ts.view(np.uint64), c.last_ts.view(np.uint64),
+                     c.service_id.astype(np.uint64), c.flags.astype(np.uint64)], 1)
+
+
+def test_global_set_is_the_same_for_every_world():
+    """global_ids (configs[2]): one trace set, cut at the same record target for every world size;
+    shard r of world G holds exactly the set's traces whose zk_trace_shard(traceId, G) == r, each
+    trace whole and trace-clustered, and the shards together are the G = 1 set."""
+    kw = dict(max_depth=6, num_services=100, target_records=40_000, global_ids=True)
+    one = tracegen_host(seed=7, num_traces=5_000, **kw)
+    assert 0 < len(one) <= 40_000
+    ref = _rows(one)
+    ref = ref[np.lexsort(ref.T[::-1])]
+    for world in (2, 3, 4, 8):
+        parts = [tracegen_host(seed=7, num_traces=5_000, rank=r, world=world, **kw) for r in range(world)]
+        for r, p in enumerate(parts):
+            u = np.unique(p.trace_id)
+            assert all(trace_shard(int(t), world) == r for t in u[:50])
+            change = np.flatnonzero(np.diff(p.trace_id.view(np.int64)) != 0)
+            assert len(change) + 1 == len(u)  # every trace one contiguous run
+        got = np.concatenate([_rows(p) for p in parts])
+        got = got[np.lexsort(got.T[::-1])]
+        assert np.array_equal(got, ref)
+    # at world 1 the global set is the per-shard set (the same traceIds): C2 and C3 agree at G = 1
+    assert np.array_equal(tracegen_host(seed=7, num_traces=5_000, max_depth=6, num_services=100,
+                                        target_records=40_000).trace_id, one.trace_id)

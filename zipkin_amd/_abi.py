@@ -155,7 +155,8 @@ class zk_tracegen_params(C.Structure):
         ("base_ts", C.c_int64),
         ("rank", C.c_uint32),
         ("world", C.c_uint32),
-        ("reserved", C.c_uint32 * 4),
+        ("global_ids", C.c_uint32),
+        ("reserved", C.c_uint32 * 3),
     ]
 
 

@@ -95,10 +95,12 @@ class DeviceColumns:
             getattr(d, k).copy_(t)
         return d
 
-    def to_host(self) -> SpanColumns:
+    def to_host(self, n: int | None = None) -> SpanColumns:
+        """The first n records (default: all) as host columns."""
+        n = self.n if n is None else min(n, self.n)
         out = []
         for k, dt in COLUMNS:
-            t = getattr(self, k)[: self.n].cpu().numpy()
+            t = getattr(self, k)[:n].cpu().numpy()
             out.append(t.view(dt))
         return SpanColumns(*out)
 
@@ -113,6 +115,7 @@ def tracegen_params(
     base_ts: int = 1_421_053_208_373_000,
     rank: int = 0,
     world: int = 1,
+    global_ids: bool = False,
 ) -> _abi.zk_tracegen_params:
     p = _abi.zk_tracegen_params()
     p.seed = seed
@@ -123,6 +126,7 @@ def tracegen_params(
     p.base_ts = base_ts
     p.rank = rank
     p.world = world
+    p.global_ids = 1 if global_ids else 0
     return p
 
 

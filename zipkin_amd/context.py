@@ -56,7 +56,6 @@ class DepsContext:
         timing: bool = False,
         table_ptr: int = 0,
         table_bytes: int = 0,
-        ablate: int = 0,
     ):
         self._L = _abi.lib()
         cfg = _abi.zk_config()
@@ -68,7 +67,6 @@ class DepsContext:
         cfg.timing = 1 if timing else 0
         cfg.table = table_ptr or None
         cfg.table_bytes = table_bytes
-        cfg.reserved[0] = ablate  # diagnostic builds only (1: join without emitting links)
         h = C.c_void_p()
         st = self._L.zk_ctx_create(C.byref(cfg), C.byref(h))
         if st != _abi.ZK_OK:

@@ -30,7 +30,6 @@ struct zk_ctx {
     bool strict = true;
     uint32_t max_trace = 131072;
     bool timing = false;
-    uint32_t ablate = 0;
     uint64_t* table = nullptr;            // S*S*kLimbs
     bool own_table = true;
     unsigned long long* stats = nullptr;  // kStatShards*ST_N
@@ -61,6 +60,7 @@ struct zk_ctx {
     void* fin_stage = nullptr;
     uint64_t records_since_reset = 0;
     bool merged = false;                  // the table holds the all-reduced job (zk_deps_note_merged)
+    bool continued = false;               // a batch was accumulated into a merged table since the reset
     uint64_t* xchg = nullptr;             // packed exchange form of the table (zk_deps_partial)
     bool folded = false;                  // zk_deps_partial folded this ctx's counters into the table tail
                                           // since the last reset / accumulate (note_merged requires it)
@@ -248,7 +248,7 @@ zk_status cluster_batch(zk_ctx* c, SpanColsDev* d) {
     const SpanColsMut A = carve_cols(c->cl_cols, n);
     const SpanColsMut B = carve_cols(c->cl_cols + carved_bytes(n), n);
     int res = 0;
-    ZK_HIP(c, launch_cluster(plan, *d, A, B, c->cl_temp, c->cus, c->stream, &res));
+    ZK_HIP(c, launch_cluster(plan, *d, A, B, c->cl_temp, c->cus, c->stream, &res, c->stats + ST_SPILL_OVERFLOW));
     const SpanColsMut& m = res ? B : A;
     *d = SpanColsDev{m.trace_id, m.span_id, m.parent_id, m.first_ts, m.last_ts, m.service_id, m.flags, n};
     return ZK_OK;
@@ -338,7 +338,6 @@ zk_status zk_ctx_create(const zk_config* cfg, zk_ctx** out) {
     c->timing = cfg->timing != 0;
     c->cus = prop.multiProcessorCount > 0 ? (uint32_t)prop.multiProcessorCount : 256;
     bucket_geometry(c->S, &c->nb, &c->cb_shift);
-    c->ablate = cfg->reserved[0];  // diagnostic ablation switch, never set by the product
     if (cfg->max_trace_records) c->max_trace = cfg->max_trace_records;
     zk_status st = ZK_OK;
     hipError_t e = hipSetDevice(c->device);
@@ -425,6 +424,7 @@ zk_status zk_deps_reset(zk_ctx* c) {
     c->tset_records = 0;
     c->records_since_reset = 0;
     c->merged = false;
+    c->continued = false;
     c->folded = false;
     return ZK_OK;
 }
@@ -451,6 +451,7 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
         ZK_HIP(c, hipMemcpyAsync(c->stats, c->table + (uint64_t)c->S * c->S * kLimbs, kTableTailBytes,
                                  hipMemcpyDeviceToDevice, c->stream));
         c->merged = false;
+        c->continued = true;
     }
     c->folded = false;  // the tail no longer holds this ctx's counters once the batch lands
     SpanColsDev d{cols->trace_id, cols->span_id, cols->parent_id, cols->first_ts,
@@ -529,7 +530,6 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
     a.spill_scratch = c->spill_scratch;
     a.spill_scratch_stride = c->spill_stride;
     a.max_trace = c->max_trace;
-    a.ablate = c->ablate;
     a.links = c->links;
     a.link_count = c->link_count;
     a.link_stride = stride;
@@ -637,7 +637,9 @@ zk_status zk_deps_finalize(zk_ctx* c, const zk_link_table* out) {
     if (st != ZK_OK) return st;
     if (s[ST_TOO_LARGE]) return fail(c, ZK_ERR_TRACE_TOO_LARGE, "trace longer than max_trace_records skipped");
     if (s[ST_SPILL_OVERFLOW])
-        return fail(c, ZK_ERR_CAPACITY, "spill list overflow");
+        return fail(c, ZK_ERR_CAPACITY,
+                    "device capacity exceeded: spill list overflow, or a clustering sub-bucket whose traceIds "
+                    "collide in every hash bit the trace pass splits on");
     if (s[ST_NOT_CLUSTERED])
         return fail(c, ZK_ERR_NOT_CLUSTERED, "a trace was split into non-adjacent runs or over two batches");
     if (s[ST_SVC_RANGE]) return fail(c, ZK_ERR_SERVICE_RANGE, "record with service_id >= num_services");
@@ -689,6 +691,9 @@ zk_status zk_ctx_timing(zk_ctx* c, zk_timing* out) {
 
 zk_status zk_deps_partial(zk_ctx* c, void** dev_ptr, uint64_t* bytes) {
     if (!c || !dev_ptr || !bytes) return ZK_ERR_INVALID_ARG;
+    // a ctx that continued a merged job holds the whole job: a second exchange would add it once per rank
+    if (c->continued)
+        return fail(c, ZK_ERR_INVALID_ARG, "zk_deps_partial after accumulating into a merged table (reset first)");
     ZK_HIP(c, hipSetDevice(c->device));
     if (!c->merged)  // a merged tail already holds the job-wide counters
         ZK_HIP(c, launch_stats_fold(c->stats, (unsigned long long*)(c->table + (uint64_t)c->S * c->S * kLimbs),
@@ -749,7 +754,10 @@ zk_status zk_tracegen_device(zk_ctx* c, const zk_tracegen_params* p, const zk_sp
         p->num_services == 0 || (p->world && p->rank >= p->world))
         return fail(c, ZK_ERR_INVALID_ARG, "bad tracegen arguments");
     ZK_HIP(c, hipSetDevice(c->device));
-    ZK_HIP(c, launch_tracegen(p, out, cap, n_records, n_traces, c->stream));
+    const hipError_t e = launch_tracegen(p, out, cap, n_records, n_traces, c->stream);
+    if (e == hipErrorInvalidValue && p->global_ids)
+        return fail(c, ZK_ERR_CAPACITY, "the shard's part of the global trace set exceeds the output capacity");
+    ZK_HIP(c, e);
     return ZK_OK;
 }
 

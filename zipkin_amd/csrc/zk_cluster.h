@@ -27,7 +27,8 @@ ClusterPlan cluster_plan(uint64_t n, uint32_t cus);
 uint64_t cluster_scratch_bytes(const ClusterPlan& p);
 // in (any order) -> trace-clustered columns in A (*result = 0) or B (*result = 1); both hold n records
 hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const SpanColsMut& A, const SpanColsMut& B,
-                          void* scratch, uint32_t cus, hipStream_t s, int* result);
+                          void* scratch, uint32_t cus, hipStream_t s, int* result,
+                          unsigned long long* capacity_fail);
 // insert the traceId of every segment start into `set` (slots: power of two; slot `slots` counts
 // traceId 0); *dup += segments whose traceId was already present
 hipError_t launch_trace_set_insert(const uint64_t* trace_id, uint64_t n, uint64_t* set, uint64_t slots,

@@ -770,7 +770,14 @@ struct TraceArgs {
     const uint32_t* sub;  // nsub + 1 sub-bucket bounds
     uint32_t nsub;
     unsigned int* next;   // work counter: sub-buckets are handed out one at a time
+    unsigned long long* fail;  // sub-buckets given up (ST_SPILL_OVERFLOW: finalize -> ZK_ERR_CAPACITY)
 };
+// A round that overflows the LDS table restarts its sub-bucket with twice the rounds. Rounds split
+// traces on bits 40.. of the trace hash, so traceIds crafted to share those bits (mix64 is invertible)
+// would overflow at every doubling: after kTrMaxDoublings the sub-bucket is given up and counted
+// (finalize fails with ZK_ERR_CAPACITY instead of the pass sweeping 2^24 rounds). Honest data needs
+// no doubling: a round's expected records are <= kTrSlots / 2 and its distinct traces fewer still.
+constexpr uint32_t kTrMaxDoublings = 6;
 
 __device__ __forceinline__ uint64_t trace_hash(uint64_t tid) { return zk_mix64(tid ^ kTraceSalt); }
 
@@ -880,6 +887,7 @@ __global__ __launch_bounds__(kTrWG) void k_cl_traces(TraceArgs a) {
         // (a round's distinct traceIds are at most its records)
         uint32_t rounds = 1;
         while (len / rounds > kTrSlots / 2) rounds <<= 1;
+        uint32_t doublings = 0;
         uint32_t slots = 64;
         while (slots < 2 * (len / rounds + 1) && slots < kTrSlots) slots <<= 1;
         uint32_t smask = slots - 1;
@@ -924,6 +932,11 @@ __global__ __launch_bounds__(kTrWG) void k_cl_traces(TraceArgs a) {
             }
             __syncthreads();
             if (s_fail) {
+                if (++doublings > kTrMaxDoublings || rounds >= (1u << 24)) {
+                    // colliding traceIds: give the sub-bucket up (its output rows stay unwritten)
+                    if (t == 0) atomicAdd(a.fail, 1ull);
+                    break;
+                }
                 // start the sub-bucket over with twice the rounds (every output position of the
                 // sub-bucket is rewritten by the new layout)
                 rounds <<= 1;
@@ -1105,7 +1118,8 @@ uint64_t cluster_scratch_bytes(const ClusterPlan& p) {
 }
 
 hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const SpanColsMut& A, const SpanColsMut& B,
-                          void* scratch, uint32_t cus, hipStream_t s, int* result) {
+                          void* scratch, uint32_t cus, hipStream_t s, int* result,
+                          unsigned long long* capacity_fail) {
     const uint64_t n = in.n;
     *result = 0;
     if (n == 0) return hipSuccess;
@@ -1133,6 +1147,7 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
     };
     TraceArgs ta{};
     ta.next = next;
+    ta.fail = capacity_fail;
     if (!p.b1) {  // P3 alone: in -> A
         const uint32_t h_sub[2] = {0u, (uint32_t)n};
         e = hipMemcpyAsync(sub, h_sub, 8, hipMemcpyHostToDevice, s);

@@ -5,11 +5,14 @@
 // ZipkinAggregateJob.scala:39-43 (`.group.sum` / `.sum` across reducers) that is 32 MB at S = 500.
 // zk_deps_partial instead carry-normalises every cell into 56-bit limbs -- m0 one, S1 two, S2 two,
 // S3 three, S4 four: 12 u64 = 96 B per cell, 24 MB at S = 500 -- each < 2^56 except a sum's top limb,
-// which holds that sum's bits above the others (S1 < 2^72, S2 < 2^112, S3 < 2^152, S4 < 2^192 with
-// fewer than 2^32 records since reset and d < 2^40 us). A SUM all-reduce over up to 256 ranks
-// therefore never carries out of a limb (256 x 2^56 = 2^64, and every top limb is far below 2^56
-// for its sum's bound), and zk_deps_note_merged rebuilds the exact sums from the summed limbs and
-// writes them back into the accumulator in its own chunk layout.
+// which holds that sum's bits above the others. With fewer than 2^32 records since reset and
+// d < 2^40 us: S1 < 2^72 (top limb < 2^16), S2 < 2^112 (top limb = bits 56..111: up to 2^56 - 1, the
+// tightest), S3 < 2^152 (top limb = bits 112..151 < 2^40), S4 < 2^192 (top limb = bits 168..191 <
+// 2^24). Every limb is therefore <= 2^56 - 1 and a SUM all-reduce over up to 256 ranks never carries
+// out of a u64 (256 x (2^56 - 1) < 2^64) -- 256 ranks is the hard limit, set by S2's top limb and by
+// every low limb alike (tests/test_multirank.py sums 256 copies of the largest cell). zk_deps_note_merged
+// rebuilds the exact sums from the summed limbs and writes them back into the accumulator in its own
+// chunk layout.
 #include "zk_internal.h"
 #include "zk_launch.h"
 

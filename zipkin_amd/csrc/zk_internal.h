@@ -95,7 +95,6 @@ struct JoinArgs {
     uint8_t* spill_scratch;
     uint64_t spill_scratch_stride;  // bytes per WG
     uint32_t max_trace;             // records
-    uint32_t ablate;                // diagnostic builds only: 1 = join but do not emit links
     // per-tile link lists written by K1: tile t's links at links[t*link_stride ...], link_count[t]
     uint64_t* links;                // (cell << 40) | duration
     uint32_t* link_count;

@@ -26,14 +26,6 @@
 #ifndef ZK_K1_WGS_PER_CU
 #define ZK_K1_WGS_PER_CU 4  // resident K1 workgroups per CU (one wave per SIMD each)
 #endif
-// A/B variant of the north star's sorted-segment design (not the product): instead of the LDS hash,
-// every record ranks itself inside its trace segment by (spanId, index) -- a rank sort, so the
-// segment's records land in s_perm in sorted order and the first of equal spanIds is the merge
-// leader -- and a child finds its parent by binary search over the sorted segment.
-#ifndef ZK_K1_SORTJOIN
-#define ZK_K1_SORTJOIN 0
-#endif
-
 namespace zk {
 namespace {
 
@@ -189,13 +181,15 @@ constexpr int kSlotA = 12;
 constexpr int kSlotB = 16;
 constexpr uint32_t kSlotP1 = 1u << 20;
 constexpr uint32_t kSlotP0 = 1u << 21;
-// ZK_K1_SEG_IN_SLOT: bits 22..30 of the slot word hold the leader's trace segment (< 512), so a probe
-// compares the segment from the word it already read and loads the occupant's spanId only on a
-// segment match (no s_seg array: one LDS round trip less per parent probe)
-#ifndef ZK_K1_SEG_IN_SLOT
-#define ZK_K1_SEG_IN_SLOT 1
-#endif
+// bits 22..30 of the slot word: the leader's trace segment (< 512)
 constexpr int kSlotSegShift = 22;
+// bit 31: the window's epoch (alternating). ZK_K1_EPOCH: a slot holding the other epoch is stale --
+// its leader of the window before empties it (CAS of its final word -> 0) -- and an inserter claims
+// it like an empty slot, so the window needs no barrier between the slot clears and the inserts.
+#ifndef ZK_K1_EPOCH
+#define ZK_K1_EPOCH 1
+#endif
+constexpr uint32_t kSlotEpoch = ZK_K1_EPOCH ? 1u << 31 : 0u;
 
 // own bits of a fragment and the "seen exactly once" core annotations it may promote to ">= 2":
 // the four 2-bit counts of cs|cr|sr|ss (bits 8..15) give ">= 1" (either bit) and ">= 2" (the high
@@ -215,26 +209,19 @@ __device__ __forceinline__ uint32_t frag_bits(uint32_t f, uint32_t* once) {
 }
 __device__ __forceinline__ bool slot_valid(uint32_t w) { return ((w >> kSlotB) & 0xFu) == 0u; }
 
-// two consecutive elements starting at i (i even, columns 16-byte aligned); zeros past `lim`
 // Two consecutive elements starting at i (i even), RAW: elements at or past `lim` are garbage and
 // every consumer masks by record index. Branch-free and unmasked on purpose: a conditional tail
 // load, or a select right after the load, makes the compiler wait (vmcnt) for the load at once,
 // which serialises the column loads and defeats the prefetch. Index i < lim reads the aligned pair
 // at i (columns are 16-B / 8-B aligned, so the pair never crosses a page even when i + 1 == lim);
 // i >= lim reads pair 0.
-// ZK_K1_HOTREAD (diagnostic builds only, results wrong): every column load is redirected into the
-// first 2^16 records, which stay in L2 -- K1's time without HBM, to split compute from streaming
-#ifndef ZK_K1_HOTREAD
-#define ZK_K1_HOTREAD 0
-#endif
-__device__ __forceinline__ uint64_t hot_index(uint64_t i) { return ZK_K1_HOTREAD ? (i & 0xFFFEull) : i; }
 __device__ __forceinline__ void ld2_u64(const uint64_t* __restrict__ p, uint64_t i, uint64_t lim, uint64_t v[2]) {
-    const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(p + hot_index(i < lim ? i : 0));
+    const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(p + (i < lim ? i : 0));
     v[0] = x.x;
     v[1] = x.y;
 }
 __device__ __forceinline__ void ld2_u32(const uint32_t* __restrict__ p, uint64_t i, uint64_t lim, uint32_t v[2]) {
-    const uint2 x = *reinterpret_cast<const uint2*>(p + hot_index(i < lim ? i : 0));
+    const uint2 x = *reinterpret_cast<const uint2*>(p + (i < lim ? i : 0));
     v[0] = x.x;
     v[1] = x.y;
 }
@@ -298,10 +285,15 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {  // set bits of m 
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+struct Window {  // two consecutive records per thread
+    uint64_t tid[2], sid[2], pid[2], first[2], last[2];
+    uint32_t svc[2], flags[2];
+    uint64_t prev;  // traceId of the record before this wave's first record
+};
+
 // boundary ballots of a window starting at ws with wn records: ev bit t = record 2t starts a trace,
 // od bit t = record 2t+1 does (this wave's lanes)
-template <class Win>
-__device__ __forceinline__ void window_ballots(const Win& w, uint64_t ws, int wn, uint64_t* ev, uint64_t* od) {
+__device__ __forceinline__ void window_ballots(const Window& w, uint64_t ws, int wn, uint64_t* ev, uint64_t* od) {
     const int t = threadIdx.x, lane = t & 63;
     uint64_t prev = lane_shr1(w.tid[1]);
     if (lane == 0) prev = (ws + 2 * t > 0) ? w.prev : ~w.tid[0];
@@ -311,76 +303,18 @@ __device__ __forceinline__ void window_ballots(const Win& w, uint64_t ws, int wn
     *od = __ballot(b1);
 }
 
-struct Window {  // two consecutive records per thread
-    uint64_t tid[2], sid[2], pid[2], first[2], last[2];
-    uint32_t svc[2], flags[2];
-    uint64_t prev;  // traceId of the record before this wave's first record
-};
-
-template <bool JOIN>
-__device__ __forceinline__ void load_window(const JoinArgs& a, uint64_t ws, Window& w) {
-    const uint64_t n = a.c.n;
-    const uint64_t i = ws + 2 * threadIdx.x;
-    ld2_u64(a.c.trace_id, i, n, w.tid);
-    ld2_u64(a.c.span_id, i, n, w.sid);
-    if constexpr (JOIN) {
-        ld2_u64(a.c.parent_id, i, n, w.pid);
-    } else {  // sketch-only pass: parentId is not read (40 B per record)
-        w.pid[0] = w.pid[1] = 0ull;
-    }
-    ld2_u64((const uint64_t*)a.c.first_ts, i, n, w.first);
-    ld2_u64((const uint64_t*)a.c.last_ts, i, n, w.last);
-    ld2_u32(a.c.service_id, i, n, w.svc);
-    ld2_u32(a.c.flags, i, n, w.flags);
-    // traceId before the pair (only lane 0's is used); unconditional for the same reason as ld2
-    w.prev = a.c.trace_id[(i > 0 && i - 1 < n) ? i - 1 : 0];
-}
-
-// ZK_K1_LATE (default): only the traceIds (what the boundary phase needs) are prefetched a window
-// ahead; the other five columns of a window are loaded at the top of its own iteration and arrive
-// during the boundary phases (26 -> 6 registers of prefetch, 120 -> 100 VGPRs). Same box,
-// interleaved, serial steps (profiles/r02/ab_late.txt): K1 1.251 -> 1.227 ms; with the freed
-// registers spent on a fifth workgroup per CU (hash factor 4 to fit the LDS): 1.233 ms.
-#ifndef ZK_K1_LATE
-#define ZK_K1_LATE 1
-#endif
-// ZK_K1_EARLY_BALLOT: take the next window's boundary ballots at the end of this window, before its
-// link stores (see the loop)
-#ifndef ZK_K1_EARLY_BALLOT
-#define ZK_K1_EARLY_BALLOT 1
-#endif
-// ZK_K1_ATOMIC_APPEND: waves claim their slice of the link list with an LDS atomic, so the window
-// needs no link-append barrier (3 barriers per window instead of 4); hash slots are emptied one
-// window later
-#ifndef ZK_K1_ATOMIC_APPEND
-#define ZK_K1_ATOMIC_APPEND 1
-#endif
-// ZK_K1_FAST_SCAN: skip the search for the window's first own trace start and for the range end
-// when the window before already found them (see phase 2)
-#ifndef ZK_K1_FAST_SCAN
-#define ZK_K1_FAST_SCAN 1
-#endif
-// ZK_K1_SLOT16: 16-byte hash slots {spanId, slot word, merged service key}: a parent probe reads
-// the parent's spanId, validity bits and service in ONE ds_read_b128 (the slot word alone needed two
-// more dependent reads: the occupant's spanId and its service). 2 x TILE slots (16 KB, the LDS of the
-// 8 x TILE u32 table); the service key array goes.
-#ifndef ZK_K1_SLOT16
-#define ZK_K1_SLOT16 0
-#endif
-// ZK_K1_EARLY_COLS: four of the six late columns loaded a phase earlier (see load_early)
-#ifndef ZK_K1_EARLY_COLS
-#define ZK_K1_EARLY_COLS 1
-#endif
+// Column loads of a window, in three groups issued at different points of the loop (round 2,
+// profiles/r02/ab_late.txt, ab_early_cols.txt): the traceIds (what the boundary phase needs) a
+// whole window ahead; spanId, first/last and service right after the window before passed its
+// merge barrier (phase 6 no longer reads them); parentId and flags at the top of the window's own
+// iteration. 26 -> 6 registers of prefetch against loading everything a window ahead (120 -> 101
+// VGPRs, K1 1.251 -> 1.227 -> 1.160 ms).
 __device__ __forceinline__ void load_tid(const JoinArgs& a, uint64_t ws, Window& w) {
     const uint64_t n = a.c.n;
     const uint64_t i = ws + 2 * threadIdx.x;
     ld2_u64(a.c.trace_id, i, n, w.tid);
-    w.prev = a.c.trace_id[hot_index((i > 0 && i - 1 < n) ? i - 1 : 0)];
+    w.prev = a.c.trace_id[(i > 0 && i - 1 < n) ? i - 1 : 0];
 }
-// ZK_K1_EARLY_COLS: the columns phase 6 no longer reads (spanId, first, last, service) are loaded
-// for the next window right after this window's merge barrier, into the same registers; only
-// parentId and flags stay at the top of the next iteration
-template <bool JOIN>
 __device__ __forceinline__ void load_early(const JoinArgs& a, uint64_t ws, Window& w) {
     const uint64_t n = a.c.n;
     const uint64_t i = ws + 2 * threadIdx.x;
@@ -395,24 +329,9 @@ __device__ __forceinline__ void load_late(const JoinArgs& a, uint64_t ws, Window
     const uint64_t i = ws + 2 * threadIdx.x;
     if constexpr (JOIN) {
         ld2_u64(a.c.parent_id, i, n, w.pid);
-    } else {
+    } else {  // sketch-only pass: parentId is not read (40 B per record)
         w.pid[0] = w.pid[1] = 0ull;
     }
-    ld2_u32(a.c.flags, i, n, w.flags);
-}
-template <bool JOIN>
-__device__ __forceinline__ void load_rest(const JoinArgs& a, uint64_t ws, Window& w) {
-    const uint64_t n = a.c.n;
-    const uint64_t i = ws + 2 * threadIdx.x;
-    ld2_u64(a.c.span_id, i, n, w.sid);
-    if constexpr (JOIN) {
-        ld2_u64(a.c.parent_id, i, n, w.pid);
-    } else {
-        w.pid[0] = w.pid[1] = 0ull;
-    }
-    ld2_u64((const uint64_t*)a.c.first_ts, i, n, w.first);
-    ld2_u64((const uint64_t*)a.c.last_ts, i, n, w.last);
-    ld2_u32(a.c.service_id, i, n, w.svc);
     ld2_u32(a.c.flags, i, n, w.flags);
 }
 
@@ -423,52 +342,36 @@ __device__ __forceinline__ void load_rest(const JoinArgs& a, uint64_t ws, Window
 // through them in windows of TILE records (two per thread, 16-byte column loads): the trace
 // boundaries of the window come from a ballot bitmask; the complete traces of the window are
 // merged, validated and joined in LDS; the incomplete last trace starts the next window (its
-// records are re-read, mostly from L2). The next window's columns are prefetched into registers
-// right after its start is known, so HBM streams while the LDS phases run. A trace longer than a
-// window goes to the spill kernel. Four workgroups per CU (<= 32 KB LDS, <= 128 VGPRs).
+// records are re-read, mostly from L2). The next window's columns are prefetched into registers,
+// so HBM streams while the LDS phases run. A trace longer than a window goes to the spill kernel.
+// Four workgroups per CU (<= 40 KB LDS, <= 128 VGPRs). Three barriers per window: boundaries,
+// staging, merge; waves claim their slice of the link list with one LDS atomic (no append barrier),
+// and hash slots are emptied one window later by their leaders.
 //
 // Hash slot word (u32): bits 0..10 leader index + 1; bits 12..15 "seen >= 1" and 16..19
 // "seen >= 2" for cs, cr, sr, ss (Span.isValid = no ">= 2" bit); bit 20 some fragment has a
-// parentId, bit 21 some fragment has none.
+// parentId, bit 21 some fragment has none; bits 22..30 the leader's trace segment, so a probe
+// compares the segment from the word it read and loads the occupant's spanId only on a match.
 // =============================================================================================
 // MODE bits: kModeJoin = the dependency path (parent join, links); kModeEmit = one sketch item
 // per merged valid span with a service (zk_rt.hip). The product dependency pass is kModeJoin.
 constexpr int kModeJoin = 1;
 constexpr int kModeEmit = 2;
-template <int TILE, int WG, int ABL, int MODE>
+template <int TILE, int WG, int MODE>
 // launch bounds: minimum waves per SIMD = resident workgroups per CU x waves per workgroup / 4 SIMDs
 __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_stream(JoinArgs a) {
-    constexpr int H = ZK_K1_SORTJOIN ? 64 : ZK_K1_SLOT16 ? 2 * TILE : ZK_HASH_FACTOR * TILE;  // load <= 1/16 (distinct spans / slots): short probe chains, since a wave waits for its longest
+    constexpr int H = ZK_HASH_FACTOR * TILE;  // load <= 1/16 (distinct spans / slots): short probe chains, since a wave waits for its longest
     constexpr int NWORD = TILE / 64;
-    static_assert(TILE == 2 * WG && TILE <= 2047, "two records per thread");
+    static_assert(TILE == 2 * WG && TILE <= 512, "two records per thread; the segment field of the slot word is 9 bits");
     __shared__ __align__(16) uint64_t s_sid[TILE];
     __shared__ __align__(16) long long s_first[TILE];
     __shared__ __align__(16) long long s_last[TILE];
     __shared__ __align__(16) uint64_t s_pid[TILE];
-#if !ZK_K1_SLOT16
     __shared__ __align__(16) uint32_t s_svck[TILE];
-#endif
-#if ZK_K1_SORTJOIN || !ZK_K1_SEG_IN_SLOT
-    __shared__ __align__(16) uint16_t s_seg[TILE];
-#endif
-    static_assert(!ZK_K1_SEG_IN_SLOT || TILE <= 512, "the segment field of the slot word is 9 bits");
-#if ZK_K1_SLOT16
-    __shared__ __align__(16) uint4 s_h16[H];  // {spanId lo, spanId hi, slot word, service key}
-#define ZK_HMETA(x) (&s_h16[x].z)
-#define ZK_HSVC(L, x) (&s_h16[x].w)
-#else
     __shared__ __align__(16) uint32_t s_ht[H];
-#define ZK_HMETA(x) (&s_ht[x])
-#define ZK_HSVC(L, x) (&s_svck[L])
-#endif
-#if ZK_K1_SORTJOIN
-    __shared__ __align__(16) uint32_t s_bits[TILE];  // merged seen-once/twice + parent bits per leader
-    __shared__ __align__(16) uint16_t s_perm[TILE];  // segment records in (spanId, index) order
-#endif
     __shared__ __align__(16) uint64_t s_mask[NWORD];
     __shared__ uint32_t s_stat[ST_N];
-    __shared__ uint32_t s_wsum[WG / 64];
-    __shared__ uint64_t s_cursor;  // ZK_K1_ATOMIC_APPEND: links (low 32) and items (high 32) appended
+    __shared__ uint64_t s_cursor;  // links (low 32) and sketch items (high 32) appended so far
     __shared__ uint32_t s_hist[kMaxBuckets];  // links per cell bucket (K2's scatter offsets)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -484,29 +387,10 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     }
     const uint64_t R1 = (R0 + a.per_wg < n) ? R0 + a.per_wg : n;
     uint64_t* __restrict__ out = a.links + (uint64_t)blockIdx.x * a.link_stride;
-#ifndef ZK_K1_TRASH_SPREAD
-#define ZK_K1_TRASH_SPREAD 0
-#endif
-#ifndef ZK_K1_OOB_STORE
-#define ZK_K1_OOB_STORE 0
-#endif
-#if ZK_K1_TRASH_SPREAD
-    // absent links go to a per-thread trash slot at the end of the list (join_geometry reserves TILE)
-    const uint64_t trash = a.link_stride - TILE + 2 * tid;
-#else
     const uint64_t trash = a.link_stride - 1;  // never a real link slot (join_geometry)
-#endif
-#if ZK_K1_OOB_STORE
-    // the link list as a buffer: an absent link is stored at an offset past num_records, which the
-    // hardware drops -- still exactly two stores per thread per window, no trash traffic
-    const __amdgpu_buffer_rsrc_t out_rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)out, (short)0, (int)((a.link_stride - 1) * 8), 0x00020000);
-#endif
     uint64_t* __restrict__ it_pay = a.rt_pay + (uint64_t)blockIdx.x * a.link_stride;
     uint32_t* __restrict__ it_svc = a.rt_svc + (uint64_t)blockIdx.x * a.link_stride;
-    uint32_t nitem = 0;       // sketch items written by this workgroup (uniform)
-    uint32_t nout = 0;        // links written by this workgroup (uniform)
-    uint64_t nrec = 0;        // records aggregated (uniform)
+    uint64_t nrec = 0;  // records aggregated (uniform)
     StatPack st;
     int fold_in = kFoldWindows;  // windows until the next stat fold (uniform)
     if (tid < ST_N) s_stat[tid] = 0u;
@@ -514,48 +398,27 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     for (uint32_t x = tid; x < a.nb; x += WG) s_hist[x] = 0u;
     constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
     uint32_t r_clear[2] = {kNoSlot, kNoSlot};  // hash slots this thread's leaders of the last window hold
+    uint32_t r_cword[2] = {0u, 0u};            // ... and the final words in them (read in phase 6)
+    uint32_t epoch = 0u;                       // this window's epoch bit (alternates)
 
     uint64_t ws = R0;         // window start (even)
     uint64_t seek = R0;       // first record that may start one of our traces
     bool seek_start = false;  // seek is known to be a trace start (uniform)
     Window cur, nxt;
     constexpr bool JOIN = (MODE & kModeJoin) != 0, EMIT = (MODE & kModeEmit) != 0;
-    constexpr bool EC = ZK_K1_EARLY_COLS && ZK_K1_LATE && ABL != 2;  // (the stream-only diagnostic has no phase 5)
-#if ZK_K1_LATE
     load_tid(a, ws, cur);
-    if constexpr (EC) load_early<JOIN>(a, ws, cur);
-    if constexpr (EC && ZK_K1_EARLY_COLS >= 2) load_late<JOIN>(a, ws, cur);
-#else
-    load_window<JOIN>(a, ws, cur);
-#endif
+    load_early(a, ws, cur);
 #pragma unroll
-#if ZK_K1_SLOT16
-    for (int x = tid; x < H; x += WG) s_h16[x] = make_uint4(0u, 0u, 0u, kSvcNone);
-#else
     for (int x = tid; x < H / 4; x += WG) reinterpret_cast<uint4*>(s_ht)[x] = make_uint4(0u, 0u, 0u, 0u);
-#endif
     uint64_t m_ev, m_od;  // this wave's boundary ballots of the current window (uniform; phase 3 reuses them)
-    constexpr bool EB = ZK_K1_EARLY_BALLOT && ABL != 2;  // (the stream-only diagnostic has no phase 7)
-    if constexpr (EB) {
-        // the first window's ballots; later windows' are taken at the end of the window before (below)
-        window_ballots(cur, ws, (int)((n - ws) < (uint64_t)TILE ? (n - ws) : (uint64_t)TILE), &m_ev, &m_od);
-        if (lane == 0) *reinterpret_cast<ulonglong2*>(&s_mask[2 * wave]) = make_ulonglong2(m_ev, m_od);
-    }
+    // the first window's ballots; later windows' are taken at the end of the window before (below)
+    window_ballots(cur, ws, (int)((n - ws) < (uint64_t)TILE ? (n - ws) : (uint64_t)TILE), &m_ev, &m_od);
+    if (lane == 0) *reinterpret_cast<ulonglong2*>(&s_mask[2 * wave]) = make_ulonglong2(m_ev, m_od);
     ZK_STAMP_DECL
     for (;;) {
-#if ZK_K1_LATE
-        if constexpr (EC) {
-            if constexpr (ZK_K1_EARLY_COLS < 2) load_late<JOIN>(a, ws, cur);
-        } else {
-            load_rest<JOIN>(a, ws, cur);
-        }
-#endif
+        load_late<JOIN>(a, ws, cur);
         const int wn = (int)((n - ws) < (uint64_t)TILE ? (n - ws) : (uint64_t)TILE);
-        // ---- 1. trace boundaries of the window -------------------------------------------------
-        if constexpr (!EB) {
-            window_ballots(cur, ws, wn, &m_ev, &m_od);
-            if (lane == 0) *reinterpret_cast<ulonglong2*>(&s_mask[2 * wave]) = make_ulonglong2(m_ev, m_od);
-        }
+        // ---- 1. trace boundaries of the window (ballots taken at the end of the window before) --
         ZK_PHASE_SYNC(0);
         // ---- 2. which records are ours, where the next window starts (uniform) ----------------
         const int lo_j = (int)(seek - ws);
@@ -563,7 +426,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         // lane w < NW holds wave w's masks: the first boundary >= lo_j (start), the first >= r1_j
         // (stop), the last of the window (last_b) and the last before this wave's records (prev_b)
         int start = -1, stop = -1, last_b = -1, prev_b = -1;  // wave-uniform (SGPRs)
-        int next_after = wn;
         {
             constexpr int NW = WG / 64;
             uint64_t ev = 0ull, od = 0ull;
@@ -573,10 +435,10 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 od = x.y;
             }
             const int base = 128 * lane;
-            // steady state (ZK_K1_FAST_SCAN): the window starts at the trace start `seek` that the
-            // window before found, and the range end R1 is beyond it -- start = lo_j, stop = none,
-            // with no search (the search would return exactly these: bit lo_j is set in the masks)
-            const bool fast = ZK_K1_FAST_SCAN && !ZK_K1_SORTJOIN && seek_start && lo_j < wn && R1 - ws >= (uint64_t)wn;
+            // steady state: the window starts at the trace start `seek` that the window before
+            // found, and the range end R1 is beyond it -- start = lo_j, stop = none, with no search
+            // (the search would return exactly these: bit lo_j is set in the masks)
+            const bool fast = seek_start && lo_j < wn && R1 - ws >= (uint64_t)wn;
             if (fast) {
                 start = lo_j;
             } else {
@@ -603,17 +465,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 const int w = 63 - (int)__clzll((long long)bp);
                 prev_b = 128 * w + __builtin_amdgcn_readlane(lb, w);
             }
-#if ZK_K1_SORTJOIN
-            {  // the first boundary after this wave's records (a segment's end), else the window end
-                const int fb = lane < NW ? first_ge(ev, od, 0) : -1;
-                const uint64_t bf = __ballot(fb >= 0) & ~((2ull << wave) - 1ull);
-                next_after = wn;
-                if (bf) {
-                    const int w = __ffsll((unsigned long long)bf) - 1;
-                    next_after = 128 * w + __builtin_amdgcn_readlane(fb, w);
-                }
-            }
-#endif
         }
         const bool at_end = ws + (uint64_t)wn >= n;
         int m;                  // records [start, m) are processed in this window
@@ -654,25 +505,21 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         }
         if (!done && next_seek >= R1) done = true;
         const uint64_t next_ws = next_seek & ~1ull;
-#if ZK_K1_LATE
-        load_tid(a, done ? ws : next_ws, nxt);
-#else
-        load_window<JOIN>(a, done ? ws : next_ws, nxt);  // in flight during the LDS phases below (unconditional: see ld2)
-#endif
+        load_tid(a, done ? ws : next_ws, nxt);  // in flight during the LDS phases below (unconditional: see ld2)
         ZK_STAMP(1);
         nrec += (uint64_t)(m - start);
-        uint64_t n_ev = 0, n_od = 0;  // the next window's ballots (EB)
-        if constexpr (ABL != 2) {  // diagnostic build: 2 = stream windows only
+        uint64_t n_ev = 0, n_od = 0;  // the next window's ballots
 
-#if ZK_K1_ATOMIC_APPEND
         // the last window's leaders empty their hash slots (see phase 7)
+#if ZK_K1_EPOCH
+        // CAS of the final word -> 0: an inserter of this window may have claimed the stale slot already
 #pragma unroll
         for (int e = 0; e < 2; ++e)
-#if ZK_K1_SLOT16
-            if (r_clear[e] != kNoSlot) s_h16[r_clear[e]] = make_uint4(0u, 0u, 0u, kSvcNone);
+            if (r_clear[e] != kNoSlot) (void)atomicCAS(&s_ht[r_clear[e]], r_cword[e], 0u);
 #else
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
             if (r_clear[e] != kNoSlot) s_ht[r_clear[e]] = 0u;
-#endif
 #endif
         // ---- 3. segment ids and LDS staging ----------------------------------------------------
         // seg = index of the trace's first record in the window (the last boundary <= j), from the
@@ -681,12 +528,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         int r_seg[2];
         uint32_t r_svck[2];
         bool r_rerr[2];
-#if ZK_K1_SLOT16
-        uint32_t r_lsvc[2];
-#endif
-#if ZK_K1_SORTJOIN
-        int r_end[2];  // end of the record's trace segment in the window
-#endif
         {
             const int j0 = 2 * tid;
             // last boundary <= j0 among this wave's records, else the one before the wave (it exists
@@ -708,56 +549,20 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 v_last[e] = ha ? cur.last[e] : (uint64_t)LLONG_MIN;
                 v_pid[e] = (f & ZK_F_HAS_PARENT) ? cur.pid[e] : ~0ull;
             }
-            uint32_t c_svck[2] = {r_svck[0], r_svck[1]};
             *reinterpret_cast<ulonglong2*>(&s_sid[j0]) = make_ulonglong2(cur.sid[0], cur.sid[1]);
             *reinterpret_cast<ulonglong2*>(&s_first[j0]) = make_ulonglong2(v_first[0], v_first[1]);
             *reinterpret_cast<ulonglong2*>(&s_last[j0]) = make_ulonglong2(v_last[0], v_last[1]);
             *reinterpret_cast<ulonglong2*>(&s_pid[j0]) = make_ulonglong2(v_pid[0], v_pid[1]);
-#if !ZK_K1_SLOT16
-            *reinterpret_cast<uint2*>(&s_svck[j0]) = make_uint2(c_svck[0], c_svck[1]);
-#else
-            r_lsvc[0] = c_svck[0];  // a leader enters its (carrier) service into its slot
-            r_lsvc[1] = c_svck[1];
-#endif
-#if ZK_K1_SORTJOIN || !ZK_K1_SEG_IN_SLOT
-            *reinterpret_cast<uint32_t*>(&s_seg[j0]) = ((uint32_t)r_seg[0] & 0xFFFFu) | ((uint32_t)r_seg[1] << 16);
-#endif
-#if ZK_K1_SORTJOIN
-            {
-                const int p0 = first_ge(m_ev, m_od, 2 * lane + 1), p1 = first_ge(m_ev, m_od, 2 * lane + 2);
-                r_end[0] = p0 >= 0 ? 128 * wave + p0 : next_after;
-                r_end[1] = p1 >= 0 ? 128 * wave + p1 : next_after;
-                uint32_t once;
-                *reinterpret_cast<uint2*>(&s_bits[j0]) =
-                    make_uint2(frag_bits(cur.flags[0], &once), frag_bits(cur.flags[1], &once));
-            }
-#endif
+            *reinterpret_cast<uint2*>(&s_svck[j0]) = make_uint2(r_svck[0], r_svck[1]);
         }
+#if !ZK_K1_EPOCH
         ZK_PHASE_SYNC(2);  // (the hash table is empty here: cleared once, then by its leaders)
+#endif
 
         // ---- 4. groupBy((id, traceId)): the first fragment to claim a slot leads --------------
         // Both records of the thread probe together (one LDS round trip per step for the pair).
         int r_leader[2];
         uint32_t r_slot[2];
-#if ZK_K1_SORTJOIN
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            r_leader[e] = -1;
-            r_slot[e] = 0u;
-            if (r_seg[e] < 0) continue;
-            const int j = 2 * tid + e;
-            const uint64_t sid = cur.sid[e];
-            int rank = 0, L = j;
-            for (int k = r_seg[e]; k < r_end[e]; ++k) {
-                const uint64_t x = s_sid[k];
-                rank += (x < sid || (x == sid && k < j)) ? 1 : 0;
-                L = (x == sid && k < L) ? k : L;
-            }
-            r_leader[e] = L;
-            s_perm[r_seg[e] + rank] = (uint16_t)j;
-        }
-        if (false)
-#endif
         {
             bool act[2];
             uint32_t word[2];
@@ -767,48 +572,43 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 act[e] = r_seg[e] >= 0;
                 r_slot[e] = slot_hash(cur.sid[e], (uint32_t)(r_seg[e] & 0xFFFF)) & (H - 1);
                 uint32_t once;
-                word[e] = (uint32_t)(2 * tid + e + 1) | frag_bits(cur.flags[e], &once);
-                if (ZK_K1_SEG_IN_SLOT) word[e] |= ((uint32_t)r_seg[e] & 0x1FFu) << kSlotSegShift;
+                word[e] = (uint32_t)(2 * tid + e + 1) | frag_bits(cur.flags[e], &once) |
+                          (((uint32_t)r_seg[e] & 0x1FFu) << kSlotSegShift) | epoch;
             }
+            uint32_t expect[2] = {0u, 0u};  // what the slot holds as far as we know: empty or stale
             while (act[0] || act[1]) {
                 uint32_t old[2];
 #pragma unroll
-                for (int e = 0; e < 2; ++e) old[e] = act[e] ? atomicCAS(ZK_HMETA(r_slot[e]), 0u, word[e]) : 0u;
+                for (int e = 0; e < 2; ++e) old[e] = act[e] ? atomicCAS(&s_ht[r_slot[e]], expect[e], word[e]) : 0u;
                 int o[2];
+                bool cur_w[2];  // the slot holds an entry of this window
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
                     o[e] = (int)(old[e] & kSlotIdx) - 1;
-                    if (act[e] && old[e] == 0u) {
+                    cur_w[e] = old[e] != 0u && (old[e] & kSlotEpoch) == epoch;
+                    if (act[e] && old[e] == expect[e]) {
                         r_leader[e] = 2 * tid + e;
                         act[e] = false;
-#if ZK_K1_SLOT16
-                        // the slot's spanId copy (read by the phase-6 probes, after two barriers) and
-                        // the leader's service (fragments that found it meanwhile min in theirs)
-                        *reinterpret_cast<uint64_t*>(&s_h16[r_slot[e]].x) = cur.sid[e];
-                        if (r_lsvc[e] != kSvcNone) atomicMin(&s_h16[r_slot[e]].w, r_lsvc[e]);
-#endif
                     }
                 }
                 uint64_t osid[2];
                 uint16_t oseg[2];
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
-#if ZK_K1_SEG_IN_SLOT
                     oseg[e] = (uint16_t)((old[e] >> kSlotSegShift) & 0x1FFu);
-                    osid[e] = (act[e] && oseg[e] == (uint16_t)r_seg[e]) ? s_sid[o[e]] : ~cur.sid[e];
-#else
-                    osid[e] = act[e] ? s_sid[o[e]] : 0ull;
-                    oseg[e] = act[e] ? s_seg[o[e]] : (uint16_t)0;
-#endif
+                    osid[e] = (act[e] && cur_w[e] && oseg[e] == (uint16_t)r_seg[e]) ? s_sid[o[e]] : ~cur.sid[e];
                 }
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
                     if (!act[e]) continue;
-                    if (osid[e] == cur.sid[e] && oseg[e] == (uint16_t)r_seg[e]) {
+                    if (!cur_w[e]) {
+                        expect[e] = old[e];  // empty, or a stale entry its leader has not cleared yet: claim it
+                    } else if (osid[e] == cur.sid[e] && oseg[e] == (uint16_t)r_seg[e]) {
                         r_leader[e] = o[e];
                         act[e] = false;
                     } else {
                         r_slot[e] = (r_slot[e] + 1) & (H - 1);
+                        expect[e] = 0u;
                     }
                 }
             }
@@ -829,22 +629,18 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                     atomicMin(&s_first[L], (long long)cur.first[e]);
                     atomicMax(&s_last[L], (long long)cur.last[e]);
                 }
-                if (r_svck[e] != kSvcNone) atomicMin(ZK_HSVC(L, r_slot[e]), r_svck[e]);
+                if (r_svck[e] != kSvcNone) atomicMin(&s_svck[L], r_svck[e]);
                 if (f & ZK_F_HAS_PARENT) atomicMin((unsigned long long*)&s_pid[L], (unsigned long long)cur.pid[e]);
                 uint32_t once;
                 const uint32_t bits = frag_bits(f, &once);
-#if ZK_K1_SORTJOIN
-                uint32_t* const wp = &s_bits[L];
-#else
-                uint32_t* const wp = ZK_HMETA(r_slot[e]);
-#endif
+                uint32_t* const wp = &s_ht[r_slot[e]];
                 const uint32_t old = atomicOr(wp, bits);
                 const uint32_t promote = once & (old >> kSlotA) & 0xFu;  // second occurrence
                 if (promote) atomicOr(wp, promote << kSlotB);
             }
         }
         ZK_PHASE_SYNC(4);
-        if constexpr (EC) load_early<JOIN>(a, done ? ws : next_ws, cur);  // see load_early
+        load_early(a, done ? ws : next_ws, cur);  // phase 6 no longer reads these registers
 
         // ---- 6. filter(isValid), join on (parentId, traceId), (cell, duration) links ----------
         uint64_t r_link[2], r_item[2];
@@ -859,16 +655,9 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             if (L < 0) continue;
             const int j = 2 * tid + e;
             const uint32_t f = cur.flags[e];
-#if ZK_K1_SORTJOIN
-            const uint32_t w = s_bits[L];
-            const uint32_t sL = s_svck[L];
-#elif ZK_K1_SLOT16
-            const uint4 q = s_h16[r_slot[e]];
-            const uint32_t w = q.z, sL = q.w;
-#else
             const uint32_t w = s_ht[r_slot[e]];
+            r_cword[e] = w;
             const uint32_t sL = s_svck[L];
-#endif
             const uint64_t pL = s_pid[L];
             bool amb = (f & ZK_F_HAS_PARENT) ? (cur.pid[e] != pL) : ((w & kSlotP1) != 0u);
             const uint32_t sk = r_svck[e];
@@ -895,67 +684,22 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             if constexpr (!JOIN) continue;
             if (!(valid && (w & kSlotP1))) continue;
             st.inc(ST_CHILD);
-#if ZK_K1_SORTJOIN
-            // binary search of the parent's spanId in the sorted segment: the first of equal spanIds
-            // is the parent span's leader
-            int P = -1;
-            uint32_t pw = 0;
-            {
-                int lo = r_seg[e], hi = r_end[e];
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    if (s_sid[s_perm[mid]] < pL)
-                        lo = mid + 1;
-                    else
-                        hi = mid;
-                }
-                if (lo < r_end[e]) {
-                    const int q = s_perm[lo];
-                    if (s_sid[q] == pL) {
-                        P = q;
-                        pw = s_bits[q];
-                    }
-                }
-            }
-            if (P < 0 || !slot_valid(pw)) {
-                st.inc(ST_MISSING_PARENT);
-                continue;
-            }
-            st.inc(ST_JOINED);
-            const uint32_t sp = s_svck[P];
-#else
             const uint16_t seg = (uint16_t)r_seg[e];
             uint32_t slot = slot_hash(pL, seg) & (H - 1);
-            uint32_t pw = 0;
-#if ZK_K1_SLOT16
-            uint32_t sp = kSvcNone;
-            for (;;) {
-                const uint4 q = s_h16[slot];  // spanId, slot word and service in one read
-                if (q.z == 0u) break;
-                if (((q.z >> kSlotSegShift) & 0x1FFu) == seg && (((uint64_t)q.y << 32) | q.x) == pL) {
-                    pw = q.z;
-                    sp = q.w;
-                    break;
-                }
-                slot = (slot + 1) & (H - 1);
-            }
-            if (pw == 0u || !slot_valid(pw)) {
-                st.inc(ST_MISSING_PARENT);
-                continue;
-            }
-            st.inc(ST_JOINED);
-#else
+            uint32_t pw = 0, sp = kSvcNone;
+            // every stale entry is gone after the merge barrier: a probe ends at the first empty slot
             for (;;) {
                 const uint32_t o = s_ht[slot];
                 if (o == 0u) break;
                 const int oi = (int)(o & kSlotIdx) - 1;
-#if ZK_K1_SEG_IN_SLOT
-                if (((o >> kSlotSegShift) & 0x1FFu) == seg && s_sid[oi] == pL) {
-#else
-                if (s_sid[oi] == pL && s_seg[oi] == seg) {
-#endif
-                    pw = o;
-                    break;
+                if (((o >> kSlotSegShift) & 0x1FFu) == seg) {
+                    const uint64_t osid = s_sid[oi];
+                    const uint32_t osvc = s_svck[oi];  // read with the spanId: one round trip
+                    if (osid == pL) {
+                        pw = o;
+                        sp = osvc;
+                        break;
+                    }
                 }
                 slot = (slot + 1) & (H - 1);
             }
@@ -964,9 +708,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 continue;
             }
             st.inc(ST_JOINED);
-            const uint32_t sp = s_svck[(pw & kSlotIdx) - 1];
-#endif
-#endif
             if (sp == kSvcNone || sL == kSvcNone) {
                 st.inc(ST_NO_SERVICE);
                 continue;
@@ -978,21 +719,17 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             }
             const uint64_t cell = (uint64_t)(sp & kSvcIdMask) * a.S + (sL & kSvcIdMask);
             r_link[e] = (cell << 40) | d;
-            if (a.nb && ABL == 0) atomicAdd(&s_hist[cell >> a.cb_shift], 1u);
+            if (a.nb) atomicAdd(&s_hist[cell >> a.cb_shift], 1u);
             ++nl;
         }
         ZK_STAMP(5);
-        // ZK_K1_EARLY_COLS >= 2: parentId and flags of the next window, now that phase 6 is done with them
-        if constexpr (EC && ZK_K1_EARLY_COLS >= 2) load_late<JOIN>(a, done ? ws : next_ws, cur);
         // ---- 7. append the window's links (and sketch items) to this workgroup's lists ----------
-        // one exclusive scan for both counts: links in bits 0..15, items in 16..31 (<= 512 each)
-        // per-wave counts and lane offsets from ballots (nl, ni are 0..2: two bits each)
+        // no barrier: each wave claims its slice of the workgroup's lists with ONE LDS atomic on a
+        // cursor (links in the low 32 bits, sketch items in the high 32); lane offsets from ballots
+        // (nl, ni are 0..2). The waves' order inside a list is whatever the atomics give -- the
+        // reduce adds exact integers, so it is free.
         const uint64_t l1 = __ballot(nl >= 1u), l2 = __ballot(nl >= 2u);
         const uint64_t i1 = EMIT ? __ballot(ni >= 1u) : 0ull, i2 = EMIT ? __ballot(ni >= 2u) : 0ull;
-#if ZK_K1_ATOMIC_APPEND
-        // no barrier: each wave claims its slice of the workgroup's lists with ONE LDS atomic on a
-        // cursor (links in the low 32 bits, sketch items in the high 32). The waves' order inside a
-        // list is whatever the atomics give -- the reduce adds exact integers, so it is free.
         uint32_t lbase = 0, ibase = 0;
         {
             const uint64_t wtot = (uint64_t)(__popcll(l1) + __popcll(l2)) | ((uint64_t)(__popcll(i1) + __popcll(i2)) << 32);
@@ -1002,54 +739,28 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             lbase = (uint32_t)old + lanes_below(l1) + lanes_below(l2);
             ibase = (uint32_t)(old >> 32) + lanes_below(i1) + lanes_below(i2);
         }
-#else
-        // one exclusive scan for both counts: links in bits 0..15, items in 16..31 (<= 512 each)
-        // per-wave counts and lane offsets from ballots (nl, ni are 0..2: two bits each)
-        const uint32_t below = (lanes_below(l1) + lanes_below(l2)) | ((lanes_below(i1) + lanes_below(i2)) << 16);
-        if (lane == 0)
-            s_wsum[wave] = (uint32_t)(__popcll(l1) + __popcll(l2)) | ((uint32_t)(__popcll(i1) + __popcll(i2)) << 16);
-        ZK_PHASE_SYNC(6);
-        uint32_t base = 0, total = 0;
-#pragma unroll
-        for (int w2 = 0; w2 < WG / 64; ++w2) {
-            const uint32_t v = s_wsum[w2];
-            if (w2 < wave) base += v;
-            total += v;
-        }
-        const uint32_t excl = base + below;
-        const uint32_t lbase = nout + (excl & 0xFFFFu), ibase = nitem + (excl >> 16);
-#endif
         // the next window's ballots, BEFORE this window's link stores: the prefetched traceIds are
         // then waited for while only they are in flight, not behind the stores (vmcnt is one queue
         // for loads and stores, and the first use of a prefetched value waits for everything older
         // in the compiler's model). s_mask is free: every wave read it in phase 2, before the
         // phase-3 barrier; the next window's phase-1 barrier publishes the new masks.
-        if (EB && !done) {
+        if (!done) {
             const uint64_t nws = next_ws;
             window_ballots(nxt, nws, (int)((n - nws) < (uint64_t)TILE ? (n - nws) : (uint64_t)TILE), &n_ev, &n_od);
             if (lane == 0) *reinterpret_cast<ulonglong2*>(&s_mask[2 * wave]) = make_ulonglong2(n_ev, n_od);
         }
-        if constexpr (ABL == 0 && JOIN) {
+        if constexpr (JOIN) {
             // exactly two stores per thread on every path (absent links go to the list's trash
             // slot), so the loop-end wait for the prefetched window can count them: vmcnt(2)
             uint32_t pos = lbase;
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const bool v = r_link[e] != ~0ull;
-#if ZK_K1_OOB_STORE
-                typedef unsigned int v2u_t __attribute__((ext_vector_type(2)));
-                const v2u_t lv = {(unsigned int)r_link[e], (unsigned int)(r_link[e] >> 32)};
-                __builtin_amdgcn_raw_buffer_store_b64(lv, out_rsrc, v ? pos * 8u : 0x7FFFFFF8u, 0, 0);
-#else
-                out[v ? (uint64_t)pos : trash + (ZK_K1_TRASH_SPREAD ? e : 0)] = r_link[e];
-#endif
+                out[v ? (uint64_t)pos : trash] = r_link[e];
                 pos += v ? 1u : 0u;
             }
-#if !ZK_K1_ATOMIC_APPEND
-            nout += total & 0xFFFFu;
-#endif
         }
-        if constexpr (ABL == 0 && EMIT) {
+        if constexpr (EMIT) {
             uint32_t pos = ibase;
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
@@ -1059,29 +770,14 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 it_svc[at] = r_isvc[e];
                 pos += v ? 1u : 0u;
             }
-#if !ZK_K1_ATOMIC_APPEND
-            nitem += total >> 16;
-#endif
         }
-#if ZK_K1_ATOMIC_APPEND
         // every leader empties its own slot in the NEXT window, after its phase-1 barrier (which
         // every wave reaches only when done probing this window) and before its phase-3 barrier
         // (after which that window inserts)
 #pragma unroll
-        for (int e = 0; e < 2; ++e) r_clear[e] = (!ZK_K1_SORTJOIN && r_leader[e] == 2 * tid + e) ? r_slot[e] : kNoSlot;
-#else
-        // every leader empties its own slot (phase 7's barrier is past all probes of this window;
-        // the next window inserts only after its phase-1 and phase-3 barriers)
-#pragma unroll
-        for (int e = 0; e < 2; ++e)
-#if ZK_K1_SLOT16
-            if (r_leader[e] == 2 * tid + e) s_h16[r_slot[e]] = make_uint4(0u, 0u, 0u, kSvcNone);
-#else
-            if (!ZK_K1_SORTJOIN && r_leader[e] == 2 * tid + e) s_ht[r_slot[e]] = 0u;
-#endif
-#endif
+        for (int e = 0; e < 2; ++e) r_clear[e] = (r_leader[e] == 2 * tid + e) ? r_slot[e] : kNoSlot;
+        epoch ^= kSlotEpoch;
         ZK_STAMP(6);
-        }  // ablate != 2
         if (--fold_in == 0) {
             fold_stats(st, s_stat);
             fold_in = kFoldWindows;
@@ -1090,28 +786,20 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         ws = next_ws;
         seek = next_seek;
         seek_start = next_seek_start;
-        if constexpr (EB) {
-            m_ev = n_ev;
-            m_od = n_od;
-        }
-#if ZK_K1_LATE
+        m_ev = n_ev;
+        m_od = n_od;
         cur.tid[0] = nxt.tid[0];
         cur.tid[1] = nxt.tid[1];
         cur.prev = nxt.prev;
-#else
-        cur = nxt;
-#endif
         // no loop-end barrier: the next window's phase-1 barrier already separates this window's
         // last LDS reads (phase 6-7) from its writes (phase 3 on), and phase 1's s_mask writes
         // from this window's reads (phases 2-3, before the barrier that ends phase 3)
         ZK_STAMP(7);
     }
     ZK_STAMP_FLUSH();
-#if ZK_K1_ATOMIC_APPEND
     __syncthreads();  // every wave's last append is in the cursor
-    nout = (uint32_t)s_cursor;
-    nitem = (uint32_t)(s_cursor >> 32);
-#endif
+    const uint32_t nout = (uint32_t)s_cursor;
+    const uint32_t nitem = (uint32_t)(s_cursor >> 32);
     if (tid == 0) {
         a.link_count[blockIdx.x] = nout;
         if constexpr (EMIT) a.rt_count[blockIdx.x] = nitem;
@@ -1388,16 +1076,12 @@ hipError_t launch_join(const JoinArgs& a, hipStream_t s) {
     if (a.c.n == 0) return hipSuccess;
     const dim3 g((unsigned)a.grid), b(kTileWG);
     const bool emit = a.rt_pay != nullptr, join = a.join != 0;
-    if (a.ablate == 1)
-        return launch_checked("k_span_join_stream<ablate 1>", k_span_join_stream<kTile, kTileWG, 1, kModeJoin>, g, b, 0, s, a);
-    if (a.ablate == 2)
-        return launch_checked("k_span_join_stream<ablate 2>", k_span_join_stream<kTile, kTileWG, 2, kModeJoin>, g, b, 0, s, a);
     if (emit && join)
-        return launch_checked("k_span_join_stream<join|emit>", k_span_join_stream<kTile, kTileWG, 0, kModeJoin | kModeEmit>,
+        return launch_checked("k_span_join_stream<join|emit>", k_span_join_stream<kTile, kTileWG, kModeJoin | kModeEmit>,
                               g, b, 0, s, a);
     if (emit)
-        return launch_checked("k_span_join_stream<emit>", k_span_join_stream<kTile, kTileWG, 0, kModeEmit>, g, b, 0, s, a);
-    return launch_checked("k_span_join_stream<join>", k_span_join_stream<kTile, kTileWG, 0, kModeJoin>, g, b, 0, s, a);
+        return launch_checked("k_span_join_stream<emit>", k_span_join_stream<kTile, kTileWG, kModeEmit>, g, b, 0, s, a);
+    return launch_checked("k_span_join_stream<join>", k_span_join_stream<kTile, kTileWG, kModeJoin>, g, b, 0, s, a);
 }
 
 hipError_t launch_spill(const JoinArgs& a, uint32_t spill_wgs, hipStream_t s) {
@@ -1433,12 +1117,8 @@ void join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, u
     const uint64_t per = ((n + g - 1) / g + kTile - 1) / kTile * kTile;
     *grid = (uint32_t)g;
     *per_wg = per ? per : kTile;
-    // a workgroup's last trace may overhang its range by < TILE; then the trash slot(s) of K1's stores
-#if ZK_K1_TRASH_SPREAD
-    *link_stride = *per_wg + 2 * kTile;
-#else
+    // a workgroup's last trace may overhang its range by < TILE; then the trash slot of K1's stores
     *link_stride = *per_wg + kTile + 1;
-#endif
 }
 
 }  // namespace zk

@@ -593,7 +593,12 @@ hipError_t partition_impl(const PartitionPlan& p, const uint32_t* svc, const uin
         x.payload = payload;
         x.out = out;
         x.S = p.S;
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const uint32_t gx = (uint32_t)(cus > 0 ? cus : 256) * (ZK_PART_XSTATIC ? ZK_PX_GRID : 1);
+        // every portion needs a workgroup: the static scatter gives portion q to blocks q, q + parts, ...
         x.parts = p.grid < kPartParts ? p.grid : kPartParts;
+        if (x.parts > gx) x.parts = gx;
         x.cursor = (unsigned int*)xp;
         xp += ((uint64_t)kPartParts * p.S * 4 + 255) & ~255ull;
         uint64_t* part_lo = (uint64_t*)xp;
@@ -607,12 +612,9 @@ hipError_t partition_impl(const PartitionPlan& p, const uint32_t* svc, const uin
         e = launch_checked("k_part_xprep", k_part_xprep, dim3((x.parts * p.S + 255) / 256), dim3(256), 0, s,
                            (const uint32_t*)offs, p.S, p.grid, x.parts, p.per_wg, n, x.cursor, part_lo, part_tiles, next);
         if (e == hipSuccess) {
-            int dev = 0, cus = 256;
-            if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            e = ZK_PART_XSTATIC ? launch_checked("k_part_xscatter_static", k_part_xscatter_static,
-                                                 dim3((cus > 0 ? cus : 256) * ZK_PX_GRID), dim3(kPxWG), 0, s, x)
-                                : launch_checked("k_part_xscatter", k_part_xscatter, dim3(cus > 0 ? cus : 256),
-                                                 dim3(kPxWG), 0, s, x);
+            e = ZK_PART_XSTATIC ? launch_checked("k_part_xscatter_static", k_part_xscatter_static, dim3(gx), dim3(kPxWG), 0,
+                                                 s, x)
+                                : launch_checked("k_part_xscatter", k_part_xscatter, dim3(gx), dim3(kPxWG), 0, s, x);
         }
     } else if (choice == kScatterLines)
         e = launch_checked("k_part_scatter_lines", k_part_scatter_lines<ZK_PART_U, ZK_PART_WG>, dim3(p.grid),

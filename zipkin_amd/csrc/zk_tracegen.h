@@ -58,6 +58,21 @@ ZK_HD uint64_t zk_tg_trace_id(uint64_t seed, uint64_t k, uint32_t rank, uint32_t
     return zk_unmix64(u * w + rank);
 }
 
+// Global trace set (zk_tracegen_params.global_ids): trace k of ONE set shared by every world size,
+// traceId = mix64^-1(v) with v = k | (seed bits << 40) unique per (seed, k). Its shard is
+// mix64(traceId) % world = v % world, so shard (rank, world) owns the traces k = k0, k0 + world, ...
+// with k0 = the first k >= 0 whose v % world == rank: the same records for every world, split.
+ZK_HD uint64_t zk_tg_global_v(uint64_t seed, uint64_t k) {
+    return (k & ((1ull << 40) - 1)) | ((zk_mix64(seed) & 0xFFFFull) << 40);
+}
+ZK_HD uint64_t zk_tg_global_trace_id(uint64_t seed, uint64_t k) { return zk_unmix64(zk_tg_global_v(seed, k)); }
+// first global trace of shard (rank, world)
+ZK_HD uint64_t zk_tg_global_k0(uint64_t seed, uint32_t rank, uint32_t world) {
+    const uint64_t w = world ? world : 1;
+    const uint64_t base = zk_tg_global_v(seed, 0) % w;  // v(k) % w = (base + k) % w for k < 2^40
+    return ((uint64_t)rank + w - base) % w;
+}
+
 struct zk_rng {
     uint64_t s;
 };
@@ -134,12 +149,11 @@ ZK_HD void zk_tg_enter(zk_rng* r, zk_tg_frame* f, int64_t time, uint32_t depth, 
     f->child_idx = 0;
 }
 
-// Generate one trace; Emit is called once per span fragment, in TraceGen order.
-// Returns the number of fragments.
+// Generate one trace with the given traceId; Emit is called once per span fragment, in TraceGen
+// order. Returns the number of fragments. The trace's content depends on (seed, traceId) only.
 template <class Emit>
-ZK_HD uint32_t zk_tg_trace(uint64_t seed, uint64_t k, uint32_t rank, uint32_t world,
-                           uint32_t max_depth, uint32_t S, int64_t base_ts, Emit& emit) {
-    const uint64_t trace_id = zk_tg_trace_id(seed, k, rank, world);
+ZK_HD uint32_t zk_tg_trace_body(uint64_t seed, uint64_t trace_id, uint32_t max_depth, uint32_t S, int64_t base_ts,
+                                Emit& emit) {
     zk_rng r;
     r.s = zk_mix64(seed ^ zk_mix64(trace_id ^ 0x5DEECE66Dull));
     zk_tg_frame stk[ZK_TG_MAX_DEPTH + 1];
@@ -193,4 +207,13 @@ ZK_HD uint32_t zk_tg_trace(uint64_t seed, uint64_t k, uint32_t rank, uint32_t wo
         p->child_idx++;
     }
     return nrec;
+}
+
+// trace k of shard (rank, world): a per-shard traceId (zk_tg_trace_id), or trace k of the global set
+// (zk_tg_global_trace_id) when `global` -- then k is the global trace index
+template <class Emit>
+ZK_HD uint32_t zk_tg_trace(uint64_t seed, uint64_t k, uint32_t rank, uint32_t world, uint32_t max_depth, uint32_t S,
+                           int64_t base_ts, Emit& emit, bool global = false) {
+    const uint64_t trace_id = global ? zk_tg_global_trace_id(seed, k) : zk_tg_trace_id(seed, k, rank, world);
+    return zk_tg_trace_body(seed, trace_id, max_depth, S, base_ts, emit);
 }

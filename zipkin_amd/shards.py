@@ -12,7 +12,6 @@ from __future__ import annotations
 
 import numpy as np
 
-from . import _abi
 from .columns import SpanColumns
 
 
@@ -159,18 +158,19 @@ def allreduce_stats(stats: dict, device="cpu", group=None) -> dict:
 
 
 class ShardedDeps:
-    """One rank of the sharded job: a DepsContext over a caller-owned (all-reducible) table.
+    """One rank of the sharded job: a DepsContext whose exchange buffer is all-reduced.
 
     step(cols): reset -> accumulate this rank's shard -> zk_deps_partial (counters folded into the
-    table's tail, the table packed into 56-bit limbs) -> ONE SUM all-reduce of that exchange buffer
-    -> note_merged (unpacked into the table) -> finalize. With
+    accumulator's tail, the accumulator packed into 56-bit limbs in the ctx's exchange buffer) -> ONE
+    SUM all-reduce of THAT buffer (never of the accumulator itself: note_merged overwrites the
+    accumulator from the exchange buffer) -> note_merged -> finalize. With
     world == 1 the all-reduce is skipped. Every rank ends with the same finalized table AND the
     same status: finalize decides errors from the job-wide counters, so a strict-mode failure on
     one shard fails every rank instead of leaving the others blocked in the next collective.
     """
 
     def __init__(self, num_services: int, *, device: int = 0, stream=None, timing: bool = False,
-                 group=None, ablate: int = 0):
+                 group=None):
         import torch
         import torch.distributed as dist
 
@@ -183,10 +183,7 @@ class ShardedDeps:
         dev = torch.device("cuda", device)
         # the library's kernels and the RCCL all-reduce must be ordered on ONE stream
         self.stream = torch.cuda.Stream(device=dev) if stream is None else stream
-        self.table = torch.zeros(_abi.table_words(num_services), dtype=torch.int64, device=dev)
-        torch.cuda.current_stream(dev).synchronize()  # the zeroed table, before the library's stream
-        self.ctx = DepsContext(num_services, device=device, stream=self.stream.cuda_stream, timing=timing,
-                               table_ptr=self.table.data_ptr(), table_bytes=self.table.numel() * 8, ablate=ablate)
+        self.ctx = DepsContext(num_services, device=device, stream=self.stream.cuda_stream, timing=timing)
 
     def step(self, cols, total_records: int | None = None, out_device=None, *, clustered: bool = False,
              verify: bool = True):
