@@ -726,6 +726,9 @@ def bench_c5(a):
     q = [rt.quantiles(s, (0.5, 0.99)) for s in range(S)]
     query_ms = (time.perf_counter() - t0) * 1e3
     achieved = n * 40 / (k1_isolated_ms * 1e-3) / 1e9  # K1 alone (serial launches), as in the c2 line
+    cpu = parity = None
+    if a.cpu_sample > 0:
+        cpu, parity = c5_parity_and_baseline(cols, min(a.cpu_sample, 4_000_000), S, stream)
     print(json.dumps({
         "metric": "spans/sec into per-service HLL distinct traceIds + duration p50/p99 (BASELINE configs[4], 1 GPU)",
         "value": n * a.steps / wall, "unit": "spans/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
@@ -739,6 +742,8 @@ def bench_c5(a):
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                      "algorithmic_bytes_per_launch": n * 40, "avg_launch_ms": k1_isolated_ms, "launches": 3,
                      "timing": "HIP events on the ctx stream around each K1 launch of serial (non-overlapped) steps"},
+        "cpu_baseline": cpu,
+        "parity": parity,
         "detail": {"event_ms_per_step": ev_ms / a.steps, "query_ms_all_services": query_ms,
                    "pipelined_k1_event_ms": join_ms,
                    "median_distinct_estimate": float(sorted(est)[S // 2]),
@@ -895,6 +900,10 @@ def bench_c4(a):
                    "frac": n * b / (phase[k] * 1e-3) / 1e9 / PEAK_HBM_GBS} for k, b in per_item.items()}
     value = n * a.steps / wall
     achieved = n * 12 / (ev_ms / a.steps * 1e-3) / 1e9  # HIP events on the step's stream
+    cpu = parity = None
+    if a.cpu_sample > 0:
+        cpu, parity = c4_parity_and_baseline(svc, keys, min(a.cpu_sample, n), S, kv, stream,
+                                             a.cpu_threads or usable_cpus())
     print(json.dumps({
         "metric": "binary annotations/sec into per-service count-min + top-K (BASELINE configs[3], 1 GPU)",
         "value": value, "unit": "annotations/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
@@ -912,9 +921,91 @@ def bench_c4(a):
                      "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                      "algorithmic_bytes_per_step": n * 12},
         "kernels": kernels,
+        "cpu_baseline": cpu,
+        "parity": parity,
         "detail": {"event_ms_per_step": ev_ms / a.steps, "topk_query_ms": query_ms,
                    "service0_top3": [(int(k), int(e)) for k, e in zip(kk[0][:3], est[0][:3])]},
     }), flush=True)
+
+
+def c5_parity_and_baseline(cols, sample, S, stream):
+    """C5's parity leg and CPU baseline on the first `sample` records (whole traces) of the timed
+    batch: a fresh device sketch fed by K1's emit mode over that prefix against oracle/realtime.py
+    (merged_span_items + RtOracle: Span.mergeSpan / isValid / serviceName / duration, HyperLogLog
+    registers, log-linear histogram) -- every register, bin and estimate identical, else the bench
+    fails. The oracle's own time on the prefix is the baseline (kind "port": numpy, one core)."""
+    import numpy as np
+
+    from oracle.realtime import RtOracle, merged_span_items
+    from zipkin_amd import DepsContext
+    from zipkin_amd.realtime import RtSketch
+
+    host = cols.to_host(sample + 100_000)
+    cut = min(sample, len(host))
+    while 0 < cut < len(host) and host.trace_id[cut] == host.trace_id[cut - 1]:
+        cut -= 1
+    part = host.take(slice(0, cut))
+    with DepsContext(S, stream=stream.cuda_stream) as ctx, RtSketch(S, stream=stream.cuda_stream) as rt:
+        rt.bind(ctx, only=True)
+        ctx.accumulate(cols, clustered=True, verify=False, n=cut)
+        gr, gh = rt.read()
+        gd = rt.distinct_traces()
+        gdrop = rt.dropped()
+        rt.unbind()
+    t0 = time.perf_counter()
+    o = RtOracle(S, p=rt.p, m=rt.m, seed=0)
+    svc, tid, dur, dropped = merged_span_items(part, S)
+    o.accumulate_merged(svc, tid, dur)
+    secs = time.perf_counter() - t0
+    od = o.distinct()
+    bad = [k for k, ok in (("registers", np.array_equal(gr, o.regs)), ("histogram", np.array_equal(gh, o.hist)),
+                           ("estimates", np.array_equal(gd, od)), ("dropped", gdrop[1] == dropped)) if not ok]
+    if bad:
+        raise RuntimeError(f"C5 parity failure on the {cut}-record prefix: {bad}")
+    cpu = {"value": cut / secs, "unit": "spans/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
+           "sample": f"first {cut} records (whole traces) of the benchmark batch; oracle/realtime.py (numpy: "
+                     f"merge, isValid, serviceName, duration, HLL p={rt.p}, histogram m={rt.m}), one core: {secs:.2f} s"}
+    parity = {"result": "exact", "records": cut,
+              "checked": "every HLL register, histogram bin and distinct estimate of all services, fresh device "
+                         "sketch (K1 emit mode) of the prefix vs oracle/realtime.py"}
+    return cpu, parity
+
+
+def c4_parity_and_baseline(svc, keys, sample, S, kv_geom, stream, threads):
+    """C4's parity leg and CPU baseline on the first `sample` items of the timed batch: a fresh
+    device sketch of that prefix against oracle/zk_kv_port.c (the C restatement of oracle/kv.py,
+    pinned to it by tests/test_kv.py): every service's full candidate list (keys and estimates, in
+    order) and the per-service totals must be identical, else the bench fails. The port's own time
+    on the prefix (median of 3, all usable cores) is the baseline (kind "port")."""
+    import numpy as np
+
+    from oracle.kv import kv_port
+    from zipkin_amd.kv import KvSketch
+
+    hs = svc[:sample].cpu().numpy().view(np.uint32)
+    hk = keys[:sample].cpu().numpy().view(np.uint64)
+    cand = kv_geom.candidates
+    with KvSketch(S, stream=stream.cuda_stream, seed=4) as g:
+        g.accumulate(svc[:sample], keys[:sample])
+        gk, ge, gc = g.topk_all(cand)
+        gt = g.totals()
+    times = []
+    for _ in range(3):
+        p = kv_port(hs, hk, S, kv_geom.width, kv_geom.depth, cand, seed=4, threads=threads)
+        times.append(p.seconds)
+    pk, pe, pc = p.topk_all(cand)
+    bad = [k for k, x, y in (("keys", gk, pk), ("estimates", ge, pe), ("counts", gc, pc), ("totals", gt, p.totals))
+           if not np.array_equal(x, y)]
+    if bad:
+        raise RuntimeError(f"C4 parity failure on the {sample}-item prefix: {bad}")
+    t = sorted(times)[1]
+    cpu = {"value": sample / t, "unit": "annotations/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
+           "sample": f"first {sample} items of the benchmark batch; oracle/zk_kv_port.c (count-min + top-{cand} per "
+                     f"service, {threads} threads), median of 3: {t:.3f} s"}
+    parity = {"result": "exact", "items": sample,
+              "checked": f"all {S} services' top-{cand} candidate lists (keys, estimates, order) and totals, fresh "
+                         "device sketch of the prefix vs oracle/zk_kv_port.c (== oracle/kv.py, tests/test_kv.py)"}
+    return cpu, parity
 
 
 if __name__ == "__main__":

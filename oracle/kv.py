@@ -169,3 +169,40 @@ def zipf_items(n: int, num_services: int, num_keys: int = 1_000_000, s: float = 
     keys = mix64(rank + np.uint64(key_salt))
     svc = rng.integers(0, num_services, size=n, dtype=np.uint32)
     return svc, keys
+
+
+class KvPortResult:
+    def __init__(self, cm, totals, keys, est, cnt, dropped, seconds, threads):
+        self.cm, self.totals, self.keys, self.est, self.cnt = cm, totals, keys, est, cnt
+        self.dropped, self.seconds, self.threads = dropped, seconds, threads
+
+    def topk_all(self, k: int):
+        """(keys uint64[S, k], est uint32[S, k], count uint32[S]) like KvSketch.topk_all."""
+        return self.keys[:, :k].copy(), self.est[:, :k].copy(), np.minimum(self.cnt, k).astype(np.uint32)
+
+
+def kv_port(service_id, key_hash, num_services: int, width: int, depth: int = 4, candidates: int = 64, seed: int = 0,
+            threads: int = 1) -> KvPortResult:
+    """oracle/zk_kv_port.c: one batch into a fresh sketch, multithreaded (C4's checker on large
+    prefixes and its CPU baseline). Same integers as KvOracle after one accumulate."""
+    import ctypes as C
+
+    from .oracle import lib
+
+    svc = np.ascontiguousarray(service_id, dtype=np.uint32)
+    keys = np.ascontiguousarray(np.asarray(key_hash).view(np.uint64) if np.asarray(key_hash).dtype == np.int64
+                                else key_hash, dtype=np.uint64)
+    S = num_services
+    cm = np.zeros((S, depth, width), np.uint32)
+    totals = np.zeros(S, np.uint64)
+    ok = np.zeros((S, candidates), np.uint64)
+    oe = np.zeros((S, candidates), np.uint32)
+    cnt = np.zeros(S, np.uint32)
+    dropped = np.zeros(1, np.uint64)
+    secs = C.c_double()
+    rc = lib().zkv_port(svc.ctypes.data, keys.ctypes.data, len(svc), S, width, depth, candidates, seed, threads,
+                        cm.ctypes.data, totals.ctypes.data, ok.ctypes.data, oe.ctypes.data, cnt.ctypes.data,
+                        dropped.ctypes.data, C.byref(secs))
+    if rc != 0:
+        raise ValueError("zkv_port: bad arguments or out of memory")
+    return KvPortResult(cm, totals, ok, oe, cnt, int(dropped[0]), secs.value, threads)

@@ -58,6 +58,9 @@ def lib():
         L.zkp_aggregate.restype = C.c_int
         L.zkp_aggregate.argtypes = [C.c_void_p] * 7 + [C.c_uint64, C.c_uint32, C.c_int, C.c_int, C.c_void_p,
                                                        C.c_void_p]
+        L.zkv_port.restype = C.c_int
+        L.zkv_port.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                               C.c_uint64, C.c_int] + [C.c_void_p] * 6 + [C.POINTER(C.c_double)]
         _lib = L
     return _lib
 

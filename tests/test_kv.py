@@ -84,6 +84,24 @@ def test_oracle_drops_out_of_range_services():
     assert o.dropped == 2 and int(o.totals.sum()) == 2
 
 
+@pytest.mark.parametrize("S,n,width,seed", [(7, 20_000, 0, 1), (500, 400_000, 0, 2), (64, 100_000, 256, 3),
+                                            (1, 5_000, 64, 4)])
+def test_c_port_equals_the_oracle(S, n, width, seed):
+    """oracle/zk_kv_port.c (the C4 line's checker on large prefixes and its CPU baseline) gives the
+    numpy restatement's counters, totals, dropped count and top lists for one batch, bit for bit."""
+    from oracle.kv import kv_port
+
+    svc, keys = zipf_items(n, S, seed=seed)
+    svc[::97] = S + 3  # out-of-range services are dropped and counted
+    o = KvOracle(S, width=width, seed=5)
+    o.accumulate(svc, keys)
+    p = kv_port(svc, keys, S, o.width, o.depth, o.cand, seed=5, threads=4)
+    assert np.array_equal(o.cm.astype(np.uint32), p.cm) and np.array_equal(o.totals, p.totals)
+    assert o.dropped == p.dropped
+    for x, y in zip(o.topk_all(o.cand), p.topk_all(o.cand)):
+        assert np.array_equal(x, y)
+
+
 def test_kv_handle_rejects_bad_config_without_device():
     import ctypes as C
 

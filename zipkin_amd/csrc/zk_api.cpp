@@ -35,7 +35,7 @@ struct zk_ctx {
     unsigned long long* stats = nullptr;  // kStatShards*ST_N
     unsigned long long* h_stats = nullptr;  // pinned host copy of stats
     hipEvent_t ev_stats = nullptr;          // recorded after the stats copy (polled, not slept on)
-    unsigned int* spill_count = nullptr;
+    unsigned int* spill_count = nullptr;  // [0] spilled traces, [1] K1's guided range counter
     uint64_t* spill_list = nullptr;
     uint64_t spill_cap = 0;
     uint8_t* spill_scratch = nullptr;
@@ -45,6 +45,7 @@ struct zk_ctx {
     uint64_t* links = nullptr;
     uint32_t* link_count = nullptr;
     uint64_t link_slots = 0;  // capacity of `links` in u64
+    uint64_t sorted_slots = 0;  // capacity of `sorted` in u64
     uint32_t link_lists = 0;  // capacity of `link_count`
     uint32_t cus = 256;
     // partitioned reduce state (nb = 0: atomic reduce)
@@ -128,14 +129,17 @@ EventPair take_pair(zk_ctx* c) {
 
 uint64_t tiles_for(uint64_t n) { return (n + join_tile_records() - 1) / join_tile_records(); }
 
-zk_status ensure_links(zk_ctx* c, uint32_t grid, uint64_t stride) {
+zk_status ensure_links(zk_ctx* c, uint32_t grid, uint64_t stride, uint64_t n) {
     const uint64_t slots = (uint64_t)grid * stride;
-    if (slots <= c->link_slots && grid <= c->link_lists) return ZK_OK;
+    // K2's bucket-sorted copy holds every link once: at most one per record
+    const uint64_t sorted_slots = n + 64 < slots ? n + 64 : slots;
+    if (slots <= c->link_slots && grid <= c->link_lists && (!c->nb || sorted_slots <= c->sorted_slots)) return ZK_OK;
     if (c->links) ZK_HIP(c, hipFree(c->links));
     if (c->link_count) ZK_HIP(c, hipFree(c->link_count));
     c->links = nullptr;
     c->link_count = nullptr;
     c->link_slots = 0;
+    c->sorted_slots = 0;
     c->link_lists = 0;
     ZK_HIP(c, hipMalloc(&c->links, slots * sizeof(uint64_t)));
     ZK_HIP(c, hipMalloc(&c->link_count, (uint64_t)grid * sizeof(uint32_t)));
@@ -148,7 +152,8 @@ zk_status ensure_links(zk_ctx* c, uint32_t grid, uint64_t stride) {
         c->sorted = nullptr;
         ZK_HIP(c, hipMalloc(&c->hist, (uint64_t)grid * c->nb * sizeof(uint32_t)));
         ZK_HIP(c, hipMalloc(&c->col_off, (uint64_t)grid * c->nb * sizeof(uint32_t)));
-        ZK_HIP(c, hipMalloc(&c->sorted, slots * sizeof(uint64_t)));
+        ZK_HIP(c, hipMalloc(&c->sorted, sorted_slots * sizeof(uint64_t)));
+        c->sorted_slots = sorted_slots;
         if (!c->bucket_base) ZK_HIP(c, hipMalloc(&c->bucket_base, (c->nb + 1) * sizeof(uint64_t)));
     }
     c->link_slots = slots;
@@ -513,12 +518,13 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
         if (vs != ZK_OK) return vs;
     }
     uint32_t grid = 0;
-    uint64_t per_wg = 0, stride = 0;
-    join_geometry(n, c->cus, &grid, &per_wg, &stride);
+    uint64_t per_wg = 0, stride = 0, chunk_max = 0;
+    uint32_t chunk_level = 0;
+    join_geometry(n, c->cus, &grid, &per_wg, &stride, &chunk_max, &chunk_level);
     zk_status st = ensure_spill(c, n);
-    if (st == ZK_OK) st = ensure_links(c, grid, stride);
+    if (st == ZK_OK) st = ensure_links(c, grid, stride, n);
     if (st != ZK_OK) return st;
-    ZK_HIP(c, hipMemsetAsync(c->spill_count, 0, 4, c->stream));
+    ZK_HIP(c, hipMemsetAsync(c->spill_count, 0, 8, c->stream));  // spill count, K1's range counter
     JoinArgs a{};
     a.c = d;
     a.table = c->table;
@@ -534,6 +540,9 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
     a.link_count = c->link_count;
     a.link_stride = stride;
     a.per_wg = per_wg;
+    a.chunk_next = c->spill_count + 1;
+    a.chunk_max = chunk_max;
+    a.chunk_level = chunk_level;
     a.grid = grid;
     a.hist = c->hist;
     a.nb = c->nb;

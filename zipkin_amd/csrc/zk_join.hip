@@ -183,13 +183,6 @@ constexpr uint32_t kSlotP1 = 1u << 20;
 constexpr uint32_t kSlotP0 = 1u << 21;
 // bits 22..30 of the slot word: the leader's trace segment (< 512)
 constexpr int kSlotSegShift = 22;
-// bit 31: the window's epoch (alternating). ZK_K1_EPOCH: a slot holding the other epoch is stale --
-// its leader of the window before empties it (CAS of its final word -> 0) -- and an inserter claims
-// it like an empty slot, so the window needs no barrier between the slot clears and the inserts.
-#ifndef ZK_K1_EPOCH
-#define ZK_K1_EPOCH 1
-#endif
-constexpr uint32_t kSlotEpoch = ZK_K1_EPOCH ? 1u << 31 : 0u;
 
 // own bits of a fragment and the "seen exactly once" core annotations it may promote to ">= 2":
 // the four 2-bit counts of cs|cr|sr|ss (bits 8..15) give ">= 1" (either bit) and ">= 2" (the high
@@ -224,6 +217,22 @@ __device__ __forceinline__ void ld2_u32(const uint32_t* __restrict__ p, uint64_t
     const uint2 x = *reinterpret_cast<const uint2*>(p + (i < lim ? i : 0));
     v[0] = x.x;
     v[1] = x.y;
+}
+
+// Start of range k of the guided schedule (even): per_level ranges of chunk_max records, then
+// per_level of half that, ... down to kChunkMin, then kChunkMin until n. Uniform scalar arithmetic.
+constexpr uint64_t kChunkMin = 8192;
+__host__ __device__ __forceinline__ uint64_t join_chunk_start(uint64_t k, uint64_t chunk_max, uint64_t per_level,
+                                                              uint64_t n) {
+    uint64_t base = 0, sz = chunk_max;
+    while (sz > kChunkMin && k >= per_level) {
+        base += per_level * sz;
+        k -= per_level;
+        sz = ((sz >> 1) + 1) & ~1ull;
+        if (sz < kChunkMin) sz = kChunkMin;
+    }
+    const uint64_t r = base + k * sz;
+    return r < n ? r : n;
 }
 
 // K1 stat counters: the per-thread 16-bit pack (StatPack) is folded into the workgroup's u32 LDS
@@ -355,6 +364,11 @@ __device__ __forceinline__ void load_late(const JoinArgs& a, uint64_t ws, Window
 // =============================================================================================
 // MODE bits: kModeJoin = the dependency path (parent join, links); kModeEmit = one sketch item
 // per merged valid span with a service (zk_rt.hip). The product dependency pass is kModeJoin.
+// ZK_K1_GUIDED: a persistent grid (one workgroup per resident slot) claims record ranges from a guided
+// schedule instead of owning one fixed range per workgroup (ZK_K1_GRID_MULT x the resident slots)
+#ifndef ZK_K1_GUIDED
+#define ZK_K1_GUIDED 1
+#endif
 constexpr int kModeJoin = 1;
 constexpr int kModeEmit = 2;
 template <int TILE, int WG, int MODE>
@@ -372,10 +386,12 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     __shared__ __align__(16) uint64_t s_mask[NWORD];
     __shared__ uint32_t s_stat[ST_N];
     __shared__ uint64_t s_cursor;  // links (low 32) and sketch items (high 32) appended so far
+    __shared__ uint32_t s_claim;   // the range just claimed (ZK_K1_GUIDED)
     __shared__ uint32_t s_hist[kMaxBuckets];  // links per cell bucket (K2's scatter offsets)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t n = a.c.n;
+#if !ZK_K1_GUIDED
     const uint64_t R0 = (uint64_t)blockIdx.x * a.per_wg;
     if (R0 >= n) {
         if (tid == 0) {
@@ -386,6 +402,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         return;
     }
     const uint64_t R1 = (R0 + a.per_wg < n) ? R0 + a.per_wg : n;
+#endif
     uint64_t* __restrict__ out = a.links + (uint64_t)blockIdx.x * a.link_stride;
     const uint64_t trash = a.link_stride - 1;  // never a real link slot (join_geometry)
     uint64_t* __restrict__ it_pay = a.rt_pay + (uint64_t)blockIdx.x * a.link_stride;
@@ -398,23 +415,38 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     for (uint32_t x = tid; x < a.nb; x += WG) s_hist[x] = 0u;
     constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
     uint32_t r_clear[2] = {kNoSlot, kNoSlot};  // hash slots this thread's leaders of the last window hold
-    uint32_t r_cword[2] = {0u, 0u};            // ... and the final words in them (read in phase 6)
-    uint32_t epoch = 0u;                       // this window's epoch bit (alternates)
 
-    uint64_t ws = R0;         // window start (even)
-    uint64_t seek = R0;       // first record that may start one of our traces
-    bool seek_start = false;  // seek is known to be a trace start (uniform)
     Window cur, nxt;
     constexpr bool JOIN = (MODE & kModeJoin) != 0, EMIT = (MODE & kModeEmit) != 0;
-    load_tid(a, ws, cur);
-    load_early(a, ws, cur);
 #pragma unroll
     for (int x = tid; x < H / 4; x += WG) reinterpret_cast<uint4*>(s_ht)[x] = make_uint4(0u, 0u, 0u, 0u);
     uint64_t m_ev, m_od;  // this wave's boundary ballots of the current window (uniform; phase 3 reuses them)
+    ZK_STAMP_DECL
+#if ZK_K1_GUIDED
+    // ranges claimed from a guided schedule (join_chunk_start): large ones first, then halving, so
+    // the workgroups run out of work within a small range of each other. A workgroup stops claiming
+    // when its link list could not take another range (join_geometry sizes the lists for 2x the
+    // even share, so the ranges are always all claimed).
+    for (;;) {
+    if (tid == 0) {
+        // (the other waves' last appends may still be landing: TILE more of slack)
+        const bool room = (uint64_t)(uint32_t)s_cursor + a.chunk_max + 2 * TILE + 2 <= a.link_stride;
+        s_claim = room ? atomicAdd(a.chunk_next, 1u) : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    const uint32_t claim = s_claim;
+    const uint64_t R0 = claim == 0xFFFFFFFFu ? n : join_chunk_start(claim, a.chunk_max, a.chunk_level, n);
+    if (R0 >= n) break;
+    const uint64_t R1 = join_chunk_start(claim + 1, a.chunk_max, a.chunk_level, n);
+#endif
+    uint64_t ws = R0;         // window start (even)
+    uint64_t seek = R0;       // first record that may start one of our traces
+    bool seek_start = false;  // seek is known to be a trace start (uniform)
+    load_tid(a, ws, cur);
+    load_early(a, ws, cur);
     // the first window's ballots; later windows' are taken at the end of the window before (below)
     window_ballots(cur, ws, (int)((n - ws) < (uint64_t)TILE ? (n - ws) : (uint64_t)TILE), &m_ev, &m_od);
     if (lane == 0) *reinterpret_cast<ulonglong2*>(&s_mask[2 * wave]) = make_ulonglong2(m_ev, m_od);
-    ZK_STAMP_DECL
     for (;;) {
         load_late<JOIN>(a, ws, cur);
         const int wn = (int)((n - ws) < (uint64_t)TILE ? (n - ws) : (uint64_t)TILE);
@@ -511,16 +543,9 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         uint64_t n_ev = 0, n_od = 0;  // the next window's ballots
 
         // the last window's leaders empty their hash slots (see phase 7)
-#if ZK_K1_EPOCH
-        // CAS of the final word -> 0: an inserter of this window may have claimed the stale slot already
-#pragma unroll
-        for (int e = 0; e < 2; ++e)
-            if (r_clear[e] != kNoSlot) (void)atomicCAS(&s_ht[r_clear[e]], r_cword[e], 0u);
-#else
 #pragma unroll
         for (int e = 0; e < 2; ++e)
             if (r_clear[e] != kNoSlot) s_ht[r_clear[e]] = 0u;
-#endif
         // ---- 3. segment ids and LDS staging ----------------------------------------------------
         // seg = index of the trace's first record in the window (the last boundary <= j), from the
         // wave's own ballots: record 2t+1 is its own segment start or shares 2t's. Staging stores
@@ -555,9 +580,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             *reinterpret_cast<ulonglong2*>(&s_pid[j0]) = make_ulonglong2(v_pid[0], v_pid[1]);
             *reinterpret_cast<uint2*>(&s_svck[j0]) = make_uint2(r_svck[0], r_svck[1]);
         }
-#if !ZK_K1_EPOCH
         ZK_PHASE_SYNC(2);  // (the hash table is empty here: cleared once, then by its leaders)
-#endif
 
         // ---- 4. groupBy((id, traceId)): the first fragment to claim a slot leads --------------
         // Both records of the thread probe together (one LDS round trip per step for the pair).
@@ -573,20 +596,17 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 r_slot[e] = slot_hash(cur.sid[e], (uint32_t)(r_seg[e] & 0xFFFF)) & (H - 1);
                 uint32_t once;
                 word[e] = (uint32_t)(2 * tid + e + 1) | frag_bits(cur.flags[e], &once) |
-                          (((uint32_t)r_seg[e] & 0x1FFu) << kSlotSegShift) | epoch;
+                          (((uint32_t)r_seg[e] & 0x1FFu) << kSlotSegShift);
             }
-            uint32_t expect[2] = {0u, 0u};  // what the slot holds as far as we know: empty or stale
             while (act[0] || act[1]) {
                 uint32_t old[2];
 #pragma unroll
-                for (int e = 0; e < 2; ++e) old[e] = act[e] ? atomicCAS(&s_ht[r_slot[e]], expect[e], word[e]) : 0u;
+                for (int e = 0; e < 2; ++e) old[e] = act[e] ? atomicCAS(&s_ht[r_slot[e]], 0u, word[e]) : 0u;
                 int o[2];
-                bool cur_w[2];  // the slot holds an entry of this window
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
                     o[e] = (int)(old[e] & kSlotIdx) - 1;
-                    cur_w[e] = old[e] != 0u && (old[e] & kSlotEpoch) == epoch;
-                    if (act[e] && old[e] == expect[e]) {
+                    if (act[e] && old[e] == 0u) {
                         r_leader[e] = 2 * tid + e;
                         act[e] = false;
                     }
@@ -596,19 +616,16 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
                     oseg[e] = (uint16_t)((old[e] >> kSlotSegShift) & 0x1FFu);
-                    osid[e] = (act[e] && cur_w[e] && oseg[e] == (uint16_t)r_seg[e]) ? s_sid[o[e]] : ~cur.sid[e];
+                    osid[e] = (act[e] && oseg[e] == (uint16_t)r_seg[e]) ? s_sid[o[e]] : ~cur.sid[e];
                 }
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
                     if (!act[e]) continue;
-                    if (!cur_w[e]) {
-                        expect[e] = old[e];  // empty, or a stale entry its leader has not cleared yet: claim it
-                    } else if (osid[e] == cur.sid[e] && oseg[e] == (uint16_t)r_seg[e]) {
+                    if (osid[e] == cur.sid[e] && oseg[e] == (uint16_t)r_seg[e]) {
                         r_leader[e] = o[e];
                         act[e] = false;
                     } else {
                         r_slot[e] = (r_slot[e] + 1) & (H - 1);
-                        expect[e] = 0u;
                     }
                 }
             }
@@ -656,7 +673,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             const int j = 2 * tid + e;
             const uint32_t f = cur.flags[e];
             const uint32_t w = s_ht[r_slot[e]];
-            r_cword[e] = w;
             const uint32_t sL = s_svck[L];
             const uint64_t pL = s_pid[L];
             bool amb = (f & ZK_F_HAS_PARENT) ? (cur.pid[e] != pL) : ((w & kSlotP1) != 0u);
@@ -687,7 +703,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             const uint16_t seg = (uint16_t)r_seg[e];
             uint32_t slot = slot_hash(pL, seg) & (H - 1);
             uint32_t pw = 0, sp = kSvcNone;
-            // every stale entry is gone after the merge barrier: a probe ends at the first empty slot
             for (;;) {
                 const uint32_t o = s_ht[slot];
                 if (o == 0u) break;
@@ -776,7 +791,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         // (after which that window inserts)
 #pragma unroll
         for (int e = 0; e < 2; ++e) r_clear[e] = (r_leader[e] == 2 * tid + e) ? r_slot[e] : kNoSlot;
-        epoch ^= kSlotEpoch;
         ZK_STAMP(6);
         if (--fold_in == 0) {
             fold_stats(st, s_stat);
@@ -796,6 +810,9 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         // from this window's reads (phases 2-3, before the barrier that ends phase 3)
         ZK_STAMP(7);
     }
+#if ZK_K1_GUIDED
+    }  // ranges
+#endif
     ZK_STAMP_FLUSH();
     __syncthreads();  // every wave's last append is in the cursor
     const uint32_t nout = (uint32_t)s_cursor;
@@ -1102,8 +1119,23 @@ extern "C" int zk_debug_stamps(unsigned long long* out, int reset) {
 }
 #endif
 
-void join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, uint64_t* link_stride) {
+void join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, uint64_t* link_stride,
+                   uint64_t* chunk_max, uint32_t* chunk_level) {
     const uint64_t windows = (n + kTile - 1) / kTile;
+#if ZK_K1_GUIDED
+    // persistent: one workgroup per resident slot; ranges from the guided schedule. The first level
+    // hands out a quarter of the batch in chunks of n / (4 g); a list holds twice the even share plus
+    // one more range, so a workgroup that stops claiming for want of room leaves the rest to others
+    uint64_t g = (uint64_t)cus * ZK_K1_WGS_PER_CU;
+    if (g > windows) g = windows ? windows : 1;
+    uint64_t cm = (n / (4 * g) + 1) & ~1ull;
+    if (cm < kChunkMin) cm = kChunkMin;
+    *grid = (uint32_t)g;
+    *chunk_max = cm;
+    *chunk_level = (uint32_t)g;
+    *per_wg = cm;
+    *link_stride = 2 * ((n + g - 1) / g) + cm + 2 * kTile + 2;
+#else
 #ifndef ZK_K1_GRID_MULT
 // workgroups per resident slot (1: persistent, every workgroup resident at once). 4: a quarter of
 // the range per workgroup, so the last workgroups' imbalance is smaller and a K1 launch shares the
@@ -1117,8 +1149,10 @@ void join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, u
     const uint64_t per = ((n + g - 1) / g + kTile - 1) / kTile * kTile;
     *grid = (uint32_t)g;
     *per_wg = per ? per : kTile;
+    *chunk_max = 0;
+    *chunk_level = 0;
     // a workgroup's last trace may overhang its range by < TILE; then the trash slot of K1's stores
     *link_stride = *per_wg + kTile + 1;
+#endif
 }
-
 }  // namespace zk

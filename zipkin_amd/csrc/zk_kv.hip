@@ -22,39 +22,14 @@
 namespace zk {
 namespace {
 
-#ifndef ZK_KV_WG
-#define ZK_KV_WG 512  // (256: candidates 1.55 -> 1.41 ms with 512 on C4)
-#endif
-constexpr int kKvWG = ZK_KV_WG;
+constexpr int kKvWG = 512;  // (256: candidates 1.55 -> 1.41 ms with 512 on C4)
 constexpr uint32_t kSetCap = 2048;  // 2^11: RowHash.set is 11 bits  // LDS hash-set slots (load <= 0.5)
 constexpr uint32_t kSortCap = 1024; // compaction sort buffer
 constexpr uint32_t kRound = 512;  // merge: entries offered between compaction checks (<= kSortCap / 2)
-#ifndef ZK_KV_PREFETCH
-#define ZK_KV_PREFETCH 4  // 8 without ZK_KV_CAND_PIPE (two 16-key buffers: 179 VGPRs, 5.6 ms on C4)
-#endif
-constexpr int kPrefetch = ZK_KV_PREFETCH;  // candidate rounds of keys in flight per thread
-#ifndef ZK_KV_SKETCH_PIPE
-// sketch: two alternating 4-key buffers (C4 sketch 2.00 -> 1.96-1.97 ms; the pass is LDS-atomic-bound,
-// profiles/r02/ab_kv_sketch_pipe.txt)
-#define ZK_KV_SKETCH_PIPE 1
-#endif
-#ifndef ZK_KV_CAND_PIPE
-// candidates: the next block's keys load while this block is estimated and inserted (C4: 3.46 ->
-// 3.22-3.26 ms, profiles/r02/ab_kv_cand_pipe.txt)
-#define ZK_KV_CAND_PIPE 1
-#endif
-#ifndef ZK_KV_PROBE1
-#define ZK_KV_PROBE1 2  // candidates: 1 every key's first set slot read before any probe chain; 2 + two slots, mask decisions
-#endif
-#ifndef ZK_KV_HOT
-#define ZK_KV_HOT 1  // sketch: one learned hot key per wave, its lanes' adds combined
-#endif
-#ifndef ZK_KV_ROWS_OUTER
-#define ZK_KV_ROWS_OUTER 1  // candidates: count-min rows as the outer loop over a thread's keys
-#endif
-#ifndef ZK_KV_DIAG
-#define ZK_KV_DIAG 0  // A/B diagnostics of the candidate pass (results wrong): 1 no set probes/inserts, 2 + no estimates
-#endif
+// candidate rounds of keys in flight per thread (two alternating buffers of 2 x 4 keys: the next
+// block's keys load while this block is estimated and inserted, C4: 3.46 -> 3.22-3.26 ms,
+// profiles/r02/ab_kv_cand_pipe.txt)
+constexpr int kPrefetch = 4;
 constexpr uint64_t kEmptyKey = ~0ull;
 
 __device__ __forceinline__ bool beats(uint32_t e1, uint64_t k1, uint32_t e2, uint64_t k2) {
@@ -278,11 +253,9 @@ __global__ __launch_bounds__(kKvWG) void k_kv_sketch(KvArgs a) {
     const uint32_t cells = a.depth * a.width;
     for (uint32_t x = threadIdx.x; x < cells; x += kKvWG) cm[x] = 0u;
     __syncthreads();
-#if ZK_KV_SKETCH_PIPE
-    constexpr int U = 4;  // keys per thread per buffer; two buffers alternate
-#else
-    constexpr int U = 8;  // keys per thread in flight
-#endif
+    // two alternating 4-key buffers (C4 sketch 2.00 -> 1.96-1.97 ms; the pass is LDS-atomic-bound,
+    // profiles/r02/ab_kv_sketch_pipe.txt)
+    constexpr int U = 4;
     constexpr uint64_t BS = (uint64_t)kKvWG * U;
     auto load = [&](uint64_t (&k)[U], uint64_t b) {
 #pragma unroll
@@ -291,7 +264,6 @@ __global__ __launch_bounds__(kKvWG) void k_kv_sketch(KvArgs a) {
             k[e] = a.keys[i < hi ? i : lo];
         }
     };
-#if ZK_KV_HOT
     // Under a skewed key distribution several lanes of one atomic instruction hold the same hot key and
     // their adds to the same counters serialise in LDS. Each wave tracks one hot key (wave-uniform):
     // the lanes holding it are counted by a ballot and their first lane adds the count. The hot key
@@ -300,7 +272,6 @@ __global__ __launch_bounds__(kKvWG) void k_kv_sketch(KvArgs a) {
     const int lane = threadIdx.x & 63;
     uint64_t hot = ~0ull;
     int probe = 0;
-#endif
     auto add = [&](const uint64_t (&k)[U], uint64_t b) {
         // row hashes unconditionally, so the loads are not sunk into the conditional (see candidates)
         RowHash rh[U];
@@ -309,7 +280,6 @@ __global__ __launch_bounds__(kKvWG) void k_kv_sketch(KvArgs a) {
 #pragma unroll
         for (int e = 0; e < U; ++e) {
             const bool valid = b + (uint64_t)e * kKvWG + threadIdx.x < hi;
-#if ZK_KV_HOT
             const uint64_t cand = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(k[e] >> 32), probe) << 32) |
                                   (uint32_t)__builtin_amdgcn_readlane((uint32_t)k[e], probe);
             probe = (probe + 1) & 63;
@@ -324,13 +294,8 @@ __global__ __launch_bounds__(kKvWG) void k_kv_sketch(KvArgs a) {
                                     : (valid ? 1u : 0u);
             if (inc)
                 for (uint32_t r = 0; r < a.depth; ++r) atomicAdd(&cm[r * a.width + rh[e].next()], inc);
-#else
-            if (valid)
-                for (uint32_t r = 0; r < a.depth; ++r) atomicAdd(&cm[r * a.width + rh[e].next()], 1u);
-#endif
         }
     };
-#if ZK_KV_SKETCH_PIPE
     uint64_t ka[U], kb[U];
     load(ka, lo);
     for (uint64_t b = lo; b < hi; b += 2 * BS) {
@@ -339,13 +304,6 @@ __global__ __launch_bounds__(kKvWG) void k_kv_sketch(KvArgs a) {
         load(ka, b + 2 * BS);
         add(kb, b + BS);  // past hi: every key is masked
     }
-#else
-    for (uint64_t b = lo; b < hi; b += BS) {
-        uint64_t k[U];
-        load(k, b);
-        add(k, b);
-    }
-#endif
     __syncthreads();
     uint32_t* g = a.cm + (uint64_t)s * cells;
     for (uint32_t x = threadIdx.x; x < cells; x += kKvWG) {
@@ -396,8 +354,7 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
         // estimates unconditionally (clamped keys past the end are harmless): a load whose only
         // uses sit in a conditional block is sunk into it, and then every key waits for HBM
         uint32_t est[J], slot[J];
-#if ZK_KV_ROWS_OUTER
-        {  // rows outer, keys inner: one loop step per row for all J keys
+        {  // rows outer, keys inner: one loop step per row for all J keys (2.86-2.93 -> 2.49-2.52 ms)
             RowHash rh[J];
 #pragma unroll
             for (int j = 0; j < J; ++j) {
@@ -410,30 +367,16 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
 #pragma unroll
                 for (int j = 0; j < J; ++j) est[j] = min(est[j], row[rh[j].next()]);
             }
-            if (ZK_KV_DIAG == 2)
-#pragma unroll
-                for (int j = 0; j < J; ++j) est[j] = (uint32_t)kq[j] | 1u;
         }
-#else
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            const RowHash rh = RowHash::from_hash(kq[j], a.wbits);  // kq: the keys' hashes
-            est[j] = ZK_KV_DIAG == 2 ? (uint32_t)kq[j] | 1u : estimate_rh(cm, a, rh);
-            slot[j] = rh.set;
-        }
-#endif
         const uint32_t has_thr = t.has_thr, thr_est = t.thr_est;
         const uint64_t thr_key = t.thr_key;
         uint32_t need = 0;
-#if ZK_KV_PROBE1
         // the first slot of every key read at once (J independent LDS reads instead of J dependent
         // probe chains): under a skewed distribution most live keys sit in their first slot; only
         // a collision walks on. No insert runs between here and B1, so plain reads are final.
         uint64_t h0[J];
 #pragma unroll
         for (int j = 0; j < J; ++j) h0[j] = t.hk[slot[j]];
-#endif
-#if ZK_KV_PROBE1 == 2
         // Decisions as bit masks (no short-circuit branches: every divergent branch costs the scalar
         // unit exec-mask bookkeeping, and the pass was bound by scalar issue, profiles/r03/
         // ab_kv_candidates.txt). The first two probe slots of every key are read at once; only a
@@ -464,39 +407,12 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
             need |= (lv & (uint32_t)(!special & absent & !hit)) << j;
             slow_m |= (lv & (uint32_t)(special | (!hit & !absent))) << j;
         }
-        if (ZK_KV_DIAG != 0) need = live_m & (uint32_t)(est[0] == 0xFFFFFFFFu);  // (never: keeps est live)
-        if (ZK_KV_DIAG == 0 && slow_m) {
+        if (slow_m) {
 #pragma unroll
             for (int j = 0; j < J; ++j)
                 if (((slow_m >> j) & 1u) && !ts_contains(t, kq[j], kq[j] == kEmptyKey ? slot[j] : (slot[j] + 2) & (kSetCap - 1)))
                     need |= 1u << j;
         }
-#else
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            // a tie with the threshold estimate is decided on the key itself (unhashed only then)
-            const bool live = b + (uint64_t)j * kKvWG + threadIdx.x < hi && est[j] != 0u &&
-                              (!has_thr || est[j] > thr_est ||
-                               (est[j] == thr_est && kv_key(kq[j], a.seeds[0]) < thr_key));
-#if ZK_KV_PROBE1
-            if (ZK_KV_DIAG == 0 && live) {
-                bool in;
-                if (kq[j] == kEmptyKey)
-                    in = ts_contains(t, kq[j], slot[j]);
-                else if (h0[j] == kq[j])
-                    in = true;
-                else if (h0[j] == kEmptyKey)
-                    in = false;
-                else
-                    in = ts_contains(t, kq[j], (slot[j] + 1) & (kSetCap - 1));
-                if (!in) need |= 1u << j;
-            }
-#else
-            if (ZK_KV_DIAG == 0 && live && !ts_contains(t, kq[j], slot[j])) need |= 1u << j;
-#endif
-            if (ZK_KV_DIAG != 0 && live) need |= (est[j] == 0xFFFFFFFFu) << j;  // (never: keeps est live)
-        }
-#endif
         if (need) atomicAdd(&t.pending[parity], (uint32_t)__popc(need));
         __syncthreads();  // B1: survivors counted
         if (threadIdx.x == 0) t.pending[parity ^ 1u] = 0u;  // the previous block's count: read by all before B1
@@ -519,7 +435,6 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
         }
         parity ^= 1u;
     };
-#if ZK_KV_CAND_PIPE
     // two key buffers, alternating: the next block's loads are in flight while this one is
     // estimated and inserted (each buffer is loaded and consumed in fixed places, so nothing is
     // copied across the back edge)
@@ -531,13 +446,6 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
         load_block(ka, b + 2 * BS);
         if (b + BS < hi) run_block(kb, b + BS);
     }
-#else
-    for (uint64_t b = lo; b < hi; b += BS) {
-        uint64_t kq[J];
-        load_block(kq, b);
-        run_block(kq, b);
-    }
-#endif
     const uint32_t n = ts_sort(t, a.seeds[0]);
     uint64_t* ok = a.unit_key + (uint64_t)u * a.cand;
     uint32_t* oe = a.unit_est + (uint64_t)u * a.cand;

@@ -35,6 +35,9 @@ struct zk_kv {
     uint64_t* qkeys = nullptr;  // estimate staging
     uint32_t* qest = nullptr;
     uint64_t qcap = 0;
+    // pinned host mirror for queries: dropped counter, per-service totals, candidate keys and
+    // estimates -- one contiguous copy each instead of strided copies into pageable memory
+    uint8_t* hq = nullptr;
     bool timing = false;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     bool ev_recorded = false;
@@ -62,16 +65,31 @@ uint32_t ilog2(uint32_t x) {
     return r;
 }
 
-zk_status check_state(zk_kv* kv, bool need_totals_ok) {
-    unsigned long long dropped = 0;
-    KV_HIP(kv, hipMemcpyAsync(&dropped, kv->dropped, 8, hipMemcpyDeviceToHost, kv->stream));
-    std::vector<uint64_t> tot(kv->a.S);
+// layout of the pinned query mirror: [dropped u64][totals u64 x S][cand keys u64 x S*cand][cand est u32 x S*cand]
+uint64_t hq_bytes(const KvArgs& a) { return 8 + (uint64_t)a.S * 8 + (uint64_t)a.S * a.cand * 12; }
+uint64_t* hq_totals(zk_kv* k) { return (uint64_t*)(k->hq + 8); }
+uint64_t* hq_keys(zk_kv* k) { return (uint64_t*)(k->hq + 8 + (uint64_t)k->a.S * 8); }
+uint32_t* hq_est(zk_kv* k) { return (uint32_t*)(k->hq + 8 + (uint64_t)k->a.S * 8 + (uint64_t)k->a.S * k->a.cand * 8); }
+
+// dropped counter + totals (+ the candidate lists) into the pinned mirror, one sync, then the
+// state checks every query makes
+zk_status check_state(zk_kv* kv, bool need_totals_ok, bool candidates = false) {
+    if (!kv->hq) KV_HIP(kv, hipHostMalloc((void**)&kv->hq, hq_bytes(kv->a), hipHostMallocDefault));
+    const KvArgs& a = kv->a;
+    KV_HIP(kv, hipMemcpyAsync(kv->hq, kv->dropped, 8, hipMemcpyDeviceToHost, kv->stream));
     if (need_totals_ok)
-        KV_HIP(kv, hipMemcpyAsync(tot.data(), kv->a.totals, tot.size() * 8, hipMemcpyDeviceToHost, kv->stream));
+        KV_HIP(kv, hipMemcpyAsync(hq_totals(kv), a.totals, (size_t)a.S * 8, hipMemcpyDeviceToHost, kv->stream));
+    if (candidates) {
+        KV_HIP(kv, hipMemcpyAsync(hq_keys(kv), a.cand_key, (size_t)a.S * a.cand * 8, hipMemcpyDeviceToHost, kv->stream));
+        KV_HIP(kv, hipMemcpyAsync(hq_est(kv), a.cand_est, (size_t)a.S * a.cand * 4, hipMemcpyDeviceToHost, kv->stream));
+    }
     KV_HIP(kv, hipStreamSynchronize(kv->stream));
+    const uint64_t dropped = *(const uint64_t*)kv->hq;
     if (dropped) return kfail(kv, ZK_ERR_SERVICE_RANGE, std::to_string(dropped) + " items with service_id >= S");
-    for (uint64_t t : tot)
-        if (t >= (1ull << 32)) return kfail(kv, ZK_ERR_CAPACITY, "a service counted >= 2^32 keys since reset");
+    if (need_totals_ok)
+        for (uint32_t s = 0; s < a.S; ++s)
+            if (hq_totals(kv)[s] >= (1ull << 32))
+                return kfail(kv, ZK_ERR_CAPACITY, "a service counted >= 2^32 keys since reset");
     return ZK_OK;
 }
 
@@ -129,6 +147,8 @@ zk_status zk_kv_create(const zk_kv_config* cfg, zk_kv** out) {
     if (e == hipSuccess) e = hipMalloc(&k->dropped, 8);
     if (e == hipSuccess) e = hipMalloc(&k->seg, (uint64_t)(S + 1) * 8);
     if (e == hipSuccess) e = hipMalloc(&k->unit_base, (uint64_t)(S + 1) * 4);
+    // the pinned query mirror up front: a first query must not pay for a pinned allocation
+    if (e == hipSuccess) e = hipHostMalloc((void**)&k->hq, hq_bytes(a), hipHostMallocDefault);
     zk_status st = e == hipSuccess ? zk_kv_reset(k) : ZK_ERR_HIP;
     if (st != ZK_OK) {
         zk_kv_destroy(k);
@@ -148,6 +168,7 @@ zk_status zk_kv_destroy(zk_kv* k) {
                     (void*)k->sorted, (void*)k->seg, (void*)k->unit_base, k->part, (void*)k->unit_key,
                     (void*)k->unit_est, k->stage, (void*)k->qkeys, (void*)k->qest})
         if (p) hipFree(p);
+    if (k->hq) hipHostFree(k->hq);
     for (hipEvent_t ev : k->ev)
         if (ev) hipEventDestroy(ev);
     if (k->own_stream && k->stream) hipStreamDestroy(k->stream);
@@ -289,12 +310,12 @@ zk_status zk_kv_topk_all(zk_kv* k, uint32_t kk, uint64_t* keys, uint32_t* est, u
     if (kk == 0 || kk > k->a.cand || !keys || !est) return kfail(k, ZK_ERR_INVALID_ARG, "k must be in 1..candidates");
     const KvArgs& a = k->a;
     KV_HIP(k, hipSetDevice(k->device));
-    KV_HIP(k, hipMemcpy2DAsync(keys, (size_t)kk * 8, a.cand_key, (size_t)a.cand * 8, (size_t)kk * 8, a.S,
-                               hipMemcpyDeviceToHost, k->stream));
-    KV_HIP(k, hipMemcpy2DAsync(est, (size_t)kk * 4, a.cand_est, (size_t)a.cand * 4, (size_t)kk * 4, a.S,
-                               hipMemcpyDeviceToHost, k->stream));
-    zk_status st = check_state(k, true);  // syncs
+    zk_status st = check_state(k, true, true);  // syncs; the candidate lists are in the pinned mirror
     if (st != ZK_OK) return st;
+    for (uint32_t s = 0; s < a.S; ++s) {
+        memcpy(keys + (uint64_t)s * kk, hq_keys(k) + (uint64_t)s * a.cand, (size_t)kk * 8);
+        memcpy(est + (uint64_t)s * kk, hq_est(k) + (uint64_t)s * a.cand, (size_t)kk * 4);
+    }
     if (count)
         for (uint32_t s = 0; s < a.S; ++s) {
             uint32_t c = 0;

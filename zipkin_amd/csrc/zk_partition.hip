@@ -18,10 +18,6 @@ namespace {
 
 constexpr int kPartWG = 256;
 constexpr int kPartU = 4;  // items per thread per iteration (loads issued before the LDS atomics)
-#ifndef ZK_PART_HIST_PIPE
-// histogram: two alternating load buffers (C4 partition 6.95 -> 6.77 ms, profiles/r02/ab_part_hist_pipe.txt)
-#define ZK_PART_HIST_PIPE 1
-#endif
 
 // range of workgroup w: a slice of one flat array (counts == nullptr) or list w of the lists form
 __device__ __forceinline__ void part_range(uint64_t n, uint64_t per, const uint32_t* counts, uint64_t* lo,
@@ -62,7 +58,7 @@ __global__ __launch_bounds__(kPartWG) void k_part_hist(const uint32_t* __restric
                 ++bad;
         }
     };
-#if ZK_PART_HIST_PIPE
+    // two alternating load buffers (C4 partition 6.95 -> 6.77 ms, profiles/r02/ab_part_hist_pipe.txt)
     // two alternating buffers: one block's loads are in flight while the other is counted
     uint32_t va[kPartU], vb[kPartU];
     load(va, lo);
@@ -72,13 +68,6 @@ __global__ __launch_bounds__(kPartWG) void k_part_hist(const uint32_t* __restric
         load(va, b + 2 * BS);
         count(vb, b + BS);  // past hi: every entry is the 0xFFFFFFFF sentinel and i >= hi
     }
-#else
-    for (uint64_t b = lo; b < hi; b += BS) {
-        uint32_t v[kPartU];
-        load(v, b);
-        count(v, b);
-    }
-#endif
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < S; i += kPartWG) hist[(uint64_t)i * grid + blockIdx.x] = h[i];
     if (bad) atomicAdd(dropped, (unsigned long long)bad);
@@ -118,12 +107,8 @@ __global__ __launch_bounds__(kPartWG) void k_part_scatter(const uint32_t* __rest
 // 8-byte pieces of 500 interleaved streams, ~8x write amplification). Same pattern as K2
 // (zk_reduce.hip k_link_scatter), with the service taken from its own column.
 constexpr uint32_t kLineMaxS = 1024;
-#ifndef ZK_PART_U
-#define ZK_PART_U 8      // items per thread per chunk (line scatter): 8192-item chunks (4: 1.80 -> 1.43 ms on C4)
-#endif
-#ifndef ZK_PART_WG
-#define ZK_PART_WG 1024  // line-scatter workgroup (512 threads x 4 items: 2.38 -> 1.76 ms on C4)
-#endif
+constexpr int kLineU = 8;      // items per thread per chunk (line scatter): 8192-item chunks (4: 1.80 -> 1.43 ms on C4)
+constexpr int kLineWG = 1024;  // line-scatter workgroup (512 threads x 4 items: 2.38 -> 1.76 ms on C4)
 // Items per output line: 8 = 64 bytes. 128-byte lines (7168-item chunks, so that the S x 128 B carry
 // fits) measured 8.99-9.03 ms against 6.93-7.00 ms for the C4 partition (profiles/r02/ab_part_lines.txt).
 constexpr int kLineItems = 8;
@@ -248,7 +233,7 @@ __global__ __launch_bounds__(WG) void k_part_scatter_lines(const uint32_t* __res
     }
 }
 
-// The scatter with write streams shared per XCD (flat input, S <= kLineMaxS; ZK_PART_XCD): the
+// The scatter with write streams shared per XCD (flat input, S <= kLineMaxS): the
 // input is cut into P <= 8 portions (groups of the histogram's workgroup ranges) and every
 // service's output range into P sub-ranges, one per portion. Workgroups start on their XCD's
 // portion (HW_REG_XCC_ID), take chunks of 8192 items in order, counting-sort a chunk by service
@@ -258,17 +243,8 @@ __global__ __launch_bounds__(WG) void k_part_scatter_lines(const uint32_t* __res
 // grid x S streams apart and need LDS carries for whole lines). A workgroup whose portion is
 // drained takes chunks of the others: placement changes only speed. Same pattern as the
 // clustering pass (zk_cluster.hip k_cl_xscatter, profiles/r03/ab_cluster_writes.txt).
-#ifndef ZK_PART_XCD
-#define ZK_PART_XCD 1
-#endif
 constexpr uint32_t kPartParts = 8;
-#ifndef ZK_PX_WG
-#define ZK_PX_WG 1024  // XCD scatter workgroup (chunks of 8 items per thread)
-#endif
-#ifndef ZK_PX_GRID
-#define ZK_PX_GRID 1   // XCD scatter workgroups per CU
-#endif
-constexpr int kPxWG = ZK_PX_WG;
+constexpr int kPxWG = 1024;  // XCD scatter workgroup (chunks of 8 items per thread), one per CU
 constexpr int kPxU = 8;
 constexpr uint32_t kPxChunk = kPxWG * kPxU;
 
@@ -308,92 +284,11 @@ __global__ void k_part_xprep(const uint32_t* __restrict__ offs, uint32_t S, uint
     }
 }
 
-__global__ __launch_bounds__(kPxWG, kPxWG / 256) void k_part_xscatter(PartX a) {
-    constexpr int BPT = (kLineMaxS + kPxWG - 1) / kPxWG;  // services per thread in the scan
-    __shared__ uint32_t s_cnt[kLineMaxS];  // items of the chunk per service
-    __shared__ uint32_t s_off[kLineMaxS];  // exclusive offsets in the sorted chunk
-    __shared__ uint32_t s_cur[kLineMaxS];  // output position of the chunk's run of each service
-    __shared__ uint64_t s_sorted[kPxChunk];
-    __shared__ uint16_t s_svc[kPxChunk];
-    __shared__ uint32_t s_tmp[32];
-    __shared__ uint32_t s_job;
-    const int t = threadIdx.x;
-    const uint32_t S = a.S;
-    const uint32_t p0 = xcc_id() % a.parts;
-    for (uint32_t b = t; b < S; b += kPxWG) s_cnt[b] = 0u;
-    for (uint32_t step = 0; step < a.parts;) {
-        const uint32_t p = (p0 + step) % a.parts;
-        __syncthreads();  // the previous chunk is done with s_job and the counts
-        if (t == 0) s_job = atomicAdd(&a.next[p], 1u);
-        __syncthreads();
-        const uint32_t j = s_job;
-        if (j >= a.part_tiles[p + 1] - a.part_tiles[p]) {  // drained: the next portion
-            ++step;
-            continue;
-        }
-        const uint64_t lo = a.part_lo[p] + (uint64_t)j * kPxChunk;
-        const uint64_t e = a.part_lo[p + 1];
-        const uint64_t hi = lo + kPxChunk < e ? lo + kPxChunk : e;
-        uint64_t v[kPxU];
-        uint32_t bk[kPxU], rank[kPxU];
-#pragma unroll
-        for (int k = 0; k < kPxU; ++k) {
-            const uint64_t i = lo + t + (uint64_t)kPxWG * k;
-            bk[k] = a.svc[i < hi ? i : lo];
-            v[k] = a.payload[i < hi ? i : lo];
-        }
-#pragma unroll
-        for (int k = 0; k < kPxU; ++k) {
-            if (lo + t + (uint64_t)kPxWG * k >= hi) bk[k] = 0xFFFFFFFFu;
-            if (a.hash) v[k] = sk_mix64(v[k] ^ a.hash_seed);
-            rank[k] = bk[k] < S ? atomicAdd(&s_cnt[bk[k]], 1u) : 0u;
-        }
-        __syncthreads();
-        uint32_t cnt;
-        {
-            uint32_t h[BPT], sum = 0;
-#pragma unroll
-            for (int q = 0; q < BPT; ++q) {
-                const uint32_t bin = t * BPT + q;
-                h[q] = bin < S ? s_cnt[bin] : 0u;
-                sum += h[q];
-            }
-            uint32_t ex = block_excl_scan<kPxWG / 64>(sum, s_tmp, &cnt);
-#pragma unroll
-            for (int q = 0; q < BPT; ++q) {
-                const uint32_t bin = t * BPT + q;
-                if (bin < S) {
-                    s_off[bin] = ex;
-                    s_cur[bin] = h[q] ? atomicAdd(&a.cursor[(uint64_t)p * S + bin], h[q]) : 0u;
-                }
-                ex += h[q];
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < kPxU; ++k)
-            if (bk[k] < S) {
-                const uint32_t q = s_off[bk[k]] + rank[k];
-                s_sorted[q] = v[k];
-                s_svc[q] = (uint16_t)bk[k];
-            }
-        __syncthreads();
-        for (uint32_t i = t; i < cnt; i += kPxWG) {
-            const uint32_t b = s_svc[i];
-            a.out[s_cur[b] + (i - s_off[b])] = s_sorted[i];
-        }
-        for (uint32_t b = t; b < S; b += kPxWG) s_cnt[b] = 0u;  // read by this thread only after the barrier above
-    }
-}
-
-// ZK_PART_XSTATIC: the same scatter with portion p's chunks taken in a static stride by the blocks
-// dispatched to XCD p (block i runs on XCD i % 8), so no chunk claim is needed, and the next chunk's
-// services and payloads loaded while this chunk is placed and stored: per chunk, the claim and the
-// load round trips left the critical path (only the cursor claims' round trip stays on it).
-#ifndef ZK_PART_XSTATIC
-#define ZK_PART_XSTATIC 1
-#endif
-__global__ __launch_bounds__(kPxWG, ZK_PX_GRID * kPxWG / 256) void k_part_xscatter_static(PartX a) {
+// Portion p's chunks are taken in a static stride by the blocks dispatched to XCD p (block i runs on
+// XCD i % 8), so no chunk claim is needed, and the next chunk's services and payloads load while this
+// chunk is placed and stored: per chunk, the claim and the load round trips left the critical path
+// (only the cursor claims' round trip stays on it; 5.41 -> 5.11-5.14 ms against claimed chunks).
+__global__ __launch_bounds__(kPxWG, kPxWG / 256) void k_part_xscatter_static(PartX a) {
     constexpr int BPT = (kLineMaxS + kPxWG - 1) / kPxWG;  // services per thread in the scan
     __shared__ uint32_t s_cnt[kLineMaxS];  // items of the chunk per service
     __shared__ uint32_t s_off[kLineMaxS];  // exclusive offsets in the sorted chunk
@@ -581,12 +476,12 @@ hipError_t partition_impl(const PartitionPlan& p, const uint32_t* svc, const uin
     // carry fit one CU (S <= 1022 at 8192-item chunks; S = 1024 faulted in round 2, before any
     // check), else item by item
     uint32_t st_lines = 0, st_items = 0, mt = 0;
-    e = kernel_attrs((const void*)k_part_scatter_lines<ZK_PART_U, ZK_PART_WG>, &st_lines, &mt);
+    e = kernel_attrs((const void*)k_part_scatter_lines<kLineU, kLineWG>, &st_lines, &mt);
     if (e == hipSuccess) e = kernel_attrs((const void*)k_part_scatter, &st_items, &mt);
     if (e != hipSuccess) return e;
     uint64_t dyn = 0;
     const int choice = partition_scatter_choice(p.S, st_lines, st_items, &dyn);
-    if (ZK_PART_XCD && !counts && p.S <= kLineMaxS && n > 0) {
+    if (!counts && p.S <= kLineMaxS && n > 0) {
         uint8_t* xp = (uint8_t*)temp + temp_bytes;
         PartX x{};
         x.svc = svc;
@@ -595,7 +490,7 @@ hipError_t partition_impl(const PartitionPlan& p, const uint32_t* svc, const uin
         x.S = p.S;
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const uint32_t gx = (uint32_t)(cus > 0 ? cus : 256) * (ZK_PART_XSTATIC ? ZK_PX_GRID : 1);
+        const uint32_t gx = (uint32_t)(cus > 0 ? cus : 256);
         // every portion needs a workgroup: the static scatter gives portion q to blocks q, q + parts, ...
         x.parts = p.grid < kPartParts ? p.grid : kPartParts;
         if (x.parts > gx) x.parts = gx;
@@ -612,13 +507,11 @@ hipError_t partition_impl(const PartitionPlan& p, const uint32_t* svc, const uin
         e = launch_checked("k_part_xprep", k_part_xprep, dim3((x.parts * p.S + 255) / 256), dim3(256), 0, s,
                            (const uint32_t*)offs, p.S, p.grid, x.parts, p.per_wg, n, x.cursor, part_lo, part_tiles, next);
         if (e == hipSuccess) {
-            e = ZK_PART_XSTATIC ? launch_checked("k_part_xscatter_static", k_part_xscatter_static, dim3(gx), dim3(kPxWG), 0,
-                                                 s, x)
-                                : launch_checked("k_part_xscatter", k_part_xscatter, dim3(gx), dim3(kPxWG), 0, s, x);
+            e = launch_checked("k_part_xscatter_static", k_part_xscatter_static, dim3(gx), dim3(kPxWG), 0, s, x);
         }
     } else if (choice == kScatterLines)
-        e = launch_checked("k_part_scatter_lines", k_part_scatter_lines<ZK_PART_U, ZK_PART_WG>, dim3(p.grid),
-                           dim3(ZK_PART_WG), dyn, s, svc, payload, n, p.per_wg, counts, p.S, p.grid, offs, out, hash,
+        e = launch_checked("k_part_scatter_lines", k_part_scatter_lines<kLineU, kLineWG>, dim3(p.grid),
+                           dim3(kLineWG), dyn, s, svc, payload, n, p.per_wg, counts, p.S, p.grid, offs, out, hash,
                            hash_seed);
     else
         e = launch_checked("k_part_scatter", k_part_scatter, dim3(p.grid), dim3(kPartWG), dyn, s, svc, payload, n,

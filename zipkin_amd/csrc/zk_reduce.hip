@@ -10,34 +10,9 @@
 #include "zk_internal.h"
 #include "zk_launch.h"
 
-#ifndef ZK_K2_U
-#define ZK_K2_U 8      // links per thread per K2 chunk
-#endif
-#ifndef ZK_K2_WG
-#define ZK_K2_WG 1024  // K2 workgroup: 8192-link chunks (512 threads: 0.236 -> 0.199 ms on C2)
-#endif
-#ifndef ZK_K2_REMAP
-// K2: list groups in XCD-major order. Same box, clustered C2 kernels (profiles/r03/ab_k2_xcd.txt):
-// K2 0.221 -> 0.217 ms, K3 0.149 -> 0.143 ms
-#define ZK_K2_REMAP 1
-#endif
-#ifndef ZK_K3_GUARD
-#define ZK_K3_GUARD 1  // K3: skip zero chunk updates
-#endif
-#ifndef ZK_K3_PACK
-#define ZK_K3_PACK 1   // K3: m0 and S1 of a short link in one packed LDS add
-#endif
-// GUARD + PACK, same box, interleaved, serial steps (profiles/r02/ab_k3pack_serial.txt): K2 + K3
-// 0.454 -> 0.405 ms, step 1.815 -> 1.766 ms
-#ifndef ZK_K3_U
-#define ZK_K3_U 4      // links per thread per K3 iteration
-#endif
-#ifndef ZK_K3_WIDE
-#define ZK_K3_WIDE 1   // K3: 42-bit pieces, 6 LDS atomics per short link (k_bucket_lds_reduce_wide)
-#endif
-#ifndef ZK_K3_PREFETCH
-#define ZK_K3_PREFETCH 1  // K3: load the next iteration's links before this one's atomics
-#endif
+constexpr int kK2U = 8;      // links per thread per K2 chunk
+constexpr int kK2WG = 1024;  // K2 workgroup: 8192-link chunks (512 threads: 0.236 -> 0.199 ms on C2)
+constexpr int kK3U = 4;      // links per thread per K3 iteration (the next iteration's links prefetched)
 
 namespace zk {
 namespace {
@@ -137,15 +112,12 @@ __global__ __launch_bounds__(WG) void k_link_scatter(ReduceArgs r, uint32_t lpw)
     __shared__ uint64_t s_sorted[C];
     __shared__ uint32_t s_tmp[32];
     extern __shared__ __attribute__((aligned(16))) uint64_t s_carry[];  // [nb][kScatterLine]
-#if ZK_K2_REMAP
     // XCD-aware order (dispatch puts block i on XCD i % 8): the blocks of one XCD take consecutive
     // list groups, so the per-bucket ranges of neighbouring lists (which share their boundary
-    // lines) are written through one L2
+    // lines) are written through one L2. Same box, clustered C2 (profiles/r03/ab_k2_xcd.txt): K2
+    // 0.221 -> 0.217 ms, K3 0.149 -> 0.143 ms
     const uint32_t gx = gridDim.x / 8, gr = gridDim.x % 8, xi = blockIdx.x % 8;
     const uint32_t w = (xi * gx + (xi < gr ? xi : gr) + blockIdx.x / 8) * lpw;  // first list of the group
-#else
-    const uint32_t w = blockIdx.x * lpw;  // first list of the group
-#endif
     const uint32_t nl = (r.lists - w) < lpw ? (r.lists - w) : lpw;
     const int tid = threadIdx.x;
     constexpr int BPT = (kMaxBuckets + WG - 1) / WG;  // buckets per thread in the scan
@@ -444,131 +416,11 @@ __global__ __launch_bounds__(1 << CB_SHIFT) void k_bucket_reduce(ReduceArgs r, u
     }
 }
 
-// K3, LDS-atomic form: one bucket per workgroup. Every link adds its 32-bit-chunk contributions to
-// the bucket's limb table in LDS with non-returning 64-bit LDS atomics -- no counting sort, no
-// per-chunk barriers and no run-length imbalance (every thread handles the same number of links).
-// Limb-major table [15][CB]: lanes with random cells spread over the banks. d < 2^32 (durations
-// under 71 minutes) touches 11 limbs; a longer d touches all 15.
-template <int CB_SHIFT, int WG, int U>
-__global__ __launch_bounds__(WG) void k_bucket_lds_reduce(ReduceArgs r, uint32_t splits) {
-    constexpr int CB = 1 << CB_SHIFT;
-    constexpr int ROWS = ZK_K3_PACK ? 16 : 15;
-    // row stride CB + 1: the 16 limbs of one cell fall in distinct banks, so the flush below can read
-    // a cell's limbs with 16 adjacent lanes and write the 128-byte cell whole
-    constexpr int RS = CB + 1;
-    __shared__ unsigned long long s_t[ROWS * RS];
-    const int tid = threadIdx.x;
-    const uint32_t b = blockIdx.x / splits, part = blockIdx.x % splits;
-    for (int x = tid; x < ROWS * RS; x += WG) s_t[x] = 0ull;
-    const uint64_t lo = r.bucket_base[b], hi = r.bucket_base[b + 1];
-    const uint64_t per = (hi - lo + splits - 1) / splits;
-    const uint64_t s0 = lo + per * part;
-    const uint64_t s1 = (s0 + per < hi) ? s0 + per : hi;
-    const uint64_t cell0 = (uint64_t)b << CB_SHIFT;
-    // packed row (ZK_K3_PACK): a link with d < 2^21 adds 2^42 + d to row 15 instead of 1 to m0 and d
-    // to S1; with < 2^20 links in the part the row holds m0 in bits 42.. and S1 below (< 2^41)
-    const bool packable = ZK_K3_PACK && (s1 - s0) < (1ull << 20);
-    constexpr uint64_t M = 0xFFFFFFFFull;
-#if ZK_K3_PREFETCH
-    // the next iteration's links are in flight while this one's LDS atomics run (one K3 wave of
-    // ~2 workgroups per CU cannot hide an HBM round trip per iteration otherwise)
-    uint64_t nxt[U];
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-        const uint64_t i = s0 + tid + (uint64_t)k * WG;
-        nxt[k] = i < s1 ? r.sorted[i] : ~0ull;
-    }
-#endif
-    __syncthreads();
-    for (uint64_t base = s0; base < s1; base += (uint64_t)WG * U) {
-        uint64_t v[U];
-#if ZK_K3_PREFETCH
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-            v[k] = nxt[k];
-            const uint64_t i = base + (uint64_t)WG * U + tid + (uint64_t)k * WG;
-            nxt[k] = i < s1 ? r.sorted[i] : ~0ull;
-        }
-#else
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-            const uint64_t i = base + tid + (uint64_t)k * WG;
-            v[k] = i < s1 ? r.sorted[i] : ~0ull;
-        }
-#endif
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-            if (v[k] == ~0ull) continue;
-            const uint32_t c = (uint32_t)((v[k] >> 40) - cell0);
-            const uint64_t d = v[k] & (kMaxDuration - 1);
-            unsigned long long* t = s_t + c;
-            if ((d >> 32) == 0) {
-                const uint64_t d2 = d * d;                                   // < 2^64
-                const unsigned __int128 d3 = (unsigned __int128)d2 * d;       // < 2^96
-                const unsigned __int128 d4 = (unsigned __int128)d2 * d2;      // < 2^128
-                const uint64_t d3lo = (uint64_t)d3, d4lo = (uint64_t)d4, d4hi = (uint64_t)(d4 >> 64);
-#if ZK_K3_GUARD
-                // the high chunks are zero for short durations (d < 2^16: d^2 >> 32, d^4 >> 64; d <
-                // 2^21: d^3 >> 64, d^4 >> 96): masked lanes skip the LDS update, an all-zero wave
-                // skips the instruction
-#define ZK_K3_ADD(q, x)                                             \
-    do {                                                            \
-        const uint64_t x_ = (x);                                    \
-        if (x_) atomicAdd(&t[(q) * RS], (unsigned long long)x_);    \
-    } while (0)
-#else
-#define ZK_K3_ADD(q, x) atomicAdd(&t[(q) * RS], (unsigned long long)(x))
-#endif
-                if (packable && d < (1ull << 21)) {
-                    atomicAdd(&t[15 * RS], (1ull << 42) | d);
-                } else {
-                    atomicAdd(&t[kLimbM0 * RS], 1ull);
-                    ZK_K3_ADD(kLimbS1, d);
-                }
-                ZK_K3_ADD(kLimbS2 + 0, d2 & M);
-                ZK_K3_ADD(kLimbS2 + 1, d2 >> 32);
-                ZK_K3_ADD(kLimbS3 + 0, d3lo & M);
-                ZK_K3_ADD(kLimbS3 + 1, d3lo >> 32);
-                ZK_K3_ADD(kLimbS3 + 2, (uint64_t)(d3 >> 64));
-                ZK_K3_ADD(kLimbS4 + 0, d4lo & M);
-                ZK_K3_ADD(kLimbS4 + 1, d4lo >> 32);
-                ZK_K3_ADD(kLimbS4 + 2, d4hi & M);
-                ZK_K3_ADD(kLimbS4 + 3, d4hi >> 32);
-#undef ZK_K3_ADD
-            } else {
-                atomicAdd(&t[kLimbM0 * RS], 1ull);
-#pragma unroll
-                for (int q = 1; q < 15; ++q) {
-                    const uint64_t x = limb_value(q, d);
-                    if (x) atomicAdd(&t[q * RS], (unsigned long long)x);
-                }
-            }
-        }
-    }
-    __syncthreads();
-    // flush: lane group of 16 = one cell, lane q = limb q, so a wave reads and writes 4 whole 128-byte
-    // cells (one thread per cell wrote 64 lines 8 bytes at a time: 3.6x WRITE_SIZE over the table)
-    static_assert(kLimbs == 16, "a cell is 16 limbs");
-    for (int x = tid; x < CB * kLimbs; x += WG) {
-        const int c = x >> 4, q = x & 15;
-        const uint64_t cell = cell0 + c;
-        if (cell >= r.cells || q == 15) continue;
-        uint64_t v = s_t[q * RS + c];
-        if constexpr (ZK_K3_PACK) {
-            const uint64_t x15 = (q <= kLimbS1) ? s_t[15 * RS + c] : 0ull;
-            if (q == kLimbM0) v += x15 >> 42;
-            if (q == kLimbS1) v += x15 & ((1ull << 42) - 1);  // S1's low limb may exceed 32 bits: value-exact
-        }
-        if (!v) continue;
-        uint64_t* dst = r.table + cell * kLimbs + q;
-        if (splits == 1)
-            *dst += v;  // this workgroup owns the cell
-        else
-            atomicAdd((unsigned long long*)dst, (unsigned long long)v);
-    }
-}
-
-// K3, wide rows (ZK_K3_WIDE): the same LDS-atomic reduce with fewer atomics per link. Each power
+// K3 (cell buckets of 512): one bucket per workgroup; every link adds its contributions to the
+// bucket's table in LDS with non-returning 64-bit LDS atomics -- no counting sort, no per-chunk
+// barriers and no run-length imbalance (every thread handles the same number of links); the next
+// iteration's links are in flight while this one's atomics run (profiles/r02/ab_k3lds.txt: equal to
+// the counting-sort K3 serially, pipelined steps 1.63 -> 1.57 ms). Wide rows (round 3): fewer atomics per link. Each power
 // sum is kept as 42-bit pieces instead of 32-bit chunks -- S1 one piece, S2 two, S3 three, S4 four,
 // each row summing < 2^42 per link over a sub-part of < 2^20 links (< 2^62) -- and a link with d <
 // 2^21 adds m0 and S1 as one packed word (2^42 + d): 6 LDS atomics for such a link (d^2 < 2^42 is one
@@ -600,23 +452,23 @@ __global__ __launch_bounds__(WG) void k_bucket_lds_reduce_wide(ReduceArgs r, uin
     for (uint64_t s0 = p0; s0 < p1 || s0 == p0; s0 += kSub) {
         const uint64_t s1 = (s0 + kSub < p1) ? s0 + kSub : p1;
         for (int x = tid; x < ROWS * RS; x += WG) s_t[x] = 0ull;
-        uint64_t nxt[ZK_K3_U];
+        uint64_t nxt[kK3U];
 #pragma unroll
-        for (int k = 0; k < ZK_K3_U; ++k) {
+        for (int k = 0; k < kK3U; ++k) {
             const uint64_t i = s0 + tid + (uint64_t)k * WG;
             nxt[k] = i < s1 ? r.sorted[i] : ~0ull;
         }
         __syncthreads();
-        for (uint64_t base = s0; base < s1; base += (uint64_t)WG * ZK_K3_U) {
-            uint64_t v[ZK_K3_U];
+        for (uint64_t base = s0; base < s1; base += (uint64_t)WG * kK3U) {
+            uint64_t v[kK3U];
 #pragma unroll
-            for (int k = 0; k < ZK_K3_U; ++k) {
+            for (int k = 0; k < kK3U; ++k) {
                 v[k] = nxt[k];
-                const uint64_t i = base + (uint64_t)WG * ZK_K3_U + tid + (uint64_t)k * WG;
+                const uint64_t i = base + (uint64_t)WG * kK3U + tid + (uint64_t)k * WG;
                 nxt[k] = i < s1 ? r.sorted[i] : ~0ull;
             }
 #pragma unroll
-            for (int k = 0; k < ZK_K3_U; ++k) {
+            for (int k = 0; k < kK3U; ++k) {
                 if (v[k] == ~0ull) continue;
                 const uint32_t c = (uint32_t)((v[k] >> 40) - cell0);
                 const uint64_t d = v[k] & (kMaxDuration - 1);
@@ -724,23 +576,15 @@ __global__ __launch_bounds__(WG) void k_bucket_lds_reduce_wide(ReduceArgs r, uin
 
 }  // namespace
 
-#ifndef ZK_K3_LDS
-// 1 (default): K3 as LDS atomics (k_bucket_lds_reduce); 0: counting sort + owner sums
-// (k_bucket_reduce). Same box, interleaved (profiles/r02/ab_k3lds.txt): serial steps equal
-// (K2 + K3 0.45 ms either way), pipelined steps 1.63 -> 1.57 ms.
-#define ZK_K3_LDS 1
-#endif
-
-#ifndef ZK_CB_MIN_SHIFT
-#define ZK_CB_MIN_SHIFT 9  // smallest cell bucket: 2^9 cells (2^8: 977 buckets at S = 500, measured
-                           // 0.46 -> 0.53 ms for K2 + K3: K2's per-bucket LDS carry doubles)
-#endif
+// smallest cell bucket: 2^9 cells (2^8: 977 buckets at S = 500, measured 0.46 -> 0.53 ms for
+// K2 + K3: K2's per-bucket LDS carry doubles)
+constexpr uint32_t kCbMinShift = 9;
 
 void bucket_geometry(uint32_t S, uint32_t* nb, uint32_t* cb_shift) {
     const uint64_t cells = (uint64_t)S * S;
     *nb = 0;
     *cb_shift = 0;
-    for (uint32_t sh = ZK_CB_MIN_SHIFT; sh <= 10; ++sh) {
+    for (uint32_t sh = kCbMinShift; sh <= 10; ++sh) {
         const uint64_t n = (cells + (1ull << sh) - 1) >> sh;
         if (n <= kMaxBuckets) {
             *nb = (uint32_t)n;
@@ -767,27 +611,14 @@ hipError_t launch_partitioned_reduce(const ReduceArgs& r, hipStream_t s) {
     uint32_t lpw = (r.lists + 1023) / 1024;
     if (lpw > (uint32_t)kScatterMaxLPW) lpw = kScatterMaxLPW;
     const uint32_t k2_grid = (r.lists + lpw - 1) / lpw;
-    e = launch_checked("k_link_scatter", k_link_scatter<ZK_K2_U, ZK_K2_WG>, dim3(k2_grid), dim3(ZK_K2_WG),
+    e = launch_checked("k_link_scatter", k_link_scatter<kK2U, kK2WG>, dim3(k2_grid), dim3(kK2WG),
                        (size_t)r.nb * kScatterLine * 8, s, r, lpw);
     if (e != hipSuccess) return e;
     const uint32_t splits = r.nb >= 256 ? 1u : (512u + r.nb - 1) / r.nb;
-#if ZK_K3_LDS
-    if (r.cb_shift == 8)
-        return launch_checked("k_bucket_lds_reduce<8>", k_bucket_lds_reduce<8, 256, ZK_K3_U>, dim3(r.nb * splits),
-                              dim3(256), 0, s, r, splits);
-    if (r.cb_shift == 9) {
-        if (ZK_K3_WIDE)
-            return launch_checked("k_bucket_lds_reduce_wide<9>", k_bucket_lds_reduce_wide<9, 512>,
-                                  dim3(r.nb * splits), dim3(512), 0, s, r, splits);
-        return launch_checked("k_bucket_lds_reduce<9>", k_bucket_lds_reduce<9, 512, ZK_K3_U>, dim3(r.nb * splits),
-                              dim3(512), 0, s, r, splits);
-    }
-#endif
-    // CB = 512: 512 threads, 4096-link chunks (36 KB LDS); CB = 1024: 1024 threads, 4096-link chunks
-    if (r.cb_shift == 8)
-        return launch_checked("k_bucket_reduce<8>", k_bucket_reduce<8, 16>, dim3(r.nb * splits), dim3(256), 0, s, r, splits);
+    // buckets of 512 cells (S <= 724): the LDS-atomic K3; of 1024 cells: the counting-sort K3
     if (r.cb_shift == 9)
-        return launch_checked("k_bucket_reduce<9>", k_bucket_reduce<9, 8>, dim3(r.nb * splits), dim3(512), 0, s, r, splits);
+        return launch_checked("k_bucket_lds_reduce_wide<9>", k_bucket_lds_reduce_wide<9, 512>, dim3(r.nb * splits),
+                              dim3(512), 0, s, r, splits);
     return launch_checked("k_bucket_reduce<10>", k_bucket_reduce<10, 4>, dim3(r.nb * splits), dim3(1024), 0, s, r, splits);
 }
 

@@ -50,11 +50,8 @@ __device__ __forceinline__ uint32_t bytewise_max(uint32_t a, uint32_t b) {
     return r;
 }
 
-// ZK_RT_SKETCH_PIPE: two alternating load buffers, as in the KV passes. C5 step within noise
-// (pipelined 1.43-1.46 vs 1.44-1.47 ms, serial equal: profiles/r02/ab_rt_sketch_pipe.txt), so off.
-#ifndef ZK_RT_SKETCH_PIPE
-#define ZK_RT_SKETCH_PIPE 0
-#endif
+// (two alternating load buffers, as in the KV passes, measured within noise: pipelined C5 1.43-1.46
+// vs 1.44-1.47 ms, serial equal, profiles/r02/ab_rt_sketch_pipe.txt -- one buffer kept)
 __global__ __launch_bounds__(kRtWG) void k_rt_sketch(RtArgs a) {
     extern __shared__ uint32_t lds[];
     const uint32_t R = 1u << a.p;        // registers per service
@@ -89,23 +86,11 @@ __global__ __launch_bounds__(kRtWG) void k_rt_sketch(RtArgs a) {
             atomicAdd(&s_bin[rt_bin(d, a.m)], 1u);
         }
     };
-#if ZK_RT_SKETCH_PIPE
-    // two alternating buffers: one block's loads are in flight while the other is added
-    uint64_t va[U], vb[U];
-    load(va, lo);
-    for (uint64_t b = lo; b < hi; b += 2 * BS) {
-        load(vb, b + BS);
-        add(va, b);
-        load(va, b + 2 * BS);
-        add(vb, b + BS);  // past hi: every item is masked
-    }
-#else
     for (uint64_t b = lo; b < hi; b += BS) {
         uint64_t v[U];
         load(v, b);
         add(v, b);
     }
-#endif
     __syncthreads();
     uint32_t* g_reg = (uint32_t*)(a.regs + (uint64_t)s * R);
     for (uint32_t x = threadIdx.x; x < (R >> 2); x += kRtWG) {

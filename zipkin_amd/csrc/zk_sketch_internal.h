@@ -68,10 +68,7 @@ hipError_t launch_unit_plan(const uint64_t* seg, uint32_t S, uint64_t unit_items
 constexpr uint32_t kKvMaxWidth = 4096;   // counters per row per service (LDS: depth*width*4 B)
 constexpr uint32_t kKvMaxDepth = 8;
 constexpr uint32_t kKvMaxCand = 256;     // candidates kept per service
-#ifndef ZK_KV_UNIT_ITEMS
-#define ZK_KV_UNIT_ITEMS 65536
-#endif
-constexpr uint64_t kKvUnitItems = ZK_KV_UNIT_ITEMS;  // keys per workgroup in the sketch / candidate passes
+constexpr uint64_t kKvUnitItems = 65536;  // keys per workgroup in the sketch / candidate passes
 
 struct KvArgs {
     uint32_t S, width, depth, wbits, cand;
