@@ -35,7 +35,7 @@ struct zk_ctx {
     unsigned long long* stats = nullptr;  // kStatShards*ST_N
     unsigned long long* h_stats = nullptr;  // pinned host copy of stats
     hipEvent_t ev_stats = nullptr;          // recorded after the stats copy (polled, not slept on)
-    unsigned int* spill_count = nullptr;  // [0] spilled traces, [1] K1's guided range counter
+    unsigned int* spill_count = nullptr;
     uint64_t* spill_list = nullptr;
     uint64_t spill_cap = 0;
     uint8_t* spill_scratch = nullptr;
@@ -518,13 +518,12 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
         if (vs != ZK_OK) return vs;
     }
     uint32_t grid = 0;
-    uint64_t per_wg = 0, stride = 0, chunk_max = 0;
-    uint32_t chunk_level = 0;
-    join_geometry(n, c->cus, &grid, &per_wg, &stride, &chunk_max, &chunk_level);
+    uint64_t per_wg = 0, stride = 0;
+    join_geometry(n, c->cus, &grid, &per_wg, &stride);
     zk_status st = ensure_spill(c, n);
     if (st == ZK_OK) st = ensure_links(c, grid, stride, n);
     if (st != ZK_OK) return st;
-    ZK_HIP(c, hipMemsetAsync(c->spill_count, 0, 8, c->stream));  // spill count, K1's range counter
+    ZK_HIP(c, hipMemsetAsync(c->spill_count, 0, 4, c->stream));
     JoinArgs a{};
     a.c = d;
     a.table = c->table;
@@ -540,9 +539,6 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
     a.link_count = c->link_count;
     a.link_stride = stride;
     a.per_wg = per_wg;
-    a.chunk_next = c->spill_count + 1;
-    a.chunk_max = chunk_max;
-    a.chunk_level = chunk_level;
     a.grid = grid;
     a.hist = c->hist;
     a.nb = c->nb;

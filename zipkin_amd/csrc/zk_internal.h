@@ -102,10 +102,6 @@ struct JoinArgs {
     // persistent K1 geometry: workgroup w owns traces starting in [w*per_wg, (w+1)*per_wg)
     uint64_t per_wg;
     uint32_t grid;
-    // guided range schedule (ZK_K1_GUIDED): ranges are claimed with chunk_next (zeroed per launch)
-    unsigned int* chunk_next;
-    uint64_t chunk_max;
-    uint32_t chunk_level;
     // cell-bucket histogram per K1 workgroup, bucket-major (hist[b * grid + w]); nb = 0 disables it
     uint32_t* hist;
     uint32_t nb;
@@ -126,8 +122,7 @@ struct JoinArgs {
 hipError_t launch_join(const JoinArgs& a, hipStream_t s);
 uint64_t join_tile_records();   // TILE (records per K1 window)
 // K1 launch geometry for n records on a device with `cus` compute units
-void join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, uint64_t* link_stride,
-                   uint64_t* chunk_max, uint32_t* chunk_level);
+void join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, uint64_t* link_stride);
 hipError_t launch_link_reduce(const uint64_t* links, const uint32_t* counts, uint64_t stride, uint64_t tiles,
                               uint64_t* table, hipStream_t s);
 // partitioned reduce (no global atomics): hist -> offsets -> bucket-sorted links -> LDS reduce

@@ -219,22 +219,6 @@ __device__ __forceinline__ void ld2_u32(const uint32_t* __restrict__ p, uint64_t
     v[1] = x.y;
 }
 
-// Start of range k of the guided schedule (even): per_level ranges of chunk_max records, then
-// per_level of half that, ... down to kChunkMin, then kChunkMin until n. Uniform scalar arithmetic.
-constexpr uint64_t kChunkMin = 8192;
-__host__ __device__ __forceinline__ uint64_t join_chunk_start(uint64_t k, uint64_t chunk_max, uint64_t per_level,
-                                                              uint64_t n) {
-    uint64_t base = 0, sz = chunk_max;
-    while (sz > kChunkMin && k >= per_level) {
-        base += per_level * sz;
-        k -= per_level;
-        sz = ((sz >> 1) + 1) & ~1ull;
-        if (sz < kChunkMin) sz = kChunkMin;
-    }
-    const uint64_t r = base + k * sz;
-    return r < n ? r : n;
-}
-
 // K1 stat counters: the per-thread 16-bit pack (StatPack) is folded into the workgroup's u32 LDS
 // totals every kFoldWindows windows (a lane adds <= 2 per stat per window, so a wave sum of 64
 // lanes stays below 2^16), and the totals go to a sharded global slot once at the end.
@@ -364,11 +348,6 @@ __device__ __forceinline__ void load_late(const JoinArgs& a, uint64_t ws, Window
 // =============================================================================================
 // MODE bits: kModeJoin = the dependency path (parent join, links); kModeEmit = one sketch item
 // per merged valid span with a service (zk_rt.hip). The product dependency pass is kModeJoin.
-// ZK_K1_GUIDED: a persistent grid (one workgroup per resident slot) claims record ranges from a guided
-// schedule instead of owning one fixed range per workgroup (ZK_K1_GRID_MULT x the resident slots)
-#ifndef ZK_K1_GUIDED
-#define ZK_K1_GUIDED 1
-#endif
 constexpr int kModeJoin = 1;
 constexpr int kModeEmit = 2;
 template <int TILE, int WG, int MODE>
@@ -386,12 +365,10 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     __shared__ __align__(16) uint64_t s_mask[NWORD];
     __shared__ uint32_t s_stat[ST_N];
     __shared__ uint64_t s_cursor;  // links (low 32) and sketch items (high 32) appended so far
-    __shared__ uint32_t s_claim;   // the range just claimed (ZK_K1_GUIDED)
     __shared__ uint32_t s_hist[kMaxBuckets];  // links per cell bucket (K2's scatter offsets)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t n = a.c.n;
-#if !ZK_K1_GUIDED
     const uint64_t R0 = (uint64_t)blockIdx.x * a.per_wg;
     if (R0 >= n) {
         if (tid == 0) {
@@ -402,7 +379,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         return;
     }
     const uint64_t R1 = (R0 + a.per_wg < n) ? R0 + a.per_wg : n;
-#endif
     uint64_t* __restrict__ out = a.links + (uint64_t)blockIdx.x * a.link_stride;
     const uint64_t trash = a.link_stride - 1;  // never a real link slot (join_geometry)
     uint64_t* __restrict__ it_pay = a.rt_pay + (uint64_t)blockIdx.x * a.link_stride;
@@ -422,23 +398,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     for (int x = tid; x < H / 4; x += WG) reinterpret_cast<uint4*>(s_ht)[x] = make_uint4(0u, 0u, 0u, 0u);
     uint64_t m_ev, m_od;  // this wave's boundary ballots of the current window (uniform; phase 3 reuses them)
     ZK_STAMP_DECL
-#if ZK_K1_GUIDED
-    // ranges claimed from a guided schedule (join_chunk_start): large ones first, then halving, so
-    // the workgroups run out of work within a small range of each other. A workgroup stops claiming
-    // when its link list could not take another range (join_geometry sizes the lists for 2x the
-    // even share, so the ranges are always all claimed).
-    for (;;) {
-    if (tid == 0) {
-        // (the other waves' last appends may still be landing: TILE more of slack)
-        const bool room = (uint64_t)(uint32_t)s_cursor + a.chunk_max + 2 * TILE + 2 <= a.link_stride;
-        s_claim = room ? atomicAdd(a.chunk_next, 1u) : 0xFFFFFFFFu;
-    }
-    __syncthreads();
-    const uint32_t claim = s_claim;
-    const uint64_t R0 = claim == 0xFFFFFFFFu ? n : join_chunk_start(claim, a.chunk_max, a.chunk_level, n);
-    if (R0 >= n) break;
-    const uint64_t R1 = join_chunk_start(claim + 1, a.chunk_max, a.chunk_level, n);
-#endif
     uint64_t ws = R0;         // window start (even)
     uint64_t seek = R0;       // first record that may start one of our traces
     bool seek_start = false;  // seek is known to be a trace start (uniform)
@@ -810,9 +769,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         // from this window's reads (phases 2-3, before the barrier that ends phase 3)
         ZK_STAMP(7);
     }
-#if ZK_K1_GUIDED
-    }  // ranges
-#endif
     ZK_STAMP_FLUSH();
     __syncthreads();  // every wave's last append is in the cursor
     const uint32_t nout = (uint32_t)s_cursor;
@@ -1119,29 +1075,16 @@ extern "C" int zk_debug_stamps(unsigned long long* out, int reset) {
 }
 #endif
 
-void join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, uint64_t* link_stride,
-                   uint64_t* chunk_max, uint32_t* chunk_level) {
+void join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, uint64_t* link_stride) {
     const uint64_t windows = (n + kTile - 1) / kTile;
-#if ZK_K1_GUIDED
-    // persistent: one workgroup per resident slot; ranges from the guided schedule. The first level
-    // hands out a quarter of the batch in chunks of n / (4 g); a list holds twice the even share plus
-    // one more range, so a workgroup that stops claiming for want of room leaves the rest to others
-    uint64_t g = (uint64_t)cus * ZK_K1_WGS_PER_CU;
-    if (g > windows) g = windows ? windows : 1;
-    uint64_t cm = (n / (4 * g) + 1) & ~1ull;
-    if (cm < kChunkMin) cm = kChunkMin;
-    *grid = (uint32_t)g;
-    *chunk_max = cm;
-    *chunk_level = (uint32_t)g;
-    *per_wg = cm;
-    *link_stride = 2 * ((n + g - 1) / g) + cm + 2 * kTile + 2;
-#else
 #ifndef ZK_K1_GRID_MULT
 // workgroups per resident slot (1: persistent, every workgroup resident at once). 4: a quarter of
 // the range per workgroup, so the last workgroups' imbalance is smaller and a K1 launch shares the
 // chip gracefully with the other table set's K2/K3 (same box, interleaved, profiles/r02/
 // ab_grid_mult_overlap.txt: serial K1 1.226 -> 1.187 ms, two-set step with full overlap 1.63-1.68 ->
-// 1.56-1.57 ms; 8: slower). K2 walks 4 lists per workgroup, so its grid stays 1024.
+// 1.56-1.57 ms; 8: slower). A persistent grid claiming ranges from a guided schedule instead:
+// K1 alone -0.6 %, pipelined step +3.7 % (profiles/r04/ab_k1_guided.txt). K2 walks 4 lists per
+// workgroup, so its grid stays 1024.
 #define ZK_K1_GRID_MULT 4
 #endif
     uint64_t g = (uint64_t)cus * ZK_K1_WGS_PER_CU * ZK_K1_GRID_MULT;  // <= 128 VGPRs, <= 40 KB LDS per WG
@@ -1149,10 +1092,6 @@ void join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, u
     const uint64_t per = ((n + g - 1) / g + kTile - 1) / kTile * kTile;
     *grid = (uint32_t)g;
     *per_wg = per ? per : kTile;
-    *chunk_max = 0;
-    *chunk_level = 0;
     // a workgroup's last trace may overhang its range by < TILE; then the trash slot of K1's stores
     *link_stride = *per_wg + kTile + 1;
-#endif
-}
-}  // namespace zk
+}}  // namespace zk
