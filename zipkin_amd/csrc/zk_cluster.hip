@@ -11,11 +11,11 @@
 //   P0 k_cl_hist     per-workgroup LDS histogram of the first digit (top hash bits) of a contiguous
 //                    input range; one exclusive scan (hipcub) of the digit-major matrix gives every
 //                    (digit, workgroup) pair a disjoint output range
-//   P1 k_cl_scatter  each workgroup re-reads its range in chunks of 8192 records: digits ranked in
+//   P1 k_cl_xscatter each workgroup re-reads its range in chunks of 8192 records: digits ranked in
 //      <global>      LDS (atomic counting sort), then column by column the chunk is loaded
 //                    coalesced, staged in LDS in digit order and written as per-digit runs at the
 //                    ranges' cursors
-//   P2 k_cl_scatter  one workgroup per first-level bucket: an LDS histogram of the second digit over
+//   P2 k_cl_xscatter one workgroup per first-level bucket: an LDS histogram of the second digit over
 //      <local>       the bucket, its scan (the sub-bucket bounds), then the same chunked scatter
 //                    inside the bucket
 //   P3 k_cl_traces   one workgroup per sub-bucket (~1k records): an LDS hash table of the
@@ -112,48 +112,11 @@ __global__ void k_cl_bounds(const uint32_t* __restrict__ offs, uint32_t nd, uint
     if (d == nd) base[nd] = (uint32_t)n;
 }
 
-// ---- P1 / P2: chunked LDS-staged scatter ---------------------------------------------------------
-#ifndef ZK_CL_SCWG
-#define ZK_CL_SCWG 1024
-#endif
-constexpr int kScWG = ZK_CL_SCWG;
-#ifndef ZK_CL_SCU
-#define ZK_CL_SCU 8
-#endif
-// diagnostic builds only (results wrong): 1 = every chunk written contiguously at its own input
-// position (the scatter's structure without its scattered stores), 2 = no column stores
-#ifndef ZK_CL_DIAG
-#define ZK_CL_DIAG 0
-#endif
-#ifndef ZK_CL_SC_GRID
-#define ZK_CL_SC_GRID 1  // P0/P1 workgroups per CU
-#endif
-constexpr int kScU = ZK_CL_SCU;
-constexpr int kScChunk = kScWG * kScU;  // 8192 records per chunk
+// ---- P1 / P2 helpers ---------------------------------------------------------------------------
 constexpr uint32_t kMaxDigits = 2048;   // <= 11 bits per level
 // levels of <= 256 digits (8 bits: every level up to 2^24 records) run a variant with byte digit
-// tags and 3 KB of digit arrays (75 KB of LDS instead of 104 KB). Two such workgroups per CU need
-// <= 64 VGPRs, which spills (52 B/lane): 9.07 ms for the clustering pass at 1e8 against 8.65 ms at
-// one workgroup per CU (profiles/r03/ab_cluster.txt)
+// tags and smaller digit arrays
 constexpr uint32_t kSmallDigits = 256;
-#ifndef ZK_CL_SMALL_GRID
-#define ZK_CL_SMALL_GRID 1  // P0/P1 workgroups per CU when the first level has <= 256 digits (2: 64 VGPRs, spills)
-#endif
-
-struct ScatterArgs {
-    SpanColsDev in;  // in.n = records of the whole batch
-    SpanColsMut out;
-    // global (P1): workgroup w owns [w * per, ...) and its digit cursors start at offs[d * grid + w]
-    uint64_t per;
-    uint32_t grid;
-    const uint32_t* offs;
-    // local (P2): workgroup b owns bucket [bucket[b], bucket[b + 1]) and writes its sub-bucket
-    // bounds to sub[b * nd + d] (and sub[nbuckets * nd] = n)
-    const uint32_t* bucket;
-    uint32_t nbuckets;
-    uint32_t* sub;
-    uint32_t shift, nd;  // digit = (hash >> shift) & (nd - 1)
-};
 
 // column C (0..6) of a batch: the u64 columns first, then service_id and flags (u32)
 template <int C>
@@ -201,7 +164,7 @@ __device__ __forceinline__ void move_columns(const SpanColsDev& in, const SpanCo
 #pragma unroll
     for (int k = 0; k < U; ++k) {
         const uint32_t i = t + k * WG;
-        if (ZK_CL_DIAG != 2 && i < cnt) col_store<C>(out, dest[k], stage[i]);
+        if (i < cnt) col_store<C>(out, dest[k], stage[i]);
     }
     __syncthreads();
     if constexpr (C < 6) move_columns<U, WG, C + 1>(in, out, base, cnt, pos, dest, stage, v);
@@ -230,303 +193,11 @@ __device__ __forceinline__ void scan_digits(const uint32_t* s_cnt, uint32_t nd, 
     }
 }
 
-template <bool LOCAL, uint32_t MAXD>
-__global__ __launch_bounds__(kScWG, (MAXD <= 256 ? ZK_CL_SMALL_GRID : ZK_CL_SC_GRID) * kScWG / 256) void k_cl_scatter(ScatterArgs a) {
-    using DigT = typename std::conditional<(MAXD <= 256), uint8_t, uint16_t>::type;
-    __shared__ uint32_t s_cur[MAXD];  // output position of each digit's next record
-    __shared__ uint32_t s_cnt[MAXD];  // records of the chunk per digit
-    __shared__ uint32_t s_off[MAXD];  // exclusive offsets of the digits inside the sorted chunk
-    __shared__ DigT s_dig[kScChunk];  // digit of the sorted chunk's record i
-    __shared__ __align__(16) uint64_t s_stage[kScChunk];
-    __shared__ uint32_t s_tmp[32];
-    const int t = threadIdx.x;
-    const uint32_t nd = a.nd, mask = nd - 1;
-    uint64_t lo, hi;
-    if constexpr (LOCAL) {
-        lo = a.bucket[blockIdx.x];
-        hi = a.bucket[blockIdx.x + 1];
-        // sweep 1: the bucket's histogram of the second digit, then the sub-bucket bounds
-        for (uint32_t d = t; d < nd; d += kScWG) s_cnt[d] = 0u;
-        __syncthreads();
-        for (uint64_t b = lo; b < hi; b += (uint64_t)kScChunk) {
-            uint64_t v[kScU];
-#pragma unroll
-            for (int k = 0; k < kScU; ++k) {
-                const uint64_t i = b + t + (uint64_t)k * kScWG;
-                v[k] = a.in.trace_id[i < hi ? i : lo];
-            }
-#pragma unroll
-            for (int k = 0; k < kScU; ++k)
-                if (b + t + (uint64_t)k * kScWG < hi) atomicAdd(&s_cnt[digit_of(part_hash(v[k]), a.shift, mask)], 1u);
-        }
-        __syncthreads();
-        scan_digits<kScWG, MAXD>(s_cnt, nd, (uint32_t)lo, s_cur, s_tmp);
-        __syncthreads();
-        for (uint32_t d = t; d < nd; d += kScWG) a.sub[(uint64_t)blockIdx.x * nd + d] = s_cur[d];
-        if (blockIdx.x == a.nbuckets - 1 && t == 0) a.sub[(uint64_t)a.nbuckets * nd] = (uint32_t)a.in.n;
-    } else {
-        lo = (uint64_t)blockIdx.x * a.per;
-        hi = lo + a.per < a.in.n ? lo + a.per : a.in.n;
-        for (uint32_t d = t; d < nd; d += kScWG) s_cur[d] = a.offs[(uint64_t)d * a.grid + blockIdx.x];
-    }
-    for (uint32_t d = t; d < nd; d += kScWG) s_cnt[d] = 0u;
-    __syncthreads();
-    for (uint64_t base = lo; base < hi; base += kScChunk) {
-        const uint32_t cnt = (uint32_t)(hi - base < (uint64_t)kScChunk ? hi - base : (uint64_t)kScChunk);
-        // 1. digits and ranks (LDS atomic counting sort: the order inside a digit is free)
-        uint32_t dg[kScU], rank[kScU];
-        uint64_t tids[kScU];
-#pragma unroll
-        for (int k = 0; k < kScU; ++k) {
-            const uint32_t j = t + k * kScWG;
-            tids[k] = a.in.trace_id[base + (j < cnt ? j : 0)];
-        }
-#pragma unroll
-        for (int k = 0; k < kScU; ++k) {
-            dg[k] = digit_of(part_hash(tids[k]), a.shift, mask);
-            rank[k] = (t + k * kScWG < cnt) ? atomicAdd(&s_cnt[dg[k]], 1u) : 0u;
-        }
-        __syncthreads();
-        // 2. digit offsets inside the chunk
-        scan_digits<kScWG, MAXD>(s_cnt, nd, 0u, s_off, s_tmp);
-        __syncthreads();
-        // 3. sorted position of each loaded record; digit of each sorted slot
-        uint32_t pos[kScU];
-        uint32_t dest[kScU];  // (record positions fit 32 bits: the bounds are u32)
-#pragma unroll
-        for (int k = 0; k < kScU; ++k) {
-            pos[k] = s_off[dg[k]] + rank[k];
-            if (t + k * kScWG < cnt) s_dig[pos[k]] = (DigT)dg[k];
-        }
-        __syncthreads();
-        // 4. output position of each sorted slot this thread writes
-#pragma unroll
-        for (int k = 0; k < kScU; ++k) {
-            const uint32_t i = t + k * kScWG;
-            const uint32_t d = i < cnt ? s_dig[i] : 0u;
-            dest[k] = i < cnt ? s_cur[d] + (i - s_off[d]) : 0u;
-            if (ZK_CL_DIAG == 1) dest[k] = (uint32_t)base + i;
-        }
-        // 5. the columns through the LDS stage (the traceIds are in registers already)
-        {
-            uint64_t v[kScU];
-#pragma unroll
-            for (int k = 0; k < kScU; ++k) v[k] = tids[k];
-            move_columns<kScU, kScWG, 0>(a.in, a.out, base, cnt, pos, dest, s_stage, v);
-        }
-        // 6. advance the cursors and clear the counts (move_columns' last barrier orders every
-        //    read of s_cur / s_off / s_cnt above before these writes)
-        for (uint32_t d = t; d < nd; d += kScWG) {
-            s_cur[d] += s_cnt[d];
-            s_cnt[d] = 0u;
-        }
-        __syncthreads();
-    }
-}
-
-// ---- P1 / P2 with write-combining carries (levels of <= 256 digits) -------------------------------
-// k_cl_scatter writes each chunk's per-digit runs as they fall: at 32 records per digit per chunk
-// both ends of every run are partial 64-B segments, and the 256 x 7 open tails of a workgroup are
-// evicted from L2 before the next chunk completes them (1.1 ms of a 3.0 ms pass,
-// profiles/r03/ab_cluster_writes.txt). Here every (digit, column) keeps the records of its last
-// incomplete 64-B segment in LDS: a chunk writes a digit's run only up to the last segment boundary
-// (plus the carried head of the segment it completes, in the same phase), and the rest becomes the
-// new carry. The head of a digit's range (not segment-aligned) and the tails at the end are the
-// only partial segments. 152 KB of LDS: one 1024-thread workgroup per CU, chunks of 4096 records.
-#ifndef ZK_CL_WC
-#define ZK_CL_WC 1  // 0: the round-2/3 scatter (runs written as they fall)
-#endif
-constexpr int kWcWG = 1024;
-constexpr int kWcU = 4;
-constexpr int kWcChunk = kWcWG * kWcU;
-constexpr uint32_t kWcDigits = 256;
-
-struct WcLds {
-    uint64_t stage[kWcChunk];        // the chunk's current column in digit order
-    uint64_t c64[5][kWcDigits][8];   // carries of the u64 columns (8 per 64-B segment)
-    uint32_t c32[2][kWcDigits][16];  // carries of the u32 columns (16 per segment)
-    uint32_t cur[kWcDigits];         // output position of each digit's next record
-    uint32_t cnt[kWcDigits];         // records of the chunk per digit
-    uint32_t off[kWcDigits];         // exclusive offsets of the digits inside the sorted chunk
-    uint32_t rs[kWcDigits];          // start of each digit's output range (not segment-aligned)
-    uint8_t dig[kWcChunk];           // digit of the sorted chunk's record i
-    uint32_t tmp[32];
-};
-
-template <int C>
-__device__ __forceinline__ void carry_put(WcLds& L, uint32_t d, uint32_t s, uint64_t v) {
-    if constexpr (C < 5)
-        L.c64[C][d][s] = v;
-    else
-        L.c32[C - 5][d][s] = (uint32_t)v;
-}
-template <int C>
-__device__ __forceinline__ uint64_t carry_get(const WcLds& L, uint32_t d, uint32_t s) {
-    if constexpr (C < 5)
-        return L.c64[C][d][s];
-    else
-        return L.c32[C - 5][d][s];
-}
-
-// the carried records of column C whose segment is complete (final: every carried record) go out
-template <int C, bool FINAL>
-__device__ __forceinline__ void carry_flush(const WcLds& L, const SpanColsMut& out, uint32_t nd) {
-    constexpr uint32_t E = C < 5 ? 8u : 16u;
-    for (uint32_t q = threadIdx.x; q < nd * E; q += kWcWG) {
-        const uint32_t d = q / E, s = q % E;
-        const uint32_t c = L.cur[d], seg = c & ~(E - 1u);
-        const uint32_t A = L.rs[d] > seg ? L.rs[d] : seg;
-        const uint32_t x = seg + s;
-        const uint32_t Z = FINAL ? c : (c + L.cnt[d]) & ~(E - 1u);
-        if (x >= A && x < c && x < Z) col_store<C>(out, x, carry_get<C>(L, d, s));
-    }
-}
-
-template <int C>
-__device__ __forceinline__ void move_columns_wc(const SpanColsDev& in, const SpanColsMut& out, uint64_t base,
-                                                uint32_t cnt, uint32_t nd, const uint32_t (&pos)[kWcU],
-                                                const uint32_t (&dest)[kWcU], const uint32_t (&dd)[kWcU], WcLds& L,
-                                                uint64_t (&v)[kWcU]) {
-    constexpr uint32_t E = C < 5 ? 8u : 16u;
-    const int t = threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < kWcU; ++k)
-        if (t + k * kWcWG < cnt) L.stage[pos[k]] = v[k];
-    __syncthreads();
-    if constexpr (C < 6) {
-#pragma unroll
-        for (int k = 0; k < kWcU; ++k) {  // the next column, in flight during this column's stores
-            const uint32_t j = t + k * kWcWG;
-            v[k] = col_load<C + 1>(in, base + (j < cnt ? j : 0));
-        }
-    }
-    uint64_t cv[kWcU];
-    uint32_t cs[kWcU];
-    bool hc[kWcU];
-#pragma unroll
-    for (int k = 0; k < kWcU; ++k) {
-        const uint32_t i = t + k * kWcWG;
-        hc[k] = false;
-        cv[k] = 0;
-        cs[k] = 0;
-        if (i < cnt) {
-            const uint32_t d = dd[k];
-            const uint32_t Z = (L.cur[d] + L.cnt[d]) & ~(E - 1u);
-            const uint64_t val = L.stage[i];
-            if (dest[k] < Z) {
-                col_store<C>(out, dest[k], val);
-            } else {
-                hc[k] = true;
-                cv[k] = val;
-                cs[k] = dest[k] & (E - 1u);
-            }
-        }
-    }
-    carry_flush<C, false>(L, out, nd);
-    __syncthreads();  // the old carries are read before the new ones overwrite their slots
-#pragma unroll
-    for (int k = 0; k < kWcU; ++k)
-        if (hc[k]) carry_put<C>(L, dd[k], cs[k], cv[k]);
-    if constexpr (C < 6) move_columns_wc<C + 1>(in, out, base, cnt, nd, pos, dest, dd, L, v);
-}
-
-template <int C>
-__device__ __forceinline__ void carry_flush_all(const WcLds& L, const SpanColsMut& out, uint32_t nd) {
-    carry_flush<C, true>(L, out, nd);
-    if constexpr (C < 6) carry_flush_all<C + 1>(L, out, nd);
-}
-
-template <bool LOCAL>
-__global__ __launch_bounds__(kWcWG, kWcWG / 256) void k_cl_scatter_wc(ScatterArgs a) {
-    __shared__ WcLds L;
-    const int t = threadIdx.x;
-    const uint32_t nd = a.nd, mask = nd - 1;
-    uint64_t lo, hi;
-    if constexpr (LOCAL) {
-        lo = a.bucket[blockIdx.x];
-        hi = a.bucket[blockIdx.x + 1];
-        // sweep 1: the bucket's histogram of the second digit, then the sub-bucket bounds
-        for (uint32_t d = t; d < nd; d += kWcWG) L.cnt[d] = 0u;
-        __syncthreads();
-        for (uint64_t b = lo; b < hi; b += (uint64_t)kWcChunk) {
-            uint64_t v[kWcU];
-#pragma unroll
-            for (int k = 0; k < kWcU; ++k) {
-                const uint64_t i = b + t + (uint64_t)k * kWcWG;
-                v[k] = a.in.trace_id[i < hi ? i : lo];
-            }
-#pragma unroll
-            for (int k = 0; k < kWcU; ++k)
-                if (b + t + (uint64_t)k * kWcWG < hi) atomicAdd(&L.cnt[digit_of(part_hash(v[k]), a.shift, mask)], 1u);
-        }
-        __syncthreads();
-        scan_digits<kWcWG, kWcDigits>(L.cnt, nd, (uint32_t)lo, L.cur, L.tmp);
-        __syncthreads();
-        for (uint32_t d = t; d < nd; d += kWcWG) a.sub[(uint64_t)blockIdx.x * nd + d] = L.cur[d];
-        if (blockIdx.x == a.nbuckets - 1 && t == 0) a.sub[(uint64_t)a.nbuckets * nd] = (uint32_t)a.in.n;
-    } else {
-        lo = (uint64_t)blockIdx.x * a.per;
-        hi = lo + a.per < a.in.n ? lo + a.per : a.in.n;
-        for (uint32_t d = t; d < nd; d += kWcWG) L.cur[d] = a.offs[(uint64_t)d * a.grid + blockIdx.x];
-    }
-    for (uint32_t d = t; d < nd; d += kWcWG) {
-        L.cnt[d] = 0u;
-        L.rs[d] = L.cur[d];
-    }
-    __syncthreads();
-    for (uint64_t base = lo; base < hi; base += kWcChunk) {
-        const uint32_t cnt = (uint32_t)(hi - base < (uint64_t)kWcChunk ? hi - base : (uint64_t)kWcChunk);
-        // 1. digits and ranks (LDS atomic counting sort: the order inside a digit is free)
-        uint32_t dg[kWcU], rank[kWcU];
-        uint64_t v[kWcU];
-#pragma unroll
-        for (int k = 0; k < kWcU; ++k) {
-            const uint32_t j = t + k * kWcWG;
-            v[k] = a.in.trace_id[base + (j < cnt ? j : 0)];
-        }
-#pragma unroll
-        for (int k = 0; k < kWcU; ++k) {
-            dg[k] = digit_of(part_hash(v[k]), a.shift, mask);
-            rank[k] = (t + k * kWcWG < cnt) ? atomicAdd(&L.cnt[dg[k]], 1u) : 0u;
-        }
-        __syncthreads();
-        // 2. digit offsets inside the chunk
-        scan_digits<kWcWG, kWcDigits>(L.cnt, nd, 0u, L.off, L.tmp);
-        __syncthreads();
-        // 3. sorted position of each loaded record; digit of each sorted slot
-        uint32_t pos[kWcU];
-#pragma unroll
-        for (int k = 0; k < kWcU; ++k) {
-            pos[k] = L.off[dg[k]] + rank[k];
-            if (t + k * kWcWG < cnt) L.dig[pos[k]] = (uint8_t)dg[k];
-        }
-        __syncthreads();
-        // 4. digit and output position of each sorted slot this thread writes
-        uint32_t dest[kWcU], dd[kWcU];
-#pragma unroll
-        for (int k = 0; k < kWcU; ++k) {
-            const uint32_t i = t + k * kWcWG;
-            dd[k] = i < cnt ? L.dig[i] : 0u;
-            dest[k] = i < cnt ? L.cur[dd[k]] + (i - L.off[dd[k]]) : 0u;
-        }
-        // 5. the columns through the LDS stage and the carries (the traceIds are in registers)
-        move_columns_wc<0>(a.in, a.out, base, cnt, nd, pos, dest, dd, L, v);
-        __syncthreads();  // every carry of this chunk is in place before the cursors move
-        // 6. advance the cursors and clear the counts
-        for (uint32_t d = t; d < nd; d += kWcWG) {
-            L.cur[d] += L.cnt[d];
-            L.cnt[d] = 0u;
-        }
-        __syncthreads();
-    }
-    // the tail of every digit's range
-    carry_flush_all<0>(L, a.out, nd);
-}
-
-// ---- P1 / P2 with streams shared per XCD (ZK_CL_XCD) ---------------------------------------------
-// In k_cl_scatter(_wc) every workgroup owns one output range per digit: 256 workgroups x 256
-// digits x 7 columns of write streams ~12 KB apart, and a run's partial tail line waits for the
-// same workgroup's next chunk. Here the input is cut into P <= 8 portions, and a digit's output
+// ---- P1 / P2 with streams shared per XCD ----------------------------------------------------------
+// With one output range per (workgroup, digit) -- the round-2/3 scatter and its write-combining
+// successor, removed after round 3 -- 256 workgroups x 256 digits x 7 columns of write streams sit
+// ~12 KB apart, and a run's partial tail line waits for the same workgroup's next chunk
+// (profiles/r03/ab_cluster_writes.txt: 2.73 / 2.97 ms per pass vs 2.05 / 1.97 here). Here the input is cut into P <= 8 portions, and a digit's output
 // range is cut into P sub-ranges, one per portion; a chunk of portion p claims its runs at the
 // portion's shared cursors (one global atomic per digit of the chunk). Workgroups start on the
 // portion of their XCD (HW_REG_XCC_ID) and take chunks in order, so at any moment the ~32
@@ -539,18 +210,9 @@ __global__ __launch_bounds__(kWcWG, kWcWG / 256) void k_cl_scatter_wc(ScatterArg
 //   P2: portion p = the first-level buckets b = p, p + P, ...; a chunk lies inside one bucket and
 //       claims its runs at the bucket's sub-bucket cursors (the scanned (bucket, digit) histogram
 //       of P2h, which also gives the sub-bucket bounds).
-#ifndef ZK_CL_XCD
-#define ZK_CL_XCD 1  // 0: the per-workgroup-range scatter (k_cl_scatter_wc)
-#endif
 constexpr uint32_t kParts = 8;
-#ifndef ZK_CL_XS_U
-#define ZK_CL_XS_U 8     // records per thread per P1/P2 chunk
-#endif
-#ifndef ZK_CL_XS_GRID
-#define ZK_CL_XS_GRID 1  // P1/P2 workgroups per CU
-#endif
-constexpr int kXsWG = 1024;
-constexpr int kXsU = ZK_CL_XS_U;
+constexpr int kXsWG = 1024;  // one P1/P2 workgroup per CU (2 or 4 smaller ones: 3.77 / 4.60 ms per pass)
+constexpr int kXsU = 8;      // records per thread per P1/P2 chunk
 constexpr uint32_t kXsChunk = kXsWG * kXsU;
 
 struct XArgs {
@@ -680,7 +342,7 @@ __global__ void k_cl_xsub(const uint32_t* __restrict__ scanned, uint64_t m, uint
 }
 
 template <bool LOCAL, uint32_t MAXD>
-__global__ __launch_bounds__(kXsWG, ZK_CL_XS_GRID * kXsWG / 256) void k_cl_xscatter(XArgs a) {
+__global__ __launch_bounds__(kXsWG, kXsWG / 256) void k_cl_xscatter(XArgs a) {
     using DigT = typename std::conditional<(MAXD <= 256), uint8_t, uint16_t>::type;
     __shared__ uint32_t s_cur[MAXD];  // output position of the chunk's run of each digit
     __shared__ uint32_t s_cnt[MAXD];  // records of the chunk per digit
@@ -752,13 +414,8 @@ __global__ __launch_bounds__(kXsWG, ZK_CL_XS_GRID * kXsWG / 256) void k_cl_xscat
 
 // ---- P3: trace runs inside each sub-bucket --------------------------------------------------------
 constexpr int kTrWG = 512;
-#ifndef ZK_CL_TR_SLOTS
-#define ZK_CL_TR_SLOTS 2048
-#endif
-#ifndef ZK_CL_TR_GRID
-#define ZK_CL_TR_GRID 2  // P3 workgroups per CU
-#endif
-constexpr uint32_t kTrSlots = ZK_CL_TR_SLOTS;  // LDS trace table: load <= 1/2 at <= kTrSlots / 2 records per round
+constexpr uint32_t kTrGrid = 2;  // P3 workgroups per CU
+constexpr uint32_t kTrSlots = 2048;  // LDS trace table: load <= 1/2 at <= kTrSlots / 2 records per round
 constexpr uint64_t kEmptyKey = ~0ull;  // a traceId equal to it takes the extra slot kTrSlots
 constexpr int kTrFast = 4096;          // sub-buckets up to this many records: the LDS-staged path
 constexpr int kTrStage = 2 * kTrFast;  // s_cur words: the fast path's u64 column stage aliases it
@@ -1049,7 +706,7 @@ uint64_t align256(uint64_t b) { return (b + 255) & ~255ull; }
 
 size_t scan_bytes(uint64_t m) {
     size_t b = 0;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)m);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)m);
     return b;
 }
 
@@ -1083,13 +740,13 @@ ClusterPlan cluster_plan(uint64_t n, uint32_t cus) {
     }
     p.nb1 = 1u << p.b1;
     p.nb2 = 1u << p.b2;
-    // P0/P1 geometry: about one resident 1024-thread workgroup per CU, whole chunks each
-    uint64_t g = (uint64_t)(cus ? cus : 256) * (p.nb1 <= kSmallDigits ? ZK_CL_SMALL_GRID : ZK_CL_SC_GRID);
-    const uint64_t chunks = (n + kScChunk - 1) / kScChunk;
+    // P0 geometry (the ranges P1's portions are cut from): one range per CU, whole chunks each
+    uint64_t g = (uint64_t)(cus ? cus : 256);
+    const uint64_t chunks = (n + kXsChunk - 1) / kXsChunk;
     if (g > chunks) g = chunks ? chunks : 1;
     p.grid = (uint32_t)g;
-    p.per = ((n + g - 1) / g + kScChunk - 1) / kScChunk * kScChunk;
-    if (!p.per) p.per = kScChunk;
+    p.per = ((n + g - 1) / g + kXsChunk - 1) / kXsChunk * kXsChunk;
+    if (!p.per) p.per = kXsChunk;
     return p;
 }
 
@@ -1171,17 +828,9 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
                        bucket);
     if (e != hipSuccess) return e;
     // P1: in -> A (first-level buckets)
-    ScatterArgs a{};
-    a.in = in;
-    a.out = A;
-    a.per = p.per;
-    a.grid = p.grid;
-    a.offs = offs;
-    a.shift = sh1;
-    a.nd = p.nb1;
     const uint32_t parts1 = p.grid < kParts ? p.grid : kParts;
     XArgs x1{};
-    if (ZK_CL_XCD) {
+    {
         x1.in = in;
         x1.out = A;
         x1.shift = sh1;
@@ -1195,18 +844,11 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
                            (const uint32_t*)offs, p.nb1, p.grid, parts1, p.per, n, cursor1, part_lo, part_tiles, xnext);
         if (e != hipSuccess) return e;
     }
-    const uint32_t gx = (cus ? cus : 256) * ZK_CL_XS_GRID;
-    e = ZK_CL_XCD ? (p.nb1 <= kSmallDigits
-                         ? launch_checked("k_cl_xscatter<global,256>", k_cl_xscatter<false, kSmallDigits>, dim3(gx),
-                                          dim3(kXsWG), 0, s, x1)
-                         : launch_checked("k_cl_xscatter<global>", k_cl_xscatter<false, kMaxDigits>, dim3(gx),
-                                          dim3(kXsWG), 0, s, x1))
-        : (ZK_CL_WC && p.nb1 <= kWcDigits)
-            ? launch_checked("k_cl_scatter_wc<global>", k_cl_scatter_wc<false>, dim3(p.grid), dim3(kWcWG), 0, s, a)
-        : p.nb1 <= kSmallDigits
-            ? launch_checked("k_cl_scatter<global,256>", k_cl_scatter<false, kSmallDigits>, dim3(p.grid), dim3(kScWG), 0,
-                             s, a)
-            : launch_checked("k_cl_scatter<global>", k_cl_scatter<false, kMaxDigits>, dim3(p.grid), dim3(kScWG), 0, s, a);
+    const uint32_t gx = cus ? cus : 256;
+    e = p.nb1 <= kSmallDigits
+            ? launch_checked("k_cl_xscatter<global,256>", k_cl_xscatter<false, kSmallDigits>, dim3(gx), dim3(kXsWG), 0, s,
+                             x1)
+            : launch_checked("k_cl_xscatter<global>", k_cl_xscatter<false, kMaxDigits>, dim3(gx), dim3(kXsWG), 0, s, x1);
     if (e != hipSuccess) return e;
     if (!p.b2) {  // P3: A -> B
         ta.in = dev(A);
@@ -1215,18 +857,10 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
         ta.nsub = p.nb1;
         *result = 1;
     } else {  // P2: A -> B (sub-buckets), P3: B -> A
-        ScatterArgs b{};
-        b.in = dev(A);
-        b.out = B;
-        b.bucket = bucket;
-        b.nbuckets = p.nb1;
-        b.sub = sub;
-        b.shift = sh1 - p.b2;
-        b.nd = p.nb2;
         const uint32_t parts2 = p.nb1 < kParts ? p.nb1 : kParts;
         const uint32_t nbp = (p.nb1 + parts2 - 1) / parts2;
         XArgs x2{};
-        if (ZK_CL_XCD) {
+        {
             x2.in = dev(A);
             x2.out = B;
             x2.shift = sh1 - p.b2;
@@ -1252,18 +886,10 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
                                    (const uint32_t*)cursor2, xl.m2 - 1, n, sub);
             if (e != hipSuccess) return e;
         }
-        e = ZK_CL_XCD ? (p.nb2 <= kSmallDigits
-                             ? launch_checked("k_cl_xscatter<local,256>", k_cl_xscatter<true, kSmallDigits>, dim3(gx),
-                                              dim3(kXsWG), 0, s, x2)
-                             : launch_checked("k_cl_xscatter<local>", k_cl_xscatter<true, kMaxDigits>, dim3(gx),
-                                              dim3(kXsWG), 0, s, x2))
-            : (ZK_CL_WC && p.nb2 <= kWcDigits)
-                ? launch_checked("k_cl_scatter_wc<local>", k_cl_scatter_wc<true>, dim3(p.nb1), dim3(kWcWG), 0, s, b)
-            : p.nb2 <= kSmallDigits
-                ? launch_checked("k_cl_scatter<local,256>", k_cl_scatter<true, kSmallDigits>, dim3(p.nb1), dim3(kScWG),
-                                 0, s, b)
-                : launch_checked("k_cl_scatter<local>", k_cl_scatter<true, kMaxDigits>, dim3(p.nb1), dim3(kScWG), 0, s,
-                                 b);
+        e = p.nb2 <= kSmallDigits
+                ? launch_checked("k_cl_xscatter<local,256>", k_cl_xscatter<true, kSmallDigits>, dim3(gx), dim3(kXsWG), 0,
+                                 s, x2)
+                : launch_checked("k_cl_xscatter<local>", k_cl_xscatter<true, kMaxDigits>, dim3(gx), dim3(kXsWG), 0, s, x2);
         if (e != hipSuccess) return e;
         ta.in = dev(B);
         ta.out = A;
@@ -1271,7 +897,7 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
         ta.nsub = p.nb1 * p.nb2;
         *result = 0;
     }
-    const uint32_t g3 = ta.nsub < ZK_CL_TR_GRID * cus ? ta.nsub : ZK_CL_TR_GRID * cus;
+    const uint32_t g3 = ta.nsub < kTrGrid * cus ? ta.nsub : kTrGrid * cus;
     return launch_checked("k_cl_traces", k_cl_traces, dim3(g3), dim3(kTrWG), 0, s, ta);
 }
 

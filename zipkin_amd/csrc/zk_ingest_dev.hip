@@ -103,9 +103,6 @@ __device__ __forceinline__ uint64_t ld_be64(P p) {
     return __builtin_bswap64(ld_u64(p));
 }
 // copy 8 / 4 bytes through a register (source read before the destination is written)
-#ifndef ZK_ING_BYTEWR
-#define ZK_ING_BYTEWR 1  // LDS destinations written byte by byte (never off alignment): 14.00 vs 14.03-14.21 ms
-#endif
 template <class D, class S>
 __device__ __forceinline__ void cp8(D d, S s) {
     const uint64_t v = ld_u64(s);
@@ -113,14 +110,11 @@ __device__ __forceinline__ void cp8(D d, S s) {
 }
 template <class S>
 __device__ __forceinline__ void cp8(lds_u8* d, S s) {
+    // LDS destinations written byte by byte (never off alignment: unaligned stores replay),
+    // 14.00 vs 14.03-14.21 ms per decode (profiles/r03/ingest_pmc.txt)
     const uint64_t v = ld_u64(s);
-    if (ZK_ING_BYTEWR) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) d[k] = (uint8_t)(v >> (8 * k));
-    } else {
-        typedef __attribute__((address_space(3), aligned(1))) uint64_t lds_u64u;
-        *(lds_u64u*)d = v;
-    }
+    for (int k = 0; k < 8; ++k) d[k] = (uint8_t)(v >> (8 * k));
 }
 template <class D, class S>
 __device__ __forceinline__ void cp4(D d, S s) {
@@ -623,199 +617,9 @@ __device__ __forceinline__ int parse_record(const IngArgs& a, uint64_t i, P src,
 // deeper goes to the global-memory decoder, like an oversized one). Accept/reject and every captured value follow
 // the host decoder (zk_ingest.cpp read_span / read_annotation / read_endpoint): last field wins,
 // an annotation's host name is reset per annotation only.
-// ZK_ING_FLAT (A/B, off): the LDS decoder walks with parse_record_flat instead of parse_record.
-// Measured on the bench's ingest workload (profiles/r03/ingest_flat_walk.txt): 15.6-15.9 ms per
-// 1.98e7 fragments against 14.1-14.3 ms -- the flat step costs ~350 instructions per token, half of
-// them scalar lane-mask logic, and the bench's spans all share one layout, so the branchy walk's
-// lanes hardly diverge. Kept as the starting point for a table-driven walk.
-#ifndef ZK_ING_FLAT
-#define ZK_ING_FLAT 0
-#endif
-namespace tw {
-constexpr uint32_t kStruct = 0, kList = 1, kMap = 2;
-// per thrift type (0..15): bytes of a value past its start (a string adds its length), as nibbles;
-// the valid value types; the container types
-constexpr uint64_t tw_width(int t) {
-    return t == T_BOOL || t == T_BYTE ? 1 : t == T_I16 ? 2 : t == T_I32 || t == T_STRING ? 4
-         : t == T_DOUBLE || t == T_I64 ? 8 : t == T_SET || t == T_LIST ? 5 : t == T_MAP ? 6 : 0;
-}
-constexpr uint64_t tw_widths() {
-    uint64_t w = 0;
-    for (int t = 0; t < 16; ++t) w |= tw_width(t) << (4 * t);
-    return w;
-}
-constexpr uint64_t kTypeWidth = tw_widths();
-constexpr uint32_t kKnownTypes = (1u << T_BOOL) | (1u << T_BYTE) | (1u << T_DOUBLE) | (1u << T_I16) | (1u << T_I32) |
-                                 (1u << T_I64) | (1u << T_STRING) | (1u << T_STRUCT) | (1u << T_MAP) | (1u << T_SET) |
-                                 (1u << T_LIST);
-constexpr uint32_t kContainerTypes = (1u << T_STRUCT) | (1u << T_MAP) | (1u << T_SET) | (1u << T_LIST);
-constexpr uint32_t kSkip = 0, kSpan = 1, kAnnList = 2, kAnn = 3, kEp = 4;
-// level word: kind (bits 0-1), semantic context (2-4), list element / map key type (8-15), map
-// value type (16-23); the level's remaining element count travels beside it
-__device__ __forceinline__ uint32_t lvl(uint32_t kind, uint32_t sem, uint32_t et, uint32_t vt) {
-    return kind | (sem << 2) | (et << 8) | (vt << 16);
-}
-}  // namespace tw
-
-// lane flags of the flat walk (one VGPR instead of a dozen lane masks)
-constexpr uint32_t F_DONE = 1u << 0, F_BAD = 1u << 1, F_DEEP = 1u << 2, F_PAR = 1u << 3, F_NAME = 1u << 4,
-                   F_INVALID = 1u << 5, F_VSET = 1u << 6, F_HOST = 1u << 7, F_HNSET = 1u << 8, F_SRV = 1u << 9,
-                   F_CLI = 1u << 10, F_SRVN = 1u << 11, F_CLIN = 1u << 12;
-
-// The record and the service name (an LDS byte offset into `base`) of the Span at [p0, p0 + len).
-// Returns like parse_record: -1 (status set), 0 (no service), 1 (*nm_off / *nl set; *nm_off = ~0u:
-// "Unknown service name"); -2: nested deeper than the register stack (nothing written: defer).
-// Every per-token decision is a select: the loop's exit is the only branch.
-__device__ __forceinline__ int parse_record_flat(const IngArgs& a, uint64_t i, const lds_u8* base, uint32_t p0,
-                                                 uint32_t len, uint32_t* nm_off, uint32_t* nl_out) {
-    using namespace tw;
-    uint32_t p = p0;
-    const uint32_t e = p0 + len;
-    uint32_t fl = 0;
-    uint32_t d = 0;
-    uint32_t mt = lvl(kStruct, kSpan, 0, 0);  // the open container (top of the stack)
-    uint32_t nt = 0;
-    uint32_t sm0 = 0, sm1 = 0, sm2 = 0, sn0 = 0, sn1 = 0, sn2 = 0;  // saved levels 0..2
-    uint64_t trace = 0, id = 0, parent = 0;
-    int64_t first = 0, last = 0;
-    uint32_t nann = 0, cnt = 0;  // cnt: 2-bit counts of cs | cr << 2 | sr << 4 | ss << 6
-    int64_t ts = 0;              // the annotation being read
-    uint32_t vl = 0, vc = 0, hn = 0, hl = 0;
-    uint32_t srv = 0, srv_len = 0, cli = 0, cli_len = 0;  // first server / client core annotation with a host
-    while (!(fl & F_DONE)) {
-        const uint64_t lo = ld_u64(base + p), hi = ld_u64(base + p + 8);  // aligned dword reads
-        const uint32_t kind = mt & 3u, sem = (mt >> 2) & 7u;
-        const uint32_t avail = e - p;
-        const bool in_struct = kind == kStruct;
-        // the token: a struct field header, or the next element of a list / map (keys and values alternate)
-        const uint32_t et = (kind == kList || (nt & 1u) == 0u) ? (mt >> 8) & 0xFFu : (mt >> 16) & 0xFFu;
-        const uint32_t t = in_struct ? (uint32_t)(lo & 0xFFu) : et;
-        const int32_t fid = in_struct ? (int32_t)(int16_t)__builtin_bswap16((uint16_t)(lo >> 8)) : -1;
-        const bool end = in_struct ? t == T_STOP : nt == 0u;
-        // ---- the value of type t at q = p + vofs
-        const uint32_t vofs = in_struct ? 3u : 0u;
-        const uint64_t vlo = in_struct ? ((lo >> 24) | (hi << 40)) : lo;
-        const uint32_t w32 = __builtin_bswap32((uint32_t)vlo);  // i32 / string length at q
-        const uint64_t w64 = __builtin_bswap64(vlo);            // i64 at q
-        // width / validity of type t from packed tables (compare chains compile to a branch tree):
-        // the value's bytes past q (a string's length word, a list's or map's header), 0 for a struct
-        const uint32_t t4 = t & 15u;
-        const bool known = t < 16u && ((kKnownTypes >> t4) & 1u);
-        const bool is_str = t == T_STRING, is_list = (t | 1u) == T_LIST, is_map = t == T_MAP;
-        const bool container = ((kContainerTypes >> t4) & 1u) & (t < 16u);
-        const int32_t lcnt = (int32_t)__builtin_bswap32((uint32_t)(vlo >> 8));
-        const int32_t mcnt = (int32_t)__builtin_bswap32((uint32_t)(vlo >> 16));
-        const uint64_t w = ((kTypeWidth >> (4u * t4)) & 15u) + (is_str ? (uint64_t)(int64_t)(int32_t)w32 : 0ull);
-        // a map's entries alternate key and value; > 2^29 entries cannot fit a 16 MiB fragment
-        const int64_t ncnt = is_list ? (int64_t)lcnt : is_map ? (mcnt > (1 << 29) ? -1ll : 2ll * mcnt) : 0ll;
-        const bool vbad = !known | (is_str & ((int32_t)w32 < 0)) | (ncnt < 0) | ((uint64_t)avail < vofs + w);
-        const bool bad = end ? (in_struct && avail < 1u) : vbad;
-        const bool val = !end && !bad;  // a value was read
-        const bool deep = val && container && d == 3u;
-        const bool push = val && container && d < 3u;
-        const bool pop = end && !bad;
-        const uint32_t q = p + vofs;
-        p += bad ? 0u : end ? (in_struct ? 1u : 0u) : vofs + (uint32_t)w;
-        // ---- semantic capture (the host's read_span / read_annotation / read_endpoint)
-        const bool sspan = val && sem == kSpan, sann = val && sem == kAnn, sep = val && sem == kEp;
-        trace = (sspan && fid == 1 && t == T_I64) ? w64 : trace;
-        id = (sspan && fid == 4 && t == T_I64) ? w64 : id;
-        const bool gpar = sspan && fid == 5 && t == T_I64;
-        parent = gpar ? w64 : parent;
-        fl |= (gpar ? F_PAR : 0u) | ((sspan && fid == 3 && is_str) ? F_NAME : 0u);
-        ts = (sann && fid == 1 && t == T_I64) ? (int64_t)w64 : ts;
-        const bool gval = sann && fid == 2 && is_str;
-        vl = gval ? w32 : vl;
-        vc = gval ? (uint32_t)((vlo >> 32) & 0xFFFFu) : vc;
-        const bool ghn = sep && fid == 3 && is_str;
-        hn = ghn ? q + 4u : hn;
-        hl = ghn ? w32 : hl;
-        fl |= (gval ? F_VSET : 0u) | ((sann && fid == 3 && t == T_STRUCT) ? F_HOST : 0u) | (ghn ? F_HNSET : 0u);
-        // ---- an annotation ends: thrift.scala:66-71 validation, Span.scala:213-240 first/last/core
-        const bool commit = pop && sem == kAnn;
-        const bool vset = (fl & F_VSET) != 0u;
-        fl |= (commit && (ts <= 0 || (vset && vl == 0u))) ? F_INVALID : 0u;
-        first = (commit && (nann == 0u || ts < first)) ? ts : first;
-        last = (commit && (nann == 0u || ts > last)) ? ts : last;
-        nann += commit ? 1u : 0u;
-        const uint32_t c0 = vc & 0xFFu, c1 = vc >> 8;
-        const bool core = commit && vset && vl == 2u &&
-                          ((c0 == 'c' && (c1 == 's' || c1 == 'r')) || (c0 == 's' && (c1 == 'r' || c1 == 's')));
-        const uint32_t c = c0 == 'c' ? (c1 == 's' ? 0u : 1u) : (c1 == 'r' ? 2u : 3u);
-        cnt += (core && ((cnt >> (2 * c)) & 3u) < 2u) ? (1u << (2 * c)) : 0u;
-        const bool hst = core && (fl & F_HOST) != 0u, named = (fl & F_HNSET) != 0u;
-        const bool tsrv = hst && c >= 2u && !(fl & F_SRV), tcli = hst && c < 2u && !(fl & F_CLI);
-        srv = tsrv ? hn : srv;
-        srv_len = tsrv ? hl : srv_len;
-        cli = tcli ? hn : cli;
-        cli_len = tcli ? hl : cli_len;
-        fl |= (tsrv ? F_SRV | (named ? F_SRVN : 0u) : 0u) | (tcli ? F_CLI | (named ? F_CLIN : 0u) : 0u);
-        // ---- push / pop on the register stack
-        uint32_t nsem = kSkip;
-        nsem = (t == T_STRUCT && sem == kAnnList) ? kAnn : nsem;
-        nsem = (t == T_STRUCT && sem == kAnn && fid == 3) ? kEp : nsem;
-        nsem = (is_list && sem == kSpan && fid == 6 && (vlo & 0xFFu) == T_STRUCT) ? kAnnList : nsem;
-        const bool nann_start = push && nsem == kAnn;  // a new annotation: reset its fields
-        ts = nann_start ? 0 : ts;
-        vl = nann_start ? 0u : vl;
-        vc = nann_start ? 0u : vc;
-        hn = nann_start ? 0u : hn;
-        hl = nann_start ? 0u : hl;
-        fl &= nann_start ? ~(F_VSET | F_HOST | F_HNSET) : ~0u;
-        nt -= (val && !in_struct) ? 1u : 0u;
-        sm0 = (push && d == 0u) ? mt : sm0;
-        sn0 = (push && d == 0u) ? nt : sn0;
-        sm1 = (push && d == 1u) ? mt : sm1;
-        sn1 = (push && d == 1u) ? nt : sn1;
-        sm2 = (push && d == 2u) ? mt : sm2;
-        sn2 = (push && d == 2u) ? nt : sn2;
-        const uint32_t nkind = is_list ? kList : is_map ? kMap : kStruct;
-        const uint32_t pm = d == 1u ? sm0 : d == 2u ? sm1 : sm2, pn = d == 1u ? sn0 : d == 2u ? sn1 : sn2;
-        mt = push ? lvl(nkind, nsem, (is_list || is_map) ? (uint32_t)(vlo & 0xFFu) : 0u,
-                        is_map ? (uint32_t)((vlo >> 8) & 0xFFu) : 0u)
-                  : (pop && d > 0u) ? pm : mt;
-        nt = push ? (uint32_t)ncnt : (pop && d > 0u) ? pn : nt;
-        fl |= (bad ? F_BAD | F_DONE : 0u) | (deep ? F_DEEP | F_DONE : 0u) | ((pop && d == 0u) ? F_DONE : 0u);
-        d = push ? d + 1u : (pop && d > 0u) ? d - 1u : d;
-    }
-    if (fl & F_DEEP) return -2;
-    if (fl & F_BAD) {
-        a.status[i] = kStUndecodable;
-        return -1;
-    }
-    if (!(fl & F_NAME) || (fl & F_INVALID)) {  // IncompleteTraceDataException / IllegalArgumentException
-        a.status[i] = kStInvalid;
-        return -1;
-    }
-    const bool has_parent = (fl & F_PAR) != 0u, srv_set = (fl & F_SRV) != 0u, cli_set = (fl & F_CLI) != 0u;
-    uint32_t f = has_parent ? ZK_F_HAS_PARENT : 0u;
-    if (nann) f |= ZK_F_HAS_ANNOTATIONS;
-    *nm_off = ~0u;
-    *nl_out = 0u;
-    if (srv_set) {
-        f |= ZK_F_SVC_SERVER;
-        if ((fl & F_SRVN) && srv_len) {
-            *nm_off = srv;
-            *nl_out = srv_len;
-        }
-    } else if (cli_set) {
-        f |= ZK_F_SVC_CLIENT;
-        if ((fl & F_CLIN) && cli_len) {
-            *nm_off = cli;
-            *nl_out = cli_len;
-        }
-    }
-    f |= ((cnt & 3u) << ZK_F_CS_SHIFT) | (((cnt >> 2) & 3u) << ZK_F_CR_SHIFT) | (((cnt >> 4) & 3u) << ZK_F_SR_SHIFT) |
-         (((cnt >> 6) & 3u) << ZK_F_SS_SHIFT);
-    a.tid[i] = trace;
-    a.sid[i] = id;
-    a.pid[i] = has_parent ? parent : 0ull;
-    a.first[i] = nann ? first : 0;
-    a.last[i] = nann ? last : 0;
-    a.flags[i] = f;
-    a.svc[i] = 0u;
-    return (srv_set || cli_set) ? 1 : 0;
-}
+// (A table-driven "flat" walk -- one token per step, every decision a select -- measured
+// 15.6-15.9 ms per 1.98e7 fragments against 14.1-14.3 ms for this branchy walk, whose lanes hardly
+// diverge on uniform layouts: profiles/r03/ingest_flat_walk.txt; removed after round 3.)
 
 // ---- fast path: the canonical layout of a stored zipkin Span (LDS decoder) ----------------------
 // Scrooge writes a Span's fields in id order (zipkinCore.thrift:27-58): 1 trace_id, 3 name, 4 id,
@@ -827,9 +631,6 @@ __device__ __forceinline__ int parse_record_flat(const IngArgs& a, uint64_t i, c
 // annotation). Anything else -- another field, another order, a missing endpoint field, a length
 // past the end -- returns -3 before anything is written, and the lane runs the generic walk: the
 // fast path accepts only byte strings on which parse_record yields exactly the same record.
-#ifndef ZK_ING_FAST
-#define ZK_ING_FAST 1  // 0: every span through the generic walk (A/B)
-#endif
 template <int W>
 struct LWin {  // W + 1 aligned dwords from the dword holding byte x; byte x + j is at compile-time j
     uint32_t d[W + 1];
@@ -1112,13 +913,7 @@ constexpr uint32_t kLdsBudget = ZK_ING_BUDGET;
 constexpr uint32_t kLdsBlock = 1024;
 constexpr uint32_t kLdsSlack = 80;  // region bytes beyond max(raw, compressed): in-place headroom + alignment
                                     // + the lane's bank skew
-#ifndef ZK_ING_UNIFORM
-#define ZK_ING_UNIFORM 1  // equal-size regions per round, placed for distinct banks (see the round setup)
-#endif
 constexpr uint32_t kLdsUniformCap = 640;  // largest region (bytes) of a uniform round
-#ifndef ZK_ING_SKEW
-#define ZK_ING_SKEW 1  // decompressed span starts 4 * (lane % 4) bytes into its region (see below)
-#endif
 
 // Snappy block from in = out + D (the same region), in place: false with *unsafe set when a step
 // would write over input bytes not yet read.
@@ -1254,7 +1049,7 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
             const uint32_t y = (uint32_t)__shfl_xor((int)mx, o);
             mx = y > mx ? y : mx;
         }
-        const bool uniform = ZK_ING_UNIFORM && mx <= kLdsUniformCap;
+        const bool uniform = mx <= kLdsUniformCap;
         uint32_t R = need, R0, k;
         bool fits;
         if (uniform) {
@@ -1297,7 +1092,7 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                 // group; lanes parsing the same field at the same offset then collide. The
                 // decompressed span starts 4 * (lane % 4) bytes in, spreading the lanes over all 32.
                 lds_u8* const lreg = (lds_u8*)reg;
-                const uint32_t skew = ZK_ING_SKEW ? 4u * (uniform ? (lane >> 4) & 3u : lane & 3u) : 0u;
+                const uint32_t skew = 4u * (uniform ? (lane >> 4) & 3u : lane & 3u);
                 const lds_u8* src = lreg + D;
                 uint64_t len = clen;
                 bool ok = true, unsafe = false;
@@ -1313,20 +1108,12 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                     const lds_u8* const lbase = (const lds_u8*)s_buf;
                     const uint32_t p0 = (uint32_t)(src - lbase);
                     uint32_t nmo, nl;
-                    int r = ZK_ING_FAST ? parse_record_fast(a, i, lbase, p0, (uint32_t)len, &nmo, &nl) : -3;
+                    int r = parse_record_fast(a, i, lbase, p0, (uint32_t)len, &nmo, &nl);
                     if (r == -3) {  // not the canonical layout: the generic walk
-#if ZK_ING_FLAT
-                        r = parse_record_flat(a, i, lbase, p0, (uint32_t)len, &nmo, &nl);
-                        if (r == -2) {
-                            a.status[i] = kStDefer;
-                            r = -1;
-                        }
-#else
                         const uint8_t* gnm = nullptr;
                         r = parse_record(a, i, src, len, &gnm, &nl);
                         nmo = (r == 1 && gnm != (const uint8_t*)a.unknown) ? (uint32_t)(gnm - (const uint8_t*)lbase)
                                                                            : ~0u;
-#endif
                     }
                     const bool unknown = nmo == ~0u;
                     const uint8_t* nm = unknown ? a.unknown : (const uint8_t*)(lbase + nmo);
