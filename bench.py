@@ -880,7 +880,13 @@ def bench_c4(a):
     torch.cuda.set_stream(stream)
     t0 = time.perf_counter()
     kk, est, cnt = kv.topk_all(10)
-    query_ms = (time.perf_counter() - t0) * 1e3
+    query_first_ms = (time.perf_counter() - t0) * 1e3
+    qt = []
+    for _ in range(5):  # a query server's steady state: the first call pays one-time HIP setup
+        t0 = time.perf_counter()
+        kv.topk_all(10)
+        qt.append((time.perf_counter() - t0) * 1e3)
+    query_ms = sorted(qt)[2]
     if a.pipeline != 0:
         kk2, est2, cnt2 = kv2.topk_all(10)
         if not (np.array_equal(kk, kk2) and np.array_equal(est, est2) and np.array_equal(cnt, cnt2)):
@@ -923,7 +929,7 @@ def bench_c4(a):
         "kernels": kernels,
         "cpu_baseline": cpu,
         "parity": parity,
-        "detail": {"event_ms_per_step": ev_ms / a.steps, "topk_query_ms": query_ms,
+        "detail": {"event_ms_per_step": ev_ms / a.steps, "topk_query_ms": query_ms, "topk_query_first_ms": query_first_ms,
                    "service0_top3": [(int(k), int(e)) for k, e in zip(kk[0][:3], est[0][:3])]},
     }), flush=True)
 

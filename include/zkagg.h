@@ -113,6 +113,14 @@ typedef struct zk_span_cols {
 #define ZK_BATCH_TRACE_CLUSTERED (1u << 1) /* all fragments of a trace are adjacent (Cassandra
                                               row-per-trace reads, StorageRecordReader.scala:49-54) */
 #define ZK_BATCH_VERIFY_TRACES   (1u << 2) /* check clustering and trace-completeness (see above) */
+/* ZK_BATCH_CONTINUES (with ZK_BATCH_TRACE_CLUSTERED): the batch's last trace may continue in the next
+ * accumulate -- a trace cut at a batch edge, as a streaming reader of row-per-trace storage cuts
+ * them. Its fragments are held back in HBM (up to max_trace_records) and joined with the next
+ * batch's leading fragments of the same traceId; a held trace may continue over any number of
+ * batches. The held trace is aggregated when a batch moves on to another traceId, when a batch
+ * arrives without the flag, at finalize and at zk_deps_partial; zk_ctx_stats does not count it
+ * before then. Costs one small edge scan and one stream synchronisation per such accumulate. */
+#define ZK_BATCH_CONTINUES       (1u << 3)
 
 typedef struct zk_config {
     uint32_t num_services;       /* S <= 4096: service ids are 0..S-1, link table is S x S */

@@ -20,6 +20,7 @@ object ZkNative {
   // zk_deps_accumulate batch flags
   final val BatchDevicePtrs = 1
   final val BatchTraceClustered = 2
+  final val BatchContinues = 8  // ZK_BATCH_CONTINUES: the batch's last trace may continue in the next call
   final val BatchVerifyTraces = 4
   // zk_store_create modes
   final val StoreAnorm = 0

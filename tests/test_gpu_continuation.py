@@ -1,0 +1,124 @@
+"""Traces cut at batch edges (ZK_BATCH_CONTINUES), through the C ABI on the GPU.
+
+The reference job has no batch boundary: every fragment of a trace meets its siblings in the
+(id, traceId) and (parentId, traceId) shuffles whatever file or split it came from
+(ZipkinAggregateJob.scala:20-33). A streaming reader of row-per-trace storage
+(StorageRecordReader.scala:49-54) cuts batches wherever its buffer fills, so a trace can straddle
+two or more batches. With ZK_BATCH_CONTINUES the library holds the batch's last trace back and joins
+it with the next batch's leading fragments of the same traceId; the result must equal the oracle's
+over the whole stream, bit for bit, and the clustering check must not fire."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+from tests.test_gpu_parity import assert_parity, cols_from_rows, star_trace
+from zipkin_amd import DepsContext, DeviceColumns, SpanColumns, ZkError, _abi, tracegen_host
+
+pytestmark = pytest.mark.gpu
+
+
+def cut(cols, points):
+    bounds = [0, *sorted(points), len(cols)]
+    return [cols.take(slice(a, b)) for a, b in zip(bounds[:-1], bounds[1:])]
+
+
+def run_stream(parts, S, device=False, verify=True, last_continues=False, **kw):
+    with DepsContext(S, **kw) as ctx:
+        for i, p in enumerate(parts):
+            b = DeviceColumns.from_host(p) if device else p
+            cont = last_continues or i + 1 < len(parts)
+            ctx.accumulate(b, clustered=True, verify=verify, continues=cont)
+        return ctx.finalize(), ctx.stats()
+
+
+@pytest.mark.parametrize("batches", [2, 3, 5])
+@pytest.mark.parametrize("device", [False, True])
+def test_traces_cut_at_batch_edges_equal_the_oracle(gpu, batches, device):
+    S = 97
+    cols = tracegen_host(61 + batches, 20_000, max_depth=6, num_services=S)
+    ref = oracle.aggregate(cols, S)
+    rng = np.random.default_rng(batches)
+    pts = rng.choice(np.arange(1, len(cols)), batches - 1, replace=False)
+    # cuts at random positions: most land inside a trace (and at odd and even offsets, so the
+    # leading run's end is both)
+    got, st = run_stream(cut(cols, pts), S, device=device)
+    assert_parity(got, st, ref)
+    assert st["not_clustered"] == 0
+
+
+def test_one_trace_over_five_batches(gpu):
+    """A 20k-record trace spread over five batches (three of them inside it entirely), between
+    ordinary traces; cut points at odd and even offsets."""
+    S = 9
+    rows = []
+    for t in range(50):
+        rows += star_trace(100 + t, 1 + t % 6, svc_root=t % S, nsvc=S)
+    big0 = len(rows)
+    rows += star_trace(7777, 10_000, nsvc=S)
+    big1 = len(rows)
+    for t in range(50):
+        rows += star_trace(900 + t, 1 + t % 5, svc_root=t % S, nsvc=S)
+    cols = cols_from_rows(rows)
+    ref = oracle.aggregate(cols, S)
+    pts = [big0 + 3, big0 + 4_001, big0 + 9_000, big0 + 15_555, big1 - 2]
+    for device in (False, True):
+        got, st = run_stream(cut(cols, pts), S, device=device)
+        assert_parity(got, st, ref)
+        assert st["not_clustered"] == 0
+
+
+def test_held_trace_is_flushed_by_finalize_and_by_a_plain_batch(gpu):
+    S = 13
+    cols = tracegen_host(71, 3_000, max_depth=5, num_services=S)
+    ref = oracle.aggregate(cols, S)
+    mid = len(cols) // 2 + 1
+    # the last batch also says "continues": finalize aggregates the held trace
+    got, st = run_stream(cut(cols, [mid]), S, last_continues=True)
+    assert_parity(got, st, ref)
+    # an empty batch without the flag flushes it too
+    with DepsContext(S) as ctx:
+        ctx.accumulate(cols.take(slice(0, mid)), clustered=True, continues=True)
+        ctx.accumulate(cols.take(slice(mid, len(cols))), clustered=True, continues=True)
+        ctx.accumulate(SpanColumns.empty(0), clustered=True)
+        st = ctx.stats()
+        assert st["records"] == len(cols)
+        assert_parity(ctx.finalize(), ctx.stats(), ref)
+
+
+def test_without_the_flag_a_cut_trace_is_detected(gpu):
+    rows = star_trace(5, 40, nsvc=5)
+    parts = cut(cols_from_rows(rows), [17])
+    with DepsContext(5) as ctx:
+        for p in parts:
+            ctx.accumulate(p, clustered=True, verify=True)
+        with pytest.raises(ZkError) as e:
+            ctx.finalize()
+        assert e.value.status == _abi.ZK_ERR_NOT_CLUSTERED
+    got, st = run_stream(parts, 5)
+    assert_parity(got, st, oracle.aggregate(cols_from_rows(rows), 5))
+
+
+def test_continues_needs_clustered_batches(gpu):
+    cols = cols_from_rows(star_trace(3, 4, nsvc=5))
+    with DepsContext(5) as ctx:
+        with pytest.raises(ZkError) as e:
+            ctx.accumulate(cols, clustered=False, continues=True)
+        assert e.value.status == _abi.ZK_ERR_INVALID_ARG
+
+
+def test_held_trace_longer_than_max_trace_is_too_large(gpu):
+    """max_trace_records bounds a held trace like any other: finalize reports it, the other traces
+    of the stream are aggregated."""
+    S = 7
+    rows = star_trace(1, 30, nsvc=S) + star_trace(2, 800, nsvc=S) + star_trace(3, 30, nsvc=S)
+    cols = cols_from_rows(rows)
+    a, b = 61, 61 + 1601  # trace 2 (1601 records) spans three batches
+    parts = cut(cols, [a + 500, a + 1100, b + 10])
+    with DepsContext(S, max_trace_records=1000) as ctx:
+        for p in parts[:-1]:
+            ctx.accumulate(p, clustered=True, continues=True)
+        ctx.accumulate(parts[-1], clustered=True)
+        with pytest.raises(ZkError) as e:
+            ctx.finalize()
+        assert e.value.status == _abi.ZK_ERR_TRACE_TOO_LARGE
+        assert ctx.stats()["trace_too_large"] == 1

@@ -40,6 +40,7 @@ ZK_F_SS_SHIFT = 14
 ZK_BATCH_DEVICE_PTRS = 1 << 0
 ZK_BATCH_TRACE_CLUSTERED = 1 << 1
 ZK_BATCH_VERIFY_TRACES = 1 << 2
+ZK_BATCH_CONTINUES = 1 << 3
 
 LIMBS_PER_CELL = 16
 TABLE_TAIL_WORDS = 16  # the folded zk_stats counters after the S*S cells (ZK_TABLE_BYTES)

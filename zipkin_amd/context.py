@@ -104,18 +104,25 @@ class DepsContext:
     def reset(self) -> None:
         self._check(self._L.zk_deps_reset(self._h))
 
-    def accumulate(self, cols, *, clustered: bool = False, verify: bool = True, n: int | None = None) -> None:
+    def accumulate(self, cols, *, clustered: bool = False, verify: bool = True, n: int | None = None,
+                   continues: bool = False) -> None:
         """One batch of span fragments.
 
         clustered: the caller promises that every trace's fragments are adjacent (Cassandra
-          row-per-trace reads); otherwise the device clusters the batch first (radix sort by traceId).
+          row-per-trace reads); otherwise the device clusters the batch first (a hash partition by
+          traceId, zk_cluster.hip).
         verify: check exactly, on the device, that no trace recurs after its run ended -- within the
           batch or across accumulate calls since the last reset (a split trace would be mis-joined);
           finalize then raises ZK_ERR_NOT_CLUSTERED. Costs one extra read of the traceId column.
+        continues (needs clustered): the batch's last trace may continue in the next accumulate
+          (ZK_BATCH_CONTINUES): its fragments are held back and joined with the next batch's leading
+          fragments of the same traceId.
         """
         flags = _abi.ZK_BATCH_TRACE_CLUSTERED if clustered else 0
         if verify:
             flags |= _abi.ZK_BATCH_VERIFY_TRACES
+        if continues:
+            flags |= _abi.ZK_BATCH_CONTINUES
         if isinstance(cols, DeviceColumns):
             ab = cols.abi(n)
             flags |= _abi.ZK_BATCH_DEVICE_PTRS

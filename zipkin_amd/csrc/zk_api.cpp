@@ -74,6 +74,15 @@ struct zk_ctx {
     uint64_t* tset = nullptr;
     uint64_t tset_slots = 0;
     uint64_t tset_records = 0;
+    // ZK_BATCH_CONTINUES: the held-back last trace of the batches so far (7 aligned columns of
+    // carry_cap records), its traceId and the batch flags it arrived with
+    uint8_t* carry = nullptr;
+    uint64_t carry_cap = 0, carry_n = 0, carry_tid = 0;
+    uint32_t carry_flags = 0;
+    uint64_t host_too_large = 0;          // held traces dropped for exceeding max_trace_records
+    bool carry_dropped = false;           // the held trace was dropped: skip the rest of it too
+    unsigned long long* edge = nullptr;   // device: the edge-run indices (k_edge_runs)
+    uint64_t* h_edge = nullptr;           // pinned: e0, e1, first and last traceId of the batch
     std::string err;
     // bound realtime sketch (zk_rt_bind)
     zk_rt* rt = nullptr;
@@ -200,6 +209,7 @@ zk_status stats_sum(zk_ctx* c, uint64_t out[ST_N]) {
     for (int s = 0; s < ST_N; ++s) out[s] = 0;
     for (int sh = 0; sh < (c->merged ? 1 : kStatShards); ++sh)
         for (int s = 0; s < ST_N; ++s) out[s] += h[(size_t)sh * ST_N + s];
+    out[ST_TOO_LARGE] += c->host_too_large;  // held-back traces that outgrew max_trace_records (this rank)
     return ZK_OK;
 }
 
@@ -403,6 +413,9 @@ zk_status zk_ctx_destroy(zk_ctx* c) {
     hipFree(c->cl_temp);
     hipFree(c->tset);
     hipFree(c->xchg);
+    hipFree(c->carry);
+    hipFree(c->edge);
+    if (c->h_edge) hipHostFree(c->h_edge);
     for (auto* v : {&c->ev_free, &c->ev_join, &c->ev_reduce, &c->ev_spill, &c->ev_fin, &c->ev_cluster})
         for (auto& p : *v) {
             hipEventDestroy(p.a);
@@ -431,7 +444,122 @@ zk_status zk_deps_reset(zk_ctx* c) {
     c->merged = false;
     c->continued = false;
     c->folded = false;
+    c->carry_n = 0;  // a held-back trace belongs to the job being reset
+    c->carry_dropped = false;
+    c->host_too_large = 0;
     return ZK_OK;
+}
+
+static zk_status accumulate_dev(zk_ctx* c, SpanColsDev d, uint32_t flags, uint32_t skip);
+static zk_status continue_batch(zk_ctx* c, const SpanColsDev& d, uint32_t flags);
+static zk_status flush_carry(zk_ctx* c);
+#define ZK_ST(call)                        \
+    do {                                   \
+        const zk_status _s = (call);       \
+        if (_s != ZK_OK) return _s;        \
+    } while (0)
+
+// append records [lo, hi) of a device batch to the carried trace
+static zk_status carry_append(zk_ctx* c, const SpanColsDev& d, uint64_t lo, uint64_t hi) {
+    if (!c->carry) {
+        c->carry_cap = (uint64_t)c->max_trace + 2;
+        ZK_HIP(c, hipMalloc(&c->carry, carved_bytes(c->carry_cap)));
+    }
+    const SpanColsMut m = carve_cols(c->carry, c->carry_cap);
+    const uint64_t k = hi - lo, at = c->carry_n;
+    ZK_HIP(c, hipMemcpyAsync(m.trace_id + at, d.trace_id + lo, k * 8, hipMemcpyDeviceToDevice, c->stream));
+    ZK_HIP(c, hipMemcpyAsync(m.span_id + at, d.span_id + lo, k * 8, hipMemcpyDeviceToDevice, c->stream));
+    ZK_HIP(c, hipMemcpyAsync(m.parent_id + at, d.parent_id + lo, k * 8, hipMemcpyDeviceToDevice, c->stream));
+    ZK_HIP(c, hipMemcpyAsync(m.first_ts + at, d.first_ts + lo, k * 8, hipMemcpyDeviceToDevice, c->stream));
+    ZK_HIP(c, hipMemcpyAsync(m.last_ts + at, d.last_ts + lo, k * 8, hipMemcpyDeviceToDevice, c->stream));
+    ZK_HIP(c, hipMemcpyAsync(m.service_id + at, d.service_id + lo, k * 4, hipMemcpyDeviceToDevice, c->stream));
+    ZK_HIP(c, hipMemcpyAsync(m.flags + at, d.flags + lo, k * 4, hipMemcpyDeviceToDevice, c->stream));
+    c->carry_n += k;
+    return ZK_OK;
+}
+
+// the held-back trace is complete: aggregate it as a batch of its own
+static zk_status flush_carry(zk_ctx* c) {
+    if (!c->carry_n) return ZK_OK;
+    const SpanColsMut m = carve_cols(c->carry, c->carry_cap);
+    const SpanColsDev d{m.trace_id, m.span_id, m.parent_id, m.first_ts, m.last_ts, m.service_id, m.flags, c->carry_n};
+    c->carry_n = 0;
+    return accumulate_dev(c, d, ZK_BATCH_DEVICE_PTRS | ZK_BATCH_TRACE_CLUSTERED | (c->carry_flags & ZK_BATCH_VERIFY_TRACES),
+                          0);
+}
+
+// A clustered batch when a trace is held back or the batch's last trace may continue: the batch's
+// leading run joins the held trace if it carries the same traceId; the held trace is aggregated once
+// the batch moves on to another trace (or the batch does not continue); with ZK_BATCH_CONTINUES the
+// batch's last run is held back for the next call. The rest of the batch goes through accumulate_dev
+// in place (from an even record, skipping the one record before it, so its columns stay aligned).
+static zk_status continue_batch(zk_ctx* c, const SpanColsDev& d, uint32_t flags) {
+    const uint64_t n = d.n, L = c->max_trace;
+    if (!c->edge) {
+        ZK_HIP(c, hipMalloc(&c->edge, 16));
+        ZK_HIP(c, hipHostMalloc((void**)&c->h_edge, 32, hipHostMallocDefault));
+    }
+    ZK_HIP(c, hipMemsetAsync(c->edge, 0xFF, 8, c->stream));
+    ZK_HIP(c, hipMemsetAsync(c->edge + 1, 0, 8, c->stream));
+    ZK_HIP(c, launch_edge_runs(d.trace_id, n, L, c->edge, c->stream));
+    ZK_HIP(c, hipMemcpyAsync(c->h_edge, c->edge, 16, hipMemcpyDeviceToHost, c->stream));
+    ZK_HIP(c, hipMemcpyAsync(c->h_edge + 2, d.trace_id, 8, hipMemcpyDeviceToHost, c->stream));
+    ZK_HIP(c, hipMemcpyAsync(c->h_edge + 3, d.trace_id + (n - 1), 8, hipMemcpyDeviceToHost, c->stream));
+    ZK_HIP(c, hipStreamSynchronize(c->stream));
+    const uint64_t e0 = c->h_edge[0], e1 = c->h_edge[1], first_tid = c->h_edge[2];
+    // end of the first run (n + 1: longer than a trace may be), start of the last run (n + 1: unknown)
+    const uint64_t first_end = e0 != ~0ull ? e0 : (n <= L + 1 ? n : n + 1);
+    const uint64_t last_start = e1 != 0 ? e1 : (n <= L + 1 ? 0 : n + 1);
+    uint64_t lead = 0;
+    if (c->carry_n || c->carry_dropped) {
+        if (first_tid == c->carry_tid) {
+            lead = first_end;
+            if (lead > n) {
+                // the leading run is longer than max_trace_records: find where it really ends (rare)
+                ZK_HIP(c, hipMemsetAsync(c->edge, 0xFF, 8, c->stream));
+                ZK_HIP(c, launch_edge_runs(d.trace_id, n, n, c->edge, c->stream));
+                ZK_HIP(c, hipMemcpyAsync(c->h_edge, c->edge, 8, hipMemcpyDeviceToHost, c->stream));
+                ZK_HIP(c, hipStreamSynchronize(c->stream));
+                lead = c->h_edge[0] != ~0ull ? c->h_edge[0] : n;
+            }
+            if (c->carry_dropped) {
+                // the rest of a trace already found too long: skipped like its beginning
+            } else if (c->carry_n + lead > L) {
+                // longer than max_trace_records: not aggregated, like any trace that long
+                c->carry_n = 0;
+                c->carry_dropped = true;
+                c->host_too_large += 1;
+            } else {
+                ZK_ST(carry_append(c, d, 0, lead));
+            }
+        }
+        c->carry_flags |= flags & ZK_BATCH_VERIFY_TRACES;
+        if (lead == n && (flags & ZK_BATCH_CONTINUES)) return ZK_OK;  // the whole batch continues the held trace
+        c->carry_dropped = false;
+        ZK_ST(flush_carry(c));
+    }
+    uint64_t hi = n;
+    if (flags & ZK_BATCH_CONTINUES) {
+        const uint64_t ls = last_start > lead ? last_start : lead;
+        if (ls < n) {  // (a last run longer than max_trace_records is not held: K1 reports it too large)
+            c->carry_flags = flags & ZK_BATCH_VERIFY_TRACES;
+            ZK_ST(carry_append(c, d, ls, n));
+            c->carry_tid = c->h_edge[3];
+            hi = ls;
+        }
+    }
+    if (hi <= lead) return ZK_OK;
+    const uint64_t lo = lead & ~1ull;
+    SpanColsDev b = d;
+    b.trace_id += lo;
+    b.span_id += lo;
+    b.parent_id += lo;
+    b.first_ts += lo;
+    b.last_ts += lo;
+    b.service_id += lo;
+    b.flags += lo;
+    b.n = hi - lo;
+    return accumulate_dev(c, b, flags & ~ZK_BATCH_CONTINUES, (uint32_t)(lead & 1));
 }
 
 zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags) {
@@ -439,10 +567,18 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
     ZK_TRY
     RoctxRange rr("zk_deps_accumulate");
     if (!cols) return fail(c, ZK_ERR_INVALID_ARG, "null columns");
-    if (flags & ~(ZK_BATCH_DEVICE_PTRS | ZK_BATCH_TRACE_CLUSTERED | ZK_BATCH_VERIFY_TRACES))
+    if (flags & ~(ZK_BATCH_DEVICE_PTRS | ZK_BATCH_TRACE_CLUSTERED | ZK_BATCH_VERIFY_TRACES | ZK_BATCH_CONTINUES))
         return fail(c, ZK_ERR_INVALID_ARG, "unknown batch flag");
+    if ((flags & ZK_BATCH_CONTINUES) && !(flags & ZK_BATCH_TRACE_CLUSTERED))
+        return fail(c, ZK_ERR_INVALID_ARG, "ZK_BATCH_CONTINUES needs a trace-clustered batch (ZK_BATCH_TRACE_CLUSTERED)");
     const uint64_t n = cols->n;
-    if (n == 0) return ZK_OK;
+    if (n == 0) {
+        if (!(flags & ZK_BATCH_CONTINUES)) {
+            c->carry_dropped = false;
+            if (c->carry_n) return flush_carry(c);
+        }
+        return ZK_OK;
+    }
     if (!cols_ok(cols)) return fail(c, ZK_ERR_INVALID_ARG, "null column pointer");
     const bool join = !c->rt || c->rt_mode == ZK_RT_WITH_DEPS;
     if (join && c->records_since_reset + n > kMaxRecordsSinceReset)
@@ -490,7 +626,24 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
         ZK_HIP(c, hipMemcpyAsync(svc, cols->service_id, n * 4, hipMemcpyHostToDevice, c->stream));
         ZK_HIP(c, hipMemcpyAsync(flg, cols->flags, n * 4, hipMemcpyHostToDevice, c->stream));
         d = SpanColsDev{tid, sid, pid, fts, lts, svc, flg, n};
+    } else if ((flags & ZK_BATCH_TRACE_CLUSTERED) &&
+               (!aligned(d.trace_id, 16) || !aligned(d.span_id, 16) || !aligned(d.parent_id, 16) ||
+                !aligned(d.first_ts, 16) || !aligned(d.last_ts, 16) || !aligned(d.service_id, 8) ||
+                !aligned(d.flags, 8))) {
+        // K1 reads two records per lane with one 16-byte (u64 columns) / 8-byte (u32) load
+        return fail(c, ZK_ERR_INVALID_ARG, "device columns must be 16-byte (u64) / 8-byte (u32) aligned");
     }
+    if (c->carry_n || c->carry_dropped || (flags & ZK_BATCH_CONTINUES)) return continue_batch(c, d, flags);
+    return accumulate_dev(c, d, flags, 0);
+    ZK_CATCH(c)
+}
+
+// One batch already in HBM. skip (0 or 1): the first record belongs to a run handled elsewhere (it
+// only keeps the column pointers 16-byte aligned); K1 starts at the trace after it.
+static zk_status accumulate_dev(zk_ctx* c, SpanColsDev d, uint32_t flags, uint32_t skip) {
+    const uint64_t n = d.n;
+    if (n <= skip) return ZK_OK;
+    const bool join = !c->rt || c->rt_mode == ZK_RT_WITH_DEPS;
     if (!(flags & ZK_BATCH_TRACE_CLUSTERED)) {
         EventPair ec;
         if (c->timing) {
@@ -506,15 +659,12 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
             ZK_HIP(c, hipEventRecord(ec.b, c->stream));
             c->ev_cluster.push_back(ec);
         }
-    } else if (flags & ZK_BATCH_DEVICE_PTRS) {
-        // K1 reads two records per lane with one 16-byte (u64 columns) / 8-byte (u32) load
-        if (!aligned(d.trace_id, 16) || !aligned(d.span_id, 16) || !aligned(d.parent_id, 16) ||
-            !aligned(d.first_ts, 16) || !aligned(d.last_ts, 16) || !aligned(d.service_id, 8) ||
-            !aligned(d.flags, 8))
-            return fail(c, ZK_ERR_INVALID_ARG, "device columns must be 16-byte (u64) / 8-byte (u32) aligned");
     }
     if (flags & ZK_BATCH_VERIFY_TRACES) {
-        const zk_status vs = verify_batch(c, d);
+        SpanColsDev v = d;  // (the skipped record's run is verified where it is handled)
+        v.trace_id += skip;
+        v.n -= skip;
+        const zk_status vs = verify_batch(c, v);
         if (vs != ZK_OK) return vs;
     }
     uint32_t grid = 0;
@@ -544,6 +694,7 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
     a.nb = c->nb;
     a.cb_shift = c->cb_shift;
     a.join = join ? 1u : 0u;
+    a.skip = skip;
     if (c->rt) {
         st = rt_prepare_lists(c->rt, grid, stride, n, &a, c->stream);
         if (st != ZK_OK) return fail(c, st, std::string("sketch: ") + rt_error(c->rt));
@@ -595,9 +746,8 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
         st = rt_consume_lists(c->rt, grid, stride, n);
         if (st != ZK_OK) return fail(c, st, std::string("sketch: ") + rt_error(c->rt));
     }
-    if (join) c->records_since_reset += n;
+    if (join) c->records_since_reset += n - skip;
     return ZK_OK;
-    ZK_CATCH(c)
 }
 
 zk_status zk_deps_finalize(zk_ctx* c, const zk_link_table* out) {
@@ -607,6 +757,7 @@ zk_status zk_deps_finalize(zk_ctx* c, const zk_link_table* out) {
     if (!out || !out->m0 || !out->m1 || !out->m2 || !out->m3 || !out->m4 || !out->present)
         return fail(c, ZK_ERR_INVALID_ARG, "null output array");
     ZK_HIP(c, hipSetDevice(c->device));
+    ZK_ST(flush_carry(c));  // the job ends here: a held-back trace is complete
     const uint64_t cells = (uint64_t)c->S * c->S;
     zk_link_table dev = *out;
     if (!out->device_ptrs) {
@@ -700,6 +851,7 @@ zk_status zk_deps_partial(zk_ctx* c, void** dev_ptr, uint64_t* bytes) {
     if (c->continued)
         return fail(c, ZK_ERR_INVALID_ARG, "zk_deps_partial after accumulating into a merged table (reset first)");
     ZK_HIP(c, hipSetDevice(c->device));
+    ZK_ST(flush_carry(c));  // the shard's part of the job ends here
     if (!c->merged)  // a merged tail already holds the job-wide counters
         ZK_HIP(c, launch_stats_fold(c->stats, (unsigned long long*)(c->table + (uint64_t)c->S * c->S * kLimbs),
                                     c->stream));

@@ -37,5 +37,9 @@ hipError_t launch_trace_set_rehash(const uint64_t* old, uint64_t old_slots, uint
                                    hipStream_t s);
 // out[0..ST_N) = sum over the kStatShards copies of the device counters
 hipError_t launch_stats_fold(const unsigned long long* shards, unsigned long long* out, hipStream_t s);
+// ZK_BATCH_CONTINUES: the batch's edge runs. out[0] = the first index i in [1, min(n, L + 1)) with
+// trace_id[i] != trace_id[i - 1] (~0 if none), out[1] = the last such index in [max(1, n - L - 1), n)
+// (0 if none). The caller zeroes out[1] and sets out[0] = ~0 first.
+hipError_t launch_edge_runs(const uint64_t* trace_id, uint64_t n, uint64_t L, unsigned long long* out, hipStream_t s);
 
 }  // namespace zk

@@ -681,6 +681,18 @@ __global__ __launch_bounds__(256) void k_trace_set_rehash(const unsigned long lo
     }
 }
 
+// the edge runs of a clustered batch (ZK_BATCH_CONTINUES): its first run's end and last run's start
+__global__ __launch_bounds__(256) void k_edge_runs(const uint64_t* __restrict__ tid, uint64_t n, uint64_t L,
+                                                   unsigned long long* __restrict__ out) {
+    const uint64_t head = n < L + 1 ? n : L + 1;
+    const uint64_t tail0 = n > L + 1 ? n - L - 1 : 1;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = 1 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < head; i += stride)
+        if (tid[i] != tid[i - 1]) atomicMin(&out[0], (unsigned long long)i);
+    for (uint64_t i = (tail0 > 1 ? tail0 : 1) + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        if (tid[i] != tid[i - 1]) atomicMax(&out[1], (unsigned long long)i);
+}
+
 // stats shards -> the 16 totals in the table's tail (zk_deps_partial)
 __global__ __launch_bounds__(256) void k_stats_fold(const unsigned long long* __restrict__ shards, int nshards,
                                                     unsigned long long* __restrict__ out) {
@@ -912,6 +924,11 @@ hipError_t launch_trace_set_rehash(const uint64_t* old, uint64_t old_slots, uint
                                    hipStream_t s) {
     return launch_checked("k_trace_set_rehash", k_trace_set_rehash, dim3(grid_for(old_slots + 1)), dim3(256), 0, s,
                           (const unsigned long long*)old, old_slots, (unsigned long long*)set, slots);
+}
+
+hipError_t launch_edge_runs(const uint64_t* trace_id, uint64_t n, uint64_t L, unsigned long long* out, hipStream_t s) {
+    if (n < 2) return hipSuccess;
+    return launch_checked("k_edge_runs", k_edge_runs, dim3(64), dim3(256), 0, s, trace_id, n, L, out);
 }
 
 hipError_t launch_stats_fold(const unsigned long long* shards, unsigned long long* out, hipStream_t s) {

@@ -107,6 +107,7 @@ struct JoinArgs {
     uint32_t nb;
     uint32_t cb_shift;  // bucket = cell >> cb_shift
     uint32_t join;      // 1: the dependency path (parent join + links); 0: sketch items only
+    uint32_t skip;      // 0 or 1: record 0 belongs to a run handled elsewhere (ZK_BATCH_CONTINUES)
     // realtime sketch items (zk_rt.hip), rt_pay == nullptr: none. K1 workgroup w writes rt_count[w]
     // items at w * link_stride; the spill kernel appends to list `grid` (capacity rt_spill_cap).
     uint64_t* rt_pay;

@@ -399,7 +399,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     uint64_t m_ev, m_od;  // this wave's boundary ballots of the current window (uniform; phase 3 reuses them)
     ZK_STAMP_DECL
     uint64_t ws = R0;         // window start (even)
-    uint64_t seek = R0;       // first record that may start one of our traces
+    uint64_t seek = R0 + (blockIdx.x == 0 ? a.skip : 0u);  // first record that may start one of our traces
     bool seek_start = false;  // seek is known to be a trace start (uniform)
     load_tid(a, ws, cur);
     load_early(a, ws, cur);
