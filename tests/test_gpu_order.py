@@ -17,20 +17,23 @@ pytestmark = pytest.mark.gpu
 
 
 def run(batches, S, **acc):
+    """verify (default True) keeps the clustering pass's P3 + K1; verify=False on batches of more
+    than 2^18 records takes the group join (k_group_join) and its fallback."""
     with DepsContext(S) as ctx:
         for b in batches:
             ctx.accumulate(b, **acc)
         return ctx.finalize(), ctx.stats()
 
 
+@pytest.mark.parametrize("verify", [True, False])
 @pytest.mark.parametrize("seed,traces,S", [(51, 20_000, 57), (52, 100_000, 500)])
-def test_any_permutation_equals_the_oracle(gpu, seed, traces, S):
+def test_any_permutation_equals_the_oracle(gpu, seed, traces, S, verify):
     cols = tracegen_host(seed, traces, max_depth=6, num_services=S)
     ref = oracle.aggregate(cols, S)
     perm = np.random.default_rng(seed).permutation(len(cols))
     shuffled = cols.take(perm)
     for batch in (shuffled, DeviceColumns.from_host(shuffled)):
-        got, st = run([batch], S)  # default: clustering pass + verification
+        got, st = run([batch], S, verify=verify)
         assert_parity(got, st, ref)
         assert st["not_clustered"] == 0
 
@@ -139,16 +142,17 @@ def unmix64(z):
     return (z ^ (z >> 30) ^ (z >> 60)) & M64
 
 
+@pytest.mark.parametrize("verify", [True, False])
 @pytest.mark.parametrize("traces,depth", [(150, 4), (1_500, 5), (6_000, 5), (40_000, 6)])
-def test_plan_shapes(gpu, traces, depth):
+def test_plan_shapes(gpu, traces, depth, verify):
     """P3 alone (<= 4096 records), P1 + P3 (<= 2048 x 256 records), and P1 + P2 + P3, host and
-    device pointers."""
+    device pointers; without verification the largest shape takes the group join."""
     S = 97
     cols = tracegen_host(55 + traces, traces, max_depth=depth, num_services=S)
     ref = oracle.aggregate(cols, S)
     perm = np.random.default_rng(traces).permutation(len(cols))
     for batch in (cols.take(perm), DeviceColumns.from_host(cols.take(perm))):
-        got, st = run([batch], S)
+        got, st = run([batch], S, verify=verify)
         assert_parity(got, st, ref)
         assert st["not_clustered"] == 0
 
@@ -233,9 +237,11 @@ def test_trace_hash_collisions_fail_with_capacity(gpu):
     assert_parity(got, st, oracle.aggregate(c, S))
 
 
-def test_shuffled_c2_shape_at_scale(gpu):
+@pytest.mark.parametrize("verify", [True, False])
+def test_shuffled_c2_shape_at_scale(gpu, verify):
     """2e7 device-generated TraceGen records (the bench's shape), shuffled on the device: the result
-    equals the clustered batch's bit for bit (m0..m4 and every counter)."""
+    equals the clustered batch's bit for bit (m0..m4 and every counter); verify=False: through the
+    group join."""
     import torch
 
     from zipkin_amd import tracegen_params
@@ -256,10 +262,48 @@ def test_shuffled_c2_shape_at_scale(gpu):
         a.accumulate(cols, clustered=True, verify=True, n=n)
         ra, sa = a.finalize(), a.stats()
     with DepsContext(S) as b:
-        b.accumulate(sc, clustered=False, verify=True)
+        b.accumulate(sc, clustered=False, verify=verify)
         rb, sb = b.finalize(), b.stats()
     for k in ("m0", "m1", "m2", "m3", "m4", "present"):
         assert np.array_equal(getattr(ra, k), getattr(rb, k)), k
     for k in sa:
         if k != "spilled_traces":
             assert sa[k] == sb[k], k
+
+
+def test_group_join_fallback(gpu):
+    """The group join's fallback: a 60k-record trace (spilled by K1), a 3k-record trace, and 900
+    crafted traces sharing their partition-hash digits (one ~4.5k-record sub-bucket) are longer than
+    the group join's LDS capacity; P3 clusters just those sub-buckets and K1 appends their links to
+    the group join's lists. Everything else (~300k records) is joined by the group join."""
+    S = 11
+    rows = star_trace(777, 30_000, nsvc=S) + star_trace(778, 1_500, nsvc=S)
+    for t in range(900):
+        tid = unmix64(((0x5A5A5A << 40) | (t * 2654435761 & ((1 << 40) - 1))) & M64) ^ PART_SALT
+        rows += star_trace(tid, 1 + t % 4, svc_root=t % S, nsvc=S)
+    for t in range(30_000):
+        rows += star_trace(100_000 + t, t % 9, svc_root=t % S, nsvc=S, fragments=1 + t % 2)
+    cols = cols_from_rows(rows)
+    assert len(cols) > 2 ** 18
+    ref = oracle.aggregate(cols, S)
+    shuffled = cols.take(np.random.default_rng(12).permutation(len(cols)))
+    for batch in (shuffled, DeviceColumns.from_host(shuffled)):
+        got, st = run([batch], S, verify=False)
+        assert_parity(got, st, ref)
+        assert st["spilled_traces"] >= 1
+
+
+def test_group_join_equals_the_trace_path(gpu, monkeypatch):
+    """The same shuffled batch through the group join and through P3 + K1 (ZK_GROUP_JOIN=0 at
+    create): identical tables and counters."""
+    S = 200
+    cols = tracegen_host(61, 60_000, max_depth=6, num_services=S)
+    shuffled = cols.take(np.random.default_rng(61).permutation(len(cols)))
+    got, st = run([shuffled], S, verify=False)
+    monkeypatch.setenv("ZK_GROUP_JOIN", "0")
+    ref, sr = run([shuffled], S, verify=False)
+    for k in ("m0", "m1", "m2", "m3", "m4", "present"):
+        assert np.array_equal(getattr(got, k), getattr(ref, k)), k
+    for k in st:
+        if k != "spilled_traces":
+            assert st[k] == sr[k], k

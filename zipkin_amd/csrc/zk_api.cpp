@@ -12,6 +12,8 @@
 #include <vector>
 
 #include "zk_cluster.h"
+#include <stdlib.h>
+
 #include "zk_internal.h"
 #include "zk_launch.h"
 #include "zk_rt_internal.h"
@@ -30,6 +32,9 @@ struct zk_ctx {
     bool strict = true;
     uint32_t max_trace = 131072;
     bool timing = false;
+    // unclustered batches through the group join (k_group_join); ZK_GROUP_JOIN=0 in the environment
+    // at create: through P3 + K1 instead (the A/B of profiles/r04/ab_group_join.txt)
+    bool group_join = true;
     uint64_t* table = nullptr;            // S*S*kLimbs
     bool own_table = true;
     unsigned long long* stats = nullptr;  // kStatShards*ST_N
@@ -236,12 +241,8 @@ SpanColsMut carve_cols(uint8_t* p, uint64_t n) {
     return m;
 }
 
-// clustering pass: d (any order) -> ctx-owned trace-clustered columns
-zk_status cluster_batch(zk_ctx* c, SpanColsDev* d) {
-    RoctxRange rr("zk_cluster_batch");
-    const uint64_t n = d->n;
-    if (n > 0xFFFFFFFFull) return fail(c, ZK_ERR_CAPACITY, "an unclustered batch is limited to 2^32-1 records");
-    const ClusterPlan plan = cluster_plan(n, c->cus);
+// the clustering pass's two column sets and scratch for n records under `plan`
+zk_status ensure_cluster(zk_ctx* c, uint64_t n, const ClusterPlan& plan) {
     const uint64_t tb = cluster_scratch_bytes(plan);
     if (n > c->cl_cap) {
         hipFree(c->cl_cols);
@@ -260,6 +261,17 @@ zk_status cluster_batch(zk_ctx* c, SpanColsDev* d) {
         ZK_HIP(c, hipMalloc(&c->cl_temp, tb));
         c->cl_temp_bytes = tb;
     }
+    return ZK_OK;
+}
+
+// clustering pass: d (any order) -> ctx-owned trace-clustered columns
+zk_status cluster_batch(zk_ctx* c, SpanColsDev* d) {
+    RoctxRange rr("zk_cluster_batch");
+    const uint64_t n = d->n;
+    if (n > 0xFFFFFFFFull) return fail(c, ZK_ERR_CAPACITY, "an unclustered batch is limited to 2^32-1 records");
+    const ClusterPlan plan = cluster_plan(n, c->cus);
+    const zk_status es = ensure_cluster(c, n, plan);
+    if (es != ZK_OK) return es;
     const SpanColsMut A = carve_cols(c->cl_cols, n);
     const SpanColsMut B = carve_cols(c->cl_cols + carved_bytes(n), n);
     int res = 0;
@@ -351,6 +363,7 @@ zk_status zk_ctx_create(const zk_config* cfg, zk_ctx** out) {
     c->S = cfg->num_services;
     c->strict = cfg->strict != 0;
     c->timing = cfg->timing != 0;
+    if (const char* e = getenv("ZK_GROUP_JOIN")) c->group_join = atoi(e) != 0;
     c->cus = prop.multiProcessorCount > 0 ? (uint32_t)prop.multiProcessorCount : 256;
     bucket_geometry(c->S, &c->nb, &c->cb_shift);
     if (cfg->max_trace_records) c->max_trace = cfg->max_trace_records;
@@ -638,12 +651,135 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
     ZK_CATCH(c)
 }
 
+// the join kernels' common arguments for n records of d
+static JoinArgs join_args(zk_ctx* c, const SpanColsDev& d) {
+    JoinArgs a{};
+    a.c = d;
+    a.table = c->table;
+    a.stats = c->stats;
+    a.S = c->S;
+    a.spill_count = c->spill_count;
+    a.spill_list = c->spill_list;
+    a.spill_cap = c->spill_cap;
+    a.spill_scratch = c->spill_scratch;
+    a.spill_scratch_stride = c->spill_stride;
+    a.max_trace = c->max_trace;
+    a.links = c->links;
+    a.link_count = c->link_count;
+    a.hist = c->hist;
+    a.nb = c->nb;
+    a.cb_shift = c->cb_shift;
+    a.join = 1u;
+    return a;
+}
+
+static zk_status reduce_links(zk_ctx* c, uint32_t grid, uint64_t stride) {
+    if (c->nb) {
+        ReduceArgs r{};
+        r.links = c->links;
+        r.counts = c->link_count;
+        r.stride = stride;
+        r.lists = grid;
+        r.hist = c->hist;
+        r.nb = c->nb;
+        r.cb_shift = c->cb_shift;
+        r.col_off = c->col_off;
+        r.bucket_base = c->bucket_base;
+        r.sorted = c->sorted;
+        r.table = c->table;
+        r.cells = (uint64_t)c->S * c->S;
+        ZK_HIP(c, launch_partitioned_reduce(r, c->stream));
+    } else {
+        ZK_HIP(c, launch_link_reduce(c->links, c->link_count, stride, grid, c->table, c->stream));
+    }
+    return ZK_OK;
+}
+
+// An unclustered batch through the group join: the clustering pass's partition (P0-P2) leaves every
+// trace inside one sub-bucket; k_group_join joins the sub-buckets in LDS, keyed by traceId. The
+// sub-buckets too long for it go through P3 (list mode) into the other column set, clustered, and K1
+// appends their links to the same lists; then K2/K3 and the spill kernel as for a clustered batch.
+static zk_status accumulate_groups(zk_ctx* c, const SpanColsDev& d, const ClusterPlan& plan) {
+    RoctxRange rr("zk_group_batch");
+    const uint64_t n = d.n;
+    ZK_ST(ensure_cluster(c, n, plan));
+    const SpanColsMut A = carve_cols(c->cl_cols, n);
+    const SpanColsMut B = carve_cols(c->cl_cols + carved_bytes(n), n);
+    EventPair ec, ej, er, es;
+    if (c->timing) {
+        ec = take_pair(c);
+        ZK_HIP(c, hipEventRecord(ec.a, c->stream));
+    }
+    ClusterGroups g{};
+    int res = 0;
+    ZK_HIP(c, launch_cluster(plan, d, A, B, c->cl_temp, c->cus, c->stream, &res, c->stats + ST_SPILL_OVERFLOW, &g));
+    if (c->timing) {
+        ZK_HIP(c, hipEventRecord(ec.b, c->stream));
+        c->ev_cluster.push_back(ec);
+    }
+    uint32_t grid = 0;
+    uint64_t per = 0, stride = 0;
+    group_join_geometry(n, c->cus, &grid, &per, &stride);
+    ZK_ST(ensure_spill(c, n));
+    ZK_ST(ensure_links(c, grid, stride, n));
+    ZK_HIP(c, hipMemsetAsync(c->spill_count, 0, 4, c->stream));
+    const SpanColsDev bd{B.trace_id, B.span_id, B.parent_id, B.first_ts, B.last_ts, B.service_id, B.flags, n};
+    const SpanColsDev ad{A.trace_id, A.span_id, A.parent_id, A.first_ts, A.last_ts, A.service_id, A.flags, n};
+    JoinArgs a = join_args(c, bd);
+    a.grid = grid;
+    a.per_wg = per;
+    a.link_stride = stride;
+    a.sub = g.sub;
+    a.nsub = g.nsub;
+    a.big_list = g.big_list;
+    a.big_count = g.big_count;
+    if (c->timing) {
+        ej = take_pair(c);
+        ZK_HIP(c, hipEventRecord(ej.a, c->stream));
+    }
+    ZK_HIP(c, launch_group_join(a, c->stream));
+    ZK_HIP(c, launch_cluster_fallback(plan, g, bd, A, c->cl_temp, c->cus, c->stream, c->stats + ST_SPILL_OVERFLOW));
+    JoinArgs f = join_args(c, ad);  // K1 over the fallback's clustered records A[0, *out_cursor)
+    f.grid = grid;
+    f.per_wg = (per + join_tile_records() - 1) / join_tile_records() * join_tile_records();
+    f.link_stride = stride;
+    f.n_dev = g.out_cursor;
+    f.append = 1u;
+    ZK_HIP(c, launch_join(f, c->stream));
+    if (c->timing) {
+        ZK_HIP(c, hipEventRecord(ej.b, c->stream));
+        c->ev_join.push_back(ej);
+        er = take_pair(c);
+        ZK_HIP(c, hipEventRecord(er.a, c->stream));
+    }
+    ZK_ST(reduce_links(c, grid, stride));
+    if (c->timing) {
+        ZK_HIP(c, hipEventRecord(er.b, c->stream));
+        c->ev_reduce.push_back(er);
+        es = take_pair(c);
+        ZK_HIP(c, hipEventRecord(es.a, c->stream));
+    }
+    ZK_HIP(c, launch_spill(f, c->spill_wgs, c->stream));
+    if (c->timing) {
+        ZK_HIP(c, hipEventRecord(es.b, c->stream));
+        c->ev_spill.push_back(es);
+    }
+    c->records_since_reset += n;
+    return ZK_OK;
+}
+
 // One batch already in HBM. skip (0 or 1): the first record belongs to a run handled elsewhere (it
 // only keeps the column pointers 16-byte aligned); K1 starts at the trace after it.
 static zk_status accumulate_dev(zk_ctx* c, SpanColsDev d, uint32_t flags, uint32_t skip) {
     const uint64_t n = d.n;
     if (n <= skip) return ZK_OK;
     const bool join = !c->rt || c->rt_mode == ZK_RT_WITH_DEPS;
+    // unclustered, without the trace check or a realtime sketch: the group join (two-level plans)
+    if (!(flags & ZK_BATCH_TRACE_CLUSTERED) && !(flags & ZK_BATCH_VERIFY_TRACES) && !c->rt && c->group_join &&
+        n <= 0xFFFFFFFFull) {
+        const ClusterPlan gp = cluster_plan(n, c->cus, true);
+        if (gp.b1 && gp.b2) return accumulate_groups(c, d, gp);
+    }
     if (!(flags & ZK_BATCH_TRACE_CLUSTERED)) {
         EventPair ec;
         if (c->timing) {

@@ -23,12 +23,27 @@ struct ClusterPlan {
     uint32_t grid;  // P0 / P1 workgroups
     uint64_t per;   // records per P0 / P1 workgroup (whole 8192-record chunks)
 };
-ClusterPlan cluster_plan(uint64_t n, uint32_t cus);
+// groups: the plan of the group join (k_group_join), sub-buckets of ~500-1000 records
+ClusterPlan cluster_plan(uint64_t n, uint32_t cus, bool groups = false);
 uint64_t cluster_scratch_bytes(const ClusterPlan& p);
-// in (any order) -> trace-clustered columns in A (*result = 0) or B (*result = 1); both hold n records
+// the partition's output for the group join: every trace inside one sub-bucket of B
+struct ClusterGroups {
+    const uint32_t* sub;             // nsub + 1 record bounds
+    uint32_t nsub;
+    uint32_t* big_list;              // sub-buckets the group join leaves to the fallback
+    unsigned int* big_count;
+    unsigned long long* out_cursor;  // the fallback's clustered records (its K1's record count)
+};
+// in (any order) -> trace-clustered columns in A (*result = 0) or B (*result = 1); both hold n records.
+// groups != nullptr and a two-level plan: P0-P2 only, B holds the sub-buckets, *groups describes them
+// (counters zeroed) and *result = 1.
 hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const SpanColsMut& A, const SpanColsMut& B,
                           void* scratch, uint32_t cus, hipStream_t s, int* result,
-                          unsigned long long* capacity_fail);
+                          unsigned long long* capacity_fail, ClusterGroups* groups = nullptr);
+// the group join's fallback: P3 over the listed sub-buckets of B into A[0, *out_cursor), clustered
+hipError_t launch_cluster_fallback(const ClusterPlan& p, const ClusterGroups& g, const SpanColsDev& B,
+                                   const SpanColsMut& A, void* scratch, uint32_t cus, hipStream_t s,
+                                   unsigned long long* capacity_fail);
 // insert the traceId of every segment start into `set` (slots: power of two; slot `slots` counts
 // traceId 0); *dup += segments whose traceId was already present
 hipError_t launch_trace_set_insert(const uint64_t* trace_id, uint64_t n, uint64_t* set, uint64_t slots,

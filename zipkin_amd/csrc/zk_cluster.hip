@@ -428,6 +428,11 @@ struct TraceArgs {
     uint32_t nsub;
     unsigned int* next;   // work counter: sub-buckets are handed out one at a time
     unsigned long long* fail;  // sub-buckets given up (ST_SPILL_OVERFLOW: finalize -> ZK_ERR_CAPACITY)
+    // list mode (the group join's fallback): only the sub-buckets list[0 .. *list_n), each written
+    // to a range claimed at out_cursor, so the listed traces end up clustered in [0, *out_cursor)
+    const uint32_t* list;
+    const unsigned int* list_n;
+    unsigned long long* out_cursor;
 };
 // A round that overflows the LDS table restarts its sub-bucket with twice the rounds. Rounds split
 // traces on bits 40.. of the trace hash, so traceIds crafted to share those bits (mix64 is invertible)
@@ -445,17 +450,28 @@ __global__ __launch_bounds__(kTrWG) void k_cl_traces(TraceArgs a) {
     __shared__ __align__(16) uint32_t s_cur[kTrStage];
     __shared__ uint32_t s_work;
     __shared__ uint32_t s_fail;
+    __shared__ uint64_t s_obase;
     __shared__ uint32_t s_tmp[32];
     const int t = threadIdx.x;
     constexpr int SPT = (kTrSlots + 1 + kTrWG - 1) / kTrWG;
     for (;;) {
         __syncthreads();  // every thread is past the previous sub-bucket's reads of s_work and the table
-        if (t == 0) s_work = atomicAdd(a.next, 1u);
+        if (t == 0) {
+            uint32_t w = atomicAdd(a.next, 1u);
+            if (a.list) {
+                w = w < *a.list_n ? a.list[w] : a.nsub;
+                if (w < a.nsub) s_obase = atomicAdd(a.out_cursor, (unsigned long long)(a.sub[w + 1] - a.sub[w]));
+            } else {
+                s_obase = w < a.nsub ? a.sub[w] : 0ull;
+            }
+            s_work = w;
+        }
         __syncthreads();
         const uint32_t w = s_work;
         if (w >= a.nsub) break;
         const uint64_t lo = a.sub[w], hi = a.sub[w + 1];
         const uint64_t len = hi - lo;
+        const uint64_t obase = s_obase;  // output position of the sub-bucket's first record
         // fast path (nearly every sub-bucket): the traceIds stay in registers, each record's rank
         // inside its trace comes back from the count's atomic, and the columns move through an LDS
         // stage with coalesced loads and stores (move_columns). The table holds up to kTrSlots / 2
@@ -531,7 +547,7 @@ __global__ __launch_bounds__(kTrWG) void k_cl_traces(TraceArgs a) {
 #pragma unroll
                 for (int k = 0; k < U; ++k) {
                     pos[k] = s_cnt[slot[k]] + rank[k];
-                    dest[k] = (uint32_t)lo + t + k * kTrWG;
+                    dest[k] = (uint32_t)obase + t + k * kTrWG;
                 }
                 move_columns<U, kTrWG, 0>(a.in, a.out, lo, (uint32_t)len, pos, dest,
                                           reinterpret_cast<uint64_t*>(s_cur), tids);
@@ -548,7 +564,7 @@ __global__ __launch_bounds__(kTrWG) void k_cl_traces(TraceArgs a) {
         uint32_t slots = 64;
         while (slots < 2 * (len / rounds + 1) && slots < kTrSlots) slots <<= 1;
         uint32_t smask = slots - 1;
-        uint64_t placed = lo;  // output position of this round's first record
+        uint64_t placed = obase;  // output position of this round's first record
         for (uint32_t r = 0; r < rounds; ++r) {
             for (uint32_t s = t; s < slots; s += kTrWG) {
                 s_key[s] = kEmptyKey;
@@ -600,7 +616,7 @@ __global__ __launch_bounds__(kTrWG) void k_cl_traces(TraceArgs a) {
                 slots = 64;
                 while (slots < 2 * (len / rounds + 1) && slots < kTrSlots) slots <<= 1;
                 smask = slots - 1;
-                placed = lo;
+                placed = obase;
                 r = ~0u;  // the loop's ++r makes it round 0
                 __syncthreads();  // every thread read s_fail before the next round clears it
                 continue;
@@ -724,12 +740,16 @@ size_t scan_bytes(uint64_t m) {
 
 }  // namespace
 
-ClusterPlan cluster_plan(uint64_t n, uint32_t cus) {
+ClusterPlan cluster_plan(uint64_t n, uint32_t cus, bool groups) {
     ClusterPlan p{};
     p.n = n;
-    // digit bits in all: sub-buckets of 1-2k records on average (P3's fast path takes up to 4096)
+    // digit bits in all: sub-buckets of 1-2k records on average (P3's fast path takes up to 4096);
+    // for the group join 3/8 of its LDS capacity, so that batches of whole sub-buckets fill it and
+    // hardly any sub-bucket exceeds it
     uint32_t bits = 0;
-    while (bits < 22 && (n >> bits) > 2048) ++bits;
+    uint64_t target = groups ? group_join_capacity() * 3 / 8 : 2048;
+    if (const char* e = groups ? getenv("ZK_CL_GROUP_TARGET") : nullptr) target = (uint64_t)atoi(e);  // A/B only
+    while (bits < 22 && (n >> bits) > target) ++bits;
     if (n <= kClusterSmall) bits = 0;  // P3 alone: one workgroup over the whole batch
     if (bits <= 8) {
         p.b1 = bits;
@@ -778,17 +798,20 @@ XLayout x_layout(const ClusterPlan& p) {
     return l;
 }
 
+// the group join's list of long sub-buckets and its two counters, at the end of the scratch
+uint64_t group_bytes(const ClusterPlan& p) { return align256((uint64_t)p.nb1 * p.nb2 * 4) + 256; }
+
 uint64_t cluster_scratch_bytes(const ClusterPlan& p) {
     const uint64_t m = (uint64_t)p.nb1 * p.grid;
     const XLayout xl = x_layout(p);
     const uint64_t sm = m > xl.m2 ? m : xl.m2;
     return 2 * align256(m * 4) + align256(((uint64_t)p.nb1 + 1) * 4) + align256(((uint64_t)p.nb1 * p.nb2 + 1) * 4) +
-           256 + xl.total + align256(scan_bytes(sm));
+           256 + xl.total + align256(scan_bytes(sm)) + group_bytes(p);
 }
 
 hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const SpanColsMut& A, const SpanColsMut& B,
                           void* scratch, uint32_t cus, hipStream_t s, int* result,
-                          unsigned long long* capacity_fail) {
+                          unsigned long long* capacity_fail, ClusterGroups* groups) {
     const uint64_t n = in.n;
     *result = 0;
     if (n == 0) return hipSuccess;
@@ -903,6 +926,16 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
                                  s, x2)
                 : launch_checked("k_cl_xscatter<local>", k_cl_xscatter<true, kMaxDigits>, dim3(gx), dim3(kXsWG), 0, s, x2);
         if (e != hipSuccess) return e;
+        if (groups) {  // the group join takes the sub-buckets from here
+            uint8_t* gp = (uint8_t*)scratch + cluster_scratch_bytes(p) - group_bytes(p);
+            groups->sub = sub;
+            groups->nsub = p.nb1 * p.nb2;
+            groups->big_list = (uint32_t*)gp;
+            groups->big_count = (unsigned int*)(gp + align256((uint64_t)p.nb1 * p.nb2 * 4));
+            groups->out_cursor = (unsigned long long*)(gp + align256((uint64_t)p.nb1 * p.nb2 * 4) + 64);
+            *result = 1;
+            return hipMemsetAsync(groups->big_count, 0, 128, s);
+        }
         ta.in = dev(B);
         ta.out = A;
         ta.sub = sub;
@@ -911,6 +944,30 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
     }
     const uint32_t g3 = ta.nsub < kTrGrid * cus ? ta.nsub : kTrGrid * cus;
     return launch_checked("k_cl_traces", k_cl_traces, dim3(g3), dim3(kTrWG), 0, s, ta);
+}
+
+hipError_t launch_cluster_fallback(const ClusterPlan& p, const ClusterGroups& g, const SpanColsDev& B,
+                                   const SpanColsMut& A, void* scratch, uint32_t cus, hipStream_t s,
+                                   unsigned long long* capacity_fail) {
+    // the work counter of launch_cluster's layout
+    const uint64_t m = (uint64_t)p.nb1 * p.grid;
+    uint8_t* bucket = (uint8_t*)scratch + 2 * align256(m * 4);
+    uint8_t* sub = bucket + align256(((uint64_t)p.nb1 + 1) * 4);
+    unsigned int* next = (unsigned int*)(sub + align256(((uint64_t)p.nb1 * p.nb2 + 1) * 4));
+    hipError_t e = hipMemsetAsync(next, 0, 4, s);
+    if (e != hipSuccess) return e;
+    TraceArgs ta{};
+    ta.in = B;
+    ta.out = A;
+    ta.sub = g.sub;
+    ta.nsub = g.nsub;
+    ta.next = next;
+    ta.fail = capacity_fail;
+    ta.list = g.big_list;
+    ta.list_n = g.big_count;
+    ta.out_cursor = g.out_cursor;
+    // one workgroup per CU: normally the list is empty and every workgroup leaves at once
+    return launch_checked("k_cl_traces<list>", k_cl_traces, dim3(cus ? cus : 256), dim3(kTrWG), 0, s, ta);
 }
 
 hipError_t launch_trace_set_insert(const uint64_t* trace_id, uint64_t n, uint64_t* set, uint64_t slots,

@@ -117,10 +117,25 @@ struct JoinArgs {
     uint64_t rt_spill_cap;
     uint64_t rt_seed;
     uint32_t rt_p;
+    // group join (k_group_join, unclustered batches): the sub-bucket bounds of the clustering pass's
+    // partition (every trace inside one sub-bucket), and the list of sub-buckets too long for LDS
+    const uint32_t* sub;      // nsub + 1 record bounds
+    uint32_t nsub;
+    uint32_t* big_list;       // [nsub] sub-bucket indices left to the fallback
+    unsigned int* big_count;
+    // K1 as the group join's fallback: the record count is on the device (n_dev, <= c.n) and the
+    // links append to the lists the group join wrote (append = 1)
+    const unsigned long long* n_dev;
+    uint32_t append;
 };
 
 // host-side launchers (implemented in the .hip files)
 hipError_t launch_join(const JoinArgs& a, hipStream_t s);
+// group join: one workgroup per CU; workgroup w owns the sub-buckets starting in [w*per_wg, (w+1)*per_wg)
+hipError_t launch_group_join(const JoinArgs& a, hipStream_t s);
+// geometry of the group join and of K1 as its fallback, sharing one set of link lists
+void group_join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, uint64_t* link_stride);
+uint32_t group_join_capacity();  // records of one sub-bucket the group join holds in LDS
 uint64_t join_tile_records();   // TILE (records per K1 window)
 // K1 launch geometry for n records on a device with `cus` compute units
 void join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, uint64_t* link_stride);

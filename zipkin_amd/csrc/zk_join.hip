@@ -302,14 +302,12 @@ __device__ __forceinline__ void window_ballots(const Window& w, uint64_t ws, int
 // merge barrier (phase 6 no longer reads them); parentId and flags at the top of the window's own
 // iteration. 26 -> 6 registers of prefetch against loading everything a window ahead (120 -> 101
 // VGPRs, K1 1.251 -> 1.227 -> 1.160 ms).
-__device__ __forceinline__ void load_tid(const JoinArgs& a, uint64_t ws, Window& w) {
-    const uint64_t n = a.c.n;
+__device__ __forceinline__ void load_tid(const JoinArgs& a, uint64_t n, uint64_t ws, Window& w) {
     const uint64_t i = ws + 2 * threadIdx.x;
     ld2_u64(a.c.trace_id, i, n, w.tid);
     w.prev = a.c.trace_id[(i > 0 && i - 1 < n) ? i - 1 : 0];
 }
-__device__ __forceinline__ void load_early(const JoinArgs& a, uint64_t ws, Window& w) {
-    const uint64_t n = a.c.n;
+__device__ __forceinline__ void load_early(const JoinArgs& a, uint64_t n, uint64_t ws, Window& w) {
     const uint64_t i = ws + 2 * threadIdx.x;
     ld2_u64(a.c.span_id, i, n, w.sid);
     ld2_u64((const uint64_t*)a.c.first_ts, i, n, w.first);
@@ -317,8 +315,7 @@ __device__ __forceinline__ void load_early(const JoinArgs& a, uint64_t ws, Windo
     ld2_u32(a.c.service_id, i, n, w.svc);
 }
 template <bool JOIN>
-__device__ __forceinline__ void load_late(const JoinArgs& a, uint64_t ws, Window& w) {
-    const uint64_t n = a.c.n;
+__device__ __forceinline__ void load_late(const JoinArgs& a, uint64_t n, uint64_t ws, Window& w) {
     const uint64_t i = ws + 2 * threadIdx.x;
     if constexpr (JOIN) {
         ld2_u64(a.c.parent_id, i, n, w.pid);
@@ -368,9 +365,16 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     __shared__ uint32_t s_hist[kMaxBuckets];  // links per cell bucket (K2's scatter offsets)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t n = a.c.n;
-    const uint64_t R0 = (uint64_t)blockIdx.x * a.per_wg;
+    // the group join's fallback: n on the device, ranges cut from it (per_wg bounds them)
+    const uint64_t n = a.n_dev ? (uint64_t)*a.n_dev : a.c.n;
+    uint64_t per = a.per_wg;
+    if (a.n_dev) {
+        const uint64_t q = ((n + a.grid - 1) / a.grid + TILE - 1) / TILE * TILE;
+        if (q < per) per = q ? q : TILE;
+    }
+    const uint64_t R0 = (uint64_t)blockIdx.x * per;
     if (R0 >= n) {
+        if (a.append) return;  // the lists and histogram keep what the group join wrote
         if (tid == 0) {
             a.link_count[blockIdx.x] = 0u;
             if (a.rt_count) a.rt_count[blockIdx.x] = 0u;
@@ -378,7 +382,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         for (uint32_t x = tid; x < a.nb; x += WG) a.hist[(uint64_t)x * a.grid + blockIdx.x] = 0u;
         return;
     }
-    const uint64_t R1 = (R0 + a.per_wg < n) ? R0 + a.per_wg : n;
+    const uint64_t R1 = (R0 + per < n) ? R0 + per : n;
     uint64_t* __restrict__ out = a.links + (uint64_t)blockIdx.x * a.link_stride;
     const uint64_t trash = a.link_stride - 1;  // never a real link slot (join_geometry)
     uint64_t* __restrict__ it_pay = a.rt_pay + (uint64_t)blockIdx.x * a.link_stride;
@@ -387,8 +391,8 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     StatPack st;
     int fold_in = kFoldWindows;  // windows until the next stat fold (uniform)
     if (tid < ST_N) s_stat[tid] = 0u;
-    if (tid == 0) s_cursor = 0ull;
-    for (uint32_t x = tid; x < a.nb; x += WG) s_hist[x] = 0u;
+    if (tid == 0) s_cursor = a.append ? (uint64_t)a.link_count[blockIdx.x] : 0ull;
+    for (uint32_t x = tid; x < a.nb; x += WG) s_hist[x] = a.append ? a.hist[(uint64_t)x * a.grid + blockIdx.x] : 0u;
     constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
     uint32_t r_clear[2] = {kNoSlot, kNoSlot};  // hash slots this thread's leaders of the last window hold
 
@@ -401,13 +405,13 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     uint64_t ws = R0;         // window start (even)
     uint64_t seek = R0 + (blockIdx.x == 0 ? a.skip : 0u);  // first record that may start one of our traces
     bool seek_start = false;  // seek is known to be a trace start (uniform)
-    load_tid(a, ws, cur);
-    load_early(a, ws, cur);
+    load_tid(a, n, ws, cur);
+    load_early(a, n, ws, cur);
     // the first window's ballots; later windows' are taken at the end of the window before (below)
     window_ballots(cur, ws, (int)((n - ws) < (uint64_t)TILE ? (n - ws) : (uint64_t)TILE), &m_ev, &m_od);
     if (lane == 0) *reinterpret_cast<ulonglong2*>(&s_mask[2 * wave]) = make_ulonglong2(m_ev, m_od);
     for (;;) {
-        load_late<JOIN>(a, ws, cur);
+        load_late<JOIN>(a, n, ws, cur);
         const int wn = (int)((n - ws) < (uint64_t)TILE ? (n - ws) : (uint64_t)TILE);
         // ---- 1. trace boundaries of the window (ballots taken at the end of the window before) --
         ZK_PHASE_SYNC(0);
@@ -496,7 +500,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         }
         if (!done && next_seek >= R1) done = true;
         const uint64_t next_ws = next_seek & ~1ull;
-        load_tid(a, done ? ws : next_ws, nxt);  // in flight during the LDS phases below (unconditional: see ld2)
+        load_tid(a, n, done ? ws : next_ws, nxt);  // in flight during the LDS phases below (unconditional: see ld2)
         ZK_STAMP(1);
         nrec += (uint64_t)(m - start);
         uint64_t n_ev = 0, n_od = 0;  // the next window's ballots
@@ -616,7 +620,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             }
         }
         ZK_PHASE_SYNC(4);
-        load_early(a, done ? ws : next_ws, cur);  // phase 6 no longer reads these registers
+        load_early(a, n, done ? ws : next_ws, cur);  // phase 6 no longer reads these registers
 
         // ---- 6. filter(isValid), join on (parentId, traceId), (cell, duration) links ----------
         uint64_t r_link[2], r_item[2];
@@ -858,7 +862,7 @@ __global__ __launch_bounds__(kSpillWG) void k_span_join_spill(JoinArgs a) {
     __shared__ unsigned long long s_end;
     __shared__ unsigned long long s_stat[ST_N];
     const uint32_t total = min(*a.spill_count, (unsigned int)a.spill_cap);
-    const uint64_t n = a.c.n;
+    const uint64_t n = a.n_dev ? (uint64_t)*a.n_dev : a.c.n;
     const uint64_t* __restrict__ tr = a.c.trace_id;
     uint8_t* base = a.spill_scratch + (uint64_t)blockIdx.x * a.spill_scratch_stride;
     StatWide st;
@@ -1030,6 +1034,387 @@ __global__ __launch_bounds__(kSpillWG) void k_span_join_spill(JoinArgs a) {
     }
 }
 
+// =============================================================================================
+// K1G: the join over hash groups (unclustered batches)
+//
+// The clustering pass's partition (zk_cluster.hip P0-P2) leaves every trace inside one sub-bucket,
+// its records in any order. Instead of clustering each sub-bucket (P3) and streaming K1 over the
+// result, one workgroup per CU takes whole sub-buckets of <= kGCap records into LDS and keys the
+// same merge and join by (traceId, spanId) and (traceId, parentId): the groupBy((id, traceId)) and
+// the (parentId, traceId) join of ZipkinAggregateJob.scala:21-33 with the traceId in the key, as
+// the reference has it, instead of a trace segment. Every record is read from HBM once (48 B);
+// P3's 104 B per record and K1's second read of the columns are gone. The next sub-bucket's columns
+// load into a second register window while this one is joined. Sub-buckets longer than kGCap
+// (a trace of > 2k records, or an unlucky hash range) are listed and left to the fallback: P3 over
+// the listed sub-buckets only, then K1 (append mode) over its output, into the same link lists.
+//
+// Slot word (u32): bits 0..11 leader position + 1; 12..21 the fragment bits of K1's slot word;
+// 22..31 a 10-bit fingerprint of the key hash, so a probe loads the occupant's traceId and spanId
+// only when the fingerprint matches.
+// =============================================================================================
+#ifndef ZK_GJ_WG
+#define ZK_GJ_WG 1024  // group-join workgroup: 2 x WG positions of LDS per batch
+#endif
+#ifndef ZK_GJ_HF
+#define ZK_GJ_HF 4  // hash slots per LDS position
+#endif
+constexpr int kGWG = ZK_GJ_WG;
+constexpr int kGCap = 2 * kGWG;      // positions of a batch in LDS (two per thread, pair-aligned)
+constexpr int kGH = ZK_GJ_HF * kGCap;  // hash slots: load <= 1/4 (~1/8 at the plan's batches)
+constexpr int kGPerCU = kGWG >= 1024 ? 1 : kGWG >= 512 ? 2 : 4;  // resident workgroups per CU (LDS)
+constexpr uint32_t kGIdx = 0xFFFu;
+constexpr int kGFpShift = 22;
+static_assert(kGCap < (int)kGIdx && kSlotP0 < (1u << kGFpShift), "slot word fields");
+
+// the 32-bit hash of key (traceId, x): tmix = traceId * golden, computed once per record
+__device__ __forceinline__ uint32_t group_hash(uint64_t tmix, uint64_t x) {
+    uint64_t h = x ^ tmix;
+    h ^= h >> 33;
+    h *= 0xFF51AFD7ED558CCDull;
+    h ^= h >> 33;
+    h *= 0xC4CEB9FE1A85EC53ull;
+    h ^= h >> 33;
+    return (uint32_t)h;
+}
+
+__device__ __forceinline__ void load_group(const JoinArgs& a, uint64_t base, Window& w) {
+    load_tid(a, a.c.n, base, w);
+    load_early(a, a.c.n, base, w);
+    load_late<true>(a, a.c.n, base, w);
+}
+
+__global__ __launch_bounds__(kGWG, kGPerCU * kGWG / 256) void k_group_join(JoinArgs a) {
+    __shared__ __align__(16) uint64_t s_tid[kGCap];
+    __shared__ __align__(16) uint64_t s_sid[kGCap];
+    __shared__ __align__(16) long long s_first[kGCap];
+    __shared__ __align__(16) long long s_last[kGCap];
+    __shared__ __align__(16) uint64_t s_pid[kGCap];
+    __shared__ __align__(16) uint32_t s_svck[kGCap];
+    __shared__ __align__(16) uint32_t s_ht[kGH];
+    __shared__ uint32_t s_stat[ST_N];
+    __shared__ uint32_t s_hist[kMaxBuckets];
+    __shared__ uint32_t s_cursor;
+    __shared__ uint32_t s_find[2];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const uint64_t n = a.c.n;
+    const uint32_t nsub = a.nsub;
+    const uint64_t R0 = (uint64_t)blockIdx.x * a.per_wg;
+    const uint64_t R1 = (R0 + a.per_wg < n) ? R0 + a.per_wg : n;
+    if (tid < ST_N) s_stat[tid] = 0u;
+    if (tid == 0) {
+        s_cursor = 0u;
+        s_find[0] = kGWG;
+        s_find[1] = nsub;
+    }
+    for (uint32_t x = tid; x < a.nb; x += kGWG) s_hist[x] = 0u;
+    for (int x = tid; x < kGH / 4; x += kGWG) reinterpret_cast<uint4*>(s_ht)[x] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    // first owned sub-bucket: the first g with sub[g] >= R0, in two parallel rounds (sub[nsub] = n > R0)
+    uint32_t g0 = nsub;
+    if (R0 < n) {
+        // samples min(t * step, nsub), t < kGWG: the last one is nsub, so some sample is >= R0
+        const uint32_t step = nsub / (kGWG - 1) + 1;
+        {
+            const uint32_t x = (uint32_t)tid * step < nsub ? (uint32_t)tid * step : nsub;
+            if (a.sub[x] >= R0) atomicMin(&s_find[0], (uint32_t)tid);
+        }
+        __syncthreads();
+        const uint32_t c = s_find[0];  // the first sample >= R0: g0 lies in (sample c-1, sample c]
+        const uint32_t lo_g = c == 0 ? 0u : (c - 1) * step + 1;
+        const uint32_t hi_g = c * step < nsub ? c * step : nsub;
+        for (uint32_t x = lo_g + tid; x <= hi_g; x += kGWG)
+            if (a.sub[x] >= R0) atomicMin(&s_find[1], x);
+        __syncthreads();
+        g0 = s_find[1];
+    }
+    // Batches: runs of whole consecutive sub-buckets of <= kGCap records in all (the keys carry the
+    // traceId, so sub-buckets share the LDS table freely). Every wave holds the bounds of the next 64
+    // sub-buckets in a lane each (one vector load, issued a batch ahead) and cuts the batch with two
+    // ballots: the longest prefix that fits and whose sub-buckets start in this workgroup's range.
+    // A sub-bucket longer than kGCap alone is listed for the fallback. (uniform)
+    auto fetch = [&](uint32_t gs) -> uint32_t {
+        const uint32_t g = gs + (uint32_t)lane;
+        return a.sub[g < nsub ? g : nsub];
+    };
+    // -> next first sub-bucket; [*lo, *hi) the batch's records (empty: none, or a window of only
+    // empty / listed sub-buckets, *more = 1: fetch at the returned index and cut again)
+    auto cut = [&](uint32_t gs, uint32_t bv, uint32_t* lo, uint32_t* hi, bool* more) -> uint32_t {
+        *lo = *hi = 0u;
+        *more = false;
+        const uint64_t own = __ballot(gs + (uint32_t)lane < nsub && bv < R1);  // sub-buckets starting in range
+        int o = 0;
+        for (;;) {
+            if (o >= 63) {
+                *more = true;
+                return gs + (uint32_t)o;
+            }
+            if (!((own >> o) & 1ull)) return nsub;  // the rest belongs to the next workgroups
+            const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bv, o);
+            const uint32_t off = b0 & 1u;
+            // lane l > o ends a batch of sub-buckets o..l-1 that fits (a prefix: the bounds rise)
+            const uint64_t fit = __ballot(lane > o && gs + (uint32_t)lane <= nsub && bv - b0 + off <= (uint32_t)kGCap);
+            // ends up to the first sub-bucket not in range
+            const uint64_t notown = ~own & (~0ull << o);
+            const int q = notown ? __ffsll((unsigned long long)notown) - 1 : 64;
+            int l = o + __popcll(fit);
+            if (l > q) l = q;
+            if (l > o) {
+                *lo = b0;
+                *hi = (uint32_t)__builtin_amdgcn_readlane((int)bv, l);
+                if (*hi == b0) *more = true;  // empty sub-buckets only
+                return gs + (uint32_t)l;
+            }
+            // sub-bucket o alone is longer than the LDS capacity
+            if (tid == 0) a.big_list[atomicAdd(a.big_count, 1u)] = gs + (uint32_t)o;  // (every wave cuts alike)
+            ++o;
+        }
+    };
+    // the next batch with records at or after gs (bv = fetch(gs)); *lo == *hi: none left
+    auto next_batch = [&](uint32_t gs, uint32_t bv, uint32_t* lo, uint32_t* hi) -> uint32_t {
+        for (;;) {
+            bool more;
+            gs = cut(gs, bv, lo, hi, &more);
+            if (!more) return gs;
+            bv = fetch(gs);
+        }
+    };
+
+    StatPack st;
+    int fold_in = kFoldWindows;
+    uint64_t nrec = 0;
+    constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+    uint32_t r_clear[2] = {kNoSlot, kNoSlot};
+    uint64_t* __restrict__ out = a.links + (uint64_t)blockIdx.x * a.link_stride;
+    const uint64_t trash = a.link_stride - 1;
+
+    auto run_group = [&](const Window& cur, uint32_t lo, uint32_t hi) {
+        const uint32_t len = hi - lo;
+        const int off = (int)(lo & 1u);
+        nrec += len;
+        // ---- stage: transformed values at positions 2t, 2t+1 (position p = record lo - off + p) ---
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+            if (r_clear[e] != kNoSlot) s_ht[r_clear[e]] = 0u;  // the previous group's leaders
+        const int j0 = 2 * tid;
+        bool act[2];
+        uint32_t r_svck[2];
+        bool r_rerr[2];
+        uint64_t tmix[2];
+        {
+            uint64_t v_first[2], v_last[2], v_pid[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                act[e] = j0 + e >= off && j0 + e < off + (int)len;
+                tmix[e] = cur.tid[e] * 0x9E3779B97F4A7C15ull;
+                r_rerr[e] = false;
+                r_svck[e] = svc_key(cur.flags[e], cur.svc[e], a.S, &r_rerr[e]);
+                const uint32_t f = cur.flags[e];
+                const bool ha = (f & ZK_F_HAS_ANNOTATIONS) != 0;
+                v_first[e] = ha ? cur.first[e] : (uint64_t)LLONG_MAX;
+                v_last[e] = ha ? cur.last[e] : (uint64_t)LLONG_MIN;
+                v_pid[e] = (f & ZK_F_HAS_PARENT) ? cur.pid[e] : ~0ull;
+            }
+            *reinterpret_cast<ulonglong2*>(&s_tid[j0]) = make_ulonglong2(cur.tid[0], cur.tid[1]);
+            *reinterpret_cast<ulonglong2*>(&s_sid[j0]) = make_ulonglong2(cur.sid[0], cur.sid[1]);
+            *reinterpret_cast<ulonglong2*>(&s_first[j0]) = make_ulonglong2(v_first[0], v_first[1]);
+            *reinterpret_cast<ulonglong2*>(&s_last[j0]) = make_ulonglong2(v_last[0], v_last[1]);
+            *reinterpret_cast<ulonglong2*>(&s_pid[j0]) = make_ulonglong2(v_pid[0], v_pid[1]);
+            *reinterpret_cast<uint2*>(&s_svck[j0]) = make_uint2(r_svck[0], r_svck[1]);
+        }
+        __syncthreads();  // staged; every slot of the previous group is empty
+        // ---- groupBy((id, traceId)): the first fragment to claim a slot leads ------------------
+        int r_leader[2];
+        uint32_t r_slot[2];
+        {
+            uint32_t word[2], fp[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                r_leader[e] = -1;
+                const uint32_t h = group_hash(tmix[e], cur.sid[e]);
+                r_slot[e] = h & (kGH - 1);
+                fp[e] = h >> kGFpShift;
+                uint32_t once;
+                word[e] = (uint32_t)(j0 + e + 1) | frag_bits(cur.flags[e], &once) | (fp[e] << kGFpShift);
+            }
+            bool pend[2] = {act[0], act[1]};
+            while (pend[0] || pend[1]) {
+                uint32_t old[2];
+#pragma unroll
+                for (int e = 0; e < 2; ++e) old[e] = pend[e] ? atomicCAS(&s_ht[r_slot[e]], 0u, word[e]) : 0u;
+                int o[2];
+                bool cand[2];
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    o[e] = (int)(old[e] & kGIdx) - 1;
+                    if (pend[e] && old[e] == 0u) {
+                        r_leader[e] = j0 + e;
+                        pend[e] = false;
+                    }
+                    cand[e] = pend[e] && (old[e] >> kGFpShift) == fp[e];
+                }
+                uint64_t osid[2], otid[2];
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    osid[e] = cand[e] ? s_sid[o[e]] : ~cur.sid[e];
+                    otid[e] = cand[e] ? s_tid[o[e]] : ~cur.tid[e];
+                }
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    if (!pend[e]) continue;
+                    if (osid[e] == cur.sid[e] && otid[e] == cur.tid[e]) {
+                        r_leader[e] = o[e];
+                        pend[e] = false;
+                    } else {
+                        r_slot[e] = (r_slot[e] + 1) & (kGH - 1);
+                    }
+                }
+            }
+        }
+        // ---- reduce(mergeSpan) into the leader (no barrier: see K1 phase 5) ----------------------
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int j = j0 + e;
+            const int L = r_leader[e];
+            if (L >= 0 && L != j) {
+                const uint32_t f = cur.flags[e];
+                if (f & ZK_F_HAS_ANNOTATIONS) {
+                    atomicMin(&s_first[L], (long long)cur.first[e]);
+                    atomicMax(&s_last[L], (long long)cur.last[e]);
+                }
+                if (r_svck[e] != kSvcNone) atomicMin(&s_svck[L], r_svck[e]);
+                if (f & ZK_F_HAS_PARENT) atomicMin((unsigned long long*)&s_pid[L], (unsigned long long)cur.pid[e]);
+                uint32_t once;
+                const uint32_t bits = frag_bits(f, &once);
+                uint32_t* const wp = &s_ht[r_slot[e]];
+                const uint32_t old = atomicOr(wp, bits);
+                const uint32_t promote = once & (old >> kSlotA) & 0xFu;
+                if (promote) atomicOr(wp, promote << kSlotB);
+            }
+        }
+        __syncthreads();  // merged
+        // ---- filter(isValid), join on (parentId, traceId), links ---------------------------------
+        uint64_t r_link[2];
+        uint32_t nl = 0;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            r_link[e] = ~0ull;
+            const int L = r_leader[e];
+            if (L < 0) continue;
+            const int j = j0 + e;
+            const uint32_t f = cur.flags[e];
+            const uint32_t w = s_ht[r_slot[e]];
+            const uint32_t sL = s_svck[L];
+            const uint64_t pL = s_pid[L];
+            bool amb = (f & ZK_F_HAS_PARENT) ? (cur.pid[e] != pL) : ((w & kSlotP1) != 0u);
+            const uint32_t sk = r_svck[e];
+            if (sk != kSvcNone && (sk >> kSvcKindShift) == (sL >> kSvcKindShift) && sk != sL) amb = true;
+            if (amb) st.inc(ST_AMBIGUOUS);
+            if (r_rerr[e]) st.inc(ST_SVC_RANGE);
+            if (L != j) continue;
+            st.inc(ST_MERGED);
+            const bool valid = slot_valid(w);
+            st.inc(valid ? ST_VALID : ST_INVALID);
+            if (!(valid && (w & kSlotP1))) continue;
+            st.inc(ST_CHILD);
+            const uint32_t hp = group_hash(tmix[e], pL);
+            const uint32_t pfp = hp >> kGFpShift;
+            uint32_t slot = hp & (kGH - 1);
+            uint32_t pw = 0, sp = kSvcNone;
+            for (;;) {
+                const uint32_t o = s_ht[slot];
+                if (o == 0u) break;
+                if ((o >> kGFpShift) == pfp) {
+                    const int oi = (int)(o & kGIdx) - 1;
+                    const uint64_t osid = s_sid[oi];
+                    const uint64_t otid = s_tid[oi];
+                    const uint32_t osvc = s_svck[oi];
+                    if (osid == pL && otid == cur.tid[e]) {
+                        pw = o;
+                        sp = osvc;
+                        break;
+                    }
+                }
+                slot = (slot + 1) & (kGH - 1);
+            }
+            if (pw == 0u || !slot_valid(pw)) {
+                st.inc(ST_MISSING_PARENT);
+                continue;
+            }
+            st.inc(ST_JOINED);
+            if (sp == kSvcNone || sL == kSvcNone) {
+                st.inc(ST_NO_SERVICE);
+                continue;
+            }
+            const uint64_t d = (uint64_t)(s_last[j] - s_first[j]);
+            if (d >= kMaxDuration) {
+                st.inc(ST_DUR_RANGE);
+                continue;
+            }
+            const uint64_t cell = (uint64_t)(sp & kSvcIdMask) * a.S + (sL & kSvcIdMask);
+            r_link[e] = (cell << 40) | d;
+            if (a.nb) atomicAdd(&s_hist[cell >> a.cb_shift], 1u);
+            ++nl;
+        }
+        // ---- append: one LDS atomic per wave claims its slice of the workgroup's list ------------
+        const uint64_t l1 = __ballot(nl >= 1u), l2 = __ballot(nl >= 2u);
+        uint32_t lbase = 0;
+        {
+            const uint32_t wtot = (uint32_t)(__popcll(l1) + __popcll(l2));
+            uint32_t old = 0;
+            if (lane == 0 && wtot) old = atomicAdd(&s_cursor, wtot);
+            lbase = (uint32_t)__shfl((int)old, 0) + lanes_below(l1) + lanes_below(l2);
+        }
+        uint32_t pos = lbase;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const bool v = r_link[e] != ~0ull;
+            out[v ? (uint64_t)pos : trash] = r_link[e];
+            pos += v ? 1u : 0u;
+        }
+#pragma unroll
+        for (int e = 0; e < 2; ++e) r_clear[e] = (r_leader[e] == j0 + e) ? r_slot[e] : kNoSlot;
+        if (--fold_in == 0) {
+            fold_stats(st, s_stat);
+            fold_in = kFoldWindows;
+        }
+        __syncthreads();  // every probe of this group is done before the next one is staged
+    };
+
+    // two register windows: one batch's columns load while the other batch is joined; the bounds
+    // of the batch after both load while the first is joined
+    Window wa, wb;
+    uint32_t la = 0, ha = 0, lb = 0, hb = 0;
+    uint32_t gs = g0;
+    uint32_t bv = fetch(gs);
+    gs = next_batch(gs, bv, &la, &ha);
+    if (ha > la) load_group(a, la & ~1u, wa);
+    bv = fetch(gs);
+    gs = next_batch(gs, bv, &lb, &hb);
+    if (hb > lb) load_group(a, lb & ~1u, wb);
+    bv = fetch(gs);
+    for (;;) {
+        if (ha <= la) break;
+        run_group(wa, la, ha);
+        gs = next_batch(gs, bv, &la, &ha);
+        if (ha > la) load_group(a, la & ~1u, wa);
+        bv = fetch(gs);
+        if (hb <= lb) break;
+        run_group(wb, lb, hb);
+        gs = next_batch(gs, bv, &lb, &hb);
+        if (hb > lb) load_group(a, lb & ~1u, wb);
+        bv = fetch(gs);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        a.link_count[blockIdx.x] = s_cursor;
+        atomicAdd(&a.stats[(uint64_t)(blockIdx.x % kStatShards) * ST_N + ST_RECORDS], (unsigned long long)nrec);
+    }
+    fold_stats(st, s_stat);
+    publish_stats(s_stat, a.stats);  // its barrier also publishes s_hist
+    for (uint32_t x = tid; x < a.nb; x += kGWG) a.hist[(uint64_t)x * a.grid + blockIdx.x] = s_hist[x];
+}
+
 // tile geometry of the shipped K1
 #ifndef ZK_K1_WG
 #define ZK_K1_WG 256  // K1 workgroup; a window is two records per thread
@@ -1063,6 +1448,26 @@ hipError_t launch_spill(const JoinArgs& a, uint32_t spill_wgs, hipStream_t s) {
 }
 
 uint64_t join_tile_records() { return kTile; }
+
+hipError_t launch_group_join(const JoinArgs& a, hipStream_t s) {
+    if (a.c.n == 0) return hipSuccess;
+    return launch_checked("k_group_join", k_group_join, dim3(a.grid), dim3(kGWG), 0, s, a);
+}
+
+uint32_t group_join_capacity() { return kGCap; }
+
+void group_join_geometry(uint64_t n, uint32_t cus, uint32_t* grid, uint64_t* per_wg, uint64_t* link_stride) {
+    uint64_t g = (uint64_t)(cus ? cus : 256) * kGPerCU;
+    const uint64_t by_n = (n + kGCap - 1) / kGCap;
+    if (g > by_n) g = by_n ? by_n : 1;
+    const uint64_t per = (n + g - 1) / g;
+    *grid = (uint32_t)g;
+    *per_wg = per ? per : 1;
+    // the group join's links (its sub-buckets start in its range: <= per + kGCap records), then the
+    // fallback K1's (a range of <= per_wg rounded to tiles, + an overhanging trace), + the trash slot
+    const uint64_t fb = (*per_wg + kTile - 1) / kTile * kTile + kTile;
+    *link_stride = *per_wg + kGCap + fb + 1;
+}
 
 #ifdef ZK_STAMPS
 extern "C" int zk_debug_stamps(unsigned long long* out, int reset) {

@@ -304,6 +304,9 @@ __global__ __launch_bounds__(kPxWG, kPxWG / 256) void k_part_xscatter_static(Par
     const uint64_t plo = a.part_lo[p], phi = a.part_lo[p + 1];
     unsigned int* const cur = a.cursor + (uint64_t)p * S;
     for (uint32_t b = t; b < S; b += kPxWG) s_cnt[b] = 0u;
+    // the zeros are published before any wave's first count (a wave's zeroing that waits behind a
+    // slow global load would otherwise erase another wave's first counts)
+    __syncthreads();
     uint64_t nv[kPxU];
     uint32_t nbk[kPxU];
     auto load = [&](uint32_t j) {
@@ -466,9 +469,24 @@ hipError_t partition_impl(const PartitionPlan& p, const uint32_t* svc, const uin
     uint32_t* offs = (uint32_t*)((uint8_t*)scratch + a);
     void* temp = (uint8_t*)scratch + 2 * a;
     size_t temp_bytes = scan_temp_bytes(m);
+    hipError_t e = hipSuccess;
+    const bool xcd = !counts && p.S <= kLineMaxS && n > 0;
+    PartX x{};
+    uint32_t gx = 0;
+    if (xcd) {
+        x.svc = svc;
+        x.payload = payload;
+        x.out = out;
+        x.S = p.S;
+        x.hash = hash;
+        x.hash_seed = hash_seed;
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        gx = (uint32_t)(cus > 0 ? cus : 256);
+    }
     const size_t lds = (size_t)p.S * 4;
-    hipError_t e = launch_checked("k_part_hist", k_part_hist, dim3(p.grid), dim3(kPartWG), lds, s, svc, n, p.per_wg,
-                                  counts, p.S, p.grid, hist, dropped);
+    e = launch_checked("k_part_hist", k_part_hist, dim3(p.grid), dim3(kPartWG), lds, s, svc, n, p.per_wg, counts, p.S,
+                       p.grid, hist, dropped);
     if (e != hipSuccess) return e;
     e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, hist, offs, (int)m, s);
     if (e != hipSuccess) return e;
@@ -481,19 +499,11 @@ hipError_t partition_impl(const PartitionPlan& p, const uint32_t* svc, const uin
     if (e != hipSuccess) return e;
     uint64_t dyn = 0;
     const int choice = partition_scatter_choice(p.S, st_lines, st_items, &dyn);
-    if (!counts && p.S <= kLineMaxS && n > 0) {
-        uint8_t* xp = (uint8_t*)temp + temp_bytes;
-        PartX x{};
-        x.svc = svc;
-        x.payload = payload;
-        x.out = out;
-        x.S = p.S;
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const uint32_t gx = (uint32_t)(cus > 0 ? cus : 256);
-        // every portion needs a workgroup: the static scatter gives portion q to blocks q, q + parts, ...
+    if (xcd) {
+        // write streams shared per XCD: portion cursors claimed per chunk
         x.parts = p.grid < kPartParts ? p.grid : kPartParts;
         if (x.parts > gx) x.parts = gx;
+        uint8_t* xp = (uint8_t*)temp + temp_bytes;
         x.cursor = (unsigned int*)xp;
         xp += ((uint64_t)kPartParts * p.S * 4 + 255) & ~255ull;
         uint64_t* part_lo = (uint64_t*)xp;
@@ -502,13 +512,10 @@ hipError_t partition_impl(const PartitionPlan& p, const uint32_t* svc, const uin
         x.part_lo = part_lo;
         x.part_tiles = part_tiles;
         x.next = next;
-        x.hash = hash;
-        x.hash_seed = hash_seed;
         e = launch_checked("k_part_xprep", k_part_xprep, dim3((x.parts * p.S + 255) / 256), dim3(256), 0, s,
                            (const uint32_t*)offs, p.S, p.grid, x.parts, p.per_wg, n, x.cursor, part_lo, part_tiles, next);
-        if (e == hipSuccess) {
+        if (e == hipSuccess)
             e = launch_checked("k_part_xscatter_static", k_part_xscatter_static, dim3(gx), dim3(kPxWG), 0, s, x);
-        }
     } else if (choice == kScatterLines)
         e = launch_checked("k_part_scatter_lines", k_part_scatter_lines<kLineU, kLineWG>, dim3(p.grid),
                            dim3(kLineWG), dyn, s, svc, payload, n, p.per_wg, counts, p.S, p.grid, offs, out, hash,
