@@ -403,18 +403,19 @@ def main():
             # set's reduce, so their event spans are not a kernel duration: detail.pipelined_k1_*.
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_span_join_stream",
+                "kernel": ("k_group_join (+ the fallback's P3 list pass and K1 append, normally empty)"
+                           if shuffled and not a.verify else "k_span_join_stream"),
                 "achieved": n * BYTES_PER_RECORD / (k1_isolated_ms * 1e-3) / 1e9,
                 "peak": PEAK_HBM_GBS,
                 "unit": "GB/s",
                 "frac": n * BYTES_PER_RECORD / (k1_isolated_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
-                "traffic": traffic,
-                "traffic_source": traffic_src,
+                "traffic": traffic if not shuffled else None,
+                "traffic_source": traffic_src if not shuffled else None,
                 "algorithmic_bytes_per_launch": n * BYTES_PER_RECORD,
                 "bytes_per_record": BYTES_PER_RECORD,
                 "avg_launch_ms": k1_isolated_ms,
                 "launches": isolated_launches,
-                "timing": "HIP events on the ctx stream around each K1 launch of serial (non-overlapped) steps",
+                "timing": "HIP events on the ctx stream around each join launch of serial (non-overlapped) steps",
                 # the whole step's algorithmic bytes (K1's input) over the step time
                 "step_frac": n * BYTES_PER_RECORD / (elapsed / a.steps) / 1e9 / PEAK_HBM_GBS,
             },

@@ -117,6 +117,7 @@ constexpr uint32_t kMaxDigits = 2048;   // <= 11 bits per level
 // levels of <= 256 digits (8 bits: every level up to 2^24 records) run a variant with byte digit
 // tags and smaller digit arrays
 constexpr uint32_t kSmallDigits = 256;
+constexpr uint32_t kMidDigits = 512;  // (the group join's plans: 9-bit levels)
 
 // column C (0..6) of a batch: the u64 columns first, then service_id and flags (u32)
 template <int C>
@@ -883,6 +884,8 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
     e = p.nb1 <= kSmallDigits
             ? launch_checked("k_cl_xscatter<global,256>", k_cl_xscatter<false, kSmallDigits>, dim3(gx), dim3(kXsWG), 0, s,
                              x1)
+        : p.nb1 <= kMidDigits
+            ? launch_checked("k_cl_xscatter<global,512>", k_cl_xscatter<false, kMidDigits>, dim3(gx), dim3(kXsWG), 0, s, x1)
             : launch_checked("k_cl_xscatter<global>", k_cl_xscatter<false, kMaxDigits>, dim3(gx), dim3(kXsWG), 0, s, x1);
     if (e != hipSuccess) return e;
     if (!p.b2) {  // P3: A -> B
@@ -924,6 +927,9 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
         e = p.nb2 <= kSmallDigits
                 ? launch_checked("k_cl_xscatter<local,256>", k_cl_xscatter<true, kSmallDigits>, dim3(gx), dim3(kXsWG), 0,
                                  s, x2)
+            : p.nb2 <= kMidDigits
+                ? launch_checked("k_cl_xscatter<local,512>", k_cl_xscatter<true, kMidDigits>, dim3(gx), dim3(kXsWG), 0, s,
+                                 x2)
                 : launch_checked("k_cl_xscatter<local>", k_cl_xscatter<true, kMaxDigits>, dim3(gx), dim3(kXsWG), 0, s, x2);
         if (e != hipSuccess) return e;
         if (groups) {  // the group join takes the sub-buckets from here
