@@ -1078,7 +1078,7 @@ __device__ __forceinline__ uint32_t group_hash(uint64_t tmix, uint64_t x) {
 }
 
 __device__ __forceinline__ void load_group(const JoinArgs& a, uint64_t base, Window& w) {
-    load_tid(a, a.c.n, base, w);
+    ld2_u64(a.c.trace_id, base + 2 * threadIdx.x, a.c.n, w.tid);
     load_early(a, a.c.n, base, w);
     load_late<true>(a, a.c.n, base, w);
 }
@@ -1099,6 +1099,7 @@ __global__ __launch_bounds__(kGWG, kGPerCU * kGWG / 256) void k_group_join(JoinA
     const int tid = threadIdx.x, lane = tid & 63;
     const uint64_t n = a.c.n;
     const uint32_t nsub = a.nsub;
+    ZK_STAMP_DECL
     const uint64_t R0 = (uint64_t)blockIdx.x * a.per_wg;
     const uint64_t R1 = (R0 + a.per_wg < n) ? R0 + a.per_wg : n;
     if (tid < ST_N) s_stat[tid] = 0u;
@@ -1188,7 +1189,12 @@ __global__ __launch_bounds__(kGWG, kGPerCU * kGWG / 256) void k_group_join(JoinA
     uint64_t* __restrict__ out = a.links + (uint64_t)blockIdx.x * a.link_stride;
     const uint64_t trash = a.link_stride - 1;
 
-    auto run_group = [&](const Window& cur, uint32_t lo, uint32_t hi) {
+    uint32_t gs = g0;
+    uint32_t bv = fetch(gs);
+    // Join batch [lo, hi) from `cur`; then cut the batch after the one in flight and load it into
+    // `cur` (no longer read) BEFORE the closing barrier: the waves issue their loads as they finish,
+    // not all at once after it (the stamps build showed 18 % of wave cycles in the load issue).
+    auto run_group = [&](Window& cur, uint32_t lo, uint32_t hi, uint32_t* nlo, uint32_t* nhi) {
         const uint32_t len = hi - lo;
         const int off = (int)(lo & 1u);
         nrec += len;
@@ -1222,7 +1228,7 @@ __global__ __launch_bounds__(kGWG, kGPerCU * kGWG / 256) void k_group_join(JoinA
             *reinterpret_cast<ulonglong2*>(&s_pid[j0]) = make_ulonglong2(v_pid[0], v_pid[1]);
             *reinterpret_cast<uint2*>(&s_svck[j0]) = make_uint2(r_svck[0], r_svck[1]);
         }
-        __syncthreads();  // staged; every slot of the previous group is empty
+        ZK_PHASE_SYNC(1);  // staged; every slot of the previous group is empty
         // ---- groupBy((id, traceId)): the first fragment to claim a slot leads ------------------
         int r_leader[2];
         uint32_t r_slot[2];
@@ -1271,6 +1277,7 @@ __global__ __launch_bounds__(kGWG, kGPerCU * kGWG / 256) void k_group_join(JoinA
                 }
             }
         }
+        ZK_STAMP(2);
         // ---- reduce(mergeSpan) into the leader (no barrier: see K1 phase 5) ----------------------
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
@@ -1292,7 +1299,7 @@ __global__ __launch_bounds__(kGWG, kGPerCU * kGWG / 256) void k_group_join(JoinA
                 if (promote) atomicOr(wp, promote << kSlotB);
             }
         }
-        __syncthreads();  // merged
+        ZK_PHASE_SYNC(3);  // merged
         // ---- filter(isValid), join on (parentId, traceId), links ---------------------------------
         uint64_t r_link[2];
         uint32_t nl = 0;
@@ -1356,6 +1363,7 @@ __global__ __launch_bounds__(kGWG, kGPerCU * kGWG / 256) void k_group_join(JoinA
             if (a.nb) atomicAdd(&s_hist[cell >> a.cb_shift], 1u);
             ++nl;
         }
+        ZK_STAMP(4);
         // ---- append: one LDS atomic per wave claims its slice of the workgroup's list ------------
         const uint64_t l1 = __ballot(nl >= 1u), l2 = __ballot(nl >= 2u);
         uint32_t lbase = 0;
@@ -1378,33 +1386,32 @@ __global__ __launch_bounds__(kGWG, kGPerCU * kGWG / 256) void k_group_join(JoinA
             fold_stats(st, s_stat);
             fold_in = kFoldWindows;
         }
-        __syncthreads();  // every probe of this group is done before the next one is staged
+        gs = next_batch(gs, bv, nlo, nhi);
+        if (*nhi > *nlo) load_group(a, *nlo & ~1u, cur);
+        bv = fetch(gs);
+        ZK_PHASE_SYNC(5);  // every probe of this group is done before the next one is staged
     };
 
     // two register windows: one batch's columns load while the other batch is joined; the bounds
     // of the batch after both load while the first is joined
     Window wa, wb;
     uint32_t la = 0, ha = 0, lb = 0, hb = 0;
-    uint32_t gs = g0;
-    uint32_t bv = fetch(gs);
     gs = next_batch(gs, bv, &la, &ha);
     if (ha > la) load_group(a, la & ~1u, wa);
     bv = fetch(gs);
     gs = next_batch(gs, bv, &lb, &hb);
     if (hb > lb) load_group(a, lb & ~1u, wb);
     bv = fetch(gs);
+    ZK_STAMP(6);
     for (;;) {
         if (ha <= la) break;
-        run_group(wa, la, ha);
-        gs = next_batch(gs, bv, &la, &ha);
-        if (ha > la) load_group(a, la & ~1u, wa);
-        bv = fetch(gs);
+        run_group(wa, la, ha, &la, &ha);
+        ZK_STAMP(6);
         if (hb <= lb) break;
-        run_group(wb, lb, hb);
-        gs = next_batch(gs, bv, &lb, &hb);
-        if (hb > lb) load_group(a, lb & ~1u, wb);
-        bv = fetch(gs);
+        run_group(wb, lb, hb, &lb, &hb);
+        ZK_STAMP(6);
     }
+    ZK_STAMP_FLUSH();
     __syncthreads();
     if (tid == 0) {
         a.link_count[blockIdx.x] = s_cursor;
