@@ -95,13 +95,17 @@ typedef struct zk_span_cols {
 /* batch flags for zk_deps_accumulate
  *
  * Fragments may come in ANY order, as the reference's shuffles allow (ZipkinAggregateJob.scala:21,
- * 28-33): without ZK_BATCH_TRACE_CLUSTERED the batch first goes through a device clustering pass:
- * a two-level MSD radix partition of the records on a hash of the traceId (a histogram pass, two
- * scatter passes that move all seven columns), then one pass that groups each sub-bucket's records
- * into whole traces -- about 328 B of HBM traffic per 48-B record. Measured on MI355X: a shuffled
- * 1e8-record batch takes 8.2-8.3 ms per accumulate against 1.40 ms clustered (5.9x; the pass also
- * needs two extra 48-B/record column buffers). ZK_BATCH_TRACE_CLUSTERED is the caller's promise
- * that the pass is unnecessary (Cassandra row-per-trace reads deliver clustered batches).
+ * 28-33): without ZK_BATCH_TRACE_CLUSTERED the batch first goes through a device partition: a
+ * two-level MSD radix partition of the records on a hash of the traceId (a histogram pass, two
+ * scatter passes that move all seven columns), after which every trace lies inside one sub-bucket.
+ * Batches of more than 2^18 records without ZK_BATCH_VERIFY_TRACES are then joined per run of whole
+ * sub-buckets in LDS with the traceId in the keys (the group join; sub-buckets longer than its LDS
+ * tile are clustered and go through the streaming join); otherwise one more pass groups each
+ * sub-bucket's records into whole traces for the streaming join. Measured on MI355X: a shuffled
+ * 1e8-record batch takes 7.1-7.3 ms per accumulate with the group join (8.6 ms with the trace pass)
+ * against 1.40-1.50 ms clustered, about 208 B of HBM traffic per 48-B record; the partition needs two
+ * extra 48-B/record column buffers. ZK_BATCH_TRACE_CLUSTERED is the caller's promise that it is
+ * unnecessary (Cassandra row-per-trace reads deliver clustered batches).
  * ZK_BATCH_VERIFY_TRACES checks that promise, and the trace-complete-batch contract, exactly: every
  * trace run's traceId is inserted into a device set of all traceIds accumulated since the last
  * reset, and a traceId seen again (a trace split into non-adjacent runs, or spread over two
