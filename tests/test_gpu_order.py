@@ -307,3 +307,41 @@ def test_group_join_equals_the_trace_path(gpu, monkeypatch):
     for k in st:
         if k != "spilled_traces":
             assert st[k] == sr[k], k
+
+
+def test_group_join_rich_spans_with_anomalies(gpu, monkeypatch):
+    """Rich spans with the injected anomalies of tests/richgen.py (missing and invalid parents,
+    duplicated core annotations, disagreeing fragments, client-only and nameless services), in 40
+    copies with distinct traceIds (> 2^18 records), shuffled: the group join equals the oracle and
+    the P3 + K1 path, every counter included."""
+    from tests.richgen import gen_traces
+    from tests.test_gpu_parity import COLS
+    from oracle.spans import span_to_record
+
+    spans = gen_traces(34, 600, max_depth=5, anomalies=0.4)
+    ids: dict = {}
+    recs = [span_to_record(s, ids) for s in spans]
+    one = SpanColumns.empty(len(recs))
+    for k in COLS:
+        getattr(one, k)[:] = [r[k] for r in recs]
+    copies = []
+    for c in range(40):
+        x = one.take(np.arange(len(one)))
+        x.trace_id[:] = x.trace_id ^ np.uint64((c * 0x9E3779B97F4A7C15) & (2**64 - 1))
+        copies.append(x)
+    cols = SpanColumns.concat(copies)
+    assert len(cols) > 2 ** 18
+    S = len(ids)
+    ref = oracle.aggregate(cols, S)
+    shuffled = cols.take(np.random.default_rng(34).permutation(len(cols)))
+    with DepsContext(S, strict=False) as ctx:
+        ctx.accumulate(shuffled, verify=False)
+        got, st = ctx.finalize(), ctx.stats()
+    assert_parity(got, st, ref)
+    monkeypatch.setenv("ZK_GROUP_JOIN", "0")
+    with DepsContext(S, strict=False) as ctx:
+        ctx.accumulate(shuffled, verify=False)
+        got2, st2 = ctx.finalize(), ctx.stats()
+    for k in ("m0", "m1", "m2", "m3", "m4", "present"):
+        assert np.array_equal(getattr(got, k), getattr(got2, k)), k
+    assert {k: v for k, v in st.items() if k != "spilled_traces"} == {k: v for k, v in st2.items() if k != "spilled_traces"}
