@@ -54,9 +54,11 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=None,
                     help="batches in flight behind the one being joined: 1 = two table/stream "
                          "sets (batch k's join overlaps batch k-1's tail), 2 = three, 0 = one set, serial steps "
-                         "(c2 takes any depth, c4/c5 use two sets when > 0). Default: 1 for c2/c5, 0 for c4, whose "
-                         "partition scatter and candidate pass each fill the LDS of a CU, so two overlapped sets only "
-                         "contend (12.06 ms serial vs 14.13 ms pipelined, profiles/r02/ab_c4_pipeline.txt)")
+                         "(c2/c3 take any depth, c4/c5 use two sets when > 0). Default: 3 for c2/c3 (four sets: "
+                         "1.447-1.448 ms per C2 step against 1.500-1.518 with two, same box, "
+                         "profiles/r04/ab_pipeline_depth.txt), 1 for c5, 0 for c4, whose partition scatter and "
+                         "candidate pass each fill the LDS of a CU, so two overlapped sets only contend "
+                         "(12.06 ms serial vs 14.13 ms pipelined, profiles/r02/ab_c4_pipeline.txt)")
     ap.add_argument("--overlap", default="full", choices=("tail", "full"),
                     help="c2 pipelined steps: full (default) = no ordering between the table sets: batch k's "
                          "join shares the GPU with batch k-1's K2/K3 (faster steps; K1's launch events then also "
@@ -85,7 +87,7 @@ def parse():
     if a.records is None:
         a.records = 1_000_000_000 if a.workload == "c3" else 100_000_000
     if a.pipeline is None:
-        a.pipeline = 0 if a.workload == "c4" else 1
+        a.pipeline = 3 if a.workload in ("c2", "c3") else 0 if a.workload == "c4" else 1
     return a
 
 
@@ -194,10 +196,10 @@ def main():
 
     pipeline = a.pipeline != 0
     if pipeline:
-        # Two table/stream sets, software-pipelined: batch k's join runs on its stream while batch
-        # k-1's tail (K2/K3, at N > 1 the all-reduce over RCCL, finalize and status check) completes
-        # on the other; every batch is still joined, reduced and finalized inside the timed region
-        # (drain() finalizes the last one).
+        # a.pipeline + 1 table/stream sets, software-pipelined: batch k's join runs on its stream while
+        # earlier batches' tails (K2/K3, at N > 1 the all-reduce over RCCL, finalize and status check)
+        # complete on the others; every batch is still joined, reduced and finalized inside the timed
+        # region (drain() finalizes the last ones).
         sets = [(ctx, None, stream, out)]
         for _ in range(a.pipeline):  # a.pipeline batches in flight behind the one being joined
             s2 = torch.cuda.Stream(device=dev)
