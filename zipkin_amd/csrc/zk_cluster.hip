@@ -244,14 +244,17 @@ __device__ __forceinline__ void xchunk(const XArgs& a, uint32_t p, uint32_t j, u
         *hi = *lo + kXsChunk < e ? *lo + kXsChunk : e;
     } else {
         const uint32_t* bt = a.bucket_tiles + (uint64_t)p * (a.nbp + 1);
-        uint32_t l = 0, r = a.nbp;  // bt[l] <= j < bt[r]
-        while (r - l > 1) {
-            const uint32_t m = (l + r) >> 1;
-            if (bt[m] <= j)
-                l = m;
-            else
-                r = m;
+        // l = the last m with bt[m] <= j: every wave reads 64 entries at once and counts by ballot
+        // (one load round trip per 64 buckets of the portion instead of a dependent binary search)
+        const uint32_t lane = threadIdx.x & 63u;
+        uint32_t l = 0;
+        for (uint32_t m0 = 0; m0 < a.nbp; m0 += 64u) {  // uniform
+            const uint32_t m = m0 + lane;
+            const uint64_t le = __ballot(m < a.nbp && bt[m < a.nbp ? m : 0] <= j);
+            l += (uint32_t)__popcll(le);
+            if (le != ~0ull) break;  // bt rises: the first entry > j ends the count
         }
+        l = l ? l - 1u : 0u;  // (bt[0] = 0 <= j always)
         const uint32_t bk = p + a.parts * l;
         *b = bk;
         *lo = (uint64_t)a.bucket[bk] + (uint64_t)(j - bt[l]) * kXsChunk;
