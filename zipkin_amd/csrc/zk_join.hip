@@ -1039,12 +1039,13 @@ __global__ __launch_bounds__(kSpillWG) void k_span_join_spill(JoinArgs a) {
 //
 // The clustering pass's partition (zk_cluster.hip P0-P2) leaves every trace inside one sub-bucket,
 // its records in any order. Instead of clustering each sub-bucket (P3) and streaming K1 over the
-// result, one workgroup per CU takes whole sub-buckets of <= kGCap records into LDS and keys the
-// same merge and join by (traceId, spanId) and (traceId, parentId): the groupBy((id, traceId)) and
-// the (parentId, traceId) join of ZipkinAggregateJob.scala:21-33 with the traceId in the key, as
-// the reference has it, instead of a trace segment. Every record is read from HBM once (48 B);
-// P3's 104 B per record and K1's second read of the columns are gone. The next sub-bucket's columns
-// load into a second register window while this one is joined. Sub-buckets longer than kGCap
+// result, one workgroup per CU takes runs of whole consecutive sub-buckets (batches of <= kGCap
+// records) into LDS and keys the same merge and join by (traceId, spanId) and (traceId, parentId):
+// the groupBy((id, traceId)) and the (parentId, traceId) join of ZipkinAggregateJob.scala:21-33 with
+// the traceId in the key, as the reference has it, instead of a trace segment. Every record is read
+// from HBM once (48 B); P3's 104 B per record and K1's second read of the columns are gone. Two
+// register windows alternate: the batch after next loads into the current batch's registers in
+// three groups, each as soon as the registers it overwrites are dead. Sub-buckets longer than kGCap
 // (a trace of > 2k records, or an unlucky hash range) are listed and left to the fallback: P3 over
 // the listed sub-buckets only, then K1 (append mode) over its output, into the same link lists.
 //
@@ -1054,9 +1055,6 @@ __global__ __launch_bounds__(kSpillWG) void k_span_join_spill(JoinArgs a) {
 // =============================================================================================
 #ifndef ZK_GJ_WG
 #define ZK_GJ_WG 1024  // group-join workgroup: 2 x WG positions of LDS per batch
-#endif
-#ifndef ZK_GJ_SPREAD
-#define ZK_GJ_SPREAD 1  // the next batch's column loads spread over the phases (A/B)
 #endif
 #ifndef ZK_GJ_HF
 #define ZK_GJ_HF 8  // hash slots per LDS position (4: +0.13 ms per 1e8 records, longer probe chains)
@@ -1199,15 +1197,15 @@ __global__ __launch_bounds__(kGWG, kGPerCU * kGWG / 256) void k_group_join(JoinA
     // not all at once after it (the stamps build showed 18 % of wave cycles in the load issue).
     auto run_group = [&](Window& cur, uint32_t lo, uint32_t hi, uint32_t* nlo, uint32_t* nhi) {
         const uint32_t len = hi - lo;
-#if ZK_GJ_SPREAD
         // The batch after the one in flight, and its column loads into `cur` spread over this batch's
         // phases as `cur`'s registers fall free (service after staging; spanId and first/last after the
         // merge; traceId, parentId and flags after the join), so the waves' load issue interleaves with
-        // compute instead of coming as one 98-KB burst. Unconditional (base 0 when there is none).
+        // compute instead of coming as one 98-KB burst (one burst before the closing barrier: 1.84 vs
+        // 1.57 ms per 1e8 records, profiles/r04/ab_group_join_spread.txt). Unconditional (base 0 when
+        // there is none).
         gs = next_batch(gs, bv, nlo, nhi);
         const uint64_t nbase = *nhi > *nlo ? (uint64_t)(*nlo & ~1u) : 0ull;
         bv = fetch(gs);
-#endif
         const int off = (int)(lo & 1u);
         nrec += len;
         // ---- stage: transformed values at positions 2t, 2t+1 (position p = record lo - off + p) ---
@@ -1241,9 +1239,7 @@ __global__ __launch_bounds__(kGWG, kGPerCU * kGWG / 256) void k_group_join(JoinA
             *reinterpret_cast<uint2*>(&s_svck[j0]) = make_uint2(r_svck[0], r_svck[1]);
         }
         ZK_PHASE_SYNC(1);  // staged; every slot of the previous group is empty
-#if ZK_GJ_SPREAD
         ld2_u32(a.c.service_id, nbase + 2 * threadIdx.x, a.c.n, cur.svc);
-#endif
         // ---- groupBy((id, traceId)): the first fragment to claim a slot leads ------------------
         int r_leader[2];
         uint32_t r_slot[2];
@@ -1315,11 +1311,9 @@ __global__ __launch_bounds__(kGWG, kGPerCU * kGWG / 256) void k_group_join(JoinA
             }
         }
         ZK_PHASE_SYNC(3);  // merged
-#if ZK_GJ_SPREAD
         ld2_u64(a.c.span_id, nbase + 2 * threadIdx.x, a.c.n, cur.sid);
         ld2_u64((const uint64_t*)a.c.first_ts, nbase + 2 * threadIdx.x, a.c.n, cur.first);
         ld2_u64((const uint64_t*)a.c.last_ts, nbase + 2 * threadIdx.x, a.c.n, cur.last);
-#endif
         // ---- filter(isValid), join on (parentId, traceId), links ---------------------------------
         uint64_t r_link[2];
         uint32_t nl = 0;
@@ -1384,11 +1378,9 @@ __global__ __launch_bounds__(kGWG, kGPerCU * kGWG / 256) void k_group_join(JoinA
             ++nl;
         }
         ZK_STAMP(4);
-#if ZK_GJ_SPREAD
         ld2_u64(a.c.trace_id, nbase + 2 * threadIdx.x, a.c.n, cur.tid);
         ld2_u64(a.c.parent_id, nbase + 2 * threadIdx.x, a.c.n, cur.pid);
         ld2_u32(a.c.flags, nbase + 2 * threadIdx.x, a.c.n, cur.flags);
-#endif
         // ---- append: one LDS atomic per wave claims its slice of the workgroup's list ------------
         const uint64_t l1 = __ballot(nl >= 1u), l2 = __ballot(nl >= 2u);
         uint32_t lbase = 0;
@@ -1411,11 +1403,6 @@ __global__ __launch_bounds__(kGWG, kGPerCU * kGWG / 256) void k_group_join(JoinA
             fold_stats(st, s_stat);
             fold_in = kFoldWindows;
         }
-#if !ZK_GJ_SPREAD
-        gs = next_batch(gs, bv, nlo, nhi);
-        if (*nhi > *nlo) load_group(a, *nlo & ~1u, cur);
-        bv = fetch(gs);
-#endif
         ZK_PHASE_SYNC(5);  // every probe of this group is done before the next one is staged
     };
 
