@@ -345,3 +345,20 @@ def test_group_join_rich_spans_with_anomalies(gpu, monkeypatch):
     for k in ("m0", "m1", "m2", "m3", "m4", "present"):
         assert np.array_equal(getattr(got, k), getattr(got2, k)), k
     assert {k: v for k, v in st.items() if k != "spilled_traces"} == {k: v for k, v in st2.items() if k != "spilled_traces"}
+
+
+def test_group_join_over_several_trace_complete_batches(gpu):
+    """Two shuffled trace-complete batches of > 2^18 records each through the group join (its
+    long-sub-bucket list, fallback cursor and per-CU link lists restart per batch): the oracle's
+    result for the union."""
+    S = 61
+    cols = tracegen_host(81, 50_000, max_depth=6, num_services=S)
+    tids = np.unique(cols.trace_id)
+    which = np.random.default_rng(81).integers(0, 2, len(tids))[np.searchsorted(tids, cols.trace_id)]
+    parts = []
+    for g in range(2):
+        idx = np.flatnonzero(which == g)
+        parts.append(cols.take(idx[np.random.default_rng(g).permutation(len(idx))]))
+    assert all(len(p) > 2 ** 18 for p in parts)
+    got, st = run(parts, S, verify=False)
+    assert_parity(got, st, oracle.aggregate(cols, S))
