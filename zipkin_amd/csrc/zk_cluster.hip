@@ -74,8 +74,11 @@ __device__ __forceinline__ bool set_insert(unsigned long long* set, uint64_t mas
 }
 
 // ---- P0: per-workgroup digit histogram -----------------------------------------------------------
-constexpr int kHistWG = 256;
-constexpr int kHistU = 8;
+// One workgroup per CU (the P0 ranges are what P1's portions are cut from): 16 waves and two
+// alternating load buffers, so one block's traceIds are in flight while the other is counted
+// (256 threads with one buffer: 0.247 ms per 1e8 records, latency-bound at 4 waves per CU).
+constexpr int kHistWG = 1024;
+constexpr int kHistU = 4;
 
 __global__ __launch_bounds__(kHistWG) void k_cl_hist(const uint64_t* __restrict__ tid, uint64_t n, uint64_t per,
                                                       uint32_t shift, uint32_t nd, uint32_t grid,
@@ -86,18 +89,28 @@ __global__ __launch_bounds__(kHistWG) void k_cl_hist(const uint64_t* __restrict_
     const uint64_t lo = (uint64_t)blockIdx.x * per;
     const uint64_t hi = lo + per < n ? lo + per : n;
     const uint32_t mask = nd - 1;
-    for (uint64_t b = lo; b < hi; b += (uint64_t)kHistWG * kHistU) {
-        uint64_t v[kHistU];
+    constexpr uint64_t BS = (uint64_t)kHistWG * kHistU;
+    auto load = [&](uint64_t (&v)[kHistU], uint64_t b) {
 #pragma unroll
         for (int e = 0; e < kHistU; ++e) {
             const uint64_t i = b + (uint64_t)e * kHistWG + threadIdx.x;
             v[e] = tid[i < hi ? i : lo];
         }
+    };
+    auto count = [&](const uint64_t (&v)[kHistU], uint64_t b) {
 #pragma unroll
         for (int e = 0; e < kHistU; ++e) {
             const uint64_t i = b + (uint64_t)e * kHistWG + threadIdx.x;
             if (i < hi) atomicAdd(&h[digit_of(part_hash(v[e]), shift, mask)], 1u);
         }
+    };
+    uint64_t va[kHistU], vb[kHistU];
+    if (lo < hi) load(va, lo);  // a trailing workgroup may own no records
+    for (uint64_t b = lo; b < hi; b += 2 * BS) {
+        load(vb, b + BS);
+        count(va, b);
+        load(va, b + 2 * BS);
+        count(vb, b + BS);  // past hi: nothing counted
     }
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < nd; d += kHistWG) hist[(uint64_t)d * grid + blockIdx.x] = h[d];
@@ -287,30 +300,47 @@ __global__ void k_cl_xprep1(const uint32_t* __restrict__ offs, uint32_t nd, uint
     }
 }
 
-// P2 work lists: the chunks of each portion's buckets (one thread per portion)
-__global__ void k_cl_xprep2(const uint32_t* __restrict__ bucket, uint32_t nb1, uint32_t parts, uint32_t nbp,
-                            uint32_t* __restrict__ bucket_tiles, uint32_t* __restrict__ part_tiles,
-                            unsigned int* __restrict__ next) {
+// P2 work lists: the chunks of each portion's buckets. One workgroup: the chunk counts of every
+// bucket in parallel into LDS, then one thread per portion scans its buckets' counts (a single
+// thread reading the bounds one bucket after another took 24 us).
+constexpr int kPrep2WG = 1024;
+__global__ __launch_bounds__(kPrep2WG) void k_cl_xprep2(const uint32_t* __restrict__ bucket, uint32_t nb1,
+                                                        uint32_t parts, uint32_t nbp,
+                                                        uint32_t* __restrict__ bucket_tiles,
+                                                        uint32_t* __restrict__ part_tiles,
+                                                        unsigned int* __restrict__ next) {
+    __shared__ uint32_t s_c[kMaxDigits];
+    __shared__ uint32_t s_tot[kParts];
+    for (uint32_t bk = threadIdx.x; bk < nb1; bk += kPrep2WG)
+        s_c[bk] = (bucket[bk + 1] - bucket[bk] + kXsChunk - 1) / kXsChunk;
+    __syncthreads();
+    const uint32_t p = threadIdx.x;
+    if (p < parts) {
+        uint32_t c = 0;
+        uint32_t* bt = bucket_tiles + (uint64_t)p * (nbp + 1);
+        for (uint32_t m = 0; m < nbp; ++m) {
+            bt[m] = c;
+            const uint32_t bk = p + parts * m;
+            if (bk < nb1) c += s_c[bk];
+        }
+        bt[nbp] = c;
+        s_tot[p] = c;
+        next[p] = 0u;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t t = 0;
-        for (uint32_t p = 0; p < parts; ++p) {
-            part_tiles[p] = t;
-            uint32_t c = 0;
-            uint32_t* bt = bucket_tiles + (uint64_t)p * (nbp + 1);
-            for (uint32_t m = 0; m < nbp; ++m) {
-                bt[m] = c;
-                const uint32_t bk = p + parts * m;
-                if (bk < nb1) c += (bucket[bk + 1] - bucket[bk] + kXsChunk - 1) / kXsChunk;
-            }
-            bt[nbp] = c;
-            t += c;
-            next[p] = 0u;
+        for (uint32_t q = 0; q < parts; ++q) {
+            part_tiles[q] = t;
+            t += s_tot[q];
         }
         part_tiles[parts] = t;
     }
 }
 
 // P2h: (bucket, second digit) counts; one workgroup per chunk of any portion
+// (4 chunks per workgroup with the next chunk's loads in flight and one flush per bucket: 0.207 vs
+// 0.197 ms, not kept: the global atomics and the load latency are not what bounds it)
 __global__ __launch_bounds__(256) void k_cl_xhist2(XArgs a) {
     __shared__ uint32_t h[kMaxDigits];
     const uint32_t k = blockIdx.x;
@@ -917,7 +947,7 @@ hipError_t launch_cluster(const ClusterPlan& p, const SpanColsDev& in, const Spa
             x2.hist = hist2;
             const uint32_t maxchunks = (uint32_t)((n + kXsChunk - 1) / kXsChunk + p.nb1);
             size_t tb2 = scan_bytes(xl.m2);
-            e = launch_checked("k_cl_xprep2", k_cl_xprep2, dim3(1), dim3(64), 0, s, (const uint32_t*)bucket, p.nb1,
+            e = launch_checked("k_cl_xprep2", k_cl_xprep2, dim3(1), dim3(kPrep2WG), 0, s, (const uint32_t*)bucket, p.nb1,
                                parts2, nbp, bucket_tiles, part_tiles, xnext);
             if (e == hipSuccess) e = hipMemsetAsync(hist2, 0, xl.m2 * 4, s);
             if (e == hipSuccess) e = launch_checked("k_cl_xhist2", k_cl_xhist2, dim3(maxchunks), dim3(256), 0, s, x2);
