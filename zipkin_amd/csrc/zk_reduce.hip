@@ -99,12 +99,15 @@ constexpr int kScatterLine = 8;  // links per 64-byte line (128-byte lines: WRIT
                                  // their LDS carry halves the resident workgroups: 1.4x slower)
 // One workgroup walks LPW consecutive K1 lists as one stream: within every bucket, list w+1's range
 // follows list w's (col_off is an exclusive scan over lists), so the per-bucket cursors and line
-// carries run on across the list boundaries and K2's grid stays ~1024 workgroups whatever K1's grid.
-constexpr int kScatterMaxLPW = 8;
+// carries run on across the list boundaries and K2's grid stays ~256 workgroups (one per CU)
+// whatever K1's grid: K2 0.221 -> 0.201 ms on C2 against ~1024 workgroups of 4 lists
+// (profiles/r04/ab_k2_grid.txt; 512: 0.211 ms).
+constexpr int kScatterMaxLPW = 16;
+constexpr uint32_t kScatterGrid = 256;
 template <int U, int WG>
 __global__ __launch_bounds__(WG) void k_link_scatter(ReduceArgs r, uint32_t lpw) {
     constexpr int C = WG * U;
-    __shared__ uint32_t s_pre[kScatterMaxLPW + 1];  // exclusive prefix of the group's list counts
+    __shared__ uint32_t s_pre[kScatterMaxLPW + 4];  // exclusive prefix of the group's list counts (+ ~0 pads)
     __shared__ uint32_t s_cur[kMaxBuckets];   // output position of each bucket's first pending link
     __shared__ uint32_t s_hist[kMaxBuckets];  // links of the chunk per bucket
     __shared__ uint32_t s_off[kMaxBuckets];   // exclusive offsets in the sorted chunk
@@ -133,6 +136,7 @@ __global__ __launch_bounds__(WG) void k_link_scatter(ReduceArgs r, uint32_t lpw)
             acc += r.counts[w + q];
         }
         s_pre[nl] = acc;
+        for (uint32_t q = nl + 1; q < kScatterMaxLPW + 4; ++q) s_pre[q] = 0xFFFFFFFFu;
     }
     __syncthreads();
     const uint32_t c = s_pre[nl];  // links of the group
@@ -147,23 +151,46 @@ __global__ __launch_bounds__(WG) void k_link_scatter(ReduceArgs r, uint32_t lpw)
         q = q < nl - 1 ? q : nl - 1;  // an empty group (c == 0) reads element 0 of its last list
         return r.links + (uint64_t)(w + q) * r.stride + (i - pre[q]);
     };
-    uint64_t nxt[U];
+    // the links of the chunk starting at element b0 into dst. Lists hold ~C links or more, so a
+    // chunk nearly always meets at most two list boundaries: its elements are then placed with two
+    // compares against the (uniform) bounds after its first list, found by a walk that only moves
+    // forward (q0); other chunks compare against every bound.
+    uint32_t q0 = 0;
+    auto load_chunk = [&](uint64_t (&dst)[U], uint32_t b0) {
+        if (b0 >= c) {  // uniform: past the group's end
 #pragma unroll
-    for (int k = 0; k < U; ++k) {
-        const uint32_t i = tid + WG * k;
-        nxt[k] = *at(i < c ? i : 0);
-    }
+            for (int k = 0; k < U; ++k) dst[k] = r.links[(uint64_t)w * r.stride];
+            return;
+        }
+        while (q0 + 1 < nl && b0 >= s_pre[q0 + 1]) ++q0;  // uniform
+        const uint32_t pa = s_pre[q0], p1 = s_pre[q0 + 1], p2 = s_pre[q0 + 2], p3 = s_pre[q0 + 3];
+        if ((uint64_t)b0 + C <= p3) {  // uniform
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const uint32_t i = b0 + tid + WG * k;
+                const uint32_t ii = i < c ? i : b0;
+                const uint32_t q = q0 + (ii >= p1 ? 1u : 0u) + (ii >= p2 ? 1u : 0u);
+                const uint32_t lo = ii >= p2 ? p2 : (ii >= p1 ? p1 : pa);
+                dst[k] = r.links[(uint64_t)(w + q) * r.stride + (ii - lo)];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const uint32_t i = b0 + tid + WG * k;
+                dst[k] = *at(i < c ? i : 0);
+            }
+        }
+    };
+    uint64_t nxt[U];
+    load_chunk(nxt, 0u);
     for (uint32_t base = 0; base < c; base += C) {
         const uint32_t cnt = (c - base) < (uint32_t)C ? (c - base) : (uint32_t)C;
         const bool last = base + C >= c;
         uint64_t v[U];
         uint32_t bk[U], rank[U];
 #pragma unroll
-        for (int k = 0; k < U; ++k) {
-            v[k] = nxt[k];
-            const uint32_t i = base + C + tid + WG * k;
-            nxt[k] = *at(i < c ? i : 0);  // next chunk in flight
-        }
+        for (int k = 0; k < U; ++k) v[k] = nxt[k];
+        load_chunk(nxt, base + C);  // next chunk in flight
 #pragma unroll
         for (int k = 0; k < U; ++k) {
             bk[k] = (uint32_t)((v[k] >> 40) >> r.cb_shift);
@@ -607,8 +634,8 @@ hipError_t launch_partitioned_reduce(const ReduceArgs& r, hipStream_t s) {
     if (e != hipSuccess) return e;
     e = launch_checked("k_bucket_base", k_bucket_base, dim3(1), dim3(1024), 0, s, r.bucket_base, r.nb);
     if (e != hipSuccess) return e;
-    // ~1024 K2 workgroups: a K1 grid larger than that is walked LPW lists per workgroup
-    uint32_t lpw = (r.lists + 1023) / 1024;
+    // ~kScatterGrid K2 workgroups: a K1 grid larger than that is walked LPW lists per workgroup
+    uint32_t lpw = (r.lists + kScatterGrid - 1) / kScatterGrid;
     if (lpw > (uint32_t)kScatterMaxLPW) lpw = kScatterMaxLPW;
     const uint32_t k2_grid = (r.lists + lpw - 1) / lpw;
     e = launch_checked("k_link_scatter", k_link_scatter<kK2U, kK2WG>, dim3(k2_grid), dim3(kK2WG),
