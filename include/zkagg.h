@@ -102,8 +102,8 @@ typedef struct zk_span_cols {
  * sub-buckets in LDS with the traceId in the keys (the group join; sub-buckets longer than its LDS
  * tile are clustered and go through the streaming join); otherwise one more pass groups each
  * sub-bucket's records into whole traces for the streaming join. Measured on MI355X: a shuffled
- * 1e8-record batch takes 7.1-7.3 ms per accumulate with the group join (8.6 ms with the trace pass)
- * against 1.40-1.50 ms clustered, about 208 B of HBM traffic per 48-B record; the partition needs two
+ * 1e8-record batch takes 6.6-7.0 ms per accumulate with the group join (8.6 ms with the trace pass)
+ * against 1.3-1.5 ms clustered, about 208 B of HBM traffic per 48-B record; the partition needs two
  * extra 48-B/record column buffers. ZK_BATCH_TRACE_CLUSTERED is the caller's promise that it is
  * unnecessary (Cassandra row-per-trace reads deliver clustered batches).
  * ZK_BATCH_VERIFY_TRACES checks that promise, and the trace-complete-batch contract, exactly: every
