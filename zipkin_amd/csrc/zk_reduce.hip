@@ -103,7 +103,8 @@ constexpr int kScatterLine = 8;  // links per 64-byte line (128-byte lines: WRIT
 // whatever K1's grid: K2 0.221 -> 0.201 ms on C2 against ~1024 workgroups of 4 lists
 // (profiles/r04/ab_k2_grid.txt; 512: 0.211 ms).
 constexpr int kScatterMaxLPW = 16;
-constexpr uint32_t kScatterGrid = 256;
+constexpr uint32_t kScatterGrid = 256;  // (512 workgroups: 0.211 ms; 4096-link chunks at two workgroups
+                                        // per CU: 0.229 ms, at one: 0.250 ms -- ab_k2_grid.txt)
 template <int U, int WG>
 __global__ __launch_bounds__(WG) void k_link_scatter(ReduceArgs r, uint32_t lpw) {
     constexpr int C = WG * U;
