@@ -142,7 +142,11 @@ typedef struct zk_config {
                                     zk_deps_note_merged overwrites this table from that buffer (an
                                     all-reduce of the table itself would be lost) */
     uint64_t table_bytes;
-    uint32_t reserved[8];
+    uint32_t trace_pass;         /* 1: unclustered batches always take the trace pass + streaming join
+                                    (P3 + K1) instead of the group join (the A/B of DESIGN.md §7b);
+                                    0: the library picks (group join for > 2^18 records without
+                                    ZK_BATCH_VERIFY_TRACES, when max_trace_records >= its LDS tile) */
+    uint32_t reserved[7];
 } zk_config;
 
 typedef struct zk_ctx zk_ctx;

@@ -143,6 +143,10 @@ zk_status   zk_rt_distinct_traces(zk_rt* rt, double* estimate);
  * N. With N = 0 all outputs are 0. */
 zk_status   zk_rt_quantiles(zk_rt* rt, uint32_t service, const double* q, uint32_t nq, int64_t* lo, int64_t* hi,
                             uint64_t* count);
+/* The same for every service at once (the query path of a dashboard over all services): lo/hi are
+ * host int64[S][nq], count host u64[S] (may be NULL). One device pass over the histograms and one
+ * copy of S x (4 + nq) words, instead of a copy and a synchronisation per service. */
+zk_status   zk_rt_quantiles_all(zk_rt* rt, const double* q, uint32_t nq, int64_t* lo, int64_t* hi, uint64_t* count);
 /* Duration t-digest of one service (BASELINE configs[4]: "duration t-digest p50/p99"): a merging
  * t-digest with the k1 scale function at the given compression (delta, e.g. 200), built from the
  * service's exact histogram -- bins in ascending order, each its midpoint weighted by its count,

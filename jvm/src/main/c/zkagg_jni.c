@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include "zkagg.h"
+#include "zkcomm.h"
 #include "zkingest.h"
 #include "zkstore.h"
 
@@ -21,6 +22,7 @@
 #define CTX(h) ((zk_ctx*)(intptr_t)(h))
 #define ING(h) ((zk_ingest*)(intptr_t)(h))
 #define STORE(h) ((zk_store*)(intptr_t)(h))
+#define COMM(h) ((zk_comm*)(intptr_t)(h))
 #define BUF(b) ((*env)->GetDirectBufferAddress(env, (b)))
 
 /* ---- dependency job ---------------------------------------------------------------------------- */
@@ -78,6 +80,49 @@ JNIEXPORT jint JNICALL FN(stats)(JNIEnv* env, jobject self, jlong h, jlongArray 
         (*env)->SetLongArrayRegion(env, out, 0, n < have ? n : have, (const jlong*)&s);
     }
     return st;
+}
+
+/* the exchange form for a host that runs its own collective: out[0] = device pointer, out[1] = bytes */
+JNIEXPORT jint JNICALL FN(depsPartial)(JNIEnv* env, jobject self, jlong h, jlongArray out) {
+    void* p = NULL;
+    uint64_t bytes = 0;
+    const jint st = zk_deps_partial(CTX(h), &p, &bytes);
+    if (st == ZK_OK) {
+        const jlong v[2] = {(jlong)(intptr_t)p, (jlong)bytes};
+        (*env)->SetLongArrayRegion(env, out, 0, 2, v);
+    }
+    return st;
+}
+
+JNIEXPORT jint JNICALL FN(depsNoteMerged)(JNIEnv* env, jobject self, jlong h, jlong totalRecords) {
+    return zk_deps_note_merged(CTX(h), (uint64_t)totalRecords);
+}
+
+JNIEXPORT jint JNICALL FN(traceShard)(JNIEnv* env, jobject self, jlong traceId, jint world) {
+    return (jint)zk_trace_shard((uint64_t)traceId, (uint32_t)world);
+}
+
+/* ---- multi-GPU (zkcomm.h) ------------------------------------------------------------------------- */
+JNIEXPORT jbyteArray JNICALL FN(commUniqueId)(JNIEnv* env, jobject self) {
+    uint8_t id[ZK_COMM_ID_BYTES];
+    if (zk_comm_unique_id(id, sizeof(id)) != ZK_OK) return NULL;
+    jbyteArray out = (*env)->NewByteArray(env, ZK_COMM_ID_BYTES);
+    if (out) (*env)->SetByteArrayRegion(env, out, 0, ZK_COMM_ID_BYTES, (const jbyte*)id);
+    return out;
+}
+
+JNIEXPORT jlong JNICALL FN(commCreate)(JNIEnv* env, jobject self, jbyteArray id, jint rank, jint world, jint dev) {
+    if ((*env)->GetArrayLength(env, id) < ZK_COMM_ID_BYTES) return 0;
+    uint8_t raw[ZK_COMM_ID_BYTES];
+    (*env)->GetByteArrayRegion(env, id, 0, ZK_COMM_ID_BYTES, (jbyte*)raw);
+    zk_comm* c = NULL;
+    return zk_comm_create(raw, sizeof(raw), (uint32_t)rank, (uint32_t)world, dev, &c) == ZK_OK ? (jlong)(intptr_t)c : 0;
+}
+
+JNIEXPORT jint JNICALL FN(commDestroy)(JNIEnv* env, jobject self, jlong comm) { return zk_comm_destroy(COMM(comm)); }
+
+JNIEXPORT jint JNICALL FN(depsAllreduce)(JNIEnv* env, jobject self, jlong h, jlong comm, jlong totalRecords) {
+    return zk_deps_allreduce(CTX(h), COMM(comm), (uint64_t)totalRecords);
 }
 
 /* ---- ingest --------------------------------------------------------------------------------------- */

@@ -17,6 +17,7 @@ object ZkNative {
   final val Ok = 0
   final val ErrNoService = 3
   final val ErrNotClustered = 7
+  final val ErrTraceTooLarge = 5
   // zk_deps_accumulate batch flags
   final val BatchDevicePtrs = 1
   final val BatchTraceClustered = 2
@@ -44,6 +45,22 @@ object ZkNative {
                             m3: Array[Double], m4: Array[Double], present: Array[Byte]): Int
   /** zk_ctx_stats: the zk_stats fields in declaration order */
   @native def stats(ctx: Long, out: Array[Long]): Int
+  /** zk_deps_partial: out(0) = device pointer of the exchange buffer, out(1) = its bytes (for a host
+    * that runs its own int64 SUM all-reduce; depsAllreduce below does it with RCCL) */
+  @native def depsPartial(ctx: Long, out: Array[Long]): Int
+  @native def depsNoteMerged(ctx: Long, totalRecords: Long): Int
+  /** zk_trace_shard: the rank that owns a traceId in a job of `world` ranks */
+  @native def traceShard(traceId: Long, world: Int): Int
+
+  // ---- multi-GPU (zkcomm.h): one process per GPU, RCCL over xGMI ---------------------------------
+  /** ZK_COMM_ID_BYTES bytes; rank 0 makes it and ships it to the other ranks; null on error */
+  @native def commUniqueId(): Array[Byte]
+  /** blocks until all `world` ranks joined; 0 on error */
+  @native def commCreate(id: Array[Byte], rank: Int, world: Int, device: Int): Long
+  @native def commDestroy(comm: Long): Int
+  /** zk_deps_partial -> RCCL int64 SUM of the exchange buffer -> zk_deps_note_merged (0 = total from
+    * the merged counters) */
+  @native def depsAllreduce(ctx: Long, comm: Long, totalRecords: Long): Int
 
   // ---- ingest (zkingest.h) -----------------------------------------------------------------------
   @native def ingestCreate(): Long

@@ -74,3 +74,18 @@ def test_jni_sources_bind_only_declared_entry_points():
     natives = set(re.findall(r"@native def (\w+)", scala))
     implemented = set(re.findall(r"JNICALL FN\((\w+)\)", c))
     assert natives == implemented, natives ^ implemented
+
+
+def test_comm_rejects_bad_arguments_without_a_collective():
+    """zkcomm.h: argument checks come before RCCL or a device is touched."""
+    L = _abi.lib()
+    uid = (C.c_uint8 * 128)()
+    h = C.c_void_p()
+    assert L.zk_comm_create(uid, 128, 1, 1, 0, C.byref(h)) == _abi.ZK_ERR_INVALID_ARG  # rank >= world
+    assert L.zk_comm_create(uid, 64, 0, 1, 0, C.byref(h)) == _abi.ZK_ERR_INVALID_ARG   # short id
+    assert L.zk_comm_create(None, 128, 0, 1, 0, C.byref(h)) == _abi.ZK_ERR_INVALID_ARG
+    assert L.zk_comm_unique_id(uid, 16) == _abi.ZK_ERR_INVALID_ARG
+    assert L.zk_comm_destroy(None) == _abi.ZK_ERR_INVALID_ARG
+    assert L.zk_deps_allreduce(None, None, 0) == _abi.ZK_ERR_INVALID_ARG
+    if not gpu_available():
+        assert L.zk_comm_create(uid, 128, 0, 1, 0, C.byref(h)) == _abi.ZK_ERR_NO_DEVICE

@@ -122,3 +122,43 @@ def test_held_trace_longer_than_max_trace_is_too_large(gpu):
             ctx.finalize()
         assert e.value.status == _abi.ZK_ERR_TRACE_TOO_LARGE
         assert ctx.stats()["trace_too_large"] == 1
+
+
+@pytest.mark.parametrize("verify", [False, True])
+def test_held_trace_then_a_batch_in_any_order(gpu, verify):
+    """A batch without ZK_BATCH_TRACE_CLUSTERED after a CONTINUES batch ends the held trace
+    (zkagg.h): the held fragments are aggregated as one trace, and the unclustered batch as a whole
+    -- its fragments of the same traceId form a trace of their own, even when the batch happens to
+    start with them (> 2^18 records, so without verification the group join takes it)."""
+    S = 61
+    cols = tracegen_host(93, 16_000, max_depth=6, num_services=S)
+    tid = cols.trace_id
+    starts = np.flatnonzero(np.r_[True, tid[1:] != tid[:-1]])
+    t0, t1 = starts[200], starts[201]  # trace 200 is cut in the middle
+    assert t1 - t0 >= 4
+    mid = (t0 + t1) // 2
+    held = cols.take(slice(0, mid))
+    rest_of_t = cols.take(slice(mid, t1))
+    tail = cols.take(slice(t1, len(cols)))
+    tail = tail.take(np.random.default_rng(93).permutation(len(tail)))
+    second = SpanColumns.concat([rest_of_t, tail])  # starts with the held trace's other fragments
+    assert len(second) > 2 ** 18
+    # expected: the two parts of trace 200 as two independent traces (its second part renamed)
+    renamed = rest_of_t.take(np.arange(len(rest_of_t)))
+    renamed.trace_id[:] = np.uint64(0xFEEDFACECAFE0001)
+    ref = oracle.aggregate(SpanColumns.concat([held, renamed, tail]), S)
+    for device in (False, True):
+        with DepsContext(S) as ctx:
+            a = DeviceColumns.from_host(held) if device else held
+            b = DeviceColumns.from_host(second) if device else second
+            ctx.accumulate(a, clustered=True, verify=verify, continues=True)
+            ctx.accumulate(b, clustered=False, verify=verify)
+            if verify:
+                # trace 200 now arrived over two accumulate calls: the check reports it
+                with pytest.raises(ZkError) as e:
+                    ctx.finalize()
+                assert e.value.status == _abi.ZK_ERR_NOT_CLUSTERED
+                assert ctx.stats()["not_clustered"] == 1
+                continue
+            got, st = ctx.finalize(), ctx.stats()
+        assert_parity(got, st, ref)

@@ -1,0 +1,109 @@
+"""The job drivers on the path the bench measures (ZipkinAggregateJob.scala:20-45 fed as
+StorageRecordReader.scala:49-54 reads rows): stored fragments in row order, cut into batches at
+arbitrary points, streamed through StoredSpanJob (host decode of batch k+1 overlapping batch k on the
+device, ZK_BATCH_TRACE_CLUSTERED | ZK_BATCH_CONTINUES), and ZipkinAggregateJob over device-resident
+row-order batches. Bar: the stored Dependencies record bit-exact (m0 exact, m1..m4 identical fp64)
+against the oracle over the decoded records; the measured job throughput is printed."""
+import time
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+from tests.bulkfrag import batches, encode, service_name
+from zipkin_amd import DeviceColumns, tracegen_host
+from zipkin_amd.aggregates import Dictionary, GpuAggregates, StoredSpanJob, ZipkinAggregateJob
+
+pytestmark = pytest.mark.gpu
+
+
+def _by_name(deps):
+    return {(l.parent.name, l.child.name): tuple(l.duration_moments) for l in deps.links}
+
+
+def _oracle_by_name(cols, S):
+    ref = oracle.aggregate(cols, S, threads=16).moments()
+    return {(service_name(p), service_name(c)): tuple(m) for (p, c), m in ref.items()}
+
+
+def test_stored_span_job_streams_ten_million_fragments(gpu):
+    S = 500
+    cols = tracegen_host(17, 1_000_000, target_records=10_000_000, max_depth=6, num_services=S)
+    assert len(cols) >= 9_900_000
+    buf, off, exp = encode(cols)
+    rng = np.random.default_rng(17)
+    cuts = np.sort(rng.choice(np.arange(1, len(cols)), 39, replace=False)).tolist()  # 40 batches
+    parts = batches(buf, off, cuts)
+    want = _oracle_by_name(exp, S)
+    store = GpuAggregates("cassandra")
+    job = StoredSpanJob(aggregates=store, top_k=5, clock=lambda: 10**15)
+    job.run(parts[:1])  # warm: buffers, kernels
+    t0 = time.perf_counter()
+    deps = job.run(parts)
+    dt = time.perf_counter() - t0
+    print(f"\nStoredSpanJob: {len(cols)} fragments ({len(buf) / 1e9:.2f} GB) in {len(parts)} batches: "
+          f"{dt:.3f} s, {len(cols) / dt:.3e} fragments/s (host decode overlapped with the device job)")
+    assert job.rejected == 0 and job.stats["records"] == len(cols)
+    assert job.stats["not_clustered"] == 0
+    assert _by_name(deps) == want
+    stored = store.getDependencies(0, 10**15)
+    assert {(l.parent.name, l.child.name) for l in stored.links} == set(want)
+    # the annotation producers saw every fragment's indexer items
+    assert all(v == ["custom.event"] for v in job.top_annotations.values())
+    assert all(v == ["http.uri"] for v in job.top_kv.values())
+
+
+def test_stored_span_job_on_the_device_decoder(gpu):
+    import torch
+
+    S = 97
+    cols = tracegen_host(18, 100_000, target_records=1_000_000, max_depth=6, num_services=S)
+    buf, off, exp = encode(cols)
+    cuts = np.sort(np.random.default_rng(18).choice(np.arange(1, len(cols)), 7, replace=False)).tolist()
+    dev = [(torch.from_numpy(b).cuda(), torch.from_numpy(o.view(np.int64)).cuda(), len(o) - 1)
+           for b, o in batches(buf, off, cuts)]
+    job = StoredSpanJob(clock=lambda: 10**15)
+    deps = job.run_device(dev)
+    assert job.rejected == 0 and job.stats["records"] == len(cols)
+    assert _by_name(deps) == _oracle_by_name(exp, S)
+
+
+def test_aggregate_job_on_device_row_batches(gpu):
+    """ZipkinAggregateJob over one 1e8-record TraceGen batch in HBM cut into 4 row-order batches at
+    arbitrary points: bit-exact against the oracle, and the job time per 1e8 records (accumulates +
+    one finalize to host + the Dependencies record) printed next to the bench's C2 step."""
+    import torch
+
+    from zipkin_amd import DepsContext, tracegen_params
+
+    S, N = 500, 100_000_000
+    p = tracegen_params(2, N // 15 + 1000, target_records=N, max_depth=6, num_services=S)
+    cols = DeviceColumns(N)
+    with DepsContext(S) as g:
+        n, _ = g.tracegen_device(p, cols)
+    torch.cuda.synchronize()
+    names = Dictionary([service_name(i) for i in range(S)])
+    cuts = sorted(np.random.default_rng(2).choice(np.arange(1, n), 3, replace=False).tolist())
+    bounds = [0, *[c + (c & 1) for c in cuts], n]  # even offsets keep the 16-B column alignment
+
+    def view(a, b):
+        v = DeviceColumns.__new__(DeviceColumns)
+        for k in ("trace_id", "span_id", "parent_id", "first_ts", "last_ts", "service_id", "flags"):
+            setattr(v, k, getattr(cols, k)[a:b])
+        v.n = v.capacity = b - a
+        return v
+
+    parts = [view(a, b) for a, b in zip(bounds[:-1], bounds[1:])]
+    job = ZipkinAggregateJob(names, clock=lambda: 10**15)
+    job.run(parts, S)  # warm
+    times = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        deps = job.run(parts, S)
+        times.append(time.perf_counter() - t0)
+    ms = sorted(times)[2] * 1e3
+    print(f"\nZipkinAggregateJob: {n} device records in 4 row batches: {ms:.3f} ms per run (median of 5), "
+          f"{n / ms * 1e3:.3e} spans/s")
+    host = cols.to_host(n)
+    assert _by_name(deps) == _oracle_by_name(host, S)
+    job.close()

@@ -16,10 +16,11 @@ from zipkin_amd import DepsContext, DeviceColumns, SpanColumns, ZkError, _abi, t
 pytestmark = pytest.mark.gpu
 
 
-def run(batches, S, **acc):
+def run(batches, S, trace_pass=False, **acc):
     """verify (default True) keeps the clustering pass's P3 + K1; verify=False on batches of more
-    than 2^18 records takes the group join (k_group_join) and its fallback."""
-    with DepsContext(S) as ctx:
+    than 2^18 records takes the group join (k_group_join) and its fallback, unless trace_pass
+    (zk_config.trace_pass) forces P3 + K1."""
+    with DepsContext(S, trace_pass=trace_pass) as ctx:
         for b in batches:
             ctx.accumulate(b, **acc)
         return ctx.finalize(), ctx.stats()
@@ -293,15 +294,14 @@ def test_group_join_fallback(gpu):
         assert st["spilled_traces"] >= 1
 
 
-def test_group_join_equals_the_trace_path(gpu, monkeypatch):
-    """The same shuffled batch through the group join and through P3 + K1 (ZK_GROUP_JOIN=0 at
-    create): identical tables and counters."""
+def test_group_join_equals_the_trace_path(gpu):
+    """The same shuffled batch through the group join and through P3 + K1 (zk_config.trace_pass):
+    identical tables and counters."""
     S = 200
     cols = tracegen_host(61, 60_000, max_depth=6, num_services=S)
     shuffled = cols.take(np.random.default_rng(61).permutation(len(cols)))
     got, st = run([shuffled], S, verify=False)
-    monkeypatch.setenv("ZK_GROUP_JOIN", "0")
-    ref, sr = run([shuffled], S, verify=False)
+    ref, sr = run([shuffled], S, verify=False, trace_pass=True)
     for k in ("m0", "m1", "m2", "m3", "m4", "present"):
         assert np.array_equal(getattr(got, k), getattr(ref, k)), k
     for k in st:
@@ -309,7 +309,7 @@ def test_group_join_equals_the_trace_path(gpu, monkeypatch):
             assert st[k] == sr[k], k
 
 
-def test_group_join_rich_spans_with_anomalies(gpu, monkeypatch):
+def test_group_join_rich_spans_with_anomalies(gpu):
     """Rich spans with the injected anomalies of tests/richgen.py (missing and invalid parents,
     duplicated core annotations, disagreeing fragments, client-only and nameless services), in 40
     copies with distinct traceIds (> 2^18 records), shuffled: the group join equals the oracle and
@@ -338,8 +338,7 @@ def test_group_join_rich_spans_with_anomalies(gpu, monkeypatch):
         ctx.accumulate(shuffled, verify=False)
         got, st = ctx.finalize(), ctx.stats()
     assert_parity(got, st, ref)
-    monkeypatch.setenv("ZK_GROUP_JOIN", "0")
-    with DepsContext(S, strict=False) as ctx:
+    with DepsContext(S, strict=False, trace_pass=True) as ctx:
         ctx.accumulate(shuffled, verify=False)
         got2, st2 = ctx.finalize(), ctx.stats()
     for k in ("m0", "m1", "m2", "m3", "m4", "present"):
@@ -362,3 +361,21 @@ def test_group_join_over_several_trace_complete_batches(gpu):
     assert all(len(p) > 2 ** 18 for p in parts)
     got, st = run(parts, S, verify=False)
     assert_parity(got, st, oracle.aggregate(cols, S))
+
+
+def test_group_join_respects_max_trace_records(gpu):
+    """max_trace_records below the group join's LDS tile: a 1500-record trace in a shuffled batch
+    of > 2^18 records without verification is too large exactly as on the clustered path (the
+    library then takes P3 + K1, which enforces the bound)."""
+    S = 31
+    rows = star_trace(4242, 749, nsvc=S)  # 1 + 2 x 749 = 1499 records
+    cols = SpanColumns.concat([cols_from_rows(rows), tracegen_host(83, 12_000, max_depth=6, num_services=S)])
+    assert len(cols) > 2 ** 18
+    shuffled = cols.take(np.random.default_rng(83).permutation(len(cols)))
+    for batch, clustered in ((shuffled, False), (cols, True)):
+        with DepsContext(S, max_trace_records=1000) as ctx:
+            ctx.accumulate(batch, clustered=clustered, verify=False)
+            with pytest.raises(ZkError) as e:
+                ctx.finalize()
+            assert e.value.status == _abi.ZK_ERR_TRACE_TOO_LARGE
+            assert ctx.stats()["trace_too_large"] == 1

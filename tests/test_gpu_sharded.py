@@ -188,3 +188,83 @@ def test_accumulate_into_merged_table_keeps_the_job_counters(gpu):
         sh.ctx.partial()
     finally:
         sh.close()
+
+
+def test_held_trace_dropped_on_one_shard_fails_every_rank(gpu):
+    """A held trace (ZK_BATCH_CONTINUES) that outgrows max_trace_records on ONE shard is counted on
+    the device, so zk_deps_partial carries it in the exchange tail and every rank's finalize returns
+    ZK_ERR_TRACE_TOO_LARGE (zkagg.h: every rank reaches the same status)."""
+    import torch
+
+    from tests.test_gpu_continuation import cut
+
+    S = 7
+    from tests.test_gpu_parity import star_trace
+
+    big = cols_from_rows(star_trace(1, 30, nsvc=S) + star_trace(2, 800, nsvc=S) + star_trace(3, 30, nsvc=S))
+    parts = cut(big, [561, 1161, 1672])
+    other = tracegen_host(48, 500, max_depth=5, num_services=S)
+    shards = [Shard(S, max_trace_records=1000) for _ in range(2)]
+    try:
+        for p in parts[:-1]:
+            shards[0].ctx.accumulate(p, clustered=True, continues=True)
+        shards[0].ctx.accumulate(parts[-1], clustered=True)
+        shards[1].ctx.accumulate(other, clustered=True, verify=True)
+        views = []
+        for sh in shards:
+            ptr, nbytes = sh.ctx.partial()
+            views.append(device_view(ptr, nbytes, torch.int64))
+        for sh in shards:
+            sh.ctx.sync()
+        total = torch.stack(views).sum(0)
+        for sh, v in zip(shards, views):
+            v.copy_(total)
+            torch.cuda.synchronize()
+            sh.ctx.note_merged(0)
+            with pytest.raises(ZkError) as e:
+                sh.ctx.finalize()
+            assert e.value.status == _abi.ZK_ERR_TRACE_TOO_LARGE
+            assert sh.ctx.stats()["trace_too_large"] == 1
+    finally:
+        for sh in shards:
+            sh.close()
+
+
+def test_global_trace_set_on_eight_device_shards_equals_the_oracle(gpu):
+    """configs[2]'s sharding at a size the oracle checks in seconds: ONE global TraceGen set whose
+    traceIds do not depend on the world size (zk_tracegen_device with global_ids), 8 shards each
+    generated on the device and accumulated in its own ctx, the exchange buffers summed as RCCL's
+    SUM all-reduce would; every rank's table is bit-exact against the oracle over the whole set
+    (generated on the host at world 1)."""
+    import torch
+
+    from zipkin_amd import DeviceColumns, tracegen_params
+
+    S, G, N = 500, 8, 2_000_000
+    whole = tracegen_host(7, N // 15 + 1000, target_records=N, max_depth=6, num_services=S, global_ids=True)
+    ref = oracle.aggregate(whole, S)
+    shards = [Shard(S) for _ in range(G)]
+    try:
+        views, n_all = [], 0
+        for r, sh in enumerate(shards):
+            p = tracegen_params(7, N // 15 + 1000, target_records=N, max_depth=6, num_services=S, rank=r, world=G,
+                                global_ids=True)
+            cols = DeviceColumns(N // G * 2 + 10_000)
+            n, _ = sh.ctx.tracegen_device(p, cols)
+            n_all += n
+            sh.ctx.accumulate(cols, clustered=True, verify=True, n=n)
+            ptr, nbytes = sh.ctx.partial()
+            views.append(device_view(ptr, nbytes, torch.int64))
+            sh._cols = cols
+        assert n_all == len(whole)
+        for sh in shards:
+            sh.ctx.sync()
+        total = torch.stack(views).sum(0)
+        for sh, v in zip(shards, views):
+            v.copy_(total)
+            torch.cuda.synchronize()
+            sh.ctx.note_merged(0)
+            assert_parity(sh.ctx.finalize(), sh.ctx.stats(), ref)
+    finally:
+        for sh in shards:
+            sh.close()

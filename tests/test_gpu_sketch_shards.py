@@ -47,9 +47,11 @@ def _assert_rt_equal(rt, ref, o):
     assert np.array_equal(regs, r2) and np.array_equal(hist, h2)
     assert np.array_equal(regs, o.regs) and np.array_equal(hist.astype(np.uint64), o.hist)
     assert np.array_equal(rt.distinct_traces(), ref.distinct_traces())
+    qs = (0.0, 0.5, 0.99, 1.0)
+    lo, hi, cnt = rt.quantiles_all(qs)  # every service in one device pass
     for s in range(0, rt.num_services, max(1, rt.num_services // 8)):
-        qs = (0.0, 0.5, 0.99, 1.0)
         assert rt.quantiles(s, qs) == ref.quantiles(s, qs) == o.quantile_bins(s, qs)
+        assert (list(zip(lo[s].tolist(), hi[s].tolist())), int(cnt[s])) == rt.quantiles(s, qs)
 
 
 @pytest.mark.parametrize("world,seed,traces,S,p", [(2, 1, 4000, 57, 12), (4, 2, 20000, 500, 14), (3, 5, 50, 9, 6)])

@@ -90,7 +90,8 @@ class zk_config(C.Structure):
         ("timing", C.c_uint32),
         ("table", C.c_void_p),
         ("table_bytes", C.c_uint64),
-        ("reserved", C.c_uint32 * 8),
+        ("trace_pass", C.c_uint32),
+        ("reserved", C.c_uint32 * 7),
     ]
 
 
@@ -279,10 +280,19 @@ _SIGNATURES = [
     ("zk_rt_accumulate_merged", C.c_int, [_P, _P, _P, _P, C.c_uint64, C.c_uint32]),
     ("zk_rt_distinct_traces", C.c_int, [_P, _P]),
     ("zk_rt_quantiles", C.c_int, [_P, C.c_uint32, _P, C.c_uint32, _P, _P, _U64P]),
+    ("zk_rt_quantiles_all", C.c_int, [_P, _P, C.c_uint32, _P, _P, _U64P]),
     ("zk_rt_tdigest", C.c_int, [_P, C.c_uint32, C.c_double, _P, _P, C.c_uint32, C.POINTER(C.c_uint32), _P, C.c_uint32, _P, C.POINTER(C.c_uint64)]),
     ("zk_rt_partial", C.c_int, [_P, C.POINTER(_P), _U64P, C.POINTER(_P), _U64P]),
     ("zk_rt_read", C.c_int, [_P, _P, _P]),
     ("zk_rt_dropped", C.c_int, [_P, _U64P, _U64P]),
+    # include/zkcomm.h: RCCL communicator and the multi-GPU merges
+    ("zk_comm_unique_id", C.c_int, [_P, C.c_uint64]),
+    ("zk_comm_create", C.c_int, [_P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int32, C.POINTER(_P)]),
+    ("zk_comm_destroy", C.c_int, [_P]),
+    ("zk_comm_last_error", C.c_char_p, [_P]),
+    ("zk_deps_allreduce", C.c_int, [_P, _P, C.c_uint64]),
+    ("zk_rt_allreduce", C.c_int, [_P, _P]),
+    ("zk_kv_allreduce", C.c_int, [_P, _P]),
     # include/zkingest.h: stored span fragments -> columnar records
     ("zk_ingest_create", C.c_int, [C.POINTER(_P)]),
     ("zk_ingest_destroy", C.c_int, [_P]),

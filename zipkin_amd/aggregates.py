@@ -388,33 +388,69 @@ def links_from_table(table, services: Dictionary) -> tuple:
 class ZipkinAggregateJob:
     """ZipkinAggregateJob.scala:10-46 with the compute on the device.
 
-    run(batches) accumulates trace-clustered column batches (one record per stored span fragment,
-    service ids from `services`), finalizes, and returns Dependencies(Time(0), Time.now, links) --
-    or None when there is no link, in which case the reference writes nothing (:43-45). With an
-    `aggregates` sink the record is stored through storeDependencies (StorageRecordWriter.scala:13-17).
+    run(batches) accumulates column batches (one record per stored span fragment, service ids from
+    `services`; host SpanColumns or device DeviceColumns), finalizes, and returns
+    Dependencies(Time(0), Time.now, links) -- or None when there is no link, in which case the
+    reference writes nothing (:43-45). With an `aggregates` sink the record is stored through
+    storeDependencies (StorageRecordWriter.scala:13-17).
+
+    order="rows" (default): batches as a row-per-trace storage reader returns them
+    (StorageRecordReader.scala:49-54) -- every trace's fragments adjacent, a trace possibly cut at a
+    batch edge -- accumulated with ZK_BATCH_TRACE_CLUSTERED | ZK_BATCH_CONTINUES, the path bench.py
+    measures. order="any": each batch holds whole traces in any order; the device clusters it.
+    verify adds ZK_BATCH_VERIFY_TRACES (the exact device check that no trace recurs).
+
+    The device context is kept between runs (a scheduled job reuses its buffers); close() frees it.
     """
 
     def __init__(self, services: Dictionary, *, device: int = 0, strict: bool = True,
-                 aggregates: Optional[Aggregates] = None, clock=now_us):
+                 aggregates: Optional[Aggregates] = None, clock=now_us, order: str = "rows", verify: bool = False):
+        if order not in ("rows", "any"):
+            raise ValueError("order is 'rows' or 'any'")
         self.services = services
         self.device = device
         self.strict = strict
         self.aggregates = aggregates
         self.clock = clock
+        self.order = order
+        self.verify = verify
         self.stats: dict = {}
+        self._ctx = None
 
-    def run(self, batches, num_services: Optional[int] = None) -> Optional[Dependencies]:
-        from .columns import SpanColumns
+    def close(self) -> None:
+        if self._ctx is not None:
+            self._ctx.close()
+            self._ctx = None
+
+    def _context(self, S: int):
         from .context import DepsContext
+
+        if self._ctx is None or self._ctx.num_services != S:
+            self.close()
+            self._ctx = DepsContext(S, device=self.device, strict=self.strict)
+        else:
+            self._ctx.reset()
+        return self._ctx
+
+    def accumulate_all(self, batches, num_services: Optional[int] = None):
+        """The job up to the finalize: every batch into a reset context (returned)."""
+        from .columns import SpanColumns
 
         if isinstance(batches, SpanColumns) or hasattr(batches, "abi"):
             batches = [batches]
-        S = num_services or max(1, len(self.services))
-        with DepsContext(S, device=self.device, strict=self.strict) as ctx:
-            for b in batches:
-                ctx.accumulate(b)
-            table = ctx.finalize()
-            self.stats = ctx.stats()
+        ctx = self._context(num_services or max(1, len(self.services)))
+        rows = self.order == "rows"
+        for b in batches:
+            ctx.accumulate(b, clustered=rows, continues=rows, verify=self.verify)
+        return ctx
+
+    def run(self, batches, num_services: Optional[int] = None) -> Optional[Dependencies]:
+        ctx = self.accumulate_all(batches, num_services)
+        table = ctx.finalize()  # the job ends here: a held-back trace is aggregated first
+        self.stats = ctx.stats()
+        return self._publish(table)
+
+    def _publish(self, table) -> Optional[Dependencies]:
         links = links_from_table(table, self.services)
         if not links:
             return None
@@ -440,17 +476,27 @@ class StoredSpanJob:
     """The aggregation job fed from the stored span bytes, with the removed producers of the
     top-annotation lists (CHANGELOG:7-8) restored next to it.
 
-    Input: trace-clustered batches of stored fragments (the Cassandra column values, i.e.
-    Snappy(TBinaryProtocol(Span)), CassieSpanStore.scala:52). Per batch the host decoder
-    (include/zkingest.h) writes the 48-B records plus the span indexer's items
-    (CassieSpanStore.scala:214-242); the device then runs the dependency job
-    (ZipkinAggregateJob.scala:20-43) and one count-min + top-K sketch each for binary-annotation
-    keys and non-core annotation values. Output, through `aggregates`: storeDependencies,
-    storeTopKeyValueAnnotations and storeTopAnnotations per service (Aggregates.scala:31-36).
+    Input: batches of stored fragments (the Cassandra column values, i.e.
+    Snappy(TBinaryProtocol(Span)), CassieSpanStore.scala:52; a list of bytes or the packed
+    (buf, offsets) form of SpanDecoder.decode) in row order: a row-per-trace reader
+    (StorageRecordReader.scala:49-54) returns every trace's fragments together and may cut a trace at
+    a batch edge. run() streams them: a worker thread decodes batch k+1 on the host (include/
+    zkingest.h: the 48-B records plus the span indexer's items, CassieSpanStore.scala:214-242) while
+    batch k runs on the device -- the dependency job (ZipkinAggregateJob.scala:20-43, accumulated with
+    ZK_BATCH_TRACE_CLUSTERED | ZK_BATCH_CONTINUES) and one count-min + top-K sketch each for
+    binary-annotation keys and non-core annotation values. run_device() takes fragments already in
+    HBM through the device decoder (dependencies only: that decoder emits no indexer items).
+    Output, through `aggregates`: storeDependencies, storeTopKeyValueAnnotations and
+    storeTopAnnotations per service (Aggregates.scala:31-36).
+
+    max_services sizes the device table (S x S cells) and the sketches before the dictionary is
+    known; a stream that names more services fails with ZK_ERR_SERVICE_RANGE. For the same reason the
+    count-min width per service is kv_width or the largest, 4096 (the auto width of <= 256 services).
     """
 
     def __init__(self, *, device: int = 0, strict: bool = True, aggregates: Optional[Aggregates] = None,
-                 clock=now_us, top_k: int = 10, snappy: bool = True, kv_width: int = 0, seed: int = 0):
+                 clock=now_us, top_k: int = 10, snappy: bool = True, kv_width: int = 0, seed: int = 0,
+                 max_services: int = 1024, verify: bool = False):
         self.device = device
         self.strict = strict
         self.aggregates = aggregates
@@ -459,6 +505,8 @@ class StoredSpanJob:
         self.snappy = snappy
         self.kv_width = kv_width
         self.seed = seed
+        self.max_services = max_services
+        self.verify = verify
         self.stats: dict = {}
         self.rejected = 0
         self.services: Optional[Dictionary] = None
@@ -466,7 +514,8 @@ class StoredSpanJob:
         self.top_annotations: Dict[str, List[str]] = {}
 
     def _decode(self, dec, blobs):
-        cap = max(16, 8 * len(blobs))
+        n = len(blobs[1]) - 1 if isinstance(blobs, tuple) else len(blobs)
+        cap = max(16, 8 * n)
         while True:
             try:
                 return dec.decode(blobs, snappy=self.snappy, strict=self.strict, items=True, item_cap=cap)
@@ -475,36 +524,52 @@ class StoredSpanJob:
                     raise
                 cap *= 4  # more binary annotations than guessed: decode the batch again
 
-    def _tops(self, dec, sketch) -> Dict[str, List[str]]:
+    def _tops(self, dec, sketch, S) -> Dict[str, List[str]]:
         keys, _, cnt = sketch.topk_all(self.top_k)
         return {dec.service_name(s_): [dec.string(int(h)) for h in keys[s_][: cnt[s_]]]
-                for s_ in range(sketch.num_services) if cnt[s_]}
+                for s_ in range(S) if cnt[s_]}
+
+    def _finish(self, ctx, names: List[str]) -> Optional[Dependencies]:
+        if len(names) > self.max_services:
+            raise _abi.ZkError(_abi.ZK_ERR_SERVICE_RANGE, f"{len(names)} services > max_services {self.max_services}")
+        self.services = Dictionary(names)
+        table = ctx.finalize()
+        self.stats = ctx.stats()
+        job = ZipkinAggregateJob(self.services, device=self.device, strict=self.strict, clock=self.clock)
+        return job._publish(table)
 
     def run(self, batches) -> Optional[Dependencies]:
+        from concurrent.futures import ThreadPoolExecutor
+
+        from .context import DepsContext
         from .ingest import SpanDecoder
         from .kv import KvSketch
 
         dec = SpanDecoder()
-        decoded = []
         self.rejected = 0
-        for blobs in batches:
-            cols, rej, kv, ann = self._decode(dec, blobs)
-            self.rejected += rej
-            decoded.append((cols, kv, ann))
-        self.services = Dictionary(dec.service_names())
-        S = max(1, len(self.services))
-        job = ZipkinAggregateJob(self.services, device=self.device, strict=self.strict, clock=self.clock)
-        deps = job.run([c for c, _, _ in decoded], num_services=S)
-        self.stats = job.stats
-        with KvSketch(S, device=self.device, width=self.kv_width, seed=self.seed) as kvs, \
-                KvSketch(S, device=self.device, width=self.kv_width, seed=self.seed) as anns:
-            for _, (ks, kh), (as_, ah) in decoded:
+        S = self.max_services
+        with DepsContext(S, device=self.device, strict=self.strict) as ctx, \
+                KvSketch(S, device=self.device, width=self.kv_width or 4096, seed=self.seed) as kvs, \
+                KvSketch(S, device=self.device, width=self.kv_width or 4096, seed=self.seed) as anns, \
+                ThreadPoolExecutor(max_workers=1) as pool:
+            it = iter(batches)
+            nxt = next(it, None)
+            fut = pool.submit(self._decode, dec, nxt) if nxt is not None else None
+            while fut is not None:
+                cols, rej, (ks, kh), (as_, ah) = fut.result()
+                nxt = next(it, None)
+                # the decoder's C call releases the GIL: batch k+1 decodes while batch k is staged and runs
+                fut = pool.submit(self._decode, dec, nxt) if nxt is not None else None
+                self.rejected += rej
+                ctx.accumulate(cols, clustered=True, continues=True, verify=self.verify)
                 if len(ks):
                     kvs.accumulate(ks, kh)
                 if len(as_):
                     anns.accumulate(as_, ah)
-            self.top_kv = self._tops(dec, kvs)
-            self.top_annotations = self._tops(dec, anns)
+            names = dec.service_names()
+            deps = self._finish(ctx, names)
+            self.top_kv = self._tops(dec, kvs, len(names))
+            self.top_annotations = self._tops(dec, anns, len(names))
         if self.aggregates is not None:
             if deps is not None:
                 self.aggregates.storeDependencies(deps)
@@ -512,4 +577,32 @@ class StoredSpanJob:
                 self.aggregates.storeTopKeyValueAnnotations(name, keys)
             for name, values in self.top_annotations.items():
                 self.aggregates.storeTopAnnotations(name, values)
+        return deps
+
+    def run_device(self, batches) -> Optional[Dependencies]:
+        """batches: (buf uint8, offsets int64[n + 1], n) torch tensors already in HBM, in row order.
+        Decoded on the device into a reused column buffer and accumulated on the same stream."""
+        import torch
+
+        from .context import DepsContext
+        from .ingest import DeviceSpanDecoder
+
+        S = self.max_services
+        self.rejected = 0
+        stream = torch.cuda.Stream(device=self.device)
+        dec = DeviceSpanDecoder(max(4096, S), device=self.device, stream=stream.cuda_stream)
+        try:
+            with DepsContext(S, device=self.device, strict=self.strict, stream=stream.cuda_stream) as ctx:
+                cols = None
+                for buf, off, n in batches:
+                    if cols is not None and cols.capacity < n:
+                        cols = None
+                    cols, rej = dec.decode_device(buf, off, n, snappy=self.snappy, strict=self.strict, out=cols)
+                    self.rejected += rej
+                    ctx.accumulate(cols, clustered=True, continues=True, verify=self.verify)
+                deps = self._finish(ctx, dec.service_names())
+        finally:
+            dec.close()
+        if self.aggregates is not None and deps is not None:
+            self.aggregates.storeDependencies(deps)
         return deps

@@ -26,9 +26,10 @@ SOURCES = [
     "zk_cluster.hip",
     "zk_launch.cpp",
     "zk_exchange.hip",
+    "zk_comm.cpp",
 ]
-HEADERS = ["zk_internal.h", "zk_cluster.h", "zk_tracegen.h", "zk_sketch_internal.h", "zk_rt_internal.h", "zk_block.h", "zk_launch.h"]
-PUBLIC_HEADERS = ["zkagg.h", "zksketch.h", "zkstore.h", "zkingest.h"]
+HEADERS = ["zk_internal.h", "zk_cluster.h", "zk_tracegen.h", "zk_sketch_internal.h", "zk_rt_internal.h", "zk_block.h", "zk_launch.h", "zk_comm.h"]
+PUBLIC_HEADERS = ["zkagg.h", "zksketch.h", "zkstore.h", "zkingest.h", "zkcomm.h"]
 LIB = PKG / "libzkagg.so"
 ARCH = os.environ.get("ZK_OFFLOAD_ARCH", "gfx950")
 
@@ -81,7 +82,7 @@ def build(force: bool = False, verbose: bool = False, variant: str = "", defines
     with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
         objs = list(ex.map(compile_one, SOURCES))
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *[str(o) for o in objs], "-L/opt/rocm/lib",
-           "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib", "-o", str(lib) + ".tmp"]
+           "-lrocprofiler-sdk-roctx", "-ldl", "-Wl,-rpath,/opt/rocm/lib", "-o", str(lib) + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -56,6 +56,7 @@ class DepsContext:
         timing: bool = False,
         table_ptr: int = 0,
         table_bytes: int = 0,
+        trace_pass: bool = False,
     ):
         self._L = _abi.lib()
         cfg = _abi.zk_config()
@@ -67,6 +68,7 @@ class DepsContext:
         cfg.timing = 1 if timing else 0
         cfg.table = table_ptr or None
         cfg.table_bytes = table_bytes
+        cfg.trace_pass = 1 if trace_pass else 0  # the A/B against the group join (zkagg.h)
         h = C.c_void_p()
         st = self._L.zk_ctx_create(C.byref(cfg), C.byref(h))
         if st != _abi.ZK_OK:

@@ -12,7 +12,7 @@
 #include <vector>
 
 #include "zk_cluster.h"
-#include <stdlib.h>
+#include "zk_comm.h"
 
 #include "zk_internal.h"
 #include "zk_launch.h"
@@ -32,8 +32,8 @@ struct zk_ctx {
     bool strict = true;
     uint32_t max_trace = 131072;
     bool timing = false;
-    // unclustered batches through the group join (k_group_join); ZK_GROUP_JOIN=0 in the environment
-    // at create: through P3 + K1 instead (the A/B of profiles/r04/ab_group_join.txt)
+    // unclustered batches through the group join (k_group_join); zk_config.trace_pass = 1: through
+    // P3 + K1 instead (the A/B of profiles/r04/ab_group_join.txt)
     bool group_join = true;
     uint64_t* table = nullptr;            // S*S*kLimbs
     bool own_table = true;
@@ -84,7 +84,6 @@ struct zk_ctx {
     uint8_t* carry = nullptr;
     uint64_t carry_cap = 0, carry_n = 0, carry_tid = 0;
     uint32_t carry_flags = 0;
-    uint64_t host_too_large = 0;          // held traces dropped for exceeding max_trace_records
     bool carry_dropped = false;           // the held trace was dropped: skip the rest of it too
     unsigned long long* edge = nullptr;   // device: the edge-run indices (k_edge_runs)
     uint64_t* h_edge = nullptr;           // pinned: e0, e1, first and last traceId of the batch
@@ -214,7 +213,6 @@ zk_status stats_sum(zk_ctx* c, uint64_t out[ST_N]) {
     for (int s = 0; s < ST_N; ++s) out[s] = 0;
     for (int sh = 0; sh < (c->merged ? 1 : kStatShards); ++sh)
         for (int s = 0; s < ST_N; ++s) out[s] += h[(size_t)sh * ST_N + s];
-    out[ST_TOO_LARGE] += c->host_too_large;  // held-back traces that outgrew max_trace_records (this rank)
     return ZK_OK;
 }
 
@@ -363,7 +361,7 @@ zk_status zk_ctx_create(const zk_config* cfg, zk_ctx** out) {
     c->S = cfg->num_services;
     c->strict = cfg->strict != 0;
     c->timing = cfg->timing != 0;
-    if (const char* e = getenv("ZK_GROUP_JOIN")) c->group_join = atoi(e) != 0;
+    c->group_join = cfg->trace_pass == 0;
     c->cus = prop.multiProcessorCount > 0 ? (uint32_t)prop.multiProcessorCount : 256;
     bucket_geometry(c->S, &c->nb, &c->cb_shift);
     if (cfg->max_trace_records) c->max_trace = cfg->max_trace_records;
@@ -459,7 +457,6 @@ zk_status zk_deps_reset(zk_ctx* c) {
     c->folded = false;
     c->carry_n = 0;  // a held-back trace belongs to the job being reset
     c->carry_dropped = false;
-    c->host_too_large = 0;
     return ZK_OK;
 }
 
@@ -494,6 +491,10 @@ static zk_status carry_append(zk_ctx* c, const SpanColsDev& d, uint64_t lo, uint
 // the held-back trace is complete: aggregate it as a batch of its own
 static zk_status flush_carry(zk_ctx* c) {
     if (!c->carry_n) return ZK_OK;
+    // (zk_deps_accumulate admits a batch with the held records counted, so this holds; checked again
+    // because the exchange limbs' headroom for 256 ranks rests on the 2^32 bound, zk_exchange.hip)
+    if (c->records_since_reset + c->carry_n > kMaxRecordsSinceReset)
+        return fail(c, ZK_ERR_CAPACITY, "more than 2^32-1 records since reset");
     const SpanColsMut m = carve_cols(c->carry, c->carry_cap);
     const SpanColsDev d{m.trace_id, m.span_id, m.parent_id, m.first_ts, m.last_ts, m.service_id, m.flags, c->carry_n};
     c->carry_n = 0;
@@ -541,7 +542,9 @@ static zk_status continue_batch(zk_ctx* c, const SpanColsDev& d, uint32_t flags)
                 // longer than max_trace_records: not aggregated, like any trace that long
                 c->carry_n = 0;
                 c->carry_dropped = true;
-                c->host_too_large += 1;
+                // counted on the device, in the stats shards that zk_deps_partial folds into the
+                // exchange tail, so every rank of a sharded job sees it (zkagg.h: same status)
+                ZK_HIP(c, launch_stat_add(c->stats + ST_TOO_LARGE, 1, c->stream));
             } else {
                 ZK_ST(carry_append(c, d, 0, lead));
             }
@@ -594,7 +597,7 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
     }
     if (!cols_ok(cols)) return fail(c, ZK_ERR_INVALID_ARG, "null column pointer");
     const bool join = !c->rt || c->rt_mode == ZK_RT_WITH_DEPS;
-    if (join && c->records_since_reset + n > kMaxRecordsSinceReset)
+    if (join && c->records_since_reset + c->carry_n + n > kMaxRecordsSinceReset)  // held records included
         return fail(c, ZK_ERR_CAPACITY, "more than 2^32-1 records since reset");
     ZK_HIP(c, hipSetDevice(c->device));
     if (c->merged) {
@@ -645,6 +648,13 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
                 !aligned(d.flags, 8))) {
         // K1 reads two records per lane with one 16-byte (u64 columns) / 8-byte (u32) load
         return fail(c, ZK_ERR_INVALID_ARG, "device columns must be 16-byte (u64) / 8-byte (u32) aligned");
+    }
+    if (!(flags & ZK_BATCH_TRACE_CLUSTERED)) {
+        // a batch in any order ends a held trace (zkagg.h): the held trace is aggregated as it is, the
+        // batch as a whole (its first run is not the held trace's continuation)
+        c->carry_dropped = false;
+        ZK_ST(flush_carry(c));
+        return accumulate_dev(c, d, flags, 0);
     }
     if (c->carry_n || c->carry_dropped || (flags & ZK_BATCH_CONTINUES)) return continue_batch(c, d, flags);
     return accumulate_dev(c, d, flags, 0);
@@ -775,8 +785,10 @@ static zk_status accumulate_dev(zk_ctx* c, SpanColsDev d, uint32_t flags, uint32
     if (n <= skip) return ZK_OK;
     const bool join = !c->rt || c->rt_mode == ZK_RT_WITH_DEPS;
     // unclustered, without the trace check or a realtime sketch: the group join (two-level plans)
+    // (only when max_trace_records >= the group join's tile: it aggregates every trace of a sub-bucket
+    // it holds, so a smaller bound could not be enforced there as K1 enforces it)
     if (!(flags & ZK_BATCH_TRACE_CLUSTERED) && !(flags & ZK_BATCH_VERIFY_TRACES) && !c->rt && c->group_join &&
-        n <= 0xFFFFFFFFull) {
+        c->max_trace >= group_join_capacity() && n <= 0xFFFFFFFFull) {
         const ClusterPlan gp = cluster_plan(n, c->cus, true);
         if (gp.b1 && gp.b2) return accumulate_groups(c, d, gp);
     }
@@ -1024,6 +1036,20 @@ zk_status zk_deps_note_merged(zk_ctx* c, uint64_t total_records) {
     c->records_since_reset = total_records;
     c->merged = true;
     return ZK_OK;
+}
+
+zk_status zk_deps_allreduce(zk_ctx* c, zk_comm* comm, uint64_t total_records) {
+    if (!c) return ZK_ERR_INVALID_ARG;
+    if (!comm) return fail(c, ZK_ERR_INVALID_ARG, "null communicator");
+    ZK_TRY
+    RoctxRange rr("zk_deps_allreduce");
+    void* x = nullptr;
+    uint64_t bytes = 0;
+    ZK_ST(zk_deps_partial(c, &x, &bytes));  // counters folded, table packed (ctx stream)
+    // ONE int64 SUM over every rank's exchange buffer, ordered after the pack on the ctx stream
+    ZK_ST(comm_allreduce(comm, x, bytes / 8, kCommI64, kCommSum, c->device, c->stream, &c->err));
+    return zk_deps_note_merged(c, total_records);
+    ZK_CATCH(c)
 }
 
 zk_status zk_rt_bind(zk_ctx* c, zk_rt* rt, uint32_t mode) {

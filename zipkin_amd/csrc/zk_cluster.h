@@ -51,6 +51,7 @@ hipError_t launch_trace_set_insert(const uint64_t* trace_id, uint64_t n, uint64_
 hipError_t launch_trace_set_rehash(const uint64_t* old, uint64_t old_slots, uint64_t* set, uint64_t slots,
                                    hipStream_t s);
 // out[0..ST_N) = sum over the kStatShards copies of the device counters
+hipError_t launch_stat_add(unsigned long long* slot, uint64_t v, hipStream_t s);
 hipError_t launch_stats_fold(const unsigned long long* shards, unsigned long long* out, hipStream_t s);
 // ZK_BATCH_CONTINUES: the batch's edge runs. out[0] = the first index i in [1, min(n, L + 1)) with
 // trace_id[i] != trace_id[i - 1] (~0 if none), out[1] = the last such index in [max(1, n - L - 1), n)

@@ -759,6 +759,11 @@ __global__ __launch_bounds__(256) void k_stats_fold(const unsigned long long* __
     }
 }
 
+// one counter += v on the stream (a held trace dropped by the host-side continuation logic)
+__global__ __launch_bounds__(64) void k_stat_add(unsigned long long* __restrict__ slot, unsigned long long v) {
+    if (threadIdx.x == 0) atomicAdd(slot, v);
+}
+
 unsigned grid_for(uint64_t n) {
     const uint64_t g = (n + 255) / 256;
     return (unsigned)(g < 8192 ? (g ? g : 1) : 8192);
@@ -782,7 +787,9 @@ ClusterPlan cluster_plan(uint64_t n, uint32_t cus, bool groups) {
     // hardly any sub-bucket exceeds it
     uint32_t bits = 0;
     uint64_t target = groups ? group_join_capacity() * 3 / 8 : 2048;
-    if (const char* e = groups ? getenv("ZK_CL_GROUP_TARGET") : nullptr) target = (uint64_t)atoi(e);  // A/B only
+#ifdef ZK_DIAG_ENV  // diagnostic builds only (tools/build_variant.py): A/B override of the sub-bucket target
+    if (const char* e = groups ? getenv("ZK_CL_GROUP_TARGET") : nullptr) target = (uint64_t)atoi(e);
+#endif
     while (bits < 22 && (n >> bits) > target) ++bits;
     if (n <= kClusterSmall) bits = 0;  // P3 alone: one workgroup over the whole batch
     if (bits <= 8) {
@@ -796,7 +803,7 @@ ClusterPlan cluster_plan(uint64_t n, uint32_t cus, bool groups) {
             p.b2 = 11;
         }
     }
-    // diagnostic A/B override of the digit split (never set by the product)
+#ifdef ZK_DIAG_ENV  // diagnostic builds only: A/B override of the digit split
     if (const char* e1 = getenv("ZK_CL_B1")) {
         const uint32_t b1 = (uint32_t)atoi(e1);
         if (b1 <= bits && b1 <= 11 && bits - b1 <= 11 && (b1 > 0 || bits == 0)) {
@@ -804,6 +811,7 @@ ClusterPlan cluster_plan(uint64_t n, uint32_t cus, bool groups) {
             p.b2 = bits - b1;
         }
     }
+#endif
     p.nb1 = 1u << p.b1;
     p.nb2 = 1u << p.b2;
     // P0 geometry (the ranges P1's portions are cut from): one range per CU, whole chunks each
@@ -1025,6 +1033,10 @@ hipError_t launch_trace_set_rehash(const uint64_t* old, uint64_t old_slots, uint
 hipError_t launch_edge_runs(const uint64_t* trace_id, uint64_t n, uint64_t L, unsigned long long* out, hipStream_t s) {
     if (n < 2) return hipSuccess;
     return launch_checked("k_edge_runs", k_edge_runs, dim3(64), dim3(256), 0, s, trace_id, n, L, out);
+}
+
+hipError_t launch_stat_add(unsigned long long* slot, uint64_t v, hipStream_t s) {
+    return launch_checked("k_stat_add", k_stat_add, dim3(1), dim3(64), 0, s, slot, (unsigned long long)v);
 }
 
 hipError_t launch_stats_fold(const unsigned long long* shards, unsigned long long* out, hipStream_t s) {

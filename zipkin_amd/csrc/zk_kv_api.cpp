@@ -5,6 +5,7 @@
 #include <string>
 #include <vector>
 
+#include "zk_comm.h"
 #include "zk_guard.h"
 #include "zk_launch.h"
 #include "zk_internal.h"
@@ -38,6 +39,10 @@ struct zk_kv {
     // pinned host mirror for queries: dropped counter, per-service totals, candidate keys and
     // estimates -- one contiguous copy each instead of strided copies into pageable memory
     uint8_t* hq = nullptr;
+    // every rank's candidate lists, gathered by zk_kv_allreduce ([lists][S][cand])
+    uint64_t* g_key = nullptr;
+    uint32_t* g_est = nullptr;
+    uint32_t g_lists = 0;
     bool timing = false;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     bool ev_recorded = false;
@@ -166,7 +171,7 @@ zk_status zk_kv_destroy(zk_kv* k) {
     if (k->stream) hipStreamSynchronize(k->stream);
     for (void* p : {(void*)k->a.cm, (void*)k->a.totals, (void*)k->a.cand_key, (void*)k->a.cand_est, (void*)k->dropped,
                     (void*)k->sorted, (void*)k->seg, (void*)k->unit_base, k->part, (void*)k->unit_key,
-                    (void*)k->unit_est, k->stage, (void*)k->qkeys, (void*)k->qest})
+                    (void*)k->unit_est, k->stage, (void*)k->qkeys, (void*)k->qest, (void*)k->g_key, (void*)k->g_est})
         if (p) hipFree(p);
     if (k->hq) hipHostFree(k->hq);
     for (hipEvent_t ev : k->ev)
@@ -414,6 +419,38 @@ zk_status zk_kv_merge_candidates(zk_kv* k, const uint64_t* keys, const uint32_t*
     a.extra_lists = lists;
     KV_HIP(k, launch_kv_merge(a, k->stream));
     return ZK_OK;
+    ZK_GUARD_END
+}
+
+zk_status zk_kv_allreduce(zk_kv* k, zk_comm* comm) {
+    ZK_GUARD_BEGIN
+    if (!k) return ZK_ERR_INVALID_ARG;
+    if (!comm) return kfail(k, ZK_ERR_INVALID_ARG, "null communicator");
+    KV_HIP(k, hipSetDevice(k->device));
+    const KvArgs& a = k->a;
+    const uint32_t W = comm_world(comm);
+    const uint64_t lk = (uint64_t)a.S * a.cand;
+    if (W > k->g_lists) {
+        KV_HIP(k, hipStreamSynchronize(k->stream));  // the old buffers may still be read
+        hipFree(k->g_key);
+        hipFree(k->g_est);
+        k->g_key = nullptr;
+        k->g_est = nullptr;
+        k->g_lists = 0;
+        KV_HIP(k, hipMalloc(&k->g_key, W * lk * 8));
+        KV_HIP(k, hipMalloc(&k->g_est, W * lk * 4));
+        k->g_lists = W;
+    }
+    // the candidate lists first (the merge overwrites them), then the counters and totals
+    zk_status st = comm_allgather(comm, a.cand_key, k->g_key, lk * 8, k->device, k->stream, &k->err);
+    if (st == ZK_OK) st = comm_allgather(comm, a.cand_est, k->g_est, lk * 4, k->device, k->stream, &k->err);
+    if (st == ZK_OK)
+        st = comm_allreduce(comm, a.cm, (uint64_t)a.S * a.depth * a.width, kCommU32, kCommSum, k->device, k->stream,
+                            &k->err);
+    if (st == ZK_OK) st = comm_allreduce(comm, a.totals, a.S, kCommU64, kCommSum, k->device, k->stream, &k->err);
+    if (st == ZK_OK) st = comm_allreduce(comm, k->dropped, 1, kCommU64, kCommSum, k->device, k->stream, &k->err);
+    if (st != ZK_OK) return st;
+    return zk_kv_merge_candidates(k, k->g_key, k->g_est, W);
     ZK_GUARD_END
 }
 

@@ -133,7 +133,80 @@ __global__ void k_rt_items(const uint32_t* __restrict__ svc, const uint64_t* __r
     }
 }
 
+// Queries of every service at once (zk_rt_distinct_traces, zk_rt_quantiles_all), one workgroup per
+// service: the exact HyperLogLog sum z = sum_j 2^(64 - M[j]) as a 128-bit integer (from a count of
+// each register value, so the result does not depend on the summation order) and the zero count;
+// the histogram's total N; for each quantile q[i] the bin holding the nearest rank
+// max(1, ceil(q N)). out row s: [z_lo, z_hi, zeros, N, bin_0 .. bin_{nq-1}]. The host finishes the
+// estimate with the same double arithmetic as hll_estimate, so both give identical results.
+__global__ __launch_bounds__(kRtWG) void k_rt_query(const uint8_t* __restrict__ regs, const uint32_t* __restrict__ hist,
+                                                   uint32_t p, uint32_t nbins, const double* __restrict__ q, uint32_t nq,
+                                                   unsigned long long* __restrict__ out) {
+    __shared__ uint32_t cnt[65];
+    __shared__ unsigned long long part[kRtWG];
+    __shared__ unsigned long long s_n;
+    const uint32_t s = blockIdx.x, t = threadIdx.x;
+    if (t < 65) cnt[t] = 0u;
+    __syncthreads();
+    const uint32_t R = 1u << p;
+    const uint32_t* rw = (const uint32_t*)(regs + (uint64_t)s * R);
+    for (uint32_t x = t; x < (R >> 2); x += kRtWG) {
+        const uint32_t w = rw[x];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) atomicAdd(&cnt[(w >> (8 * k)) & 0xFFu], 1u);
+    }
+    // the histogram: each thread one contiguous chunk of bins
+    const uint32_t chunk = (nbins + kRtWG - 1) / kRtWG;
+    const uint32_t b0 = t * chunk < nbins ? t * chunk : nbins, b1 = b0 + chunk < nbins ? b0 + chunk : nbins;
+    const uint32_t* h = hist + (uint64_t)s * nbins;
+    unsigned long long local = 0;
+    for (uint32_t b = b0; b < b1; ++b) local += h[b];
+    part[t] = local;
+    __syncthreads();
+    unsigned long long* o = out + (uint64_t)s * (4u + nq);
+    if (t == 0) {
+        unsigned __int128 z = 0;
+        for (int v = 0; v <= 64; ++v) z += (unsigned __int128)cnt[v] << (64 - v);
+        unsigned long long N = 0;
+        for (uint32_t k = 0; k < kRtWG; ++k) {  // exclusive prefix of the chunks, in place
+            const unsigned long long c = part[k];
+            part[k] = N;
+            N += c;
+        }
+        o[0] = (unsigned long long)z;
+        o[1] = (unsigned long long)(z >> 64);
+        o[2] = cnt[0];
+        o[3] = N;
+        for (uint32_t i = 0; i < nq; ++i) o[4 + i] = 0ull;
+        s_n = N;
+    }
+    __syncthreads();
+    const unsigned long long N = s_n;
+    if (N == 0) return;
+    const unsigned long long excl = part[t];
+    for (uint32_t i = 0; i < nq; ++i) {
+        unsigned long long rank = (unsigned long long)ceil(q[i] * (double)N);
+        if (rank < 1) rank = 1;
+        if (rank > N) rank = N;
+        if (excl < rank && excl + local >= rank) {
+            unsigned long long cum = excl;
+            for (uint32_t b = b0; b < b1; ++b) {
+                cum += h[b];
+                if (cum >= rank) {
+                    o[4 + i] = b;
+                    break;
+                }
+            }
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t launch_rt_query(const uint8_t* regs, const uint32_t* hist, uint32_t S, uint32_t p, uint32_t nbins,
+                           const double* q, uint32_t nq, unsigned long long* out, hipStream_t s) {
+    return launch_checked("k_rt_query", k_rt_query, dim3(S), dim3(kRtWG), 0, s, regs, hist, p, nbins, q, nq, out);
+}
 
 hipError_t launch_rt_sketch(const RtArgs& a, hipStream_t s) {
     if (!a.max_units) return hipSuccess;

@@ -7,6 +7,7 @@
 #include <string>
 #include <vector>
 
+#include "zk_comm.h"
 #include "zk_guard.h"
 #include "zk_launch.h"
 #include "zk_internal.h"
@@ -42,6 +43,10 @@ struct zk_rt {
     // merged-span staging
     void* stage = nullptr;
     uint64_t stage_cap = 0;
+    // all-service queries (k_rt_query): quantiles, its output and the pinned host mirror
+    double* q_dev = nullptr;
+    unsigned long long* q_out = nullptr;
+    unsigned long long* q_host = nullptr;
     std::string err;
 };
 
@@ -105,14 +110,9 @@ zk_status sketch_items(zk_rt* r, const PartitionPlan& plan, bool lists, const ui
     return ZK_OK;
 }
 
-double hll_estimate(const uint8_t* M, uint32_t p) {
+// z = sum of 2^(64 - M[j]) = 2^64 * sum 2^-M[j], exact (k_rt_query counts it on the device)
+double hll_estimate(unsigned __int128 z, uint64_t zeros, uint32_t p) {
     const uint32_t mm = 1u << p;
-    unsigned __int128 z = 0;  // sum of 2^(64 - M[j]) = 2^64 * sum 2^-M[j], exact
-    uint32_t zeros = 0;
-    for (uint32_t j = 0; j < mm; ++j) {
-        z += (unsigned __int128)1 << (64 - M[j]);
-        zeros += M[j] == 0;
-    }
     const double Z = ldexp((double)z, -64);
     const double m = (double)mm;
     double alpha;
@@ -267,6 +267,21 @@ void rt_set_stream(zk_rt* r, hipStream_t s) {
     }
 }
 
+// every service's HLL sums and the bins of up to kRtQueryMaxQ quantiles, one kernel and one copy
+// into the pinned mirror: row s of r->q_host = [z_lo, z_hi, zeros, N, bins...]
+zk_status rt_query(zk_rt* r, const double* q, uint32_t nq) {
+    if (!r->q_out) {
+        RT_HIP(r, hipMalloc(&r->q_dev, kRtQueryMaxQ * sizeof(double)));
+        RT_HIP(r, hipMalloc(&r->q_out, (uint64_t)r->S * (4 + kRtQueryMaxQ) * 8));
+        RT_HIP(r, hipHostMalloc((void**)&r->q_host, (uint64_t)r->S * (4 + kRtQueryMaxQ) * 8, hipHostMallocDefault));
+    }
+    if (nq) RT_HIP(r, hipMemcpyAsync(r->q_dev, q, nq * sizeof(double), hipMemcpyHostToDevice, r->stream));
+    RT_HIP(r, launch_rt_query(r->regs, r->hist, r->S, r->p, r->nbins, r->q_dev, nq, r->q_out, r->stream));
+    RT_HIP(r, hipMemcpyAsync(r->q_host, r->q_out, (uint64_t)r->S * (4 + nq) * 8, hipMemcpyDeviceToHost, r->stream));
+    RT_HIP(r, hipStreamSynchronize(r->stream));
+    return ZK_OK;
+}
+
 }  // namespace zk
 
 extern "C" {
@@ -322,8 +337,10 @@ zk_status zk_rt_destroy(zk_rt* r) {
     hipSetDevice(r->device);
     if (r->stream) hipStreamSynchronize(r->stream);
     for (void* q : {(void*)r->regs, (void*)r->hist, (void*)r->dropped, (void*)r->pay, (void*)r->svc, (void*)r->count,
-                    (void*)r->sorted, (void*)r->seg, (void*)r->unit_base, r->part, r->stage})
+                    (void*)r->sorted, (void*)r->seg, (void*)r->unit_base, r->part, r->stage, (void*)r->q_dev,
+                    (void*)r->q_out})
         if (q) hipFree(q);
+    if (r->q_host) hipHostFree(r->q_host);
     // a caller-provided stream is not ours to destroy; a private one is
     delete r;
     return ZK_OK;
@@ -405,10 +422,42 @@ zk_status zk_rt_read(zk_rt* r, uint8_t* registers, uint32_t* histogram) {
 zk_status zk_rt_distinct_traces(zk_rt* r, double* estimate) {
     ZK_GUARD_BEGIN
     if (!r || !estimate) return ZK_ERR_INVALID_ARG;
-    std::vector<uint8_t> regs((uint64_t)r->S << r->p);
-    zk_status st = zk_rt_read(r, regs.data(), nullptr);
+    RT_HIP(r, hipSetDevice(r->device));
+    const zk_status st = rt_query(r, nullptr, 0);
     if (st != ZK_OK) return st;
-    for (uint32_t s = 0; s < r->S; ++s) estimate[s] = hll_estimate(regs.data() + ((uint64_t)s << r->p), r->p);
+    for (uint32_t s = 0; s < r->S; ++s) {
+        const unsigned long long* o = r->q_host + (uint64_t)s * 4;
+        estimate[s] = hll_estimate(((unsigned __int128)o[1] << 64) | o[0], o[2], r->p);
+    }
+    return ZK_OK;
+    ZK_GUARD_END
+}
+
+zk_status zk_rt_quantiles_all(zk_rt* r, const double* q, uint32_t nq, int64_t* lo, int64_t* hi, uint64_t* count) {
+    ZK_GUARD_BEGIN
+    if (!r) return ZK_ERR_INVALID_ARG;
+    if (nq && (!q || !lo || !hi)) return rfail(r, ZK_ERR_INVALID_ARG, "null array");
+    for (uint32_t i = 0; i < nq; ++i)
+        if (!(q[i] >= 0.0 && q[i] <= 1.0)) return rfail(r, ZK_ERR_INVALID_ARG, "quantile outside [0, 1]");
+    RT_HIP(r, hipSetDevice(r->device));
+    for (uint32_t i0 = 0; i0 < nq || (i0 == 0 && count); i0 += kRtQueryMaxQ) {
+        const uint32_t k = nq - i0 < kRtQueryMaxQ ? nq - i0 : kRtQueryMaxQ;
+        const zk_status st = rt_query(r, q + i0, k);
+        if (st != ZK_OK) return st;
+        for (uint32_t s = 0; s < r->S; ++s) {
+            const unsigned long long* o = r->q_host + (uint64_t)s * (4 + k);
+            if (count) count[s] = o[3];
+            for (uint32_t i = 0; i < k; ++i) {
+                int64_t* l = lo + (uint64_t)s * nq + i0 + i;
+                int64_t* h = hi + (uint64_t)s * nq + i0 + i;
+                if (o[3])
+                    bin_bounds((uint32_t)o[4 + i], r->m, l, h);
+                else
+                    *l = *h = 0;
+            }
+        }
+        if (!nq) break;
+    }
     return ZK_OK;
     ZK_GUARD_END
 }
@@ -501,6 +550,20 @@ zk_status zk_rt_dropped(zk_rt* r, uint64_t* service_range, uint64_t* duration_ra
     if (service_range) *service_range = d[0];
     if (duration_range) *duration_range = d[1];
     return ZK_OK;
+    ZK_GUARD_END
+}
+
+zk_status zk_rt_allreduce(zk_rt* r, zk_comm* comm) {
+    ZK_GUARD_BEGIN
+    if (!r) return ZK_ERR_INVALID_ARG;
+    if (!comm) return rfail(r, ZK_ERR_INVALID_ARG, "null communicator");
+    RT_HIP(r, hipSetDevice(r->device));
+    // registers by MAX, bins and the two drop counters by SUM, on the sketch's (bound ctx's) stream
+    zk_status st = comm_allreduce(comm, r->regs, (uint64_t)r->S << r->p, kCommU8, kCommMax, r->device, r->stream, &r->err);
+    if (st == ZK_OK)
+        st = comm_allreduce(comm, r->hist, (uint64_t)r->S * r->nbins, kCommU32, kCommSum, r->device, r->stream, &r->err);
+    if (st == ZK_OK) st = comm_allreduce(comm, r->dropped, 2, kCommU64, kCommSum, r->device, r->stream, &r->err);
+    return st;
     ZK_GUARD_END
 }
 

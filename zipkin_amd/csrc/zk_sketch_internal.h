@@ -132,6 +132,10 @@ struct RtArgs {
     uint32_t max_units;
 };
 hipError_t launch_rt_sketch(const RtArgs& a, hipStream_t s);
+// per service: [z_lo, z_hi, zero registers, N, the bin of each q[i]] (u64 x (4 + nq)), k_rt_query
+constexpr uint32_t kRtQueryMaxQ = 32;
+hipError_t launch_rt_query(const uint8_t* regs, const uint32_t* hist, uint32_t S, uint32_t p, uint32_t nbins,
+                           const double* q, uint32_t nq, unsigned long long* out, hipStream_t s);
 // merged-span input -> (svc, payload) items; invalid items get svc = 0xFFFFFFFF (dropped by the
 // partition) and are counted in dropped[0] (service) / dropped[1] (duration)
 hipError_t launch_rt_items(const uint32_t* svc, const uint64_t* trace_id, const int64_t* dur, uint64_t n, uint32_t S,

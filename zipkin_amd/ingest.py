@@ -43,15 +43,24 @@ class SpanDecoder:
         if st != _abi.ZK_OK:
             raise _abi.ZkError(st, self._L.zk_ingest_last_error(self._h).decode() or _abi.status_str(st))
 
-    def decode(self, blobs: Sequence[bytes], *, snappy: bool = True, strict: bool = True, items: bool = False,
+    def decode(self, blobs, *, snappy: bool = True, strict: bool = True, items: bool = False,
                item_cap: int | None = None):
-        """Decode stored fragments (one bytes object each). Returns (SpanColumns, rejected) or, with
-        items=True, (SpanColumns, rejected, (kv_service, kv_key), (ann_service, ann_value))."""
-        n = len(blobs)
-        offsets = np.zeros(n + 1, np.uint64)
-        if n:
-            offsets[1:] = np.cumsum([len(b) for b in blobs], dtype=np.uint64)
-        buf = np.frombuffer(b"".join(blobs) or b"\0", dtype=np.uint8)
+        """Decode stored fragments: a sequence of bytes objects (one per fragment), or the packed
+        form (buf uint8[total], offsets uint64[n + 1]) -- fragment i is buf[offsets[i]:offsets[i+1]].
+        Returns (SpanColumns, rejected) or, with items=True, (SpanColumns, rejected,
+        (kv_service, kv_key), (ann_service, ann_value))."""
+        if isinstance(blobs, tuple) and len(blobs) == 2 and isinstance(blobs[0], np.ndarray):
+            buf = np.ascontiguousarray(blobs[0], dtype=np.uint8)
+            offsets = np.ascontiguousarray(blobs[1], dtype=np.uint64)
+            n = len(offsets) - 1
+            if not len(buf):
+                buf = np.zeros(1, np.uint8)
+        else:
+            n = len(blobs)
+            offsets = np.zeros(n + 1, np.uint64)
+            if n:
+                offsets[1:] = np.cumsum([len(b) for b in blobs], dtype=np.uint64)
+            buf = np.frombuffer(b"".join(blobs) or b"\0", dtype=np.uint8)
         cols = SpanColumns.empty(n)
         nout, nrej = C.c_uint64(), C.c_uint64()
         it = None

@@ -113,6 +113,18 @@ class RtSketch:
                                             C.byref(cnt)))
         return [(int(a), int(b)) for a, b in zip(lo, hi)], int(cnt.value)
 
+    def quantiles_all(self, qs=(0.5, 0.99)):
+        """(lo int64[S, nq], hi int64[S, nq], count uint64[S]) for every service at once
+        (zk_rt_quantiles_all: one device pass and one copy)."""
+        q = np.ascontiguousarray(qs, dtype=np.float64)
+        S = self.num_services
+        lo = np.zeros((S, len(q)), np.int64)
+        hi = np.zeros((S, len(q)), np.int64)
+        cnt = np.zeros(S, np.uint64)
+        self._check(self._L.zk_rt_quantiles_all(self._h, q.ctypes.data, len(q), lo.ctypes.data, hi.ctypes.data,
+                                                cnt.ctypes.data_as(_abi._U64P)))
+        return lo, hi, cnt
+
     def tdigest(self, service: int, compression: float = 200.0, qs=(0.5, 0.99)):
         """(centroid means, centroid weights, t-digest estimates of qs, count) of one service's
         duration digest (zk_rt_tdigest: a merging t-digest over the exact histogram)."""
