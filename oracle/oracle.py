@@ -61,6 +61,9 @@ def lib():
         L.zkv_port.restype = C.c_int
         L.zkv_port.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                C.c_uint64, C.c_int] + [C.c_void_p] * 6 + [C.POINTER(C.c_double)]
+        L.zkr_port.restype = C.c_int
+        L.zkr_port.argtypes = [C.c_void_p] * 6 + [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, C.c_int,
+                                                  C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_double)]
         _lib = L
     return _lib
 

@@ -267,3 +267,36 @@ def tdigest_quantile(cent, vmin: int, vmax: int, N: int, q: float) -> float:
     a = N - w / 2
     t = (idx - a) / (w / 2) if w > 0 else 0.0
     return mean + min(t, 1.0) * (vmax - mean)
+
+
+class RtPortResult:
+    def __init__(self, regs, hist, dropped, seconds, threads):
+        self.regs, self.hist, self.seconds, self.threads = regs, hist, seconds, threads
+        self.dropped_service, self.dropped_duration = int(dropped[0]), int(dropped[1])
+        self.p = int(regs.shape[1]).bit_length() - 1
+
+    def distinct(self) -> np.ndarray:
+        return np.array([hll_estimate(self.regs[s], self.p) for s in range(self.regs.shape[0])])
+
+
+def rt_port(cols, num_services: int, p: int = 14, m: int = 7, seed: int = 0, threads: int = 1) -> RtPortResult:
+    """oracle/zk_rt_port.c: one TRACE-CLUSTERED batch into fresh sketches, multithreaded (C5's
+    checker on large prefixes and its CPU baseline). Same registers and bins as
+    RtOracle.accumulate_merged(*merged_span_items(cols)) (tests/test_realtime.py)."""
+    import ctypes as C
+
+    from .oracle import lib
+
+    arrs = [np.ascontiguousarray(cols.trace_id, np.uint64), np.ascontiguousarray(cols.span_id, np.uint64),
+            np.ascontiguousarray(cols.first_ts, np.int64), np.ascontiguousarray(cols.last_ts, np.int64),
+            np.ascontiguousarray(cols.service_id, np.uint32), np.ascontiguousarray(cols.flags, np.uint32)]
+    S = num_services
+    regs = np.zeros((S, 1 << p), np.uint8)
+    hist = np.zeros((S, nbins(m)), np.uint64)
+    dropped = np.zeros(2, np.uint64)
+    secs = C.c_double()
+    rc = lib().zkr_port(*[a.ctypes.data for a in arrs], len(arrs[0]), S, p, m, seed, threads, regs.ctypes.data,
+                        hist.ctypes.data, dropped.ctypes.data, C.byref(secs))
+    if rc != 0:
+        raise ValueError("zkr_port: bad arguments or out of memory")
+    return RtPortResult(regs, hist, dropped, secs.value, threads)

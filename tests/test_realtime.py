@@ -119,6 +119,27 @@ def test_items_equal_span_level_semantics():
     assert got == want
 
 
+@pytest.mark.parametrize("threads", [1, 5])
+def test_c_port_equals_the_numpy_oracle(threads):
+    """oracle/zk_rt_port.c (C5's large-prefix checker and CPU baseline) against RtOracle over
+    merged_span_items: rich spans with anomalies (clustered by traceId) and a TraceGen batch."""
+    from oracle.realtime import rt_port
+    from zipkin_amd import tracegen_host
+
+    spans = gen_traces(12, 400, max_depth=5, anomalies=0.4)
+    ids: dict = {}
+    rich = to_columns(spans, ids)
+    rich = rich.take(np.argsort(rich.trace_id, kind="stable"))
+    for cols, S, p, m in ((rich, len(ids), 10, 5), (tracegen_host(9, 5000, max_depth=6, num_services=57), 57, 14, 7)):
+        o = RtOracle(S, p=p, m=m, seed=3)
+        svc, tid, dur, dropped = merged_span_items(cols, S)
+        o.accumulate_merged(svc, tid, dur)
+        r = rt_port(cols, S, p=p, m=m, seed=3, threads=threads)
+        assert np.array_equal(r.regs, o.regs) and np.array_equal(r.hist, o.hist)
+        assert r.dropped_duration == dropped and r.dropped_service == 0
+        assert np.array_equal(r.distinct(), o.distinct())
+
+
 def test_rt_handle_rejects_bad_config_without_device():
     import ctypes as C
 

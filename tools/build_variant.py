@@ -53,7 +53,7 @@ def main():
             objs = list(ex.map(cc, srcs))
         out = ROOT / "zipkin_amd" / f"libzkagg_{a.name}.so"
         subprocess.run([zb._hipcc(), f"--offload-arch={zb.ARCH}", "-shared", "-fPIC", *map(str, objs), "-L/opt/rocm/lib",
-                        "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib", "-o", str(out)], check=True)
+                        "-lrocprofiler-sdk-roctx", "-ldl", "-Wl,-rpath,/opt/rocm/lib", "-o", str(out)], check=True)
         print(out)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)

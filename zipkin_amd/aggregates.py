@@ -128,6 +128,54 @@ class Dependencies:
                             tuple(merged.values()))
 
 
+_DEP_LINK_DTYPE = np.dtype([("parent", "<u4"), ("child", "<u4"), ("m0", "<i8"), ("m1", "<f8"), ("m2", "<f8"),
+                            ("m3", "<f8"), ("m4", "<f8")])  # zk_dep_link (zkstore.h), 48 B
+
+
+class LinkList:
+    """The links of a Dependencies record kept in their compact C form (zk_dep_link[n] + the service
+    names of its ids): a tuple of DependencyLinks built only when first read, so a job over 10^5
+    (parent, child) pairs returns its record without 10^5 Python objects, and storeDependencies
+    passes the array to the store as it is."""
+
+    def __init__(self, raw: np.ndarray, names: List[str]):
+        self._raw, self._names, self._items = raw, names, None
+
+    def _all(self) -> tuple:
+        if self._items is None:
+            nm, r = self._names, self._raw
+            self._items = tuple(
+                DependencyLink(Service(nm[int(p)]), Service(nm[int(c)]), Moments(int(m0), float(a), float(b), float(x),
+                                                                                  float(y)))
+                for p, c, m0, a, b, x, y in zip(r["parent"], r["child"], r["m0"], r["m1"], r["m2"], r["m3"], r["m4"]))
+        return self._items
+
+    def __len__(self):
+        return len(self._raw)
+
+    def __iter__(self):
+        return iter(self._all())
+
+    def __getitem__(self, i):
+        return self._all()[i]
+
+    def __eq__(self, other):
+        return tuple(self._all()) == tuple(other)
+
+    def __ne__(self, other):
+        return not self == other
+
+    def __hash__(self):
+        return hash(self._all())
+
+    def __repr__(self):
+        return repr(self._all())
+
+    def compact(self):
+        """(zk_dep_link structured array, names of its ids)."""
+        return self._raw, self._names
+
+
 class Dictionary:
     """Host-owned string <-> id dictionary (service names, annotation values / keys)."""
 
@@ -248,9 +296,19 @@ class GpuAggregates(Aggregates):
 
     # -- dependencies -------------------------------------------------------------------------
     def storeDependencies(self, dependencies: Dependencies) -> None:
-        n = len(dependencies.links)
+        links = dependencies.links
+        n = len(links)
+        if isinstance(links, LinkList):  # a job's compact record: remap its ids to this store's names
+            raw, names = links.compact()
+            remap = np.array([self.services.id(x) for x in names] or [0], np.uint32)
+            arr = raw.copy()
+            arr["parent"] = remap[raw["parent"]]
+            arr["child"] = remap[raw["child"]]
+            self._check(self._L.zk_store_put_dependencies(self._h, int(dependencies.start_time),
+                                                          int(dependencies.end_time), arr.ctypes.data, n))
+            return
         arr = (_abi.zk_dep_link * max(n, 1))()
-        for i, l in enumerate(dependencies.links):
+        for i, l in enumerate(links):
             arr[i] = _abi.zk_dep_link(self.services.id(l.parent.name), self.services.id(l.child.name),
                                       _to_c(l.duration_moments))
         self._check(self._L.zk_store_put_dependencies(self._h, int(dependencies.start_time),
@@ -363,7 +421,8 @@ def cassandra_row_key(start_time_us: int) -> int:
 
 
 def links_from_table(table, services: Dictionary) -> tuple:
-    """The present cells of a finalized host LinkTable as DependencyLinks (zk_link_table_compact)."""
+    """The present cells of a finalized host LinkTable as DependencyLinks (zk_link_table_compact),
+    kept compact (LinkList) until read."""
     L = _abi.lib()
     S = table.num_services
     t = _abi.zk_link_table()
@@ -374,15 +433,11 @@ def links_from_table(table, services: Dictionary) -> tuple:
     st = L.zk_link_table_compact(C.byref(t), S, None, 0, C.byref(n))
     if st != _abi.ZK_OK:
         raise _abi.ZkError(st, _abi.status_str(st))
-    arr = (_abi.zk_dep_link * max(n.value, 1))()
-    st = L.zk_link_table_compact(C.byref(t), S, arr, n.value, C.byref(n))
+    raw = np.zeros(max(n.value, 1), _DEP_LINK_DTYPE)
+    st = L.zk_link_table_compact(C.byref(t), S, raw.ctypes.data, n.value, C.byref(n))
     if st != _abi.ZK_OK:
         raise _abi.ZkError(st, _abi.status_str(st))
-    return tuple(
-        DependencyLink(Service(services.name(arr[i].parent)), Service(services.name(arr[i].child)),
-                       _from_c(arr[i].moments))
-        for i in range(n.value)
-    )
+    return LinkList(raw[: n.value], [services.name(i) for i in range(min(S, len(services)))])
 
 
 class ZipkinAggregateJob:
