@@ -27,7 +27,7 @@
 #define ZK_K1_WGS_PER_CU 4  // resident K1 workgroups per CU (one wave per SIMD each)
 #endif
 #ifndef ZK_K1_FUSE
-#define ZK_K1_FUSE 1  // adjacent fragments of one span merged in registers before the hash (round 5)
+#define ZK_K1_FUSE 0  // 1: adjacent fragments of one span merged in registers before the hash (round 5 A/B: +6 %, profiles/r05/ab_k1_fuse.txt)
 #endif
 namespace zk {
 namespace {
@@ -71,12 +71,24 @@ __device__ __forceinline__ unsigned long long zk_memtime() {
         ZK_STAMP(8);     \
     } while (0)
 
+#ifndef ZK_K1_HASH32
+#define ZK_K1_HASH32 0
+#endif
 __device__ __forceinline__ uint32_t slot_hash(uint64_t sid, uint32_t seg) {
+#if ZK_K1_HASH32
+    // spanIds are random 64-bit words (Span.id, zipkinCore.thrift:53): fold the halves and the trace
+    // segment, one 32-bit multiply; the low bits index the table (a poor spread only lengthens probe
+    // chains, never changes a result)
+    uint32_t x = (uint32_t)sid ^ (uint32_t)(sid >> 32) ^ ((seg + 1u) * 0x9E3779B9u);
+    x *= 0x85EBCA6Bu;
+    return x ^ (x >> 15);
+#else
     uint64_t x = sid ^ ((uint64_t)(seg + 1) * 0x9E3779B97F4A7C15ull);
     x ^= x >> 33;
     x *= 0xFF51AFD7ED558CCDull;
     x ^= x >> 33;
     return (uint32_t)x;
+#endif
 }
 
 __device__ __forceinline__ uint32_t svc_key(uint32_t flags, uint32_t svc, uint32_t S, bool* range_err) {
