@@ -348,6 +348,10 @@ def main():
     if rank == 0 and world == 1 and c3 and a.cpu_sample > 0:
         # configs[2] pinned at full size: the CPU port over the WHOLE global set, bit for bit
         cpu, full = c3_full_oracle(clustered_cols, n, S, a.cpu_threads or usable_cpus(), out, st, digest)
+    elif rank == 0 and world == 1 and a.cpu_sample > 0 and shuffled:
+        # the shuffled batch as it is (any order: no prefix of it is trace-complete) through the port's
+        # hash-partitioned mode, against the GPU's table of the same batch
+        cpu, parity = shuffled_oracle(cols, n, S, a.cpu_threads or usable_cpus(), out, st)
     elif rank == 0 and world == 1 and a.cpu_sample > 0:
         cpu, parity = cpu_baseline(clustered_cols, min(a.cpu_sample, n), S, a.cpu_threads or usable_cpus(), dev)
     if c3:
@@ -426,7 +430,7 @@ def main():
                 "step_frac": n * BYTES_PER_RECORD / (elapsed / a.steps) / 1e9 / PEAK_HBM_GBS,
             },
             "cpu_baseline": cpu,
-            "parity": parity if not shuffled else {"prefix_vs_oracle": parity, "shuffled_vs_clustered": shuffled_parity},
+            "parity": parity if not shuffled else {"full_vs_oracle": parity, "shuffled_vs_clustered": shuffled_parity},
             "detail": {
                 "event_ms_per_step": ev_ms / a.steps,
                 # K1 event spans inside the timed (pipelined) steps: they also cover the other table
@@ -524,6 +528,33 @@ def c3_full_oracle(cols, n, S, threads, out, st, digest):
             "checked": "m0..m4, present and all counters of the GPU's finalized table == oracle/zk_cpu_port.c "
                        "over every record of the global set"}
     return cpu, full
+
+
+def shuffled_oracle(cols, n, S, threads, out, st):
+    """The shuffled line's parity leg and CPU baseline: the whole shuffled batch copied to the host and
+    aggregated by oracle/zk_cpu_port.c in its hash-partitioned mode (any record order; bit-identical
+    to oracle/zk_oracle.c by tests/test_cpu_port.py); its m0..m4, present and counters must equal the
+    GPU's finalized table of the same batch, else the bench fails. The port's time is the baseline."""
+    import numpy as np
+
+    from oracle import oracle
+
+    host = cols.to_host(n)
+    rp = oracle.aggregate_port(host, S, threads=threads, clustered=False)
+    m0, ms = rp.dense()
+    ref = {"m0": m0.view(np.int64), "m1": ms[0], "m2": ms[1], "m3": ms[2], "m4": ms[3],
+           "present": (m0 > 0).astype(np.uint8)}
+    bad = [k for k in ref if not np.array_equal(out[k].cpu().numpy(), ref[k])]
+    bad += [k for k, v in rp.stats.items() if k != "spilled_traces" and st[k] != v]
+    if bad:
+        raise RuntimeError(f"shuffled batch: the GPU table differs from oracle/zk_cpu_port.c: {bad}")
+    cpu = {"value": n / rp.seconds, "unit": "spans/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
+           "sample": f"the whole shuffled batch ({n} records in random order), oracle/zk_cpu_port.c hash-partitioned "
+                     f"mode, {threads} threads, one run: {rp.seconds:.2f} s"}
+    parity = {"result": "exact", "records": n, "links": int((m0 > 0).sum()),
+              "checked": "m0..m4, present and all counters of the shuffled batch's GPU table == oracle/zk_cpu_port.c "
+                         "(hash-partitioned, any order) over the whole batch"}
+    return cpu, parity
 
 
 def cpu_baseline(cols, sample, S, threads, dev):
@@ -680,6 +711,24 @@ def bench_ingest(a):
     t0 = time.perf_counter()
     hcols, _ = hd.decode(blobs)
     cpu_s = time.perf_counter() - t0
+    # parity leg: the first and the last replica of the device's decoded columns == the host decoder
+    # (zk_ingest_spans) on the same fragments, service ids compared by name (each decoder numbers its
+    # own dictionary in the order it meets the names)
+    dnames, hnames = dec.service_names(), hd.service_names()
+    bad = []
+    all_host = cols.to_host(n)
+    for rep in sorted({0, reps - 1}):
+        got = all_host.take(slice(rep * m, (rep + 1) * m))
+        for k in ("trace_id", "span_id", "parent_id", "first_ts", "last_ts", "flags"):
+            if not np.array_equal(getattr(got, k), getattr(hcols, k)):
+                bad.append(f"{k}@{rep}")
+        if [dnames[i] for i in got.service_id.tolist()] != [hnames[i] for i in hcols.service_id.tolist()]:
+            bad.append(f"service@{rep}")
+    if bad:
+        raise RuntimeError(f"ingest: device decode differs from the host decoder: {bad}")
+    parity = {"result": "exact", "fragments": 2 * m if reps > 1 else m,
+              "checked": "all 7 columns of the first and last replica (service ids by name) == the host decoder "
+                         "zk_ingest_spans on the same bytes"}
     value = n * a.steps / wall
     algo = in_bytes + n * BYTES_PER_RECORD
     achieved = algo / (ev_ms / a.steps * 1e-3) / 1e9
@@ -695,6 +744,7 @@ def bench_ingest(a):
                      "algorithmic_bytes_per_step": algo},
         "cpu_baseline": {"value": m / cpu_s, "unit": "fragments/s", "cores": 1, "kind": "port",
                          "sample": f"{m} fragments through the host decoder (zk_ingest_spans)"},
+        "parity": parity,
         "detail": {"event_ms_per_step": ev_ms / a.steps, "services": dec.num_services},
     }), flush=True)
 
