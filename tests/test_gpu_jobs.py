@@ -96,14 +96,29 @@ def test_aggregate_job_on_device_row_batches(gpu):
     parts = [view(a, b) for a, b in zip(bounds[:-1], bounds[1:])]
     job = ZipkinAggregateJob(names, clock=lambda: 10**15)
     job.run(parts, S)  # warm
-    times = []
+    times, acc_t, fin_t = [], [], []
     for _ in range(5):
         t0 = time.perf_counter()
-        deps = job.run(parts, S)
-        times.append(time.perf_counter() - t0)
+        ctx = job.accumulate_all(parts, S)
+        ctx.sync()
+        t1 = time.perf_counter()
+        table = ctx.finalize()
+        t2 = time.perf_counter()
+        deps = job._publish(table)
+        t3 = time.perf_counter()
+        times.append(t3 - t0)
+        acc_t.append(t1 - t0)
+        fin_t.append(t2 - t1)
     ms = sorted(times)[2] * 1e3
-    print(f"\nZipkinAggregateJob: {n} device records in 4 row batches: {ms:.3f} ms per run (median of 5), "
-          f"{n / ms * 1e3:.3e} spans/s")
+    print(f"\nZipkinAggregateJob: {n} device records in 4 row batches: {ms:.3f} ms per run (median of 5: "
+          f"accumulates {sorted(acc_t)[2] * 1e3:.3f} ms, finalize to host {sorted(fin_t)[2] * 1e3:.3f} ms, "
+          f"record {ms - (sorted(acc_t)[2] + sorted(fin_t)[2]) * 1e3:.3f} ms), {n / ms * 1e3:.3e} spans/s")
+    # a longer job: the same four batches twice more (the multiset of records, three times)
+    t0 = time.perf_counter()
+    job.run(parts * 3, S)
+    ms3 = (time.perf_counter() - t0) * 1e3
+    print(f"ZipkinAggregateJob: {3 * n} device records in 12 row batches: {ms3:.3f} ms, "
+          f"{ms3 / 3:.3f} ms per 1e8-record third, {3 * n / ms3 * 1e3:.3e} spans/s")
     host = cols.to_host(n)
     assert _by_name(deps) == _oracle_by_name(host, S)
     job.close()
