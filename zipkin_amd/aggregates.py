@@ -133,17 +133,36 @@ _DEP_LINK_DTYPE = np.dtype([("parent", "<u4"), ("child", "<u4"), ("m0", "<i8"), 
 
 
 class LinkList:
-    """The links of a Dependencies record kept in their compact C form (zk_dep_link[n] + the service
-    names of its ids): a tuple of DependencyLinks built only when first read, so a job over 10^5
-    (parent, child) pairs returns its record without 10^5 Python objects, and storeDependencies
-    passes the array to the store as it is."""
+    """The links of a Dependencies record kept in the job's finalized form until read: the dense
+    host table (present cells = links) and the service names of its ids. The compact zk_dep_link
+    array (zk_link_table_compact, cell order) is built on first use, the DependencyLink objects on
+    first iteration -- so a job over 10^5 (parent, child) pairs returns its record without 10^5 Python
+    objects, and storeDependencies passes the compact array to the store as it is."""
 
-    def __init__(self, raw: np.ndarray, names: List[str]):
-        self._raw, self._names, self._items = raw, names, None
+    def __init__(self, table, names: List[str]):
+        self._table, self._names = table, names
+        self._raw = self._items = None
+        self._n = int(np.count_nonzero(table.present))
+
+    def compact(self):
+        """(zk_dep_link structured array, names of its ids)."""
+        if self._raw is None:
+            t = self._table
+            ct = _abi.zk_link_table()
+            ct.m0, ct.m1, ct.m2, ct.m3, ct.m4 = (a.ctypes.data for a in (t.m0, t.m1, t.m2, t.m3, t.m4))
+            ct.present = t.present.ctypes.data
+            ct.device_ptrs = 0
+            raw = np.empty(max(self._n, 1), _DEP_LINK_DTYPE)
+            n = C.c_uint64()
+            st = _abi.lib().zk_link_table_compact(C.byref(ct), t.num_services, raw.ctypes.data, self._n, C.byref(n))
+            if st != _abi.ZK_OK:
+                raise _abi.ZkError(st, _abi.status_str(st))
+            self._raw = raw[: n.value]
+        return self._raw, self._names
 
     def _all(self) -> tuple:
         if self._items is None:
-            nm, r = self._names, self._raw
+            nm, r = self._names, self.compact()[0]
             self._items = tuple(
                 DependencyLink(Service(nm[int(p)]), Service(nm[int(c)]), Moments(int(m0), float(a), float(b), float(x),
                                                                                   float(y)))
@@ -151,7 +170,7 @@ class LinkList:
         return self._items
 
     def __len__(self):
-        return len(self._raw)
+        return self._n
 
     def __iter__(self):
         return iter(self._all())
@@ -170,10 +189,6 @@ class LinkList:
 
     def __repr__(self):
         return repr(self._all())
-
-    def compact(self):
-        """(zk_dep_link structured array, names of its ids)."""
-        return self._raw, self._names
 
 
 class Dictionary:
@@ -420,24 +435,10 @@ def cassandra_row_key(start_time_us: int) -> int:
     return int(_abi.lib().zk_dependencies_row_key(int(start_time_us)))
 
 
-def links_from_table(table, services: Dictionary) -> tuple:
+def links_from_table(table, services: Dictionary) -> "LinkList":
     """The present cells of a finalized host LinkTable as DependencyLinks (zk_link_table_compact),
-    kept compact (LinkList) until read."""
-    L = _abi.lib()
-    S = table.num_services
-    t = _abi.zk_link_table()
-    t.m0, t.m1, t.m2, t.m3, t.m4 = (a.ctypes.data for a in (table.m0, table.m1, table.m2, table.m3, table.m4))
-    t.present = table.present.ctypes.data
-    t.device_ptrs = 0
-    n = C.c_uint64()
-    st = L.zk_link_table_compact(C.byref(t), S, None, 0, C.byref(n))
-    if st != _abi.ZK_OK:
-        raise _abi.ZkError(st, _abi.status_str(st))
-    raw = np.zeros(max(n.value, 1), _DEP_LINK_DTYPE)
-    st = L.zk_link_table_compact(C.byref(t), S, raw.ctypes.data, n.value, C.byref(n))
-    if st != _abi.ZK_OK:
-        raise _abi.ZkError(st, _abi.status_str(st))
-    return LinkList(raw[: n.value], [services.name(i) for i in range(min(S, len(services)))])
+    kept in the table's form (LinkList) until read."""
+    return LinkList(table, [services.name(i) for i in range(min(table.num_services, len(services)))])
 
 
 class ZipkinAggregateJob:

@@ -148,9 +148,9 @@ class DepsContext:
             t.device_ptrs = 1
             self._check(self._L.zk_deps_finalize(self._h, C.byref(t)))
             return None
-        m0 = np.zeros(cells, np.uint64)
-        ms = [np.zeros(cells, np.float64) for _ in range(4)]
-        pr = np.zeros(cells, np.uint8)
+        m0 = np.empty(cells, np.uint64)  # (finalize writes every cell)
+        ms = [np.empty(cells, np.float64) for _ in range(4)]
+        pr = np.empty(cells, np.uint8)
         t.m0 = m0.ctypes.data
         t.m1, t.m2, t.m3, t.m4 = (a.ctypes.data for a in ms)
         t.present = pr.ctypes.data

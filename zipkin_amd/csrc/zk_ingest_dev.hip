@@ -979,121 +979,6 @@ __device__ __forceinline__ bool snappy_inplace(lds_u8* out, uint64_t D, uint64_t
     return o == len;
 }
 
-#ifndef ZK_ING_SNAPPY2
-#define ZK_ING_SNAPPY2 0  // 1: copies batched per 32 bytes, one round trip per tag header (round-5 A/B)
-#endif
-#if ZK_ING_SNAPPY2
-// n (1..32) bytes from src to dst in LDS, with dst <= src or the ranges apart: the source is read
-// as aligned dwords in ONE round trip (every read issued before any write), the destination written
-// as aligned dwords with byte writes at its unaligned head and tail. Register indices are all
-// compile-time (the tail dword is picked by selects), so nothing spills to scratch.
-__device__ __forceinline__ void lds_copy32(lds_u8* dst, const lds_u8* src, uint32_t n) {
-    const uint32_t sa = (uint32_t)(uintptr_t)src, da = (uint32_t)(uintptr_t)dst;
-    const lds_u32* sw = (const lds_u32*)(uintptr_t)(sa & ~3u);
-    const uint32_t ss = sa & 3u;
-    const uint32_t nw = (ss + n + 3) >> 2;  // dwords that hold the source, 1..9
-    uint32_t w[10];
-#pragma unroll
-    for (int j = 0; j < 10; ++j) w[j] = sw[(uint32_t)j < nw ? j : nw - 1];
-    const uint32_t hd = (4u - (da & 3u)) & 3u;
-    const uint32_t h = hd < n ? hd : n;      // head bytes up to dst's alignment
-    const uint32_t m = (n - h) >> 2;         // whole dwords after the head
-    const uint32_t t = (n - h) & 3u;         // tail bytes
-    const uint32_t q = (ss + h) >> 2, s2 = (ss + h) & 3u;  // q is 0 or 1
-    // head: source bytes 0..h-1 at stream position ss + k
-    const uint32_t w01 = __builtin_amdgcn_alignbyte(w[1], w[0], ss);  // source bytes 0..3
-#pragma unroll
-    for (uint32_t k = 0; k < 3; ++k)
-        if (k < h) dst[k] = (uint8_t)(w01 >> (8 * k));
-    lds_u32* dw = (lds_u32*)(uintptr_t)(da + h);
-    uint32_t tv = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) {
-        const uint32_t v = q ? __builtin_amdgcn_alignbyte(w[k + 2], w[k + 1], s2) : __builtin_amdgcn_alignbyte(w[k + 1], w[k], s2);
-        if (k < m) dw[k] = v;
-        tv = k == m ? v : tv;
-    }
-    lds_u8* tb = dst + h + 4 * m;
-#pragma unroll
-    for (uint32_t k = 0; k < 3; ++k)
-        if (k < t) tb[k] = (uint8_t)(tv >> (8 * k));
-}
-
-// l bytes from src to dst (dst <= src, or the ranges apart), 32 at a time
-__device__ __forceinline__ void lds_copy(lds_u8* dst, const lds_u8* src, uint64_t l) {
-    for (uint64_t k = 0; k < l; k += 32) lds_copy32(dst + k, src + k, (uint32_t)(l - k < 32 ? l - k : 32));
-}
-
-// Snappy back-reference of l bytes at distance off: pieces that never read what they write (the
-// first `off` bytes, then the repeated pattern at distance off, 2 off, 4 off, ...)
-__device__ __forceinline__ void lds_backref(lds_u8* out, uint64_t o, uint64_t off, uint64_t l) {
-    uint64_t done = 0, dist = off;
-    while (done < l) {
-        const uint64_t c = l - done < dist ? l - done : dist;
-        lds_copy(out + o + done, out + o + done - dist, c);
-        done += c;
-        dist += c;
-    }
-}
-
-// snappy_inplace with the header and tag bytes of a step read in one round trip and the copies
-// above; the same checks and the same output
-__device__ __forceinline__ bool snappy_inplace2(lds_u8* out, uint64_t D, uint64_t n, uint64_t len, bool* unsafe) {
-    const lds_u8* in = out + D;
-    uint64_t dl, hdr;
-    if (!snappy_hdr(in, n, &dl, &hdr) || dl != len) return false;
-    uint64_t o = 0, i = hdr;
-    while (i < n) {
-        const uint64_t x = ld_u64(in + i);  // the tag and up to 7 following bytes (the region has slack)
-        const uint32_t tag = (uint32_t)x & 0xFFu;
-        const uint32_t kind = tag & 3u;
-        uint64_t l, off = 0, step;
-        if (kind == 0) {
-            l = tag >> 2;
-            step = 1;
-            if (l >= 60) {
-                const uint32_t nb = (uint32_t)l - 59;  // 1..4 length bytes
-                l = (x >> 8) & (nb == 4 ? 0xFFFFFFFFull : ((1ull << (8 * nb)) - 1ull));
-                step += nb;
-            }
-            l += 1;
-            if (i + step + l > n || o + l > len) return false;
-            if (o > D + i + step) {  // the output would pass the input still to be read
-                *unsafe = true;
-                return false;
-            }
-            lds_copy(out + o, in + i + step, l);
-            i += step + l;
-            o += l;
-            continue;
-        }
-        if (kind == 1) {
-            l = ((tag >> 2) & 7u) + 4;
-            off = ((uint64_t)(tag >> 5) << 8) | ((x >> 8) & 0xFFu);
-            step = 2;
-        } else if (kind == 2) {
-            l = (tag >> 2) + 1;
-            off = (x >> 8) & 0xFFFFu;
-            step = 3;
-        } else {
-            l = (tag >> 2) + 1;
-            off = (x >> 8) & 0xFFFFFFFFull;
-            step = 5;
-        }
-        if (i + step > n) return false;
-        i += step;
-        if (off == 0 || off > o || o + l > len) return false;
-        if (o + l > D + i) {  // the copy would reach the next unread input byte
-            *unsafe = true;
-            return false;
-        }
-        lds_backref(out, o, off, l);
-        o += l;
-    }
-    return o == len;
-}
-#endif
-
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -1212,11 +1097,7 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                 uint64_t len = clen;
                 bool ok = true, unsafe = false;
                 if (a.snappy) {
-#if ZK_ING_SNAPPY2
-                    ok = snappy_inplace2(lreg + skew, D - skew, clen, raw, &unsafe);
-#else
                     ok = snappy_inplace(lreg + skew, D - skew, clen, raw, &unsafe);
-#endif
                     src = lreg + skew;
                     len = raw;
                 }
