@@ -26,9 +26,6 @@
 #ifndef ZK_K1_WGS_PER_CU
 #define ZK_K1_WGS_PER_CU 4  // resident K1 workgroups per CU (one wave per SIMD each)
 #endif
-#ifndef ZK_K1_FUSE
-#define ZK_K1_FUSE 0  // 1: adjacent fragments of one span merged in registers before the hash (round 5 A/B: +6 %, profiles/r05/ab_k1_fuse.txt)
-#endif
 namespace zk {
 namespace {
 
@@ -71,24 +68,12 @@ __device__ __forceinline__ unsigned long long zk_memtime() {
         ZK_STAMP(8);     \
     } while (0)
 
-#ifndef ZK_K1_HASH32
-#define ZK_K1_HASH32 0
-#endif
 __device__ __forceinline__ uint32_t slot_hash(uint64_t sid, uint32_t seg) {
-#if ZK_K1_HASH32
-    // spanIds are random 64-bit words (Span.id, zipkinCore.thrift:53): fold the halves and the trace
-    // segment, one 32-bit multiply; the low bits index the table (a poor spread only lengthens probe
-    // chains, never changes a result)
-    uint32_t x = (uint32_t)sid ^ (uint32_t)(sid >> 32) ^ ((seg + 1u) * 0x9E3779B9u);
-    x *= 0x85EBCA6Bu;
-    return x ^ (x >> 15);
-#else
     uint64_t x = sid ^ ((uint64_t)(seg + 1) * 0x9E3779B97F4A7C15ull);
     x ^= x >> 33;
     x *= 0xFF51AFD7ED558CCDull;
     x ^= x >> 33;
     return (uint32_t)x;
-#endif
 }
 
 __device__ __forceinline__ uint32_t svc_key(uint32_t flags, uint32_t svc, uint32_t S, bool* range_err) {
@@ -146,9 +131,8 @@ __device__ __forceinline__ void emit_link(uint64_t* __restrict__ table, uint32_t
     add_chunk(c + kLimbS4 + 4, w2);
 }
 
-// packed per-thread stat counters of K1: 4 x 16-bit fields per u64 (a thread adds <= 3 per stat per
-// window -- its two records and a fragment one of them absorbed; folded every kFoldWindows = 256
-// windows, so a wave sum of 64 lanes stays below 3 x 64 x 256 < 2^16)
+// packed per-thread stat counters of K1: 4 x 16-bit fields per u64 (a thread adds <= 2 per stat per
+// window; folded every kFoldWindows windows, so a wave sum of 64 lanes stays below 2^16)
 struct StatPack {
     uint64_t w[4] = {0, 0, 0, 0};
     __device__ __forceinline__ void inc(int s, uint32_t v = 1) { w[s >> 2] += (uint64_t)v << (16 * (s & 3)); }
@@ -236,7 +220,7 @@ __device__ __forceinline__ void ld2_u32(const uint32_t* __restrict__ p, uint64_t
 }
 
 // K1 stat counters: the per-thread 16-bit pack (StatPack) is folded into the workgroup's u32 LDS
-// totals every kFoldWindows windows (a lane adds <= 3 per stat per window, so a wave sum of 64
+// totals every kFoldWindows windows (a lane adds <= 2 per stat per window, so a wave sum of 64
 // lanes stays below 2^16), and the totals go to a sharded global slot once at the end.
 constexpr int kFoldWindows = 256;
 
@@ -290,22 +274,6 @@ __device__ __forceinline__ uint64_t lane_shr1(uint64_t v) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x138, 0xF, 0xF, false);
     return ((uint64_t)hi << 32) | lo;
 }
-// lane l+1's value (wave_shl:1 DPP); lane 63 gets 0
-__device__ __forceinline__ uint32_t lane_shl1_u32(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
-}
-__device__ __forceinline__ uint64_t lane_shl1(uint64_t v) {
-    return ((uint64_t)lane_shl1_u32((uint32_t)(v >> 32)) << 32) | lane_shl1_u32((uint32_t)v);
-}
-__device__ __forceinline__ uint32_t lane_shr1_u32(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
-}
-// slot bits of two fragments of one span merged: ">= 1" = A0 | A1, ">= 2" = B0 | B1 | (A0 & A1),
-// parent presence ORed (the same bits the second fragment's atomicOr + promotion would leave)
-__device__ __forceinline__ uint32_t fuse_bits(uint32_t b0, uint32_t b1) {
-    return b0 | b1 | (((b0 & b1) >> kSlotA & 0xFu) << kSlotB);
-}
-__device__ __forceinline__ uint32_t bits_once(uint32_t b) { return (b >> kSlotA) & ~(b >> kSlotB) & 0xFu; }
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {  // set bits of m in lanes < this lane
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -548,15 +516,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         int r_seg[2];
         uint32_t r_svck[2];
         bool r_rerr[2];
-#if ZK_K1_FUSE
-        bool r_abs[2];                  // the record merged into the record before it (no hash entry)
-        uint32_t r_fb[2], r_once[2];    // slot bits (merged for a pair's first record)
-        uint32_t r_msvc[2];             // service key after the pair merge
-        uint64_t r_ppid = ~0ull;        // the absorbed partner's parentId, its service key, whether it has a parent
-        uint32_t r_psvc = kSvcNone;
-        bool r_php = false;
-        int r_part = 0;                 // 1: record 0 absorbed record 1; 2: record 1 absorbed lane t+1's record 0
-#endif
         {
             const int j0 = 2 * tid;
             // last boundary <= j0 among this wave's records, else the one before the wave (it exists
@@ -578,71 +537,11 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 v_last[e] = ha ? cur.last[e] : (uint64_t)LLONG_MIN;
                 v_pid[e] = (f & ZK_F_HAS_PARENT) ? cur.pid[e] : ~0ull;
             }
-#if ZK_K1_FUSE
-            // A span's fragments are adjacent in a Cassandra row read (the column name starts with the
-            // span id, CassieSpanStore.scala:76-77; TraceGen writes each callee's server fragment right
-            // before its client fragment): a fragment equal in (segment, spanId) to the record before
-            // it is merged into that record in registers, and only the pair's first record enters the
-            // hash -- with the pair's merged values and slot bits, exactly what the second fragment's
-            // CAS hit and merge atomics would have left. Pairs inside a thread (j0, j1) and across
-            // lanes (lane t-1's j1, lane t's j0, by DPP) fuse; a third adjacent fragment, and any
-            // fragment that is not adjacent, takes the hash path as before.
-            {
-                const uint32_t fb0 = frag_bits(cur.flags[0], &r_once[0]), fb1 = frag_bits(cur.flags[1], &r_once[1]);
-                r_fb[0] = fb0;
-                r_fb[1] = fb1;
-                const bool same_a = r_seg[0] >= 0 && r_seg[1] == r_seg[0] && cur.sid[1] == cur.sid[0];
-                const uint64_t psid = lane_shr1(cur.sid[1]);
-                const int pseg = (int)lane_shr1_u32((uint32_t)r_seg[1]);
-                const bool same_prev = lane > 0 && r_seg[0] >= 0 && pseg == r_seg[0] && psid == cur.sid[0];
-                const bool fuse_a = same_a && !same_prev;
-                const bool prev_fuse_a = lane_shr1_u32(fuse_a ? 1u : 0u) != 0u;
-                r_abs[0] = same_prev && !prev_fuse_a;  // j0 merges into lane t-1's j1
-                r_abs[1] = fuse_a;                     // j1 merges into j0
-                // lane t+1's j0 for this lane's j1
-                const bool nb = lane_shl1_u32(r_abs[0] ? 1u : 0u) != 0u && lane < 63;
-                const uint64_t nb_first = lane_shl1(v_first[0]), nb_last = lane_shl1(v_last[0]);
-                const uint64_t nb_pid = lane_shl1(v_pid[0]);
-                const uint32_t nb_svck = lane_shl1_u32(r_svck[0]), nb_fb = lane_shl1_u32(fb0);
-                const bool nb_hp = (lane_shl1_u32(cur.flags[0]) & ZK_F_HAS_PARENT) != 0u;
-                if (fuse_a) {
-                    v_first[0] = (long long)v_first[1] < (long long)v_first[0] ? v_first[1] : v_first[0];
-                    v_last[0] = (long long)v_last[1] > (long long)v_last[0] ? v_last[1] : v_last[0];
-                    v_pid[0] = v_pid[1] < v_pid[0] ? v_pid[1] : v_pid[0];
-                    r_msvc[0] = r_svck[1] < r_svck[0] ? r_svck[1] : r_svck[0];
-                    r_fb[0] = fuse_bits(fb0, fb1);
-                    r_once[0] = bits_once(r_fb[0]);
-                    // the absorbed record's own values, for its ambiguity check against the span
-                    r_ppid = v_pid[1];
-                    r_psvc = r_svck[1];
-                    r_php = (cur.flags[1] & ZK_F_HAS_PARENT) != 0u;
-                } else {
-                    r_msvc[0] = r_svck[0];
-                }
-                r_msvc[1] = r_svck[1];
-                if (nb) {
-                    v_first[1] = (long long)nb_first < (long long)v_first[1] ? nb_first : v_first[1];
-                    v_last[1] = (long long)nb_last > (long long)v_last[1] ? nb_last : v_last[1];
-                    r_ppid = nb_pid;
-                    r_psvc = nb_svck;
-                    r_php = nb_hp;
-                    v_pid[1] = nb_pid < v_pid[1] ? nb_pid : v_pid[1];
-                    r_msvc[1] = nb_svck < r_svck[1] ? nb_svck : r_svck[1];
-                    r_fb[1] = fuse_bits(fb1, nb_fb);
-                    r_once[1] = bits_once(r_fb[1]);
-                }
-                r_part = fuse_a ? 1 : nb ? 2 : 0;  // which of this thread's records absorbed a partner
-            }
-#endif
             *reinterpret_cast<ulonglong2*>(&s_sid[j0]) = make_ulonglong2(cur.sid[0], cur.sid[1]);
             *reinterpret_cast<ulonglong2*>(&s_first[j0]) = make_ulonglong2(v_first[0], v_first[1]);
             *reinterpret_cast<ulonglong2*>(&s_last[j0]) = make_ulonglong2(v_last[0], v_last[1]);
             *reinterpret_cast<ulonglong2*>(&s_pid[j0]) = make_ulonglong2(v_pid[0], v_pid[1]);
-#if ZK_K1_FUSE
-            *reinterpret_cast<uint2*>(&s_svck[j0]) = make_uint2(r_msvc[0], r_msvc[1]);
-#else
             *reinterpret_cast<uint2*>(&s_svck[j0]) = make_uint2(r_svck[0], r_svck[1]);
-#endif
         }
         ZK_PHASE_SYNC(2);  // (the hash table is empty here: cleared once, then by its leaders)
 
@@ -657,15 +556,10 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             for (int e = 0; e < 2; ++e) {
                 r_leader[e] = -1;
                 r_slot[e] = slot_hash(cur.sid[e], (uint32_t)(r_seg[e] & 0xFFFF)) & (H - 1);
-#if ZK_K1_FUSE
-                act[e] = r_seg[e] >= 0 && !r_abs[e];
-                word[e] = (uint32_t)(2 * tid + e + 1) | r_fb[e] | (((uint32_t)r_seg[e] & 0x1FFu) << kSlotSegShift);
-#else
                 act[e] = r_seg[e] >= 0;
                 uint32_t once;
                 word[e] = (uint32_t)(2 * tid + e + 1) | frag_bits(cur.flags[e], &once) |
                           (((uint32_t)r_seg[e] & 0x1FFu) << kSlotSegShift);
-#endif
             }
             while (act[0] || act[1]) {
                 uint32_t old[2];
@@ -710,15 +604,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             const int j = 2 * tid + e;
             const int L = r_leader[e];
             if (L >= 0 && L != j) {
-#if ZK_K1_FUSE
-                // (rare once adjacent fragments fuse: a fragment that is not next to its span's leader)
-                // the record's staged values are the pair's merged ones; sentinels are no-ops
-                atomicMin(&s_first[L], s_first[j]);
-                atomicMax(&s_last[L], s_last[j]);
-                atomicMin(&s_svck[L], s_svck[j]);
-                atomicMin((unsigned long long*)&s_pid[L], (unsigned long long)s_pid[j]);
-                const uint32_t bits = r_fb[e], once = r_once[e];
-#else
                 const uint32_t f = cur.flags[e];
                 if (f & ZK_F_HAS_ANNOTATIONS) {
                     atomicMin(&s_first[L], (long long)cur.first[e]);
@@ -728,7 +613,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
                 if (f & ZK_F_HAS_PARENT) atomicMin((unsigned long long*)&s_pid[L], (unsigned long long)cur.pid[e]);
                 uint32_t once;
                 const uint32_t bits = frag_bits(f, &once);
-#endif
                 uint32_t* const wp = &s_ht[r_slot[e]];
                 const uint32_t old = atomicOr(wp, bits);
                 const uint32_t promote = once & (old >> kSlotA) & 0xFu;  // second occurrence
@@ -748,14 +632,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             r_item[e] = ~0ull;
             r_isvc[e] = 0u;
             const int L = r_leader[e];
-#if ZK_K1_FUSE
-            if (L < 0) {
-                if (r_abs[e] && r_rerr[e]) st.inc(ST_SVC_RANGE);  // (an absorbed record's range error)
-                continue;
-            }
-#else
             if (L < 0) continue;
-#endif
             const int j = 2 * tid + e;
             const uint32_t f = cur.flags[e];
             const uint32_t w = s_ht[r_slot[e]];
@@ -766,13 +643,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             if (sk != kSvcNone && (sk >> kSvcKindShift) == (sL >> kSvcKindShift) && sk != sL) amb = true;
             if (amb) st.inc(ST_AMBIGUOUS);
             if (r_rerr[e]) st.inc(ST_SVC_RANGE);
-#if ZK_K1_FUSE
-            if (r_part == e + 1) {  // the fragment this record absorbed, checked against the same span
-                bool pamb = r_php ? (r_ppid != pL) : ((w & kSlotP1) != 0u);
-                if (r_psvc != kSvcNone && (r_psvc >> kSvcKindShift) == (sL >> kSvcKindShift) && r_psvc != sL) pamb = true;
-                if (pamb) st.inc(ST_AMBIGUOUS);
-            }
-#endif
             if (L != j) continue;
             st.inc(ST_MERGED);
             const bool valid = slot_valid(w);
