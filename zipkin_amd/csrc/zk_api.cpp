@@ -80,13 +80,13 @@ struct zk_ctx {
     uint64_t tset_slots = 0;
     uint64_t tset_records = 0;
     // ZK_BATCH_CONTINUES: the held-back last trace of the batches so far (7 aligned columns of
-    // carry_cap records), its traceId and the batch flags it arrived with
+    // carry_cap records) and its state, both on the device and decided there (zk_cluster.h
+    // CarryState): a batch costs the host no round trip
     uint8_t* carry = nullptr;
-    uint64_t carry_cap = 0, carry_n = 0, carry_tid = 0;
-    uint32_t carry_flags = 0;
-    bool carry_dropped = false;           // the held trace was dropped: skip the rest of it too
-    unsigned long long* edge = nullptr;   // device: the edge-run indices (k_edge_runs)
-    uint64_t* h_edge = nullptr;           // pinned: e0, e1, first and last traceId of the batch
+    uint64_t carry_cap = 0;
+    CarryState* cs = nullptr;
+    bool maybe_carry = false;             // a CONTINUES batch since the last flush: the carry may hold records
+    bool any_verify = false;              // a batch since the reset asked for ZK_BATCH_VERIFY_TRACES
     std::string err;
     // bound realtime sketch (zk_rt_bind)
     zk_rt* rt = nullptr;
@@ -285,12 +285,11 @@ uint64_t pow2_at_least(uint64_t x) {
     return p;
 }
 
-// ZK_BATCH_VERIFY_TRACES: grow the traceId set (load <= 1/2 even if every record were its own
-// trace) and insert the batch's trace runs
-zk_status verify_batch(zk_ctx* c, const SpanColsDev& d) {
-    RoctxRange rr("zk_verify_traces");
-    const uint64_t need = pow2_at_least(2 * (c->tset_records + d.n) > (1ull << 16) ? 2 * (c->tset_records + d.n)
-                                                                                   : (1ull << 16));
+// ZK_BATCH_VERIFY_TRACES: grow the traceId set for `more` records (load <= 1/2 even if every record
+// were its own trace)
+zk_status ensure_tset(zk_ctx* c, uint64_t more) {
+    const uint64_t need = pow2_at_least(2 * (c->tset_records + more) > (1ull << 16) ? 2 * (c->tset_records + more)
+                                                                                    : (1ull << 16));
     if (need > c->tset_slots) {
         uint64_t* nt = nullptr;
         if (hipMalloc(&nt, (need + 1) * 8) != hipSuccess) {
@@ -312,9 +311,17 @@ zk_status verify_batch(zk_ctx* c, const SpanColsDev& d) {
         c->tset = nt;
         c->tset_slots = need;
     }
+    c->tset_records += more;
+    return ZK_OK;
+}
+
+// ... and insert the batch's trace runs
+zk_status verify_batch(zk_ctx* c, const SpanColsDev& d) {
+    RoctxRange rr("zk_verify_traces");
+    const zk_status st = ensure_tset(c, d.n);
+    if (st != ZK_OK) return st;
     ZK_HIP(c, launch_trace_set_insert(d.trace_id, d.n, c->tset, c->tset_slots, &c->stats[ST_NOT_CLUSTERED],
                                       c->stream));
-    c->tset_records += d.n;
     return ZK_OK;
 }
 
@@ -425,8 +432,7 @@ zk_status zk_ctx_destroy(zk_ctx* c) {
     hipFree(c->tset);
     hipFree(c->xchg);
     hipFree(c->carry);
-    hipFree(c->edge);
-    if (c->h_edge) hipHostFree(c->h_edge);
+    hipFree(c->cs);
     for (auto* v : {&c->ev_free, &c->ev_join, &c->ev_reduce, &c->ev_spill, &c->ev_fin, &c->ev_cluster})
         for (auto& p : *v) {
             hipEventDestroy(p.a);
@@ -444,6 +450,40 @@ zk_status zk_ctx_sync(zk_ctx* c) {
     return ZK_OK;
 }
 
+// the device-side continuation's batch range for K1 (zk_cluster.h CarryState)
+struct DevRange {
+    const uint32_t* skip_dev;
+    const unsigned long long* n_dev;
+};
+static zk_status accumulate_dev(zk_ctx* c, SpanColsDev d, uint32_t flags, uint32_t skip,
+                                const DevRange* dr = nullptr);
+static zk_status continue_batch(zk_ctx* c, const SpanColsDev& d, uint32_t flags);
+static zk_status flush_carry(zk_ctx* c);
+#define ZK_ST(call)                        \
+    do {                                   \
+        const zk_status _s = (call);       \
+        if (_s != ZK_OK) return _s;        \
+    } while (0)
+
+// the carry state of a fresh job: nothing held, the edge slots ready for k_edge_runs
+static zk_status carry_state_reset(zk_ctx* c) {
+    ZK_HIP(c, hipMemsetAsync(c->cs, 0, sizeof(CarryState), c->stream));
+    ZK_HIP(c, hipMemsetAsync(&c->cs->edge[0], 0xFF, 8, c->stream));
+    return ZK_OK;
+}
+
+static zk_status ensure_carry(zk_ctx* c) {
+    if (!c->carry) {
+        c->carry_cap = (uint64_t)c->max_trace + 2;  // a held run has <= max_trace + 1 records
+        ZK_HIP(c, hipMalloc(&c->carry, carved_bytes(c->carry_cap)));
+    }
+    if (!c->cs) {
+        ZK_HIP(c, hipMalloc(&c->cs, sizeof(CarryState)));
+        ZK_ST(carry_state_reset(c));
+    }
+    return ZK_OK;
+}
+
 zk_status zk_deps_reset(zk_ctx* c) {
     if (!c) return ZK_ERR_INVALID_ARG;
     ZK_HIP(c, hipSetDevice(c->device));
@@ -455,128 +495,13 @@ zk_status zk_deps_reset(zk_ctx* c) {
     c->merged = false;
     c->continued = false;
     c->folded = false;
-    c->carry_n = 0;  // a held-back trace belongs to the job being reset
-    c->carry_dropped = false;
+    // a held-back trace belongs to the job being reset
+    c->maybe_carry = false;
+    c->any_verify = false;
+    if (c->cs) ZK_ST(carry_state_reset(c));
     return ZK_OK;
 }
 
-static zk_status accumulate_dev(zk_ctx* c, SpanColsDev d, uint32_t flags, uint32_t skip);
-static zk_status continue_batch(zk_ctx* c, const SpanColsDev& d, uint32_t flags);
-static zk_status flush_carry(zk_ctx* c);
-#define ZK_ST(call)                        \
-    do {                                   \
-        const zk_status _s = (call);       \
-        if (_s != ZK_OK) return _s;        \
-    } while (0)
-
-// append records [lo, hi) of a device batch to the carried trace
-static zk_status carry_append(zk_ctx* c, const SpanColsDev& d, uint64_t lo, uint64_t hi) {
-    if (!c->carry) {
-        c->carry_cap = (uint64_t)c->max_trace + 2;
-        ZK_HIP(c, hipMalloc(&c->carry, carved_bytes(c->carry_cap)));
-    }
-    const SpanColsMut m = carve_cols(c->carry, c->carry_cap);
-    const uint64_t k = hi - lo, at = c->carry_n;
-    ZK_HIP(c, hipMemcpyAsync(m.trace_id + at, d.trace_id + lo, k * 8, hipMemcpyDeviceToDevice, c->stream));
-    ZK_HIP(c, hipMemcpyAsync(m.span_id + at, d.span_id + lo, k * 8, hipMemcpyDeviceToDevice, c->stream));
-    ZK_HIP(c, hipMemcpyAsync(m.parent_id + at, d.parent_id + lo, k * 8, hipMemcpyDeviceToDevice, c->stream));
-    ZK_HIP(c, hipMemcpyAsync(m.first_ts + at, d.first_ts + lo, k * 8, hipMemcpyDeviceToDevice, c->stream));
-    ZK_HIP(c, hipMemcpyAsync(m.last_ts + at, d.last_ts + lo, k * 8, hipMemcpyDeviceToDevice, c->stream));
-    ZK_HIP(c, hipMemcpyAsync(m.service_id + at, d.service_id + lo, k * 4, hipMemcpyDeviceToDevice, c->stream));
-    ZK_HIP(c, hipMemcpyAsync(m.flags + at, d.flags + lo, k * 4, hipMemcpyDeviceToDevice, c->stream));
-    c->carry_n += k;
-    return ZK_OK;
-}
-
-// the held-back trace is complete: aggregate it as a batch of its own
-static zk_status flush_carry(zk_ctx* c) {
-    if (!c->carry_n) return ZK_OK;
-    // (zk_deps_accumulate admits a batch with the held records counted, so this holds; checked again
-    // because the exchange limbs' headroom for 256 ranks rests on the 2^32 bound, zk_exchange.hip)
-    if (c->records_since_reset + c->carry_n > kMaxRecordsSinceReset)
-        return fail(c, ZK_ERR_CAPACITY, "more than 2^32-1 records since reset");
-    const SpanColsMut m = carve_cols(c->carry, c->carry_cap);
-    const SpanColsDev d{m.trace_id, m.span_id, m.parent_id, m.first_ts, m.last_ts, m.service_id, m.flags, c->carry_n};
-    c->carry_n = 0;
-    return accumulate_dev(c, d, ZK_BATCH_DEVICE_PTRS | ZK_BATCH_TRACE_CLUSTERED | (c->carry_flags & ZK_BATCH_VERIFY_TRACES),
-                          0);
-}
-
-// A clustered batch when a trace is held back or the batch's last trace may continue: the batch's
-// leading run joins the held trace if it carries the same traceId; the held trace is aggregated once
-// the batch moves on to another trace (or the batch does not continue); with ZK_BATCH_CONTINUES the
-// batch's last run is held back for the next call. The rest of the batch goes through accumulate_dev
-// in place (from an even record, skipping the one record before it, so its columns stay aligned).
-static zk_status continue_batch(zk_ctx* c, const SpanColsDev& d, uint32_t flags) {
-    const uint64_t n = d.n, L = c->max_trace;
-    if (!c->edge) {
-        ZK_HIP(c, hipMalloc(&c->edge, 16));
-        ZK_HIP(c, hipHostMalloc((void**)&c->h_edge, 32, hipHostMallocDefault));
-    }
-    ZK_HIP(c, hipMemsetAsync(c->edge, 0xFF, 8, c->stream));
-    ZK_HIP(c, hipMemsetAsync(c->edge + 1, 0, 8, c->stream));
-    ZK_HIP(c, launch_edge_runs(d.trace_id, n, L, c->edge, c->stream));
-    ZK_HIP(c, hipMemcpyAsync(c->h_edge, c->edge, 16, hipMemcpyDeviceToHost, c->stream));
-    ZK_HIP(c, hipMemcpyAsync(c->h_edge + 2, d.trace_id, 8, hipMemcpyDeviceToHost, c->stream));
-    ZK_HIP(c, hipMemcpyAsync(c->h_edge + 3, d.trace_id + (n - 1), 8, hipMemcpyDeviceToHost, c->stream));
-    ZK_HIP(c, hipStreamSynchronize(c->stream));
-    const uint64_t e0 = c->h_edge[0], e1 = c->h_edge[1], first_tid = c->h_edge[2];
-    // end of the first run (n + 1: longer than a trace may be), start of the last run (n + 1: unknown)
-    const uint64_t first_end = e0 != ~0ull ? e0 : (n <= L + 1 ? n : n + 1);
-    const uint64_t last_start = e1 != 0 ? e1 : (n <= L + 1 ? 0 : n + 1);
-    uint64_t lead = 0;
-    if (c->carry_n || c->carry_dropped) {
-        if (first_tid == c->carry_tid) {
-            lead = first_end;
-            if (lead > n) {
-                // the leading run is longer than max_trace_records: find where it really ends (rare)
-                ZK_HIP(c, hipMemsetAsync(c->edge, 0xFF, 8, c->stream));
-                ZK_HIP(c, launch_edge_runs(d.trace_id, n, n, c->edge, c->stream));
-                ZK_HIP(c, hipMemcpyAsync(c->h_edge, c->edge, 8, hipMemcpyDeviceToHost, c->stream));
-                ZK_HIP(c, hipStreamSynchronize(c->stream));
-                lead = c->h_edge[0] != ~0ull ? c->h_edge[0] : n;
-            }
-            if (c->carry_dropped) {
-                // the rest of a trace already found too long: skipped like its beginning
-            } else if (c->carry_n + lead > L) {
-                // longer than max_trace_records: not aggregated, like any trace that long
-                c->carry_n = 0;
-                c->carry_dropped = true;
-                // counted on the device, in the stats shards that zk_deps_partial folds into the
-                // exchange tail, so every rank of a sharded job sees it (zkagg.h: same status)
-                ZK_HIP(c, launch_stat_add(c->stats + ST_TOO_LARGE, 1, c->stream));
-            } else {
-                ZK_ST(carry_append(c, d, 0, lead));
-            }
-        }
-        c->carry_flags |= flags & ZK_BATCH_VERIFY_TRACES;
-        if (lead == n && (flags & ZK_BATCH_CONTINUES)) return ZK_OK;  // the whole batch continues the held trace
-        c->carry_dropped = false;
-        ZK_ST(flush_carry(c));
-    }
-    uint64_t hi = n;
-    if (flags & ZK_BATCH_CONTINUES) {
-        const uint64_t ls = last_start > lead ? last_start : lead;
-        if (ls < n) {  // (a last run longer than max_trace_records is not held: K1 reports it too large)
-            c->carry_flags = flags & ZK_BATCH_VERIFY_TRACES;
-            ZK_ST(carry_append(c, d, ls, n));
-            c->carry_tid = c->h_edge[3];
-            hi = ls;
-        }
-    }
-    if (hi <= lead) return ZK_OK;
-    const uint64_t lo = lead & ~1ull;
-    SpanColsDev b = d;
-    b.trace_id += lo;
-    b.span_id += lo;
-    b.parent_id += lo;
-    b.first_ts += lo;
-    b.last_ts += lo;
-    b.service_id += lo;
-    b.flags += lo;
-    b.n = hi - lo;
-    return accumulate_dev(c, b, flags & ~ZK_BATCH_CONTINUES, (uint32_t)(lead & 1));
-}
 
 zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags) {
     if (!c) return ZK_ERR_INVALID_ARG;
@@ -589,15 +514,12 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
         return fail(c, ZK_ERR_INVALID_ARG, "ZK_BATCH_CONTINUES needs a trace-clustered batch (ZK_BATCH_TRACE_CLUSTERED)");
     const uint64_t n = cols->n;
     if (n == 0) {
-        if (!(flags & ZK_BATCH_CONTINUES)) {
-            c->carry_dropped = false;
-            if (c->carry_n) return flush_carry(c);
-        }
+        if (!(flags & ZK_BATCH_CONTINUES)) return flush_carry(c);
         return ZK_OK;
     }
     if (!cols_ok(cols)) return fail(c, ZK_ERR_INVALID_ARG, "null column pointer");
     const bool join = !c->rt || c->rt_mode == ZK_RT_WITH_DEPS;
-    if (join && c->records_since_reset + c->carry_n + n > kMaxRecordsSinceReset)  // held records included
+    if (join && c->records_since_reset + n > kMaxRecordsSinceReset)  // (held records counted with their batch)
         return fail(c, ZK_ERR_CAPACITY, "more than 2^32-1 records since reset");
     ZK_HIP(c, hipSetDevice(c->device));
     if (c->merged) {
@@ -652,11 +574,10 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
     if (!(flags & ZK_BATCH_TRACE_CLUSTERED)) {
         // a batch in any order ends a held trace (zkagg.h): the held trace is aggregated as it is, the
         // batch as a whole (its first run is not the held trace's continuation)
-        c->carry_dropped = false;
         ZK_ST(flush_carry(c));
         return accumulate_dev(c, d, flags, 0);
     }
-    if (c->carry_n || c->carry_dropped || (flags & ZK_BATCH_CONTINUES)) return continue_batch(c, d, flags);
+    if (c->maybe_carry || (flags & ZK_BATCH_CONTINUES)) return continue_batch(c, d, flags);
     return accumulate_dev(c, d, flags, 0);
     ZK_CATCH(c)
 }
@@ -780,7 +701,11 @@ static zk_status accumulate_groups(zk_ctx* c, const SpanColsDev& d, const Cluste
 
 // One batch already in HBM. skip (0 or 1): the first record belongs to a run handled elsewhere (it
 // only keeps the column pointers 16-byte aligned); K1 starts at the trace after it.
-static zk_status accumulate_dev(zk_ctx* c, SpanColsDev d, uint32_t flags, uint32_t skip) {
+static JoinArgs carry_join_args(zk_ctx* c, const JoinArgs* like);
+
+// dr: K1's skip and record count on the device (a batch under ZK_BATCH_CONTINUES); the carry's join
+// then follows the batch's spill pass, into the same realtime lists
+static zk_status accumulate_dev(zk_ctx* c, SpanColsDev d, uint32_t flags, uint32_t skip, const DevRange* dr) {
     const uint64_t n = d.n;
     if (n <= skip) return ZK_OK;
     const bool join = !c->rt || c->rt_mode == ZK_RT_WITH_DEPS;
@@ -843,8 +768,13 @@ static zk_status accumulate_dev(zk_ctx* c, SpanColsDev d, uint32_t flags, uint32
     a.cb_shift = c->cb_shift;
     a.join = join ? 1u : 0u;
     a.skip = skip;
+    if (dr) {
+        a.skip_dev = dr->skip_dev;
+        a.n_dev = dr->n_dev;
+    }
     if (c->rt) {
-        st = rt_prepare_lists(c->rt, grid, stride, n, &a, c->stream);
+        // (the spill list also takes the carry's items under dr)
+        st = rt_prepare_lists(c->rt, grid, stride, n + (dr ? c->carry_cap : 0), &a, c->stream);
         if (st != ZK_OK) return fail(c, st, std::string("sketch: ") + rt_error(c->rt));
     }
     EventPair ej, er, es;
@@ -886,15 +816,103 @@ static zk_status accumulate_dev(zk_ctx* c, SpanColsDev d, uint32_t flags, uint32
         ZK_HIP(c, hipEventRecord(es.a, c->stream));
     }
     ZK_HIP(c, launch_spill(a, c->spill_wgs, c->stream));
+    if (dr) {
+        const JoinArgs f = carry_join_args(c, &a);
+        ZK_HIP(c, launch_spill(f, 1, c->stream));
+    }
     if (c->timing) {
         ZK_HIP(c, hipEventRecord(es.b, c->stream));
         c->ev_spill.push_back(es);
     }
     if (c->rt) {
-        st = rt_consume_lists(c->rt, grid, stride, n);
+        st = rt_consume_lists(c->rt, grid, stride, n + (dr ? c->carry_cap : 0));
         if (st != ZK_OK) return fail(c, st, std::string("sketch: ") + rt_error(c->rt));
     }
     if (join) c->records_since_reset += n - skip;
+    return ZK_OK;
+}
+
+// The carry's join: the spill kernel over the carry columns, one trace of flush_n records (its list
+// is the one entry cs->zero = record 0, its length cs->flush_cnt). `like`: the batch's join
+// arguments whose realtime lists it shares (nullptr: none yet).
+static JoinArgs carry_join_args(zk_ctx* c, const JoinArgs* like) {
+    const SpanColsMut m = carve_cols(c->carry, c->carry_cap);
+    JoinArgs f = join_args(c, SpanColsDev{m.trace_id, m.span_id, m.parent_id, m.first_ts, m.last_ts, m.service_id,
+                                          m.flags, c->carry_cap});
+    f.spill_count = &c->cs->flush_cnt;
+    f.spill_list = (uint64_t*)&c->cs->zero;
+    f.spill_cap = 1;
+    f.n_dev = &c->cs->flush_n;
+    f.join = (!c->rt || c->rt_mode == ZK_RT_WITH_DEPS) ? 1u : 0u;
+    if (like) {
+        f.grid = like->grid;
+        f.link_stride = like->link_stride;
+        f.rt_pay = like->rt_pay;
+        f.rt_svc = like->rt_svc;
+        f.rt_count = like->rt_count;
+        f.rt_dropped = like->rt_dropped;
+        f.rt_spill_cap = like->rt_spill_cap;
+        f.rt_seed = like->rt_seed;
+        f.rt_p = like->rt_p;
+    }
+    return f;
+}
+
+// A clustered batch while a trace may be held, or whose last trace may continue: everything is
+// decided on the device (k_carry_plan), so nothing waits for the host. The batch's leading run joins
+// the held trace when it carries the same traceId; the held trace is joined (the spill kernel) once
+// the batch moves on to another trace (or does not continue); with ZK_BATCH_CONTINUES the batch's
+// last run becomes the new carry. K1 takes the rest of the batch: records below hi, from the first
+// trace boundary after record 0 when record 0's run is the held trace's.
+static zk_status continue_batch(zk_ctx* c, const SpanColsDev& d, uint32_t flags) {
+    RoctxRange rr("zk_continue_batch");
+    ZK_ST(ensure_carry(c));
+    const uint64_t n = d.n;
+    const uint32_t cont = (flags & ZK_BATCH_CONTINUES) ? 1u : 0u;
+    const uint32_t ver = (flags & ZK_BATCH_VERIFY_TRACES) ? 1u : 0u;
+    ZK_HIP(c, launch_edge_runs(d.trace_id, n, c->max_trace, &c->cs->edge[0], c->stream));
+    ZK_HIP(c, launch_carry_plan(c->cs, d.trace_id, n, c->max_trace, cont, ver, c->stats + ST_TOO_LARGE, c->stream));
+    const SpanColsMut m = carve_cols(c->carry, c->carry_cap);
+    ZK_HIP(c, launch_carry_copy(c->cs, d, m, 0, c->stream));
+    if (ver) c->any_verify = true;
+    if (c->any_verify) {
+        // the held trace's records were counted with their batch; its run is checked when it is joined,
+        // the batch's runs below hi now (not record 0's when that is the held trace's)
+        ZK_ST(ensure_tset(c, n));
+        ZK_HIP(c, launch_trace_set_insert(m.trace_id, c->carry_cap, c->tset, c->tset_slots,
+                                          &c->stats[ST_NOT_CLUSTERED], c->stream, &c->cs->flush_vn));
+        if (ver)
+            ZK_HIP(c, launch_trace_set_insert(d.trace_id, n, c->tset, c->tset_slots, &c->stats[ST_NOT_CLUSTERED],
+                                              c->stream, &c->cs->hi, &c->cs->skip));
+    }
+    const DevRange dr{&c->cs->skip, &c->cs->hi};
+    ZK_ST(accumulate_dev(c, d, flags & ~(ZK_BATCH_CONTINUES | ZK_BATCH_VERIFY_TRACES), 0, &dr));
+    ZK_HIP(c, launch_carry_copy(c->cs, d, m, 1, c->stream));  // (after the carry's join read the old carry)
+    c->maybe_carry = cont != 0;
+    return ZK_OK;
+}
+
+// the held-back trace is complete: join it as a trace of its own
+static zk_status flush_carry(zk_ctx* c) {
+    if (!c->maybe_carry) return ZK_OK;
+    c->maybe_carry = false;
+    ZK_HIP(c, launch_carry_plan(c->cs, nullptr, 0, c->max_trace, 0, 0, c->stats + ST_TOO_LARGE, c->stream));
+    if (c->any_verify) {
+        const SpanColsMut m = carve_cols(c->carry, c->carry_cap);
+        ZK_ST(ensure_tset(c, 0));
+        ZK_HIP(c, launch_trace_set_insert(m.trace_id, c->carry_cap, c->tset, c->tset_slots,
+                                          &c->stats[ST_NOT_CLUSTERED], c->stream, &c->cs->flush_vn));
+    }
+    JoinArgs f = carry_join_args(c, nullptr);
+    if (c->rt) {  // its sketch items: one list (list 0 of a zero-width list set)
+        const zk_status st = rt_prepare_lists(c->rt, 0, 0, c->carry_cap, &f, c->stream);
+        if (st != ZK_OK) return fail(c, st, std::string("sketch: ") + rt_error(c->rt));
+    }
+    ZK_HIP(c, launch_spill(f, 1, c->stream));
+    if (c->rt) {
+        const zk_status st = rt_consume_lists(c->rt, 0, 0, c->carry_cap);
+        if (st != ZK_OK) return fail(c, st, std::string("sketch: ") + rt_error(c->rt));
+    }
     return ZK_OK;
 }
 

@@ -45,9 +45,11 @@ hipError_t launch_cluster_fallback(const ClusterPlan& p, const ClusterGroups& g,
                                    const SpanColsMut& A, void* scratch, uint32_t cus, hipStream_t s,
                                    unsigned long long* capacity_fail);
 // insert the traceId of every segment start into `set` (slots: power of two; slot `slots` counts
-// traceId 0); *dup += segments whose traceId was already present
+// traceId 0); *dup += segments whose traceId was already present. Device limits (either may be
+// null): only segments starting below *n_dev, and not the one at record 0 when *skip_dev.
 hipError_t launch_trace_set_insert(const uint64_t* trace_id, uint64_t n, uint64_t* set, uint64_t slots,
-                                   unsigned long long* dup, hipStream_t s);
+                                   unsigned long long* dup, hipStream_t s,
+                                   const unsigned long long* n_dev = nullptr, const uint32_t* skip_dev = nullptr);
 hipError_t launch_trace_set_rehash(const uint64_t* old, uint64_t old_slots, uint64_t* set, uint64_t slots,
                                    hipStream_t s);
 // out[0..ST_N) = sum over the kStatShards copies of the device counters
@@ -57,5 +59,37 @@ hipError_t launch_stats_fold(const unsigned long long* shards, unsigned long lon
 // trace_id[i] != trace_id[i - 1] (~0 if none), out[1] = the last such index in [max(1, n - L - 1), n)
 // (0 if none). The caller zeroes out[1] and sets out[0] = ~0 first.
 hipError_t launch_edge_runs(const uint64_t* trace_id, uint64_t n, uint64_t L, unsigned long long* out, hipStream_t s);
+
+// ZK_BATCH_CONTINUES decided on the device, so a batch costs no host round trip. The held trace
+// (the carry: 7 columns of <= max_trace + 2 records) and its state live in HBM; per batch
+// k_carry_plan reads the batch's edge runs and the state, mirrors the rules of zkagg.h (the leading
+// run continues the held trace when it has its traceId; the held trace is complete once a batch
+// moves on; a held trace longer than max_trace_records is dropped and counted once; with CONTINUES
+// the batch's last run is held back) and writes the batch's plan, which the copies, the trace check,
+// K1 (skip_dev, n_dev = &hi) and the carry's join (the spill kernel over the carry, one entry) read.
+struct CarryState {
+    unsigned long long edge[2];   // k_edge_runs' output for the batch; the plan resets it to {~0, 0}
+    unsigned long long n;         // records held in the carry
+    unsigned long long tid;       // their traceId
+    unsigned int dropped;         // the held trace outgrew max_trace_records: its rest is skipped
+    unsigned int verify;          // a batch that carried it asked for ZK_BATCH_VERIFY_TRACES
+    // the current batch's plan
+    unsigned long long append_at; // the batch's records [0, append_n) go to carry[append_at, ...)
+    unsigned long long append_n;
+    unsigned long long flush_n;   // carry records [0, flush_n) are joined now, as one trace (0: none)
+    unsigned long long flush_vn;  // ... and inserted into the trace set (flush_n or 0)
+    unsigned long long hi;        // K1 and the trace check: the batch's records below hi
+    unsigned long long tail_lo;   // the batch's records [tail_lo, n) are the new carry (>= n: none)
+    unsigned long long zero;      // the carry join's spill list: one entry, record 0
+    unsigned int flush_cnt;       // its length (flush_n > 0)
+    unsigned int skip;            // K1: record 0's run belongs to the carry
+};
+// plan of one batch (n > 0 records, trace-clustered), or with n == 0 a flush: the held trace is
+// complete (finalize, a batch in any order, an empty batch without CONTINUES)
+hipError_t launch_carry_plan(CarryState* cs, const uint64_t* trace_id, uint64_t n, uint64_t max_trace,
+                             uint32_t continues, uint32_t verify, unsigned long long* too_large, hipStream_t s);
+// which = 0: the batch's leading records into the carry (append); 1: the batch's tail (new carry)
+hipError_t launch_carry_copy(const CarryState* cs, const SpanColsDev& batch, const SpanColsMut& carry, int which,
+                             hipStream_t s);
 
 }  // namespace zk

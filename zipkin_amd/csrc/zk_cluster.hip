@@ -704,10 +704,14 @@ __global__ __launch_bounds__(kTrWG) void k_cl_traces(TraceArgs a) {
 
 __global__ __launch_bounds__(256) void k_trace_set_insert(const uint64_t* __restrict__ tid, uint64_t n,
                                                           unsigned long long* __restrict__ set, uint64_t slots,
-                                                          unsigned long long* __restrict__ dup) {
+                                                          unsigned long long* __restrict__ dup,
+                                                          const unsigned long long* __restrict__ n_dev,
+                                                          const uint32_t* __restrict__ skip_dev) {
     uint32_t found = 0;
     const uint64_t mask = slots - 1;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    if (n_dev && *n_dev < n) n = *n_dev;
+    const uint64_t i0 = (skip_dev && *skip_dev) ? 1 : 0;  // record 0's run: the held trace's
+    for (uint64_t i = i0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t t = tid[i];
         if (i > 0 && tid[i - 1] == t) continue;
         if (t == 0ull) {
@@ -741,6 +745,112 @@ __global__ __launch_bounds__(256) void k_edge_runs(const uint64_t* __restrict__ 
         if (tid[i] != tid[i - 1]) atomicMin(&out[0], (unsigned long long)i);
     for (uint64_t i = (tail0 > 1 ? tail0 : 1) + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
         if (tid[i] != tid[i - 1]) atomicMax(&out[1], (unsigned long long)i);
+}
+
+// ZK_BATCH_CONTINUES on the device (zk_cluster.h CarryState): one thread applies the rules that
+// zk_deps_accumulate documents for held traces to this batch (n > 0) or flushes the carry (n == 0).
+__global__ __launch_bounds__(64) void k_carry_plan(CarryState* __restrict__ cs, const uint64_t* __restrict__ tid,
+                                                   uint64_t n, uint64_t L, uint32_t continues, uint32_t verify,
+                                                   unsigned long long* __restrict__ too_large) {
+    if (threadIdx.x != 0) return;
+    constexpr uint64_t kUnknown = ~0ull;  // an edge run longer than the L + 1 records searched
+    cs->append_n = 0;
+    cs->append_at = 0;
+    cs->flush_n = 0;
+    cs->flush_vn = 0;
+    cs->zero = 0;
+    cs->skip = 0;
+    cs->hi = 0;
+    cs->tail_lo = kUnknown;
+    auto flush = [&]() {  // the held trace is complete: join it now
+        cs->flush_n = cs->n;
+        cs->flush_vn = cs->verify ? cs->n : 0;
+        cs->n = 0;
+        cs->verify = 0;
+    };
+    if (n == 0) {
+        cs->dropped = 0;
+        flush();
+        cs->flush_cnt = cs->flush_n ? 1u : 0u;
+        return;
+    }
+    const uint64_t e0 = cs->edge[0], e1 = cs->edge[1];
+    cs->edge[0] = ~0ull;  // ready for the next batch's k_edge_runs
+    cs->edge[1] = 0;
+    const uint64_t t0 = tid[0], tn = tid[n - 1];
+    // the whole batch is one trace: no boundary in the searched head (all of it when n <= L + 1), or
+    // none in head and tail and the same traceId at both ends (trace-clustered)
+    const bool no_head = e0 == ~0ull, no_tail = e1 == 0;
+    const bool one_run = no_head && (n <= L + 1 || (no_tail && t0 == tn));
+    // end of the leading run, start of the last one (a run longer than L + 1 is only known to be long;
+    // a held run has at most L + 1 records, the carry holds L + 2)
+    const uint64_t first_end = one_run ? n : (no_head ? kUnknown : e0);
+    const uint64_t last_start = one_run ? (n <= L + 1 ? 0 : kUnknown) : (no_tail ? kUnknown : e1);
+    uint64_t lead = 0;
+    if (cs->n || cs->dropped) {
+        if (t0 == cs->tid) {
+            lead = first_end;
+            if (cs->dropped) {
+                // the rest of a trace already found too long: skipped like its beginning
+            } else if (lead == kUnknown || cs->n + lead > L) {
+                cs->n = 0;  // longer than max_trace_records: not aggregated, counted once
+                cs->dropped = 1;
+                atomicAdd(too_large, 1ull);
+            } else {
+                cs->append_at = cs->n;
+                cs->append_n = lead;
+                cs->n += lead;
+            }
+        }
+        cs->verify |= verify;
+        if (lead == n && continues) {  // the whole batch continues the held trace
+            cs->flush_cnt = 0;
+            return;
+        }
+        cs->dropped = 0;
+        flush();
+    }
+    cs->flush_cnt = cs->flush_n ? 1u : 0u;
+    uint64_t hi = n;
+    if (continues && last_start != kUnknown) {
+        // (a last run longer than L + 1 is not held: K1 reports it too large; the leading run ends
+        // at or before the last run's start unless the batch is one run)
+        const uint64_t ls = (lead != kUnknown && lead > last_start) ? lead : last_start;
+        if (ls < n) {
+            cs->tail_lo = ls;
+            cs->n = n - ls;
+            cs->tid = tn;
+            cs->verify = verify;
+            hi = ls;
+        }
+    }
+    cs->hi = hi;
+    cs->skip = lead ? 1u : 0u;  // K1 starts at the first trace boundary after record 0
+}
+
+__global__ __launch_bounds__(256) void k_carry_copy(const CarryState* __restrict__ cs, SpanColsDev b, SpanColsMut m,
+                                                    int which) {
+    uint64_t lo, len, at;
+    if (which == 0) {
+        lo = 0;
+        len = cs->append_n;
+        at = cs->append_at;
+    } else {
+        lo = cs->tail_lo;
+        len = lo < b.n ? b.n - lo : 0;
+        at = 0;
+    }
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < len; k += stride) {
+        const uint64_t i = lo + k, j = at + k;
+        m.trace_id[j] = b.trace_id[i];
+        m.span_id[j] = b.span_id[i];
+        m.parent_id[j] = b.parent_id[i];
+        m.first_ts[j] = b.first_ts[i];
+        m.last_ts[j] = b.last_ts[i];
+        m.service_id[j] = b.service_id[i];
+        m.flags[j] = b.flags[i];
+    }
 }
 
 // stats shards -> the 16 totals in the table's tail (zk_deps_partial)
@@ -1018,10 +1128,22 @@ hipError_t launch_cluster_fallback(const ClusterPlan& p, const ClusterGroups& g,
 }
 
 hipError_t launch_trace_set_insert(const uint64_t* trace_id, uint64_t n, uint64_t* set, uint64_t slots,
-                                   unsigned long long* dup, hipStream_t s) {
+                                   unsigned long long* dup, hipStream_t s, const unsigned long long* n_dev,
+                                   const uint32_t* skip_dev) {
     if (n == 0) return hipSuccess;
     return launch_checked("k_trace_set_insert", k_trace_set_insert, dim3(grid_for(n)), dim3(256), 0, s, trace_id, n,
-                          (unsigned long long*)set, slots, dup);
+                          (unsigned long long*)set, slots, dup, n_dev, skip_dev);
+}
+
+hipError_t launch_carry_plan(CarryState* cs, const uint64_t* trace_id, uint64_t n, uint64_t max_trace,
+                             uint32_t continues, uint32_t verify, unsigned long long* too_large, hipStream_t s) {
+    return launch_checked("k_carry_plan", k_carry_plan, dim3(1), dim3(64), 0, s, cs, trace_id, n, max_trace, continues,
+                          verify, too_large);
+}
+
+hipError_t launch_carry_copy(const CarryState* cs, const SpanColsDev& batch, const SpanColsMut& carry, int which,
+                             hipStream_t s) {
+    return launch_checked("k_carry_copy", k_carry_copy, dim3(64), dim3(256), 0, s, cs, batch, carry, which);
 }
 
 hipError_t launch_trace_set_rehash(const uint64_t* old, uint64_t old_slots, uint64_t* set, uint64_t slots,

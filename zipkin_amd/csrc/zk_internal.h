@@ -127,6 +127,8 @@ struct JoinArgs {
     // links append to the lists the group join wrote (append = 1)
     const unsigned long long* n_dev;
     uint32_t append;
+    // ZK_BATCH_CONTINUES on the device: skip read from here when set (and n from n_dev)
+    const uint32_t* skip_dev;
 };
 
 // host-side launchers (implemented in the .hip files)

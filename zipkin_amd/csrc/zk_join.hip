@@ -403,7 +403,10 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     uint64_t m_ev, m_od;  // this wave's boundary ballots of the current window (uniform; phase 3 reuses them)
     ZK_STAMP_DECL
     uint64_t ws = R0;         // window start (even)
-    uint64_t seek = R0 + (blockIdx.x == 0 ? a.skip : 0u);  // first record that may start one of our traces
+    // first record that may start one of our traces (skip: record 0's run is the held trace's,
+    // decided on the device when the batch continues one, zk_cluster.hip k_carry_plan)
+    const uint32_t skip0 = a.skip_dev ? *a.skip_dev : a.skip;
+    uint64_t seek = R0 + (blockIdx.x == 0 ? skip0 : 0u);
     bool seek_start = false;  // seek is known to be a trace start (uniform)
     load_tid(a, n, ws, cur);
     load_early(a, n, ws, cur);
