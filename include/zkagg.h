@@ -123,7 +123,8 @@ typedef struct zk_span_cols {
  * batch's leading fragments of the same traceId; a held trace may continue over any number of
  * batches. The held trace is aggregated when a batch moves on to another traceId, when a batch
  * arrives without the flag, at finalize and at zk_deps_partial; zk_ctx_stats does not count it
- * before then. Costs one small edge scan and one stream synchronisation per such accumulate. */
+ * before then. Decided on the device (no host round trip): one small kernel finds the batch's
+ * edge runs (scanning from both ends until a trace boundary) and applies these rules. */
 #define ZK_BATCH_CONTINUES       (1u << 3)
 
 typedef struct zk_config {

@@ -16,6 +16,19 @@ from . import _abi
 from .columns import DeviceColumns, SpanColumns
 
 
+def _host_buffer(nbytes: int) -> np.ndarray:
+    """nbytes of host memory as a uint8 array: page-locked (torch's caching host allocator, so
+    repeated finalizes reuse the block) when a HIP device is visible to torch, else ordinary memory."""
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            return torch.empty(nbytes, dtype=torch.uint8, pin_memory=True).numpy()
+    except Exception:  # pragma: no cover - torch missing or without a device: pageable memory
+        pass
+    return np.empty(nbytes, np.uint8)
+
+
 @dataclass
 class LinkTable:
     """Dense S x S table: cell p*S + c is DependencyLink(parent=p, child=c)."""
@@ -148,9 +161,12 @@ class DepsContext:
             t.device_ptrs = 1
             self._check(self._L.zk_deps_finalize(self._h, C.byref(t)))
             return None
-        m0 = np.empty(cells, np.uint64)  # (finalize writes every cell)
-        ms = [np.empty(cells, np.float64) for _ in range(4)]
-        pr = np.empty(cells, np.uint8)
+        # (finalize writes every cell) into page-locked host memory when torch has it: the device
+        # copies then land directly (~2x the pageable rate for the 41 B per cell)
+        buf = _host_buffer(cells * 41)
+        m0 = buf[: cells * 8].view(np.uint64)
+        ms = [buf[cells * 8 * (k + 1): cells * 8 * (k + 2)].view(np.float64) for k in range(4)]
+        pr = buf[cells * 40: cells * 41]
         t.m0 = m0.ctypes.data
         t.m1, t.m2, t.m3, t.m4 = (a.ctypes.data for a in ms)
         t.present = pr.ctypes.data

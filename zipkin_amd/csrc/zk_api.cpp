@@ -52,6 +52,7 @@ struct zk_ctx {
     uint64_t link_slots = 0;  // capacity of `links` in u64
     uint64_t sorted_slots = 0;  // capacity of `sorted` in u64
     uint32_t link_lists = 0;  // capacity of `link_count`
+    uint32_t col_off_lists = 0;  // capacity of `col_off` in lists (x nb)
     uint32_t cus = 256;
     // partitioned reduce state (nb = 0: atomic reduce)
     uint32_t nb = 0, cb_shift = 0;
@@ -115,6 +116,12 @@ zk_status hip_fail(zk_ctx* c, hipError_t e, const char* where) {
         if (_e != hipSuccess) return hip_fail(ctx, _e, #call); \
     } while (0)
 
+#define ZK_ST(call)                        \
+    do {                                   \
+        const zk_status _s = (call);       \
+        if (_s != ZK_OK) return _s;        \
+    } while (0)
+
 // No C++ exception crosses the C ABI (zkagg.h: "never throws or aborts").
 #define ZK_TRY try {
 #define ZK_CATCH(ctx)                                                                      \
@@ -146,31 +153,39 @@ zk_status ensure_links(zk_ctx* c, uint32_t grid, uint64_t stride, uint64_t n) {
     const uint64_t slots = (uint64_t)grid * stride;
     // K2's bucket-sorted copy holds every link once: at most one per record
     const uint64_t sorted_slots = n + 64 < slots ? n + 64 : slots;
-    if (slots <= c->link_slots && grid <= c->link_lists && (!c->nb || sorted_slots <= c->sorted_slots)) return ZK_OK;
-    if (c->links) ZK_HIP(c, hipFree(c->links));
-    if (c->link_count) ZK_HIP(c, hipFree(c->link_count));
-    c->links = nullptr;
-    c->link_count = nullptr;
-    c->link_slots = 0;
-    c->sorted_slots = 0;
-    c->link_lists = 0;
-    ZK_HIP(c, hipMalloc(&c->links, slots * sizeof(uint64_t)));
-    ZK_HIP(c, hipMalloc(&c->link_count, (uint64_t)grid * sizeof(uint32_t)));
-    if (c->nb) {
+    const bool set_ok = slots <= c->link_slots && grid <= c->link_lists;
+    const bool scratch_ok = !c->nb || (sorted_slots <= c->sorted_slots && grid <= c->col_off_lists);
+    if (set_ok && scratch_ok) return ZK_OK;
+    if (!set_ok) {  // the link lists
+        hipFree(c->links);
+        hipFree(c->link_count);
         hipFree(c->hist);
+        c->links = nullptr;
+        c->link_count = nullptr;
+        c->hist = nullptr;
+        c->link_slots = 0;
+        c->link_lists = 0;
+        ZK_HIP(c, hipMalloc(&c->links, slots * sizeof(uint64_t)));
+        ZK_HIP(c, hipMalloc(&c->link_count, (uint64_t)grid * sizeof(uint32_t)));
+        if (c->nb) ZK_HIP(c, hipMalloc(&c->hist, (uint64_t)grid * c->nb * sizeof(uint32_t)));
+        c->link_slots = slots;
+        c->link_lists = grid;
+    }
+    if (!scratch_ok) {  // K2/K3's scratch
+        const uint64_t ss = sorted_slots > c->sorted_slots ? sorted_slots : c->sorted_slots;
+        const uint32_t gl = grid > c->col_off_lists ? grid : c->col_off_lists;
         hipFree(c->col_off);
         hipFree(c->sorted);
-        c->hist = nullptr;
         c->col_off = nullptr;
         c->sorted = nullptr;
-        ZK_HIP(c, hipMalloc(&c->hist, (uint64_t)grid * c->nb * sizeof(uint32_t)));
-        ZK_HIP(c, hipMalloc(&c->col_off, (uint64_t)grid * c->nb * sizeof(uint32_t)));
-        ZK_HIP(c, hipMalloc(&c->sorted, sorted_slots * sizeof(uint64_t)));
-        c->sorted_slots = sorted_slots;
+        c->sorted_slots = 0;
+        c->col_off_lists = 0;
+        ZK_HIP(c, hipMalloc(&c->col_off, (uint64_t)gl * c->nb * sizeof(uint32_t)));
+        ZK_HIP(c, hipMalloc(&c->sorted, ss * sizeof(uint64_t)));
+        c->sorted_slots = ss;
+        c->col_off_lists = gl;
         if (!c->bucket_base) ZK_HIP(c, hipMalloc(&c->bucket_base, (c->nb + 1) * sizeof(uint64_t)));
     }
-    c->link_slots = slots;
-    c->link_lists = grid;
     return ZK_OK;
 }
 
@@ -459,16 +474,10 @@ static zk_status accumulate_dev(zk_ctx* c, SpanColsDev d, uint32_t flags, uint32
                                 const DevRange* dr = nullptr);
 static zk_status continue_batch(zk_ctx* c, const SpanColsDev& d, uint32_t flags);
 static zk_status flush_carry(zk_ctx* c);
-#define ZK_ST(call)                        \
-    do {                                   \
-        const zk_status _s = (call);       \
-        if (_s != ZK_OK) return _s;        \
-    } while (0)
 
-// the carry state of a fresh job: nothing held, the edge slots ready for k_edge_runs
+// the carry state of a fresh job: nothing held
 static zk_status carry_state_reset(zk_ctx* c) {
     ZK_HIP(c, hipMemsetAsync(c->cs, 0, sizeof(CarryState), c->stream));
-    ZK_HIP(c, hipMemsetAsync(&c->cs->edge[0], 0xFF, 8, c->stream));
     return ZK_OK;
 }
 
@@ -740,13 +749,14 @@ static zk_status accumulate_dev(zk_ctx* c, SpanColsDev d, uint32_t flags, uint32
         const zk_status vs = verify_batch(c, v);
         if (vs != ZK_OK) return vs;
     }
-    uint32_t grid = 0;
+        uint32_t grid = 0;
     uint64_t per_wg = 0, stride = 0;
     join_geometry(n, c->cus, &grid, &per_wg, &stride);
+    if (dr) stride += join_tile_records();  // list 0 also takes the held trace's links (K1, one workgroup)
     zk_status st = ensure_spill(c, n);
     if (st == ZK_OK) st = ensure_links(c, grid, stride, n);
     if (st != ZK_OK) return st;
-    ZK_HIP(c, hipMemsetAsync(c->spill_count, 0, 4, c->stream));
+    if (!dr) ZK_HIP(c, hipMemsetAsync(c->spill_count, 0, 4, c->stream));  // (else k_carry_plan zeroed it)
     JoinArgs a{};
     a.c = d;
     a.table = c->table;
@@ -783,6 +793,15 @@ static zk_status accumulate_dev(zk_ctx* c, SpanColsDev d, uint32_t flags, uint32
         ZK_HIP(c, hipEventRecord(ej.a, c->stream));
     }
     ZK_HIP(c, launch_join(a, c->stream));
+    JoinArgs f{};
+    if (dr) {
+        // the held trace joined now (k_carry_plan: flush_n records of the carry, 0: none): by K1 on
+        // one workgroup appending to list 0 (its spill list of one entry takes it when it outgrows a
+        // window), or with a realtime sketch bound, whose item lists K1 cannot append to, by the spill
+        // kernel alone
+        f = carry_join_args(c, &a);
+        if (!c->rt) ZK_HIP(c, launch_join(f, c->stream, 1));
+    }
     if (c->timing) {
         ZK_HIP(c, hipEventRecord(ej.b, c->stream));
         c->ev_join.push_back(ej);
@@ -816,10 +835,7 @@ static zk_status accumulate_dev(zk_ctx* c, SpanColsDev d, uint32_t flags, uint32
         ZK_HIP(c, hipEventRecord(es.a, c->stream));
     }
     ZK_HIP(c, launch_spill(a, c->spill_wgs, c->stream));
-    if (dr) {
-        const JoinArgs f = carry_join_args(c, &a);
-        ZK_HIP(c, launch_spill(f, 1, c->stream));
-    }
+    if (dr) ZK_HIP(c, launch_spill(f, 1, c->stream));
     if (c->timing) {
         ZK_HIP(c, hipEventRecord(es.b, c->stream));
         c->ev_spill.push_back(es);
@@ -832,29 +848,24 @@ static zk_status accumulate_dev(zk_ctx* c, SpanColsDev d, uint32_t flags, uint32
     return ZK_OK;
 }
 
-// The carry's join: the spill kernel over the carry columns, one trace of flush_n records (its list
-// is the one entry cs->zero = record 0, its length cs->flush_cnt). `like`: the batch's join
-// arguments whose realtime lists it shares (nullptr: none yet).
+// The carry's join: one trace of flush_n records of the carry columns, its spill list the one entry
+// cs->zero = record 0 of length cs->flush_cnt. `like`: the batch's join arguments, whose geometry,
+// link lists (K1 appends to list 0) and realtime lists it shares (nullptr: a flush alone, by the
+// spill kernel).
 static JoinArgs carry_join_args(zk_ctx* c, const JoinArgs* like) {
     const SpanColsMut m = carve_cols(c->carry, c->carry_cap);
-    JoinArgs f = join_args(c, SpanColsDev{m.trace_id, m.span_id, m.parent_id, m.first_ts, m.last_ts, m.service_id,
-                                          m.flags, c->carry_cap});
+    const SpanColsDev cd{m.trace_id, m.span_id, m.parent_id, m.first_ts, m.last_ts, m.service_id, m.flags,
+                         c->carry_cap};
+    JoinArgs f = like ? *like : join_args(c, cd);
+    f.c = cd;
     f.spill_count = &c->cs->flush_cnt;
     f.spill_list = (uint64_t*)&c->cs->zero;
     f.spill_cap = 1;
     f.n_dev = &c->cs->flush_n;
+    f.skip_dev = nullptr;
+    f.skip = 0;
+    f.append = 1;
     f.join = (!c->rt || c->rt_mode == ZK_RT_WITH_DEPS) ? 1u : 0u;
-    if (like) {
-        f.grid = like->grid;
-        f.link_stride = like->link_stride;
-        f.rt_pay = like->rt_pay;
-        f.rt_svc = like->rt_svc;
-        f.rt_count = like->rt_count;
-        f.rt_dropped = like->rt_dropped;
-        f.rt_spill_cap = like->rt_spill_cap;
-        f.rt_seed = like->rt_seed;
-        f.rt_p = like->rt_p;
-    }
     return f;
 }
 
@@ -870,24 +881,19 @@ static zk_status continue_batch(zk_ctx* c, const SpanColsDev& d, uint32_t flags)
     const uint64_t n = d.n;
     const uint32_t cont = (flags & ZK_BATCH_CONTINUES) ? 1u : 0u;
     const uint32_t ver = (flags & ZK_BATCH_VERIFY_TRACES) ? 1u : 0u;
-    ZK_HIP(c, launch_edge_runs(d.trace_id, n, c->max_trace, &c->cs->edge[0], c->stream));
-    ZK_HIP(c, launch_carry_plan(c->cs, d.trace_id, n, c->max_trace, cont, ver, c->stats + ST_TOO_LARGE, c->stream));
-    const SpanColsMut m = carve_cols(c->carry, c->carry_cap);
-    ZK_HIP(c, launch_carry_copy(c->cs, d, m, 0, c->stream));
     if (ver) c->any_verify = true;
-    if (c->any_verify) {
-        // the held trace's records were counted with their batch; its run is checked when it is joined,
-        // the batch's runs below hi now (not record 0's when that is the held trace's)
-        ZK_ST(ensure_tset(c, n));
-        ZK_HIP(c, launch_trace_set_insert(m.trace_id, c->carry_cap, c->tset, c->tset_slots,
-                                          &c->stats[ST_NOT_CLUSTERED], c->stream, &c->cs->flush_vn));
-        if (ver)
-            ZK_HIP(c, launch_trace_set_insert(d.trace_id, n, c->tset, c->tset_slots, &c->stats[ST_NOT_CLUSTERED],
-                                              c->stream, &c->cs->hi, &c->cs->skip));
-    }
+    // (the held trace's records were counted with their batch; its run is checked when it is joined)
+    if (c->any_verify) ZK_ST(ensure_tset(c, n));
+    const SpanColsMut m = carve_cols(c->carry, c->carry_cap);
+    ZK_HIP(c, launch_carry_plan(c->cs, d, m, c->max_trace, cont, ver, c->rt ? 0u : 1u, c->stats + ST_TOO_LARGE,
+                                c->spill_count, c->any_verify ? c->tset : nullptr, c->tset_slots,
+                                &c->stats[ST_NOT_CLUSTERED], c->stream));
+    if (ver)  // the batch's runs below hi (not record 0's when that is the held trace's)
+        ZK_HIP(c, launch_trace_set_insert(d.trace_id, n, c->tset, c->tset_slots, &c->stats[ST_NOT_CLUSTERED],
+                                          c->stream, &c->cs->hi, &c->cs->skip));
     const DevRange dr{&c->cs->skip, &c->cs->hi};
     ZK_ST(accumulate_dev(c, d, flags & ~(ZK_BATCH_CONTINUES | ZK_BATCH_VERIFY_TRACES), 0, &dr));
-    ZK_HIP(c, launch_carry_copy(c->cs, d, m, 1, c->stream));  // (after the carry's join read the old carry)
+    ZK_HIP(c, launch_carry_tail(c->cs, d, m, c->stream));  // (after the carry's join read the old carry)
     c->maybe_carry = cont != 0;
     return ZK_OK;
 }
@@ -896,15 +902,15 @@ static zk_status continue_batch(zk_ctx* c, const SpanColsDev& d, uint32_t flags)
 static zk_status flush_carry(zk_ctx* c) {
     if (!c->maybe_carry) return ZK_OK;
     c->maybe_carry = false;
-    ZK_HIP(c, launch_carry_plan(c->cs, nullptr, 0, c->max_trace, 0, 0, c->stats + ST_TOO_LARGE, c->stream));
-    if (c->any_verify) {
-        const SpanColsMut m = carve_cols(c->carry, c->carry_cap);
-        ZK_ST(ensure_tset(c, 0));
-        ZK_HIP(c, launch_trace_set_insert(m.trace_id, c->carry_cap, c->tset, c->tset_slots,
-                                          &c->stats[ST_NOT_CLUSTERED], c->stream, &c->cs->flush_vn));
-    }
+    if (c->any_verify) ZK_ST(ensure_tset(c, 0));
+    const SpanColsMut m = carve_cols(c->carry, c->carry_cap);
+    ZK_HIP(c, launch_carry_plan(c->cs, SpanColsDev{}, m, c->max_trace, 0, 0, 0, c->stats + ST_TOO_LARGE, nullptr,
+                                c->any_verify ? c->tset : nullptr, c->tset_slots, &c->stats[ST_NOT_CLUSTERED],
+                                c->stream));
     JoinArgs f = carry_join_args(c, nullptr);
     if (c->rt) {  // its sketch items: one list (list 0 of a zero-width list set)
+        f.grid = 0;
+        f.link_stride = 0;
         const zk_status st = rt_prepare_lists(c->rt, 0, 0, c->carry_cap, &f, c->stream);
         if (st != ZK_OK) return fail(c, st, std::string("sketch: ") + rt_error(c->rt));
     }
@@ -1075,7 +1081,7 @@ zk_status zk_rt_bind(zk_ctx* c, zk_rt* rt, uint32_t mode) {
     if (mode != ZK_RT_WITH_DEPS && mode != ZK_RT_ONLY) return fail(c, ZK_ERR_INVALID_ARG, "unknown sketch mode");
     if (rt && rt_device(rt) != c->device) return fail(c, ZK_ERR_INVALID_ARG, "sketch and ctx on different devices");
     if (c->rt && c->rt != rt) {
-        ZK_HIP(c, hipStreamSynchronize(c->stream));
+            ZK_HIP(c, hipStreamSynchronize(c->stream));
         rt_set_stream(c->rt, nullptr);
     }
     c->rt = rt;

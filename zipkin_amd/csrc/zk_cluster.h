@@ -55,20 +55,14 @@ hipError_t launch_trace_set_rehash(const uint64_t* old, uint64_t old_slots, uint
 // out[0..ST_N) = sum over the kStatShards copies of the device counters
 hipError_t launch_stat_add(unsigned long long* slot, uint64_t v, hipStream_t s);
 hipError_t launch_stats_fold(const unsigned long long* shards, unsigned long long* out, hipStream_t s);
-// ZK_BATCH_CONTINUES: the batch's edge runs. out[0] = the first index i in [1, min(n, L + 1)) with
-// trace_id[i] != trace_id[i - 1] (~0 if none), out[1] = the last such index in [max(1, n - L - 1), n)
-// (0 if none). The caller zeroes out[1] and sets out[0] = ~0 first.
-hipError_t launch_edge_runs(const uint64_t* trace_id, uint64_t n, uint64_t L, unsigned long long* out, hipStream_t s);
-
 // ZK_BATCH_CONTINUES decided on the device, so a batch costs no host round trip. The held trace
 // (the carry: 7 columns of <= max_trace + 2 records) and its state live in HBM; per batch
-// k_carry_plan reads the batch's edge runs and the state, mirrors the rules of zkagg.h (the leading
-// run continues the held trace when it has its traceId; the held trace is complete once a batch
-// moves on; a held trace longer than max_trace_records is dropped and counted once; with CONTINUES
-// the batch's last run is held back) and writes the batch's plan, which the copies, the trace check,
-// K1 (skip_dev, n_dev = &hi) and the carry's join (the spill kernel over the carry, one entry) read.
+// k_carry_plan finds the batch's edge runs, mirrors the rules of zkagg.h (the leading run continues
+// the held trace when it has its traceId; the held trace is complete once a batch moves on; a held
+// trace longer than max_trace_records is dropped and counted once; with CONTINUES the batch's last
+// run is held back) and writes the batch's plan, which the trace check, K1 (skip_dev, n_dev = &hi),
+// the carry's join (K1 on one workgroup, or the spill kernel) and the tail copy read.
 struct CarryState {
-    unsigned long long edge[2];   // k_edge_runs' output for the batch; the plan resets it to {~0, 0}
     unsigned long long n;         // records held in the carry
     unsigned long long tid;       // their traceId
     unsigned int dropped;         // the held trace outgrew max_trace_records: its rest is skipped
@@ -84,12 +78,16 @@ struct CarryState {
     unsigned int flush_cnt;       // its length (flush_n > 0)
     unsigned int skip;            // K1: record 0's run belongs to the carry
 };
-// plan of one batch (n > 0 records, trace-clustered), or with n == 0 a flush: the held trace is
-// complete (finalize, a batch in any order, an empty batch without CONTINUES)
-hipError_t launch_carry_plan(CarryState* cs, const uint64_t* trace_id, uint64_t n, uint64_t max_trace,
-                             uint32_t continues, uint32_t verify, unsigned long long* too_large, hipStream_t s);
-// which = 0: the batch's leading records into the carry (append); 1: the batch's tail (new carry)
-hipError_t launch_carry_copy(const CarryState* cs, const SpanColsDev& batch, const SpanColsMut& carry, int which,
+// plan of one batch (batch.n > 0 records, trace-clustered), or with batch.n == 0 a flush: the held
+// trace is complete (finalize, a batch in any order, an empty batch without CONTINUES). It also
+// appends the batch's leading run to the carry, zeroes *spill_count (the batch's K1 spill list;
+// may be null) and, when set != null, inserts the joined carry's traceId into the trace set.
+// k1_joins: K1 joins a flushed carry (flush_cnt starts at 0); else the spill kernel (flush_cnt = 1).
+hipError_t launch_carry_plan(CarryState* cs, const SpanColsDev& batch, const SpanColsMut& carry, uint64_t max_trace,
+                             uint32_t continues, uint32_t verify, uint32_t k1_joins, unsigned long long* too_large,
+                             unsigned int* spill_count, uint64_t* set, uint64_t slots, unsigned long long* dup,
                              hipStream_t s);
+// the batch's tail -> the carry (the new held trace)
+hipError_t launch_carry_tail(const CarryState* cs, const SpanColsDev& batch, const SpanColsMut& carry, hipStream_t s);
 
 }  // namespace zk

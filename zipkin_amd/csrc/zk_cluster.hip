@@ -735,121 +735,166 @@ __global__ __launch_bounds__(256) void k_trace_set_rehash(const unsigned long lo
     }
 }
 
-// the edge runs of a clustered batch (ZK_BATCH_CONTINUES): its first run's end and last run's start
-__global__ __launch_bounds__(256) void k_edge_runs(const uint64_t* __restrict__ tid, uint64_t n, uint64_t L,
-                                                   unsigned long long* __restrict__ out) {
-    const uint64_t head = n < L + 1 ? n : L + 1;
-    const uint64_t tail0 = n > L + 1 ? n - L - 1 : 1;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = 1 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < head; i += stride)
-        if (tid[i] != tid[i - 1]) atomicMin(&out[0], (unsigned long long)i);
-    for (uint64_t i = (tail0 > 1 ? tail0 : 1) + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-        if (tid[i] != tid[i - 1]) atomicMax(&out[1], (unsigned long long)i);
-}
-
-// ZK_BATCH_CONTINUES on the device (zk_cluster.h CarryState): one thread applies the rules that
-// zk_deps_accumulate documents for held traces to this batch (n > 0) or flushes the carry (n == 0).
-__global__ __launch_bounds__(64) void k_carry_plan(CarryState* __restrict__ cs, const uint64_t* __restrict__ tid,
-                                                   uint64_t n, uint64_t L, uint32_t continues, uint32_t verify,
-                                                   unsigned long long* __restrict__ too_large) {
-    if (threadIdx.x != 0) return;
-    constexpr uint64_t kUnknown = ~0ull;  // an edge run longer than the L + 1 records searched
-    cs->append_n = 0;
-    cs->append_at = 0;
-    cs->flush_n = 0;
-    cs->flush_vn = 0;
-    cs->zero = 0;
-    cs->skip = 0;
-    cs->hi = 0;
-    cs->tail_lo = kUnknown;
-    auto flush = [&]() {  // the held trace is complete: join it now
-        cs->flush_n = cs->n;
-        cs->flush_vn = cs->verify ? cs->n : 0;
-        cs->n = 0;
-        cs->verify = 0;
-    };
-    if (n == 0) {
-        cs->dropped = 0;
-        flush();
-        cs->flush_cnt = cs->flush_n ? 1u : 0u;
-        return;
+// ZK_BATCH_CONTINUES on the device (zk_cluster.h CarryState), one workgroup: the batch's edge runs
+// (the first trace boundary in [1, min(n, L + 1)), the last in [max(1, n - L - 1), n), searched 256
+// records at a time from each end, so a batch of short traces costs a few hundred bytes), then one
+// thread applies the rules that zk_deps_accumulate documents for held traces to this batch (n > 0)
+// or flushes the carry (n == 0), then the workgroup appends the batch's leading run to the carry.
+__global__ __launch_bounds__(256) void k_carry_plan(CarryState* __restrict__ cs, SpanColsDev b, SpanColsMut m,
+                                                    uint64_t L, uint32_t continues, uint32_t verify,
+                                                    uint32_t k1_joins, unsigned long long* __restrict__ too_large,
+                                                    unsigned int* __restrict__ spill_count,
+                                                    unsigned long long* __restrict__ set, uint64_t slots,
+                                                    unsigned long long* __restrict__ dup) {
+    __shared__ unsigned long long s_e0, s_e1, s_at, s_len;
+    const uint32_t t = threadIdx.x;
+    const uint64_t n = b.n;
+    const uint64_t* __restrict__ tid = b.trace_id;
+    if (t == 0) {
+        s_e0 = ~0ull;
+        s_e1 = 0;
+        if (spill_count) *spill_count = 0;  // the batch's K1 spill list starts empty
     }
-    const uint64_t e0 = cs->edge[0], e1 = cs->edge[1];
-    cs->edge[0] = ~0ull;  // ready for the next batch's k_edge_runs
-    cs->edge[1] = 0;
-    const uint64_t t0 = tid[0], tn = tid[n - 1];
-    // the whole batch is one trace: no boundary in the searched head (all of it when n <= L + 1), or
-    // none in head and tail and the same traceId at both ends (trace-clustered)
-    const bool no_head = e0 == ~0ull, no_tail = e1 == 0;
-    const bool one_run = no_head && (n <= L + 1 || (no_tail && t0 == tn));
-    // end of the leading run, start of the last one (a run longer than L + 1 is only known to be long;
-    // a held run has at most L + 1 records, the carry holds L + 2)
-    const uint64_t first_end = one_run ? n : (no_head ? kUnknown : e0);
-    const uint64_t last_start = one_run ? (n <= L + 1 ? 0 : kUnknown) : (no_tail ? kUnknown : e1);
-    uint64_t lead = 0;
-    if (cs->n || cs->dropped) {
-        if (t0 == cs->tid) {
-            lead = first_end;
-            if (cs->dropped) {
-                // the rest of a trace already found too long: skipped like its beginning
-            } else if (lead == kUnknown || cs->n + lead > L) {
-                cs->n = 0;  // longer than max_trace_records: not aggregated, counted once
-                cs->dropped = 1;
-                atomicAdd(too_large, 1ull);
-            } else {
-                cs->append_at = cs->n;
-                cs->append_n = lead;
-                cs->n += lead;
+    __syncthreads();
+    if (n >= 2) {
+        const uint64_t head = n < L + 1 ? n : L + 1;
+        for (uint64_t base = 1; base < head; base += 256) {
+            const uint64_t i = base + t;
+            if (i < head && tid[i] != tid[i - 1]) atomicMin(&s_e0, (unsigned long long)i);
+            __syncthreads();
+            const bool found = s_e0 != ~0ull;
+            __syncthreads();  // (read by all before another round's atomics)
+            if (found) break;
+        }
+        const uint64_t tail0 = n > L + 1 ? n - L - 1 : 1;
+        for (uint64_t top = n; top > tail0; top = top > tail0 + 256 ? top - 256 : tail0) {
+            const uint64_t lo = top > tail0 + 256 ? top - 256 : tail0;
+            const uint64_t i = lo + t;
+            if (i < top && tid[i] != tid[i - 1]) atomicMax(&s_e1, (unsigned long long)i);
+            __syncthreads();
+            const bool found = s_e1 != 0;
+            __syncthreads();
+            if (found) break;
+        }
+    }
+    if (t == 0) {
+        constexpr uint64_t kUnknown = ~0ull;  // an edge run longer than the L + 1 records searched
+        cs->append_n = 0;
+        cs->append_at = 0;
+        cs->flush_n = 0;
+        cs->flush_vn = 0;
+        cs->zero = 0;
+        cs->skip = 0;
+        cs->hi = 0;
+        cs->tail_lo = kUnknown;
+        const uint64_t held_tid = cs->tid;
+        auto flush = [&]() {  // the held trace is complete: join it now
+            cs->flush_n = cs->n;
+            cs->flush_vn = cs->verify ? cs->n : 0;
+            cs->n = 0;
+            cs->verify = 0;
+        };
+        bool done = false;
+        if (n == 0) {
+            cs->dropped = 0;
+            flush();
+            done = true;
+        }
+        uint64_t lead = 0;
+        if (!done) {
+            const uint64_t e0 = s_e0, e1 = s_e1;
+            const uint64_t t0 = tid[0], tn = tid[n - 1];
+            // the whole batch is one trace: no boundary in the searched head (all of it when
+            // n <= L + 1), or none in head and tail and the same traceId at both ends (trace-clustered)
+            const bool no_head = e0 == ~0ull, no_tail = e1 == 0;
+            const bool one_run = no_head && (n <= L + 1 || (no_tail && t0 == tn));
+            // end of the leading run, start of the last one (a run longer than L + 1 is only known to
+            // be long; a held run has at most L + 1 records, the carry holds L + 2)
+            const uint64_t first_end = one_run ? n : (no_head ? kUnknown : e0);
+            const uint64_t last_start = one_run ? (n <= L + 1 ? 0 : kUnknown) : (no_tail ? kUnknown : e1);
+            if (cs->n || cs->dropped) {
+                if (t0 == cs->tid) {
+                    lead = first_end;
+                    if (cs->dropped) {
+                        // the rest of a trace already found too long: skipped like its beginning
+                    } else if (lead == kUnknown || cs->n + lead > L) {
+                        cs->n = 0;  // longer than max_trace_records: not aggregated, counted once
+                        cs->dropped = 1;
+                        atomicAdd(too_large, 1ull);
+                    } else {
+                        cs->append_at = cs->n;
+                        cs->append_n = lead;
+                        cs->n += lead;
+                    }
+                }
+                cs->verify |= verify;
+                if (lead == n && continues) {
+                    done = true;  // the whole batch continues the held trace
+                } else {
+                    cs->dropped = 0;
+                    flush();
+                }
+            }
+            if (!done) {
+                uint64_t hi = n;
+                if (continues && last_start != kUnknown) {
+                    // (a last run longer than L + 1 is not held: K1 reports it too large; the leading
+                    // run ends at or before the last run's start unless the batch is one run)
+                    const uint64_t ls = (lead != kUnknown && lead > last_start) ? lead : last_start;
+                    if (ls < n) {
+                        cs->tail_lo = ls;
+                        cs->n = n - ls;
+                        cs->tid = tn;
+                        cs->verify = verify;
+                        hi = ls;
+                    }
+                }
+                cs->hi = hi;
+                cs->skip = lead ? 1u : 0u;  // K1 starts at the first trace boundary after record 0
             }
         }
-        cs->verify |= verify;
-        if (lead == n && continues) {  // the whole batch continues the held trace
-            cs->flush_cnt = 0;
-            return;
+        // who joins a flushed carry: K1 over it (one workgroup, its own spill list, which K1 fills when
+        // the trace outgrows a window) or, for a flush alone, the spill kernel (one list entry)
+        cs->flush_cnt = (!k1_joins && cs->flush_n) ? 1u : 0u;
+        // the held trace's run in the trace set (ZK_BATCH_VERIFY_TRACES): inserted when it is joined
+        if (set && cs->flush_vn) {
+            bool seen;
+            if (held_tid == 0ull)
+                seen = atomicAdd(&set[slots], 1ull) > 0ull;
+            else
+                seen = set_insert(set, slots - 1, held_tid);
+            if (seen) atomicAdd(dup, 1ull);
         }
-        cs->dropped = 0;
-        flush();
+        s_at = cs->append_at;
+        s_len = cs->append_n;
     }
-    cs->flush_cnt = cs->flush_n ? 1u : 0u;
-    uint64_t hi = n;
-    if (continues && last_start != kUnknown) {
-        // (a last run longer than L + 1 is not held: K1 reports it too large; the leading run ends
-        // at or before the last run's start unless the batch is one run)
-        const uint64_t ls = (lead != kUnknown && lead > last_start) ? lead : last_start;
-        if (ls < n) {
-            cs->tail_lo = ls;
-            cs->n = n - ls;
-            cs->tid = tn;
-            cs->verify = verify;
-            hi = ls;
-        }
+    __syncthreads();
+    const uint64_t at = s_at, len = s_len;
+    for (uint64_t k = t; k < len; k += 256) {  // the leading run into the held trace
+        m.trace_id[at + k] = b.trace_id[k];
+        m.span_id[at + k] = b.span_id[k];
+        m.parent_id[at + k] = b.parent_id[k];
+        m.first_ts[at + k] = b.first_ts[k];
+        m.last_ts[at + k] = b.last_ts[k];
+        m.service_id[at + k] = b.service_id[k];
+        m.flags[at + k] = b.flags[k];
     }
-    cs->hi = hi;
-    cs->skip = lead ? 1u : 0u;  // K1 starts at the first trace boundary after record 0
 }
 
-__global__ __launch_bounds__(256) void k_carry_copy(const CarryState* __restrict__ cs, SpanColsDev b, SpanColsMut m,
-                                                    int which) {
-    uint64_t lo, len, at;
-    if (which == 0) {
-        lo = 0;
-        len = cs->append_n;
-        at = cs->append_at;
-    } else {
-        lo = cs->tail_lo;
-        len = lo < b.n ? b.n - lo : 0;
-        at = 0;
-    }
+// the batch's tail [tail_lo, n) -> the carry (after the carry's join has read the old one)
+__global__ __launch_bounds__(256) void k_carry_tail(const CarryState* __restrict__ cs, SpanColsDev b, SpanColsMut m) {
+    const uint64_t lo = cs->tail_lo;
+    const uint64_t len = lo < b.n ? b.n - lo : 0;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < len; k += stride) {
-        const uint64_t i = lo + k, j = at + k;
-        m.trace_id[j] = b.trace_id[i];
-        m.span_id[j] = b.span_id[i];
-        m.parent_id[j] = b.parent_id[i];
-        m.first_ts[j] = b.first_ts[i];
-        m.last_ts[j] = b.last_ts[i];
-        m.service_id[j] = b.service_id[i];
-        m.flags[j] = b.flags[i];
+        const uint64_t i = lo + k;
+        m.trace_id[k] = b.trace_id[i];
+        m.span_id[k] = b.span_id[i];
+        m.parent_id[k] = b.parent_id[i];
+        m.first_ts[k] = b.first_ts[i];
+        m.last_ts[k] = b.last_ts[i];
+        m.service_id[k] = b.service_id[i];
+        m.flags[k] = b.flags[i];
     }
 }
 
@@ -1135,26 +1180,22 @@ hipError_t launch_trace_set_insert(const uint64_t* trace_id, uint64_t n, uint64_
                           (unsigned long long*)set, slots, dup, n_dev, skip_dev);
 }
 
-hipError_t launch_carry_plan(CarryState* cs, const uint64_t* trace_id, uint64_t n, uint64_t max_trace,
-                             uint32_t continues, uint32_t verify, unsigned long long* too_large, hipStream_t s) {
-    return launch_checked("k_carry_plan", k_carry_plan, dim3(1), dim3(64), 0, s, cs, trace_id, n, max_trace, continues,
-                          verify, too_large);
+hipError_t launch_carry_plan(CarryState* cs, const SpanColsDev& batch, const SpanColsMut& carry, uint64_t max_trace,
+                             uint32_t continues, uint32_t verify, uint32_t k1_joins, unsigned long long* too_large,
+                             unsigned int* spill_count, uint64_t* set, uint64_t slots, unsigned long long* dup,
+                             hipStream_t s) {
+    return launch_checked("k_carry_plan", k_carry_plan, dim3(1), dim3(256), 0, s, cs, batch, carry, max_trace,
+                          continues, verify, k1_joins, too_large, spill_count, (unsigned long long*)set, slots, dup);
 }
 
-hipError_t launch_carry_copy(const CarryState* cs, const SpanColsDev& batch, const SpanColsMut& carry, int which,
-                             hipStream_t s) {
-    return launch_checked("k_carry_copy", k_carry_copy, dim3(64), dim3(256), 0, s, cs, batch, carry, which);
+hipError_t launch_carry_tail(const CarryState* cs, const SpanColsDev& batch, const SpanColsMut& carry, hipStream_t s) {
+    return launch_checked("k_carry_tail", k_carry_tail, dim3(64), dim3(256), 0, s, cs, batch, carry);
 }
 
 hipError_t launch_trace_set_rehash(const uint64_t* old, uint64_t old_slots, uint64_t* set, uint64_t slots,
                                    hipStream_t s) {
     return launch_checked("k_trace_set_rehash", k_trace_set_rehash, dim3(grid_for(old_slots + 1)), dim3(256), 0, s,
                           (const unsigned long long*)old, old_slots, (unsigned long long*)set, slots);
-}
-
-hipError_t launch_edge_runs(const uint64_t* trace_id, uint64_t n, uint64_t L, unsigned long long* out, hipStream_t s) {
-    if (n < 2) return hipSuccess;
-    return launch_checked("k_edge_runs", k_edge_runs, dim3(64), dim3(256), 0, s, trace_id, n, L, out);
 }
 
 hipError_t launch_stat_add(unsigned long long* slot, uint64_t v, hipStream_t s) {

@@ -49,9 +49,19 @@ __device__ __forceinline__ uint64_t d_mix64(uint64_t z) {
 
 __device__ __forceinline__ uint64_t d_hash(const uint8_t* s, uint32_t n) {  // == zk_hash_string
     uint64_t h = 0xCBF29CE484222325ull;
-    for (uint32_t i = 0; i < n; ++i) {
-        h ^= s[i];
-        h *= 0x100000001B3ull;
+    // 16 bytes' loads issued before the multiply chain consumes them (one round trip per 16 bytes
+    // instead of one per byte)
+    for (uint32_t i0 = 0; i0 < n; i0 += 16) {
+        uint8_t v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = i0 + j < n ? s[i0 + j] : 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (i0 + j < n) {
+                h ^= v[j];
+                h *= 0x100000001B3ull;
+            }
+        }
     }
     h = d_mix64(h);
     return h ? h : 1ull;
@@ -889,8 +899,18 @@ __device__ __forceinline__ bool try_resolve(const IngArgs& a, uint64_t i, const 
     const uint32_t id = a.d_id[slot];
     if (id == kNoId || id >= a.max_services || a.d_len[slot] != nl) return false;
     const uint8_t* y = (const uint8_t*)(uintptr_t)a.d_ptr[slot];
-    for (uint32_t q = 0; q < nl; ++q)
-        if (nm[q] != y[q]) return false;
+    for (uint32_t q0 = 0; q0 < nl; q0 += 16) {  // 16 bytes of each side in flight at once
+        uint8_t u[16], v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            u[j] = q0 + j < nl ? nm[q0 + j] : 0;
+            v[j] = q0 + j < nl ? y[q0 + j] : 0;
+        }
+        bool eq = true;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) eq &= u[j] == v[j];
+        if (!eq) return false;
+    }
     a.svc[i] = id;
     return true;
 }

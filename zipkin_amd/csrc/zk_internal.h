@@ -132,7 +132,8 @@ struct JoinArgs {
 };
 
 // host-side launchers (implemented in the .hip files)
-hipError_t launch_join(const JoinArgs& a, hipStream_t s);
+// blocks != 0: only workgroups [0, blocks) of the a.grid geometry (K1 joining a held trace)
+hipError_t launch_join(const JoinArgs& a, hipStream_t s, uint32_t blocks = 0);
 // group join: one workgroup per CU; workgroup w owns the sub-buckets starting in [w*per_wg, (w+1)*per_wg)
 hipError_t launch_group_join(const JoinArgs& a, hipStream_t s);
 // geometry of the group join and of K1 as its fallback, sharing one set of link lists

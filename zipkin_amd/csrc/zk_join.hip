@@ -1454,9 +1454,9 @@ uint64_t spill_scratch_bytes_per_wg(uint32_t max_trace) {
     return (b + 255) & ~255ull;
 }
 
-hipError_t launch_join(const JoinArgs& a, hipStream_t s) {
+hipError_t launch_join(const JoinArgs& a, hipStream_t s, uint32_t blocks) {
     if (a.c.n == 0) return hipSuccess;
-    const dim3 g((unsigned)a.grid), b(kTileWG);
+    const dim3 g((unsigned)(blocks ? blocks : a.grid)), b(kTileWG);
     const bool emit = a.rt_pay != nullptr, join = a.join != 0;
     if (emit && join)
         return launch_checked("k_span_join_stream<join|emit>", k_span_join_stream<kTile, kTileWG, kModeJoin | kModeEmit>,
