@@ -162,3 +162,45 @@ def test_held_trace_then_a_batch_in_any_order(gpu, verify):
                 continue
             got, st = ctx.finalize(), ctx.stats()
         assert_parity(got, st, ref)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_random_streams_equal_the_oracle(gpu, seed):
+    """The device-side held-trace state machine under random streams: TraceGen traces with long star
+    traces (600-3000 records, longer than K1's 512-record window) mixed in, cut at random points
+    (inside traces, at trace boundaries, 1-record batches, a batch inside one trace), empty CONTINUES
+    batches between them, host and device pointers and ZK_BATCH_VERIFY_TRACES chosen per batch. Each
+    stream equals the oracle over the whole stream, bit for bit, with no clustering report."""
+    rng = np.random.default_rng(seed)
+    S = 41
+    base = tracegen_host(1000 + seed, 3_000, max_depth=5, num_services=S)
+    tid = base.trace_id
+    starts = np.flatnonzero(np.r_[True, tid[1:] != tid[:-1]])
+    bounds = list(starts) + [len(base)]
+    pieces, big_at = [], set(rng.choice(len(starts), 6, replace=False).tolist())
+    for t in range(len(starts)):
+        pieces.append(base.take(slice(bounds[t], bounds[t + 1])))
+        if t in big_at:
+            n_children = int(rng.integers(300, 1500))
+            pieces.append(cols_from_rows(star_trace(0xB16000 + 97 * t + seed, n_children, svc_root=t % S, nsvc=S)))
+    cols = SpanColumns.concat(pieces)
+    n = len(cols)
+    ref = oracle.aggregate(cols, S)
+    tid = cols.trace_id
+    tstarts = np.flatnonzero(np.r_[True, tid[1:] != tid[:-1]])
+    cuts = set(rng.choice(np.arange(1, n), 25, replace=False).tolist())  # mostly inside traces
+    cuts |= set(rng.choice(tstarts[1:], 8, replace=False).tolist())  # at trace boundaries
+    c0 = int(rng.integers(1, n - 2))
+    cuts |= {c0, c0 + 1}  # a one-record batch
+    parts = cut(cols, sorted(cuts))
+    with DepsContext(S) as ctx:
+        for i, p in enumerate(parts):
+            dev = bool(rng.integers(0, 2))
+            b = DeviceColumns.from_host(p) if dev else p
+            ctx.accumulate(b, clustered=True, verify=bool(rng.integers(0, 2)), continues=i + 1 < len(parts))
+            if rng.random() < 0.15:
+                ctx.accumulate(SpanColumns.empty(0), clustered=True, continues=True)
+        got, st = ctx.finalize(), ctx.stats()
+    assert_parity(got, st, ref)
+    assert st["not_clustered"] == 0
+    assert st["records"] == n

@@ -88,6 +88,10 @@ class DepsContext:
             raise _abi.ZkError(st, _abi.status_str(st))
         self._h = h
         self.num_services = num_services
+        # device batches accumulated since the last drain: their memory must outlive the ctx stream's
+        # reads (zkagg.h), and a torch tensor dropped by the caller returns to torch's caching
+        # allocator at once, where the next allocation may reuse it while the ctx stream still reads
+        self._inflight: list = []
 
     # -- plumbing ---------------------------------------------------------------------------
     def _check(self, st: int) -> None:
@@ -96,8 +100,9 @@ class DepsContext:
 
     def close(self) -> None:
         if getattr(self, "_h", None):
-            self._L.zk_ctx_destroy(self._h)
+            self._L.zk_ctx_destroy(self._h)  # (drains the stream)
             self._h = None
+        self._inflight = []
 
     def __enter__(self):
         return self
@@ -118,6 +123,13 @@ class DepsContext:
     # -- dependency path --------------------------------------------------------------------
     def reset(self) -> None:
         self._check(self._L.zk_deps_reset(self._h))
+
+    _MAX_INFLIGHT = 8  # device batches kept alive before a drain
+
+    def _hold(self, cols) -> None:
+        self._inflight.append(cols)
+        if len(self._inflight) > self._MAX_INFLIGHT:
+            self.sync()
 
     def accumulate(self, cols, *, clustered: bool = False, verify: bool = True, n: int | None = None,
                    continues: bool = False) -> None:
@@ -141,6 +153,7 @@ class DepsContext:
         if isinstance(cols, DeviceColumns):
             ab = cols.abi(n)
             flags |= _abi.ZK_BATCH_DEVICE_PTRS
+            self._hold(cols)
         elif isinstance(cols, SpanColumns):
             ab = cols.abi()
         else:
@@ -159,7 +172,8 @@ class DepsContext:
             for k in ("m0", "m1", "m2", "m3", "m4", "present"):
                 setattr(t, k, out_device[k].data_ptr())
             t.device_ptrs = 1
-            self._check(self._L.zk_deps_finalize(self._h, C.byref(t)))
+            self._check(self._L.zk_deps_finalize(self._h, C.byref(t)))  # (waits for the counters)
+            self._inflight = []
             return None
         # (finalize writes every cell) into page-locked host memory when torch has it: the device
         # copies then land directly (~2x the pageable rate for the 41 B per cell)
@@ -171,7 +185,8 @@ class DepsContext:
         t.m1, t.m2, t.m3, t.m4 = (a.ctypes.data for a in ms)
         t.present = pr.ctypes.data
         t.device_ptrs = 0
-        self._check(self._L.zk_deps_finalize(self._h, C.byref(t)))
+        self._check(self._L.zk_deps_finalize(self._h, C.byref(t)))  # (synchronous)
+        self._inflight = []
         return LinkTable(S, m0, *ms, pr)
 
     def stats(self) -> dict:
@@ -186,6 +201,7 @@ class DepsContext:
 
     def sync(self) -> None:
         self._check(self._L.zk_ctx_sync(self._h))
+        self._inflight = []
 
     def partial(self) -> tuple[int, int]:
         """(device pointer, bytes) of the exact table + counter tail, counters folded in (enqueued

@@ -42,6 +42,13 @@ class KvSketch:
         self._check(self._L.zk_kv_geometry(h, C.byref(w), C.byref(d), C.byref(c)))
         self.width, self.depth, self.candidates = w.value, d.value, c.value
         self.seed = seed
+        self._inflight: list = []  # device batches the stream may still read (see DepsContext._hold)
+
+    def _drain(self) -> None:
+        """Wait for the sketch's stream (zk_kv_totals synchronises it) and release held batches."""
+        tot = np.zeros(self.num_services, np.uint64)
+        self._check(self._L.zk_kv_totals(self._h, tot.ctypes.data))
+        self._inflight = []
 
     def _check(self, st: int) -> None:
         if st != _abi.ZK_OK:
@@ -55,8 +62,9 @@ class KvSketch:
 
     def close(self) -> None:
         if getattr(self, "_h", None):
-            self._L.zk_kv_destroy(self._h)
+            self._L.zk_kv_destroy(self._h)  # (drains the stream)
             self._h = None
+        self._inflight = []
 
     def __enter__(self):
         return self
@@ -91,6 +99,10 @@ class KvSketch:
             k = np.ascontiguousarray(np.asarray(key_hash).view(np.uint64) if np.asarray(key_hash).dtype == np.int64
                                      else key_hash, dtype=np.uint64)
         self._check(self._L.zk_kv_accumulate(self._h, _ptr(s), _ptr(k), n, flags))
+        if flags:
+            self._inflight.append((s, k))
+            if len(self._inflight) > 8:
+                self._drain()
 
     def topk_all(self, k: int):
         """(keys uint64[S, k], est uint32[S, k], count uint32[S]); row s best first."""

@@ -97,6 +97,12 @@ class RtSketch:
             t = np.ascontiguousarray(t.view(np.uint64) if t.dtype == np.int64 else t, dtype=np.uint64)
             d = np.ascontiguousarray(duration, dtype=np.int64)
         self._check(self._L.zk_rt_accumulate_merged(self._h, _ptr(s), _ptr(t), _ptr(d), n, flags))
+        if flags:  # device batches the stream may still read (see DepsContext._hold)
+            inflight = self.__dict__.setdefault("_inflight", [])
+            inflight.append((s, t, d))
+            if len(inflight) > 8:
+                self._check(self._L.zk_rt_dropped(self._h, None, None))  # (synchronises the stream)
+                inflight.clear()
 
     def distinct_traces(self) -> np.ndarray:
         out = np.zeros(self.num_services, np.float64)
