@@ -49,6 +49,9 @@ extern "C" {
 #define ZK_CODEC_SNAPPY_THRIFT 1u  /* raw Snappy block of the above (the stored Cassandra value) */
 
 #define ZK_INGEST_STRICT 1u        /* fail the batch on the first span the reference rejects */
+#define ZK_INGEST_ONE_THREAD 2u    /* host decoder: decode on the calling thread only (by default up to
+                                      16 threads decode contiguous ranges; records, items, service ids
+                                      and errors are the same either way) */
 /* Both decoders (host zk_ingest_spans, device zk_ingest_dev_spans) reject a Snappy fragment whose
  * header announces more than ZK_INGEST_MAX_FRAGMENT bytes, or more than the format can expand its
  * payload to (a 3-byte copy emits at most 64 bytes: < ZK_SNAPPY_MAX_EXPANSION x), before any

@@ -573,3 +573,54 @@ def test_device_decoded_bytes_to_dependencies(gpu):
         got = ctx.finalize()
     ref = aggregate_job(spans, strict=False)
     assert {(names[p], names[c]): tuple(m) for p, c, m in got.links()} == {k: tuple(m) for k, m in ref.exact().items()}
+
+
+# ---- the host decoder's threads ------------------------------------------------------------------
+def _decode_both(blobs, **kw):
+    one, many = SpanDecoder(), SpanDecoder()
+    out = []
+    for dec, flag in ((one, True), (many, False)):
+        try:
+            out.append(("ok", dec.decode(blobs, one_thread=flag, **kw), dec.service_names()))
+        except ZkError as e:
+            out.append(("err", (e.status, e.message), dec.service_names()))
+    return out
+
+
+@pytest.mark.parametrize("strict", [False, True])
+def test_threaded_decode_equals_one_thread(strict):
+    """A batch large enough for several decode threads (contiguous ranges, then one ordered commit)
+    gives the records, items (in order), service ids, rejected count and first error of a one-thread
+    decode -- with bad and undecodable fragments spread over every range."""
+    spans = gen_traces(61, 1200, max_depth=5, anomalies=0.3)
+    blobs = encode_all(spans)
+    assert len(blobs) >= 8 * 2048, len(blobs)
+    ok, bads = bad_spans()
+    rnd = random.Random(61)
+    for k in range(24):  # lenient: skipped and counted; strict: the first one fails the batch
+        at = rnd.randrange(len(blobs)) if k else len(blobs) // 2 + 3
+        blobs.insert(at, T.snappy(bads[k % len(bads)][1]) if k % 3 else b"\x7f\x00garbage")
+    a, b = _decode_both(blobs, strict=strict, items=True)
+    assert a[0] == b[0] == ("err" if strict else "ok")
+    assert a[2] == b[2]  # the dictionary, ids in order of first appearance
+    if strict:
+        assert a[1] == b[1]
+        return
+    (ca, ra, kva, ana), (cb, rb, kvb, anb) = a[1], b[1]
+    assert ra == rb == 24
+    assert records(ca) == records(cb)
+    for x, y in zip(kva + ana, kvb + anb):
+        assert np.array_equal(x, y)
+
+
+def test_threaded_decode_bad_offsets_and_item_overflow():
+    spans = gen_traces(62, 1000, max_depth=5)
+    blobs = encode_all(spans)
+    a, b = _decode_both(blobs, items=True, item_cap=5000)
+    assert a[0] == b[0] == "err" and a[1] == b[1] and a[1][0] == _abi.ZK_ERR_CAPACITY and a[2] == b[2]
+    buf = np.frombuffer(b"".join(blobs), dtype=np.uint8)
+    offs = np.zeros(len(blobs) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in blobs])
+    offs[len(blobs) * 3 // 4] = offs[len(blobs) * 3 // 4 + 1] + 1  # not ascending, in a later range
+    a, b = _decode_both((buf, offs), strict=False)
+    assert a[0] == b[0] == "err" and a[1] == b[1] and a[1][0] == _abi.ZK_ERR_INVALID_ARG and a[2] == b[2]

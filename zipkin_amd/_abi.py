@@ -207,6 +207,7 @@ class zk_ingest_items(C.Structure):
 ZK_CODEC_THRIFT = 0
 ZK_CODEC_SNAPPY_THRIFT = 1
 ZK_INGEST_STRICT = 1
+ZK_INGEST_ONE_THREAD = 2
 
 
 class zk_moments(C.Structure):

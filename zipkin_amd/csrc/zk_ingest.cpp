@@ -7,6 +7,7 @@
 #include <string.h>
 
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -353,6 +354,182 @@ uint64_t mix64(uint64_t z) {
 
 }  // namespace
 
+// ---- phase 1 of zk_ingest_spans: one thread's range of fragments -------------------------------
+constexpr uint32_t kIngestThreads = 16;          // decode threads (the GPU box gives a process 16 CPUs)
+constexpr uint64_t kIngestMinPerThread = 2048;   // fragments per thread at least
+
+struct Item {
+    int32_t name;  // the host's service name: index into DecodeRange::names
+    uint32_t str;  // the key / value string: index into DecodeRange::strs
+    uint64_t hash;
+};
+struct Decoded {
+    uint64_t index;  // fragment index in the batch
+    uint64_t tid, sid, pid;
+    int64_t first, last;
+    uint32_t flags;
+    int32_t svc_name;  // -1: no service
+    uint32_t kv0, kv_n, ann0, ann_n;
+};
+struct DecodeRange {
+    uint64_t lo = 0, hi = 0;
+    std::vector<Decoded> recs;
+    std::vector<Item> kv, ann;
+    std::vector<std::string> names, strs;
+    std::unordered_map<std::string, int32_t> name_ix;
+    std::unordered_map<uint64_t, uint32_t> str_ix;
+    uint64_t rejected = 0;
+    uint64_t err_index = UINT64_MAX;  // first fragment that fails the batch (strict / bad offsets)
+    zk_status err_status = ZK_OK;
+    std::string err;
+
+    int32_t name(const Host& h) {  // thrift.scala:36-43: null or "" -> Endpoint.UnknownServiceName
+        std::string s = (h.svc && h.svc_len) ? std::string(h.svc, h.svc_len) : std::string(kUnknownService);
+        auto it = name_ix.find(s);
+        if (it != name_ix.end()) return it->second;
+        const int32_t ix = (int32_t)names.size();
+        name_ix.emplace(s, ix);
+        names.push_back(std::move(s));
+        return ix;
+    }
+    Item item(const Host& h, const char* s, uint32_t l) {
+        const uint64_t hash = zk_hash_string(s, l);
+        auto it = str_ix.find(hash);
+        uint32_t ix;
+        if (it != str_ix.end()) {
+            ix = it->second;
+        } else {
+            ix = (uint32_t)strs.size();
+            str_ix.emplace(hash, ix);
+            strs.emplace_back(s ? s : "", s ? l : 0);
+        }
+        return Item{name(h), ix, hash};
+    }
+};
+
+void decode_range(const uint8_t* buf, const uint64_t* offsets, uint32_t codec, bool strict, bool want_kv,
+                  bool want_ann, DecodeRange* d) {
+    std::vector<uint8_t> scratch;
+    SpanT s;
+    std::vector<const Ann*> distinct;
+    d->recs.reserve(d->hi - d->lo);
+    for (uint64_t i = d->lo; i < d->hi; ++i) {
+        if (offsets[i + 1] < offsets[i]) {
+            d->err_index = i;
+            d->err_status = ZK_ERR_INVALID_ARG;
+            d->err = "offsets not ascending at span " + std::to_string(i);
+            return;
+        }
+        const uint8_t* p = buf + offsets[i];
+        uint64_t len = offsets[i + 1] - offsets[i];
+        if (codec == ZK_CODEC_SNAPPY_THRIFT) {
+            if (!snappy_uncompress(p, len, &scratch)) {
+                if (strict) {
+                    d->err_index = i;
+                    d->err_status = ZK_ERR_INVALID_SPAN;
+                    d->err = "span " + std::to_string(i) + ": corrupt snappy block";
+                    return;
+                }
+                ++d->rejected;
+                continue;
+            }
+            p = scratch.data();
+            len = scratch.size();
+        }
+        s.clear();
+        Rd r{p, p + len};
+        const char* why = nullptr;
+        if (!read_span(r, &s))
+            why = "undecodable thrift span";
+        else if (!s.has_name)
+            why = "No name set in Span";  // IncompleteTraceDataException (thrift.scala:101-104)
+        else
+            for (const Ann& a : s.anns) {
+                if (a.ts <= 0) {
+                    why = "Annotation must have a timestamp";  // thrift.scala:66-67
+                    break;
+                }
+                if (a.value && a.value_len == 0) {
+                    why = "Annotation must have a value";  // thrift.scala:69-70
+                    break;
+                }
+            }
+        if (why) {
+            if (strict) {
+                d->err_index = i;
+                d->err_status = ZK_ERR_INVALID_SPAN;
+                d->err = "span " + std::to_string(i) + ": " + why;
+                return;
+            }
+            ++d->rejected;
+            continue;
+        }
+        // ---- the record (SURVEY Appendix A.1) ----
+        uint32_t f = s.has_parent ? ZK_F_HAS_PARENT : 0u;
+        int64_t first = 0, last = 0;
+        uint32_t cnt[4] = {0, 0, 0, 0};  // cs, cr, sr, ss
+        const Host* srv = nullptr;
+        const Host* cli = nullptr;
+        for (size_t q = 0; q < s.anns.size(); ++q) {
+            const Ann& a = s.anns[q];
+            if (q == 0 || a.ts < first) first = a.ts;
+            if (q == 0 || a.ts > last) last = a.ts;
+            if (is_core(a.value, a.value_len)) {
+                const int c = a.value[0] == 'c' ? (a.value[1] == 's' ? 0 : 1) : (a.value[1] == 'r' ? 2 : 3);
+                if (cnt[c] < 2) ++cnt[c];
+                if (a.host.present) {
+                    if (c >= 2 && !srv) srv = &a.host;
+                    if (c < 2 && !cli) cli = &a.host;
+                }
+            }
+        }
+        if (!s.anns.empty()) f |= ZK_F_HAS_ANNOTATIONS;
+        int32_t svc = -1;
+        if (srv) {
+            f |= ZK_F_SVC_SERVER;
+            svc = d->name(*srv);
+        } else if (cli) {
+            f |= ZK_F_SVC_CLIENT;
+            svc = d->name(*cli);
+        }
+        f |= (cnt[0] << ZK_F_CS_SHIFT) | (cnt[1] << ZK_F_CR_SHIFT) | (cnt[2] << ZK_F_SR_SHIFT) | (cnt[3] << ZK_F_SS_SHIFT);
+        Decoded rec{i, (uint64_t)s.trace_id, (uint64_t)s.id, s.has_parent ? (uint64_t)s.parent_id : 0ull,
+                    s.anns.empty() ? 0 : first, s.anns.empty() ? 0 : last, f, svc,
+                    (uint32_t)d->kv.size(), 0u, (uint32_t)d->ann.size(), 0u};
+        // ---- indexer items: only spans with a last annotation (CassieSpanStore.scala:214-218) ----
+        if (!s.anns.empty()) {
+            if (want_kv)
+                for (const BinAnn& b : s.banns)  // :235-241 one per binary annotation with a host
+                    if (b.host.present) d->kv.push_back(d->item(b.host, b.key, b.key_len));
+            if (want_ann) {
+                // :222-233 non-core annotations grouped by value; the group's min (Annotation.compare:
+                // (a.timestamp - b.timestamp).toInt, Annotation.scala:36-38; min keeps the first of
+                // equals) yields one item if it has a host
+                distinct.clear();
+                for (const Ann& a : s.anns) {
+                    if (is_core(a.value, a.value_len)) continue;
+                    bool seen = false;
+                    for (const Ann*& dd : distinct) {
+                        if (dd->value_len == a.value_len &&
+                            (a.value_len == 0 || memcmp(dd->value, a.value, a.value_len) == 0) &&
+                            (dd->value == nullptr) == (a.value == nullptr)) {
+                            if ((int32_t)(uint32_t)((uint64_t)dd->ts - (uint64_t)a.ts) > 0) dd = &a;  // truncated compare
+                            seen = true;
+                            break;
+                        }
+                    }
+                    if (!seen) distinct.push_back(&a);
+                }
+                for (const Ann* a : distinct)
+                    if (a->host.present) d->ann.push_back(d->item(a->host, a->value, a->value_len));
+            }
+        }
+        rec.kv_n = (uint32_t)d->kv.size() - rec.kv0;
+        rec.ann_n = (uint32_t)d->ann.size() - rec.ann0;
+        d->recs.push_back(rec);
+    }
+}
+
 struct zk_ingest {
     std::unordered_map<std::string, uint32_t> svc_ids;
     std::vector<std::string> svc_names;
@@ -383,6 +560,9 @@ struct zk_ingest {
         const uint64_t h = zk_hash_string(s, l);
         if (strings.find(h) == strings.end()) strings.emplace(h, std::string(s ? s : "", s ? l : 0));
         return h;
+    }
+    void keep(uint64_t h, const std::string& s) {  // the string behind a hash (the first one seen)
+        if (strings.find(h) == strings.end()) strings.emplace(h, s);
     }
 };
 
@@ -445,6 +625,43 @@ zk_status zk_ingest_spans(zk_ingest* g, const uint8_t* buf, const uint64_t* offs
         g->err = "unknown codec";
         return ZK_ERR_INVALID_ARG;
     }
+    const bool strict = (flags & ZK_INGEST_STRICT) != 0;
+    const bool want_kv = items && items->kv_service && items->kv_key;
+    const bool want_ann = items && items->ann_service && items->ann_value;
+    // Phase 1, in parallel over contiguous fragment ranges: decode and validate every fragment into
+    // a thread-local list (names copied into the thread's own table). Phase 2, in input order on
+    // this thread: assign service ids (in order of first appearance, exactly as a one-pass decode
+    // would), write the records and items, intern the strings, stop at the first error.
+    uint32_t T = std::thread::hardware_concurrency();
+    T = T < 1 ? 1 : T > kIngestThreads ? kIngestThreads : T;
+    if (flags & ZK_INGEST_ONE_THREAD) T = 1;
+    if (n / kIngestMinPerThread < T) T = (uint32_t)(n / kIngestMinPerThread) > 1 ? (uint32_t)(n / kIngestMinPerThread) : 1;
+    std::vector<DecodeRange> part(T);
+    auto work = [&](uint32_t t) noexcept {  // (nothing may escape a worker thread)
+        DecodeRange& d = part[t];
+        d.lo = n * t / T;
+        d.hi = n * (t + 1) / T;
+        try {
+            decode_range(buf, offsets, codec, strict, want_kv, want_ann, &d);
+        } catch (...) {
+            d.err_index = d.lo;
+            d.err_status = ZK_ERR_CAPACITY;
+            d.err = "host allocation failed";
+        }
+    };
+    std::vector<std::thread> th;
+    uint32_t started = 1;
+    try {
+        th.reserve(T - 1);
+        for (uint32_t t = 1; t < T; ++t) {
+            th.emplace_back(work, t);
+            ++started;
+        }
+    } catch (...) {  // a thread that cannot start: its range and the rest run here
+    }
+    for (uint32_t t = started; t < T; ++t) work(t);
+    work(0);
+    for (auto& x : th) x.join();
     uint64_t* o_tid = (uint64_t*)out->trace_id;
     uint64_t* o_sid = (uint64_t*)out->span_id;
     uint64_t* o_pid = (uint64_t*)out->parent_id;
@@ -452,135 +669,60 @@ zk_status zk_ingest_spans(zk_ingest* g, const uint8_t* buf, const uint64_t* offs
     int64_t* o_last = (int64_t*)out->last_ts;
     uint32_t* o_svc = (uint32_t*)out->service_id;
     uint32_t* o_flags = (uint32_t*)out->flags;
-    const bool strict = (flags & ZK_INGEST_STRICT) != 0;
     bool item_overflow = false;
     uint64_t k = 0;
-    std::vector<const Ann*> distinct;
-    for (uint64_t i = 0; i < n; ++i) {
-        if (offsets[i + 1] < offsets[i]) {
-            g->err = "offsets not ascending at span " + std::to_string(i);
-            return ZK_ERR_INVALID_ARG;
-        }
-        const uint8_t* p = buf + offsets[i];
-        uint64_t len = offsets[i + 1] - offsets[i];
-        if (codec == ZK_CODEC_SNAPPY_THRIFT) {
-            if (!snappy_uncompress(p, len, &g->scratch)) {
-                if (strict) {
-                    g->err = "span " + std::to_string(i) + ": corrupt snappy block";
-                    return ZK_ERR_INVALID_SPAN;
-                }
-                ++*n_rejected;
-                continue;
-            }
-            p = g->scratch.data();
-            len = g->scratch.size();
-        }
-        SpanT& s = g->span;
-        s.clear();
-        Rd r{p, p + len};
-        const char* why = nullptr;
-        if (!read_span(r, &s))
-            why = "undecodable thrift span";
-        else if (!s.has_name)
-            why = "No name set in Span";  // IncompleteTraceDataException (thrift.scala:101-104)
-        else
-            for (const Ann& a : s.anns) {
-                if (a.ts <= 0) {
-                    why = "Annotation must have a timestamp";  // thrift.scala:66-67
-                    break;
-                }
-                if (a.value && a.value_len == 0) {
-                    why = "Annotation must have a value";  // thrift.scala:69-70
-                    break;
-                }
-            }
-        if (why) {
-            if (strict) {
-                g->err = "span " + std::to_string(i) + ": " + why;
-                return ZK_ERR_INVALID_SPAN;
-            }
-            ++*n_rejected;
-            continue;
-        }
-        // ---- the record (SURVEY Appendix A.1) ----
-        uint32_t f = s.has_parent ? ZK_F_HAS_PARENT : 0u;
-        int64_t first = 0, last = 0;
-        uint32_t cnt[4] = {0, 0, 0, 0};  // cs, cr, sr, ss
-        const Host* srv = nullptr;
-        const Host* cli = nullptr;
-        for (size_t q = 0; q < s.anns.size(); ++q) {
-            const Ann& a = s.anns[q];
-            if (q == 0 || a.ts < first) first = a.ts;
-            if (q == 0 || a.ts > last) last = a.ts;
-            if (is_core(a.value, a.value_len)) {
-                const int c = a.value[0] == 'c' ? (a.value[1] == 's' ? 0 : 1) : (a.value[1] == 'r' ? 2 : 3);
-                if (cnt[c] < 2) ++cnt[c];
-                if (a.host.present) {
-                    if (c >= 2 && !srv) srv = &a.host;
-                    if (c < 2 && !cli) cli = &a.host;
-                }
-            }
-        }
-        if (!s.anns.empty()) f |= ZK_F_HAS_ANNOTATIONS;
-        uint32_t svc = 0;
-        if (srv) {
-            f |= ZK_F_SVC_SERVER;
-            svc = g->service(*srv);
-        } else if (cli) {
-            f |= ZK_F_SVC_CLIENT;
-            svc = g->service(*cli);
-        }
-        f |= (cnt[0] << ZK_F_CS_SHIFT) | (cnt[1] << ZK_F_CR_SHIFT) | (cnt[2] << ZK_F_SR_SHIFT) | (cnt[3] << ZK_F_SS_SHIFT);
-        o_tid[k] = (uint64_t)s.trace_id;
-        o_sid[k] = (uint64_t)s.id;
-        o_pid[k] = s.has_parent ? (uint64_t)s.parent_id : 0ull;
-        o_first[k] = s.anns.empty() ? 0 : first;
-        o_last[k] = s.anns.empty() ? 0 : last;
-        o_svc[k] = svc;
-        o_flags[k] = f;
-        ++k;
-        // ---- indexer items: only spans with a last annotation (CassieSpanStore.scala:214-218) ----
-        if (!items || s.anns.empty()) continue;
-        if (items->kv_service && items->kv_key) {
-            for (const BinAnn& b : s.banns) {  // :235-241 one per binary annotation with a host
-                if (!b.host.present) continue;
+    for (uint32_t t = 0; t < T; ++t) {
+        DecodeRange& d = part[t];
+        std::vector<int64_t> gid(d.names.size(), -1);
+        auto id_of = [&](int32_t name) -> uint32_t {
+            if (gid[name] < 0) gid[name] = g->exact(d.names[name]);
+            return (uint32_t)gid[name];
+        };
+        std::vector<uint8_t> kept(d.strs.size(), 0);  // strings of this range already interned
+        auto keep = [&](const Item& it) {
+            if (kept[it.str]) return;
+            kept[it.str] = 1;
+            g->keep(it.hash, d.strs[it.str]);
+        };
+        for (const Decoded& r : d.recs) {
+            if (r.index >= d.err_index) break;  // records after this range's first error are not committed
+            uint32_t svc = 0;
+            if (r.svc_name >= 0) svc = id_of(r.svc_name);
+            o_tid[k] = r.tid;
+            o_sid[k] = r.sid;
+            o_pid[k] = r.pid;
+            o_first[k] = r.first;
+            o_last[k] = r.last;
+            o_svc[k] = svc;
+            o_flags[k] = r.flags;
+            ++k;
+            for (uint32_t q = r.kv0; q < r.kv0 + r.kv_n; ++q) {  // :235-241 one per binary annotation with a host
                 if (items->kv_n >= items->kv_cap) {
                     item_overflow = true;
                     continue;
                 }
-                items->kv_service[items->kv_n] = g->service(b.host);
-                items->kv_key[items->kv_n] = g->intern(b.key, b.key_len);
+                const Item& it = d.kv[q];
+                items->kv_service[items->kv_n] = id_of(it.name);
+                items->kv_key[items->kv_n] = it.hash;
+                keep(it);
                 ++items->kv_n;
             }
-        }
-        if (items->ann_service && items->ann_value) {
-            // :222-233 non-core annotations grouped by value; the group's min (Annotation.compare:
-            // (a.timestamp - b.timestamp).toInt, Annotation.scala:36-38; min keeps the first of
-            // equals) yields one item if it has a host
-            distinct.clear();
-            for (const Ann& a : s.anns) {
-                if (is_core(a.value, a.value_len)) continue;
-                bool seen = false;
-                for (const Ann*& d : distinct) {
-                    if (d->value_len == a.value_len && (a.value_len == 0 || memcmp(d->value, a.value, a.value_len) == 0) &&
-                        (d->value == nullptr) == (a.value == nullptr)) {
-                        if ((int32_t)(uint32_t)((uint64_t)d->ts - (uint64_t)a.ts) > 0) d = &a;  // truncated compare
-                        seen = true;
-                        break;
-                    }
-                }
-                if (!seen) distinct.push_back(&a);
-            }
-            for (const Ann* a : distinct) {
-                if (!a->host.present) continue;
+            for (uint32_t q = r.ann0; q < r.ann0 + r.ann_n; ++q) {
                 if (items->ann_n >= items->ann_cap) {
                     item_overflow = true;
                     continue;
                 }
-                items->ann_service[items->ann_n] = g->service(a->host);
-                items->ann_value[items->ann_n] = g->intern(a->value, a->value_len);
+                const Item& it = d.ann[q];
+                items->ann_service[items->ann_n] = id_of(it.name);
+                items->ann_value[items->ann_n] = it.hash;
+                keep(it);
                 ++items->ann_n;
             }
+        }
+        *n_rejected += d.rejected;
+        if (d.err_index != UINT64_MAX) {  // the first error of the batch (ranges are in input order)
+            g->err = d.err;
+            return d.err_status;
         }
     }
     *n_out = k;

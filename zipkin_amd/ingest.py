@@ -44,11 +44,13 @@ class SpanDecoder:
             raise _abi.ZkError(st, self._L.zk_ingest_last_error(self._h).decode() or _abi.status_str(st))
 
     def decode(self, blobs, *, snappy: bool = True, strict: bool = True, items: bool = False,
-               item_cap: int | None = None):
+               item_cap: int | None = None, one_thread: bool = False):
         """Decode stored fragments: a sequence of bytes objects (one per fragment), or the packed
         form (buf uint8[total], offsets uint64[n + 1]) -- fragment i is buf[offsets[i]:offsets[i+1]].
         Returns (SpanColumns, rejected) or, with items=True, (SpanColumns, rejected,
-        (kv_service, kv_key), (ann_service, ann_value))."""
+        (kv_service, kv_key), (ann_service, ann_value)). one_thread: decode on the calling thread
+        only (ZK_INGEST_ONE_THREAD; the default splits large batches over up to 16 threads, with the
+        same results)."""
         if isinstance(blobs, tuple) and len(blobs) == 2 and isinstance(blobs[0], np.ndarray):
             buf = np.ascontiguousarray(blobs[0], dtype=np.uint8)
             offsets = np.ascontiguousarray(blobs[1], dtype=np.uint64)
@@ -71,7 +73,7 @@ class SpanDecoder:
             it = _abi.zk_ingest_items(arrs[0].ctypes.data, arrs[1].ctypes.data, cap, 0,
                                       arrs[2].ctypes.data, arrs[3].ctypes.data, cap, 0)
         codec = _abi.ZK_CODEC_SNAPPY_THRIFT if snappy else _abi.ZK_CODEC_THRIFT
-        flags = _abi.ZK_INGEST_STRICT if strict else 0
+        flags = (_abi.ZK_INGEST_STRICT if strict else 0) | (_abi.ZK_INGEST_ONE_THREAD if one_thread else 0)
         ab = cols.abi()
         self._check(self._L.zk_ingest_spans(self._h, buf.ctypes.data, offsets.ctypes.data, n, codec, flags,
                                             C.byref(ab), C.byref(nout), C.byref(nrej),
