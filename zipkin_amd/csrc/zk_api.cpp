@@ -892,8 +892,18 @@ static zk_status continue_batch(zk_ctx* c, const SpanColsDev& d, uint32_t flags)
         ZK_HIP(c, launch_trace_set_insert(d.trace_id, n, c->tset, c->tset_slots, &c->stats[ST_NOT_CLUSTERED],
                                           c->stream, &c->cs->hi, &c->cs->skip));
     const DevRange dr{&c->cs->skip, &c->cs->hi};
-    ZK_ST(accumulate_dev(c, d, flags & ~(ZK_BATCH_CONTINUES | ZK_BATCH_VERIFY_TRACES), 0, &dr));
-    ZK_HIP(c, launch_carry_tail(c->cs, d, m, c->stream));  // (after the carry's join read the old carry)
+    zk_status st = accumulate_dev(c, d, flags & ~(ZK_BATCH_CONTINUES | ZK_BATCH_VERIFY_TRACES), 0, &dr);
+    if (st == ZK_OK) {
+        const hipError_t e = launch_carry_tail(c->cs, d, m, c->stream);  // (after the carry's join read the old one)
+        if (e != hipSuccess) st = hip_fail(c, e, "launch_carry_tail");
+    }
+    if (st != ZK_OK) {
+        // the plan already moved the held-trace state past this batch: drop the held trace rather than
+        // join a carry whose copy never ran (the batch failed; reset before reusing the job)
+        c->maybe_carry = false;
+        (void)hipMemsetAsync(c->cs, 0, sizeof(CarryState), c->stream);
+        return st;
+    }
     c->maybe_carry = cont != 0;
     return ZK_OK;
 }
