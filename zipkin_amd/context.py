@@ -175,8 +175,9 @@ class DepsContext:
             self._check(self._L.zk_deps_finalize(self._h, C.byref(t)))  # (waits for the counters)
             self._inflight = []
             return None
-        # (finalize writes every cell) into page-locked host memory when torch has it: the device
-        # copies then land directly (~2x the pageable rate for the 41 B per cell)
+        # (finalize writes every cell) into page-locked host memory when torch has it, laid out as
+        # the library's staging block [m0 | m1 | m2 | m3 | m4 | present]: one device copy lands
+        # directly (~2x the pageable rate for the 41 B per cell)
         buf = _host_buffer(cells * 41)
         m0 = buf[: cells * 8].view(np.uint64)
         ms = [buf[cells * 8 * (k + 1): cells * 8 * (k + 2)].view(np.float64) for k in range(4)]

@@ -962,7 +962,13 @@ zk_status zk_deps_finalize(zk_ctx* c, const zk_link_table* out) {
         ZK_HIP(c, hipEventRecord(ef.b, c->stream));
         c->ev_fin.push_back(ef);
     }
-    if (!out->device_ptrs) {
+    const uint8_t* h0 = (const uint8_t*)out->m0;
+    const bool one_block = !out->device_ptrs && (const uint8_t*)out->m1 == h0 + cells * 8 &&
+                           (const uint8_t*)out->m2 == h0 + cells * 16 && (const uint8_t*)out->m3 == h0 + cells * 24 &&
+                           (const uint8_t*)out->m4 == h0 + cells * 32 && (const uint8_t*)out->present == h0 + cells * 40;
+    if (one_block) {  // the caller's arrays are laid out like the staging block: one copy
+        ZK_HIP(c, hipMemcpyAsync(out->m0, dev.m0, cells * 41, hipMemcpyDeviceToHost, c->stream));
+    } else if (!out->device_ptrs) {
         ZK_HIP(c, hipMemcpyAsync(out->m0, dev.m0, cells * 8, hipMemcpyDeviceToHost, c->stream));
         ZK_HIP(c, hipMemcpyAsync(out->m1, dev.m1, cells * 8, hipMemcpyDeviceToHost, c->stream));
         ZK_HIP(c, hipMemcpyAsync(out->m2, dev.m2, cells * 8, hipMemcpyDeviceToHost, c->stream));
