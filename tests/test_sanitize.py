@@ -43,3 +43,26 @@ def test_parsers_store_and_oracle_are_sanitizer_clean(fuzz_bin, tmp_path):
     r = subprocess.run([str(fuzz_bin), str(corpus), "20000"], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "sanitized run ok" in r.stdout
+
+
+def test_threaded_decoder_is_race_free(tmp_path):
+    """ThreadSanitizer build of the same driver: the host decoder's thread pool over 40k-fragment
+    batches (clean and mutated, both codecs, lenient and strict) reports no data race."""
+    if not shutil.which("g++"):
+        pytest.skip("no host C++ compiler")
+    r = subprocess.run(["make", "-s", "-C", str(ROOT / "tools" / "sanitize"), "tsan"], capture_output=True, text=True)
+    if r.returncode != 0 and "tsan" in (r.stderr or "").lower():
+        pytest.skip("no ThreadSanitizer runtime: " + r.stderr[-300:])
+    assert r.returncode == 0, r.stderr[-2000:]
+    spans = gen_traces(72, 40, max_depth=4, anomalies=0.2)
+    corpus = tmp_path / "corpus.bin"
+    with open(corpus, "wb") as f:
+        for s in spans:
+            raw = T.span(s)
+            for blob in (raw, T.snappy(raw)):
+                f.write(struct.pack("<I", len(blob)) + blob)
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:exitcode=66")
+    r = subprocess.run([str(BIN.parent / "fuzz_host_tsan"), str(corpus), "200"], capture_output=True, text=True,
+                       timeout=600, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "sanitized run ok" in r.stdout

@@ -174,6 +174,20 @@ int main(int argc, char** argv) {
         decoded += decode(g, b, codec, 0);
         decoded += decode(g, b, codec, ZK_INGEST_STRICT);
     }
+    // large batches: the decoder's thread pool (contiguous ranges, one ordered commit), clean and
+    // with mutated fragments spread over the ranges, against the one-thread decode
+    for (int rep = 0; rep < 3; ++rep) {
+        Batch b;
+        while (b.off.size() < 40001) {
+            const auto& c = corpus[rnd() % corpus.size()];
+            b.add(rep && rnd() % 8 == 0 ? mutate(c) : c);
+        }
+        for (uint32_t codec = 0; codec < 2; ++codec) {
+            decoded += decode(g, b, codec, 0);
+            decoded += decode(g, b, codec, ZK_INGEST_ONE_THREAD);
+            decoded += decode(g, b, codec, ZK_INGEST_STRICT);
+        }
+    }
     for (long it = 0; it < iters; ++it) {
         Batch b;
         const int m = 1 + (int)(rnd() % 16);

@@ -6,6 +6,9 @@
 // Every read is bounds-checked: corrupt input is an error, never a crash.
 #include <string.h>
 
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -530,13 +533,85 @@ void decode_range(const uint8_t* buf, const uint64_t* offsets, uint32_t codec, b
     }
 }
 
+// The decode threads of one zk_ingest, kept across calls (starting 15 threads per batch would cost
+// about as much as decoding a small one) and joined when the decoder is destroyed. run(T, fn) calls
+// fn(t) for every t < T -- t = 0 on the calling thread -- and returns when all are done; ranges
+// without a worker (a thread that could not start) run on the calling thread.
+class DecodePool {
+  public:
+    DecodePool() = default;
+    DecodePool(const DecodePool&) = delete;
+    DecodePool& operator=(const DecodePool&) = delete;
+    ~DecodePool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+    void run(uint32_t T, const std::function<void(uint32_t)>& fn) {
+        if (T <= 1) {
+            fn(0);
+            return;
+        }
+        while (workers_.size() < T - 1) {
+            const uint32_t idx = (uint32_t)workers_.size() + 1;
+            try {
+                workers_.emplace_back([this, idx] { loop(idx); });
+            } catch (...) {
+                break;
+            }
+        }
+        const uint32_t nw = (uint32_t)workers_.size() < T - 1 ? (uint32_t)workers_.size() : T - 1;
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            job_ = &fn;
+            width_ = nw;
+            pending_ = nw;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (uint32_t t = nw + 1; t < T; ++t) fn(t);
+        fn(0);
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [&] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+
+  private:
+    void loop(uint32_t idx) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(uint32_t)>* job;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                if (idx > width_) continue;  // not part of this run
+                job = job_;
+            }
+            (*job)(idx);
+            std::lock_guard<std::mutex> lk(m_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(uint32_t)>* job_ = nullptr;
+    uint32_t width_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
 struct zk_ingest {
     std::unordered_map<std::string, uint32_t> svc_ids;
     std::vector<std::string> svc_names;
     std::unordered_map<uint64_t, std::string> strings;
-    std::vector<uint8_t> scratch;
-    SpanT span;
     std::string err;
+    DecodePool pool;
 
     uint32_t service(const Host& h) {
         // thrift.scala:36-43: null or "" service name -> Endpoint.UnknownServiceName
@@ -555,11 +630,6 @@ struct zk_ingest {
         svc_ids.emplace(name, id);
         svc_names.push_back(std::move(name));
         return id;
-    }
-    uint64_t intern(const char* s, uint32_t l) {
-        const uint64_t h = zk_hash_string(s, l);
-        if (strings.find(h) == strings.end()) strings.emplace(h, std::string(s ? s : "", s ? l : 0));
-        return h;
     }
     void keep(uint64_t h, const std::string& s) {  // the string behind a hash (the first one seen)
         if (strings.find(h) == strings.end()) strings.emplace(h, s);
@@ -637,7 +707,7 @@ zk_status zk_ingest_spans(zk_ingest* g, const uint8_t* buf, const uint64_t* offs
     if (flags & ZK_INGEST_ONE_THREAD) T = 1;
     if (n / kIngestMinPerThread < T) T = (uint32_t)(n / kIngestMinPerThread) > 1 ? (uint32_t)(n / kIngestMinPerThread) : 1;
     std::vector<DecodeRange> part(T);
-    auto work = [&](uint32_t t) noexcept {  // (nothing may escape a worker thread)
+    const std::function<void(uint32_t)> work = [&](uint32_t t) noexcept {  // (nothing may escape a worker thread)
         DecodeRange& d = part[t];
         d.lo = n * t / T;
         d.hi = n * (t + 1) / T;
@@ -649,19 +719,7 @@ zk_status zk_ingest_spans(zk_ingest* g, const uint8_t* buf, const uint64_t* offs
             d.err = "host allocation failed";
         }
     };
-    std::vector<std::thread> th;
-    uint32_t started = 1;
-    try {
-        th.reserve(T - 1);
-        for (uint32_t t = 1; t < T; ++t) {
-            th.emplace_back(work, t);
-            ++started;
-        }
-    } catch (...) {  // a thread that cannot start: its range and the rest run here
-    }
-    for (uint32_t t = started; t < T; ++t) work(t);
-    work(0);
-    for (auto& x : th) x.join();
+    g->pool.run(T, work);
     uint64_t* o_tid = (uint64_t*)out->trace_id;
     uint64_t* o_sid = (uint64_t*)out->span_id;
     uint64_t* o_pid = (uint64_t*)out->parent_id;
