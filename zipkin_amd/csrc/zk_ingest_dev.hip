@@ -1415,17 +1415,27 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     a.snappy = codec == ZK_CODEC_SNAPPY_THRIFT;
     a.raw_len = (uint64_t*)take(8 * n1);
     a.raw_off = (uint64_t*)take(8 * n1);
-    a.tid = (uint64_t*)take(8 * n1);
-    a.sid = (uint64_t*)take(8 * n1);
-    a.pid = (uint64_t*)take(8 * n1);
-    a.first = (int64_t*)take(8 * n1);
-    a.last = (int64_t*)take(8 * n1);
+    // records are written straight into the caller's columns at their fragment index; when some
+    // fragment is dropped they are copied here and compacted back (below)
+    zk_span_cols tmp{};
+    tmp.trace_id = (uint64_t*)take(8 * n1);
+    tmp.span_id = (uint64_t*)take(8 * n1);
+    tmp.parent_id = (uint64_t*)take(8 * n1);
+    tmp.first_ts = (int64_t*)take(8 * n1);
+    tmp.last_ts = (int64_t*)take(8 * n1);
     a.svc_hash = (uint64_t*)take(8 * n1);
     a.name_ptr = (uint64_t*)take(8 * n1);
     take(8 * n1);  // (spare)
-    a.flags = (uint32_t*)take(4 * n1);
-    a.svc = (uint32_t*)take(4 * n1);
+    tmp.flags = (uint32_t*)take(4 * n1);
+    tmp.service_id = (uint32_t*)take(4 * n1);
     a.name_len = (uint32_t*)take(4 * n1);
+    a.tid = (uint64_t*)out->trace_id;
+    a.sid = (uint64_t*)out->span_id;
+    a.pid = (uint64_t*)out->parent_id;
+    a.first = (int64_t*)out->first_ts;
+    a.last = (int64_t*)out->last_ts;
+    a.flags = (uint32_t*)out->flags;
+    a.svc = (uint32_t*)out->service_id;
     a.keep = (uint32_t*)take(4 * n1);
     a.pos = (uint32_t*)take(4 * n1);
     a.status = take(n1);
@@ -1507,20 +1517,19 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
         ING_HIP(g, hipMemcpyAsync(g->d_id, g->slot_id.data(), g->slot_id.size() * 4, hipMemcpyHostToDevice, s));
         ING_HIP(g, hipMemcpyAsync(g->d_ptr, ptr.data(), ptr.size() * 8, hipMemcpyHostToDevice, s));
     }
-    // D4, scan, D5
+    // D4, the status counts
     ING_HIP(g, launch_checked("k_ing_lookup", k_ing_lookup, grid, blk, 0, s, a));
-    ING_HIP(g, hipMemsetAsync(a.keep + n, 0, 4, s));
-    ING_HIP(g, hipcub::DeviceScan::ExclusiveSum(g->cub, need, a.keep, a.pos, (int)n1, s));
     ING_HIP(g, hipMemsetAsync(g->counts, 0, 8 * 8, s));
     ING_HIP(g, hipMemsetAsync(g->counts + 8, 0xFF, 8, s));
     ING_HIP(g, launch_checked("k_ing_count", k_ing_count, grid, blk, 0, s, (const uint8_t*)a.status, n, g->counts,
                               (unsigned int*)(g->counts + 8)));
     unsigned long long c[9];
-    uint32_t kept = 0;
     ING_HIP(g, hipMemcpyAsync(c, g->counts, 9 * 8, hipMemcpyDeviceToHost, s));
-    ING_HIP(g, hipMemcpyAsync(&kept, a.pos + n, 4, hipMemcpyDeviceToHost, s));
     ING_HIP(g, hipStreamSynchronize(s));
     for (uint8_t* r : retired) hipFree(r);
+    uint64_t dropped = 0;  // every fragment whose status is not ok is not a record
+    for (int q = 0; q < 8; ++q) dropped += c[q];
+    const uint64_t kept = n - dropped;
     const unsigned first_bad = (unsigned)(c[8] & 0xFFFFFFFFu);
     if (c[kStCollision])
         return dfail(g, ZK_ERR_INVALID_SPAN, "two service names share a 64-bit hash (fragment " +
@@ -1532,7 +1541,27 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     if (strict && bad)
         return dfail(g, ZK_ERR_INVALID_SPAN, "span " + std::to_string(first_bad) + ": " +
                                                  (c[kStUndecodable] ? "undecodable or invalid span" : "invalid span"));
-    ING_HIP(g, launch_checked("k_ing_compact", k_ing_compact, grid, blk, 0, s, a, *out));
+    if (dropped) {
+        // D5: the records sit at their fragment index in the caller's columns; copy them aside and
+        // compact them back in input order
+        ING_HIP(g, hipMemsetAsync(a.keep + n, 0, 4, s));
+        ING_HIP(g, hipcub::DeviceScan::ExclusiveSum(g->cub, need, a.keep, a.pos, (int)n1, s));
+        ING_HIP(g, hipMemcpyAsync((void*)tmp.trace_id, out->trace_id, 8 * n, hipMemcpyDeviceToDevice, s));
+        ING_HIP(g, hipMemcpyAsync((void*)tmp.span_id, out->span_id, 8 * n, hipMemcpyDeviceToDevice, s));
+        ING_HIP(g, hipMemcpyAsync((void*)tmp.parent_id, out->parent_id, 8 * n, hipMemcpyDeviceToDevice, s));
+        ING_HIP(g, hipMemcpyAsync((void*)tmp.first_ts, out->first_ts, 8 * n, hipMemcpyDeviceToDevice, s));
+        ING_HIP(g, hipMemcpyAsync((void*)tmp.last_ts, out->last_ts, 8 * n, hipMemcpyDeviceToDevice, s));
+        ING_HIP(g, hipMemcpyAsync((void*)tmp.service_id, out->service_id, 4 * n, hipMemcpyDeviceToDevice, s));
+        ING_HIP(g, hipMemcpyAsync((void*)tmp.flags, out->flags, 4 * n, hipMemcpyDeviceToDevice, s));
+        a.tid = (uint64_t*)tmp.trace_id;
+        a.sid = (uint64_t*)tmp.span_id;
+        a.pid = (uint64_t*)tmp.parent_id;
+        a.first = (int64_t*)tmp.first_ts;
+        a.last = (int64_t*)tmp.last_ts;
+        a.flags = (uint32_t*)tmp.flags;
+        a.svc = (uint32_t*)tmp.service_id;
+        ING_HIP(g, launch_checked("k_ing_compact", k_ing_compact, grid, blk, 0, s, a, *out));
+    }
     ING_HIP(g, hipStreamSynchronize(s));
     *n_out = kept;
     *n_rejected = bad;
