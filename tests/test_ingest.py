@@ -460,6 +460,35 @@ def test_device_decoder_large_fragments_take_the_global_path(gpu, snappy):
     assert _named(dcols.to_host(), dd.service_names()) == _named(hcols, hd.service_names())
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("scratch", [1, 200, 30000])
+def test_device_decoder_scratch_exhaustion_decodes_again(gpu, monkeypatch, scratch):
+    """The Snappy scratch (deferred fragments' Spans, names of new services) is bump-allocated from
+    one counter; a decoder created with a tiny one runs out, grows it and decodes the fragments that
+    missed out again: records and rejections equal the host decoder's, batch after batch."""
+    import dataclasses
+
+    from zipkin_amd.ingest import DeviceSpanDecoder
+
+    monkeypatch.setenv("ZK_INGEST_SCRATCH_BYTES", str(scratch))
+    rnd = random.Random(79)
+    hd = SpanDecoder()
+    dd = DeviceSpanDecoder(256)
+    for batch in range(3):
+        spans = gen_traces(790 + batch, 200, max_depth=4, anomalies=0.3)
+        out = []
+        for k, s in enumerate(spans):
+            if k % 53 == 3:  # deferred to the global path: needs scratch for its whole Span
+                pad = BinaryAnnotation("blob", bytes(rnd.getrandbits(8) for _ in range(22000)), "BYTES", None)
+                s = dataclasses.replace(s, binary_annotations=s.binary_annotations + (pad,))
+            out.append(s)
+        blobs = encode_all(out, True)
+        hcols, hrej = hd.decode(blobs, snappy=True, strict=False)
+        dcols, drej = dd.decode(blobs, snappy=True, strict=False)
+        assert drej == hrej
+        assert _named(dcols.to_host(), dd.service_names()) == _named(hcols, hd.service_names())
+
+
 def _snappy_runs_then_literals(data: bytes) -> bytes:
     """A legal Snappy block no standard compressor writes: runs of one byte as a literal plus
     64-byte copies (offset 1), every other byte as its own 1-byte literal. After a long run the

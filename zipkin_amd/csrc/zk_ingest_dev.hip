@@ -6,10 +6,11 @@
 // Appendix A.1, written straight into HBM columns. One lane per fragment: the Snappy block and the
 // thrift walk are sequential within a fragment, fragments are independent.
 //
-//   D1 k_ing_rawlen     Snappy header varint -> uncompressed length per fragment
-//   (hipcub scan)       -> scratch offset per fragment
-//   D2 k_ing_decode     decompress into scratch, walk the Span, validate, derive the record and the
-//                       service name (FNV-1a 64 + splitmix64 of its bytes, as zk_hash_string)
+//   D2 k_ing_decode_lds per fragment: its extent and Snappy header (the uncompressed length, loaded
+//                       one round ahead), decompress in LDS, walk the Span, validate, derive the
+//                       record and the service name (FNV-1a 64 + splitmix64 of its bytes, as
+//                       zk_hash_string); k_ing_decode takes the fragments it defers, in global
+//                       memory, with scratch bump-allocated from one counter
 //   D3 k_ing_dict_insert  claim a slot per new service hash in the persistent open-addressing table
 //   (host)              give new slots ids in slot order and copy their names to the device arena
 //   D4 k_ing_lookup     service hash -> id, the name bytes compared with the arena's (exact)
@@ -17,7 +18,10 @@
 //   D5 k_ing_compact    accepted records -> the caller's columns, input order kept
 //
 // Every byte read is bounds-checked: corrupt input marks the fragment undecodable, never faults.
+#include <stdlib.h>
 #include <string.h>
+
+#include <algorithm>
 
 #include <hipcub/hipcub.hpp>
 #include <string>
@@ -32,10 +36,12 @@ namespace {
 
 constexpr uint32_t kIngWG = 256;
 constexpr uint32_t kMaxRaw = ZK_INGEST_MAX_FRAGMENT;  // largest uncompressed fragment accepted (16 MiB)
-constexpr uint32_t kBadLen = 0xFFFFFFFFu;
 constexpr uint64_t kEmpty = 0ull;            // empty dictionary slot (hash 0 is stored as 1)
 constexpr uint32_t kNoId = 0xFFFFFFFFu;
-constexpr uint8_t kStOk = 0, kStInvalid = 1, kStUndecodable = 2, kStCollision = 3, kStRange = 4, kStDefer = 5;
+// kStDefer: the global-memory kernel decodes it; kStNoScratch: the scratch ran out, decoded again
+// after it grows (neither is left when the batch ends)
+constexpr uint8_t kStOk = 0, kStInvalid = 1, kStUndecodable = 2, kStCollision = 3, kStRange = 4, kStDefer = 5,
+                  kStNoScratch = 6;
 const char kUnknown[] = "Unknown service name";  // Endpoint.UnknownServiceName (thrift.scala:36-43)
 
 enum : uint8_t { T_STOP = 0, T_BOOL = 2, T_BYTE = 3, T_DOUBLE = 4, T_I16 = 6, T_I32 = 8, T_I64 = 10,
@@ -408,9 +414,9 @@ struct IngArgs {
     const uint64_t* offsets;
     uint64_t n;
     uint32_t snappy;
-    uint64_t* raw_len;   // n (+1 for the scan)
-    uint64_t* raw_off;   // n + 1
-    uint8_t* scratch;
+    uint8_t* scratch;                   // Snappy: deferred fragments' Spans and copied-out names
+    uint64_t scratch_cap;
+    unsigned long long* scratch_used;   // bump counter (may run past scratch_cap: see kStNoScratch)
     // per-fragment results
     uint8_t* status;
     uint64_t* tid;
@@ -435,18 +441,38 @@ struct IngArgs {
     const uint8_t* unknown;  // device copy of kUnknown
 };
 
-__global__ __launch_bounds__(kIngWG) void k_ing_rawlen(IngArgs a) {
-    const uint64_t i = (uint64_t)blockIdx.x * kIngWG + threadIdx.x;
-    if (i >= a.n) return;
-    const uint64_t b = a.offsets[i], e = a.offsets[i + 1];
-    uint64_t len = e >= b ? e - b : 0, hdr;
-    if (e < b)
-        len = kBadLen;
-    else if (a.snappy && !(snappy_hdr(a.buf + b, e - b, &len, &hdr) && len <= kMaxRaw &&
-                           len <= (e - b - hdr) * (uint64_t)ZK_SNAPPY_MAX_EXPANSION))
-        len = kBadLen;
-    a.raw_len[i] = len == kBadLen ? 0 : len;
-    a.status[i] = len == kBadLen ? kStUndecodable : kStOk;
+// A fragment's first bytes (its Snappy header varint is at most 5), issued as independent loads:
+// one round trip. Bytes past the fragment read as 0x80 (a continuation), so they never end it.
+__device__ __forceinline__ void head_bytes(const IngArgs& a, bool have, uint64_t b, uint64_t e, uint32_t h[5]) {
+    const uint64_t n = have && a.snappy && e > b ? e - b : 0;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) h[j] = (uint64_t)j < n ? a.buf[b + j] : 0x80u;
+}
+
+// D1 per fragment, as the host decoder's checks: offsets ascending; for Snappy a well-formed header
+// whose length is at most kMaxRaw and at most ZK_SNAPPY_MAX_EXPANSION x the compressed bytes after it.
+// *raw: the uncompressed length (0 for the thrift codec).
+__device__ __forceinline__ uint8_t head_status(bool snappy, uint64_t b, uint64_t e, const uint32_t h[5], uint64_t* raw) {
+    *raw = 0;
+    if (e < b) return kStUndecodable;
+    if (!snappy) return kStOk;
+    uint64_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        v |= (uint64_t)(h[j] & 0x7Fu) << (7 * j);
+        if (!(h[j] & 0x80u)) {
+            if (v > kMaxRaw || v > (e - b - (uint64_t)(j + 1)) * (uint64_t)ZK_SNAPPY_MAX_EXPANSION) return kStUndecodable;
+            *raw = v;
+            return kStOk;
+        }
+    }
+    return kStUndecodable;
+}
+
+// bytes of the scratch, or null when it is exhausted (the fragment is then marked kStNoScratch)
+__device__ __forceinline__ uint8_t* scratch_take(const IngArgs& a, uint64_t bytes) {
+    const unsigned long long off = atomicAdd(a.scratch_used, (unsigned long long)bytes);
+    return off + bytes <= a.scratch_cap ? a.scratch + off : nullptr;
 }
 
 template <class P>
@@ -852,28 +878,35 @@ __device__ __forceinline__ void publish_name(const IngArgs& a, uint64_t i, const
     a.name_len[i] = nl;
 }
 
-// D2 (global memory): every fragment, or only those the LDS kernel deferred
-__global__ __launch_bounds__(kIngWG) void k_ing_decode(IngArgs a, uint32_t deferred_only) {
+// D2 (global memory): the fragments marked `mode` (kStDefer by the LDS kernel, or kStNoScratch)
+__global__ __launch_bounds__(kIngWG) void k_ing_decode(IngArgs a, uint32_t mode) {
     const uint64_t i = (uint64_t)blockIdx.x * kIngWG + threadIdx.x;
-    if (i >= a.n) return;
-    if (deferred_only) {
-        if (a.status[i] != kStDefer) return;
-        a.status[i] = kStOk;
-    }
+    if (i >= a.n || a.status[i] != mode) return;
+    a.status[i] = kStOk;
     a.keep[i] = 0u;
     a.svc_hash[i] = 0ull;
-    if (a.status[i] != kStOk) return;
     const uint64_t b = a.offsets[i], e = a.offsets[i + 1];
     const uint8_t* src = a.buf + b;
     uint64_t len = e - b;
     if (a.snappy) {
-        uint8_t* dst = a.scratch + a.raw_off[i];
-        if (!snappy_block(src, len, dst, a.raw_len[i])) {
+        uint32_t h[5];
+        uint64_t raw;
+        head_bytes(a, true, b, e, h);
+        if (head_status(true, b, e, h, &raw) != kStOk) {  // (checked before it was deferred)
+            a.status[i] = kStUndecodable;
+            return;
+        }
+        uint8_t* dst = scratch_take(a, raw);
+        if (!dst) {
+            a.status[i] = kStNoScratch;
+            return;
+        }
+        if (!snappy_block(src, len, dst, raw)) {
             a.status[i] = kStUndecodable;
             return;
         }
         src = dst;
-        len = a.raw_len[i];
+        len = raw;
     }
     const uint8_t* nm;
     uint32_t nl;
@@ -1044,19 +1077,26 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
     const uint64_t blk0 = (uint64_t)blockIdx.x * kLdsBlock;
     const uint64_t blk1 = blk0 + kLdsBlock < a.n ? blk0 + kLdsBlock : a.n;
     ING_STAMP_DECL
+    // a round's fragment extents and Snappy headers are loaded during the round before (the first
+    // round's here), so no round starts with a dependent global round trip
+    bool nh = blk0 + lane < blk1;
+    uint64_t nb = nh ? a.offsets[blk0 + lane] : 0, ne = nh ? a.offsets[blk0 + lane + 1] : 0;
+    uint32_t hb[5];
+    head_bytes(a, nh, nb, ne, hb);
     for (uint64_t f0 = blk0; f0 < blk1;) {  // uniform
         const uint64_t i = f0 + lane;
         const bool have = i < blk1;
-        uint64_t b = 0, clen = 0, raw = 0;
+        const uint64_t b = nb;
+        uint64_t clen = 0, raw = 0;
         uint32_t need = 0;
         uint8_t st = kStInvalid;
         if (have) {
-            st = a.status[i];
-            b = a.offsets[i];
-            clen = a.offsets[i + 1] - b;  // (not monotone offsets were marked undecodable by D1)
-            raw = a.snappy ? a.raw_len[i] : 0;
-            const uint64_t r = ((raw > clen ? raw : clen) + kLdsSlack + 15) & ~15ull;
-            need = st == kStOk ? (r > kLdsBudget ? kLdsBudget + 1 : (uint32_t)r) : 0u;
+            st = head_status(a.snappy, nb, ne, hb, &raw);
+            if (st == kStOk) {
+                clen = ne - nb;
+                const uint64_t r = ((raw > clen ? raw : clen) + kLdsSlack + 15) & ~15ull;
+                need = r > kLdsBudget ? kLdsBudget + 1 : (uint32_t)r;
+            }
         }
         // Uniform layout (every region of the round has the size R of the largest, R / 16 odd, lane
         // L at L * R with a skew of 4 * (L / 16) bytes): lanes parsing the same field offset then
@@ -1088,17 +1128,22 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
             fits = incl <= kLdsBudget;
         }
         ING_STAMP(0);
+        // the next round's extents (its copy-in below waits for them in passing: loads return in order)
+        nh = f0 + k + lane < blk1;
+        nb = nh ? a.offsets[f0 + k + lane] : 0;
+        ne = nh ? a.offsets[f0 + k + lane + 1] : 0;
+        const bool go = lane < k && have && st == kStOk && fits;
+        uint32_t D = 0, mis = 0;
+        uint8_t* reg = s_buf + R0;
         if (lane < k && have) {
             a.keep[i] = 0u;
             a.svc_hash[i] = 0ull;
-            if (st == kStOk && !fits) {
-                a.status[i] = kStDefer;
-            } else if (st == kStOk) {
-                const uint32_t mis = (uint32_t)((uintptr_t)(a.buf + b) & 15u);
+            a.status[i] = st == kStOk && !fits ? kStDefer : st;
+            if (go) {
+                mis = (uint32_t)((uintptr_t)(a.buf + b) & 15u);
                 // input at offset D of the region (D = mis mod 16): its aligned 16-B blocks cover
                 // [D - mis, D + clen + 15] inside [0, R) since R >= clen + kLdsSlack
-                const uint32_t D = ((R - 16u - (uint32_t)clen - mis) & ~15u) + mis;
-                uint8_t* reg = s_buf + R0;
+                D = ((R - 16u - (uint32_t)clen - mis) & ~15u) + mis;
                 // 16-B blocks through a global-space pointer (global_load, not a flat load)
                 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
                 typedef const __attribute__((address_space(1))) u32x4 g_u32x4;
@@ -1106,56 +1151,64 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                 const uint32_t nblk = (uint32_t)((clen + mis + 15) >> 4);
                 u32x4* dst = reinterpret_cast<u32x4*>(reg + D - mis);
                 for (uint32_t c = 0; c < nblk; ++c) dst[c] = g[c];
-                ING_STAMP(1);
-                // the region as an LDS pointer: the decoder's byte and word reads become ds_read_*.
-                // Regions start on 16-byte boundaries, i.e. on one of 8 bank offsets of a 32-bank
-                // group; lanes parsing the same field at the same offset then collide. The
-                // decompressed span starts 4 * (lane % 4) bytes in, spreading the lanes over all 32.
-                lds_u8* const lreg = (lds_u8*)reg;
-                const uint32_t skew = 4u * (uniform ? (lane >> 4) & 3u : lane & 3u);
-                const lds_u8* src = lreg + D;
-                uint64_t len = clen;
-                bool ok = true, unsafe = false;
-                if (a.snappy) {
-                    ok = snappy_inplace(lreg + skew, D - skew, clen, raw, &unsafe);
-                    src = lreg + skew;
-                    len = raw;
+            }
+        }
+        head_bytes(a, nh, nb, ne, hb);  // the next round's headers, in flight during this round's decode
+        if (go) {
+            ING_STAMP(1);
+            // the region as an LDS pointer: the decoder's byte and word reads become ds_read_*.
+            // Regions start on 16-byte boundaries, i.e. on one of 8 bank offsets of a 32-bank
+            // group; lanes parsing the same field at the same offset then collide. The
+            // decompressed span starts 4 * (lane % 4) bytes in, spreading the lanes over all 32.
+            lds_u8* const lreg = (lds_u8*)reg;
+            const uint32_t skew = 4u * (uniform ? (lane >> 4) & 3u : lane & 3u);
+            const lds_u8* src = lreg + D;
+            uint64_t len = clen;
+            bool ok = true, unsafe = false;
+            if (a.snappy) {
+                ok = snappy_inplace(lreg + skew, D - skew, clen, raw, &unsafe);
+                src = lreg + skew;
+                len = raw;
+            }
+            ING_STAMP(2);
+            if (!ok) {
+                a.status[i] = unsafe ? kStDefer : kStUndecodable;
+            } else {
+                const lds_u8* const lbase = (const lds_u8*)s_buf;
+                const uint32_t p0 = (uint32_t)(src - lbase);
+                uint32_t nmo, nl;
+                int r = parse_record_fast(a, i, lbase, p0, (uint32_t)len, &nmo, &nl);
+                if (r == -3) {  // not the canonical layout: the generic walk
+                    const uint8_t* gnm = nullptr;
+                    r = parse_record(a, i, src, len, &gnm, &nl);
+                    nmo = (r == 1 && gnm != (const uint8_t*)a.unknown) ? (uint32_t)(gnm - (const uint8_t*)lbase)
+                                                                       : ~0u;
                 }
-                ING_STAMP(2);
-                if (!ok) {
-                    a.status[i] = unsafe ? kStDefer : kStUndecodable;
-                } else {
-                    const lds_u8* const lbase = (const lds_u8*)s_buf;
-                    const uint32_t p0 = (uint32_t)(src - lbase);
-                    uint32_t nmo, nl;
-                    int r = parse_record_fast(a, i, lbase, p0, (uint32_t)len, &nmo, &nl);
-                    if (r == -3) {  // not the canonical layout: the generic walk
-                        const uint8_t* gnm = nullptr;
-                        r = parse_record(a, i, src, len, &gnm, &nl);
-                        nmo = (r == 1 && gnm != (const uint8_t*)a.unknown) ? (uint32_t)(gnm - (const uint8_t*)lbase)
-                                                                           : ~0u;
-                    }
-                    const bool unknown = nmo == ~0u;
-                    const uint8_t* nm = unknown ? a.unknown : (const uint8_t*)(lbase + nmo);
-                    if (unknown) nl = sizeof(kUnknown) - 1;
-                    ING_STAMP(3);
-                    if (r >= 0) {
-                        if (r && !try_resolve(a, i, nm, nl, d_hash(nm, nl))) {
-                            if (!unknown) {  // the name lies in this lane's own bytes
-                                const uint64_t off = nmo - p0;
-                                if (a.snappy) {
-                                    uint8_t* gd = a.scratch + a.raw_off[i] + off;  // copy out to the scratch
+                const bool unknown = nmo == ~0u;
+                const uint8_t* nm = unknown ? a.unknown : (const uint8_t*)(lbase + nmo);
+                if (unknown) nl = sizeof(kUnknown) - 1;
+                ING_STAMP(3);
+                if (r >= 0) {
+                    if (r && !try_resolve(a, i, nm, nl, d_hash(nm, nl))) {
+                        if (!unknown) {  // the name lies in this lane's own bytes
+                            const uint64_t off = nmo - p0;
+                            if (a.snappy) {
+                                uint8_t* gd = scratch_take(a, nl);  // copy out to the scratch
+                                if (gd) {
 #pragma clang loop vectorize(disable)
                                     for (uint32_t q = 0; q < nl; ++q) gd[q] = nm[q];
-                                    nm = gd;
                                 } else {
-                                    nm = a.buf + b + off;  // thrift codec: the name is in the input buffer
+                                    a.status[i] = kStNoScratch;
+                                    r = -1;
                                 }
+                                nm = gd;
+                            } else {
+                                nm = a.buf + b + off;  // thrift codec: the name is in the input buffer
                             }
-                            publish_name(a, i, nm, nl);
                         }
-                        a.keep[i] = 1u;
+                        if (r >= 0) publish_name(a, i, nm, nl);
                     }
+                    if (r >= 0) a.keep[i] = 1u;
                 }
             }
         }
@@ -1272,11 +1325,12 @@ struct zk_ingest_dev {
     // per-batch scratch
     void* batch = nullptr;
     uint64_t batch_cap = 0;
-    uint8_t* scratch = nullptr;
+    uint8_t* scratch = nullptr;  // Snappy: bump-allocated per batch (deferred Spans, new names)
     uint64_t scratch_cap = 0;
+    uint64_t scratch_min = 0;    // first size (ZK_INGEST_SCRATCH_BYTES; else from the batch size)
     void* cub = nullptr;
     size_t cub_cap = 0;
-    unsigned long long* counts = nullptr;  // [8] per status + first_bad
+    unsigned long long* counts = nullptr;  // [8] per status, [8] first_bad, [10] scratch bytes taken
     std::string err;
 };
 
@@ -1327,6 +1381,7 @@ zk_status zk_ingest_dev_create(int32_t device, void* stream, uint32_t max_servic
         }
     }
     g->arena_cap = 1 << 16;
+    if (const char* sb = getenv("ZK_INGEST_SCRATCH_BYTES")) g->scratch_min = strtoull(sb, nullptr, 10);
     if (e == hipSuccess) e = hipMalloc(&g->d_key, (uint64_t)t * 8);
     if (e == hipSuccess) e = hipMalloc(&g->d_id, (uint64_t)t * 4);
     if (e == hipSuccess) e = hipMalloc(&g->d_ptr, (uint64_t)t * 8);
@@ -1395,7 +1450,7 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     ING_HIP(g, hipSetDevice(g->device));
     // per-fragment arrays: 8-byte columns first, then 4-byte, then 1-byte
     const uint64_t n1 = n + 1;
-    const uint64_t bytes = align256(8 * n1) * 10 + align256(4 * n1) * 5 + align256(n1);
+    const uint64_t bytes = align256(8 * n1) * 8 + align256(4 * n1) * 5 + align256(n1);
     if (bytes > g->batch_cap) {
         hipFree(g->batch);
         g->batch = nullptr;
@@ -1413,8 +1468,6 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     a.offsets = offsets;
     a.n = n;
     a.snappy = codec == ZK_CODEC_SNAPPY_THRIFT;
-    a.raw_len = (uint64_t*)take(8 * n1);
-    a.raw_off = (uint64_t*)take(8 * n1);
     // records are written straight into the caller's columns at their fragment index; when some
     // fragment is dropped they are copied here and compacted back (below)
     zk_span_cols tmp{};
@@ -1448,46 +1501,56 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     a.unknown = g->arena;
     const dim3 grid((unsigned)((n + kIngWG - 1) / kIngWG)), blk(kIngWG);
     hipStream_t s = g->stream;
-    // D1 + scan: scratch offsets
-    ING_HIP(g, launch_checked("k_ing_rawlen", k_ing_rawlen, grid, blk, 0, s, a));
-    size_t need = 0, need2 = 0;
-    ING_HIP(g, hipcub::DeviceScan::ExclusiveSum(nullptr, need, a.raw_len, a.raw_off, (int)n1, s));
-    ING_HIP(g, hipcub::DeviceScan::ExclusiveSum(nullptr, need2, a.keep, a.pos, (int)n1, s));
-    if (need2 > need) need = need2;
+    size_t need = 0;
+    ING_HIP(g, hipcub::DeviceScan::ExclusiveSum(nullptr, need, a.keep, a.pos, (int)n1, s));
     if (need > g->cub_cap) {
         hipFree(g->cub);
         g->cub = nullptr;
         ING_HIP(g, hipMalloc(&g->cub, need));
         g->cub_cap = need;
     }
-    ING_HIP(g, hipMemsetAsync(a.raw_len + n, 0, 8, s));
-    ING_HIP(g, hipcub::DeviceScan::ExclusiveSum(g->cub, need, a.raw_len, a.raw_off, (int)n1, s));
-    uint64_t total = 0;
-    if (a.snappy) {
-        ING_HIP(g, hipMemcpyAsync(&total, a.raw_off + n, 8, hipMemcpyDeviceToHost, s));
-        ING_HIP(g, hipStreamSynchronize(s));
-        if (total + 1 > g->scratch_cap) {
-            hipFree(g->scratch);
-            g->scratch = nullptr;
-            ING_HIP(g, hipMalloc(&g->scratch, total + 1));
-            g->scratch_cap = total + 1;
-        }
+    if (a.snappy && !g->scratch) {
+        const uint64_t cap = g->scratch_min ? g->scratch_min : std::max<uint64_t>(1ull << 26, 24 * n);
+        ING_HIP(g, hipMalloc(&g->scratch, cap));
+        g->scratch_cap = cap;
     }
+    unsigned long long* used = g->counts + 10;
+    ING_HIP(g, hipMemsetAsync(used, 0, 8, s));
     a.scratch = g->scratch;
-    // D2, D3
+    a.scratch_cap = g->scratch_cap;
+    a.scratch_used = used;
+    // D1 + D2, D3
     ING_HIP(g, launch_checked("k_ing_decode_lds", k_ing_decode_lds, dim3((unsigned)((n + kLdsBlock - 1) / kLdsBlock)),
                               dim3(kLdsWG), 0, s, a));
-    ING_HIP(g, launch_checked("k_ing_decode", k_ing_decode, grid, blk, 0, s, a, 1u));  // the deferred waves
+    ING_HIP(g, launch_checked("k_ing_decode", k_ing_decode, grid, blk, 0, s, a, (uint32_t)kStDefer));
     ING_HIP(g, launch_checked("k_ing_dict_insert", k_ing_dict_insert, grid, blk, 0, s, a));
-    // ids for new slots, in slot order; their names into the device arena
     std::vector<uint64_t> key(g->table), ptr(g->table);
     std::vector<uint32_t> len(g->table);
-    ING_HIP(g, hipMemcpyAsync(key.data(), g->d_key, key.size() * 8, hipMemcpyDeviceToHost, s));
-    ING_HIP(g, hipMemcpyAsync(ptr.data(), g->d_ptr, ptr.size() * 8, hipMemcpyDeviceToHost, s));
-    ING_HIP(g, hipMemcpyAsync(len.data(), g->d_len, len.size() * 4, hipMemcpyDeviceToHost, s));
-    ING_HIP(g, hipStreamSynchronize(s));
+    std::vector<uint8_t*> retired;  // old arenas and scratch stay valid until this batch's lookups are done
+    for (;;) {
+        unsigned long long taken = 0;
+        ING_HIP(g, hipMemcpyAsync(key.data(), g->d_key, key.size() * 8, hipMemcpyDeviceToHost, s));
+        ING_HIP(g, hipMemcpyAsync(ptr.data(), g->d_ptr, ptr.size() * 8, hipMemcpyDeviceToHost, s));
+        ING_HIP(g, hipMemcpyAsync(len.data(), g->d_len, len.size() * 4, hipMemcpyDeviceToHost, s));
+        ING_HIP(g, hipMemcpyAsync(&taken, used, 8, hipMemcpyDeviceToHost, s));
+        ING_HIP(g, hipStreamSynchronize(s));
+        if (taken <= g->scratch_cap) break;
+        // the scratch ran out (kStNoScratch fragments): a larger one, and those fragments again
+        uint64_t cap = 2 * g->scratch_cap;
+        if (cap < taken) cap = taken;
+        retired.push_back(g->scratch);
+        g->scratch = nullptr;
+        g->scratch_cap = 0;
+        ING_HIP(g, hipMalloc(&g->scratch, cap));
+        g->scratch_cap = cap;
+        ING_HIP(g, hipMemsetAsync(used, 0, 8, s));
+        a.scratch = g->scratch;
+        a.scratch_cap = cap;
+        ING_HIP(g, launch_checked("k_ing_decode", k_ing_decode, grid, blk, 0, s, a, (uint32_t)kStNoScratch));
+        ING_HIP(g, launch_checked("k_ing_dict_insert", k_ing_dict_insert, grid, blk, 0, s, a));
+    }
+    // ids for new slots, in slot order; their names into the device arena
     bool changed = false;
-    std::vector<uint8_t*> retired;  // old arenas stay valid until this batch's lookups are done
     for (uint32_t q = 0; q < g->table; ++q) {
         if (key[q] == kEmpty || g->slot_id[q] != kNoId) continue;
         std::string nm(len[q], '\0');
