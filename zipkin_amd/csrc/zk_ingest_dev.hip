@@ -964,8 +964,15 @@ constexpr uint32_t kLdsWG = 64;
 #endif
 constexpr uint32_t kLdsBudget = ZK_ING_BUDGET;
 constexpr uint32_t kLdsBlock = 1024;
-constexpr uint32_t kLdsSlack = 80;  // region bytes beyond max(raw, compressed): in-place headroom + alignment
-                                    // + the lane's bank skew
+// Region bytes beyond max(raw, compressed): the input's placement (16 B of block tail + up to 15 of
+// misalignment) and the lane's bank skew (up to 12). A region of raw + slack bytes also holds the
+// output's final lead over the input (raw - compressed); a Snappy stream whose lead is larger part
+// way through is caught by the in-place check and deferred. 48 (was 80): 55 lanes per round instead
+// of 51 on the bench's fragments, 6.47 -> 5.97 ms (profiles/r05/ab_ingest_slack.txt).
+#ifndef ZK_ING_SLACK
+#define ZK_ING_SLACK 48
+#endif
+constexpr uint32_t kLdsSlack = ZK_ING_SLACK;
 constexpr uint32_t kLdsUniformCap = 640;  // largest region (bytes) of a uniform round
 
 // Snappy block from in = out + D (the same region), in place: false with *unsafe set when a step
