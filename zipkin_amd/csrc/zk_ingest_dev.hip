@@ -976,7 +976,12 @@ constexpr uint32_t kLdsSlack = ZK_ING_SLACK;
 constexpr uint32_t kLdsUniformCap = 640;  // largest region (bytes) of a uniform round
 
 // Snappy block from in = out + D (the same region), in place: false with *unsafe set when a step
-// would write over input bytes not yet read.
+// would write over input bytes not yet read. ZK_ING_OVERCOPY: a literal or a copy (offset >= 8)
+// runs as whole 8-byte steps when the output trails the unread input by 8 bytes or more, instead
+// of 8-byte steps and a byte loop for the rest (each byte a dependent LDS read and write).
+#ifndef ZK_ING_OVERCOPY
+#define ZK_ING_OVERCOPY 1
+#endif
 __device__ __forceinline__ bool snappy_inplace(lds_u8* out, uint64_t D, uint64_t n, uint64_t len, bool* unsafe) {
     const lds_u8* in = out + D;
     uint64_t dl, hdr;
@@ -1004,6 +1009,15 @@ __device__ __forceinline__ bool snappy_inplace(lds_u8* out, uint64_t D, uint64_t
                 return false;
             }
             uint64_t k = 0;
+#if ZK_ING_OVERCOPY
+            if (o + 8 <= D + i) {  // whole 8-byte steps: the last writes < 8 bytes past the literal, over
+                                   // input already read or output the next tags write again
+                for (; k < l; k += 8) cp8(out + o + k, in + i + k);
+                i += l;
+                o += l;
+                continue;
+            }
+#endif
             for (; k + 8 <= l; k += 8) cp8(out + o + k, in + i + k);
             #pragma clang loop vectorize(disable)  // (a vectorised byte loop reads LDS with unaligned ds_read_b128)
             for (; k < l; ++k) out[o + k] = in[i + k];
@@ -1033,6 +1047,13 @@ __device__ __forceinline__ bool snappy_inplace(lds_u8* out, uint64_t D, uint64_t
             *unsafe = true;
             return false;
         }
+#if ZK_ING_OVERCOPY
+        if (off >= 8 && o + l + 8 <= D + i) {  // whole 8-byte steps (each reads bytes already written)
+            for (uint64_t k = 0; k < l; k += 8) cp8(out + o + k, out + o - off + k);
+            o += l;
+            continue;
+        }
+#endif
         backref_copy(out, o, off, l);
         o += l;
     }
