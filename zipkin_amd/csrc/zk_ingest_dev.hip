@@ -1060,6 +1060,99 @@ __device__ __forceinline__ bool snappy_inplace(lds_u8* out, uint64_t D, uint64_t
     return o == len;
 }
 
+#ifndef ZK_ING_SNAPPY_PIPE
+#define ZK_ING_SNAPPY_PIPE 1
+#endif
+__device__ __forceinline__ void st8(lds_u8* d, uint64_t v) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = (uint8_t)(v >> (8 * k));
+}
+
+// snappy_inplace with one dependent LDS round trip per tag instead of up to three (tag, then its
+// parameter bytes, then the source): a tag and its parameters come from an 8-byte window read
+// while the previous tag's copy was in flight, and a copy's source is read 16 bytes at a time
+// before its stores. The window lies at or past in + i, above every byte the tag's copy writes
+// (the in-place checks below), so reading it first is safe. Same result, same failures, same
+// unsafe verdicts as snappy_inplace.
+__device__ __forceinline__ bool snappy_inplace_pipe(lds_u8* out, uint64_t D, uint64_t n, uint64_t len, bool* unsafe) {
+    const lds_u8* in = out + D;
+    uint64_t dl, hdr;
+    if (!snappy_hdr(in, n, &dl, &hdr) || dl != len) return false;
+    uint64_t o = 0, i = hdr;
+    uint64_t w = ld_u64(in + i);  // in[i, i + 8): bytes past n are region bytes, used only after a bounds check
+    while (i < n) {
+        const uint32_t tag = (uint32_t)w & 0xFFu;
+        const uint32_t kind = tag & 3u;
+        uint64_t l, src, off = 0;  // src: the copy's source, as an offset from out
+        bool whole8, pairs;
+        if (kind == 0) {
+            l = tag >> 2;
+            uint64_t s = i + 1;
+            if (l >= 60) {
+                const uint32_t nb = (uint32_t)l - 59;
+                if (s + nb > n) return false;
+                l = (w >> 8) & (nb == 4 ? 0xFFFFFFFFull : ((1ull << (8 * nb)) - 1));
+                s += nb;
+            }
+            l += 1;
+            if (s + l > n || o + l > len) return false;
+            if (o > D + s) {
+                *unsafe = true;
+                return false;
+            }
+            i = s + l;
+            src = D + s;
+            whole8 = o + 8 <= D + s;  // as snappy_inplace's overcopy condition
+            pairs = true;             // the source lies above the stores
+        } else {
+            uint64_t adv;
+            if (kind == 1) {
+                adv = 2;
+                l = ((tag >> 2) & 7) + 4;
+                off = ((uint64_t)(tag >> 5) << 8) | ((w >> 8) & 0xFFu);
+            } else if (kind == 2) {
+                adv = 3;
+                l = (tag >> 2) + 1;
+                off = (w >> 8) & 0xFFFFu;
+            } else {
+                adv = 5;
+                l = (tag >> 2) + 1;
+                off = (w >> 8) & 0xFFFFFFFFull;
+            }
+            if (i + adv > n) return false;
+            i += adv;
+            if (off == 0 || off > o || o + l > len) return false;
+            if (o + l > D + i) {
+                *unsafe = true;
+                return false;
+            }
+            src = o - off;
+            whole8 = off >= 8 && o + l + 8 <= D + i;
+            pairs = off >= 16;  // a 16-byte read never reaches this copy's own stores
+        }
+        const uint64_t wn = ld_u64(in + i);  // the next tag's window, ahead of this tag's stores
+        if (whole8 && pairs) {
+            for (uint64_t k = 0; k < l; k += 16) {
+                const uint64_t v0 = ld_u64(out + src + k), v1 = ld_u64(out + src + k + 8);
+                st8(out + o + k, v0);
+                if (k + 8 < l) st8(out + o + k + 8, v1);
+            }
+        } else if (whole8) {
+            for (uint64_t k = 0; k < l; k += 8) cp8(out + o + k, out + src + k);
+        } else if (kind == 0) {
+            uint64_t k = 0;
+            for (; k + 8 <= l; k += 8) cp8(out + o + k, out + src + k);
+            #pragma clang loop vectorize(disable)  // (a vectorised byte loop reads LDS with unaligned ds_read_b128)
+            for (; k < l; ++k) out[o + k] = out[src + k];
+        } else {
+            backref_copy(out, o, off, l);
+        }
+        o += l;
+        w = wn;
+    }
+    return o == len;
+}
+
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -1194,7 +1287,11 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
             uint64_t len = clen;
             bool ok = true, unsafe = false;
             if (a.snappy) {
+#if ZK_ING_SNAPPY_PIPE
+                ok = snappy_inplace_pipe(lreg + skew, D - skew, clen, raw, &unsafe);
+#else
                 ok = snappy_inplace(lreg + skew, D - skew, clen, raw, &unsafe);
+#endif
                 src = lreg + skew;
                 len = raw;
             }
