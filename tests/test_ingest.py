@@ -489,6 +489,35 @@ def test_device_decoder_scratch_exhaustion_decodes_again(gpu, monkeypatch, scrat
         assert _named(dcols.to_host(), dd.service_names()) == _named(hcols, hd.service_names())
 
 
+@pytest.mark.gpu
+def test_device_decoder_names_around_the_inline_prefix(gpu):
+    """The LDS decoder resolves a known name from the dictionary slot's first 16 bytes, then the
+    arena for the rest: names of 0-40 bytes, exactly 16 and 17, and names sharing a 16-byte
+    prefix, over several batches (each name resolved from the dictionary after its first batch)."""
+    import dataclasses
+
+    from zipkin_amd.ingest import DeviceSpanDecoder
+
+    base = ["", "a", "svc-15-bytes-xx", "svc-16-bytes-xxx", "svc-16-bytes-xxxy", "svc-16-bytes-xxxz",
+            "prefix-sixteen--" + "A" * 16, "prefix-sixteen--" + "A" * 15 + "B", "n" * 40, "é-ünïcode-名前"]
+    rnd = random.Random(81)
+    hd = SpanDecoder()
+    dd = DeviceSpanDecoder(64)
+    for batch in range(4):
+        spans = gen_traces(810 + batch, 150, max_depth=4)
+        out = []
+        for s in spans:
+            nm = rnd.choice(base)
+            anns = tuple(dataclasses.replace(x, host=Endpoint(x.host.ipv4, x.host.port, nm)) if x.host else x
+                         for x in s.annotations)
+            out.append(dataclasses.replace(s, annotations=anns))
+        blobs = encode_all(out, True)
+        hcols, hrej = hd.decode(blobs, snappy=True, strict=False)
+        dcols, drej = dd.decode(blobs, snappy=True, strict=False)
+        assert drej == hrej
+        assert _named(dcols.to_host(), dd.service_names()) == _named(hcols, hd.service_names())
+
+
 def _snappy_runs_then_literals(data: bytes) -> bytes:
     """A legal Snappy block no standard compressor writes: runs of one byte as a literal plus
     64-byte copies (offset 1), every other byte as its own 1-byte literal. After a long run the

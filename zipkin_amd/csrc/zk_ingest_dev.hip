@@ -436,6 +436,7 @@ struct IngArgs {
     uint32_t* d_id;
     uint64_t* d_ptr;     // device address of the slot's name (arena after assignment)
     uint32_t* d_len;
+    const uint8_t* d_name16;  // the first 16 bytes of each named slot's name (zero padded), 16-B aligned
     uint32_t d_mask;
     uint32_t max_services;
     const uint8_t* unknown;  // device copy of kUnknown
@@ -948,6 +949,84 @@ __device__ __forceinline__ bool try_resolve(const IngArgs& a, uint64_t i, const 
     return true;
 }
 
+#ifndef ZK_ING_NAME16
+#define ZK_ING_NAME16 1
+#endif
+// try_resolve for the LDS decoder in one global round trip for names of at most 16 bytes: the
+// name's first 16 bytes are loaded once (hashed and compared from registers), and the first probe
+// reads the slot's key, id, length and inline name bytes together. *h: the name's hash (for
+// publish_name when it does not resolve).
+__device__ __forceinline__ bool resolve16(const IngArgs& a, uint64_t i, const uint8_t* nm, uint32_t nl, uint64_t* h_out) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    uint8_t u[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) u[j] = (uint32_t)j < nl ? nm[j] : 0;
+    uint64_t h = 0xCBF29CE484222325ull;  // == d_hash
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        if ((uint32_t)j < nl) {
+            h ^= u[j];
+            h *= 0x100000001B3ull;
+        }
+    }
+    for (uint32_t q0 = 16; q0 < nl; q0 += 16) {
+        uint8_t v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = q0 + j < nl ? nm[q0 + j] : 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (q0 + j < nl) {
+                h ^= v[j];
+                h *= 0x100000001B3ull;
+            }
+        }
+    }
+    h = d_mix64(h);
+    h = h ? h : 1ull;
+    *h_out = h;
+    uint32_t slot = (uint32_t)h & a.d_mask;
+    uint64_t k;
+    uint32_t id, dl;
+    u32x4 n16;
+    for (uint32_t step = 0;; ++step) {
+        k = a.d_key[slot];
+        id = a.d_id[slot];
+        dl = a.d_len[slot];
+        n16 = *(const u32x4*)(a.d_name16 + 16ull * slot);
+        if (k == h) break;
+        if (k == kEmpty || step >= a.d_mask) return false;
+        slot = (slot + 1) & a.d_mask;
+    }
+    if (id == kNoId || id >= a.max_services || dl != nl) return false;
+    bool eq = true;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) eq &= (uint32_t)u[j] == ((n16[j >> 2] >> (8 * (j & 3))) & 0xFFu);  // (zero padded)
+    if (!eq) return false;
+    if (nl > 16) {
+        const uint8_t* y = (const uint8_t*)(uintptr_t)a.d_ptr[slot];
+        for (uint32_t q0 = 16; q0 < nl; q0 += 16) {
+            uint8_t x[16], v[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                x[j] = q0 + j < nl ? nm[q0 + j] : 0;
+                v[j] = q0 + j < nl ? y[q0 + j] : 0;
+            }
+            bool e2 = true;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) e2 &= x[j] == v[j];
+            if (!e2) return false;
+        }
+    }
+    a.svc[i] = id;
+    return true;
+}
+
+__device__ __forceinline__ void publish_name_h(const IngArgs& a, uint64_t i, const uint8_t* nm, uint32_t nl, uint64_t h) {
+    a.svc_hash[i] = h;
+    a.name_ptr[i] = (uint64_t)(uintptr_t)nm;
+    a.name_len[i] = nl;
+}
+
 // D2 (LDS): one wave per block of kLdsBlock consecutive fragments, in rounds. A round takes the
 // next fragments (at most 64, one per lane) whose LDS regions fit the wave's kLdsBudget bytes. A
 // lane's region holds its decompressed Span at the front and its compressed bytes at the back
@@ -1314,7 +1393,12 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                 if (unknown) nl = sizeof(kUnknown) - 1;
                 ING_STAMP(3);
                 if (r >= 0) {
+#if ZK_ING_NAME16
+                    uint64_t nh = 0;
+                    if (r && !resolve16(a, i, nm, nl, &nh)) {
+#else
                     if (r && !try_resolve(a, i, nm, nl, d_hash(nm, nl))) {
+#endif
                         if (!unknown) {  // the name lies in this lane's own bytes
                             const uint64_t off = nmo - p0;
                             if (a.snappy) {
@@ -1331,7 +1415,11 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                                 nm = a.buf + b + off;  // thrift codec: the name is in the input buffer
                             }
                         }
+#if ZK_ING_NAME16
+                        if (r >= 0) publish_name_h(a, i, nm, nl, nh);
+#else
                         if (r >= 0) publish_name(a, i, nm, nl);
+#endif
                     }
                     if (r >= 0) a.keep[i] = 1u;
                 }
@@ -1443,6 +1531,8 @@ struct zk_ingest_dev {
     uint32_t* d_id = nullptr;
     uint64_t* d_ptr = nullptr;
     uint32_t* d_len = nullptr;
+    uint8_t* d_name16 = nullptr;     // 16 bytes per slot: the first bytes of its name (zero padded)
+    std::vector<uint8_t> name16;     // host mirror
     uint8_t* arena = nullptr;  // names, device copy (kUnknown first)
     uint64_t arena_cap = 0, arena_used = 0;
     std::vector<std::string> names;
@@ -1496,6 +1586,7 @@ zk_status zk_ingest_dev_create(int32_t device, void* stream, uint32_t max_servic
     while (t < 2 * max_services) t <<= 1;
     g->table = t;
     g->slot_id.assign(t, kNoId);
+    g->name16.assign((size_t)t * 16, 0);
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) {
         if (stream) {
@@ -1511,6 +1602,8 @@ zk_status zk_ingest_dev_create(int32_t device, void* stream, uint32_t max_servic
     if (e == hipSuccess) e = hipMalloc(&g->d_id, (uint64_t)t * 4);
     if (e == hipSuccess) e = hipMalloc(&g->d_ptr, (uint64_t)t * 8);
     if (e == hipSuccess) e = hipMalloc(&g->d_len, (uint64_t)t * 4);
+    if (e == hipSuccess) e = hipMalloc(&g->d_name16, (uint64_t)t * 16);
+    if (e == hipSuccess) e = hipMemsetAsync(g->d_name16, 0, (uint64_t)t * 16, g->stream);
     if (e == hipSuccess) e = hipMalloc(&g->arena, g->arena_cap);
     if (e == hipSuccess) e = hipMalloc(&g->counts, 16 * 8);
     if (e == hipSuccess) e = hipMemsetAsync(g->d_key, 0, (uint64_t)t * 8, g->stream);
@@ -1536,6 +1629,7 @@ zk_status zk_ingest_dev_destroy(zk_ingest_dev* g) {
     hipFree(g->d_id);
     hipFree(g->d_ptr);
     hipFree(g->d_len);
+    hipFree(g->d_name16);
     hipFree(g->arena);
     hipFree(g->counts);
     hipFree(g->batch);
@@ -1621,6 +1715,7 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     a.d_id = g->d_id;
     a.d_ptr = g->d_ptr;
     a.d_len = g->d_len;
+    a.d_name16 = g->d_name16;
     a.d_mask = g->table - 1;
     a.max_services = g->max_services;
     a.unknown = g->arena;
@@ -1698,12 +1793,14 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
         ptr[q] = (uint64_t)(uintptr_t)(g->arena + g->arena_used);
         g->arena_used += len[q];
         g->slot_id[q] = (uint32_t)g->names.size();
+        memcpy(&g->name16[(size_t)q * 16], nm.data(), std::min<size_t>(16, nm.size()));
         g->names.push_back(std::move(nm));
         changed = true;
     }
     if (changed) {
         ING_HIP(g, hipMemcpyAsync(g->d_id, g->slot_id.data(), g->slot_id.size() * 4, hipMemcpyHostToDevice, s));
         ING_HIP(g, hipMemcpyAsync(g->d_ptr, ptr.data(), ptr.size() * 8, hipMemcpyHostToDevice, s));
+        ING_HIP(g, hipMemcpyAsync(g->d_name16, g->name16.data(), g->name16.size(), hipMemcpyHostToDevice, s));
     }
     // D4, the status counts
     ING_HIP(g, launch_checked("k_ing_lookup", k_ing_lookup, grid, blk, 0, s, a));
