@@ -1271,6 +1271,22 @@ __device__ __forceinline__ unsigned long long ing_memtime() {
 #define ING_STAMP_FLUSH()
 #endif
 
+// ZK_ING_PREFETCH: the next round's fragments' first kPreBlk 16-byte blocks are loaded into
+// registers during this round (with their headers), so a round's copy-in waits on no global load
+// for fragments of up to kPreBlk * 16 - 15 bytes.
+#ifndef ZK_ING_PREFETCH
+#define ZK_ING_PREFETCH 1
+#endif
+constexpr int kPreBlk = 16;
+typedef unsigned int ing_u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) ing_u32x4 ing_g_u32x4;
+
+__device__ __forceinline__ uint32_t copy_blocks(const uint8_t* buf, uint64_t b, uint64_t e, bool h, ing_g_u32x4** g) {
+    const uint32_t mis = (uint32_t)((uintptr_t)(buf + b) & 15u);
+    *g = (ing_g_u32x4*)((uintptr_t)(buf + b) & ~(uintptr_t)15);
+    return h && e > b ? (uint32_t)((e - b + mis + 15) >> 4) : 0u;
+}
+
 __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
     __shared__ __align__(16) uint8_t s_buf[kLdsBudget];
     const uint32_t lane = threadIdx.x;
@@ -1283,6 +1299,16 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
     uint64_t nb = nh ? a.offsets[blk0 + lane] : 0, ne = nh ? a.offsets[blk0 + lane + 1] : 0;
     uint32_t hb[5];
     head_bytes(a, nh, nb, ne, hb);
+#if ZK_ING_PREFETCH
+    ing_u32x4 pre[kPreBlk];
+    {
+        ing_g_u32x4* pg;
+        const uint32_t pn = copy_blocks(a.buf, nb, ne, nh, &pg);
+#pragma unroll
+        for (int c = 0; c < kPreBlk; ++c)
+            if ((uint32_t)c < pn) pre[c] = pg[c];
+    }
+#endif
     for (uint64_t f0 = blk0; f0 < blk1;) {  // uniform
         const uint64_t i = f0 + lane;
         const bool have = i < blk1;
@@ -1345,15 +1371,29 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                 // [D - mis, D + clen + 15] inside [0, R) since R >= clen + kLdsSlack
                 D = ((R - 16u - (uint32_t)clen - mis) & ~15u) + mis;
                 // 16-B blocks through a global-space pointer (global_load, not a flat load)
-                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-                typedef const __attribute__((address_space(1))) u32x4 g_u32x4;
-                g_u32x4* g = (g_u32x4*)((uintptr_t)(a.buf + b) & ~(uintptr_t)15);
+                ing_g_u32x4* g = (ing_g_u32x4*)((uintptr_t)(a.buf + b) & ~(uintptr_t)15);
                 const uint32_t nblk = (uint32_t)((clen + mis + 15) >> 4);
-                u32x4* dst = reinterpret_cast<u32x4*>(reg + D - mis);
+                ing_u32x4* dst = reinterpret_cast<ing_u32x4*>(reg + D - mis);
+#if ZK_ING_PREFETCH
+#pragma unroll
+                for (int c = 0; c < kPreBlk; ++c)
+                    if ((uint32_t)c < nblk) dst[c] = pre[c];
+                for (uint32_t c = kPreBlk; c < nblk; ++c) dst[c] = g[c];
+#else
                 for (uint32_t c = 0; c < nblk; ++c) dst[c] = g[c];
+#endif
             }
         }
         head_bytes(a, nh, nb, ne, hb);  // the next round's headers, in flight during this round's decode
+#if ZK_ING_PREFETCH
+        {
+            ing_g_u32x4* pg;
+            const uint32_t pn = copy_blocks(a.buf, nb, ne, nh, &pg);
+#pragma unroll
+            for (int c = 0; c < kPreBlk; ++c)
+                if ((uint32_t)c < pn) pre[c] = pg[c];
+        }
+#endif
         if (go) {
             ING_STAMP(1);
             // the region as an LDS pointer: the decoder's byte and word reads become ds_read_*.
