@@ -108,6 +108,10 @@ zk_status   zk_ingest_dev_spans(zk_ingest_dev* ing, const uint8_t* buf, const ui
                                 uint32_t codec, uint32_t flags, const zk_span_cols* out, uint64_t* n_out,
                                 uint64_t* n_rejected);
 zk_status   zk_ingest_dev_num_services(const zk_ingest_dev* ing, uint32_t* n);
+/* Snappy scratch (deferred fragments' Spans, names not yet in the dictionary): bump-allocated per
+ * batch and grown when a batch runs out (the fragments that missed out are decoded again). `bytes`
+ * sets its size from the next batch on; 0 = automatic (max(64 MiB, 24 B per fragment)). */
+zk_status   zk_ingest_dev_set_scratch(zk_ingest_dev* ing, uint64_t bytes);
 zk_status   zk_ingest_dev_service_name(const zk_ingest_dev* ing, uint32_t id, char* buf, uint64_t cap,
                                        uint64_t* len);
 

@@ -462,7 +462,7 @@ def test_device_decoder_large_fragments_take_the_global_path(gpu, snappy):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("scratch", [1, 200, 30000])
-def test_device_decoder_scratch_exhaustion_decodes_again(gpu, monkeypatch, scratch):
+def test_device_decoder_scratch_exhaustion_decodes_again(gpu, scratch):
     """The Snappy scratch (deferred fragments' Spans, names of new services) is bump-allocated from
     one counter; a decoder created with a tiny one runs out, grows it and decodes the fragments that
     missed out again: records and rejections equal the host decoder's, batch after batch."""
@@ -470,10 +470,9 @@ def test_device_decoder_scratch_exhaustion_decodes_again(gpu, monkeypatch, scrat
 
     from zipkin_amd.ingest import DeviceSpanDecoder
 
-    monkeypatch.setenv("ZK_INGEST_SCRATCH_BYTES", str(scratch))
     rnd = random.Random(79)
     hd = SpanDecoder()
-    dd = DeviceSpanDecoder(256)
+    dd = DeviceSpanDecoder(256, scratch_bytes=scratch)
     for batch in range(3):
         spans = gen_traces(790 + batch, 200, max_depth=4, anomalies=0.3)
         out = []

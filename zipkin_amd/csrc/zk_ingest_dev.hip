@@ -18,7 +18,6 @@
 //   D5 k_ing_compact    accepted records -> the caller's columns, input order kept
 //
 // Every byte read is bounds-checked: corrupt input marks the fragment undecodable, never faults.
-#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -1582,7 +1581,7 @@ struct zk_ingest_dev {
     uint64_t batch_cap = 0;
     uint8_t* scratch = nullptr;  // Snappy: bump-allocated per batch (deferred Spans, new names)
     uint64_t scratch_cap = 0;
-    uint64_t scratch_min = 0;    // first size (ZK_INGEST_SCRATCH_BYTES; else from the batch size)
+    uint64_t scratch_min = 0;    // first size (zk_ingest_dev_set_scratch; 0: from the batch size)
     void* cub = nullptr;
     size_t cub_cap = 0;
     unsigned long long* counts = nullptr;  // [8] per status, [8] first_bad, [10] scratch bytes taken
@@ -1637,7 +1636,6 @@ zk_status zk_ingest_dev_create(int32_t device, void* stream, uint32_t max_servic
         }
     }
     g->arena_cap = 1 << 16;
-    if (const char* sb = getenv("ZK_INGEST_SCRATCH_BYTES")) g->scratch_min = strtoull(sb, nullptr, 10);
     if (e == hipSuccess) e = hipMalloc(&g->d_key, (uint64_t)t * 8);
     if (e == hipSuccess) e = hipMalloc(&g->d_id, (uint64_t)t * 4);
     if (e == hipSuccess) e = hipMalloc(&g->d_ptr, (uint64_t)t * 8);
@@ -1682,6 +1680,19 @@ zk_status zk_ingest_dev_destroy(zk_ingest_dev* g) {
 }
 
 const char* zk_ingest_dev_last_error(const zk_ingest_dev* g) { return g ? g->err.c_str() : "null decoder"; }
+
+zk_status zk_ingest_dev_set_scratch(zk_ingest_dev* g, uint64_t bytes) {
+    ZK_GUARD_BEGIN
+    if (!g) return ZK_ERR_INVALID_ARG;
+    ING_HIP(g, hipSetDevice(g->device));
+    ING_HIP(g, hipStreamSynchronize(g->stream));  // no batch may still use the old scratch
+    hipFree(g->scratch);
+    g->scratch = nullptr;
+    g->scratch_cap = 0;
+    g->scratch_min = bytes;  // allocated by the next Snappy batch
+    return ZK_OK;
+    ZK_GUARD_END
+}
 
 #ifdef ZK_ING_STAMPS
 int zk_debug_ing_stamps(unsigned long long* out, int reset) {

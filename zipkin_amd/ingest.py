@@ -135,7 +135,8 @@ class DeviceSpanDecoder:
     `decode_device(buf, offsets, n)` takes torch tensors (uint8 bytes, int64 offsets[n+1]) on the
     device; `decode(blobs)` uploads a list of bytes objects first (tests, small batches)."""
 
-    def __init__(self, max_services: int = 4096, *, device: int = 0, stream: int | None = None):
+    def __init__(self, max_services: int = 4096, *, device: int = 0, stream: int | None = None,
+                 scratch_bytes: int = 0):
         self._L = _abi.lib()
         h = C.c_void_p()
         st = self._L.zk_ingest_dev_create(device, stream, max_services, C.byref(h))
@@ -143,6 +144,10 @@ class DeviceSpanDecoder:
             raise _abi.ZkError(st, _abi.status_str(st))
         self._h = h
         self.device = device
+        if scratch_bytes:  # the Snappy scratch's first size (zk_ingest_dev_set_scratch); it grows on demand
+            st = self._L.zk_ingest_dev_set_scratch(self._h, scratch_bytes)
+            if st != _abi.ZK_OK:
+                raise _abi.ZkError(st, _abi.status_str(st))
 
     def close(self) -> None:
         if getattr(self, "_h", None):
