@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-T=r05f
+T=${TAG:-r05f}
 if [ "${PART:-a}" = a ]; then
   timeout -k 10 700 python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests/ > gpurun_out/${T}_gpu_tests.txt 2>&1 || { echo "tests failed"; tail -30 gpurun_out/${T}_gpu_tests.txt; exit 1; }
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.txt 2>&1 || { echo "smoke failed"; exit 1; }
@@ -19,5 +19,6 @@ else
   done
   timeout -k 10 400 python -u bench.py --order shuffled > gpurun_out/${T}_shuffled.json 2> gpurun_out/${T}_shuffled.err || { echo "shuffled failed"; tail gpurun_out/${T}_shuffled.err; exit 1; }
   timeout -k 10 500 python -u -m pytest -q -s --timeout 400 --timeout-method thread tests/test_gpu_jobs.py > gpurun_out/${T}_jobs.txt 2>&1 || { echo "jobs failed"; tail -20 gpurun_out/${T}_jobs.txt; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof_ingest -o ingest --output-format csv -- python3 bench.py --workload ingest --steps 10 --cpu-sample 0 > gpurun_out/${T}_prof_ingest.log 2>&1 || { echo "ingest rocprof failed"; exit 1; }
 fi
 echo "part ${PART:-a} done"

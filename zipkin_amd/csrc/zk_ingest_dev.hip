@@ -429,6 +429,10 @@ struct IngArgs {
     uint64_t* name_ptr;  // device address of the service name bytes
     uint32_t* name_len;
     uint32_t* keep;      // 1 = record goes to the output (n + 1 for the scan)
+    uint32_t* pub;       // fragments that published a name for D3/D4 (count in *pub_n)
+    unsigned long long* pub_n;
+    uint32_t* def;       // fragments the LDS decoder deferred (count in *def_n)
+    unsigned long long* def_n;
     uint32_t* pos;       // n + 1
     // dictionary
     uint64_t* d_key;
@@ -872,16 +876,47 @@ __device__ __forceinline__ int parse_record_fast(const IngArgs& a, uint64_t i, c
     return (srv_set || cli_set) ? 1 : 0;
 }
 
+// ZK_ING_LISTS: the LDS decoder lists the fragments it defers and every decoder lists the
+// fragments that publish a name, so the deferred decode, D3 and D4 visit those alone (after the
+// first batches of a decoder both lists are empty) instead of sweeping all n fragments.
+#ifndef ZK_ING_LISTS
+#define ZK_ING_LISTS 1
+#endif
+// one atomic per wave: the active lanes take consecutive entries
+__device__ __forceinline__ void list_add(uint32_t* list, unsigned long long* cnt, uint64_t i) {
+    const unsigned long long mask = __ballot(1);
+    const uint32_t lane = __lane_id();
+    const uint32_t leader = (uint32_t)__ffsll(mask) - 1u;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(cnt, (unsigned long long)__popcll(mask));
+    base = __shfl(base, (int)leader);
+    list[base + (uint64_t)__popcll(mask & ((1ull << lane) - 1ull))] = (uint32_t)i;
+}
+
 __device__ __forceinline__ void publish_name(const IngArgs& a, uint64_t i, const uint8_t* nm, uint32_t nl) {
     a.svc_hash[i] = d_hash(nm, nl);
     a.name_ptr[i] = (uint64_t)(uintptr_t)nm;
     a.name_len[i] = nl;
+#if ZK_ING_LISTS
+    list_add(a.pub, a.pub_n, i);
+#endif
 }
 
-// D2 (global memory): the fragments marked `mode` (kStDefer by the LDS kernel, or kStNoScratch)
-__global__ __launch_bounds__(kIngWG) void k_ing_decode(IngArgs a, uint32_t mode) {
-    const uint64_t i = (uint64_t)blockIdx.x * kIngWG + threadIdx.x;
-    if (i >= a.n || a.status[i] != mode) return;
+// the fragment index of work item t of a list kernel (grid-stride over the list, or over all n)
+#if ZK_ING_LISTS
+#define ING_FOR_LIST(list, cnt, i)                                                              \
+    const uint64_t ing_m = *(cnt);                                                              \
+    for (uint64_t ing_t = (uint64_t)blockIdx.x * kIngWG + threadIdx.x; ing_t < ing_m;           \
+         ing_t += (uint64_t)gridDim.x * kIngWG)                                                 \
+        if (const uint64_t i = (list)[ing_t]; true)
+#else
+#define ING_FOR_LIST(list, cnt, i)                                                              \
+    for (uint64_t i = (uint64_t)blockIdx.x * kIngWG + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * kIngWG)
+#endif
+
+// D2 (global memory): a fragment marked `mode` (kStDefer by the LDS kernel, or kStNoScratch)
+__device__ __forceinline__ void ing_decode_one(const IngArgs& a, uint64_t i, uint32_t mode) {
+    if (a.status[i] != mode) return;
     a.status[i] = kStOk;
     a.keep[i] = 0u;
     a.svc_hash[i] = 0ull;
@@ -914,6 +949,16 @@ __global__ __launch_bounds__(kIngWG) void k_ing_decode(IngArgs a, uint32_t mode)
     if (r < 0) return;
     if (r) publish_name(a, i, nm, nl);
     a.keep[i] = 1u;
+}
+
+// the deferred fragments (the LDS decoder's list), or every fragment marked kStNoScratch
+__global__ __launch_bounds__(kIngWG) void k_ing_decode(IngArgs a, uint32_t mode) {
+    if (mode == kStDefer) {
+        ING_FOR_LIST(a.def, a.def_n, i) ing_decode_one(a, i, mode);
+    } else {
+        for (uint64_t i = (uint64_t)blockIdx.x * kIngWG + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * kIngWG)
+            ing_decode_one(a, i, mode);
+    }
 }
 
 // A name the dictionary already holds (an id assigned by an earlier batch) resolves right here:
@@ -1024,6 +1069,9 @@ __device__ __forceinline__ void publish_name_h(const IngArgs& a, uint64_t i, con
     a.svc_hash[i] = h;
     a.name_ptr[i] = (uint64_t)(uintptr_t)nm;
     a.name_len[i] = nl;
+#if ZK_ING_LISTS
+    list_add(a.pub, a.pub_n, i);
+#endif
 }
 
 // D2 (LDS): one wave per block of kLdsBlock consecutive fragments, in rounds. A round takes the
@@ -1364,6 +1412,9 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
             a.keep[i] = 0u;
             a.svc_hash[i] = 0ull;
             a.status[i] = st == kStOk && !fits ? kStDefer : st;
+#if ZK_ING_LISTS
+            if (st == kStOk && !fits) list_add(a.def, a.def_n, i);
+#endif
             if (go) {
                 mis = (uint32_t)((uintptr_t)(a.buf + b) & 15u);
                 // input at offset D of the region (D = mis mod 16): its aligned 16-B blocks cover
@@ -1416,6 +1467,9 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
             ING_STAMP(2);
             if (!ok) {
                 a.status[i] = unsafe ? kStDefer : kStUndecodable;
+#if ZK_ING_LISTS
+                if (unsafe) list_add(a.def, a.def_n, i);
+#endif
             } else {
                 const lds_u8* const lbase = (const lds_u8*)s_buf;
                 const uint32_t p0 = (uint32_t)(src - lbase);
@@ -1472,9 +1526,8 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
     ING_STAMP_FLUSH();
 }
 
-__global__ __launch_bounds__(kIngWG) void k_ing_dict_insert(IngArgs a) {
-    const uint64_t i = (uint64_t)blockIdx.x * kIngWG + threadIdx.x;
-    if (i >= a.n || !a.keep[i]) return;
+__device__ __forceinline__ void ing_insert_one(const IngArgs& a, uint64_t i) {
+    if (!a.keep[i]) return;
     const uint64_t h = a.svc_hash[i];
     if (!h) return;
     uint32_t slot = (uint32_t)h & a.d_mask;
@@ -1497,9 +1550,12 @@ __global__ __launch_bounds__(kIngWG) void k_ing_dict_insert(IngArgs a) {
     }
 }
 
-__global__ __launch_bounds__(kIngWG) void k_ing_lookup(IngArgs a) {
-    const uint64_t i = (uint64_t)blockIdx.x * kIngWG + threadIdx.x;
-    if (i >= a.n || !a.keep[i]) return;
+__global__ __launch_bounds__(kIngWG) void k_ing_dict_insert(IngArgs a) {
+    ING_FOR_LIST(a.pub, a.pub_n, i) ing_insert_one(a, i);
+}
+
+__device__ __forceinline__ void ing_lookup_one(const IngArgs& a, uint64_t i) {
+    if (!a.keep[i]) return;
     const uint64_t h = a.svc_hash[i];
     if (!h) return;
     uint32_t slot = (uint32_t)h & a.d_mask;
@@ -1530,6 +1586,10 @@ __global__ __launch_bounds__(kIngWG) void k_ing_lookup(IngArgs a) {
         return;
     }
     a.svc[i] = id;
+}
+
+__global__ __launch_bounds__(kIngWG) void k_ing_lookup(IngArgs a) {
+    ING_FOR_LIST(a.pub, a.pub_n, i) ing_lookup_one(a, i);
 }
 
 __global__ __launch_bounds__(kIngWG) void k_ing_compact(IngArgs a, zk_span_cols o) {
@@ -1584,7 +1644,8 @@ struct zk_ingest_dev {
     uint64_t scratch_min = 0;    // first size (zk_ingest_dev_set_scratch; 0: from the batch size)
     void* cub = nullptr;
     size_t cub_cap = 0;
-    unsigned long long* counts = nullptr;  // [8] per status, [8] first_bad, [10] scratch bytes taken
+    unsigned long long* counts = nullptr;  // [8] per status, [8] first_bad, [10] scratch bytes taken,
+                                           // [11] / [12] published / deferred list lengths
     std::string err;
 };
 
@@ -1720,7 +1781,7 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     ING_HIP(g, hipSetDevice(g->device));
     // per-fragment arrays: 8-byte columns first, then 4-byte, then 1-byte
     const uint64_t n1 = n + 1;
-    const uint64_t bytes = align256(8 * n1) * 8 + align256(4 * n1) * 5 + align256(n1);
+    const uint64_t bytes = align256(8 * n1) * 8 + align256(4 * n1) * 7 + align256(n1);
     if (bytes > g->batch_cap) {
         hipFree(g->batch);
         g->batch = nullptr;
@@ -1761,6 +1822,8 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     a.svc = (uint32_t*)out->service_id;
     a.keep = (uint32_t*)take(4 * n1);
     a.pos = (uint32_t*)take(4 * n1);
+    a.pub = (uint32_t*)take(4 * n1);
+    a.def = (uint32_t*)take(4 * n1);
     a.status = take(n1);
     a.d_key = g->d_key;
     a.d_id = g->d_id;
@@ -1771,6 +1834,7 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     a.max_services = g->max_services;
     a.unknown = g->arena;
     const dim3 grid((unsigned)((n + kIngWG - 1) / kIngWG)), blk(kIngWG);
+    const dim3 lgrid(std::min<unsigned>(grid.x, 2048u));  // the list kernels (grid-stride)
     hipStream_t s = g->stream;
     size_t need = 0;
     ING_HIP(g, hipcub::DeviceScan::ExclusiveSum(nullptr, need, a.keep, a.pos, (int)n1, s));
@@ -1786,15 +1850,17 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
         g->scratch_cap = cap;
     }
     unsigned long long* used = g->counts + 10;
-    ING_HIP(g, hipMemsetAsync(used, 0, 8, s));
+    ING_HIP(g, hipMemsetAsync(used, 0, 3 * 8, s));  // scratch taken, pub_n, def_n
+    a.pub_n = g->counts + 11;
+    a.def_n = g->counts + 12;
     a.scratch = g->scratch;
     a.scratch_cap = g->scratch_cap;
     a.scratch_used = used;
     // D1 + D2, D3
     ING_HIP(g, launch_checked("k_ing_decode_lds", k_ing_decode_lds, dim3((unsigned)((n + kLdsBlock - 1) / kLdsBlock)),
                               dim3(kLdsWG), 0, s, a));
-    ING_HIP(g, launch_checked("k_ing_decode", k_ing_decode, grid, blk, 0, s, a, (uint32_t)kStDefer));
-    ING_HIP(g, launch_checked("k_ing_dict_insert", k_ing_dict_insert, grid, blk, 0, s, a));
+    ING_HIP(g, launch_checked("k_ing_decode", k_ing_decode, lgrid, blk, 0, s, a, (uint32_t)kStDefer));
+    ING_HIP(g, launch_checked("k_ing_dict_insert", k_ing_dict_insert, lgrid, blk, 0, s, a));
     std::vector<uint64_t> key(g->table), ptr(g->table);
     std::vector<uint32_t> len(g->table);
     std::vector<uint8_t*> retired;  // old arenas and scratch stay valid until this batch's lookups are done
@@ -1817,8 +1883,8 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
         ING_HIP(g, hipMemsetAsync(used, 0, 8, s));
         a.scratch = g->scratch;
         a.scratch_cap = cap;
-        ING_HIP(g, launch_checked("k_ing_decode", k_ing_decode, grid, blk, 0, s, a, (uint32_t)kStNoScratch));
-        ING_HIP(g, launch_checked("k_ing_dict_insert", k_ing_dict_insert, grid, blk, 0, s, a));
+        ING_HIP(g, launch_checked("k_ing_decode", k_ing_decode, lgrid, blk, 0, s, a, (uint32_t)kStNoScratch));
+        ING_HIP(g, launch_checked("k_ing_dict_insert", k_ing_dict_insert, lgrid, blk, 0, s, a));
     }
     // ids for new slots, in slot order; their names into the device arena
     bool changed = false;
@@ -1854,7 +1920,7 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
         ING_HIP(g, hipMemcpyAsync(g->d_name16, g->name16.data(), g->name16.size(), hipMemcpyHostToDevice, s));
     }
     // D4, the status counts
-    ING_HIP(g, launch_checked("k_ing_lookup", k_ing_lookup, grid, blk, 0, s, a));
+    ING_HIP(g, launch_checked("k_ing_lookup", k_ing_lookup, lgrid, blk, 0, s, a));
     ING_HIP(g, hipMemsetAsync(g->counts, 0, 8 * 8, s));
     ING_HIP(g, hipMemsetAsync(g->counts + 8, 0xFF, 8, s));
     ING_HIP(g, launch_checked("k_ing_count", k_ing_count, grid, blk, 0, s, (const uint8_t*)a.status, n, g->counts,
