@@ -1089,6 +1089,17 @@ constexpr uint32_t kLdsWG = 64;
 #define ZK_ING_BUDGET 20480  // LDS bytes per wave (8 waves per CU)
 #endif
 constexpr uint32_t kLdsBudget = ZK_ING_BUDGET;
+// ZK_ING_TAIL: 1 = a region keeps 16 bytes after its input for the copy-in's last 16-byte block;
+// 0 = that block may spill up to 15 bytes into the next region's first bytes (output the next
+// lane writes before it reads them), with 16 bytes kept free at the end of the wave's buffer.
+// ZK_ING_SKEW: 1 = a lane's Span starts 4 * (lane group) bytes into its region (bank spread).
+#ifndef ZK_ING_TAIL
+#define ZK_ING_TAIL 1
+#endif
+#ifndef ZK_ING_SKEW
+#define ZK_ING_SKEW 0  // off since round 5: 4.70 -> 4.65 ms (profiles/r05/ab_ingest_layout.txt)
+#endif
+constexpr uint32_t kLdsUse = kLdsBudget - (ZK_ING_TAIL ? 0u : 16u);  // bytes the regions may take
 constexpr uint32_t kLdsBlock = 1024;
 // Region bytes beyond max(raw, compressed): the input's placement (16 B of block tail + up to 15 of
 // misalignment) and the lane's bank skew (up to 12). A region of raw + slack bytes also holds the
@@ -1368,7 +1379,7 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
             if (st == kStOk) {
                 clen = ne - nb;
                 const uint64_t r = ((raw > clen ? raw : clen) + kLdsSlack + 15) & ~15ull;
-                need = r > kLdsBudget ? kLdsBudget + 1 : (uint32_t)r;
+                need = r > kLdsUse ? kLdsUse + 1 : (uint32_t)r;
             }
         }
         // Uniform layout (every region of the round has the size R of the largest, R / 16 odd, lane
@@ -1388,17 +1399,17 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
         if (uniform) {
             R = mx < 16u ? 16u : mx;
             if (((R >> 4) & 1u) == 0u) R += 16u;
-            k = kLdsBudget / R;
+            k = kLdsUse / R;
             if (k > 64u) k = 64u;
             R0 = lane * R;
             fits = true;
         } else {
             const uint32_t incl = wave_incl_scan(need);
             // this round: the longest prefix of lanes that fits (at least lane 0, to make progress)
-            k = (uint32_t)__popcll(__ballot(have && incl <= kLdsBudget));
+            k = (uint32_t)__popcll(__ballot(have && incl <= kLdsUse));
             if (k == 0) k = 1;  // lane 0 alone does not fit: deferred below
             R0 = incl - need;
-            fits = incl <= kLdsBudget;
+            fits = incl <= kLdsUse;
         }
         ING_STAMP(0);
         // the next round's extents (its copy-in below waits for them in passing: loads return in order)
@@ -1419,7 +1430,7 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                 mis = (uint32_t)((uintptr_t)(a.buf + b) & 15u);
                 // input at offset D of the region (D = mis mod 16): its aligned 16-B blocks cover
                 // [D - mis, D + clen + 15] inside [0, R) since R >= clen + kLdsSlack
-                D = ((R - 16u - (uint32_t)clen - mis) & ~15u) + mis;
+                D = ((R - (ZK_ING_TAIL ? 16u : 0u) - (uint32_t)clen - mis) & ~15u) + mis;
                 // 16-B blocks through a global-space pointer (global_load, not a flat load)
                 ing_g_u32x4* g = (ing_g_u32x4*)((uintptr_t)(a.buf + b) & ~(uintptr_t)15);
                 const uint32_t nblk = (uint32_t)((clen + mis + 15) >> 4);
@@ -1451,7 +1462,7 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
             // group; lanes parsing the same field at the same offset then collide. The
             // decompressed span starts 4 * (lane % 4) bytes in, spreading the lanes over all 32.
             lds_u8* const lreg = (lds_u8*)reg;
-            const uint32_t skew = 4u * (uniform ? (lane >> 4) & 3u : lane & 3u);
+            const uint32_t skew = ZK_ING_SKEW ? 4u * (uniform ? (lane >> 4) & 3u : lane & 3u) : 0u;
             const lds_u8* src = lreg + D;
             uint64_t len = clen;
             bool ok = true, unsafe = false;
