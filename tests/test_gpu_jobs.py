@@ -52,6 +52,21 @@ def test_stored_span_job_streams_ten_million_fragments(gpu):
     assert all(v == ["custom.event"] for v in job.top_annotations.values())
     assert all(v == ["http.uri"] for v in job.top_kv.values())
 
+    # the same 40 batches already in HBM, through the device decoder (run_device: dependencies only)
+    import torch
+
+    dev = [(torch.from_numpy(b).cuda(), torch.from_numpy(o.view(np.int64)).cuda(), len(o) - 1) for b, o in parts]
+    torch.cuda.synchronize()
+    djob = StoredSpanJob(clock=lambda: 10**15, max_services=S)
+    djob.run_device(dev[:1])  # warm
+    t0 = time.perf_counter()
+    ddeps = djob.run_device(dev)
+    ddt = time.perf_counter() - t0
+    print(f"StoredSpanJob.run_device: the same {len(cols)} fragments in HBM, {len(dev)} batches: {ddt * 1e3:.1f} ms, "
+          f"{len(cols) / ddt:.3e} fragments/s (device decode + accumulate + finalize)")
+    assert djob.rejected == 0 and djob.stats["records"] == len(cols)
+    assert _by_name(ddeps) == want
+
 
 def test_stored_span_job_on_the_device_decoder(gpu):
     import torch

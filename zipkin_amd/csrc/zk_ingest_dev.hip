@@ -433,6 +433,8 @@ struct IngArgs {
     unsigned long long* pub_n;
     uint32_t* def;       // fragments the LDS decoder deferred (count in *def_n)
     unsigned long long* def_n;
+    unsigned long long* claims;  // dictionary slots D3 claimed in this batch
+    uint32_t lds_block;          // fragments per wave of the LDS decoder
     uint32_t* pos;       // n + 1
     // dictionary
     uint64_t* d_key;
@@ -1074,7 +1076,7 @@ __device__ __forceinline__ void publish_name_h(const IngArgs& a, uint64_t i, con
 #endif
 }
 
-// D2 (LDS): one wave per block of kLdsBlock consecutive fragments, in rounds. A round takes the
+// D2 (LDS): one wave per block of a.lds_block consecutive fragments, in rounds. A round takes the
 // next fragments (at most 64, one per lane) whose LDS regions fit the wave's kLdsBudget bytes. A
 // lane's region holds its decompressed Span at the front and its compressed bytes at the back
 // (copied in with aligned 16-B loads): Snappy decompresses in place, front to back, and a step
@@ -1100,7 +1102,8 @@ constexpr uint32_t kLdsBudget = ZK_ING_BUDGET;
 #define ZK_ING_SKEW 0  // off since round 5: 4.70 -> 4.65 ms (profiles/r05/ab_ingest_layout.txt)
 #endif
 constexpr uint32_t kLdsUse = kLdsBudget - (ZK_ING_TAIL ? 0u : 16u);  // bytes the regions may take
-constexpr uint32_t kLdsBlock = 1024;
+constexpr uint32_t kLdsBlock = 1024;  // fragments per wave for large batches; smaller batches take
+                                      // smaller blocks (lds_block_for) so that they still fill the GPU
 // Region bytes beyond max(raw, compressed): the input's placement (16 B of block tail + up to 15 of
 // misalignment) and the lane's bank skew (up to 12). A region of raw + slack bytes also holds the
 // output's final lead over the input (raw - compressed); a Snappy stream whose lead is larger part
@@ -1348,8 +1351,8 @@ __device__ __forceinline__ uint32_t copy_blocks(const uint8_t* buf, uint64_t b, 
 __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
     __shared__ __align__(16) uint8_t s_buf[kLdsBudget];
     const uint32_t lane = threadIdx.x;
-    const uint64_t blk0 = (uint64_t)blockIdx.x * kLdsBlock;
-    const uint64_t blk1 = blk0 + kLdsBlock < a.n ? blk0 + kLdsBlock : a.n;
+    const uint64_t blk0 = (uint64_t)blockIdx.x * a.lds_block;
+    const uint64_t blk1 = blk0 + a.lds_block < a.n ? blk0 + a.lds_block : a.n;
     ING_STAMP_DECL
     // a round's fragment extents and Snappy headers are loaded during the round before (the first
     // round's here), so no round starts with a dependent global round trip
@@ -1554,6 +1557,7 @@ __device__ __forceinline__ void ing_insert_one(const IngArgs& a, uint64_t i) {
         if (old == kEmpty) {  // the first claimant names the slot (verified against the others in D4)
             a.d_ptr[slot] = a.name_ptr[i];
             a.d_len[slot] = a.name_len[i];
+            atomicAdd(a.claims, 1ull);
             return;
         }
         if (old == h) return;
@@ -1579,8 +1583,14 @@ __device__ __forceinline__ void ing_lookup_one(const IngArgs& a, uint64_t i) {
         }
         slot = (slot + 1) & a.d_mask;
     }
-    const uint32_t id = slot == kNoId ? kNoId : a.d_id[slot];
-    if (id == kNoId || id >= a.max_services) {
+    if (slot == kNoId) {  // not in the table (a full table)
+        a.status[i] = kStRange;
+        a.keep[i] = 0u;
+        return;
+    }
+    const uint32_t id = a.d_id[slot];
+    if (id == kNoId) return;  // claimed in this batch, id not given yet: the host runs D4 again
+    if (id >= a.max_services) {
         a.status[i] = kStRange;  // more distinct services than the decoder was sized for
         a.keep[i] = 0u;
         return;
@@ -1614,6 +1624,17 @@ __global__ __launch_bounds__(kIngWG) void k_ing_compact(IngArgs a, zk_span_cols 
     ((int64_t*)o.last_ts)[p] = a.last[i];
     ((uint32_t*)o.service_id)[p] = a.svc[i];
     ((uint32_t*)o.flags)[p] = a.flags[i];
+}
+
+// the names of a batch's new dictionary slots, gathered into the arena in one launch (from the
+// scratch or the input buffer where D2 published them)
+__global__ void k_ing_gather_names(const uint64_t* __restrict__ src, const uint64_t* __restrict__ dst_off,
+                                   const uint32_t* __restrict__ len, uint32_t m, uint8_t* __restrict__ arena) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    const uint8_t* x = (const uint8_t*)(uintptr_t)src[k];
+    uint8_t* y = arena + dst_off[k];
+    for (uint32_t q = 0; q < len[k]; ++q) y[q] = x[q];
 }
 
 __global__ void k_ing_count(const uint8_t* status, uint64_t n, unsigned long long* counts, unsigned int* first_bad) {
@@ -1656,7 +1677,8 @@ struct zk_ingest_dev {
     void* cub = nullptr;
     size_t cub_cap = 0;
     unsigned long long* counts = nullptr;  // [8] per status, [8] first_bad, [10] scratch bytes taken,
-                                           // [11] / [12] published / deferred list lengths
+                                           // [11] / [12] published / deferred list lengths, [13] claims
+    unsigned long long* h_counts = nullptr;  // pinned host copy of counts[0..13]
     std::string err;
 };
 
@@ -1716,6 +1738,7 @@ zk_status zk_ingest_dev_create(int32_t device, void* stream, uint32_t max_servic
     if (e == hipSuccess) e = hipMemsetAsync(g->d_name16, 0, (uint64_t)t * 16, g->stream);
     if (e == hipSuccess) e = hipMalloc(&g->arena, g->arena_cap);
     if (e == hipSuccess) e = hipMalloc(&g->counts, 16 * 8);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&g->h_counts, 16 * 8, hipHostMallocDefault);
     if (e == hipSuccess) e = hipMemsetAsync(g->d_key, 0, (uint64_t)t * 8, g->stream);
     if (e == hipSuccess) e = hipMemsetAsync(g->d_id, 0xFF, (uint64_t)t * 4, g->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(g->arena, kUnknown, sizeof(kUnknown) - 1, hipMemcpyHostToDevice, g->stream);
@@ -1742,6 +1765,7 @@ zk_status zk_ingest_dev_destroy(zk_ingest_dev* g) {
     hipFree(g->d_name16);
     hipFree(g->arena);
     hipFree(g->counts);
+    hipHostFree(g->h_counts);
     hipFree(g->batch);
     hipFree(g->scratch);
     hipFree(g->cub);
@@ -1861,84 +1885,131 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
         g->scratch_cap = cap;
     }
     unsigned long long* used = g->counts + 10;
-    ING_HIP(g, hipMemsetAsync(used, 0, 3 * 8, s));  // scratch taken, pub_n, def_n
+    ING_HIP(g, hipMemsetAsync(used, 0, 4 * 8, s));  // scratch taken, pub_n, def_n, claims
     a.pub_n = g->counts + 11;
     a.def_n = g->counts + 12;
+    a.claims = g->counts + 13;
     a.scratch = g->scratch;
     a.scratch_cap = g->scratch_cap;
     a.scratch_used = used;
     // D1 + D2, D3
-    ING_HIP(g, launch_checked("k_ing_decode_lds", k_ing_decode_lds, dim3((unsigned)((n + kLdsBlock - 1) / kLdsBlock)),
+    // fragments per wave: 1024 once a batch gives ~4096 waves (2 per wave slot of 256 CUs x 8), else
+    // the power of two that does, at least 128 (~2 rounds of a wave)
+    a.lds_block = 128;
+    while (a.lds_block < kLdsBlock && (uint64_t)a.lds_block * 4096 < n) a.lds_block <<= 1;
+    ING_HIP(g, launch_checked("k_ing_decode_lds", k_ing_decode_lds, dim3((unsigned)((n + a.lds_block - 1) / a.lds_block)),
                               dim3(kLdsWG), 0, s, a));
     ING_HIP(g, launch_checked("k_ing_decode", k_ing_decode, lgrid, blk, 0, s, a, (uint32_t)kStDefer));
     ING_HIP(g, launch_checked("k_ing_dict_insert", k_ing_dict_insert, lgrid, blk, 0, s, a));
-    std::vector<uint64_t> key(g->table), ptr(g->table);
-    std::vector<uint32_t> len(g->table);
+    // D4 and the status counts, then one small read: in the steady state (no scratch overflow, no
+    // new service names) this is the batch's only host round trip
+    unsigned long long* const hc = g->h_counts;
+    auto lookup_and_count = [&]() -> hipError_t {
+        hipError_t e = launch_checked("k_ing_lookup", k_ing_lookup, lgrid, blk, 0, s, a);
+        if (e == hipSuccess) e = hipMemsetAsync(g->counts, 0, 8 * 8, s);
+        if (e == hipSuccess) e = hipMemsetAsync(g->counts + 8, 0xFF, 8, s);
+        if (e == hipSuccess)
+            e = launch_checked("k_ing_count", k_ing_count, grid, blk, 0, s, (const uint8_t*)a.status, n, g->counts,
+                               (unsigned int*)(g->counts + 8));
+        if (e == hipSuccess) e = hipMemcpyAsync(hc, g->counts, 14 * 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        return e;
+    };
+    ING_HIP(g, lookup_and_count());
     std::vector<uint8_t*> retired;  // old arenas and scratch stay valid until this batch's lookups are done
-    for (;;) {
-        unsigned long long taken = 0;
+    if (hc[10] > g->scratch_cap || hc[13] > 0) {
+        while (hc[10] > g->scratch_cap) {
+            // the scratch ran out (kStNoScratch fragments): a larger one, and those fragments again
+            uint64_t cap = 2 * g->scratch_cap;
+            if (cap < hc[10]) cap = hc[10];
+            retired.push_back(g->scratch);
+            g->scratch = nullptr;
+            g->scratch_cap = 0;
+            ING_HIP(g, hipMalloc(&g->scratch, cap));
+            g->scratch_cap = cap;
+            ING_HIP(g, hipMemsetAsync(used, 0, 8, s));
+            a.scratch = g->scratch;
+            a.scratch_cap = cap;
+            ING_HIP(g, launch_checked("k_ing_decode", k_ing_decode, lgrid, blk, 0, s, a, (uint32_t)kStNoScratch));
+            ING_HIP(g, launch_checked("k_ing_dict_insert", k_ing_dict_insert, lgrid, blk, 0, s, a));
+            ING_HIP(g, hipMemcpyAsync(hc + 10, used, 8, hipMemcpyDeviceToHost, s));
+            ING_HIP(g, hipStreamSynchronize(s));
+        }
+        // ids for new slots, in slot order; their names into the device arena
+        std::vector<uint64_t> key(g->table), ptr(g->table);
+        std::vector<uint32_t> len(g->table);
         ING_HIP(g, hipMemcpyAsync(key.data(), g->d_key, key.size() * 8, hipMemcpyDeviceToHost, s));
         ING_HIP(g, hipMemcpyAsync(ptr.data(), g->d_ptr, ptr.size() * 8, hipMemcpyDeviceToHost, s));
         ING_HIP(g, hipMemcpyAsync(len.data(), g->d_len, len.size() * 4, hipMemcpyDeviceToHost, s));
-        ING_HIP(g, hipMemcpyAsync(&taken, used, 8, hipMemcpyDeviceToHost, s));
         ING_HIP(g, hipStreamSynchronize(s));
-        if (taken <= g->scratch_cap) break;
-        // the scratch ran out (kStNoScratch fragments): a larger one, and those fragments again
-        uint64_t cap = 2 * g->scratch_cap;
-        if (cap < taken) cap = taken;
-        retired.push_back(g->scratch);
-        g->scratch = nullptr;
-        g->scratch_cap = 0;
-        ING_HIP(g, hipMalloc(&g->scratch, cap));
-        g->scratch_cap = cap;
-        ING_HIP(g, hipMemsetAsync(used, 0, 8, s));
-        a.scratch = g->scratch;
-        a.scratch_cap = cap;
-        ING_HIP(g, launch_checked("k_ing_decode", k_ing_decode, lgrid, blk, 0, s, a, (uint32_t)kStNoScratch));
-        ING_HIP(g, launch_checked("k_ing_dict_insert", k_ing_dict_insert, lgrid, blk, 0, s, a));
-    }
-    // ids for new slots, in slot order; their names into the device arena
-    bool changed = false;
-    for (uint32_t q = 0; q < g->table; ++q) {
-        if (key[q] == kEmpty || g->slot_id[q] != kNoId) continue;
-        std::string nm(len[q], '\0');
-        if (len[q]) ING_HIP(g, hipMemcpy(&nm[0], (const void*)(uintptr_t)ptr[q], len[q], hipMemcpyDeviceToHost));
-        if (g->arena_used + len[q] > g->arena_cap) {
-            uint64_t cap = g->arena_cap;
-            while (cap < g->arena_used + len[q]) cap *= 2;
-            uint8_t* na = nullptr;
-            ING_HIP(g, hipMalloc(&na, cap));
-            ING_HIP(g, hipMemcpy(na, g->arena, g->arena_used, hipMemcpyDeviceToDevice));
-            // repoint the named slots at the new arena
-            for (uint32_t r = 0; r < g->table; ++r)
-                if (g->slot_id[r] != kNoId) ptr[r] = (uint64_t)(uintptr_t)na + (ptr[r] - (uint64_t)(uintptr_t)g->arena);
-            retired.push_back(g->arena);
-            g->arena = na;
-            g->arena_cap = cap;
-            a.unknown = na;
+        // the new slots in slot order, their names gathered into the arena by one kernel and read
+        // back in one copy
+        std::vector<uint32_t> fresh;
+        uint64_t total = 0;
+        for (uint32_t q = 0; q < g->table; ++q)
+            if (key[q] != kEmpty && g->slot_id[q] == kNoId) {
+                fresh.push_back(q);
+                total += len[q];
+            }
+        const bool changed = !fresh.empty();
+        if (changed) {
+            if (g->arena_used + total > g->arena_cap) {
+                uint64_t cap = g->arena_cap;
+                while (cap < g->arena_used + total) cap *= 2;
+                uint8_t* na = nullptr;
+                ING_HIP(g, hipMalloc(&na, cap));
+                ING_HIP(g, hipMemcpyAsync(na, g->arena, g->arena_used, hipMemcpyDeviceToDevice, s));
+                // repoint the named slots at the new arena
+                for (uint32_t r = 0; r < g->table; ++r)
+                    if (g->slot_id[r] != kNoId)
+                        ptr[r] = (uint64_t)(uintptr_t)na + (ptr[r] - (uint64_t)(uintptr_t)g->arena);
+                retired.push_back(g->arena);
+                g->arena = na;
+                g->arena_cap = cap;
+                a.unknown = na;
+            }
+            const uint32_t m = (uint32_t)fresh.size();
+            std::vector<uint64_t> gsrc(m), goff(m);
+            std::vector<uint32_t> glen(m);
+            uint64_t at = g->arena_used;
+            for (uint32_t k = 0; k < m; ++k) {
+                gsrc[k] = ptr[fresh[k]];
+                goff[k] = at;
+                glen[k] = len[fresh[k]];
+                at += glen[k];
+            }
+            uint8_t* gt = nullptr;  // the gather's table: sources, arena offsets, lengths
+            ING_HIP(g, hipMalloc(&gt, (uint64_t)m * 20));
+            retired.push_back(gt);
+            ING_HIP(g, hipMemcpyAsync(gt, gsrc.data(), (uint64_t)m * 8, hipMemcpyHostToDevice, s));
+            ING_HIP(g, hipMemcpyAsync(gt + (uint64_t)m * 8, goff.data(), (uint64_t)m * 8, hipMemcpyHostToDevice, s));
+            ING_HIP(g, hipMemcpyAsync(gt + (uint64_t)m * 16, glen.data(), (uint64_t)m * 4, hipMemcpyHostToDevice, s));
+            ING_HIP(g, launch_checked("k_ing_gather_names", k_ing_gather_names, dim3((m + 255) / 256), dim3(256), 0, s,
+                                      (const uint64_t*)gt, (const uint64_t*)(gt + (uint64_t)m * 8),
+                                      (const uint32_t*)(gt + (uint64_t)m * 16), m, g->arena));
+            std::string bytes(total, '\0');
+            if (total)
+                ING_HIP(g, hipMemcpyAsync(&bytes[0], g->arena + g->arena_used, total, hipMemcpyDeviceToHost, s));
+            ING_HIP(g, hipStreamSynchronize(s));
+            for (uint32_t k = 0; k < m; ++k) {
+                const uint32_t q = fresh[k];
+                std::string nm = bytes.substr(goff[k] - g->arena_used, glen[k]);
+                ptr[q] = (uint64_t)(uintptr_t)(g->arena + goff[k]);
+                g->slot_id[q] = (uint32_t)g->names.size();
+                memcpy(&g->name16[(size_t)q * 16], nm.data(), std::min<size_t>(16, nm.size()));
+                g->names.push_back(std::move(nm));
+            }
+            g->arena_used = at;
         }
-        if (len[q]) ING_HIP(g, hipMemcpy(g->arena + g->arena_used, nm.data(), len[q], hipMemcpyHostToDevice));
-        ptr[q] = (uint64_t)(uintptr_t)(g->arena + g->arena_used);
-        g->arena_used += len[q];
-        g->slot_id[q] = (uint32_t)g->names.size();
-        memcpy(&g->name16[(size_t)q * 16], nm.data(), std::min<size_t>(16, nm.size()));
-        g->names.push_back(std::move(nm));
-        changed = true;
+        if (changed) {
+            ING_HIP(g, hipMemcpyAsync(g->d_id, g->slot_id.data(), g->slot_id.size() * 4, hipMemcpyHostToDevice, s));
+            ING_HIP(g, hipMemcpyAsync(g->d_ptr, ptr.data(), ptr.size() * 8, hipMemcpyHostToDevice, s));
+            ING_HIP(g, hipMemcpyAsync(g->d_name16, g->name16.data(), g->name16.size(), hipMemcpyHostToDevice, s));
+        }
+        ING_HIP(g, lookup_and_count());  // D4 again, now that every claimed slot has its id
     }
-    if (changed) {
-        ING_HIP(g, hipMemcpyAsync(g->d_id, g->slot_id.data(), g->slot_id.size() * 4, hipMemcpyHostToDevice, s));
-        ING_HIP(g, hipMemcpyAsync(g->d_ptr, ptr.data(), ptr.size() * 8, hipMemcpyHostToDevice, s));
-        ING_HIP(g, hipMemcpyAsync(g->d_name16, g->name16.data(), g->name16.size(), hipMemcpyHostToDevice, s));
-    }
-    // D4, the status counts
-    ING_HIP(g, launch_checked("k_ing_lookup", k_ing_lookup, lgrid, blk, 0, s, a));
-    ING_HIP(g, hipMemsetAsync(g->counts, 0, 8 * 8, s));
-    ING_HIP(g, hipMemsetAsync(g->counts + 8, 0xFF, 8, s));
-    ING_HIP(g, launch_checked("k_ing_count", k_ing_count, grid, blk, 0, s, (const uint8_t*)a.status, n, g->counts,
-                              (unsigned int*)(g->counts + 8)));
     unsigned long long c[9];
-    ING_HIP(g, hipMemcpyAsync(c, g->counts, 9 * 8, hipMemcpyDeviceToHost, s));
-    ING_HIP(g, hipStreamSynchronize(s));
+    memcpy(c, hc, sizeof(c));
     for (uint8_t* r : retired) hipFree(r);
     uint64_t dropped = 0;  // every fragment whose status is not ok is not a record
     for (int q = 0; q < 8; ++q) dropped += c[q];
@@ -1974,8 +2045,8 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
         a.flags = (uint32_t*)tmp.flags;
         a.svc = (uint32_t*)tmp.service_id;
         ING_HIP(g, launch_checked("k_ing_compact", k_ing_compact, grid, blk, 0, s, a, *out));
+        ING_HIP(g, hipStreamSynchronize(s));
     }
-    ING_HIP(g, hipStreamSynchronize(s));
     *n_out = kept;
     *n_rejected = bad;
     return ZK_OK;
