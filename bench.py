@@ -79,6 +79,12 @@ def parse():
                          "binary annotations; c5: per-service HLL + duration histogram from span fragments; "
                          "ingest: device decode of stored Snappy+thrift fragments into columns")
     ap.add_argument("--fragments", type=int, default=20_000_000, help="ingest: stored fragments per step")
+    ap.add_argument("--comm", default=None, choices=("zk", "torch"),
+                    help="N > 1: the exchange's collective. zk (default with RCCL) = the library's own "
+                         "communicator, zk_deps_allreduce / zk_rt_allreduce (include/zkcomm.h), the call the "
+                         "JVM drop-in makes (GpuDependenciesJob.scala); torch = torch.distributed all_reduce "
+                         "of the same exchange buffer (default for the gloo rehearsal, where RCCL cannot run "
+                         "two ranks on one GPU)")
     ap.add_argument("--items", type=int, default=1_000_000_000,
                     help="c4: binary annotations per step (BASELINE configs[3]: 1e9, 12 GB in HBM)")
     a = ap.parse_args()
@@ -88,7 +94,44 @@ def parse():
         a.records = 1_000_000_000 if a.workload in ("c3", "c5") else 100_000_000
     if a.pipeline is None:
         a.pipeline = 3 if a.workload in ("c2", "c3") else 0 if a.workload == "c4" else 1
+    if a.comm is None:
+        a.comm = "zk" if os.environ.get("ZK_BENCH_BACKEND", "nccl") == "nccl" else "torch"
     return a
+
+
+def init_dist():
+    """(world, rank, local, dist or None): one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE from the
+    launcher; ZK_BENCH_BACKEND=gloo is the correctness rehearsal with several ranks on one GPU."""
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world == 1:
+        torch.cuda.set_device(0)
+        return 1, 0, 0, None
+    import torch.distributed as dist
+
+    backend = os.environ.get("ZK_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
+    torch.cuda.set_device(local)
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend)
+    return world, rank, local, dist
+
+
+def zk_comms(dist, rank, world, local, count):
+    """`count` communicators of the library (include/zkcomm.h), one per table/stream set: rank 0 makes
+    the RCCL unique ids, torch.distributed's bootstrap hands them to the other ranks (the JVM host does
+    the same over its own channel), every rank opens them in the same order."""
+    from zipkin_amd.comm import Comm, unique_id
+
+    ids = [[unique_id() for _ in range(count)] if rank == 0 else None]
+    dist.broadcast_object_list(ids, src=0)
+    return [Comm(u, rank, world, device=local) for u in ids[0]]
 
 
 def main():
@@ -104,25 +147,9 @@ def main():
     if a.workload == "ingest":
         return bench_ingest(a)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        # ZK_BENCH_BACKEND=gloo: a correctness rehearsal of the N>1 path with several ranks on one
-        # GPU (not a measurement); the driver's runs use RCCL, one rank per GPU
-        backend = os.environ.get("ZK_BENCH_BACKEND", "nccl")
-        if backend != "nccl":
-            local = local % torch.cuda.device_count()
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(0)
+    # ZK_BENCH_BACKEND=gloo: a correctness rehearsal of the N>1 path with several ranks on one GPU
+    # (not a measurement); the driver's runs use RCCL, one rank per GPU
+    world, rank, local, dist = init_dist()
     dev = torch.device("cuda", local)
 
     from zipkin_amd import DepsContext, DeviceColumns, tracegen_params
@@ -177,16 +204,48 @@ def main():
         "present": torch.empty(cells, dtype=torch.uint8, device=dev),
     }
 
+    nsets = (a.pipeline + 1) if a.pipeline != 0 else 1
+    comms, comm_note = None, None
+    if dist is not None and a.comm == "zk":
+        try:
+            comms = zk_comms(dist, rank, world, local, nsets)
+        except Exception as e:  # reported in the line; the same exchange then goes through torch
+            comm_note = f"zk_comm_create failed ({e}); torch.distributed all_reduce used instead"
+            print(f"[bench] {comm_note}", file=sys.stderr, flush=True)
+            comms = None
+        ok = torch.tensor([1 if comms is not None else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # every rank takes the same path
+        if int(ok.item()) == 0 and comms is not None:
+            for cm in comms:
+                cm.close()
+            comms = None
+            comm_note = comm_note or "zk_comm_create failed on another rank; torch.distributed all_reduce used instead"
+    ar_events = []  # (start, end) HIP events around the all-reduce of the serial warmup steps
+
+    def exchange(c, s, i, timed=False):
+        """N > 1: the merge of the ranks' tables (ZipkinAggregateJob.scala:39-43 .group.sum / .sum), on
+        the set's stream s, after its accumulate and before its finalize."""
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+        if comms is not None:
+            # zk_deps_allreduce: partial (counters folded, 56-bit limbs) -> RCCL int64 SUM -> note_merged
+            comms[i].allreduce_deps(c, total_hint)
+        else:
+            xp, xb = c.partial()
+            # the same exact limb + counter SUM through torch.distributed
+            allreduce_table(device_view(xp, xb, torch.int64, local))
+            c.note_merged(total_hint)
+        if timed:
+            e1.record(s)
+            ar_events.append((e0, e1))
+
     def step_serial():
         ctx.reset()
         # device-generated batches are trace-clustered by construction (zk_tracegen_device)
         ctx.accumulate(cols, clustered=not shuffled, verify=a.verify)
         if dist is not None:
-            # counters folded into the table tail, the table packed into 56-bit limbs (same stream)
-            xp, xb = ctx.partial()
-            # exact limb + counter SUM over xGMI (RCCL): shards are disjoint traces
-            allreduce_table(device_view(xp, xb, torch.int64, local))
-            ctx.note_merged(total_hint)
+            exchange(ctx, stream, 0, timed=True)
         ctx.finalize(out_device=out)
 
     step = step_serial
@@ -213,7 +272,8 @@ def main():
             pc.finalize(out_device=po)
 
         def step():  # noqa: F811
-            c, t, s, o = sets[state["k"] % len(sets)]
+            i = state["k"] % len(sets)
+            c, t, s, o = sets[i]
             state["k"] += 1
             torch.cuda.set_stream(s)
             c.reset()
@@ -225,9 +285,7 @@ def main():
                 ev.record(s)
                 state["reduced"] = ev
             if dist is not None:
-                xp, xb = c.partial()
-                allreduce_table(device_view(xp, xb, torch.int64, local))  # ordered on s; the host does not wait
-                c.note_merged(total_hint)
+                exchange(c, s, i)  # ordered on s; the host does not wait
             state["pending"].append((c, t, s, o))
             if len(state["pending"]) > a.pipeline:
                 finalize_oldest()
@@ -291,6 +349,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     total_records = total_hint  # the records every rank actually aggregated (shards differ in size)
+    allreduce_ms = None
+    if ar_events:
+        ms = [e0.elapsed_time(e1) for e0, e1 in ar_events[1:]] or [ar_events[0][0].elapsed_time(ar_events[0][1])]
+        allreduce_ms = sorted(ms)[len(ms) // 2]
     value = total_records * a.steps / elapsed
     join_calls = tm1["join_calls"] - tm0["join_calls"]
     join_avg_ms = (tm1["join_ms_total"] - tm0["join_ms_total"]) / max(1, join_calls)
@@ -400,6 +462,11 @@ def main():
                 "services": S,
                 "max_depth": a.max_depth,
                 "parallelism": f"traceId-hash shards x{world}" + (", RCCL all-reduce of the link table" if world > 1 else ""),
+                "collective": (None if world == 1 else
+                               "zk_deps_allreduce: libzkagg's own RCCL communicator (include/zkcomm.h), the JVM "
+                               "drop-in's call" if comms is not None else
+                               f"torch.distributed all_reduce ({os.environ.get('ZK_BENCH_BACKEND', 'nccl')}) of "
+                               "zk_deps_partial's exchange buffer" + (f" -- {comm_note}" if comm_note else "")),
                 "step": "reset + span_join + spill + [all-reduce] + finalize(m0..m4) + status check"
                         + ((f" ({a.pipeline + 1} table sets: batch k's join follows batch k-1's reduce and overlaps "
                             "its [all-reduce,] finalize, status check and reset)") if pipeline and a.overlap == "tail" else
@@ -433,6 +500,9 @@ def main():
             "parity": parity if not shuffled else {"full_vs_oracle": parity, "shuffled_vs_clustered": shuffled_parity},
             "detail": {
                 "event_ms_per_step": ev_ms / a.steps,
+                # N > 1: the exchange alone (partial + collective + note_merged), HIP events on the ctx
+                # stream around it in the serial warmup steps, median (24 MB int64 SUM at S = 500)
+                "allreduce_ms": allreduce_ms,
                 # K1 event spans inside the timed (pipelined) steps: they also cover the other table
                 # set's K2/K3 that share the chip with K1, so they are longer than the kernel
                 "pipelined_k1_event_ms": join_avg_ms,
@@ -450,6 +520,8 @@ def main():
         }
         print(json.dumps(line), flush=True)
     ctx.close()
+    for cm in comms or ():
+        cm.close()
     if dist is not None:
         dist.destroy_process_group()
 
@@ -706,11 +778,18 @@ def bench_ingest(a):
         assert rej == 0 and cols.n == n
 
     wall, ev_ms = _timed(step, a.steps, a.warmup, stream)
-    # CPU baseline: the host decoder (one thread) on the 200k-fragment set
+    # CPU baseline: the host decoder (zk_ingest_spans, its own pool of up to 16 threads) on the
+    # ~200k-fragment set, warm: one untimed decode starts the pool and fills the dictionary, then the
+    # median of 5 timed decodes
     hd = SpanDecoder()
-    t0 = time.perf_counter()
     hcols, _ = hd.decode(blobs)
-    cpu_s = time.perf_counter() - t0
+    ts = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        hd.decode(blobs)
+        ts.append(time.perf_counter() - t0)
+    cpu_s = sorted(ts)[2]
+    cpu_threads = max(1, min(16, os.cpu_count() or 1, m // 2048))  # zk_ingest.cpp kIngestThreads / MinPerThread
     # parity leg: the first and the last replica of the device's decoded columns == the host decoder
     # (zk_ingest_spans) on the same fragments, service ids compared by name (each decoder numbers its
     # own dictionary in the order it meets the names)
@@ -742,8 +821,10 @@ def bench_ingest(a):
         "roofline": {"bound": "hbm", "kernel": "whole decode (5 kernels + 2 scans)", "achieved": achieved,
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                      "algorithmic_bytes_per_step": algo},
-        "cpu_baseline": {"value": m / cpu_s, "unit": "fragments/s", "cores": 1, "kind": "port",
-                         "sample": f"{m} fragments through the host decoder (zk_ingest_spans)"},
+        "cpu_baseline": {"value": m / cpu_s, "unit": "fragments/s", "cores": cpu_threads, "kind": "port",
+                         "cpu": cpu_model(),
+                         "sample": f"{m} fragments through the host decoder (zk_ingest_spans, {cpu_threads} threads, "
+                                   f"warm pool and dictionary), median of 5: {cpu_s * 1e3:.1f} ms"},
         "parity": parity,
         "detail": {"event_ms_per_step": ev_ms / a.steps, "services": dec.num_services},
     }), flush=True)
@@ -761,23 +842,44 @@ def bench_c5(a):
 
     from zipkin_amd.realtime import RtSketch
 
-    torch.cuda.set_device(0)
-    dev = torch.device("cuda", 0)
+    # N > 1 (configs[4]: "RCCL max/merge across 8 GPUs"): ONE global set of a.records spans sharded by
+    # mix64(traceId) % N like C3; every step merges the ranks' sketches with zk_rt_allreduce (HLL
+    # registers by MAX, histogram bins by SUM) through the library's own communicator
+    world, rank, local, dist = init_dist()
+    dev = torch.device("cuda", local)
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
     S = a.services
-    ctx = DepsContext(S, device=0, stream=stream.cuda_stream, timing=True)
-    rt = RtSketch(S, stream=stream.cuda_stream)
+    ctx = DepsContext(S, device=local, stream=stream.cuda_stream, timing=True)
+    rt = RtSketch(S, device=local, stream=stream.cuda_stream)
     rt.bind(ctx, only=True)
     p = tracegen_params(a.seed, int(a.records / 15) + 1000, target_records=a.records, max_depth=a.max_depth,
-                        num_services=S)
-    cols = DeviceColumns(a.records, device="cuda:0")
+                        num_services=S, rank=rank, world=world, global_ids=world > 1)
+    cap = a.records if world == 1 else int(a.records / world * 1.02) + 1_000_000
+    cols = DeviceColumns(cap, device=f"cuda:{local}")
     n, ntr = ctx.tracegen_device(p, cols)
+    total = n
+    if dist is not None:
+        tt = torch.tensor([n], dtype=torch.int64, device=dev)
+        dist.all_reduce(tt)
+        total = int(tt.item())
+    comms = (zk_comms(dist, rank, world, local, 2 if a.pipeline != 0 else 1)
+             if dist is not None and a.comm == "zk" else None)
+
+    def merge(r, i):
+        if dist is None:
+            return
+        if comms is not None:
+            comms[i].allreduce_rt(r)  # zk_rt_allreduce on the sketch's stream
+        else:
+            from zipkin_amd.shards import merge_rt
+            merge_rt(r, device=local)
 
     def step_serial():
         ctx.reset()
         rt.reset()
-        ctx.accumulate(cols, clustered=True, verify=False)
+        ctx.accumulate(cols, clustered=True, verify=False, n=n)
+        merge(rt, 0)
 
     # K1 alone: a few serial steps before the timed run (untimed)
     step_serial()
@@ -792,22 +894,32 @@ def bench_c5(a):
     if a.pipeline != 0:
         # two context/sketch/stream sets: batch k's K1 overlaps batch k-1's partition + sketch
         stream2 = torch.cuda.Stream(device=dev)
-        ctx2 = DepsContext(S, device=0, stream=stream2.cuda_stream, timing=False)
-        rt2 = RtSketch(S, stream=stream2.cuda_stream)
+        ctx2 = DepsContext(S, device=local, stream=stream2.cuda_stream, timing=False)
+        rt2 = RtSketch(S, device=local, stream=stream2.cuda_stream)
         rt2.bind(ctx2, only=True)
         sets = [(ctx, rt, stream), (ctx2, rt2, stream2)]
         k = [0]
 
         def step():  # noqa: F811
-            c, r, s = sets[k[0] % 2]
+            i = k[0] % 2
+            c, r, s = sets[i]
             k[0] += 1
             torch.cuda.set_stream(s)
             c.reset()
             r.reset()
-            c.accumulate(cols, clustered=True, verify=False)
+            c.accumulate(cols, clustered=True, verify=False, n=n)
+            merge(r, i)
 
     tm0 = ctx.timing()
-    wall, ev_ms = _timed(step, a.steps, max(2, a.warmup), stream)
+    if dist is not None:
+        torch.cuda.synchronize()
+        dist.barrier()
+    wall, ev_ms = _timed(step, a.steps, max(2, a.warmup), stream, [sets[1][2]] if a.pipeline != 0 else ())
+    if dist is not None:
+        dist.barrier()
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
     torch.cuda.set_stream(stream)
     tm1 = ctx.timing()
     calls = tm1["join_calls"] - tm0["join_calls"]
@@ -831,16 +943,38 @@ def bench_c5(a):
     query_first_ms, query_ms = qt[0], sorted(qt[1:])[2]
     achieved = n * 40 / (k1_isolated_ms * 1e-3) / 1e9  # K1 alone (serial launches), as in the c2 line
     cpu = parity = None
-    if a.cpu_sample > 0:
+    if dist is not None:
+        # every rank holds the merged sketch: registers and bins must agree across ranks
+        import hashlib
+
+        regs, hist = rt.read()
+        dg = hashlib.sha256(regs.tobytes() + hist.tobytes()).hexdigest()
+        dgs = [None] * world
+        dist.all_gather_object(dgs, dg)
+        if len(set(dgs)) != 1:
+            raise RuntimeError(f"C5 at N = {world}: the ranks' merged sketches differ")
+        parity = {"ranks_agree": True, "sha256": dg,
+                  "checked": "HLL registers + histogram bins of every service identical on every rank after "
+                             "the all-reduce"}
+    elif a.cpu_sample > 0:
         cpu, parity = c5_parity_and_baseline(cols, min(a.cpu_sample, n), S, stream, a.cpu_threads or usable_cpus())
+    for cm in comms or ():
+        cm.close()
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     print(json.dumps({
-        "metric": "spans/sec into per-service HLL distinct traceIds + duration p50/p99 (BASELINE configs[4], 1 GPU)",
-        "value": n * a.steps / wall, "unit": "spans/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": wall * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "metric": f"spans/sec into per-service HLL distinct traceIds + duration p50/p99 (BASELINE configs[4], {world} GPU)",
+        "value": total * a.steps / wall, "unit": "spans/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": wall * 1e3 / a.steps, "higher_is_better": True,
+        "scaling": "weak" if world == 1 else "strong", "vs_baseline": None,
         "dtype": "u64", "data": "synthetic (zipkin-tracegen-shaped, generated on device)",
         "config": {"workload": f"C5: {n:.3g} span records (BASELINE configs[4]: over 1B spans), {S} services, "
                                "HLL p=14 + log-linear histogram m=7 (t-digest p50/p99 built from it)",
-                   "records": n, "traces": ntr, "services": S,
+                   "records": total, "records_per_gpu": n, "traces_per_gpu": ntr, "services": S,
+                   "collective": (None if world == 1 else "zk_rt_allreduce (libzkagg's RCCL communicator)"
+                                  if comms is not None else "torch.distributed (zipkin_amd/shards.merge_rt)"),
                    "step": "reset + K1 (merge, isValid, serviceName, duration; sketch items) + partition + sketch"
                            + (" (two sets: batch k's K1 overlaps batch k-1's partition + sketch)" if a.pipeline else "")},
         "roofline": {"bound": "hbm", "kernel": "k_span_join_stream<..., kModeEmit>", "achieved": achieved,
@@ -855,6 +989,8 @@ def bench_c5(a):
                    "median_distinct_estimate": float(sorted(est)[S // 2]),
                    "p50_p99_bins_service0": [(int(qlo[0][i]), int(qhi[0][i])) for i in range(2)]},
     }), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 def bench_c1(a):

@@ -12,8 +12,12 @@
  * Conventions (mirroring the reference's error behaviour without exceptions):
  *  - every entry point returns zk_status (0 = OK) and never throws or aborts;
  *  - zk_last_error(ctx) gives a human-readable message for the last failure;
- *  - inputs are caller-owned and only borrowed for the duration of the call
- *    (device pointers must stay valid until the ctx stream has drained them);
+ *  - inputs are caller-owned. HOST pointers are borrowed for the duration of the
+ *    call only: an entry point that stages host inputs waits until its copies have
+ *    read them (page-locked memory included), so the caller may reuse the buffers as
+ *    soon as it returns. DEVICE pointers (ZK_BATCH_DEVICE_PTRS) are read by kernels
+ *    queued on the ctx stream and must stay valid and unmodified until that stream has
+ *    drained them (zk_ctx_sync, or an event recorded after the call);
  *  - outputs go to caller buffers; sizes are queried by passing NULL;
  *  - a ctx is NOT thread-safe (one ctx per host thread, or an external lock:
  *    the reference serialises store writes with `synchronized`,
@@ -56,6 +60,8 @@ typedef enum zk_status {
     ZK_ERR_INVALID_SPAN = 11,    /* ingest: a span the reference's thrift conversion rejects (null
                                     name, annotation timestamp <= 0 or empty value,
                                     thrift.scala:64-121), or bytes that do not decode */
+    ZK_ERR_RANK_FAILED = 12,     /* multi-GPU: another rank of the job failed before the exchange
+                                    (zk_deps_abort); the merged table is incomplete */
 } zk_status;
 
 /* ------------------------------------------------------------------------------------------
@@ -245,6 +251,15 @@ zk_status zk_deps_finalize(zk_ctx* ctx, const zk_link_table* out);
 #define ZK_XCHG_BYTES(S) ((uint64_t)(S) * (uint64_t)(S) * 96u + 128u)
 zk_status zk_deps_partial(zk_ctx* ctx, void** dev_ptr, uint64_t* bytes);
 zk_status zk_deps_note_merged(zk_ctx* ctx, uint64_t total_records);
+/* A rank that fails on the host before the exchange (an undecodable span, a batch the library
+   refused, a service outside the job's list) must still make the job's collective call, or every
+   other rank waits in it forever. zk_deps_abort marks this ctx's part of the job as failed: its next
+   zk_deps_partial returns a zero table whose counter tail carries one abort mark (2^48 added to the
+   records word; records per job stay < 2^40, so up to 256 marks never reach the count), the
+   all-reduce adds it into every rank's tail, and after zk_deps_note_merged finalize returns
+   ZK_ERR_RANK_FAILED on EVERY rank. The records count the merged tail reports excludes the marks.
+   zk_deps_reset clears the mark. */
+zk_status zk_deps_abort(zk_ctx* ctx);
 
 /* ---- synthetic zipkin-tracegen workload (TraceGen.scala:50-143) ------------------------------
  * Counter-based, so host and device produce bit-identical records for the same parameters.

@@ -48,6 +48,8 @@ zk_status   zk_comm_unique_id(uint8_t* id, uint64_t bytes);  /* bytes >= ZK_COMM
 zk_status   zk_comm_create(const uint8_t* id, uint64_t bytes, uint32_t rank, uint32_t world, int32_t device,
                            zk_comm** out);
 zk_status   zk_comm_destroy(zk_comm* comm);
+/* the handle's last collective error; NULL: why the calling thread's last zk_comm_unique_id /
+   zk_comm_create failed (RCCL's message) */
 const char* zk_comm_last_error(const zk_comm* comm);
 
 /* total_records: records of the whole job (bounds the capacity check), 0 = read it from the merged

@@ -98,6 +98,8 @@ JNIEXPORT jint JNICALL FN(depsNoteMerged)(JNIEnv* env, jobject self, jlong h, jl
     return zk_deps_note_merged(CTX(h), (uint64_t)totalRecords);
 }
 
+JNIEXPORT jint JNICALL FN(depsAbort)(JNIEnv* env, jobject self, jlong h) { return zk_deps_abort(CTX(h)); }
+
 JNIEXPORT jint JNICALL FN(traceShard)(JNIEnv* env, jobject self, jlong traceId, jint world) {
     return (jint)zk_trace_shard((uint64_t)traceId, (uint32_t)world);
 }

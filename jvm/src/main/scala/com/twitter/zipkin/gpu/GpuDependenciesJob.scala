@@ -21,7 +21,9 @@
  * split by Cassandra/HBase row key is; other sources keep the spans with
  * ZkNative.traceShard(traceId, world) == rank). After the last batch every rank calls depsAllreduce --
  * one RCCL int64 SUM of the exact table's exchange form, the reference's cross-reducer .group.sum /
- * .sum (:39-43) -- and finalizes the same job-wide table with the same status; rank 0 stores it.
+ * .sum (:39-43) -- and finalizes the same job-wide table with the same status; rank 0 stores it. A
+ * rank that fails on the host before the exchange still makes that call, with an abort mark
+ * (`guarded`), so the others fail with ErrRankFailed instead of blocking in RCCL.
  *
  * Output: Dependencies(Time.epoch, Time.now, links) stored through `aggregates`, or nothing when no
  * link exists (:43-45). Strict mode turns a joined span without a service name into a failure, the
@@ -62,6 +64,7 @@ class GpuDependenciesJob(aggregates: Aggregates, device: Int = 0, strict: Boolea
   private[this] def fail(ctx: Long, st: Int): Nothing = {
     val msg = ZkNative.lastError(ctx)
     if (st == ZkNative.ErrNoService) throw new NoSuchElementException(s"None.get: $msg") // the reference's crash
+    if (st == ZkNative.ErrRankFailed) throw new IllegalStateException(s"another rank of the job failed: $msg")
     throw new IllegalStateException(s"zk status $st: $msg")
   }
 
@@ -118,6 +121,18 @@ class GpuDependenciesJob(aggregates: Aggregates, device: Int = 0, strict: Boolea
     }
   }
 
+  /** the rank's part of the job before the exchange. A rank that fails here on the host (an
+    * undecodable span, a refused batch, a service outside the job's list, the decoder thread) still
+    * makes the job's one collective call, with an abort mark (zk_deps_abort): every other rank's
+    * finalize then fails with ErrRankFailed instead of waiting in the all-reduce forever. */
+  private[this] def guarded(ctx: Long, comm: Long)(part: => Unit): Unit =
+    try part catch {
+      case e: Throwable if comm != 0 =>
+        ZkNative.depsAbort(ctx)
+        ZkNative.depsAllreduce(ctx, comm, 0L) // (its own status is moot: this rank rethrows)
+        throw e
+    }
+
   /** rank 0 stores the job's record (every rank holds the same one) */
   private[this] def store(d: Option[Dependencies]): Future[Option[Dependencies]] = d match {
     case Some(deps) if shard.forall(_.rank == 0) => aggregates.storeDependencies(deps).map(_ => d)
@@ -129,12 +144,14 @@ class GpuDependenciesJob(aggregates: Aggregates, device: Int = 0, strict: Boolea
     val names = new Dictionary
     services.foreach(names.id)
     val out = withCtx { (ctx, comm) =>
-      for (b <- batches) {
-        val c = new Columns(b.size)
-        b.foreach(put(c, _, names))
-        require(names.size <= numServices, s"more than $numServices service names")
-        require(shard.isEmpty || names.size == services.size, "a span names a service outside the job's list")
-        accumulate(ctx, c, b.size, 0)
+      guarded(ctx, comm) {
+        for (b <- batches) {
+          val c = new Columns(b.size)
+          b.foreach(put(c, _, names))
+          require(names.size <= numServices, s"more than $numServices service names")
+          require(shard.isEmpty || names.size == services.size, "a span names a service outside the job's list")
+          accumulate(ctx, c, b.size, 0)
+        }
       }
       finish(ctx, comm, names.name)
     }
@@ -160,17 +177,19 @@ class GpuDependenciesJob(aggregates: Aggregates, device: Int = 0, strict: Boolea
     def submit(vals: Seq[Array[Byte]]) = decoder.submit(new Callable[(Columns, Long)] { def call() = decode(vals) })
     try {
       val out = withCtx { (ctx, comm) =>
-        // batch k accumulates (PCIe staging + device work) while batch k+1 decodes on the other thread
-        var next = if (batches.hasNext) Some(submit(batches.next())) else None
-        while (next.isDefined) {
-          val (c, n) = next.get.get()
-          next = if (batches.hasNext) Some(submit(batches.next())) else None
-          // the reader cuts batches anywhere: the batch's last trace may continue in the next one
-          accumulate(ctx, c, n, ZkNative.BatchTraceClustered | ZkNative.BatchContinues)
+        guarded(ctx, comm) {
+          // batch k accumulates (PCIe staging + device work) while batch k+1 decodes on the other thread
+          var next = if (batches.hasNext) Some(submit(batches.next())) else None
+          while (next.isDefined) {
+            val (c, n) = next.get.get()
+            next = if (batches.hasNext) Some(submit(batches.next())) else None
+            // the reader cuts batches anywhere: the batch's last trace may continue in the next one
+            accumulate(ctx, c, n, ZkNative.BatchTraceClustered | ZkNative.BatchContinues)
+          }
+          val S = ZkNative.ingestNumServices(ing)
+          require(S <= numServices, s"$S service names > numServices = $numServices")
+          require(shard.isEmpty || S == services.size, "a stored span names a service outside the job's list")
         }
-        val S = ZkNative.ingestNumServices(ing)
-        require(S <= numServices, s"$S service names > numServices = $numServices")
-        require(shard.isEmpty || S == services.size, "a stored span names a service outside the job's list")
         finish(ctx, comm, i => ZkNative.ingestServiceName(ing, i))
       }
       store(out)

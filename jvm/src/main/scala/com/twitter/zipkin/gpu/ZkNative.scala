@@ -18,6 +18,7 @@ object ZkNative {
   final val ErrNoService = 3
   final val ErrNotClustered = 7
   final val ErrTraceTooLarge = 5
+  final val ErrRankFailed = 12
   // zk_deps_accumulate batch flags
   final val BatchDevicePtrs = 1
   final val BatchTraceClustered = 2
@@ -49,6 +50,9 @@ object ZkNative {
     * that runs its own int64 SUM all-reduce; depsAllreduce below does it with RCCL) */
   @native def depsPartial(ctx: Long, out: Array[Long]): Int
   @native def depsNoteMerged(ctx: Long, totalRecords: Long): Int
+  /** zk_deps_abort: this rank failed before the exchange; after the all-reduce every rank's finalize
+    * returns ErrRankFailed (so no rank is left waiting in the collective) */
+  @native def depsAbort(ctx: Long): Int
   /** zk_trace_shard: the rank that owns a traceId in a job of `world` ranks */
   @native def traceShard(traceId: Long, world: Int): Int
 

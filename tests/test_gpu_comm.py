@@ -76,3 +76,34 @@ def test_sketch_allreduce_at_world_one_is_identity(comm):
         for a, b in zip(before, after):
             assert np.array_equal(a, b)
         assert np.array_equal(tot, kv.totals())
+
+
+def test_aborted_rank_through_the_communicator(comm):
+    """zk_deps_abort + zk_deps_allreduce (the JVM job's failure path): finalize fails with
+    ZK_ERR_RANK_FAILED instead of a rank waiting in the collective; reset clears the mark."""
+    S = 57
+    cols = tracegen_host(33, 3_000, max_depth=6, num_services=S)
+    with DepsContext(S) as ctx:
+        ctx.accumulate(cols, clustered=True)
+        ctx.abort()
+        comm.allreduce_deps(ctx)
+        with pytest.raises(ZkError) as e:
+            ctx.finalize()
+        assert e.value.status == _abi.ZK_ERR_RANK_FAILED
+        ctx.reset()
+        ctx.accumulate(cols, clustered=True)
+        comm.allreduce_deps(ctx)
+        assert_parity(ctx.finalize(), ctx.stats(), oracle.aggregate(cols, S))
+
+
+def test_comm_create_error_text(gpu):
+    """A failed zk_comm_create reports RCCL's reason through zk_comm_last_error(NULL)."""
+    from zipkin_amd import _abi as A
+
+    L = A.lib()
+    import ctypes as C
+
+    h = C.c_void_p()
+    st = L.zk_comm_create((C.c_uint8 * 128)(), 128, 0, 1, 99, C.byref(h))  # no device 99
+    assert st == A.ZK_ERR_NO_DEVICE and not h.value
+    assert b"device" in L.zk_comm_last_error(None)

@@ -204,3 +204,40 @@ def test_random_streams_equal_the_oracle(gpu, seed):
     assert_parity(got, st, ref)
     assert st["not_clustered"] == 0
     assert st["records"] == n
+
+
+@pytest.mark.parametrize("only", [False, True])
+@pytest.mark.parametrize("device", [False, True])
+def test_continued_stream_feeds_a_bound_sketch_like_one_batch(gpu, only, device):
+    """The carry path with a realtime sketch bound (zk_rt_bind, ZK_RT_WITH_DEPS and ZK_RT_ONLY): the
+    held trace's merged spans reach the sketch through the spill kernel (K1 cannot append to the item
+    lists there), so a stream cut inside traces must leave the HLL registers, the histogram bins
+    and the drop counts exactly as one uncut batch does -- and, with the dependency join, the table
+    equal to the oracle."""
+    from zipkin_amd.realtime import RtSketch
+
+    S = 61
+    cols = tracegen_host(67, 15_000, max_depth=6, num_services=S)
+    rng = np.random.default_rng(67)
+    parts = cut(cols, rng.choice(np.arange(1, len(cols)), 4, replace=False))
+
+    def run(batches):
+        with DepsContext(S, strict=False) as ctx, RtSketch(S) as rt:
+            rt.bind(ctx, only=only)
+            for i, p in enumerate(batches):
+                b = DeviceColumns.from_host(p) if device else p
+                ctx.accumulate(b, clustered=True, verify=True, continues=i + 1 < len(batches))
+            got = None if only else ctx.finalize()
+            st = ctx.stats()
+            ctx.sync()
+            regs, hist = rt.read()
+            return got, st, regs.copy(), hist.copy(), rt.dropped()
+
+    one = run([cols])
+    many = run(parts)
+    assert np.array_equal(one[2], many[2]), "HLL registers differ"
+    assert np.array_equal(one[3], many[3]), "histogram bins differ"
+    assert one[4] == many[4]
+    assert one[2].any() and one[3].any()
+    if not only:
+        assert_parity(many[0], many[1], oracle.aggregate(cols, S))

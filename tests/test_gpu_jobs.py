@@ -109,7 +109,7 @@ def test_aggregate_job_on_device_row_batches(gpu):
         return v
 
     parts = [view(a, b) for a, b in zip(bounds[:-1], bounds[1:])]
-    job = ZipkinAggregateJob(names, clock=lambda: 10**15)
+    job = ZipkinAggregateJob(names, clock=lambda: 10**15, order="rows", verify=False)
     job.run(parts, S)  # warm
     times, acc_t, fin_t = [], [], []
     for _ in range(5):
@@ -137,3 +137,57 @@ def test_aggregate_job_on_device_row_batches(gpu):
     host = cols.to_host(n)
     assert _by_name(deps) == _oracle_by_name(host, S)
     job.close()
+
+
+def test_default_job_takes_batches_in_any_order(gpu):
+    """ZipkinAggregateJob's defaults (order="any", verify=True) accept what the reference's groupBy
+    traceId accepts (ZipkinAggregateJob.scala:21-22,28-33): each batch's fragments in any order. A
+    trace that recurs in a later batch fails the job instead of being joined in two halves."""
+    from zipkin_amd import ZkError, _abi
+
+    S = 61
+    cols = tracegen_host(41, 20_000, max_depth=6, num_services=S)
+    names = Dictionary([service_name(i) for i in range(S)])
+    # three batches of whole traces (by traceId), each shuffled
+    part = (cols.trace_id % np.uint64(3)).astype(np.int64)
+    rng = np.random.default_rng(41)
+    parts = []
+    for k in range(3):
+        idx = np.flatnonzero(part == k)
+        parts.append(cols.take(rng.permutation(idx)))
+    job = ZipkinAggregateJob(names, clock=lambda: 10**15)
+    deps = job.run(parts, S)
+    assert _by_name(deps) == _oracle_by_name(cols, S)
+    assert job.stats["not_clustered"] == 0
+    # a trace cut across two batches: detected, not mis-joined
+    idx = rng.permutation(len(cols))
+    halves = [cols.take(np.sort(idx[: len(cols) // 2])), cols.take(np.sort(idx[len(cols) // 2:]))]
+    with pytest.raises(ZkError) as e:
+        job.run(halves, S)
+    assert e.value.status == _abi.ZK_ERR_NOT_CLUSTERED
+    job.close()
+
+
+def test_run_device_waits_for_the_callers_stream(gpu):
+    """StoredSpanJob.run_device reads tensors the caller's current stream is still writing: the
+    job's stream is ordered after it (no torch.cuda.synchronize() by the caller)."""
+    import torch
+
+    S = 97
+    cols = tracegen_host(43, 50_000, target_records=400_000, max_depth=6, num_services=S)
+    buf, off, exp = encode(cols)
+    cuts = np.sort(np.random.default_rng(43).choice(np.arange(1, len(cols)), 3, replace=False)).tolist()
+    host = batches(buf, off, cuts)
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        # the caller's stream: busy first, then the non_blocking uploads from pinned memory
+        x = torch.randn(2048, 2048, device="cuda")
+        for _ in range(8):
+            x = (x @ x) * (1.0 / 2048)
+        dev = [(torch.from_numpy(b).pin_memory().cuda(non_blocking=True),
+                torch.from_numpy(o.view(np.int64)).pin_memory().cuda(non_blocking=True), len(o) - 1)
+               for b, o in host]
+        job = StoredSpanJob(clock=lambda: 10**15, max_services=S)
+        deps = job.run_device(dev)
+    assert job.rejected == 0 and job.stats["records"] == len(cols)
+    assert _by_name(deps) == _oracle_by_name(exp, S)

@@ -268,3 +268,49 @@ def test_global_trace_set_on_eight_device_shards_equals_the_oracle(gpu):
     finally:
         for sh in shards:
             sh.close()
+
+
+def test_aborted_rank_fails_every_rank_after_the_exchange(gpu):
+    """zk_deps_abort (a rank that failed on the host before the exchange, GpuDependenciesJob.guarded):
+    its exchange buffer is a zero table whose tail carries one abort mark, the SUM delivers the mark
+    to every rank, and every rank's finalize returns ZK_ERR_RANK_FAILED; the merged records count
+    excludes the mark. A reset clears it."""
+    import torch
+
+    S, world = 97, 4
+    cols = tracegen_host(44, 6000, max_depth=6, num_services=S)
+    parts = split(cols, world)
+    shards = [Shard(S) for _ in range(world)]
+    try:
+        views = []
+        for r, (sh, p) in enumerate(zip(shards, parts)):
+            sh.ctx.accumulate(p, clustered=True, verify=True)
+            if r == 2:
+                sh.ctx.abort()
+            ptr, nbytes = sh.ctx.partial()
+            views.append(device_view(ptr, nbytes, torch.int64))
+        for sh in shards:
+            sh.ctx.sync()
+        aborted = views[2].cpu().numpy()
+        assert not aborted[:-16].any() and aborted[-16] == 1 << 48 and not aborted[-15:].any()
+        total = torch.stack(views).sum(0)
+        for r, (sh, v) in enumerate(zip(shards, views)):
+            v.copy_(total)
+            torch.cuda.synchronize()
+            sh.ctx.note_merged(0)
+            with pytest.raises(ZkError) as e:
+                sh.ctx.finalize()
+            assert e.value.status == _abi.ZK_ERR_RANK_FAILED
+            st = sh.ctx.stats()
+            assert st["records"] == sum(len(p) for i, p in enumerate(parts) if i != 2)
+        # the next job on the same contexts is clean again
+        for sh in shards:
+            sh.ctx.reset()
+        outs, _ = run_sharded(cols, S, 2)
+        ref = oracle.aggregate(cols, S)
+        for got, st, status in outs:
+            assert status is None
+            assert_parity(got, st, ref)
+    finally:
+        for sh in shards:
+            sh.close()

@@ -35,7 +35,7 @@ def main():
         return v
 
     parts = [view(a, b) for a, b in zip(bounds[:-1], bounds[1:])]
-    job = ZipkinAggregateJob(names, clock=lambda: 10**15)
+    job = ZipkinAggregateJob(names, clock=lambda: 10**15, order="rows", verify=False)
     job.run(parts, S)
     acc, enq = [], []
     for _ in range(R):

@@ -26,6 +26,7 @@ ZK_ERR_NO_DEVICE = 8
 ZK_ERR_SERVICE_RANGE = 9
 ZK_ERR_UNSUPPORTED = 10
 ZK_ERR_INVALID_SPAN = 11
+ZK_ERR_RANK_FAILED = 12
 
 # record flags
 ZK_F_HAS_PARENT = 1 << 0
@@ -245,6 +246,7 @@ _SIGNATURES = [
     ("zk_deps_finalize", C.c_int, [_P, C.POINTER(zk_link_table)]),
     ("zk_deps_partial", C.c_int, [_P, C.POINTER(_P), C.POINTER(C.c_uint64)]),
     ("zk_deps_note_merged", C.c_int, [_P, C.c_uint64]),
+    ("zk_deps_abort", C.c_int, [_P]),
     ("zk_trace_shard", C.c_uint32, [C.c_uint64, C.c_uint32]),
     (
         "zk_tracegen_host",

@@ -450,17 +450,21 @@ class ZipkinAggregateJob:
     reference writes nothing (:43-45). With an `aggregates` sink the record is stored through
     storeDependencies (StorageRecordWriter.scala:13-17).
 
-    order="rows" (default): batches as a row-per-trace storage reader returns them
+    order="any" (default): each batch holds whole traces, its fragments in any order -- what the
+    reference's groupBy traceId accepts (:21-22, 28-33); the device clusters every batch. With
+    verify=True (the default) a trace that recurs in a later batch fails the job
+    (ZK_ERR_NOT_CLUSTERED) instead of being joined in two halves.
+    order="rows": batches as a row-per-trace storage reader returns them
     (StorageRecordReader.scala:49-54) -- every trace's fragments adjacent, a trace possibly cut at a
     batch edge -- accumulated with ZK_BATCH_TRACE_CLUSTERED | ZK_BATCH_CONTINUES, the path bench.py
-    measures. order="any": each batch holds whole traces in any order; the device clusters it.
-    verify adds ZK_BATCH_VERIFY_TRACES (the exact device check that no trace recurs).
+    measures. A caller opts in to it for input it knows to be row-ordered; verify=True then also
+    checks that promise exactly on the device (a split trace fails the job), verify=False trusts it.
 
     The device context is kept between runs (a scheduled job reuses its buffers); close() frees it.
     """
 
     def __init__(self, services: Dictionary, *, device: int = 0, strict: bool = True,
-                 aggregates: Optional[Aggregates] = None, clock=now_us, order: str = "rows", verify: bool = False):
+                 aggregates: Optional[Aggregates] = None, clock=now_us, order: str = "any", verify: bool = True):
         if order not in ("rows", "any"):
             raise ValueError("order is 'rows' or 'any'")
         self.services = services
@@ -651,6 +655,13 @@ class StoredSpanJob:
             with DepsContext(S, device=self.device, strict=self.strict, stream=stream.cuda_stream) as ctx:
                 cols = None
                 for buf, off, n in batches:
+                    # the caller's tensors may still be in flight on its current stream (a
+                    # non_blocking copy, a kernel that writes them; a lazy iterator makes each batch
+                    # just before it is read): the job's stream waits for everything queued there, and
+                    # the caller's allocator keeps the batch's memory until the job's stream is done
+                    stream.wait_stream(torch.cuda.current_stream(self.device))
+                    buf.record_stream(stream)
+                    off.record_stream(stream)
                     if cols is not None and cols.capacity < n:
                         cols = None
                     cols, rej = dec.decode_device(buf, off, n, snappy=self.snappy, strict=self.strict, out=cols)

@@ -19,9 +19,10 @@ ID_BYTES = 128  # ZK_COMM_ID_BYTES
 def unique_id() -> bytes:
     """ZK_COMM_ID_BYTES bytes for zk_comm_create (rank 0 makes it and ships it to the others)."""
     buf = (C.c_uint8 * ID_BYTES)()
-    st = _abi.lib().zk_comm_unique_id(buf, ID_BYTES)
+    L = _abi.lib()
+    st = L.zk_comm_unique_id(buf, ID_BYTES)
     if st != _abi.ZK_OK:
-        raise _abi.ZkError(st, _abi.status_str(st))
+        raise _abi.ZkError(st, L.zk_comm_last_error(None).decode() or _abi.status_str(st))
     return bytes(buf)
 
 
@@ -34,7 +35,7 @@ class Comm:
         h = C.c_void_p()
         st = self._L.zk_comm_create(src, ID_BYTES, rank, world, device, C.byref(h))
         if st != _abi.ZK_OK:
-            raise _abi.ZkError(st, _abi.status_str(st))
+            raise _abi.ZkError(st, self._L.zk_comm_last_error(None).decode() or _abi.status_str(st))
         self._h = h
         self.rank, self.world, self.device = rank, world, device
 

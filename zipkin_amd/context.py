@@ -211,6 +211,11 @@ class DepsContext:
         self._check(self._L.zk_deps_partial(self._h, C.byref(p), C.byref(b)))
         return int(p.value or 0), int(b.value)
 
+    def abort(self) -> None:
+        """zk_deps_abort: this rank failed on the host before the exchange; its next partial carries
+        an abort mark, so after the all-reduce finalize raises ZK_ERR_RANK_FAILED on every rank."""
+        self._check(self._L.zk_deps_abort(self._h))
+
     def note_merged(self, total_records: int) -> None:
         """The table now holds the merged job: finalize/stats use the merged counters."""
         self._check(self._L.zk_deps_note_merged(self._h, total_records))

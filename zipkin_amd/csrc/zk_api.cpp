@@ -63,12 +63,14 @@ struct zk_ctx {
     // host-pointer input staging
     void* stage = nullptr;
     uint64_t stage_cap = 0;
+    hipEvent_t ev_stage = nullptr;  // after the staging copies: the call returns once they read the caller's memory
     // finalize staging for host outputs
     void* fin_stage = nullptr;
     uint64_t records_since_reset = 0;
     bool merged = false;                  // the table holds the all-reduced job (zk_deps_note_merged)
     bool continued = false;               // a batch was accumulated into a merged table since the reset
     uint64_t* xchg = nullptr;             // packed exchange form of the table (zk_deps_partial)
+    bool aborted = false;                 // zk_deps_abort: the next exchange carries an abort mark
     bool folded = false;                  // zk_deps_partial folded this ctx's counters into the table tail
                                           // since the last reset / accumulate (note_merged requires it)
     // clustering pass for unclustered batches (zk_cluster.hip)
@@ -206,7 +208,11 @@ zk_status ensure_spill(zk_ctx* c, uint64_t n) {
     return ZK_OK;
 }
 
-zk_status stats_sum(zk_ctx* c, uint64_t out[ST_N]) {
+// zk_deps_abort's mark in the exchange tail's records word (zkagg.h)
+constexpr int kAbortShift = 48;
+constexpr uint64_t kAbortUnit = 1ull << kAbortShift;
+
+zk_status stats_sum(zk_ctx* c, uint64_t out[ST_N], uint64_t* aborted_ranks = nullptr) {
     // The counters end every finalize (the job's status), so their round trip is on the step's
     // critical path: a pinned destination and a polled event instead of a blocking stream sync
     // (whose wake-up leaves the GPU idle for tens of microseconds before the next step's work).
@@ -228,6 +234,8 @@ zk_status stats_sum(zk_ctx* c, uint64_t out[ST_N]) {
     for (int s = 0; s < ST_N; ++s) out[s] = 0;
     for (int sh = 0; sh < (c->merged ? 1 : kStatShards); ++sh)
         for (int s = 0; s < ST_N; ++s) out[s] += h[(size_t)sh * ST_N + s];
+    if (aborted_ranks) *aborted_ranks = out[ST_RECORDS] >> kAbortShift;
+    out[ST_RECORDS] &= kAbortUnit - 1;  // the abort marks of zk_deps_abort ride in the high bits
     return ZK_OK;
 }
 
@@ -360,6 +368,7 @@ const char* zk_status_str(zk_status s) {
         case ZK_ERR_SERVICE_RANGE: return "service_id >= num_services";
         case ZK_ERR_UNSUPPORTED: return "unsupported";
         case ZK_ERR_INVALID_SPAN: return "invalid or undecodable span";
+        case ZK_ERR_RANK_FAILED: return "another rank of the job failed (zk_deps_abort)";
     }
     return "unknown status";
 }
@@ -431,6 +440,7 @@ zk_status zk_ctx_destroy(zk_ctx* c) {
     hipFree(c->stats);
     if (c->h_stats) hipHostFree(c->h_stats);
     if (c->ev_stats) hipEventDestroy(c->ev_stats);
+    if (c->ev_stage) hipEventDestroy(c->ev_stage);
     hipFree(c->spill_count);
     hipFree(c->spill_list);
     hipFree(c->spill_scratch);
@@ -504,6 +514,7 @@ zk_status zk_deps_reset(zk_ctx* c) {
     c->merged = false;
     c->continued = false;
     c->folded = false;
+    c->aborted = false;
     // a held-back trace belongs to the job being reset
     c->maybe_carry = false;
     c->any_verify = false;
@@ -572,6 +583,13 @@ zk_status zk_deps_accumulate(zk_ctx* c, const zk_span_cols* cols, uint32_t flags
         ZK_HIP(c, hipMemcpyAsync(lts, cols->last_ts, n * 8, hipMemcpyHostToDevice, c->stream));
         ZK_HIP(c, hipMemcpyAsync(svc, cols->service_id, n * 4, hipMemcpyHostToDevice, c->stream));
         ZK_HIP(c, hipMemcpyAsync(flg, cols->flags, n * 4, hipMemcpyHostToDevice, c->stream));
+        // host columns are borrowed for the duration of the call only (zkagg.h): from page-locked
+        // memory the copies above are DMA reads that run after this call would return, so the call
+        // waits until they have consumed the caller's buffers (queued behind the stream's earlier
+        // work; the PCIe path, never the bench value)
+        if (!c->ev_stage) ZK_HIP(c, hipEventCreateWithFlags(&c->ev_stage, hipEventDisableTiming));
+        ZK_HIP(c, hipEventRecord(c->ev_stage, c->stream));
+        ZK_HIP(c, hipEventSynchronize(c->ev_stage));
         d = SpanColsDev{tid, sid, pid, fts, lts, svc, flg, n};
     } else if ((flags & ZK_BATCH_TRACE_CLUSTERED) &&
                (!aligned(d.trace_id, 16) || !aligned(d.span_id, 16) || !aligned(d.parent_id, 16) ||
@@ -976,9 +994,12 @@ zk_status zk_deps_finalize(zk_ctx* c, const zk_link_table* out) {
         ZK_HIP(c, hipMemcpyAsync(out->m4, dev.m4, cells * 8, hipMemcpyDeviceToHost, c->stream));
         ZK_HIP(c, hipMemcpyAsync(out->present, dev.present, cells, hipMemcpyDeviceToHost, c->stream));
     }
-    uint64_t s[ST_N];
-    zk_status st = stats_sum(c, s);
+    uint64_t s[ST_N], aborted = 0;
+    zk_status st = stats_sum(c, s, &aborted);
     if (st != ZK_OK) return st;
+    if (aborted)
+        return fail(c, ZK_ERR_RANK_FAILED,
+                    std::to_string(aborted) + " rank(s) of the job failed before the exchange (zk_deps_abort)");
     if (s[ST_TOO_LARGE]) return fail(c, ZK_ERR_TRACE_TOO_LARGE, "trace longer than max_trace_records skipped");
     if (s[ST_SPILL_OVERFLOW])
         return fail(c, ZK_ERR_CAPACITY,
@@ -1049,6 +1070,15 @@ zk_status zk_deps_partial(zk_ctx* c, void** dev_ptr, uint64_t* bytes) {
         return fail(c, ZK_ERR_CAPACITY, "no device memory for the exchange buffer");
     }
     ZK_HIP(c, launch_table_pack(c->table, c->S, c->xchg, c->stream));  // 56-bit limbs + the counter tail
+    if (c->aborted) {
+        // a failed rank contributes nothing but its abort mark (the exchange still happens, so the
+        // other ranks are not left waiting in the collective)
+        static const uint64_t mark = kAbortUnit;
+        ZK_HIP(c, hipMemsetAsync(c->xchg, 0, exchange_bytes(c->S), c->stream));
+        ZK_HIP(c, hipMemcpyAsync((uint8_t*)c->xchg + exchange_bytes(c->S) - kTableTailBytes + ST_RECORDS * 8, &mark,
+                                 8, hipMemcpyHostToDevice, c->stream));
+        ZK_HIP(c, hipStreamSynchronize(c->stream));  // (`mark` is pageable: nothing reads it later)
+    }
     c->folded = true;
     *dev_ptr = c->xchg;
     *bytes = exchange_bytes(c->S);
@@ -1069,12 +1099,18 @@ zk_status zk_deps_note_merged(zk_ctx* c, uint64_t total_records) {
         ZK_HIP(c, hipMemcpyAsync(&rec, c->table + (uint64_t)c->S * c->S * kLimbs + ST_RECORDS, 8,
                                  hipMemcpyDeviceToHost, c->stream));
         ZK_HIP(c, hipStreamSynchronize(c->stream));
-        total_records = rec;
+        total_records = rec & (kAbortUnit - 1);  // (abort marks excluded)
     }
     if (total_records > kMaxRecordsSinceReset)
         return fail(c, ZK_ERR_CAPACITY, "merged table exceeds 2^32-1 records");
     c->records_since_reset = total_records;
     c->merged = true;
+    return ZK_OK;
+}
+
+zk_status zk_deps_abort(zk_ctx* c) {
+    if (!c) return ZK_ERR_INVALID_ARG;
+    c->aborted = true;
     return ZK_OK;
 }
 

@@ -67,6 +67,10 @@ std::string nccl_msg(const Rccl* r, const char* what, ncclResult_t e) {
     return std::string(what) + ": " + r->error_string(e);
 }
 
+// why the last zk_comm_unique_id / zk_comm_create on this thread failed (no handle to hold it):
+// zk_comm_last_error(NULL) returns it
+thread_local std::string t_create_err;
+
 }  // namespace
 
 struct zk_comm {
@@ -96,6 +100,7 @@ zk_status comm_allreduce(zk_comm* c, void* buf, uint64_t count, CommType t, Comm
     const ncclResult_t e = r->all_reduce(buf, buf, (size_t)count, dt, op == kCommSum ? ncclSum : ncclMax, c->comm, s);
     if (e != ncclSuccess) {
         *err = nccl_msg(r, "ncclAllReduce", e);
+        c->err = *err;  // (the handle's zk_comm_last_error as well)
         return ZK_ERR_HIP;
     }
     return ZK_OK;
@@ -116,6 +121,7 @@ zk_status comm_allgather(zk_comm* c, const void* send, void* recv, uint64_t byte
     const ncclResult_t e = r->all_gather(send, recv, (size_t)bytes, ncclUint8, c->comm, s);
     if (e != ncclSuccess) {
         *err = nccl_msg(r, "ncclAllGather", e);
+        c->err = *err;
         return ZK_ERR_HIP;
     }
     return ZK_OK;
@@ -130,9 +136,16 @@ zk_status zk_comm_unique_id(uint8_t* id, uint64_t bytes) {
     if (!id || bytes < ZK_COMM_ID_BYTES) return ZK_ERR_INVALID_ARG;
     static_assert(sizeof(ncclUniqueId) == ZK_COMM_ID_BYTES, "RCCL unique id size");
     const Rccl* r = rccl();
-    if (!r) return ZK_ERR_UNSUPPORTED;
+    if (!r) {
+        t_create_err = rccl_state().err;
+        return ZK_ERR_UNSUPPORTED;
+    }
     ncclUniqueId u;
-    if (r->get_unique_id(&u) != ncclSuccess) return ZK_ERR_HIP;
+    const ncclResult_t e = r->get_unique_id(&u);
+    if (e != ncclSuccess) {
+        t_create_err = nccl_msg(r, "ncclGetUniqueId", e);
+        return ZK_ERR_HIP;
+    }
     memcpy(id, &u, ZK_COMM_ID_BYTES);
     return ZK_OK;
     ZK_GUARD_END
@@ -145,17 +158,29 @@ zk_status zk_comm_create(const uint8_t* id, uint64_t bytes, uint32_t rank, uint3
     *out = nullptr;
     if (!id || bytes < ZK_COMM_ID_BYTES || world == 0 || rank >= world || world > 256) return ZK_ERR_INVALID_ARG;
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0 || device < 0 || device >= ndev) return ZK_ERR_NO_DEVICE;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0 || device < 0 || device >= ndev) {
+        t_create_err = "no HIP device " + std::to_string(device);
+        return ZK_ERR_NO_DEVICE;
+    }
     const Rccl* r = rccl();
-    if (!r) return ZK_ERR_UNSUPPORTED;
-    if (hipSetDevice(device) != hipSuccess) return ZK_ERR_HIP;
+    if (!r) {
+        t_create_err = rccl_state().err;
+        return ZK_ERR_UNSUPPORTED;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        t_create_err = "hipSetDevice failed";
+        return ZK_ERR_HIP;
+    }
     ncclUniqueId u;
     memcpy(&u, id, ZK_COMM_ID_BYTES);
     zk_comm* c = new zk_comm();
     c->rank = rank;
     c->world = world;
     c->device = device;
-    if (r->comm_init_rank(&c->comm, (int)world, u, (int)rank) != ncclSuccess) {
+    const ncclResult_t e = r->comm_init_rank(&c->comm, (int)world, u, (int)rank);
+    if (e != ncclSuccess) {
+        t_create_err = nccl_msg(r, "ncclCommInitRank", e) + " (rank " + std::to_string(rank) + " of " +
+                       std::to_string(world) + ")";
         delete c;
         return ZK_ERR_HIP;
     }
@@ -178,7 +203,7 @@ zk_status zk_comm_destroy(zk_comm* c) {
 }
 
 const char* zk_comm_last_error(const zk_comm* c) {
-    if (!c) return rccl() ? "null communicator" : rccl_state().err.c_str();
+    if (!c) return !t_create_err.empty() ? t_create_err.c_str() : rccl() ? "null communicator" : rccl_state().err.c_str();
     return c->err.c_str();
 }
 

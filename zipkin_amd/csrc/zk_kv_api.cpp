@@ -227,6 +227,9 @@ zk_status zk_kv_accumulate(zk_kv* k, const uint32_t* svc, const uint64_t* keys, 
         uint32_t* ds = (uint32_t*)((uint8_t*)k->stage + ((n * 8 + 255) & ~255ull));
         KV_HIP(k, hipMemcpyAsync(dk, keys, n * 8, hipMemcpyHostToDevice, k->stream));
         KV_HIP(k, hipMemcpyAsync(ds, svc, n * 4, hipMemcpyHostToDevice, k->stream));
+        // host inputs are borrowed for the call only (zkagg.h): wait until the copies (DMA reads of
+        // page-locked memory run after an async call returns) have consumed them
+        KV_HIP(k, hipStreamSynchronize(k->stream));
         keys = dk;
         svc = ds;
     }

@@ -396,6 +396,8 @@ zk_status zk_rt_accumulate_merged(zk_rt* r, const uint32_t* service_id, const ui
         RT_HIP(r, hipMemcpyAsync(ds, service_id, n * 4, hipMemcpyHostToDevice, r->stream));
         RT_HIP(r, hipMemcpyAsync(dt, trace_id, n * 8, hipMemcpyHostToDevice, r->stream));
         RT_HIP(r, hipMemcpyAsync(dd, duration, n * 8, hipMemcpyHostToDevice, r->stream));
+        // host inputs are borrowed for the call only (zkagg.h): wait until the copies have read them
+        RT_HIP(r, hipStreamSynchronize(r->stream));
         service_id = ds;
         trace_id = dt;
         duration = dd;
