@@ -208,12 +208,18 @@ __device__ __forceinline__ bool slot_valid(uint32_t w) { return ((w >> kSlotB) &
 // which serialises the column loads and defeats the prefetch. Index i < lim reads the aligned pair
 // at i (columns are 16-B / 8-B aligned, so the pair never crosses a page even when i + 1 == lim);
 // i >= lim reads pair 0.
-// diagnostic builds only (results wrong): ZK_K1_DIAG_HOT redirects every column load into the first
-// 2^16 records, which stay in L2 -- K1's time with HBM taken out
+// Diagnostic builds only (results wrong; profiles/r06/k1_sensitivity_ab.txt): ZK_K1_DIAG_HOT
+// redirects every column load into the first 2^16 records (L2-resident: K1 with HBM reads taken
+// out), ZK_K1_DIAG_NOFIRST drops the first_ts column (8 B / record fewer read), ZK_K1_DIAG_NOSTORE
+// drops the link stores, ZK_K1_DIAG_TRASHONLY sends both stores of every lane to the trash slot.
+// Each reports no links (K2/K3 then index nothing).
 #ifdef ZK_K1_DIAG_HOT
 #define ZK_HOTIDX(i) ((i) & 0xFFFFull)
 #else
 #define ZK_HOTIDX(i) (i)
+#endif
+#if defined(ZK_K1_DIAG_HOT) || defined(ZK_K1_DIAG_NOFIRST) || defined(ZK_K1_DIAG_NOSTORE) || defined(ZK_K1_DIAG_TRASHONLY)
+#define ZK_K1_DIAG 1
 #endif
 __device__ __forceinline__ void ld2_u64(const uint64_t* __restrict__ p, uint64_t i, uint64_t lim, uint64_t v[2]) {
     const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(p + ZK_HOTIDX(i < lim ? i : 0));
@@ -312,13 +318,7 @@ __device__ __forceinline__ void window_ballots(const Window& w, uint64_t ws, int
 __device__ __forceinline__ void load_tid(const JoinArgs& a, uint64_t n, uint64_t ws, Window& w) {
     const uint64_t i = ws + 2 * threadIdx.x;
     ld2_u64(a.c.trace_id, i, n, w.tid);
-#ifdef ZK_K1_PREV_SCALAR
-    // only lane 0's `prev` is read (window_ballots): one wave-uniform load instead of 64 lanes'
-    const uint64_t i0 = ws + 128u * (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    w.prev = a.c.trace_id[ZK_HOTIDX((i0 > 0 && i0 - 1 < n) ? i0 - 1 : 0)];
-#else
     w.prev = a.c.trace_id[ZK_HOTIDX((i > 0 && i - 1 < n) ? i - 1 : 0)];
-#endif
 }
 __device__ __forceinline__ void load_early(const JoinArgs& a, uint64_t n, uint64_t ws, Window& w) {
     const uint64_t i = ws + 2 * threadIdx.x;
@@ -328,7 +328,7 @@ __device__ __forceinline__ void load_early(const JoinArgs& a, uint64_t n, uint64
 #endif
     ld2_u64((const uint64_t*)a.c.last_ts, i, n, w.last);
 #ifdef ZK_K1_DIAG_NOFIRST
-    w.first[0] = w.last[0] - 5;  // diagnostic: one column (8 B / record) fewer, same links
+    w.first[0] = w.last[0] - 5;
     w.first[1] = w.last[1] - 5;
 #endif
     ld2_u32(a.c.service_id, i, n, w.svc);
@@ -414,16 +414,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     for (uint32_t x = tid; x < a.nb; x += WG) s_hist[x] = a.append ? a.hist[(uint64_t)x * a.grid + blockIdx.x] : 0u;
     constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
     uint32_t r_clear[2] = {kNoSlot, kNoSlot};  // hash slots this thread's leaders of the last window hold
-#ifdef ZK_K1_TOUCH
-    uint32_t touch_prev = 0, touch_acc = 0;  // experiment: L2/MALL touch of the window after next
-#endif
-#ifdef ZK_K1_DIAG_WRFULL
-    uint32_t nwin_diag = 0;
-#endif
-#ifdef ZK_K1_STORE_EVERY2
-    uint64_t held_link[2] = {~0ull, ~0ull}, held_at[2] = {0, 0};
-    uint32_t held_n = 0;  // (uniform: every wave's windows alternate together)
-#endif
 
     Window cur, nxt;
     constexpr bool JOIN = (MODE & kModeJoin) != 0, EMIT = (MODE & kModeEmit) != 0;
@@ -439,24 +429,11 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     bool seek_start = false;  // seek is known to be a trace start (uniform)
     load_tid(a, n, ws, cur);
     load_early(a, n, ws, cur);
-#ifdef ZK_K1_LATE_BEFORE_STORES
-    load_late<JOIN>(a, n, ws, cur);
-    if constexpr (JOIN) {
-        // two stores to the trash slot after the first window's loads, as every later window has its
-        // two link stores after the next window's loads: the compiler's wait counting (vmcnt, one
-        // in-order queue of loads and stores) then sees the same order on the loop's entry and back
-        // edges, and waits for the column loads only, never for the link stores behind them
-        out[trash] = ~0ull;
-        out[trash] = ~0ull;
-    }
-#endif
     // the first window's ballots; later windows' are taken at the end of the window before (below)
     window_ballots(cur, ws, (int)((n - ws) < (uint64_t)TILE ? (n - ws) : (uint64_t)TILE), &m_ev, &m_od);
     if (lane == 0) *reinterpret_cast<ulonglong2*>(&s_mask[2 * wave]) = make_ulonglong2(m_ev, m_od);
     for (;;) {
-#ifndef ZK_K1_LATE_BEFORE_STORES
         load_late<JOIN>(a, n, ws, cur);
-#endif
         const int wn = (int)((n - ws) < (uint64_t)TILE ? (n - ws) : (uint64_t)TILE);
         // ---- 1. trace boundaries of the window (ballots taken at the end of the window before) --
         ZK_PHASE_SYNC(0);
@@ -545,27 +522,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         }
         if (!done && next_seek >= R1) done = true;
         const uint64_t next_ws = next_seek & ~1ull;
-#ifndef ZK_K1_TID_AFTER_STAGE
         load_tid(a, n, done ? ws : next_ws, nxt);  // in flight during the LDS phases below (unconditional: see ld2)
-#endif
-#ifdef ZK_K1_TOUCH
-        // experiment: one load instruction per wave touches every 128-B line of this wave's slice of
-        // the window after next in all seven columns (lane l: column l / 8, line l % 8), so those lines
-        // are in L2 / MALL when that window's real loads come; the value is consumed a window later
-        uint32_t touch_now;
-        {
-            const int col = lane >> 3, line = lane & 7;
-            const uint64_t r0 = next_ws + (uint64_t)(ZK_K1_TOUCH) * TILE + 128u * (uint64_t)wave;
-            const bool wide = col < 5 || col == 7;
-            uint64_t rec = r0 + (uint64_t)(wide ? line * 16 : (line & 3) * 32);
-            rec = rec < n ? rec : 0;
-            const uint32_t* p32 = (const uint32_t*)(col == 0 || col == 7 ? (const void*)a.c.trace_id
-                                  : col == 1 ? (const void*)a.c.span_id : col == 2 ? (const void*)a.c.parent_id
-                                  : col == 3 ? (const void*)a.c.first_ts : col == 4 ? (const void*)a.c.last_ts
-                                  : col == 5 ? (const void*)a.c.service_id : (const void*)a.c.flags);
-            touch_now = p32[wide ? 2 * rec : rec];
-        }
-#endif
         ZK_STAMP(1);
         nrec += (uint64_t)(m - start);
         uint64_t n_ev = 0, n_od = 0;  // the next window's ballots
@@ -608,11 +565,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             *reinterpret_cast<ulonglong2*>(&s_pid[j0]) = make_ulonglong2(v_pid[0], v_pid[1]);
             *reinterpret_cast<uint2*>(&s_svck[j0]) = make_uint2(r_svck[0], r_svck[1]);
         }
-#ifdef ZK_K1_TID_AFTER_STAGE
-        // the next window's traceIds issued after the staging waited for this window's columns, so that
-        // wait need not cover the previous window's link stores either (they are the youngest then)
-        load_tid(a, n, done ? ws : next_ws, nxt);
-#endif
         ZK_PHASE_SYNC(2);  // (the hash table is empty here: cleared once, then by its leaders)
 
         // ---- 4. groupBy((id, traceId)): the first fragment to claim a slot leads --------------
@@ -771,62 +723,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             ++nl;
         }
         ZK_STAMP(5);
-#ifdef ZK_K1_LATE_BEFORE_STORES
-        // parentId and flags of the next window, issued BEFORE this window's link stores: the next
-        // window's staging then waits only for loads older than the stores (vmcnt counts loads and
-        // stores in one in-order queue, and a store's completion under load takes microseconds)
-        load_late<JOIN>(a, n, done ? ws : next_ws, cur);
-#endif
-#if defined(ZK_K1_PAD_VALU) || defined(ZK_K1_PAD_SALU)
-        {  // diagnostic sensitivity builds only: N extra independent VALU / SALU instructions per window
-            uint32_t pv0 = (uint32_t)tid, pv1 = pv0 + 1u, pv2 = pv0 + 2u, pv3 = pv0 + 3u;
-#ifdef ZK_K1_PAD_VALU
-#pragma unroll
-            for (int q = 0; q < ZK_K1_PAD_VALU / 4; ++q)
-                asm volatile("v_add_u32 %0, 1, %0\n\tv_add_u32 %1, 1, %1\n\tv_add_u32 %2, 1, %2\n\tv_add_u32 %3, 1, %3"
-                             : "+v"(pv0), "+v"(pv1), "+v"(pv2), "+v"(pv3));
-#endif
-#ifdef ZK_K1_PAD_SALU
-            uint32_t ps0 = (uint32_t)blockIdx.x, ps1 = ps0 + 1u;
-#pragma unroll
-            for (int q = 0; q < ZK_K1_PAD_SALU / 2; ++q)
-                asm volatile("s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1" : "+s"(ps0), "+s"(ps1));
-            pv0 += ps0 ^ ps1;
-#endif
-            if ((pv0 ^ pv1 ^ pv2 ^ pv3) == 0xFFFFFFFFu) s_stat[0] = 0;  // keep them live (never true in practice)
-        }
-#endif
-#ifdef ZK_K1_PAD_LDS_RT
-        {  // diagnostic: N extra DEPENDENT LDS round trips per window (each read's address from the last)
-            uint32_t addr = (uint32_t)(uintptr_t)&s_svck[tid & (TILE - 1)];
-            uint32_t v = 0;
-#pragma unroll
-            for (int q = 0; q < ZK_K1_PAD_LDS_RT; ++q) {
-                asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
-                addr += (v & 0u);  // (a dependence the hardware must wait for; v & 0 is not folded in asm)
-            }
-            if (v == 0x12345678u) s_stat[0] = 0;
-        }
-#endif
-#ifdef ZK_K1_PAD_LDS_TP
-        {  // diagnostic: N extra independent conflict-free LDS reads per window, then one wait
-            const uint32_t addr = (uint32_t)(uintptr_t)&s_sid[(2 * tid) & (TILE - 1)];
-            uint64_t acc = 0, v;
-#pragma unroll
-            for (int q = 0; q < ZK_K1_PAD_LDS_TP; ++q) {
-                asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(addr) : "memory");
-                acc ^= v;
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (acc == 0x123456789ull) s_stat[0] = 0;
-        }
-#endif
-#ifdef ZK_K1_PAD_VMWAIT
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // diagnostic: drain every in-flight load once per window
-#endif
-#ifdef ZK_K1_PAD_BAR
-        __syncthreads();  // diagnostic: one more workgroup barrier per window
-#endif
         // ---- 7. append the window's links (and sketch items) to this workgroup's lists ----------
         // no barrier: each wave claims its slice of the workgroup's lists with ONE LDS atomic on a
         // cursor (links in the low 32 bits, sketch items in the high 32); lane offsets from ballots
@@ -848,10 +744,6 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         // for loads and stores, and the first use of a prefetched value waits for everything older
         // in the compiler's model). s_mask is free: every wave read it in phase 2, before the
         // phase-3 barrier; the next window's phase-1 barrier publishes the new masks.
-#ifdef ZK_K1_TOUCH
-        touch_acc ^= touch_prev;  // the touch of the window before (long landed)
-        touch_prev = touch_now;
-#endif
         if (!done) {
             const uint64_t nws = next_ws;
             window_ballots(nxt, nws, (int)((n - nws) < (uint64_t)TILE ? (n - nws) : (uint64_t)TILE), &n_ev, &n_od);
@@ -861,63 +753,10 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             // exactly two stores per thread on every path (absent links go to the list's trash
             // slot), so the loop-end wait for the prefetched window can count them: vmcnt(2)
             uint32_t pos = lbase;
-#if defined(ZK_K1_NOTRASH)
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {  // experiment: absent links not stored at all (masked lanes)
-                if (r_link[e] != ~0ull) out[pos++] = r_link[e];
-            }
-#elif defined(ZK_K1_DIAG_WRFULL)
-            {  // diagnostic (results wrong): every wave writes its 128 link slots, present or not, as one
-               // wave-private 1-KB block, two contiguous 512-B stores (2x the bytes, all full lines)
-                const uint64_t span = (a.per_wg / TILE) * TILE;
-                const uint64_t at = span ? ((uint64_t)nwin_diag * TILE + 128u * (uint64_t)wave) % span : 0;
-                out[at + lane] = r_link[0];  // two fully contiguous 512-B stores per wave (inside the list)
-                out[at + 64 + lane] = r_link[1];
-                ++nwin_diag;
-                (void)pos;
-            }
-#elif defined(ZK_K1_DIAG_HALFSTORE)
-            {  // diagnostic (results wrong): only the first record's link of each thread is stored
-                const bool v = r_link[0] != ~0ull;
-                out[v ? (uint64_t)pos : trash] = r_link[0];
-            }
-#elif defined(ZK_K1_NTSTORE)
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {  // experiment: non-temporal link stores
-                const bool v = r_link[e] != ~0ull;
-                __builtin_nontemporal_store(r_link[e], &out[v ? (uint64_t)pos : trash]);
-                pos += v ? 1u : 0u;
-            }
-#elif defined(ZK_K1_DIAG_TRASHONLY)
-            // diagnostic (results wrong): the same two store instructions, every lane to the trash slot
+#if defined(ZK_K1_DIAG_TRASHONLY)
             out[trash] = r_link[0];
             out[trash] = r_link[1];
-            (void)pos;
-#elif defined(ZK_K1_STORE_EVERY2)
-            {  // experiment: a window's links are held in registers and stored with the next window's,
-               // so a wave writes every other window (twice the bytes per write episode)
-                uint64_t at[2];
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const bool v = r_link[e] != ~0ull;
-                    at[e] = v ? (uint64_t)pos : trash;
-                    pos += v ? 1u : 0u;
-                }
-                if (held_n) {
-                    out[held_at[0]] = held_link[0];
-                    out[held_at[1]] = held_link[1];
-                    out[at[0]] = r_link[0];
-                    out[at[1]] = r_link[1];
-                    held_n = 0;
-                } else {
-                    held_at[0] = at[0];
-                    held_at[1] = at[1];
-                    held_link[0] = r_link[0];
-                    held_link[1] = r_link[1];
-                    held_n = 1;
-                }
-            }
-#elif !defined(ZK_K1_DIAG_NOSTORE)  // diagnostic: no link stores
+#elif !defined(ZK_K1_DIAG_NOSTORE)
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const bool v = r_link[e] != ~0ull;
@@ -964,23 +803,9 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         ZK_STAMP(7);
     }
     ZK_STAMP_FLUSH();
-#ifdef ZK_K1_STORE_EVERY2
-    if constexpr (JOIN) {
-        if (held_n) {
-            out[held_at[0]] = held_link[0];
-            out[held_at[1]] = held_link[1];
-        }
-    }
-#endif
-#ifdef ZK_K1_TOUCH
-    if ((touch_acc ^ touch_prev) == 0x9E3779B9u) s_stat[0] = 0;  // keep the touches live
-#endif
     __syncthreads();  // every wave's last append is in the cursor
-#if defined(ZK_K1_DIAG_WRFULL) || defined(ZK_K1_DIAG_HALFSTORE) || defined(ZK_K1_DIAG_NOSTORE) || defined(ZK_K1_DIAG_HOT) || \
-    defined(ZK_K1_DIAG_TRASHONLY)
-    // diagnostic builds write lists K2/K3 must not read (values not links, or stale slots): report
-    // no links and an empty histogram, so the reduce has nothing to index
-    if (tid == 0) s_cursor = 0ull;
+#ifdef ZK_K1_DIAG
+    if (tid == 0) s_cursor = 0ull;  // the lists hold no links K2/K3 may read
     for (uint32_t x = tid; x < a.nb; x += WG) s_hist[x] = 0u;
     __syncthreads();
 #endif
