@@ -166,6 +166,46 @@ zk_status   zk_rt_read(zk_rt* rt, uint8_t* registers, uint32_t* histogram);
 /* items dropped since reset: service_id >= S, or duration outside [0, 2^40) us */
 zk_status   zk_rt_dropped(zk_rt* rt, uint64_t* service_range, uint64_t* duration_range);
 
+/* ------------------------------------------------------------------------------------------
+ * Realtime link store: the state behind RealtimeAggregates (zipkin-common/.../storage/
+ * RealtimeAggregates.scala:26-38; zipkinQuery.thrift:234-251 -- "given a time stamp, server
+ * service name and rpc name, fetch all of the client services calling in paired with the lists of
+ * every span duration / every trace id from the server to client"). The reference declares the
+ * trait but only implements NullRealtimeAggregates.
+ *
+ * Those lists are the dependency job's join rows before its group.sum: one (parent = client
+ * service, child = server service, child duration, traceId) row per joined child span
+ * (ZipkinAggregateJob.scala:25-37). Bound to a dependency ctx, every later zk_deps_accumulate writes
+ * one item per link it emits (K1 and the spill kernel, beside the link, in the same pass) and
+ * appends them to the store's window in HBM (16 B per link; grown as it fills: one link per record at
+ * most). zk_rl_server_links answers one server service: every row whose child is `server`, as
+ * parent ids, durations (us) and traceIds, ordered by (parent, duration, traceId) -- one filter pass
+ * over the window, then a host sort of that server's rows. zk_rl_reset starts a new window (the
+ * host keeps one store per time window). The ctx and the store must agree on num_services; a store
+ * cannot share a ctx with a ZK_RT_WITH_DEPS sketch (ZK_ERR_UNSUPPORTED), and unclustered batches take
+ * the streaming join (not the group join) while a store is bound. The record has no span name, so the
+ * trait's rpcName is not a key here (GpuRealtimeAggregates).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct zk_rl_config {
+    uint32_t num_services;  /* S <= 4096, the ctx's */
+    int32_t  device;
+    void*    stream;        /* hipStream_t or NULL for a private stream (the bound ctx's while bound) */
+    uint32_t reserved[8];
+} zk_rl_config;
+
+typedef struct zk_rl zk_rl;
+
+zk_status   zk_rl_create(const zk_rl_config* cfg, zk_rl** out);
+zk_status   zk_rl_destroy(zk_rl* rl);
+const char* zk_rl_last_error(const zk_rl* rl);
+zk_status   zk_rl_reset(zk_rl* rl);
+zk_status   zk_rl_bind(zk_ctx* ctx, zk_rl* rl);   /* rl = NULL unbinds */
+/* links in the window since reset (syncs); dropped: items past the window's capacity (0) */
+zk_status   zk_rl_count(zk_rl* rl, uint64_t* items, uint64_t* dropped);
+/* every link whose child service is `server` (host arrays of cap entries; all NULL: *n = the count) */
+zk_status   zk_rl_server_links(zk_rl* rl, uint32_t server, uint32_t* parent, int64_t* duration,
+                               uint64_t* trace_id, uint64_t cap, uint64_t* n);
+
 #ifdef __cplusplus
 }
 #endif

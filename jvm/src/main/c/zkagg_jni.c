@@ -16,6 +16,7 @@
 #include "zkagg.h"
 #include "zkcomm.h"
 #include "zkingest.h"
+#include "zksketch.h"
 #include "zkstore.h"
 
 #define FN(name) Java_com_twitter_zipkin_gpu_ZkNative_00024_##name
@@ -23,6 +24,7 @@
 #define ING(h) ((zk_ingest*)(intptr_t)(h))
 #define STORE(h) ((zk_store*)(intptr_t)(h))
 #define COMM(h) ((zk_comm*)(intptr_t)(h))
+#define RL(h) ((zk_rl*)(intptr_t)(h))
 #define BUF(b) ((*env)->GetDirectBufferAddress(env, (b)))
 
 /* ---- dependency job ---------------------------------------------------------------------------- */
@@ -125,6 +127,48 @@ JNIEXPORT jint JNICALL FN(commDestroy)(JNIEnv* env, jobject self, jlong comm) { 
 
 JNIEXPORT jint JNICALL FN(depsAllreduce)(JNIEnv* env, jobject self, jlong h, jlong comm, jlong totalRecords) {
     return zk_deps_allreduce(CTX(h), COMM(comm), (uint64_t)totalRecords);
+}
+
+/* ---- realtime link store (zksketch.h zk_rl_*, behind RealtimeAggregates) ---------------------------- */
+JNIEXPORT jlong JNICALL FN(rlCreate)(JNIEnv* env, jobject self, jint S, jint dev) {
+    zk_rl_config c;
+    zk_rl* h = NULL;
+    memset(&c, 0, sizeof(c));
+    c.num_services = (uint32_t)S;
+    c.device = dev;
+    return zk_rl_create(&c, &h) == ZK_OK ? (jlong)(intptr_t)h : 0;
+}
+
+JNIEXPORT jint JNICALL FN(rlDestroy)(JNIEnv* env, jobject self, jlong rl) { return zk_rl_destroy(RL(rl)); }
+
+JNIEXPORT jint JNICALL FN(rlReset)(JNIEnv* env, jobject self, jlong rl) { return zk_rl_reset(RL(rl)); }
+
+JNIEXPORT jint JNICALL FN(rlBind)(JNIEnv* env, jobject self, jlong h, jlong rl) { return zk_rl_bind(CTX(h), RL(rl)); }
+
+JNIEXPORT jstring JNICALL FN(rlLastError)(JNIEnv* env, jobject self, jlong rl) {
+    return (*env)->NewStringUTF(env, zk_rl_last_error(RL(rl)));
+}
+
+/* the server's rows as 3 longs each (parent, duration, traceId), ordered by (parent, duration,
+   traceId); null on error */
+JNIEXPORT jlongArray JNICALL FN(rlServerLinks)(JNIEnv* env, jobject self, jlong rl, jint server) {
+    uint64_t n = 0;
+    if (zk_rl_server_links(RL(rl), (uint32_t)server, NULL, NULL, NULL, 0, &n) != ZK_OK) return NULL;
+    uint32_t* par = (uint32_t*)malloc((n ? n : 1) * sizeof(uint32_t));
+    int64_t* dur = (int64_t*)malloc((n ? n : 1) * sizeof(int64_t));
+    uint64_t* tid = (uint64_t*)malloc((n ? n : 1) * sizeof(uint64_t));
+    jlongArray out = NULL;
+    if (par && dur && tid && (n == 0 || zk_rl_server_links(RL(rl), (uint32_t)server, par, dur, tid, n, &n) == ZK_OK)) {
+        out = (*env)->NewLongArray(env, (jsize)(3 * n));
+        for (uint64_t i = 0; out && i < n; ++i) {
+            const jlong row[3] = {(jlong)par[i], (jlong)dur[i], (jlong)tid[i]};
+            (*env)->SetLongArrayRegion(env, out, (jsize)(3 * i), 3, row);
+        }
+    }
+    free(par);
+    free(dur);
+    free(tid);
+    return out;
 }
 
 /* ---- ingest --------------------------------------------------------------------------------------- */

@@ -35,14 +35,14 @@
  */
 package com.twitter.zipkin.gpu
 
-import java.nio.{ByteBuffer, ByteOrder}
 import java.util.concurrent.{Callable, Executors}
 
 import com.twitter.algebird.Moments
 import com.twitter.util.{Future, Time}
-import com.twitter.zipkin.Constants
 import com.twitter.zipkin.common.{Dependencies, DependencyLink, Service, Span}
 import com.twitter.zipkin.storage.Aggregates
+
+import SpanRecords.{Columns, direct, put}
 
 /** rank / world of a multi-GPU job and the communicator id rank 0 made (ZkNative.commUniqueId) */
 final case class GpuShard(rank: Int, world: Int, commId: Array[Byte])
@@ -52,14 +52,6 @@ class GpuDependenciesJob(aggregates: Aggregates, device: Int = 0, strict: Boolea
                          services: Seq[String] = Nil, shard: Option[GpuShard] = None) {
   require(shard.isEmpty || services.nonEmpty, "a multi-GPU job needs the service list every rank numbers alike")
   require(services.size <= numServices, "more services than numServices")
-
-  private[this] def direct(n: Int, width: Int) =
-    ByteBuffer.allocateDirect(math.max(1, n) * width).order(ByteOrder.LITTLE_ENDIAN)
-
-  private[this] final class Columns(n: Int) {
-    val traceId = direct(n, 8); val spanId = direct(n, 8); val parentId = direct(n, 8)
-    val firstTs = direct(n, 8); val lastTs = direct(n, 8); val serviceId = direct(n, 4); val flags = direct(n, 4)
-  }
 
   private[this] def fail(ctx: Long, st: Int): Nothing = {
     val msg = ZkNative.lastError(ctx)
@@ -73,25 +65,6 @@ class GpuDependenciesJob(aggregates: Aggregates, device: Int = 0, strict: Boolea
   private[this] def accumulate(ctx: Long, c: Columns, n: Long, flags: Int): Unit =
     check(ctx, ZkNative.accumulate(ctx, c.traceId, c.spanId, c.parentId, c.firstTs, c.lastTs, c.serviceId, c.flags,
       n, flags | (if (verify) ZkNative.BatchVerifyTraces else 0)))
-
-  /** the record of one stored fragment (SURVEY.md Appendix A.1; zkagg.h ZK_F_*) */
-  private[this] def put(c: Columns, s: Span, names: Dictionary): Unit = {
-    val ts = s.annotations.map(_.timestamp)
-    def host(vals: Seq[String]) =
-      s.annotations.find(a => vals.contains(a.value) && a.host.isDefined).flatMap(_.host).map(_.serviceName)
-    val server = host(Seq(Constants.ServerRecv, Constants.ServerSend))
-    val client = host(Seq(Constants.ClientSend, Constants.ClientRecv))
-    var f = 0
-    if (s.parentId.isDefined) f |= 1
-    if (ts.nonEmpty) f |= 2
-    val svc = server.map { n => f |= 8; names.id(n) }.orElse(client.map { n => f |= 4; names.id(n) }).getOrElse(0)
-    for ((v, shift) <- Seq(Constants.ClientSend -> 8, Constants.ClientRecv -> 10, Constants.ServerRecv -> 12,
-                           Constants.ServerSend -> 14))
-      f |= math.min(2, s.annotations.count(_.value == v)) << shift
-    c.traceId.putLong(s.traceId); c.spanId.putLong(s.id); c.parentId.putLong(s.parentId.getOrElse(0L))
-    c.firstTs.putLong(if (ts.nonEmpty) ts.min else 0L); c.lastTs.putLong(if (ts.nonEmpty) ts.max else 0L)
-    c.serviceId.putInt(svc); c.flags.putInt(f)
-  }
 
   /** [all-reduce across ranks,] finalize; the Dependencies record of the whole job on every rank */
   private[this] def finish(ctx: Long, comm: Long, names: Int => String): Option[Dependencies] = {

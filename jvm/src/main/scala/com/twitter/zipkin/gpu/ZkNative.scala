@@ -66,6 +66,18 @@ object ZkNative {
     * the merged counters) */
   @native def depsAllreduce(ctx: Long, comm: Long, totalRecords: Long): Int
 
+  // ---- realtime link store (zksketch.h zk_rl_*): the state behind GpuRealtimeAggregates -----------
+  /** 0 on error */
+  @native def rlCreate(numServices: Int, device: Int): Long
+  @native def rlDestroy(rl: Long): Int
+  @native def rlReset(rl: Long): Int
+  /** K1 of every later accumulate on ctx writes its join rows into rl (rl = 0 unbinds) */
+  @native def rlBind(ctx: Long, rl: Long): Int
+  @native def rlLastError(rl: Long): String
+  /** the rows whose child (server) service is `server`: (parent, duration us, traceId) triples ordered
+    * by (parent, duration, traceId); null on error */
+  @native def rlServerLinks(rl: Long, server: Int): Array[Long]
+
   // ---- ingest (zkingest.h) -----------------------------------------------------------------------
   @native def ingestCreate(): Long
   @native def ingestDestroy(ing: Long): Int

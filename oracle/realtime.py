@@ -300,3 +300,80 @@ def rt_port(cols, num_services: int, p: int = 14, m: int = 7, seed: int = 0, thr
     if rc != 0:
         raise ValueError("zkr_port: bad arguments or out of memory")
     return RtPortResult(regs, hist, dropped, secs.value, threads)
+
+
+# ---- the realtime link store (zk_rl_*, RealtimeAggregates) --------------------------------------
+F_HAS_PARENT = 1 << 0
+
+
+def joined_links(cols, num_services: int):
+    """Every join row of the dependency job, before its group.sum: (parent service, child service,
+    child duration, traceId) per joined child span -- ZipkinAggregateJob.scala:21-37 on columnar
+    fragments: mergeSpan over (traceId, spanId) (Span.scala:148-169; parentId = the min over the
+    fragments that carry one, the deterministic rule zk_oracle.c uses), isValid (:236-240), the join
+    on (parentId, traceId) against a valid merged parent, both serviceNames (:125-131, server side
+    first), duration = last - first annotation (:228-230) below 2^40 us. Returns four arrays in
+    (parent, child, duration, traceId) order."""
+    tid = np.asarray(cols.trace_id, dtype=np.uint64)
+    sid = np.asarray(cols.span_id, dtype=np.uint64)
+    pid = np.asarray(cols.parent_id, dtype=np.uint64)
+    flags = np.asarray(cols.flags, dtype=np.uint32)
+    svc = np.asarray(cols.service_id, dtype=np.uint32)
+    first = np.asarray(cols.first_ts, dtype=np.int64)
+    last = np.asarray(cols.last_ts, dtype=np.int64)
+    empty = (np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.uint64))
+    if len(tid) == 0:
+        return empty
+    order = np.lexsort((sid, tid))
+    tid_s, sid_s, f = tid[order], sid[order], flags[order]
+    start = np.r_[True, (tid_s[1:] != tid_s[:-1]) | (sid_s[1:] != sid_s[:-1])]
+    gid = np.cumsum(start) - 1
+    G = int(gid[-1]) + 1
+    ha = (f & F_HAS_ANNOTATIONS) != 0
+    fmin = np.full(G, np.iinfo(np.int64).max, np.int64)
+    lmax = np.full(G, np.iinfo(np.int64).min, np.int64)
+    np.minimum.at(fmin, gid[ha], first[order][ha])
+    np.maximum.at(lmax, gid[ha], last[order][ha])
+    kind = np.where(f & F_SVC_SERVER, 0, np.where(f & F_SVC_CLIENT, 1, 2)).astype(np.int64)
+    s_ = svc[order].astype(np.int64)
+    has = (kind < 2) & (s_ < num_services)
+    key = np.full(G, 1 << 62, np.int64)
+    np.minimum.at(key, gid[has], (kind[has] << 30) | s_[has])
+    counts = np.zeros((G, 4), np.int64)
+    for c, sh in enumerate((8, 10, 12, 14)):
+        np.add.at(counts[:, c], gid, ((f >> sh) & 3).astype(np.int64))
+    valid = (counts <= 1).all(axis=1)
+    hp = (f & F_HAS_PARENT) != 0
+    gpar = np.full(G, np.iinfo(np.uint64).max, np.uint64)
+    np.minimum.at(gpar, gid[hp], pid[order][hp])
+    has_par = np.zeros(G, bool)
+    has_par[gid[hp]] = True
+    gtid, gsid = tid_s[start], sid_s[start]
+    # the parent: the merged span (traceId, parentId), valid
+    child = np.flatnonzero(valid & has_par)
+    lo = np.searchsorted(gtid, gtid[child], side="left")
+    hi = np.searchsorted(gtid, gtid[child], side="right")
+    par = np.full(len(child), -1, np.int64)
+    for i, (a, b) in enumerate(zip(lo, hi)):  # (a trace's groups are contiguous and spanId-sorted)
+        j = a + int(np.searchsorted(gsid[a:b], gpar[child[i]]))
+        if j < b and gsid[j] == gpar[child[i]] and valid[j]:
+            par[i] = j
+    ok = par >= 0
+    child, par = child[ok], par[ok]
+    none = 1 << 62
+    ok = (key[child] != none) & (key[par] != none)
+    child, par = child[ok], par[ok]
+    d = lmax[child] - fmin[child]
+    ok = (fmin[child] != np.iinfo(np.int64).max) & (d >= 0) & (d < MAX_DURATION)
+    child, par, d = child[ok], par[ok], d[ok]
+    mask = (1 << 30) - 1
+    return key[par] & mask, key[child] & mask, d, gtid[child]
+
+
+def server_links(links, server: int):
+    """The rows of `server` (the child side), ordered by (parent, duration, traceId): what
+    zk_rl_server_links returns."""
+    p, c, d, t = links
+    sel = np.flatnonzero(c == server)
+    o = np.lexsort((t[sel], d[sel], p[sel]))
+    return p[sel][o], d[sel][o], t[sel][o]

@@ -188,6 +188,15 @@ class zk_rt_config(C.Structure):
     ]
 
 
+class zk_rl_config(C.Structure):
+    _fields_ = [
+        ("num_services", C.c_uint32),
+        ("device", C.c_int32),
+        ("stream", C.c_void_p),
+        ("reserved", C.c_uint32 * 8),
+    ]
+
+
 ZK_RT_WITH_DEPS = 0
 ZK_RT_ONLY = 1
 
@@ -288,6 +297,14 @@ _SIGNATURES = [
     ("zk_rt_partial", C.c_int, [_P, C.POINTER(_P), _U64P, C.POINTER(_P), _U64P]),
     ("zk_rt_read", C.c_int, [_P, _P, _P]),
     ("zk_rt_dropped", C.c_int, [_P, _U64P, _U64P]),
+    # include/zksketch.h: realtime link store (RealtimeAggregates)
+    ("zk_rl_create", C.c_int, [C.POINTER(zk_rl_config), C.POINTER(_P)]),
+    ("zk_rl_destroy", C.c_int, [_P]),
+    ("zk_rl_last_error", C.c_char_p, [_P]),
+    ("zk_rl_reset", C.c_int, [_P]),
+    ("zk_rl_bind", C.c_int, [_P, _P]),
+    ("zk_rl_count", C.c_int, [_P, _U64P, _U64P]),
+    ("zk_rl_server_links", C.c_int, [_P, C.c_uint32, _P, _P, _P, C.c_uint64, _U64P]),
     # include/zkcomm.h: RCCL communicator and the multi-GPU merges
     ("zk_comm_unique_id", C.c_int, [_P, C.c_uint64]),
     ("zk_comm_create", C.c_int, [_P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int32, C.POINTER(_P)]),

@@ -271,6 +271,140 @@ class NullAggregates(Aggregates):
         pass
 
 
+class RealtimeAggregates:
+    """trait RealtimeAggregates (zipkin-common/.../storage/RealtimeAggregates.scala:26-38): for a
+    time stamp (us), a server service name and an rpc name, a map from every client service calling
+    that server to a list -- of every span duration (getSpanDurations) or every trace id
+    (getServiceNamesToTraceIds) of those calls (zipkinQuery.thrift:234-251)."""
+
+    def close(self) -> None:
+        raise NotImplementedError
+
+    def getSpanDurations(self, timeStamp: int, serverServiceName: str, rpcName: str) -> Dict[str, List[int]]:
+        raise NotImplementedError
+
+    def getServiceNamesToTraceIds(self, timeStamp: int, serverServiceName: str, rpcName: str) -> Dict[str, List[int]]:
+        raise NotImplementedError
+
+
+class NullRealtimeAggregates(RealtimeAggregates):
+    """NullRealtimeAggregates (RealtimeAggregates.scala:40-51): empty maps."""
+
+    def close(self) -> None:
+        pass
+
+    def getSpanDurations(self, timeStamp, serverServiceName, rpcName) -> Dict[str, List[int]]:
+        return {}
+
+    def getServiceNamesToTraceIds(self, timeStamp, serverServiceName, rpcName) -> Dict[str, List[int]]:
+        return {}
+
+
+def _signed64(x: int) -> int:
+    """a traceId as the JVM's Long (zipkinQuery.thrift i64)"""
+    return x - (1 << 64) if x >= 1 << 63 else x
+
+
+class _DeviceLinkWindow:
+    """One time window of GpuRealtimeAggregates on the device: a DepsContext with a RealtimeLinks
+    store bound (K1 writes the join rows beside its links)."""
+
+    def __init__(self, num_services: int, device: int):
+        from .context import DepsContext
+        from .realtime import RealtimeLinks
+
+        self.ctx = DepsContext(num_services, device=device, strict=False)
+        self.rl = RealtimeLinks(num_services, device=device)
+        self.rl.bind(self.ctx)
+
+    def add(self, cols, clustered: bool) -> None:
+        self.ctx.accumulate(cols, clustered=clustered, verify=False)
+
+    def server_links(self, server: int):
+        self.ctx.sync()
+        return self.rl.server_links(server)
+
+    def close(self) -> None:
+        self.rl.close()
+        self.ctx.close()
+
+
+class GpuRealtimeAggregates(RealtimeAggregates):
+    """RealtimeAggregates over the device's join rows (include/zksketch.h zk_rl_*).
+
+    The rows the trait's lists are made of are the dependency job's join rows before its group.sum
+    (ZipkinAggregateJob.scala:25-37): parent span's service = the CLIENT service, child span's
+    service = the SERVER service, the child span's duration, the trace id. `accumulate(batch,
+    timestamp)` runs the device join over a batch of span fragments (any order; whole traces per
+    batch) into the time window holding `timestamp` (windows of `window_us`, the last `keep` kept);
+    the queries answer from the window holding `timeStamp` (Time in us, ThriftQueryService.scala:317-
+    335), with an empty map for an unknown window or server name:
+
+      getSpanDurations(t, server, rpc)          {client: every call's duration in us, ascending}
+      getServiceNamesToTraceIds(t, server, rpc) {client: the calls' distinct trace ids, ascending,
+                                                 as signed 64-bit Longs}
+
+    rpcName is not a key: the 48-B record carries no span name (the dependency job never reads
+    one), so both answers cover every rpc of the server; the web UI passes spanName.getOrElse("")
+    (Handlers.scala:83-104). `window_factory(num_services)` builds a window (default: the device);
+    the CPU tests pass the oracle's."""
+
+    def __init__(self, services: Dictionary, *, window_us: int = 3_600_000_000, keep: int = 24, device: int = 0,
+                 window_factory=None):
+        if window_us <= 0 or keep <= 0:
+            raise ValueError("window_us and keep must be positive")
+        self.services = services
+        self.window_us = int(window_us)
+        self.keep = int(keep)
+        self._factory = window_factory or (lambda S: _DeviceLinkWindow(S, device))
+        self._windows: Dict[int, object] = {}
+
+    def _window(self, timestamp_us: int, create: bool):
+        w = int(timestamp_us) // self.window_us
+        win = self._windows.get(w)
+        if win is None and create:
+            win = self._factory(max(1, len(self.services)))
+            self._windows[w] = win
+            for old in sorted(self._windows)[:-self.keep]:  # the oldest windows leave the store
+                self._windows.pop(old).close()
+        return win
+
+    def accumulate(self, cols, timestamp_us: int, *, clustered: bool = False) -> None:
+        """One batch of span fragments (service ids from `services`) into the window of timestamp_us."""
+        self._window(timestamp_us, True).add(cols, clustered)
+
+    def _rows(self, timeStamp: int, serverServiceName: str):
+        win = self._window(timeStamp, False)
+        if win is None or serverServiceName not in self.services:
+            return None
+        return win.server_links(self.services.id(serverServiceName))
+
+    def getSpanDurations(self, timeStamp: int, serverServiceName: str, rpcName: str) -> Dict[str, List[int]]:
+        rows = self._rows(timeStamp, serverServiceName)
+        if rows is None:
+            return {}
+        par, dur, _ = rows
+        out: Dict[str, List[int]] = {}
+        for p, d in zip(par.tolist(), dur.tolist()):  # (rows come ordered by parent, then duration)
+            out.setdefault(self.services.name(p), []).append(int(d))
+        return out
+
+    def getServiceNamesToTraceIds(self, timeStamp: int, serverServiceName: str, rpcName: str) -> Dict[str, List[int]]:
+        rows = self._rows(timeStamp, serverServiceName)
+        if rows is None:
+            return {}
+        par, _, tid = rows
+        out: Dict[str, set] = {}
+        for p, t in zip(par.tolist(), tid.tolist()):
+            out.setdefault(self.services.name(p), set()).add(int(t))
+        return {k: sorted(_signed64(t) for t in v) for k, v in out.items()}
+
+    def close(self) -> None:
+        for win in self._windows.values():
+            win.close()
+        self._windows = {}
+
+
 class GpuAggregates(Aggregates):
     """Aggregates over a zk_store with one reference backend's storage semantics (zkstore.h):
     "anorm" (AnormAggregates: a row per record, containment window, top lists are stubs),

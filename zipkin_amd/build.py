@@ -27,8 +27,9 @@ SOURCES = [
     "zk_launch.cpp",
     "zk_exchange.hip",
     "zk_comm.cpp",
+    "zk_rl.hip",
 ]
-HEADERS = ["zk_internal.h", "zk_cluster.h", "zk_tracegen.h", "zk_sketch_internal.h", "zk_rt_internal.h", "zk_block.h", "zk_launch.h", "zk_comm.h"]
+HEADERS = ["zk_internal.h", "zk_cluster.h", "zk_tracegen.h", "zk_sketch_internal.h", "zk_rt_internal.h", "zk_block.h", "zk_launch.h", "zk_comm.h", "zk_rl_internal.h"]
 PUBLIC_HEADERS = ["zkagg.h", "zksketch.h", "zkstore.h", "zkingest.h", "zkcomm.h"]
 LIB = PKG / "libzkagg.so"
 ARCH = os.environ.get("ZK_OFFLOAD_ARCH", "gfx950")

@@ -16,6 +16,7 @@
 
 #include "zk_internal.h"
 #include "zk_launch.h"
+#include "zk_rl_internal.h"
 #include "zk_rt_internal.h"
 
 using namespace zk;
@@ -94,6 +95,8 @@ struct zk_ctx {
     // bound realtime sketch (zk_rt_bind)
     zk_rt* rt = nullptr;
     uint32_t rt_mode = ZK_RT_WITH_DEPS;
+    // bound realtime link store (zk_rl_bind): K1 writes an item beside every link
+    zk_rl* rl = nullptr;
     // timing
     std::vector<EventPair> ev_free, ev_join, ev_reduce, ev_spill, ev_fin, ev_cluster;
     zk_timing tm{};
@@ -435,6 +438,7 @@ zk_status zk_ctx_destroy(zk_ctx* c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->rt) rt_set_stream(c->rt, nullptr);
+    if (c->rl) rl_set_stream(c->rl, nullptr);
     if (c->own_table) hipFree(c->table);
     c->table = nullptr;
     hipFree(c->stats);
@@ -739,7 +743,7 @@ static zk_status accumulate_dev(zk_ctx* c, SpanColsDev d, uint32_t flags, uint32
     // unclustered, without the trace check or a realtime sketch: the group join (two-level plans)
     // (only when max_trace_records >= the group join's tile: it aggregates every trace of a sub-bucket
     // it holds, so a smaller bound could not be enforced there as K1 enforces it)
-    if (!(flags & ZK_BATCH_TRACE_CLUSTERED) && !(flags & ZK_BATCH_VERIFY_TRACES) && !c->rt && c->group_join &&
+    if (!(flags & ZK_BATCH_TRACE_CLUSTERED) && !(flags & ZK_BATCH_VERIFY_TRACES) && !c->rt && !c->rl && c->group_join &&
         c->max_trace >= group_join_capacity() && n <= 0xFFFFFFFFull) {
         const ClusterPlan gp = cluster_plan(n, c->cus, true);
         if (gp.b1 && gp.b2) return accumulate_groups(c, d, gp);
@@ -805,6 +809,10 @@ static zk_status accumulate_dev(zk_ctx* c, SpanColsDev d, uint32_t flags, uint32
         st = rt_prepare_lists(c->rt, grid, stride, n + (dr ? c->carry_cap : 0), &a, c->stream);
         if (st != ZK_OK) return fail(c, st, std::string("sketch: ") + rt_error(c->rt));
     }
+    if (c->rl && join) {  // realtime link items beside the links (the spill list also takes the carry's)
+        st = rl_prepare_lists(c->rl, grid, stride, n + (dr ? c->carry_cap : 0), &a, c->stream);
+        if (st != ZK_OK) return fail(c, st, std::string("realtime links: ") + rl_error(c->rl));
+    }
     EventPair ej, er, es;
     if (c->timing) {
         ej = take_pair(c);
@@ -861,6 +869,10 @@ static zk_status accumulate_dev(zk_ctx* c, SpanColsDev d, uint32_t flags, uint32
     if (c->rt) {
         st = rt_consume_lists(c->rt, grid, stride, n + (dr ? c->carry_cap : 0));
         if (st != ZK_OK) return fail(c, st, std::string("sketch: ") + rt_error(c->rt));
+    }
+    if (c->rl && join) {
+        st = rl_consume_lists(c->rl, c->link_count, grid, stride, n + (dr ? c->carry_cap : 0));
+        if (st != ZK_OK) return fail(c, st, std::string("realtime links: ") + rl_error(c->rl));
     }
     if (join) c->records_since_reset += n - skip;
     return ZK_OK;
@@ -942,10 +954,21 @@ static zk_status flush_carry(zk_ctx* c) {
         const zk_status st = rt_prepare_lists(c->rt, 0, 0, c->carry_cap, &f, c->stream);
         if (st != ZK_OK) return fail(c, st, std::string("sketch: ") + rt_error(c->rt));
     }
+    const bool links = c->rl && f.join;
+    if (links) {  // its link items: the spill list of a zero-width list set
+        f.grid = 0;
+        f.link_stride = 0;
+        const zk_status st = rl_prepare_lists(c->rl, 0, 0, c->carry_cap, &f, c->stream);
+        if (st != ZK_OK) return fail(c, st, std::string("realtime links: ") + rl_error(c->rl));
+    }
     ZK_HIP(c, launch_spill(f, 1, c->stream));
     if (c->rt) {
         const zk_status st = rt_consume_lists(c->rt, 0, 0, c->carry_cap);
         if (st != ZK_OK) return fail(c, st, std::string("sketch: ") + rt_error(c->rt));
+    }
+    if (links) {
+        const zk_status st = rl_consume_lists(c->rl, c->link_count, 0, 0, c->carry_cap);
+        if (st != ZK_OK) return fail(c, st, std::string("realtime links: ") + rl_error(c->rl));
     }
     return ZK_OK;
 }
@@ -1128,10 +1151,27 @@ zk_status zk_deps_allreduce(zk_ctx* c, zk_comm* comm, uint64_t total_records) {
     ZK_CATCH(c)
 }
 
+zk_status zk_rl_bind(zk_ctx* c, zk_rl* rl) {
+    if (!c) return ZK_ERR_INVALID_ARG;
+    if (rl && rl_device(rl) != c->device) return fail(c, ZK_ERR_INVALID_ARG, "link store and ctx on different devices");
+    if (rl && rl_services(rl) != c->S) return fail(c, ZK_ERR_INVALID_ARG, "link store and ctx differ in num_services");
+    if (rl && c->rt && c->rt_mode == ZK_RT_WITH_DEPS)
+        return fail(c, ZK_ERR_UNSUPPORTED, "a realtime link store and a ZK_RT_WITH_DEPS sketch on one ctx");
+    if (c->rl && c->rl != rl) {
+        ZK_HIP(c, hipStreamSynchronize(c->stream));
+        rl_set_stream(c->rl, nullptr);
+    }
+    c->rl = rl;
+    if (rl) rl_set_stream(rl, c->stream);  // one stream orders the ctx's and the store's work
+    return ZK_OK;
+}
+
 zk_status zk_rt_bind(zk_ctx* c, zk_rt* rt, uint32_t mode) {
     if (!c) return ZK_ERR_INVALID_ARG;
     if (mode != ZK_RT_WITH_DEPS && mode != ZK_RT_ONLY) return fail(c, ZK_ERR_INVALID_ARG, "unknown sketch mode");
     if (rt && rt_device(rt) != c->device) return fail(c, ZK_ERR_INVALID_ARG, "sketch and ctx on different devices");
+    if (rt && c->rl && mode == ZK_RT_WITH_DEPS)
+        return fail(c, ZK_ERR_UNSUPPORTED, "a ZK_RT_WITH_DEPS sketch and a realtime link store on one ctx");
     if (c->rt && c->rt != rt) {
             ZK_HIP(c, hipStreamSynchronize(c->stream));
         rt_set_stream(c->rt, nullptr);

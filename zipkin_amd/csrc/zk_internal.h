@@ -129,6 +129,14 @@ struct JoinArgs {
     uint32_t append;
     // ZK_BATCH_CONTINUES on the device: skip read from here when set (and n from n_dev)
     const uint32_t* skip_dev;
+    // realtime link items (zk_rl, a bound RealtimeAggregates store), lk_key == nullptr: none. One item
+    // per emitted link, at the link's own list position: key ((child * S + parent) << 40) | duration,
+    // and the child's traceId; the spill kernel appends to list `grid` (lk_spill_count, capacity
+    // lk_spill_cap items)
+    uint64_t* lk_key;
+    uint64_t* lk_tid;
+    uint32_t* lk_spill_count;
+    uint64_t lk_spill_cap;
 };
 
 // host-side launchers (implemented in the .hip files)

@@ -366,6 +366,7 @@ __device__ __forceinline__ void load_late(const JoinArgs& a, uint64_t n, uint64_
 // per merged valid span with a service (zk_rt.hip). The product dependency pass is kModeJoin.
 constexpr int kModeJoin = 1;
 constexpr int kModeEmit = 2;
+constexpr int kModeLinks = 4;  // with kModeJoin: a realtime link item beside every link (zk_rl)
 template <int TILE, int WG, int MODE>
 // launch bounds: minimum waves per SIMD = resident workgroups per CU x waves per workgroup / 4 SIMDs
 __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_stream(JoinArgs a) {
@@ -416,7 +417,8 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
     uint32_t r_clear[2] = {kNoSlot, kNoSlot};  // hash slots this thread's leaders of the last window hold
 
     Window cur, nxt;
-    constexpr bool JOIN = (MODE & kModeJoin) != 0, EMIT = (MODE & kModeEmit) != 0;
+    constexpr bool JOIN = (MODE & kModeJoin) != 0, EMIT = (MODE & kModeEmit) != 0, LINKS = (MODE & kModeLinks) != 0;
+    static_assert(!LINKS || (JOIN && !EMIT), "link items ride on the join's links");
 #pragma unroll
     for (int x = tid; x < H / 4; x += WG) reinterpret_cast<uint4*>(s_ht)[x] = make_uint4(0u, 0u, 0u, 0u);
     uint64_t m_ev, m_od;  // this wave's boundary ballots of the current window (uniform; phase 3 reuses them)
@@ -647,6 +649,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
         // ---- 6. filter(isValid), join on (parentId, traceId), (cell, duration) links ----------
         uint64_t r_link[2], r_item[2];
         uint32_t r_isvc[2];
+        uint64_t r_lkey[2] = {0, 0};  // kModeLinks: the link's realtime item key (child-major cell | d)
         uint32_t nl = 0, ni = 0;
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
@@ -719,6 +722,7 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
             }
             const uint64_t cell = (uint64_t)(sp & kSvcIdMask) * a.S + (sL & kSvcIdMask);
             r_link[e] = (cell << 40) | d;
+            if constexpr (LINKS) r_lkey[e] = (((uint64_t)(sL & kSvcIdMask) * a.S + (sp & kSvcIdMask)) << 40) | d;
             if (a.nb) atomicAdd(&s_hist[cell >> a.cb_shift], 1u);
             ++nl;
         }
@@ -760,7 +764,12 @@ __global__ __launch_bounds__(WG, ZK_K1_WGS_PER_CU * WG / 256) void k_span_join_s
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const bool v = r_link[e] != ~0ull;
-                out[v ? (uint64_t)pos : trash] = r_link[e];
+                const uint64_t at = v ? (uint64_t)pos : trash;
+                out[at] = r_link[e];
+                if constexpr (LINKS) {  // the realtime link item at the link's own position
+                    a.lk_key[(uint64_t)blockIdx.x * a.link_stride + at] = r_lkey[e];
+                    a.lk_tid[(uint64_t)blockIdx.x * a.link_stride + at] = cur.tid[e];
+                }
                 pos += v ? 1u : 0u;
             }
 #else
@@ -1049,10 +1058,19 @@ __global__ __launch_bounds__(kSpillWG) void k_span_join_spill(JoinArgs a) {
                     st.inc(ST_NO_SERVICE);
                 } else {
                     const uint64_t d = (uint64_t)(ld_sc(&sc.last[Ld]) - ld_sc(&sc.first[Ld]));
-                    if (d >= kMaxDuration)
+                    if (d >= kMaxDuration) {
                         st.inc(ST_DUR_RANGE);
-                    else
+                    } else {
                         emit_link(a.table, (spv & kSvcIdMask) * a.S + (sL & kSvcIdMask), d);
+                        if (a.lk_key) {  // the realtime link item, appended to the spill list
+                            const uint32_t q = atomicAdd(a.lk_spill_count, 1u);
+                            if (q < a.lk_spill_cap) {
+                                const uint64_t at = (uint64_t)a.grid * a.link_stride + q;
+                                a.lk_key[at] = (((uint64_t)(sL & kSvcIdMask) * a.S + (spv & kSvcIdMask)) << 40) | d;
+                                a.lk_tid[at] = a.c.trace_id[gi];
+                            }
+                        }
+                    }
                 }
             } else {
                 st.inc(ST_MISSING_PARENT);
@@ -1489,6 +1507,9 @@ hipError_t launch_join(const JoinArgs& a, hipStream_t s, uint32_t blocks) {
     if (a.c.n == 0) return hipSuccess;
     const dim3 g((unsigned)(blocks ? blocks : a.grid)), b(kTileWG);
     const bool emit = a.rt_pay != nullptr, join = a.join != 0;
+    if (a.lk_key && join && !emit)
+        return launch_checked("k_span_join_stream<join|links>", k_span_join_stream<kTile, kTileWG, kModeJoin | kModeLinks>,
+                              g, b, 0, s, a);
     if (emit && join)
         return launch_checked("k_span_join_stream<join|emit>", k_span_join_stream<kTile, kTileWG, kModeJoin | kModeEmit>,
                               g, b, 0, s, a);

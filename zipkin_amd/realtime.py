@@ -162,3 +162,80 @@ class RtSketch:
         rp, rb, hp, hb = C.c_void_p(), C.c_uint64(), C.c_void_p(), C.c_uint64()
         self._check(self._L.zk_rt_partial(self._h, C.byref(rp), C.byref(rb), C.byref(hp), C.byref(hb)))
         return int(rp.value), int(rb.value), int(hp.value), int(hb.value)
+
+
+class RealtimeLinks:
+    """The realtime link store (zk_rl_*): every join row (parent service, child service, child
+    duration, traceId) of the dependency path since the last reset, kept in HBM and queried by
+    server (child) service -- the state behind RealtimeAggregates (GpuRealtimeAggregates below in
+    zipkin_amd/aggregates.py). Bound to a DepsContext, K1 writes the rows beside its links."""
+
+    def __init__(self, num_services: int, *, device: int = 0, stream: int | None = None):
+        self._L = _abi.lib()
+        cfg = _abi.zk_rl_config()
+        cfg.num_services = num_services
+        cfg.device = device
+        cfg.stream = stream
+        h = C.c_void_p()
+        st = self._L.zk_rl_create(C.byref(cfg), C.byref(h))
+        if st != _abi.ZK_OK:
+            raise _abi.ZkError(st, _abi.status_str(st))
+        self._h = h
+        self.num_services = num_services
+        self._bound = None
+
+    def _check(self, st: int) -> None:
+        if st != _abi.ZK_OK:
+            raise _abi.ZkError(st, self._L.zk_rl_last_error(self._h).decode() or _abi.status_str(st))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self.unbind()
+            self._L.zk_rl_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def bind(self, ctx) -> None:
+        st = self._L.zk_rl_bind(ctx.handle, self._h)
+        if st != _abi.ZK_OK:
+            raise _abi.ZkError(st, self._L.zk_last_error(ctx.handle).decode())
+        self._bound = ctx
+
+    def unbind(self) -> None:
+        if self._bound is not None and getattr(self._bound, "_h", None):
+            self._L.zk_rl_bind(self._bound.handle, None)
+        self._bound = None
+
+    def reset(self) -> None:
+        self._check(self._L.zk_rl_reset(self._h))
+
+    def count(self) -> tuple[int, int]:
+        """(rows in the window, rows dropped past its capacity -- always 0)."""
+        n, d = C.c_uint64(), C.c_uint64()
+        self._check(self._L.zk_rl_count(self._h, C.byref(n), C.byref(d)))
+        return int(n.value), int(d.value)
+
+    def server_links(self, server: int):
+        """(parent ids uint32, durations int64 us, traceIds uint64) of every row whose child service
+        is `server`, ordered by (parent, duration, traceId)."""
+        n = C.c_uint64()
+        self._check(self._L.zk_rl_server_links(self._h, server, None, None, None, 0, C.byref(n)))
+        m = int(n.value)
+        par = np.zeros(max(1, m), np.uint32)
+        dur = np.zeros(max(1, m), np.int64)
+        tid = np.zeros(max(1, m), np.uint64)
+        if m:
+            self._check(self._L.zk_rl_server_links(self._h, server, par.ctypes.data, dur.ctypes.data, tid.ctypes.data,
+                                                   m, C.byref(n)))
+        return par[:m], dur[:m], tid[:m]
