@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-5 final session, part A (PART=a): the whole -m gpu suite, smoke, the default bench (C2), its
+# Round-6 validation session, part A (PART=a): the whole -m gpu suite, smoke, the default bench (C2), its
 # rocprof kernel stats (serial steps) and K1's HBM counters (two --pmc passes); part B (PART=b): the
 # other bench lines and the job drivers. Every GPU step has its own limit; the first failure ends it.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-T=${TAG:-r05f}
+T=${TAG:-r06m}
 if [ "${PART:-a}" = a ]; then
   timeout -k 10 700 python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests/ > gpurun_out/${T}_gpu_tests.txt 2>&1 || { echo "tests failed"; tail -30 gpurun_out/${T}_gpu_tests.txt; exit 1; }
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.txt 2>&1 || { echo "smoke failed"; exit 1; }
