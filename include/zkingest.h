@@ -95,7 +95,7 @@ zk_status zk_ingest_string(const zk_ingest* ing, uint64_t hash, char* buf, uint6
 /* ---- the same decoder on the device -------------------------------------------------------
  * zk_ingest_dev decodes fragments that are already in HBM (buf and offsets are device pointers)
  * into device columns, one lane per fragment (Snappy block, thrift walk, validation and record as
- * above; no indexer items). Its service dictionary lives on the device: a batch's new names get ids
+ * above; the indexer items through zk_ingest_dev_spans_items). Its service dictionary lives on the device: a batch's new names get ids
  * in the order of their hash-table slots (not in order of first appearance; names whose hashes
  * collide in the table may swap ids between runs), names are compared byte for byte. At most `max_services` distinct names
  * (ZK_ERR_SERVICE_RANGE past that). Thrift nesting deeper than 16 levels inside skipped fields is
@@ -107,6 +107,19 @@ const char* zk_ingest_dev_last_error(const zk_ingest_dev* ing);
 zk_status   zk_ingest_dev_spans(zk_ingest_dev* ing, const uint8_t* buf, const uint64_t* offsets, uint64_t n,
                                 uint32_t codec, uint32_t flags, const zk_span_cols* out, uint64_t* n_out,
                                 uint64_t* n_rejected);
+/* The same decode with the span indexer's items (as zk_ingest_spans: CassieSpanStore.scala:214-242),
+ * written to DEVICE buffers: kv_service / kv_key and ann_service / ann_value are device pointers
+ * (either pair NULL or cap 0: not produced). Service ids are this decoder's; within a batch the items
+ * come in no particular order (the sketches take a batch as a set), the multiset per batch equals the
+ * host decoder's. ZK_ERR_CAPACITY when a buffer is too small (records and the first cap items are
+ * still written; kv_n / ann_n are the items written). n < 2^30. The strings behind key / value hashes
+ * are kept on the host side of the decoder: zk_ingest_dev_string. Slower than zk_ingest_dev_spans
+ * (a second build of the decoder: a captured-string set probe per item, no copy-in prefetch). */
+zk_status   zk_ingest_dev_spans_items(zk_ingest_dev* ing, const uint8_t* buf, const uint64_t* offsets, uint64_t n,
+                                      uint32_t codec, uint32_t flags, const zk_span_cols* out, uint64_t* n_out,
+                                      uint64_t* n_rejected, zk_ingest_items* items);
+/* the string behind a key / value hash an items batch of this decoder has seen (two-phase) */
+zk_status   zk_ingest_dev_string(const zk_ingest_dev* ing, uint64_t hash, char* buf, uint64_t cap, uint64_t* len);
 zk_status   zk_ingest_dev_num_services(const zk_ingest_dev* ing, uint32_t* n);
 /* Snappy scratch (deferred fragments' Spans, names not yet in the dictionary): bump-allocated per
  * batch and grown when a batch runs out (the fragments that missed out are decoded again). `bytes`

@@ -52,20 +52,29 @@ def test_stored_span_job_streams_ten_million_fragments(gpu):
     assert all(v == ["custom.event"] for v in job.top_annotations.values())
     assert all(v == ["http.uri"] for v in job.top_kv.values())
 
-    # the same 40 batches already in HBM, through the device decoder (run_device: dependencies only)
+    # the same 40 batches already in HBM, through the device decoder: with the indexer items (the
+    # default) and dependencies only
     import torch
 
     dev = [(torch.from_numpy(b).cuda(), torch.from_numpy(o.view(np.int64)).cuda(), len(o) - 1) for b, o in parts]
     torch.cuda.synchronize()
-    djob = StoredSpanJob(clock=lambda: 10**15, max_services=S)
-    djob.run_device(dev[:1])  # warm
-    t0 = time.perf_counter()
-    ddeps = djob.run_device(dev)
-    ddt = time.perf_counter() - t0
-    print(f"StoredSpanJob.run_device: the same {len(cols)} fragments in HBM, {len(dev)} batches: {ddt * 1e3:.1f} ms, "
-          f"{len(cols) / ddt:.3e} fragments/s (device decode + accumulate + finalize)")
-    assert djob.rejected == 0 and djob.stats["records"] == len(cols)
-    assert _by_name(ddeps) == want
+    for indexer in (True, False):
+        dstore = GpuAggregates("cassandra")
+        djob = StoredSpanJob(aggregates=dstore, top_k=5, clock=lambda: 10**15, max_services=S)
+        djob.run_device(dev[:1], indexer=indexer)  # warm
+        t0 = time.perf_counter()
+        ddeps = djob.run_device(dev, indexer=indexer)
+        ddt = time.perf_counter() - t0
+        what = "decode with indexer items + accumulate + 2 sketches" if indexer else "decode + accumulate"
+        print(f"StoredSpanJob.run_device(indexer={indexer}): the same {len(cols)} fragments in HBM, {len(dev)} "
+              f"batches: {ddt * 1e3:.1f} ms, {len(cols) / ddt:.3e} fragments/s ({what} + finalize)")
+        assert djob.rejected == 0 and djob.stats["records"] == len(cols)
+        assert _by_name(ddeps) == want
+        if indexer:  # the device decoder's items give run()'s top lists, stored the same way
+            assert djob.top_kv == job.top_kv and djob.top_annotations == job.top_annotations
+            for svc in job.top_kv:
+                assert dstore.getTopKeyValueAnnotations(svc) == store.getTopKeyValueAnnotations(svc)
+                assert dstore.getTopAnnotations(svc) == store.getTopAnnotations(svc)
 
 
 def test_stored_span_job_on_the_device_decoder(gpu):
@@ -77,10 +86,44 @@ def test_stored_span_job_on_the_device_decoder(gpu):
     cuts = np.sort(np.random.default_rng(18).choice(np.arange(1, len(cols)), 7, replace=False)).tolist()
     dev = [(torch.from_numpy(b).cuda(), torch.from_numpy(o.view(np.int64)).cuda(), len(o) - 1)
            for b, o in batches(buf, off, cuts)]
-    job = StoredSpanJob(clock=lambda: 10**15)
+    job = StoredSpanJob(clock=lambda: 10**15, top_k=5)
     deps = job.run_device(dev)
     assert job.rejected == 0 and job.stats["records"] == len(cols)
     assert _by_name(deps) == _oracle_by_name(exp, S)
+    hjob = StoredSpanJob(clock=lambda: 10**15, top_k=5)
+    hjob.run(batches(buf, off, cuts))
+    assert job.top_kv == hjob.top_kv and job.top_annotations == hjob.top_annotations
+    assert len(job.top_kv) == S
+
+
+def test_run_device_top_lists_equal_run_on_rich_spans(gpu):
+    """run_device's indexer items on spans with several binary annotations, distinct non-core
+    values and hosts other than the span's service: the same top lists as the host-decode run()."""
+    import torch
+
+    from tests.richgen import gen_traces
+    from tests.test_ingest import encode_all
+
+    spans = gen_traces(207, 3000, max_depth=5, anomalies=0.0)
+    by_trace: dict = {}
+    for sp in spans:
+        by_trace.setdefault(sp.trace_id, []).append(sp)
+    traces = list(by_trace.values())
+    host_batches, dev = [], []
+    for i in range(0, len(traces), 400):
+        blobs = encode_all([sp for t in traces[i:i + 400] for sp in t])
+        offs = np.zeros(len(blobs) + 1, np.int64)
+        offs[1:] = np.cumsum([len(b) for b in blobs])
+        host_batches.append(blobs)
+        dev.append((torch.from_numpy(np.frombuffer(b"".join(blobs), np.uint8).copy()).cuda(),
+                    torch.from_numpy(offs).cuda(), len(blobs)))
+    hjob = StoredSpanJob(clock=lambda: 10**15, top_k=8, strict=False)
+    hdeps = hjob.run(host_batches)
+    djob = StoredSpanJob(clock=lambda: 10**15, top_k=8, strict=False)
+    ddeps = djob.run_device(dev)
+    assert _by_name(ddeps) == _by_name(hdeps)
+    assert djob.top_kv == hjob.top_kv and djob.top_annotations == hjob.top_annotations
+    assert sum(len(v) for v in djob.top_kv.values()) > 20
 
 
 def test_aggregate_job_on_device_row_batches(gpu):

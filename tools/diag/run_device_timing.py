@@ -30,11 +30,12 @@ def main():
     torch.cuda.synchronize()
     job = StoredSpanJob(clock=lambda: 10**15, max_services=S)
     job.run_device(dev[:1])
-    for _ in range(2):
-        t0 = time.perf_counter()
-        job.run_device(dev)
-        print(f"run_device: {len(cols)} fragments, {len(dev)} batches: {(time.perf_counter() - t0) * 1e3:.1f} ms",
-              flush=True)
+    for indexer in (False, True, False, True):
+        for _ in range(2):
+            t0 = time.perf_counter()
+            job.run_device(dev, indexer=indexer)
+            print(f"run_device(indexer={indexer}): {len(cols)} fragments, {len(dev)} batches: "
+                  f"{(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
 
     # the phases, by hand, on one stream (as run_device)
     stream = torch.cuda.Stream()

@@ -679,7 +679,8 @@ class StoredSpanJob:
     batch k runs on the device -- the dependency job (ZipkinAggregateJob.scala:20-43, accumulated with
     ZK_BATCH_TRACE_CLUSTERED | ZK_BATCH_CONTINUES) and one count-min + top-K sketch each for
     binary-annotation keys and non-core annotation values. run_device() takes fragments already in
-    HBM through the device decoder (dependencies only: that decoder emits no indexer items).
+    HBM through the device decoder, which emits the same indexer items on the device
+    (zk_ingest_dev_spans_items; indexer=False: dependencies only, the decoder's faster build).
     Output, through `aggregates`: storeDependencies, storeTopKeyValueAnnotations and
     storeTopAnnotations per service (Aggregates.scala:31-36).
 
@@ -773,20 +774,29 @@ class StoredSpanJob:
                 self.aggregates.storeTopAnnotations(name, values)
         return deps
 
-    def run_device(self, batches) -> Optional[Dependencies]:
+    def run_device(self, batches, *, indexer: bool = True) -> Optional[Dependencies]:
         """batches: (buf uint8, offsets int64[n + 1], n) torch tensors already in HBM, in row order.
-        Decoded on the device into a reused column buffer and accumulated on the same stream."""
+        Decoded on the device into a reused column buffer and accumulated on the same stream; with
+        `indexer` the decoder's items feed the two count-min + top-K sketches as in run()."""
+        import contextlib
+
         import torch
 
         from .context import DepsContext
         from .ingest import DeviceSpanDecoder
+        from .kv import KvSketch
 
         S = self.max_services
         self.rejected = 0
         stream = torch.cuda.Stream(device=self.device)
         dec = DeviceSpanDecoder(max(4096, S), device=self.device, stream=stream.cuda_stream)
+        width = self.kv_width or 4096
         try:
-            with DepsContext(S, device=self.device, strict=self.strict, stream=stream.cuda_stream) as ctx:
+            with DepsContext(S, device=self.device, strict=self.strict, stream=stream.cuda_stream) as ctx, \
+                    (KvSketch(S, device=self.device, stream=stream.cuda_stream, width=width, seed=self.seed) if indexer
+                     else contextlib.nullcontext()) as kvs, \
+                    (KvSketch(S, device=self.device, stream=stream.cuda_stream, width=width, seed=self.seed) if indexer
+                     else contextlib.nullcontext()) as anns:
                 cols = None
                 for buf, off, n in batches:
                     # the caller's tensors may still be in flight on its current stream (a
@@ -798,12 +808,31 @@ class StoredSpanJob:
                     off.record_stream(stream)
                     if cols is not None and cols.capacity < n:
                         cols = None
-                    cols, rej = dec.decode_device(buf, off, n, snappy=self.snappy, strict=self.strict, out=cols)
+                    if indexer:
+                        cols, rej, (ks, kh), (as_, ah) = dec.decode_device(
+                            buf, off, n, snappy=self.snappy, strict=self.strict, out=cols, items=True)
+                    else:
+                        cols, rej = dec.decode_device(buf, off, n, snappy=self.snappy, strict=self.strict, out=cols)
                     self.rejected += rej
                     ctx.accumulate(cols, clustered=True, continues=True, verify=self.verify)
-                deps = self._finish(ctx, dec.service_names())
+                    if indexer:
+                        if len(ks):
+                            kvs.accumulate(ks, kh)
+                        if len(as_):
+                            anns.accumulate(as_, ah)
+                names = dec.service_names()
+                deps = self._finish(ctx, names)
+                if indexer:
+                    self.top_kv = self._tops(dec, kvs, len(names))
+                    self.top_annotations = self._tops(dec, anns, len(names))
         finally:
             dec.close()
-        if self.aggregates is not None and deps is not None:
-            self.aggregates.storeDependencies(deps)
+        if self.aggregates is not None:
+            if deps is not None:
+                self.aggregates.storeDependencies(deps)
+            if indexer:
+                for name, keys in self.top_kv.items():
+                    self.aggregates.storeTopKeyValueAnnotations(name, keys)
+                for name, values in self.top_annotations.items():
+                    self.aggregates.storeTopAnnotations(name, values)
         return deps

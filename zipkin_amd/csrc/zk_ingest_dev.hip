@@ -24,6 +24,7 @@
 
 #include <hipcub/hipcub.hpp>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "zk_guard.h"
@@ -445,6 +446,32 @@ struct IngArgs {
     uint32_t d_mask;
     uint32_t max_services;
     const uint8_t* unknown;  // device copy of kUnknown
+    // ---- the span indexer's items (zk_ingest_dev_spans_items; items == 0: none) ----
+    uint32_t items;
+    uint32_t* kv_svc;            // item service: an id, or a reference resolved by k_ing_item_fixup
+    uint64_t* kv_key;
+    uint64_t kv_cap;
+    uint32_t* an_svc;
+    uint64_t* an_val;
+    uint64_t an_cap;
+    uint32_t* skip_kv;           // per fragment: items a failed attempt already appended
+    uint32_t* skip_an;
+    uint64_t* s_key;             // set of the key / value hashes whose strings are captured
+    uint32_t s_mask;
+    uint64_t* ns_hash;           // strings captured in this batch (hash, global bytes, length)
+    uint64_t* ns_ptr;
+    uint32_t* ns_len;
+    uint64_t ns_cap;
+    uint64_t* x_hash;            // item hosts not yet in the dictionary (published like a fragment's
+    uint64_t* x_ptr;             // service name; D3 / D4 run over them as over fragments)
+    uint32_t* x_len;
+    uint32_t* x_svc;
+    uint32_t* x_keep;
+    uint8_t* x_status;
+    uint32_t* x_list;
+    uint64_t x_cap;
+    unsigned long long* icnt;    // [0] kv items [1] annotation items [2] captured strings [3] extra names
+                                 // [4] attempts failed on a full string set
 };
 
 // A fragment's first bytes (its Snappy header varint is at most 5), issued as independent loads:
@@ -712,8 +739,10 @@ __device__ __forceinline__ bool fits(uint32_t avail, uint32_t at, int32_t len) {
     return len >= 0 && (uint64_t)avail >= (uint64_t)at + (uint32_t)len;
 }
 
+// lay (for the item walk): [0] the first annotation's offset, [1] their count, [2] the first binary
+// annotation's offset, [3] their count
 __device__ __forceinline__ int parse_record_fast(const IngArgs& a, uint64_t i, const lds_u8* base, uint32_t p0,
-                                                 uint32_t len, uint32_t* nm_off, uint32_t* nl_out) {
+                                                 uint32_t len, uint32_t* nm_off, uint32_t* nl_out, uint32_t lay[4]) {
     constexpr int kNo = -3;
     const uint32_t e = p0 + len;
     uint32_t p = p0;
@@ -738,6 +767,8 @@ __device__ __forceinline__ int parse_record_fast(const IngArgs& a, uint64_t i, c
     const uint32_t q2 = has_parent ? 30u : 19u;
     if (e - p < q2 || lh != fh(T_LIST, 6) || let != T_STRUCT || na < 0) return kNo;
     p += q2;
+    lay[0] = p;
+    lay[1] = (uint32_t)na;
     int64_t first = 0, last = 0;
     uint32_t nann = 0, cnt = 0;
     bool invalid = false, srv_set = false, cli_set = false;
@@ -805,6 +836,8 @@ __device__ __forceinline__ int parse_record_fast(const IngArgs& a, uint64_t i, c
         if (d.u8<3>() != T_STRUCT || nb < 0) return kNo;
         p += 8u;
     }
+    lay[2] = p;
+    lay[3] = (uint32_t)nb;
     for (int32_t k = 0; k < nb; ++k) {
         // [0B 0001] key [0B 0002] value [08 0003] annotation_type, then STOP or [0C 0004] endpoint STOP STOP
         LWin<2> k1;
@@ -916,53 +949,6 @@ __device__ __forceinline__ void publish_name(const IngArgs& a, uint64_t i, const
     for (uint64_t i = (uint64_t)blockIdx.x * kIngWG + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * kIngWG)
 #endif
 
-// D2 (global memory): a fragment marked `mode` (kStDefer by the LDS kernel, or kStNoScratch)
-__device__ __forceinline__ void ing_decode_one(const IngArgs& a, uint64_t i, uint32_t mode) {
-    if (a.status[i] != mode) return;
-    a.status[i] = kStOk;
-    a.keep[i] = 0u;
-    a.svc_hash[i] = 0ull;
-    const uint64_t b = a.offsets[i], e = a.offsets[i + 1];
-    const uint8_t* src = a.buf + b;
-    uint64_t len = e - b;
-    if (a.snappy) {
-        uint32_t h[5];
-        uint64_t raw;
-        head_bytes(a, true, b, e, h);
-        if (head_status(true, b, e, h, &raw) != kStOk) {  // (checked before it was deferred)
-            a.status[i] = kStUndecodable;
-            return;
-        }
-        uint8_t* dst = scratch_take(a, raw);
-        if (!dst) {
-            a.status[i] = kStNoScratch;
-            return;
-        }
-        if (!snappy_block(src, len, dst, raw)) {
-            a.status[i] = kStUndecodable;
-            return;
-        }
-        src = dst;
-        len = raw;
-    }
-    const uint8_t* nm;
-    uint32_t nl;
-    const int r = parse_record(a, i, src, len, &nm, &nl);
-    if (r < 0) return;
-    if (r) publish_name(a, i, nm, nl);
-    a.keep[i] = 1u;
-}
-
-// the deferred fragments (the LDS decoder's list), or every fragment marked kStNoScratch
-__global__ __launch_bounds__(kIngWG) void k_ing_decode(IngArgs a, uint32_t mode) {
-    if (mode == kStDefer) {
-        ING_FOR_LIST(a.def, a.def_n, i) ing_decode_one(a, i, mode);
-    } else {
-        for (uint64_t i = (uint64_t)blockIdx.x * kIngWG + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * kIngWG)
-            ing_decode_one(a, i, mode);
-    }
-}
-
 // A name the dictionary already holds (an id assigned by an earlier batch) resolves right here:
 // the slot of its hash, its bytes compared exactly with the arena's. svc_hash stays 0, so D3/D4
 // skip the fragment. Anything else (a new name, a hash collision, an id out of range) is published
@@ -1002,7 +988,8 @@ __device__ __forceinline__ bool try_resolve(const IngArgs& a, uint64_t i, const 
 // name's first 16 bytes are loaded once (hashed and compared from registers), and the first probe
 // reads the slot's key, id, length and inline name bytes together. *h: the name's hash (for
 // publish_name when it does not resolve).
-__device__ __forceinline__ bool resolve16(const IngArgs& a, uint64_t i, const uint8_t* nm, uint32_t nl, uint64_t* h_out) {
+__device__ __forceinline__ bool resolve16_id(const IngArgs& a, const uint8_t* nm, uint32_t nl, uint64_t* h_out,
+                                             uint32_t* id_out) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     uint8_t u[16];
 #pragma unroll
@@ -1063,6 +1050,13 @@ __device__ __forceinline__ bool resolve16(const IngArgs& a, uint64_t i, const ui
             if (!e2) return false;
         }
     }
+    *id_out = id;
+    return true;
+}
+
+__device__ __forceinline__ bool resolve16(const IngArgs& a, uint64_t i, const uint8_t* nm, uint32_t nl, uint64_t* h_out) {
+    uint32_t id;
+    if (!resolve16_id(a, nm, nl, h_out, &id)) return false;
     a.svc[i] = id;
     return true;
 }
@@ -1074,6 +1068,440 @@ __device__ __forceinline__ void publish_name_h(const IngArgs& a, uint64_t i, con
 #if ZK_ING_LISTS
     list_add(a.pub, a.pub_n, i);
 #endif
+}
+
+// ---- the span indexer's items (zk_ingest_dev_spans_items) ---------------------------------------
+// CassieSpanStore.scala:214-242 as the host decoder restates it (zk_ingest.cpp, "indexer items"):
+// only a span with an annotation is indexed; one key-value item per binary annotation with a host
+// (that host's service, the key's hash); one annotation item per distinct non-core annotation value,
+// from the group's minimum under Annotation.compare ((a.timestamp - b.timestamp).toInt, the first of
+// equals kept, Annotation.scala:36-38), and only if that annotation has a host. Items are appended
+// in any order (the sketches take a batch as a set). An item's service is resolved after D4: a host
+// whose name is the fragment's own service refers to the fragment (kRefFrag), a name the dictionary
+// holds resolves at once, a new one is published like a service name (kRefExtra: the extra list,
+// which D3 / D4 run over as over fragments). A string whose hash is not in the captured set is
+// copied out (scratch) and listed for the host, which keeps the hash -> string map.
+// An attempt that runs out of scratch (or finds the set / extra list full) fails its fragment
+// (kStNoScratch, decoded again after the host grows them); the items it appended stay, and
+// skip_kv / skip_an tell the next attempt to pass over them (each kind is emitted in a fixed order).
+constexpr uint32_t kRefFrag = 0x80000000u, kRefExtra = 0xC0000000u, kRefMask = 0x3FFFFFFFu;
+constexpr uint32_t kUnknownLen = sizeof(kUnknown) - 1;
+
+struct ItemState {
+    uint32_t seen[2];  // this fragment's items handled so far ([0] key-value, [1] annotation)
+    uint32_t skip[2];  // appended by an earlier attempt
+    bool fail;
+};
+
+__device__ __forceinline__ bool bytes_eq(const uint8_t* x, const uint8_t* y, uint32_t l) {
+    for (uint32_t q = 0; q < l; ++q)
+        if (x[q] != y[q]) return false;
+    return true;
+}
+
+// global bytes for a string the set or the dictionary keeps: g itself, else a scratch copy
+__device__ __forceinline__ const uint8_t* global_copy(const IngArgs& a, const uint8_t* s, uint32_t l, const uint8_t* g) {
+    if (g || l == 0) return g ? g : a.unknown;
+    uint8_t* d = scratch_take(a, l);
+    if (!d) return nullptr;
+#pragma clang loop vectorize(disable)
+    for (uint32_t q = 0; q < l; ++q) d[q] = s[q];
+    return d;
+}
+
+// the key / value hash into the captured set (one probe when it is known); a probe run longer than
+// kSetProbes counts as a full set (the host grows it: the set is kept at most half full between batches)
+constexpr uint32_t kSetProbes = 256;
+__device__ bool capture_string(const IngArgs& a, uint64_t h, const uint8_t* s, uint32_t l, const uint8_t* g) {
+    uint32_t slot = (uint32_t)h & a.s_mask;
+    const uint8_t* ptr = nullptr;
+    for (uint32_t step = 0; step < kSetProbes && step <= a.s_mask; ++step) {
+        const uint64_t k = a.s_key[slot];
+        if (k == h) return true;
+        if (k == kEmpty) {
+            if (!ptr && !(ptr = global_copy(a, s, l, g))) return false;  // scratch exhausted
+            const unsigned long long old =
+                atomicCAS((unsigned long long*)&a.s_key[slot], (unsigned long long)kEmpty, (unsigned long long)h);
+            if (old == kEmpty) {
+                const unsigned long long x = atomicAdd(&a.icnt[2], 1ull);  // < ns_cap: one entry per slot
+                if (x < a.ns_cap) {
+                    a.ns_hash[x] = h;
+                    a.ns_ptr[x] = (uint64_t)(uintptr_t)ptr;
+                    a.ns_len[x] = l;
+                }
+                return true;
+            }
+            if (old == h) return true;
+        }
+        slot = (slot + 1) & a.s_mask;
+    }
+    atomicAdd(&a.icnt[4], 1ull);  // the set is full
+    return false;
+}
+
+// an item host's service (nm / nl: the effective name, g: its global bytes or null)
+__device__ bool item_service(const IngArgs& a, uint64_t i, const uint8_t* nm, uint32_t nl, const uint8_t* g,
+                             const uint8_t* snm, uint32_t snl, bool snamed, uint32_t* enc) {
+    if (snamed && nl == snl && bytes_eq(nm, snm, nl)) {
+        *enc = kRefFrag | (uint32_t)i;
+        return true;
+    }
+    uint64_t h;
+    uint32_t id;
+    if (resolve16_id(a, nm, nl, &h, &id)) {
+        *enc = id;
+        return true;
+    }
+    const uint8_t* ptr = global_copy(a, nm, nl, g);
+    if (!ptr) return false;
+    const unsigned long long x = atomicAdd(&a.icnt[3], 1ull);
+    if (x >= a.x_cap) return false;  // the extra list is full (the host sees the count past x_cap)
+    a.x_hash[x] = h;
+    a.x_ptr[x] = (uint64_t)(uintptr_t)ptr;
+    a.x_len[x] = nl;
+    a.x_keep[x] = 1u;
+    a.x_status[x] = kStOk;
+    a.x_list[x] = (uint32_t)x;
+    *enc = kRefExtra | (uint32_t)x;
+    return true;
+}
+
+// one atomic per wave: the active lanes take consecutive items of `kind`
+__device__ __forceinline__ void item_append(const IngArgs& a, uint32_t kind, uint32_t enc, uint64_t h) {
+    const unsigned long long mask = __ballot(1);
+    const uint32_t lane = __lane_id();
+    const uint32_t leader = (uint32_t)__ffsll(mask) - 1u;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(&a.icnt[kind], (unsigned long long)__popcll(mask));
+    base = __shfl(base, (int)leader);
+    const uint64_t pos = base + (uint64_t)__popcll(mask & ((1ull << lane) - 1ull));
+    if (kind == 0) {
+        if (pos < a.kv_cap) {
+            a.kv_svc[pos] = enc;
+            a.kv_key[pos] = h;
+        }
+    } else if (pos < a.an_cap) {
+        a.an_svc[pos] = enc;
+        a.an_val[pos] = h;
+    }
+}
+
+// one item: its host's name (hl == 0: absent or "", i.e. kUnknown), its key / value string, and the
+// global copies of both (null: in LDS only); snm / snl / snamed: the fragment's own service
+__device__ void item_emit(const IngArgs& a, uint64_t i, ItemState& st, uint32_t kind, const uint8_t* hn, uint32_t hl,
+                          const uint8_t* hg, const uint8_t* s, uint32_t sl, const uint8_t* sg, const uint8_t* snm,
+                          uint32_t snl, bool snamed) {
+    if (st.fail) return;
+    if (st.seen[kind] < st.skip[kind]) {
+        ++st.seen[kind];
+        return;
+    }
+    if (hl == 0) {
+        hn = a.unknown;
+        hg = a.unknown;
+        hl = kUnknownLen;
+    }
+    const uint64_t h = d_hash(s, sl);
+    uint32_t enc;
+    if (!capture_string(a, h, s, sl, sg) || !item_service(a, i, hn, hl, hg, snm, snl, snamed, &enc)) {
+        st.fail = true;
+        return;
+    }
+    item_append(a, kind, enc, h);
+    ++st.seen[kind];
+}
+
+// -- the canonical layout (parse_record_fast accepted the span; lay: its list offsets and counts) --
+struct FAnn {
+    int64_t ts;
+    uint32_t next, voff, vl, vc, hoff, hl;
+    bool host;
+};
+__device__ __forceinline__ void fast_ann(const lds_u8* base, uint32_t p, FAnn& A) {
+    LWin<6> c;  // [0A 0001] timestamp [0B 0002] value
+    c.load(base, p);
+    A.ts = (int64_t)c.be64<3>();
+    A.vl = c.be32<14>();
+    A.vc = c.raw32<18>() & 0xFFFFu;
+    A.voff = p + 18u;
+    const uint32_t q = p + 18u + A.vl;
+    LWin<6> h;  // STOP, or [0C 0003] {[08 0001] ipv4 [06 0002] port [0B 0003] service_name} STOP STOP
+    h.load(base, q);
+    A.host = h.u8<0>() != T_STOP;
+    A.hl = A.host ? h.be32<18>() : 0u;
+    A.hoff = q + 22u;
+    A.next = A.host ? q + 24u + A.hl : q + 1u;
+}
+__device__ __forceinline__ bool fast_core(const FAnn& A) {
+    const uint32_t c0 = A.vc & 0xFFu, c1 = A.vc >> 8;
+    return A.vl == 2u && ((c0 == 'c' && (c1 == 's' || c1 == 'r')) || (c0 == 's' && (c1 == 'r' || c1 == 's')));
+}
+
+// gb: base as a generic pointer; gx: the global address of base offset 0 (0: the bytes are in LDS only)
+__device__ void items_fast(const IngArgs& a, uint64_t i, ItemState& st, const lds_u8* base, const uint32_t lay[4],
+                           uintptr_t gx, const uint8_t* snm, uint32_t snl, bool snamed) {
+    if (lay[1] == 0u) return;  // not indexed (CassieSpanStore.scala:214-218)
+    const uint8_t* gb = (const uint8_t*)base;
+    auto G = [&](uint32_t off) -> const uint8_t* { return gx ? (const uint8_t*)(gx + off) : nullptr; };
+    uint32_t p = lay[0];
+    for (uint32_t k = 0; k < lay[1] && !st.fail; ++k) {
+        FAnn A;
+        fast_ann(base, p, A);
+        if (!fast_core(A)) {
+            bool rep = true;  // the first of its value?
+            uint32_t q = lay[0];
+            for (uint32_t j = 0; j < k; ++j) {
+                FAnn B;
+                fast_ann(base, q, B);
+                if (!fast_core(B) && B.vl == A.vl && bytes_eq(gb + B.voff, gb + A.voff, A.vl)) {
+                    rep = false;
+                    break;
+                }
+                q = B.next;
+            }
+            if (rep) {
+                FAnn M = A;  // the group's minimum
+                q = A.next;
+                for (uint32_t j = k + 1; j < lay[1]; ++j) {
+                    FAnn B;
+                    fast_ann(base, q, B);
+                    if (!fast_core(B) && B.vl == A.vl && (int32_t)(uint32_t)((uint64_t)M.ts - (uint64_t)B.ts) > 0 &&
+                        bytes_eq(gb + B.voff, gb + A.voff, A.vl))
+                        M = B;
+                    q = B.next;
+                }
+                if (M.host)
+                    item_emit(a, i, st, 1u, gb + M.hoff, M.hl, G(M.hoff), gb + A.voff, A.vl, G(A.voff), snm, snl, snamed);
+            }
+        }
+        p = A.next;
+    }
+    p = lay[2];
+    for (uint32_t k = 0; k < lay[3] && !st.fail; ++k) {
+        // [0B 0001] key [0B 0002] value [08 0003] annotation_type, then STOP or [0C 0004] endpoint STOP STOP
+        LWin<2> k1;
+        k1.load(base, p);
+        const uint32_t kl = k1.be32<3>(), koff = p + 7u;
+        LWin<2> k2;
+        k2.load(base, koff + kl);
+        const uint32_t p3 = koff + kl + 7u + k2.be32<3>();
+        LWin<8> k3;
+        k3.load(base, p3);
+        const bool host = k3.u8<7>() != T_STOP;
+        const uint32_t hl = host ? k3.be32<25>() : 0u, hoff = p3 + 29u;
+        if (host) item_emit(a, i, st, 0u, gb + hoff, hl, G(hoff), gb + koff, kl, G(koff), snm, snl, snamed);
+        p = host ? p3 + 31u + hl : p3 + 8u;
+    }
+}
+
+// -- any layout (the generic walk accepted the span): the host decoder's read_span semantics --
+template <class P>
+struct GAnn {
+    int64_t ts;
+    P v;  // null: no value field
+    uint32_t vl;
+    bool host;
+    P hn;  // null: the host has no service_name field
+    uint32_t hl;
+};
+template <class P>
+struct GBann {
+    P k;
+    uint32_t kl;
+    bool host;
+    P hn;
+    uint32_t hl;
+};
+// the annotations (field 6 lists) or binary annotations (field 8 lists) of a span, in order
+template <class P>
+struct GItemIter {
+    DRdT<P> r;
+    int32_t left;
+    int16_t list_id;
+    __device__ bool next_elem() {  // positions r at the next element of a list_id list of structs
+        for (;;) {
+            if (left > 0) {
+                --left;
+                return true;
+            }
+            uint8_t t;
+            int16_t fid;
+            if (!r.field(&t, &fid)) return false;
+            if (fid == list_id && t == T_LIST) {
+                const uint8_t et = r.u8();
+                const int32_t c = r.i32();
+                if (!r.ok || c < 0) return false;
+                if (et == T_STRUCT)
+                    left = c;
+                else
+                    for (int32_t q = 0; r.ok && q < c; ++q) skip_flat(r, et);
+            } else {
+                skip_flat(r, t);
+            }
+            if (!r.ok) return false;
+        }
+    }
+    __device__ bool next(GAnn<P>& A) {
+        if (!next_elem()) return false;
+        A.ts = 0;
+        A.v = nullptr;
+        A.vl = 0;
+        A.host = false;
+        A.hn = nullptr;
+        A.hl = 0;
+        for (;;) {
+            uint8_t at;
+            int16_t aid;
+            if (!r.field(&at, &aid)) break;
+            if (aid == 1 && at == T_I64)
+                A.ts = r.i64();
+            else if (aid == 2 && at == T_STRING)
+                r.str(&A.v, &A.vl);
+            else if (aid == 3 && at == T_STRUCT) {
+                A.host = true;
+                read_endpoint(r, &A.hn, &A.hl);
+            } else
+                skip_flat(r, at);
+        }
+        return r.ok;
+    }
+    __device__ bool next(GBann<P>& B) {
+        if (!next_elem()) return false;
+        B.k = nullptr;
+        B.kl = 0;
+        B.host = false;
+        B.hn = nullptr;
+        B.hl = 0;
+        for (;;) {
+            uint8_t bt;
+            int16_t bid;
+            if (!r.field(&bt, &bid)) break;
+            if (bid == 1 && bt == T_STRING)
+                r.str(&B.k, &B.kl);
+            else if (bid == 4 && bt == T_STRUCT) {
+                B.host = true;
+                read_endpoint(r, &B.hn, &B.hl);
+            } else
+                skip_flat(r, bt);
+        }
+        return r.ok;
+    }
+};
+
+template <class P>
+__device__ __forceinline__ bool g_same_value(const GAnn<P>& A, const GAnn<P>& B) {
+    if ((A.v == nullptr) != (B.v == nullptr) || A.vl != B.vl) return false;
+    return A.v == nullptr || A.vl == 0 || bytes_eq((const uint8_t*)A.v, (const uint8_t*)B.v, A.vl);
+}
+
+// gsrc: the global address of src (null: src is in LDS only)
+template <class P>
+__device__ void items_generic(const IngArgs& a, uint64_t i, ItemState& st, P src, uint64_t len, const uint8_t* gsrc,
+                              const uint8_t* snm, uint32_t snl, bool snamed) {
+    auto G = [&](P p) -> const uint8_t* { return gsrc ? gsrc + (p - src) : nullptr; };
+    GItemIter<P> o{DRdT<P>{src, src + len, true}, 0, 6};
+    GAnn<P> A, B;
+    {
+        GItemIter<P> z = o;
+        if (!z.next(A)) return;  // no annotation: not indexed
+    }
+    int c;
+    for (uint32_t k = 0; !st.fail && o.next(A); ++k) {
+        if (is_core(A.v, A.vl, &c)) continue;
+        bool rep = true;
+        GItemIter<P> e{DRdT<P>{src, src + len, true}, 0, 6};
+        for (uint32_t j = 0; j < k && e.next(B); ++j)
+            if (!is_core(B.v, B.vl, &c) && g_same_value(A, B)) {
+                rep = false;
+                break;
+            }
+        if (!rep) continue;
+        GAnn<P> M = A;
+        GItemIter<P> l = o;
+        while (l.next(B))
+            if (!is_core(B.v, B.vl, &c) && g_same_value(A, B) &&
+                (int32_t)(uint32_t)((uint64_t)M.ts - (uint64_t)B.ts) > 0)
+                M = B;
+        if (!M.host) continue;
+        const bool hv = M.hn != nullptr && M.hl > 0;
+        const bool vv = A.v != nullptr && A.vl > 0;
+        item_emit(a, i, st, 1u, hv ? (const uint8_t*)M.hn : nullptr, hv ? M.hl : 0u, hv ? G(M.hn) : nullptr,
+                  vv ? (const uint8_t*)A.v : a.unknown, vv ? A.vl : 0u, vv ? G(A.v) : a.unknown, snm, snl, snamed);
+    }
+    GItemIter<P> b{DRdT<P>{src, src + len, true}, 0, 8};
+    GBann<P> K;
+    while (!st.fail && b.next(K)) {
+        if (!K.host) continue;
+        const bool hv = K.hn != nullptr && K.hl > 0;
+        const bool kv = K.k != nullptr && K.kl > 0;
+        item_emit(a, i, st, 0u, hv ? (const uint8_t*)K.hn : nullptr, hv ? K.hl : 0u, hv ? G(K.hn) : nullptr,
+                  kv ? (const uint8_t*)K.k : a.unknown, kv ? K.kl : 0u, kv ? G(K.k) : a.unknown, snm, snl, snamed);
+    }
+}
+
+__device__ __forceinline__ void items_failed(const IngArgs& a, uint64_t i, const ItemState& st) {
+    a.status[i] = kStNoScratch;
+    a.skip_kv[i] = st.seen[0];
+    a.skip_an[i] = st.seen[1];
+}
+
+// D2 (global memory): a fragment marked `mode` (kStDefer by the LDS kernel, or kStNoScratch)
+template <bool kItems>
+__device__ __forceinline__ void ing_decode_one(const IngArgs& a, uint64_t i, uint32_t mode) {
+    if (a.status[i] != mode) return;
+    a.status[i] = kStOk;
+    a.keep[i] = 0u;
+    a.svc_hash[i] = 0ull;
+    const uint64_t b = a.offsets[i], e = a.offsets[i + 1];
+    const uint8_t* src = a.buf + b;
+    uint64_t len = e - b;
+    if (a.snappy) {
+        uint32_t h[5];
+        uint64_t raw;
+        head_bytes(a, true, b, e, h);
+        if (head_status(true, b, e, h, &raw) != kStOk) {  // (checked before it was deferred)
+            a.status[i] = kStUndecodable;
+            return;
+        }
+        uint8_t* dst = scratch_take(a, raw);
+        if (!dst) {
+            a.status[i] = kStNoScratch;
+            return;
+        }
+        if (!snappy_block(src, len, dst, raw)) {
+            a.status[i] = kStUndecodable;
+            return;
+        }
+        src = dst;
+        len = raw;
+    }
+    const uint8_t* nm;
+    uint32_t nl;
+    const int r = parse_record(a, i, src, len, &nm, &nl);
+    if (r < 0) return;
+    if (r) publish_name(a, i, nm, nl);
+    if constexpr (kItems) {  // a deferred fragment's first attempt (skips 0), or a failed one's next
+        ItemState st{{0u, 0u}, {a.skip_kv[i], a.skip_an[i]}, false};
+        items_generic(a, i, st, src, len, src, nm, nl, r == 1);
+        if (st.fail) {
+            items_failed(a, i, st);
+            return;
+        }
+    }
+    a.keep[i] = 1u;
+}
+
+// the deferred fragments (the LDS decoder's list), or every fragment marked kStNoScratch
+// kItems: the items build of the decoders (zk_ingest_dev_spans_items), compiled apart so that the
+// records-only kernels keep their registers
+template <bool kItems>
+__global__ __launch_bounds__(kIngWG) void k_ing_decode(IngArgs a, uint32_t mode) {
+    if (mode == kStDefer) {
+        ING_FOR_LIST(a.def, a.def_n, i) ing_decode_one<kItems>(a, i, mode);
+    } else {
+        for (uint64_t i = (uint64_t)blockIdx.x * kIngWG + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * kIngWG)
+            ing_decode_one<kItems>(a, i, mode);
+    }
 }
 
 // D2 (LDS): one wave per block of a.lds_block consecutive fragments, in rounds. A round takes the
@@ -1348,7 +1776,9 @@ __device__ __forceinline__ uint32_t copy_blocks(const uint8_t* buf, uint64_t b, 
     return h && e > b ? (uint32_t)((e - b + mis + 15) >> 4) : 0u;
 }
 
+template <bool kItems>
 __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
+    constexpr bool kPre = ZK_ING_PREFETCH && !kItems;  // (the items build has no registers for it)
     __shared__ __align__(16) uint8_t s_buf[kLdsBudget];
     const uint32_t lane = threadIdx.x;
     const uint64_t blk0 = (uint64_t)blockIdx.x * a.lds_block;
@@ -1360,16 +1790,14 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
     uint64_t nb = nh ? a.offsets[blk0 + lane] : 0, ne = nh ? a.offsets[blk0 + lane + 1] : 0;
     uint32_t hb[5];
     head_bytes(a, nh, nb, ne, hb);
-#if ZK_ING_PREFETCH
     ing_u32x4 pre[kPreBlk];
-    {
+    if constexpr (kPre) {
         ing_g_u32x4* pg;
         const uint32_t pn = copy_blocks(a.buf, nb, ne, nh, &pg);
 #pragma unroll
         for (int c = 0; c < kPreBlk; ++c)
             if ((uint32_t)c < pn) pre[c] = pg[c];
     }
-#endif
     for (uint64_t f0 = blk0; f0 < blk1;) {  // uniform
         const uint64_t i = f0 + lane;
         const bool have = i < blk1;
@@ -1425,6 +1853,10 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
         if (lane < k && have) {
             a.keep[i] = 0u;
             a.svc_hash[i] = 0ull;
+            if constexpr (kItems) {
+                a.skip_kv[i] = 0u;
+                a.skip_an[i] = 0u;
+            }
             a.status[i] = st == kStOk && !fits ? kStDefer : st;
 #if ZK_ING_LISTS
             if (st == kStOk && !fits) list_add(a.def, a.def_n, i);
@@ -1438,26 +1870,24 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                 ing_g_u32x4* g = (ing_g_u32x4*)((uintptr_t)(a.buf + b) & ~(uintptr_t)15);
                 const uint32_t nblk = (uint32_t)((clen + mis + 15) >> 4);
                 ing_u32x4* dst = reinterpret_cast<ing_u32x4*>(reg + D - mis);
-#if ZK_ING_PREFETCH
+                if constexpr (kPre) {
 #pragma unroll
-                for (int c = 0; c < kPreBlk; ++c)
-                    if ((uint32_t)c < nblk) dst[c] = pre[c];
-                for (uint32_t c = kPreBlk; c < nblk; ++c) dst[c] = g[c];
-#else
-                for (uint32_t c = 0; c < nblk; ++c) dst[c] = g[c];
-#endif
+                    for (int c = 0; c < kPreBlk; ++c)
+                        if ((uint32_t)c < nblk) dst[c] = pre[c];
+                    for (uint32_t c = kPreBlk; c < nblk; ++c) dst[c] = g[c];
+                } else {
+                    for (uint32_t c = 0; c < nblk; ++c) dst[c] = g[c];
+                }
             }
         }
         head_bytes(a, nh, nb, ne, hb);  // the next round's headers, in flight during this round's decode
-#if ZK_ING_PREFETCH
-        {
+        if constexpr (kPre) {
             ing_g_u32x4* pg;
             const uint32_t pn = copy_blocks(a.buf, nb, ne, nh, &pg);
 #pragma unroll
             for (int c = 0; c < kPreBlk; ++c)
                 if ((uint32_t)c < pn) pre[c] = pg[c];
         }
-#endif
         if (go) {
             ING_STAMP(1);
             // the region as an LDS pointer: the decoder's byte and word reads become ds_read_*.
@@ -1487,8 +1917,9 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
             } else {
                 const lds_u8* const lbase = (const lds_u8*)s_buf;
                 const uint32_t p0 = (uint32_t)(src - lbase);
-                uint32_t nmo, nl;
-                int r = parse_record_fast(a, i, lbase, p0, (uint32_t)len, &nmo, &nl);
+                uint32_t nmo, nl, lay[4];
+                int r = parse_record_fast(a, i, lbase, p0, (uint32_t)len, &nmo, &nl, lay);
+                const bool fast = r != -3;
                 if (r == -3) {  // not the canonical layout: the generic walk
                     const uint8_t* gnm = nullptr;
                     r = parse_record(a, i, src, len, &gnm, &nl);
@@ -1527,6 +1958,19 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
 #else
                         if (r >= 0) publish_name(a, i, nm, nl);
 #endif
+                    }
+                    if (kItems && r >= 0) {
+                        // the global address of LDS offset 0 (thrift codec: the input buffer)
+                        const uintptr_t gx = a.snappy ? 0 : (uintptr_t)(a.buf + b) - p0;
+                        ItemState st{{0u, 0u}, {0u, 0u}, false};
+                        if (fast)
+                            items_fast(a, i, st, lbase, lay, gx, nm, nl, r == 1);
+                        else
+                            items_generic(a, i, st, src, len, gx ? (const uint8_t*)(gx + p0) : nullptr, nm, nl, r == 1);
+                        if (st.fail) {
+                            items_failed(a, i, st);
+                            r = -1;
+                        }
                     }
                     if (r >= 0) a.keep[i] = 1u;
                 }
@@ -1646,6 +2090,50 @@ __global__ void k_ing_count(const uint8_t* status, uint64_t n, unsigned long lon
     atomicMin(first_bad, (unsigned int)(i < 0xFFFFFFFFull ? i : 0xFFFFFFFEull));
 }
 
+// the extra names' D4 failures: [5] collisions, [6] more services than max_services
+// The extra names run through D3 / D4 as an IngArgs whose per-fragment arrays are the extra
+// list's (x.n = its capacity: the count may have run past it in a failed attempt)
+#define ING_FOR_EXTRA(x, i)                                                                        \
+    const uint64_t ing_m = *(x).pub_n < (x).n ? *(x).pub_n : (x).n;                                \
+    for (uint64_t ing_t = (uint64_t)blockIdx.x * kIngWG + threadIdx.x; ing_t < ing_m;             \
+         ing_t += (uint64_t)gridDim.x * kIngWG)                                                   \
+        if (const uint64_t i = (x).pub[ing_t]; true)
+
+__global__ __launch_bounds__(kIngWG) void k_ing_dict_insert_x(IngArgs x) {
+    ING_FOR_EXTRA(x, i) ing_insert_one(x, i);
+}
+__global__ __launch_bounds__(kIngWG) void k_ing_lookup_x(IngArgs x) {
+    ING_FOR_EXTRA(x, i) ing_lookup_one(x, i);
+}
+__global__ __launch_bounds__(kIngWG) void k_ing_count_extra(IngArgs x) {
+    ING_FOR_EXTRA(x, i) {
+        const uint8_t s = x.status[i];
+        if (s == kStCollision) atomicAdd(&x.icnt[5], 1ull);
+        if (s == kStRange) atomicAdd(&x.icnt[6], 1ull);
+    }
+}
+
+// item service references -> dictionary ids (after D4 of the fragments and the extra names; a.svc
+// still holds the records at their fragment index)
+__global__ __launch_bounds__(kIngWG) void k_ing_item_fixup(IngArgs a, uint64_t nkv, uint64_t nan) {
+    for (uint64_t t = (uint64_t)blockIdx.x * kIngWG + threadIdx.x; t < nkv + nan; t += (uint64_t)gridDim.x * kIngWG) {
+        uint32_t* sv = t < nkv ? &a.kv_svc[t] : &a.an_svc[t - nkv];
+        const uint32_t v = *sv;
+        if (v & kRefFrag) *sv = (v & (kRefExtra & ~kRefFrag)) ? a.x_svc[v & kRefMask] : a.svc[v & kRefMask];
+    }
+}
+
+// the captured-string set into a larger table (keys are distinct)
+__global__ void k_ing_set_rehash(const uint64_t* __restrict__ old, uint64_t n_old, uint64_t* nw, uint32_t mask) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_old) return;
+    const uint64_t k = old[t];
+    if (k == kEmpty) return;
+    uint32_t slot = (uint32_t)k & mask;
+    while (atomicCAS((unsigned long long*)&nw[slot], (unsigned long long)kEmpty, (unsigned long long)k) != kEmpty)
+        slot = (slot + 1) & mask;
+}
+
 }  // namespace
 }  // namespace zk
 
@@ -1677,8 +2165,18 @@ struct zk_ingest_dev {
     void* cub = nullptr;
     size_t cub_cap = 0;
     unsigned long long* counts = nullptr;  // [8] per status, [8] first_bad, [10] scratch bytes taken,
-                                           // [11] / [12] published / deferred list lengths, [13] claims
-    unsigned long long* h_counts = nullptr;  // pinned host copy of counts[0..13]
+                                           // [11] / [12] published / deferred list lengths, [13] claims,
+                                           // [16..23) IngArgs::icnt (items)
+    unsigned long long* h_counts = nullptr;  // pinned host copy of counts[0..23)
+    // the span indexer's items (zk_ingest_dev_spans_items)
+    uint64_t* s_key = nullptr;  // the captured-string set (hashes), open addressing
+    uint32_t s_cap = 0;
+    uint64_t s_count = 0;
+    std::unordered_map<uint64_t, std::string> strings;  // hash -> the string first captured for it
+    uint8_t* ns = nullptr;      // this batch's captured strings: hash u64 [s_cap], ptr u64, len u32
+    uint64_t ns_cap = 0;
+    uint8_t* xs = nullptr;      // extra names: hash, ptr u64; len, svc, keep, list u32; status u8 [x_cap]
+    uint64_t x_cap = 0;
     std::string err;
 };
 
@@ -1737,8 +2235,8 @@ zk_status zk_ingest_dev_create(int32_t device, void* stream, uint32_t max_servic
     if (e == hipSuccess) e = hipMalloc(&g->d_name16, (uint64_t)t * 16);
     if (e == hipSuccess) e = hipMemsetAsync(g->d_name16, 0, (uint64_t)t * 16, g->stream);
     if (e == hipSuccess) e = hipMalloc(&g->arena, g->arena_cap);
-    if (e == hipSuccess) e = hipMalloc(&g->counts, 16 * 8);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&g->h_counts, 16 * 8, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc(&g->counts, 32 * 8);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&g->h_counts, 32 * 8, hipHostMallocDefault);
     if (e == hipSuccess) e = hipMemsetAsync(g->d_key, 0, (uint64_t)t * 8, g->stream);
     if (e == hipSuccess) e = hipMemsetAsync(g->d_id, 0xFF, (uint64_t)t * 4, g->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(g->arena, kUnknown, sizeof(kUnknown) - 1, hipMemcpyHostToDevice, g->stream);
@@ -1769,6 +2267,9 @@ zk_status zk_ingest_dev_destroy(zk_ingest_dev* g) {
     hipFree(g->batch);
     hipFree(g->scratch);
     hipFree(g->cub);
+    hipFree(g->s_key);
+    hipFree(g->ns);
+    hipFree(g->xs);
     if (g->own_stream && g->stream) hipStreamDestroy(g->stream);
     delete g;
     return ZK_OK;
@@ -1801,13 +2302,113 @@ int zk_debug_ing_stamps(unsigned long long* out, int reset) {
 }
 #endif
 
-zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* offsets, uint64_t n,
-                              uint32_t codec, uint32_t flags, const zk_span_cols* out, uint64_t* n_out,
-                              uint64_t* n_rejected) {
-    ZK_GUARD_BEGIN
+}  // extern "C"
+
+namespace {
+
+// the captured-string set at a larger capacity (the caller holds the stream)
+hipError_t grow_string_set(zk_ingest_dev* g, uint32_t cap) {
+    uint64_t* nk = nullptr;
+    hipError_t e = hipMalloc(&nk, (uint64_t)cap * 8);
+    if (e == hipSuccess) e = hipMemsetAsync(nk, 0, (uint64_t)cap * 8, g->stream);
+    if (e == hipSuccess && g->s_key)
+        e = launch_checked("k_ing_set_rehash", k_ing_set_rehash, dim3((g->s_cap + 255) / 256), dim3(256), 0, g->stream,
+                           (const uint64_t*)g->s_key, (uint64_t)g->s_cap, nk, cap - 1);
+    if (e == hipSuccess) e = hipStreamSynchronize(g->stream);
+    if (e != hipSuccess) {
+        hipFree(nk);
+        return e;
+    }
+    hipFree(g->s_key);
+    g->s_key = nk;
+    g->s_cap = cap;
+    return hipSuccess;
+}
+
+// the list of captured strings (one entry per set slot at most), its first `keep` entries kept
+hipError_t size_new_strings(zk_ingest_dev* g, uint64_t keep) {
+    if (g->ns_cap >= g->s_cap) return hipSuccess;
+    uint8_t* nn = nullptr;
+    const uint64_t c = g->s_cap;
+    hipError_t e = hipMalloc(&nn, c * 20);
+    if (e == hipSuccess && keep) {
+        e = hipMemcpyAsync(nn, g->ns, keep * 8, hipMemcpyDeviceToDevice, g->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(nn + c * 8, g->ns + g->ns_cap * 8, keep * 8, hipMemcpyDeviceToDevice, g->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(nn + c * 16, g->ns + g->ns_cap * 16, keep * 4, hipMemcpyDeviceToDevice, g->stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(g->stream);
+    if (e != hipSuccess) {
+        hipFree(nn);
+        return e;
+    }
+    hipFree(g->ns);
+    g->ns = nn;
+    g->ns_cap = c;
+    return hipSuccess;
+}
+
+// the extra-name list at capacity c, its first `keep` entries kept
+hipError_t size_extra(zk_ingest_dev* g, uint64_t c, uint64_t keep) {
+    uint8_t* nx = nullptr;
+    hipError_t e = hipMalloc(&nx, c * 33);
+    const uint64_t o = g->x_cap;
+    // layout: hash [c] u64, ptr [c] u64, len [c] u32, svc [c] u32, keep [c] u32, list [c] u32, status [c] u8
+    const uint64_t off_new[7] = {0, c * 8, c * 16, c * 20, c * 24, c * 28, c * 32};
+    const uint64_t off_old[7] = {0, o * 8, o * 16, o * 20, o * 24, o * 28, o * 32};
+    const uint64_t w[7] = {8, 8, 4, 4, 4, 4, 1};
+    for (int k = 0; k < 7 && e == hipSuccess && keep; ++k)
+        e = hipMemcpyAsync(nx + off_new[k], g->xs + off_old[k], keep * w[k], hipMemcpyDeviceToDevice, g->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(g->stream);
+    if (e != hipSuccess) {
+        hipFree(nx);
+        return e;
+    }
+    hipFree(g->xs);
+    g->xs = nx;
+    g->x_cap = c;
+    return hipSuccess;
+}
+
+void bind_items(zk_ingest_dev* g, IngArgs& a, IngArgs& x) {
+    a.s_key = g->s_key;
+    a.s_mask = g->s_cap - 1;
+    a.ns_hash = (uint64_t*)g->ns;
+    a.ns_ptr = (uint64_t*)(g->ns + g->ns_cap * 8);
+    a.ns_len = (uint32_t*)(g->ns + g->ns_cap * 16);
+    a.ns_cap = g->ns_cap;
+    const uint64_t c = g->x_cap;
+    a.x_hash = (uint64_t*)g->xs;
+    a.x_ptr = (uint64_t*)(g->xs + c * 8);
+    a.x_len = (uint32_t*)(g->xs + c * 16);
+    a.x_svc = (uint32_t*)(g->xs + c * 20);
+    a.x_keep = (uint32_t*)(g->xs + c * 24);
+    a.x_list = (uint32_t*)(g->xs + c * 28);
+    a.x_status = g->xs + c * 32;
+    a.x_cap = c;
+    // the extra names as "fragments" of D3 / D4
+    x = a;
+    x.n = c;
+    x.svc_hash = a.x_hash;
+    x.name_ptr = a.x_ptr;
+    x.name_len = a.x_len;
+    x.svc = a.x_svc;
+    x.keep = a.x_keep;
+    x.status = a.x_status;
+    x.pub = a.x_list;
+    x.pub_n = a.icnt + 3;
+}
+
+zk_status ingest_batch(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* offsets, uint64_t n, uint32_t codec,
+                       uint32_t flags, const zk_span_cols* out, uint64_t* n_out, uint64_t* n_rejected,
+                       zk_ingest_items* items) {
     if (!g || !n_out || !n_rejected) return ZK_ERR_INVALID_ARG;
     *n_out = *n_rejected = 0;
+    if (items) items->kv_n = items->ann_n = 0;
+    const bool want_kv = items && items->kv_service && items->kv_key && items->kv_cap;
+    const bool want_ann = items && items->ann_service && items->ann_value && items->ann_cap;
     if (n == 0) return ZK_OK;
+    if (items && n >= (1ull << 30)) return dfail(g, ZK_ERR_INVALID_ARG, "items: batch of 2^30 fragments or more");
     if (!buf || !offsets || !out || !out->trace_id || !out->span_id || !out->parent_id || !out->first_ts ||
         !out->last_ts || !out->service_id || !out->flags)
         return ZK_ERR_INVALID_ARG;
@@ -1816,7 +2417,7 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     ING_HIP(g, hipSetDevice(g->device));
     // per-fragment arrays: 8-byte columns first, then 4-byte, then 1-byte
     const uint64_t n1 = n + 1;
-    const uint64_t bytes = align256(8 * n1) * 8 + align256(4 * n1) * 7 + align256(n1);
+    const uint64_t bytes = align256(8 * n1) * 8 + align256(4 * n1) * 9 + align256(n1);
     if (bytes > g->batch_cap) {
         hipFree(g->batch);
         g->batch = nullptr;
@@ -1859,6 +2460,8 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     a.pos = (uint32_t*)take(4 * n1);
     a.pub = (uint32_t*)take(4 * n1);
     a.def = (uint32_t*)take(4 * n1);
+    a.skip_kv = (uint32_t*)take(4 * n1);
+    a.skip_an = (uint32_t*)take(4 * n1);
     a.status = take(n1);
     a.d_key = g->d_key;
     a.d_id = g->d_id;
@@ -1868,6 +2471,22 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     a.d_mask = g->table - 1;
     a.max_services = g->max_services;
     a.unknown = g->arena;
+    a.icnt = g->counts + 16;
+    IngArgs ax{};  // the extra names (items only)
+    if (items) {
+        a.items = 1;
+        a.kv_svc = want_kv ? items->kv_service : nullptr;
+        a.kv_key = want_kv ? items->kv_key : nullptr;
+        a.kv_cap = want_kv ? items->kv_cap : 0;
+        a.an_svc = want_ann ? items->ann_service : nullptr;
+        a.an_val = want_ann ? items->ann_value : nullptr;
+        a.an_cap = want_ann ? items->ann_cap : 0;
+        if (!g->s_key) ING_HIP(g, grow_string_set(g, 1u << 16));
+        while (g->s_count * 2 > g->s_cap) ING_HIP(g, grow_string_set(g, g->s_cap * 2));
+        ING_HIP(g, size_new_strings(g, 0));
+        if (!g->xs) ING_HIP(g, size_extra(g, 4096, 0));
+        ING_HIP(g, hipMemsetAsync(a.icnt, 0, 7 * 8, g->stream));
+    }
     const dim3 grid((unsigned)((n + kIngWG - 1) / kIngWG)), blk(kIngWG);
     const dim3 lgrid(std::min<unsigned>(grid.x, 2048u));  // the list kernels (grid-stride)
     hipStream_t s = g->stream;
@@ -1892,15 +2511,23 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     a.scratch = g->scratch;
     a.scratch_cap = g->scratch_cap;
     a.scratch_used = used;
+    if (items) bind_items(g, a, ax);  // (ax copies a: every field of a is set by now)
     // D1 + D2, D3
     // fragments per wave: 1024 once a batch gives ~4096 waves (2 per wave slot of 256 CUs x 8), else
     // the power of two that does, at least 128 (~2 rounds of a wave)
     a.lds_block = 128;
     while (a.lds_block < kLdsBlock && (uint64_t)a.lds_block * 4096 < n) a.lds_block <<= 1;
-    ING_HIP(g, launch_checked("k_ing_decode_lds", k_ing_decode_lds, dim3((unsigned)((n + a.lds_block - 1) / a.lds_block)),
-                              dim3(kLdsWG), 0, s, a));
-    ING_HIP(g, launch_checked("k_ing_decode", k_ing_decode, lgrid, blk, 0, s, a, (uint32_t)kStDefer));
+    const dim3 dgrid((unsigned)((n + a.lds_block - 1) / a.lds_block));
+    if (items) {
+        ING_HIP(g, launch_checked("k_ing_decode_lds", k_ing_decode_lds<true>, dgrid, dim3(kLdsWG), 0, s, a));
+        ING_HIP(g, launch_checked("k_ing_decode", k_ing_decode<true>, lgrid, blk, 0, s, a, (uint32_t)kStDefer));
+    } else {
+        ING_HIP(g, launch_checked("k_ing_decode_lds", k_ing_decode_lds<false>, dgrid, dim3(kLdsWG), 0, s, a));
+        ING_HIP(g, launch_checked("k_ing_decode", k_ing_decode<false>, lgrid, blk, 0, s, a, (uint32_t)kStDefer));
+    }
     ING_HIP(g, launch_checked("k_ing_dict_insert", k_ing_dict_insert, lgrid, blk, 0, s, a));
+    const dim3 xgrid(64);  // the extra-name list kernels (grid-stride; the list is short)
+    if (items) ING_HIP(g, launch_checked("k_ing_dict_insert_x", k_ing_dict_insert_x, xgrid, blk, 0, s, ax));
     // D4 and the status counts, then one small read: in the steady state (no scratch overflow, no
     // new service names) this is the batch's only host round trip
     unsigned long long* const hc = g->h_counts;
@@ -1911,28 +2538,54 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
         if (e == hipSuccess)
             e = launch_checked("k_ing_count", k_ing_count, grid, blk, 0, s, (const uint8_t*)a.status, n, g->counts,
                                (unsigned int*)(g->counts + 8));
-        if (e == hipSuccess) e = hipMemcpyAsync(hc, g->counts, 14 * 8, hipMemcpyDeviceToHost, s);
+        if (items) {
+            if (e == hipSuccess) e = launch_checked("k_ing_lookup_x", k_ing_lookup_x, xgrid, blk, 0, s, ax);
+            if (e == hipSuccess) e = hipMemsetAsync(a.icnt + 5, 0, 2 * 8, s);
+            if (e == hipSuccess) e = launch_checked("k_ing_count_extra", k_ing_count_extra, xgrid, blk, 0, s, ax);
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(hc, g->counts, (items ? 23 : 14) * 8, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         return e;
     };
     ING_HIP(g, lookup_and_count());
     std::vector<uint8_t*> retired;  // old arenas and scratch stay valid until this batch's lookups are done
-    if (hc[10] > g->scratch_cap || hc[13] > 0) {
-        while (hc[10] > g->scratch_cap) {
+    unsigned long long* const ic = hc + 16;  // the host copy of a.icnt
+    auto items_short = [&]() { return items && (ic[4] > 0 || ic[3] > g->x_cap); };
+    if (hc[10] > g->scratch_cap || hc[13] > 0 || items_short()) {
+        while (hc[10] > g->scratch_cap || items_short()) {
             // the scratch ran out (kStNoScratch fragments): a larger one, and those fragments again
-            uint64_t cap = 2 * g->scratch_cap;
-            if (cap < hc[10]) cap = hc[10];
-            retired.push_back(g->scratch);
-            g->scratch = nullptr;
-            g->scratch_cap = 0;
-            ING_HIP(g, hipMalloc(&g->scratch, cap));
-            g->scratch_cap = cap;
-            ING_HIP(g, hipMemsetAsync(used, 0, 8, s));
-            a.scratch = g->scratch;
-            a.scratch_cap = cap;
-            ING_HIP(g, launch_checked("k_ing_decode", k_ing_decode, lgrid, blk, 0, s, a, (uint32_t)kStNoScratch));
+            if (hc[10] > g->scratch_cap) {
+                uint64_t cap = 2 * g->scratch_cap;
+                if (cap < hc[10]) cap = hc[10];
+                retired.push_back(g->scratch);
+                g->scratch = nullptr;
+                g->scratch_cap = 0;
+                ING_HIP(g, hipMalloc(&g->scratch, cap));
+                g->scratch_cap = cap;
+                ING_HIP(g, hipMemsetAsync(used, 0, 8, s));
+                a.scratch = g->scratch;
+                a.scratch_cap = cap;
+            }
+            if (items_short()) {  // the string set or the extra list filled up: larger ones
+                if (ic[3] > g->x_cap) {
+                    const uint64_t old = g->x_cap;
+                    ING_HIP(g, size_extra(g, std::max<uint64_t>(2 * old, 2 * ic[3]), old));
+                    ING_HIP(g, hipMemcpyAsync(a.icnt + 3, &old, 8, hipMemcpyHostToDevice, s));
+                    ING_HIP(g, hipStreamSynchronize(s));
+                }
+                if (ic[4] > 0) {
+                    ING_HIP(g, grow_string_set(g, g->s_cap * 2));
+                    ING_HIP(g, size_new_strings(g, std::min<uint64_t>(ic[2], g->ns_cap)));
+                }
+                ING_HIP(g, hipMemsetAsync(a.icnt + 4, 0, 8, s));
+                ING_HIP(g, hipStreamSynchronize(s));
+                bind_items(g, a, ax);
+            }
+            ING_HIP(g, launch_checked("k_ing_decode", items ? k_ing_decode<true> : k_ing_decode<false>, lgrid, blk, 0, s,
+                                      a, (uint32_t)kStNoScratch));
             ING_HIP(g, launch_checked("k_ing_dict_insert", k_ing_dict_insert, lgrid, blk, 0, s, a));
-            ING_HIP(g, hipMemcpyAsync(hc + 10, used, 8, hipMemcpyDeviceToHost, s));
+            if (items) ING_HIP(g, launch_checked("k_ing_dict_insert_x", k_ing_dict_insert_x, xgrid, blk, 0, s, ax));
+            ING_HIP(g, hipMemcpyAsync(hc + 10, used, (items ? 13 : 1) * 8, hipMemcpyDeviceToHost, s));
             ING_HIP(g, hipStreamSynchronize(s));
         }
         // ids for new slots, in slot order; their names into the device arena
@@ -2010,6 +2663,38 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     }
     unsigned long long c[9];
     memcpy(c, hc, sizeof(c));
+    unsigned long long icf[7] = {0, 0, 0, 0, 0, 0, 0};
+    if (items) memcpy(icf, ic, sizeof(icf));
+    if (items && icf[2]) {
+        // the strings captured in this batch -> the host map (before any error return: their hashes
+        // are in the device set from now on)
+        const uint64_t m = std::min<uint64_t>(icf[2], g->ns_cap);
+        std::vector<uint64_t> hh(m), pp(m), off(m);
+        std::vector<uint32_t> ll(m);
+        ING_HIP(g, hipMemcpyAsync(hh.data(), a.ns_hash, m * 8, hipMemcpyDeviceToHost, s));
+        ING_HIP(g, hipMemcpyAsync(pp.data(), a.ns_ptr, m * 8, hipMemcpyDeviceToHost, s));
+        ING_HIP(g, hipMemcpyAsync(ll.data(), a.ns_len, m * 4, hipMemcpyDeviceToHost, s));
+        ING_HIP(g, hipStreamSynchronize(s));
+        uint64_t total = 0;
+        for (uint64_t k = 0; k < m; ++k) {
+            off[k] = total;
+            total += ll[k];
+        }
+        std::string bytes(total, '\0');
+        if (total) {
+            uint8_t* gt = nullptr;  // destination offsets, then the gathered bytes
+            ING_HIP(g, hipMalloc(&gt, m * 8 + total));
+            retired.push_back(gt);
+            ING_HIP(g, hipMemcpyAsync(gt, off.data(), m * 8, hipMemcpyHostToDevice, s));
+            ING_HIP(g, launch_checked("k_ing_gather_names", k_ing_gather_names, dim3((unsigned)((m + 255) / 256)), dim3(256),
+                                      0, s, (const uint64_t*)a.ns_ptr, (const uint64_t*)gt, (const uint32_t*)a.ns_len,
+                                      (uint32_t)m, gt + m * 8));
+            ING_HIP(g, hipMemcpyAsync(&bytes[0], gt + m * 8, total, hipMemcpyDeviceToHost, s));
+            ING_HIP(g, hipStreamSynchronize(s));
+        }
+        for (uint64_t k = 0; k < m; ++k) g->strings.emplace(hh[k], bytes.substr(off[k], ll[k]));
+        g->s_count += m;
+    }
     for (uint8_t* r : retired) hipFree(r);
     uint64_t dropped = 0;  // every fragment whose status is not ok is not a record
     for (int q = 0; q < 8; ++q) dropped += c[q];
@@ -2018,13 +2703,21 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     if (c[kStCollision])
         return dfail(g, ZK_ERR_INVALID_SPAN, "two service names share a 64-bit hash (fragment " +
                                                   std::to_string(first_bad) + ")");
-    if (c[kStRange])
+    if (icf[5]) return dfail(g, ZK_ERR_INVALID_SPAN, "two service names (an item's host) share a 64-bit hash");
+    if (c[kStRange] || icf[6])
         return dfail(g, ZK_ERR_SERVICE_RANGE, "more distinct service names than max_services");
     const bool strict = (flags & ZK_INGEST_STRICT) != 0;
     const uint64_t bad = c[kStInvalid] + c[kStUndecodable];
     if (strict && bad)
         return dfail(g, ZK_ERR_INVALID_SPAN, "span " + std::to_string(first_bad) + ": " +
                                                  (c[kStUndecodable] ? "undecodable or invalid span" : "invalid span"));
+    const uint64_t nkv = std::min<uint64_t>(icf[0], a.kv_cap), nan = std::min<uint64_t>(icf[1], a.an_cap);
+    if (nkv + nan) {  // item services (references to a fragment's record or an extra name) -> ids
+        ING_HIP(g, launch_checked("k_ing_item_fixup", k_ing_item_fixup,
+                                  dim3((unsigned)std::min<uint64_t>((nkv + nan + kIngWG - 1) / kIngWG, 4096)), blk, 0, s,
+                                  a, nkv, nan));
+        if (!dropped) ING_HIP(g, hipStreamSynchronize(s));
+    }
     if (dropped) {
         // D5: the records sit at their fragment index in the caller's columns; copy them aside and
         // compact them back in input order
@@ -2049,6 +2742,46 @@ zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64
     }
     *n_out = kept;
     *n_rejected = bad;
+    if (items) {
+        items->kv_n = nkv;
+        items->ann_n = nan;
+        if ((want_kv && icf[0] > a.kv_cap) || (want_ann && icf[1] > a.an_cap))
+            return dfail(g, ZK_ERR_CAPACITY, "item buffers too small: " + std::to_string(icf[0]) + " key-value and " +
+                                                 std::to_string(icf[1]) + " annotation items");
+    }
+    return ZK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* offsets, uint64_t n,
+                              uint32_t codec, uint32_t flags, const zk_span_cols* out, uint64_t* n_out,
+                              uint64_t* n_rejected) {
+    ZK_GUARD_BEGIN
+    return ingest_batch(g, buf, offsets, n, codec, flags, out, n_out, n_rejected, nullptr);
+    ZK_GUARD_END
+}
+
+zk_status zk_ingest_dev_spans_items(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* offsets, uint64_t n,
+                                    uint32_t codec, uint32_t flags, const zk_span_cols* out, uint64_t* n_out,
+                                    uint64_t* n_rejected, zk_ingest_items* items) {
+    ZK_GUARD_BEGIN
+    if (!items) return ZK_ERR_INVALID_ARG;
+    return ingest_batch(g, buf, offsets, n, codec, flags, out, n_out, n_rejected, items);
+    ZK_GUARD_END
+}
+
+zk_status zk_ingest_dev_string(const zk_ingest_dev* g, uint64_t hash, char* buf, uint64_t cap, uint64_t* len) {
+    ZK_GUARD_BEGIN
+    if (!g || !len) return ZK_ERR_INVALID_ARG;
+    auto it = g->strings.find(hash);
+    if (it == g->strings.end()) return ZK_ERR_INVALID_ARG;
+    *len = it->second.size();
+    if (!buf) return ZK_OK;
+    if (cap < it->second.size()) return ZK_ERR_CAPACITY;
+    memcpy(buf, it->second.data(), it->second.size());
     return ZK_OK;
     ZK_GUARD_END
 }

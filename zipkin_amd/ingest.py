@@ -164,21 +164,55 @@ class DeviceSpanDecoder:
         if st != _abi.ZK_OK:
             raise _abi.ZkError(st, self._L.zk_ingest_dev_last_error(self._h).decode() or _abi.status_str(st))
 
-    def decode_device(self, buf, offsets, n: int, *, snappy: bool = True, strict: bool = True, out=None):
-        """-> (DeviceColumns with .n = records written, rejected)."""
+    def decode_device(self, buf, offsets, n: int, *, snappy: bool = True, strict: bool = True, out=None,
+                      items: bool = False, item_cap: int | None = None):
+        """-> (DeviceColumns with .n = records written, rejected), or with items=True
+        (cols, rejected, (kv_service, kv_key), (ann_service, ann_value)): the span indexer's items as
+        device tensors (int32 service ids of this decoder, int64 hashes = uint64 bit patterns), in no
+        particular order within the batch (zk_ingest_dev_spans_items). item_cap: the items per kind
+        to allow for (default 2n + 16; a batch with more is decoded again with 4x the room)."""
+        import torch
+
         from .columns import DeviceColumns
 
-        cols = out if out is not None else DeviceColumns(max(1, n), device=f"cuda:{self.device}")
+        dev = f"cuda:{self.device}"
+        cols = out if out is not None else DeviceColumns(max(1, n), device=dev)
         nout, nrej = C.c_uint64(), C.c_uint64()
         ab = cols.abi(n)
         codec = _abi.ZK_CODEC_SNAPPY_THRIFT if snappy else _abi.ZK_CODEC_THRIFT
-        self._check(self._L.zk_ingest_dev_spans(self._h, buf.data_ptr(), offsets.data_ptr(), n, codec,
-                                                _abi.ZK_INGEST_STRICT if strict else 0, C.byref(ab),
-                                                C.byref(nout), C.byref(nrej)))
+        flags = _abi.ZK_INGEST_STRICT if strict else 0
+        if not items:
+            self._check(self._L.zk_ingest_dev_spans(self._h, buf.data_ptr(), offsets.data_ptr(), n, codec, flags,
+                                                    C.byref(ab), C.byref(nout), C.byref(nrej)))
+            cols.n = int(nout.value)
+            return cols, int(nrej.value)
+        cap = item_cap if item_cap is not None else 2 * n + 16
+        while True:
+            ks = torch.empty(cap, dtype=torch.int32, device=dev)
+            kh = torch.empty(cap, dtype=torch.int64, device=dev)
+            as_ = torch.empty(cap, dtype=torch.int32, device=dev)
+            ah = torch.empty(cap, dtype=torch.int64, device=dev)
+            it = _abi.zk_ingest_items(ks.data_ptr(), kh.data_ptr(), cap, 0, as_.data_ptr(), ah.data_ptr(), cap, 0)
+            st = self._L.zk_ingest_dev_spans_items(self._h, buf.data_ptr(), offsets.data_ptr(), n, codec, flags,
+                                                   C.byref(ab), C.byref(nout), C.byref(nrej), C.byref(it))
+            if st == _abi.ZK_ERR_CAPACITY and (it.kv_n == cap or it.ann_n == cap):
+                cap *= 4  # more items than guessed: the batch again
+                continue
+            self._check(st)
+            break
         cols.n = int(nout.value)
-        return cols, int(nrej.value)
+        return cols, int(nrej.value), (ks[: it.kv_n], kh[: it.kv_n]), (as_[: it.ann_n], ah[: it.ann_n])
 
-    def decode(self, blobs: Sequence[bytes], *, snappy: bool = True, strict: bool = True):
+    def string(self, h: int) -> str:
+        """The key / value string behind a hash an items batch has seen (zk_ingest_dev_string)."""
+        ln = C.c_uint64()
+        h = int(h) & 0xFFFFFFFFFFFFFFFF
+        self._check(self._L.zk_ingest_dev_string(self._h, h, None, 0, C.byref(ln)))
+        buf = C.create_string_buffer(max(1, ln.value))
+        self._check(self._L.zk_ingest_dev_string(self._h, h, buf, ln.value, C.byref(ln)))
+        return buf.raw[: ln.value].decode("utf-8", "surrogateescape")
+
+    def decode(self, blobs: Sequence[bytes], *, snappy: bool = True, strict: bool = True, items: bool = False):
         import torch
 
         dev = f"cuda:{self.device}"
@@ -188,7 +222,7 @@ class DeviceSpanDecoder:
         raw = np.frombuffer(b"".join(blobs) or b"\0", dtype=np.uint8)
         buf = torch.from_numpy(raw.copy()).to(dev)
         off = torch.from_numpy(offsets).to(dev)
-        return self.decode_device(buf, off, len(blobs), snappy=snappy, strict=strict)
+        return self.decode_device(buf, off, len(blobs), snappy=snappy, strict=strict, items=items)
 
     @property
     def num_services(self) -> int:
