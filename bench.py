@@ -85,6 +85,9 @@ def parse():
                          "JVM drop-in makes (GpuDependenciesJob.scala); torch = torch.distributed all_reduce "
                          "of the same exchange buffer (default for the gloo rehearsal, where RCCL cannot run "
                          "two ranks on one GPU)")
+    ap.add_argument("--layout", default="separate", choices=("separate", "packed"),
+                    help="c2/c3: the device columns as seven allocations (separate) or back to back in one "
+                         "(packed, DeviceColumns(packed=True))")
     ap.add_argument("--items", type=int, default=1_000_000_000,
                     help="c4: binary annotations per step (BASELINE configs[3]: 1e9, 12 GB in HBM)")
     a = ap.parse_args()
@@ -173,7 +176,7 @@ def main():
         p = tracegen_params(a.seed, traces_cap, target_records=a.records, max_depth=a.max_depth, num_services=S,
                             rank=rank, world=world)
         cap = a.records
-    cols = DeviceColumns(cap, device=f"cuda:{local}")
+    cols = DeviceColumns(cap, device=f"cuda:{local}", packed=a.layout == "packed")
     n, ntr = ctx.tracegen_device(p, cols)
     total_hint = n * world  # records of the whole job per step (exact below, before the timed steps)
     if dist is not None:
@@ -187,7 +190,7 @@ def main():
         g = torch.Generator(device=dev)
         g.manual_seed(a.seed + 1000 * rank)
         perm = torch.randperm(n, device=dev, generator=g)
-        sc = DeviceColumns(n, device=f"cuda:{local}")
+        sc = DeviceColumns(n, device=f"cuda:{local}", packed=a.layout == "packed")
         for k in ("trace_id", "span_id", "parent_id", "first_ts", "last_ts", "service_id", "flags"):
             torch.index_select(getattr(cols, k)[:n], 0, perm, out=getattr(sc, k))
         # the gathers run on `stream`; the second table set's context later writes memory torch may
@@ -856,7 +859,7 @@ def bench_c5(a):
     p = tracegen_params(a.seed, int(a.records / 15) + 1000, target_records=a.records, max_depth=a.max_depth,
                         num_services=S, rank=rank, world=world, global_ids=world > 1)
     cap = a.records if world == 1 else int(a.records / world * 1.02) + 1_000_000
-    cols = DeviceColumns(cap, device=f"cuda:{local}")
+    cols = DeviceColumns(cap, device=f"cuda:{local}", packed=a.layout == "packed")
     n, ntr = ctx.tracegen_device(p, cols)
     total = n
     if dist is not None:

@@ -66,11 +66,26 @@ class SpanColumns:
 class DeviceColumns:
     """The same seven columns as torch tensors in HBM (u64 columns stored as int64)."""
 
-    def __init__(self, n: int, device: str = "cuda"):
+    def __init__(self, n: int, device: str = "cuda", packed: bool = False):
+        """packed: the seven columns back to back in ONE allocation (each column 256-B aligned), so
+        that their bases are not all aligned alike (seven separate allocations start on the same
+        large alignment, and the same record index of every column then lands on the same HBM
+        channel); the ABI takes any 16-B aligned column pointers either way."""
         import torch
 
         self.n = n
         self.capacity = n
+        if packed:
+            offs, at = [], 0
+            for _, dt in COLUMNS:
+                offs.append(at)
+                at += (n * np.dtype(dt).itemsize + 255) // 256 * 256
+            self._block = torch.empty(max(at, 1), dtype=torch.uint8, device=device)
+            for (k, dt), o in zip(COLUMNS, offs):
+                w = np.dtype(dt).itemsize
+                view = self._block[o:o + n * w].view(torch.int64 if w == 8 else torch.int32)
+                setattr(self, k, view)
+            return
         self.trace_id = torch.empty(n, dtype=torch.int64, device=device)
         self.span_id = torch.empty(n, dtype=torch.int64, device=device)
         self.parent_id = torch.empty(n, dtype=torch.int64, device=device)
