@@ -79,6 +79,9 @@ def parse():
                          "binary annotations; c5: per-service HLL + duration histogram from span fragments; "
                          "ingest: device decode of stored Snappy+thrift fragments into columns")
     ap.add_argument("--fragments", type=int, default=20_000_000, help="ingest: stored fragments per step")
+    ap.add_argument("--ingest-items", type=int, default=0,
+                    help="ingest: 1 = decode with the span indexer's items (zk_ingest_dev_spans_items), checked "
+                         "against the host decoder's items as a multiset per replica")
     ap.add_argument("--comm", default=None, choices=("zk", "torch"),
                     help="N > 1: the exchange's collective. zk (default with RCCL) = the library's own "
                          "communicator, zk_deps_allreduce / zk_rt_allreduce (include/zkcomm.h), the call the "
@@ -774,10 +777,15 @@ def bench_ingest(a):
     in_bytes = int(offs[-1])
     dec = DeviceSpanDecoder(max(4096, a.services), stream=stream.cuda_stream)
     cols = None
+    items = None
 
     def step():
-        nonlocal cols
-        cols, rej = dec.decode_device(buf, off, n, out=cols)
+        nonlocal cols, items
+        if a.ingest_items:
+            cols, rej, kv, an = dec.decode_device(buf, off, n, out=cols, items=True, item_cap=2 * n)
+            items = (kv, an)
+        else:
+            cols, rej = dec.decode_device(buf, off, n, out=cols)
         assert rej == 0 and cols.n == n
 
     wall, ev_ms = _timed(step, a.steps, a.warmup, stream)
@@ -811,11 +819,24 @@ def bench_ingest(a):
     parity = {"result": "exact", "fragments": 2 * m if reps > 1 else m,
               "checked": "all 7 columns of the first and last replica (service ids by name) == the host decoder "
                          "zk_ingest_spans on the same bytes"}
+    if a.ingest_items:
+        _, _, (hks, hkh), (has_, hah) = hd.decode(blobs, items=True)
+        hid = {nm: i for i, nm in enumerate(hnames)}
+        d2h = np.array([hid.get(nm, -1) for nm in dnames], np.int64)  # device id -> host id (by name)
+        for (ds, dh), hs, hh, kind in ((items[0], hks, hkh, "kv"), (items[1], has_, hah, "annotation")):
+            got_s, got_h = d2h[ds.cpu().numpy().astype(np.int64)], dh.cpu().numpy()
+            want_s, want_h = np.tile(hs.astype(np.int64), reps), np.tile(hh.view(np.int64), reps)
+            go, wo = np.lexsort((got_h, got_s)), np.lexsort((want_h, want_s))
+            if not (np.array_equal(got_s[go], want_s[wo]) and np.array_equal(got_h[go], want_h[wo])):
+                raise RuntimeError(f"ingest: device {kind} items differ from the host decoder's")
+        parity["items"] = ("key-value and annotation items of the whole batch == the host decoder's items of the "
+                           "set x replicas, as multisets of (service name, hash)")
     value = n * a.steps / wall
     algo = in_bytes + n * BYTES_PER_RECORD
     achieved = algo / (ev_ms / a.steps * 1e-3) / 1e9
     print(json.dumps({
-        "metric": "stored span fragments/sec decoded into columns (Snappy + thrift, on device)",
+        "metric": "stored span fragments/sec decoded into columns (Snappy + thrift, on device)"
+                  + (" with the span indexer's items" if a.ingest_items else ""),
         "value": value, "unit": "fragments/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": wall * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u8", "data": "synthetic (tracegen records as thrift Spans, Snappy-compressed, replicated)",

@@ -142,6 +142,7 @@ def _assert_same(k, o, kk):
     (1, 1, 64, 1, 1),
     (3, 1000, 64, 2, 8),
     (57, 50_000, 0, 4, 64),
+    (7, 200_000, 0, 4, 64),  # >= kKvSmallPerService keys per service: the counters through LDS (the others: global)
     (500, 300_000, 0, 4, 16),
     (1022, 200_000, 0, 2, 32),  # largest S whose line-scatter carry fits the LDS
     (1024, 200_000, 0, 2, 32),  # one past it: item-by-item scatter (the line kernel would not launch)

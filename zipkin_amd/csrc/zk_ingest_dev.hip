@@ -470,8 +470,18 @@ struct IngArgs {
     uint8_t* x_status;
     uint32_t* x_list;
     uint64_t x_cap;
-    unsigned long long* icnt;    // [0] kv items [1] annotation items [2] captured strings [3] extra names
-                                 // [4] attempts failed on a full string set
+    unsigned long long* icnt;    // [0] / [1] kv / annotation items appended directly (the global-memory
+                                 // decoder) [2] captured strings [3] extra names [4] attempts failed on a
+                                 // full string set [5] / [6] extra-name collisions / range errors
+                                 // [7] / [8] chunked items dropped (staging full) [9] / [10] chunked items
+                                 // kept [11] / [12] chunks taken
+    // the LDS decoder's items go to per-wave chunks of kItemChunk slots (one global atomic per chunk,
+    // not per wave-append: every wave appending to one counter serialised on its L2 atomic unit),
+    // compacted into the caller's buffers after the batch (k_ing_item_compact)
+    uint32_t* ck_svc[2];
+    uint64_t* ck_key[2];
+    uint32_t* ck_fill[2];        // items in each chunk
+    uint32_t ck_cap;             // chunks per kind
 };
 
 // A fragment's first bytes (its Snappy header varint is at most 5), issued as independent loads:
@@ -1085,17 +1095,35 @@ __device__ __forceinline__ void publish_name_h(const IngArgs& a, uint64_t i, con
 // (kStNoScratch, decoded again after the host grows them); the items it appended stay, and
 // skip_kv / skip_an tell the next attempt to pass over them (each kind is emitted in a fixed order).
 constexpr uint32_t kRefFrag = 0x80000000u, kRefExtra = 0xC0000000u, kRefMask = 0x3FFFFFFFu;
+// ZK_ING_ITEMS_DIAG (diagnostic builds only, results wrong): 1 = the items build without the item walk,
+// 2 = the walk without emitting, 3 = emitting without the append
+#ifndef ZK_ING_ITEMS_DIAG
+#define ZK_ING_ITEMS_DIAG 0
+#endif
 constexpr uint32_t kUnknownLen = sizeof(kUnknown) - 1;
 
 struct ItemState {
     uint32_t seen[2];  // this fragment's items handled so far ([0] key-value, [1] annotation)
     uint32_t skip[2];  // appended by an earlier attempt
     bool fail;
+    uint64_t known[2];  // the lane's last string hash of each kind found in the set (0: none): the
+                        // same key / value in the lane's next fragment skips the set probe
 };
 
+// 16 bytes of each side in flight at once (one round trip per 16 bytes, not one per byte)
 __device__ __forceinline__ bool bytes_eq(const uint8_t* x, const uint8_t* y, uint32_t l) {
-    for (uint32_t q = 0; q < l; ++q)
-        if (x[q] != y[q]) return false;
+    for (uint32_t q0 = 0; q0 < l; q0 += 16) {
+        uint8_t u[16], v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            u[j] = q0 + j < l ? x[q0 + j] : 0;
+            v[j] = q0 + j < l ? y[q0 + j] : 0;
+        }
+        bool eq = true;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) eq &= u[j] == v[j];
+        if (!eq) return false;
+    }
     return true;
 }
 
@@ -1112,7 +1140,7 @@ __device__ __forceinline__ const uint8_t* global_copy(const IngArgs& a, const ui
 // the key / value hash into the captured set (one probe when it is known); a probe run longer than
 // kSetProbes counts as a full set (the host grows it: the set is kept at most half full between batches)
 constexpr uint32_t kSetProbes = 256;
-__device__ bool capture_string(const IngArgs& a, uint64_t h, const uint8_t* s, uint32_t l, const uint8_t* g) {
+__device__ __forceinline__ bool capture_string(const IngArgs& a, uint64_t h, const uint8_t* s, uint32_t l, const uint8_t* g) {
     uint32_t slot = (uint32_t)h & a.s_mask;
     const uint8_t* ptr = nullptr;
     for (uint32_t step = 0; step < kSetProbes && step <= a.s_mask; ++step) {
@@ -1140,7 +1168,7 @@ __device__ bool capture_string(const IngArgs& a, uint64_t h, const uint8_t* s, u
 }
 
 // an item host's service (nm / nl: the effective name, g: its global bytes or null)
-__device__ bool item_service(const IngArgs& a, uint64_t i, const uint8_t* nm, uint32_t nl, const uint8_t* g,
+__device__ __forceinline__ bool item_service(const IngArgs& a, uint64_t i, const uint8_t* nm, uint32_t nl, const uint8_t* g,
                              const uint8_t* snm, uint32_t snl, bool snamed, uint32_t* enc) {
     if (snamed && nl == snl && bytes_eq(nm, snm, nl)) {
         *enc = kRefFrag | (uint32_t)i;
@@ -1166,8 +1194,46 @@ __device__ bool item_service(const IngArgs& a, uint64_t i, const uint8_t* nm, ui
     return true;
 }
 
-// one atomic per wave: the active lanes take consecutive items of `kind`
-__device__ __forceinline__ void item_append(const IngArgs& a, uint32_t kind, uint32_t enc, uint64_t h) {
+constexpr uint32_t kItemChunk = 512, kNoChunk = 0xFFFFFFFFu;
+
+// ch (the LDS decoder): the wave's current chunk and its fill per kind, {c0, used0, c1, used1} in LDS;
+// null (the global-memory decoder): one atomic per wave-append on the direct counters
+__device__ __forceinline__ void item_append(const IngArgs& a, uint32_t kind, uint32_t enc, uint64_t h, uint32_t* ch) {
+    if (ch) {
+        const unsigned long long m = __ballot(1);
+        const uint32_t ln = __lane_id();
+        const uint32_t ld = (uint32_t)__ffsll(m) - 1u;
+        const uint32_t cnt = (uint32_t)__popcll(m), r = (uint32_t)__popcll(m & ((1ull << ln) - 1ull));
+        const uint32_t c = ch[2 * kind], used = ch[2 * kind + 1];
+        uint32_t pc, pj;
+        if (used + cnt <= kItemChunk) {
+            pc = c;
+            pj = used + r;
+            if (ln == ld) ch[2 * kind + 1] = used + cnt;
+        } else {
+            uint32_t nc = 0;
+            if (ln == ld) {
+                nc = (uint32_t)atomicAdd(&a.icnt[11 + kind], 1ull);
+                if (c < a.ck_cap) a.ck_fill[kind][c] = kItemChunk;  // (c is full now)
+            }
+            nc = (uint32_t)__shfl((int)nc, (int)ld);
+            const uint32_t room = kItemChunk - used;
+            pc = r < room ? c : nc;
+            pj = r < room ? used + r : r - room;
+            if (ln == ld) {
+                ch[2 * kind] = nc;
+                ch[2 * kind + 1] = cnt - room;
+            }
+        }
+        if (pc < a.ck_cap) {
+            const uint64_t q = (uint64_t)pc * kItemChunk + pj;
+            a.ck_svc[kind][q] = enc;
+            a.ck_key[kind][q] = h;
+        } else {
+            atomicAdd(&a.icnt[7 + kind], 1ull);
+        }
+        return;
+    }
     const unsigned long long mask = __ballot(1);
     const uint32_t lane = __lane_id();
     const uint32_t leader = (uint32_t)__ffsll(mask) - 1u;
@@ -1188,10 +1254,10 @@ __device__ __forceinline__ void item_append(const IngArgs& a, uint32_t kind, uin
 
 // one item: its host's name (hl == 0: absent or "", i.e. kUnknown), its key / value string, and the
 // global copies of both (null: in LDS only); snm / snl / snamed: the fragment's own service
-__device__ void item_emit(const IngArgs& a, uint64_t i, ItemState& st, uint32_t kind, const uint8_t* hn, uint32_t hl,
+__device__ __forceinline__ void item_emit(const IngArgs& a, uint64_t i, ItemState& st, uint32_t kind, const uint8_t* hn, uint32_t hl,
                           const uint8_t* hg, const uint8_t* s, uint32_t sl, const uint8_t* sg, const uint8_t* snm,
-                          uint32_t snl, bool snamed) {
-    if (st.fail) return;
+                          uint32_t snl, bool snamed, uint32_t* ch) {
+    if (st.fail || ZK_ING_ITEMS_DIAG == 2) return;
     if (st.seen[kind] < st.skip[kind]) {
         ++st.seen[kind];
         return;
@@ -1203,11 +1269,16 @@ __device__ void item_emit(const IngArgs& a, uint64_t i, ItemState& st, uint32_t 
     }
     const uint64_t h = d_hash(s, sl);
     uint32_t enc;
-    if (!capture_string(a, h, s, sl, sg) || !item_service(a, i, hn, hl, hg, snm, snl, snamed, &enc)) {
+    if ((h != st.known[kind] && !capture_string(a, h, s, sl, sg)) ||
+        !item_service(a, i, hn, hl, hg, snm, snl, snamed, &enc)) {
         st.fail = true;
         return;
     }
-    item_append(a, kind, enc, h);
+    st.known[kind] = h;
+    if (ZK_ING_ITEMS_DIAG == 3) {
+        if (enc == 0x12345u) a.icnt[6] = h;  // (keeps the work)
+    } else
+        item_append(a, kind, enc, h, ch);
     ++st.seen[kind];
 }
 
@@ -1238,9 +1309,9 @@ __device__ __forceinline__ bool fast_core(const FAnn& A) {
 }
 
 // gb: base as a generic pointer; gx: the global address of base offset 0 (0: the bytes are in LDS only)
-__device__ void items_fast(const IngArgs& a, uint64_t i, ItemState& st, const lds_u8* base, const uint32_t lay[4],
-                           uintptr_t gx, const uint8_t* snm, uint32_t snl, bool snamed) {
-    if (lay[1] == 0u) return;  // not indexed (CassieSpanStore.scala:214-218)
+__device__ __forceinline__ void items_fast(const IngArgs& a, uint64_t i, ItemState& st, const lds_u8* base, const uint32_t lay[4],
+                           uintptr_t gx, const uint8_t* snm, uint32_t snl, bool snamed, uint32_t* ch) {
+    if (lay[1] == 0u || ZK_ING_ITEMS_DIAG == 1) return;  // not indexed (CassieSpanStore.scala:214-218)
     const uint8_t* gb = (const uint8_t*)base;
     auto G = [&](uint32_t off) -> const uint8_t* { return gx ? (const uint8_t*)(gx + off) : nullptr; };
     uint32_t p = lay[0];
@@ -1271,7 +1342,7 @@ __device__ void items_fast(const IngArgs& a, uint64_t i, ItemState& st, const ld
                     q = B.next;
                 }
                 if (M.host)
-                    item_emit(a, i, st, 1u, gb + M.hoff, M.hl, G(M.hoff), gb + A.voff, A.vl, G(A.voff), snm, snl, snamed);
+                    item_emit(a, i, st, 1u, gb + M.hoff, M.hl, G(M.hoff), gb + A.voff, A.vl, G(A.voff), snm, snl, snamed, ch);
             }
         }
         p = A.next;
@@ -1289,7 +1360,7 @@ __device__ void items_fast(const IngArgs& a, uint64_t i, ItemState& st, const ld
         k3.load(base, p3);
         const bool host = k3.u8<7>() != T_STOP;
         const uint32_t hl = host ? k3.be32<25>() : 0u, hoff = p3 + 29u;
-        if (host) item_emit(a, i, st, 0u, gb + hoff, hl, G(hoff), gb + koff, kl, G(koff), snm, snl, snamed);
+        if (host) item_emit(a, i, st, 0u, gb + hoff, hl, G(hoff), gb + koff, kl, G(koff), snm, snl, snamed, ch);
         p = host ? p3 + 31u + hl : p3 + 8u;
     }
 }
@@ -1397,7 +1468,7 @@ __device__ __forceinline__ bool g_same_value(const GAnn<P>& A, const GAnn<P>& B)
 // gsrc: the global address of src (null: src is in LDS only)
 template <class P>
 __device__ void items_generic(const IngArgs& a, uint64_t i, ItemState& st, P src, uint64_t len, const uint8_t* gsrc,
-                              const uint8_t* snm, uint32_t snl, bool snamed) {
+                              const uint8_t* snm, uint32_t snl, bool snamed, uint32_t* ch) {
     auto G = [&](P p) -> const uint8_t* { return gsrc ? gsrc + (p - src) : nullptr; };
     GItemIter<P> o{DRdT<P>{src, src + len, true}, 0, 6};
     GAnn<P> A, B;
@@ -1426,7 +1497,7 @@ __device__ void items_generic(const IngArgs& a, uint64_t i, ItemState& st, P src
         const bool hv = M.hn != nullptr && M.hl > 0;
         const bool vv = A.v != nullptr && A.vl > 0;
         item_emit(a, i, st, 1u, hv ? (const uint8_t*)M.hn : nullptr, hv ? M.hl : 0u, hv ? G(M.hn) : nullptr,
-                  vv ? (const uint8_t*)A.v : a.unknown, vv ? A.vl : 0u, vv ? G(A.v) : a.unknown, snm, snl, snamed);
+                  vv ? (const uint8_t*)A.v : a.unknown, vv ? A.vl : 0u, vv ? G(A.v) : a.unknown, snm, snl, snamed, ch);
     }
     GItemIter<P> b{DRdT<P>{src, src + len, true}, 0, 8};
     GBann<P> K;
@@ -1435,7 +1506,7 @@ __device__ void items_generic(const IngArgs& a, uint64_t i, ItemState& st, P src
         const bool hv = K.hn != nullptr && K.hl > 0;
         const bool kv = K.k != nullptr && K.kl > 0;
         item_emit(a, i, st, 0u, hv ? (const uint8_t*)K.hn : nullptr, hv ? K.hl : 0u, hv ? G(K.hn) : nullptr,
-                  kv ? (const uint8_t*)K.k : a.unknown, kv ? K.kl : 0u, kv ? G(K.k) : a.unknown, snm, snl, snamed);
+                  kv ? (const uint8_t*)K.k : a.unknown, kv ? K.kl : 0u, kv ? G(K.k) : a.unknown, snm, snl, snamed, ch);
     }
 }
 
@@ -1481,8 +1552,8 @@ __device__ __forceinline__ void ing_decode_one(const IngArgs& a, uint64_t i, uin
     if (r < 0) return;
     if (r) publish_name(a, i, nm, nl);
     if constexpr (kItems) {  // a deferred fragment's first attempt (skips 0), or a failed one's next
-        ItemState st{{0u, 0u}, {a.skip_kv[i], a.skip_an[i]}, false};
-        items_generic(a, i, st, src, len, src, nm, nl, r == 1);
+        ItemState st{{0u, 0u}, {a.skip_kv[i], a.skip_an[i]}, false, {0ull, 0ull}};
+        items_generic(a, i, st, src, len, src, nm, nl, r == 1, nullptr);
         if (st.fail) {
             items_failed(a, i, st);
             return;
@@ -1779,8 +1850,15 @@ __device__ __forceinline__ uint32_t copy_blocks(const uint8_t* buf, uint64_t b, 
 template <bool kItems>
 __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
     constexpr bool kPre = ZK_ING_PREFETCH && !kItems;  // (the items build has no registers for it)
+    uint64_t known[2] = {0ull, 0ull};  // items: the lane's last string hashes found in the set
     __shared__ __align__(16) uint8_t s_buf[kLdsBudget];
+    // items: the wave's item chunks ({chunk, used} per kind) in the last 16 bytes (the regions keep off)
+    constexpr uint32_t kUse = kItems ? kLdsUse - 16u : kLdsUse;
+    uint32_t* const ch = kItems ? (uint32_t*)(s_buf + kLdsBudget - 16u) : nullptr;
     const uint32_t lane = threadIdx.x;
+    if constexpr (kItems) {
+        if (lane < 4) ch[lane] = (lane & 1u) ? kItemChunk : kNoChunk;  // no chunk yet: the first append takes one
+    }
     const uint64_t blk0 = (uint64_t)blockIdx.x * a.lds_block;
     const uint64_t blk1 = blk0 + a.lds_block < a.n ? blk0 + a.lds_block : a.n;
     ING_STAMP_DECL
@@ -1810,7 +1888,7 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
             if (st == kStOk) {
                 clen = ne - nb;
                 const uint64_t r = ((raw > clen ? raw : clen) + kLdsSlack + 15) & ~15ull;
-                need = r > kLdsUse ? kLdsUse + 1 : (uint32_t)r;
+                need = r > kUse ? kUse + 1 : (uint32_t)r;
             }
         }
         // Uniform layout (every region of the round has the size R of the largest, R / 16 odd, lane
@@ -1830,17 +1908,17 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
         if (uniform) {
             R = mx < 16u ? 16u : mx;
             if (((R >> 4) & 1u) == 0u) R += 16u;
-            k = kLdsUse / R;
+            k = kUse / R;
             if (k > 64u) k = 64u;
             R0 = lane * R;
             fits = true;
         } else {
             const uint32_t incl = wave_incl_scan(need);
             // this round: the longest prefix of lanes that fits (at least lane 0, to make progress)
-            k = (uint32_t)__popcll(__ballot(have && incl <= kLdsUse));
+            k = (uint32_t)__popcll(__ballot(have && incl <= kUse));
             if (k == 0) k = 1;  // lane 0 alone does not fit: deferred below
             R0 = incl - need;
-            fits = incl <= kLdsUse;
+            fits = incl <= kUse;
         }
         ING_STAMP(0);
         // the next round's extents (its copy-in below waits for them in passing: loads return in order)
@@ -1962,11 +2040,14 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
                     if (kItems && r >= 0) {
                         // the global address of LDS offset 0 (thrift codec: the input buffer)
                         const uintptr_t gx = a.snappy ? 0 : (uintptr_t)(a.buf + b) - p0;
-                        ItemState st{{0u, 0u}, {0u, 0u}, false};
+                        ItemState st{{0u, 0u}, {0u, 0u}, false, {known[0], known[1]}};
                         if (fast)
-                            items_fast(a, i, st, lbase, lay, gx, nm, nl, r == 1);
+                            items_fast(a, i, st, lbase, lay, gx, nm, nl, r == 1, ch);
                         else
-                            items_generic(a, i, st, src, len, gx ? (const uint8_t*)(gx + p0) : nullptr, nm, nl, r == 1);
+                            items_generic(a, i, st, src, len, gx ? (const uint8_t*)(gx + p0) : nullptr, nm, nl, r == 1,
+                                          ch);
+                        known[0] = st.known[0];
+                        known[1] = st.known[1];
                         if (st.fail) {
                             items_failed(a, i, st);
                             r = -1;
@@ -1980,6 +2061,12 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
         f0 += k;
         __syncthreads();  // one wave: this round's LDS accesses complete before the next round's copies
         ING_STAMP(5);
+    }
+    if constexpr (kItems) {  // the fill of the wave's last chunk of each kind
+        if (lane < 2) {
+            const uint32_t c = ch[2 * lane];
+            if (c < a.ck_cap) a.ck_fill[lane][c] = ch[2 * lane + 1];
+        }
     }
     ING_STAMP_FLUSH();
 }
@@ -2123,6 +2210,42 @@ __global__ __launch_bounds__(kIngWG) void k_ing_item_fixup(IngArgs a, uint64_t n
     }
 }
 
+// The caller's item buffers of one kind: the LDS decoder's chunks (in chunk order, each chunk's fill;
+// off = exclusive scan of the fills), then the global-memory decoder's direct items. [9 + kind] = the
+// chunked items kept.
+__global__ __launch_bounds__(kIngWG) void k_ing_item_compact(IngArgs a, uint32_t kind, uint32_t nch,
+                                                             const uint32_t* __restrict__ off, uint64_t ndirect,
+                                                             uint32_t* __restrict__ out_svc, uint64_t* __restrict__ out_key,
+                                                             uint64_t cap) {
+    const uint64_t F = nch ? (uint64_t)off[nch - 1] + a.ck_fill[kind][nch - 1] : 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.icnt[9 + kind] = F;
+    const uint64_t nc = (uint64_t)nch * kItemChunk;
+    const uint32_t* dsvc = kind ? a.an_svc : a.kv_svc;
+    const uint64_t* dkey = kind ? a.an_val : a.kv_key;
+    for (uint64_t t = (uint64_t)blockIdx.x * kIngWG + threadIdx.x; t < nc + ndirect; t += (uint64_t)gridDim.x * kIngWG) {
+        uint64_t dst, src;
+        const uint32_t* ss;
+        const uint64_t* sk;
+        if (t < nc) {
+            const uint32_t c = (uint32_t)(t / kItemChunk), j = (uint32_t)(t % kItemChunk);
+            if (j >= a.ck_fill[kind][c]) continue;
+            dst = (uint64_t)off[c] + j;
+            src = t;
+            ss = a.ck_svc[kind];
+            sk = a.ck_key[kind];
+        } else {
+            dst = F + (t - nc);
+            src = t - nc;
+            ss = dsvc;
+            sk = dkey;
+        }
+        if (dst < cap) {
+            out_svc[dst] = ss[src];
+            out_key[dst] = sk[src];
+        }
+    }
+}
+
 // the captured-string set into a larger table (keys are distinct)
 __global__ void k_ing_set_rehash(const uint64_t* __restrict__ old, uint64_t n_old, uint64_t* nw, uint32_t mask) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2177,6 +2300,8 @@ struct zk_ingest_dev {
     uint64_t ns_cap = 0;
     uint8_t* xs = nullptr;      // extra names: hash, ptr u64; len, svc, keep, list u32; status u8 [x_cap]
     uint64_t x_cap = 0;
+    uint8_t* istage = nullptr;  // item staging: the global decoder's direct items, the LDS decoder's chunks
+    uint64_t istage_cap = 0;
     std::string err;
 };
 
@@ -2270,6 +2395,7 @@ zk_status zk_ingest_dev_destroy(zk_ingest_dev* g) {
     hipFree(g->s_key);
     hipFree(g->ns);
     hipFree(g->xs);
+    hipFree(g->istage);
     if (g->own_stream && g->stream) hipStreamDestroy(g->stream);
     delete g;
     return ZK_OK;
@@ -2475,17 +2601,52 @@ zk_status ingest_batch(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* off
     IngArgs ax{};  // the extra names (items only)
     if (items) {
         a.items = 1;
-        a.kv_svc = want_kv ? items->kv_service : nullptr;
-        a.kv_key = want_kv ? items->kv_key : nullptr;
         a.kv_cap = want_kv ? items->kv_cap : 0;
-        a.an_svc = want_ann ? items->ann_service : nullptr;
-        a.an_val = want_ann ? items->ann_value : nullptr;
         a.an_cap = want_ann ? items->ann_cap : 0;
+        // staging: the direct items (as many as the caller's buffers take) and the chunks (the
+        // caller's capacity in chunks plus one partly filled chunk per LDS-decoder wave)
+        uint64_t waves = 0;
+        {
+            uint32_t lb = 128;
+            while (lb < kLdsBlock && (uint64_t)lb * 4096 < n) lb <<= 1;
+            waves = (n + lb - 1) / lb;
+        }
+        const uint64_t ck_cap = (std::max(a.kv_cap, a.an_cap) + kItemChunk - 1) / kItemChunk + waves + 1;
+        if (ck_cap > 0xFFFFFFF0ull) return dfail(g, ZK_ERR_INVALID_ARG, "items: item buffers too large");
+        const uint64_t ck_items = ck_cap * kItemChunk;
+        const uint64_t need_st = align256(a.kv_cap * 4) + align256(a.kv_cap * 8) + align256(a.an_cap * 4) +
+                                 align256(a.an_cap * 8) + 2 * (align256(ck_items * 4) + align256(ck_items * 8) +
+                                                               2 * align256(ck_cap * 4));
+        if (need_st > g->istage_cap) {
+            ING_HIP(g, hipStreamSynchronize(g->stream));  // (a previous batch's compaction may still read it)
+            hipFree(g->istage);
+            g->istage = nullptr;
+            g->istage_cap = 0;
+            ING_HIP(g, hipMalloc(&g->istage, need_st));
+            g->istage_cap = need_st;
+        }
+        uint8_t* q = g->istage;
+        auto takei = [&](uint64_t b) {
+            uint8_t* r = q;
+            q += align256(b);
+            return r;
+        };
+        a.kv_svc = (uint32_t*)takei(a.kv_cap * 4);
+        a.kv_key = (uint64_t*)takei(a.kv_cap * 8);
+        a.an_svc = (uint32_t*)takei(a.an_cap * 4);
+        a.an_val = (uint64_t*)takei(a.an_cap * 8);
+        for (int k = 0; k < 2; ++k) {
+            a.ck_svc[k] = (uint32_t*)takei(ck_items * 4);
+            a.ck_key[k] = (uint64_t*)takei(ck_items * 8);
+            a.ck_fill[k] = (uint32_t*)takei(ck_cap * 4);
+            takei(ck_cap * 4);  // the fills' exclusive scan (ck_off below)
+        }
+        a.ck_cap = (uint32_t)ck_cap;
         if (!g->s_key) ING_HIP(g, grow_string_set(g, 1u << 16));
         while (g->s_count * 2 > g->s_cap) ING_HIP(g, grow_string_set(g, g->s_cap * 2));
         ING_HIP(g, size_new_strings(g, 0));
         if (!g->xs) ING_HIP(g, size_extra(g, 4096, 0));
-        ING_HIP(g, hipMemsetAsync(a.icnt, 0, 7 * 8, g->stream));
+        ING_HIP(g, hipMemsetAsync(a.icnt, 0, 13 * 8, g->stream));
     }
     const dim3 grid((unsigned)((n + kIngWG - 1) / kIngWG)), blk(kIngWG);
     const dim3 lgrid(std::min<unsigned>(grid.x, 2048u));  // the list kernels (grid-stride)
@@ -2543,7 +2704,7 @@ zk_status ingest_batch(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* off
             if (e == hipSuccess) e = hipMemsetAsync(a.icnt + 5, 0, 2 * 8, s);
             if (e == hipSuccess) e = launch_checked("k_ing_count_extra", k_ing_count_extra, xgrid, blk, 0, s, ax);
         }
-        if (e == hipSuccess) e = hipMemcpyAsync(hc, g->counts, (items ? 23 : 14) * 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(hc, g->counts, (items ? 29 : 14) * 8, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         return e;
     };
@@ -2585,7 +2746,7 @@ zk_status ingest_batch(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* off
                                       a, (uint32_t)kStNoScratch));
             ING_HIP(g, launch_checked("k_ing_dict_insert", k_ing_dict_insert, lgrid, blk, 0, s, a));
             if (items) ING_HIP(g, launch_checked("k_ing_dict_insert_x", k_ing_dict_insert_x, xgrid, blk, 0, s, ax));
-            ING_HIP(g, hipMemcpyAsync(hc + 10, used, (items ? 13 : 1) * 8, hipMemcpyDeviceToHost, s));
+            ING_HIP(g, hipMemcpyAsync(hc + 10, used, (items ? 19 : 1) * 8, hipMemcpyDeviceToHost, s));
             ING_HIP(g, hipStreamSynchronize(s));
         }
         // ids for new slots, in slot order; their names into the device arena
@@ -2663,7 +2824,7 @@ zk_status ingest_batch(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* off
     }
     unsigned long long c[9];
     memcpy(c, hc, sizeof(c));
-    unsigned long long icf[7] = {0, 0, 0, 0, 0, 0, 0};
+    unsigned long long icf[13] = {0};
     if (items) memcpy(icf, ic, sizeof(icf));
     if (items && icf[2]) {
         // the strings captured in this batch -> the host map (before any error return: their hashes
@@ -2711,7 +2872,43 @@ zk_status ingest_batch(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* off
     if (strict && bad)
         return dfail(g, ZK_ERR_INVALID_SPAN, "span " + std::to_string(first_bad) + ": " +
                                                  (c[kStUndecodable] ? "undecodable or invalid span" : "invalid span"));
-    const uint64_t nkv = std::min<uint64_t>(icf[0], a.kv_cap), nan = std::min<uint64_t>(icf[1], a.an_cap);
+    uint64_t nkv = 0, nan = 0, tot[2] = {0, 0};
+    if (items) {
+        // the chunks and the direct items into the caller's buffers (k_ing_item_compact), then the item
+        // services' references -> ids (k_ing_item_fixup, on the caller's buffers)
+        uint32_t* out_s[2] = {items->kv_service, items->ann_service};
+        uint64_t* out_k[2] = {items->kv_key, items->ann_value};
+        const uint64_t cap[2] = {a.kv_cap, a.an_cap};
+        for (int k = 0; k < 2; ++k) {
+            if (!cap[k]) continue;
+            const uint32_t nch = (uint32_t)std::min<uint64_t>(icf[11 + k], a.ck_cap);
+            uint32_t* off = a.ck_fill[k] + align256((uint64_t)a.ck_cap * 4) / 4;
+            if (nch) {
+                size_t nb = 0;
+                ING_HIP(g, hipcub::DeviceScan::ExclusiveSum(nullptr, nb, a.ck_fill[k], off, (int)nch, s));
+                if (nb > g->cub_cap) {
+                    ING_HIP(g, hipStreamSynchronize(s));
+                    hipFree(g->cub);
+                    g->cub = nullptr;
+                    ING_HIP(g, hipMalloc(&g->cub, nb));
+                    g->cub_cap = nb;
+                }
+                ING_HIP(g, hipcub::DeviceScan::ExclusiveSum(g->cub, nb, a.ck_fill[k], off, (int)nch, s));
+            }
+            const uint64_t nd = std::min<uint64_t>(icf[k], cap[k]);
+            const uint64_t work = (uint64_t)nch * kItemChunk + nd;
+            ING_HIP(g, launch_checked("k_ing_item_compact", k_ing_item_compact,
+                                      dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((work + kIngWG - 1) / kIngWG, 8192))),
+                                      blk, 0, s, a, (uint32_t)k, nch, (const uint32_t*)off, nd, out_s[k], out_k[k], cap[k]));
+        }
+        ING_HIP(g, hipMemcpyAsync(hc + 25, a.icnt + 9, 2 * 8, hipMemcpyDeviceToHost, s));
+        ING_HIP(g, hipStreamSynchronize(s));
+        for (int k = 0; k < 2; ++k) tot[k] = cap[k] ? hc[25 + k] + icf[k] + icf[7 + k] : 0;
+        nkv = std::min<uint64_t>(tot[0], cap[0]);
+        nan = std::min<uint64_t>(tot[1], cap[1]);
+        a.kv_svc = items->kv_service;
+        a.an_svc = items->ann_service;
+    }
     if (nkv + nan) {  // item services (references to a fragment's record or an extra name) -> ids
         ING_HIP(g, launch_checked("k_ing_item_fixup", k_ing_item_fixup,
                                   dim3((unsigned)std::min<uint64_t>((nkv + nan + kIngWG - 1) / kIngWG, 4096)), blk, 0, s,
@@ -2745,9 +2942,9 @@ zk_status ingest_batch(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* off
     if (items) {
         items->kv_n = nkv;
         items->ann_n = nan;
-        if ((want_kv && icf[0] > a.kv_cap) || (want_ann && icf[1] > a.an_cap))
-            return dfail(g, ZK_ERR_CAPACITY, "item buffers too small: " + std::to_string(icf[0]) + " key-value and " +
-                                                 std::to_string(icf[1]) + " annotation items");
+        if ((want_kv && tot[0] > a.kv_cap) || (want_ann && tot[1] > a.an_cap))
+            return dfail(g, ZK_ERR_CAPACITY, "item buffers too small: " + std::to_string(tot[0]) + " key-value and " +
+                                                 std::to_string(tot[1]) + " annotation items");
     }
     return ZK_OK;
 }

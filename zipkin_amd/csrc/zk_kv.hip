@@ -171,14 +171,18 @@ __device__ uint32_t ts_sort(TopSet& t, uint64_t seed) {
     }
     __syncthreads();
     const uint32_t n = t.gcount;
-    for (uint32_t x = n + threadIdx.x; x < kSortCap; x += kKvWG) {
+    // the bitonic network over the next power of two >= n only (a small unit or a merge of few lists
+    // sorts 64-256 entries: 21-36 barrier stages instead of 55)
+    uint32_t P = 2;
+    while (P < n) P <<= 1;
+    for (uint32_t x = n + threadIdx.x; x < P; x += kKvWG) {
         t.sk[x] = kEmptyKey;
         t.se[x] = 0u;  // padding never beats a real entry (real estimates are >= 1)
     }
     __syncthreads();
-    for (uint32_t k = 2; k <= kSortCap; k <<= 1) {
+    for (uint32_t k = 2; k <= P; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t x = threadIdx.x; x < kSortCap; x += kKvWG) {
+            for (uint32_t x = threadIdx.x; x < P; x += kKvWG) {
                 const uint32_t y = x ^ j;
                 if (y > x) {
                     const bool best_first = (x & k) == 0;
@@ -243,16 +247,26 @@ __device__ __forceinline__ void unit_range(const KvArgs& a, uint32_t s, uint32_t
     *hi = *lo + len < e ? *lo + len : e;
 }
 
+// kSmall (batches of a few thousand keys per service, StoredSpanJob's per-batch sketches): the
+// counters stay in global memory -- the sketch adds to them with global atomics, the candidate and
+// merge passes estimate from them -- instead of a 4 x width row block per unit moved through LDS (the
+// per-unit fixed cost that dominated small batches: 64 KB in, 64 KB flushed, per service and batch).
+// The sums and the estimates are the same integers either way.
+template <bool kSmall>
 __global__ __launch_bounds__(kKvWG) void k_kv_sketch(KvArgs a) {
-    extern __shared__ uint32_t cm[];
+    extern __shared__ uint32_t cm_lds[];
     const uint32_t u = blockIdx.x;
     if (u >= a.unit_base[a.S]) return;
     const uint32_t s = find_service(a.unit_base, a.S, u);
     uint64_t lo, hi;
     unit_range(a, s, u, &lo, &hi);
     const uint32_t cells = a.depth * a.width;
-    for (uint32_t x = threadIdx.x; x < cells; x += kKvWG) cm[x] = 0u;
-    __syncthreads();
+    uint32_t* const g = a.cm + (uint64_t)s * cells;
+    uint32_t* const cm = kSmall ? g : cm_lds;
+    if constexpr (!kSmall) {
+        for (uint32_t x = threadIdx.x; x < cells; x += kKvWG) cm[x] = 0u;
+        __syncthreads();
+    }
     // two alternating 4-key buffers (C4 sketch 2.00 -> 1.96-1.97 ms; the pass is LDS-atomic-bound,
     // profiles/r02/ab_kv_sketch_pipe.txt)
     constexpr int U = 4;
@@ -304,11 +318,12 @@ __global__ __launch_bounds__(kKvWG) void k_kv_sketch(KvArgs a) {
         load(ka, b + 2 * BS);
         add(kb, b + BS);  // past hi: every key is masked
     }
-    __syncthreads();
-    uint32_t* g = a.cm + (uint64_t)s * cells;
-    for (uint32_t x = threadIdx.x; x < cells; x += kKvWG) {
-        const uint32_t v = cm[x];
-        if (v) atomicAdd(&g[x], v);
+    if constexpr (!kSmall) {
+        __syncthreads();
+        for (uint32_t x = threadIdx.x; x < cells; x += kKvWG) {
+            const uint32_t v = cm[x];
+            if (v) atomicAdd(&g[x], v);
+        }
     }
     if (threadIdx.x == 0) atomicAdd((unsigned long long*)&a.totals[s], (unsigned long long)(hi - lo));
 }
@@ -319,15 +334,17 @@ __device__ void load_cm(uint32_t* cm, const KvArgs& a, uint32_t s) {
     for (uint32_t x = threadIdx.x; x < cells; x += kKvWG) cm[x] = g[x];
 }
 
+template <bool kSmall>
 __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
-    extern __shared__ uint32_t cm[];
+    extern __shared__ uint32_t cm_lds[];
     __shared__ TopSet t;
     const uint32_t u = blockIdx.x;
     if (u >= a.unit_base[a.S]) return;
     const uint32_t s = find_service(a.unit_base, a.S, u);
     uint64_t lo, hi;
     unit_range(a, s, u, &lo, &hi);
-    load_cm(cm, a, s);
+    const uint32_t* const cm = kSmall ? a.cm + (uint64_t)s * a.depth * a.width : cm_lds;
+    if constexpr (!kSmall) load_cm(cm_lds, a, s);
     ts_init(t);  // contains the barrier that publishes cm
     // Blocks of J = 8 keys per thread (4096 per workgroup), in two alternating key buffers: one
     // block's loads are in flight while the other is processed (a register ring carried across the
@@ -456,11 +473,13 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
 }
 
 // one workgroup per service: previous candidates + this batch's unit lists (+ extra lists)
+template <bool kSmall>
 __global__ __launch_bounds__(kKvWG) void k_kv_merge(KvArgs a, uint32_t use_units) {
-    extern __shared__ uint32_t cm[];
+    extern __shared__ uint32_t cm_lds[];
     __shared__ TopSet t;
     const uint32_t s = blockIdx.x;
-    load_cm(cm, a, s);
+    const uint32_t* const cm = kSmall ? a.cm + (uint64_t)s * a.depth * a.width : cm_lds;
+    if constexpr (!kSmall) load_cm(cm_lds, a, s);
     ts_init(t);
     const uint32_t C = a.cand;
     const uint32_t u0 = use_units ? a.unit_base[s] : 0, u1 = use_units ? a.unit_base[s + 1] : 0;
@@ -511,19 +530,24 @@ __global__ void k_kv_estimate(KvArgs a, uint32_t s, const uint64_t* __restrict__
 
 }  // namespace
 
-hipError_t launch_kv_sketch(const KvArgs& a, hipStream_t s) {
+hipError_t launch_kv_sketch(const KvArgs& a, hipStream_t s, bool small) {
     if (!a.max_units) return hipSuccess;
-    return launch_checked("k_kv_sketch", k_kv_sketch, dim3(a.max_units), dim3(kKvWG), (size_t)a.depth * a.width * 4, s, a);
-}
-
-hipError_t launch_kv_candidates(const KvArgs& a, hipStream_t s) {
-    if (!a.max_units) return hipSuccess;
-    return launch_checked("k_kv_candidates", k_kv_candidates, dim3(a.max_units), dim3(kKvWG),
+    if (small) return launch_checked("k_kv_sketch", k_kv_sketch<true>, dim3(a.max_units), dim3(kKvWG), 0, s, a);
+    return launch_checked("k_kv_sketch", k_kv_sketch<false>, dim3(a.max_units), dim3(kKvWG),
                           (size_t)a.depth * a.width * 4, s, a);
 }
 
-hipError_t launch_kv_merge(const KvArgs& a, hipStream_t s) {
-    return launch_checked("k_kv_merge", k_kv_merge, dim3(a.S), dim3(kKvWG), (size_t)a.depth * a.width * 4, s, a,
+hipError_t launch_kv_candidates(const KvArgs& a, hipStream_t s, bool small) {
+    if (!a.max_units) return hipSuccess;
+    if (small)
+        return launch_checked("k_kv_candidates", k_kv_candidates<true>, dim3(a.max_units), dim3(kKvWG), 0, s, a);
+    return launch_checked("k_kv_candidates", k_kv_candidates<false>, dim3(a.max_units), dim3(kKvWG),
+                          (size_t)a.depth * a.width * 4, s, a);
+}
+
+hipError_t launch_kv_merge(const KvArgs& a, hipStream_t s, bool small) {
+    if (small) return launch_checked("k_kv_merge", k_kv_merge<true>, dim3(a.S), dim3(kKvWG), 0, s, a, a.max_units ? 1u : 0u);
+    return launch_checked("k_kv_merge", k_kv_merge<false>, dim3(a.S), dim3(kKvWG), (size_t)a.depth * a.width * 4, s, a,
                           a.max_units ? 1u : 0u);
 }
 

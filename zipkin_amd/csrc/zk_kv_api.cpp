@@ -284,11 +284,12 @@ zk_status zk_kv_accumulate(zk_kv* k, const uint32_t* svc, const uint64_t* keys, 
     a.extra_key = nullptr;
     a.extra_est = nullptr;
     a.extra_lists = 0;
-    KV_HIP(k, launch_kv_sketch(a, k->stream));
+    const bool small = n < (uint64_t)a.S * kKvSmallPerService;
+    KV_HIP(k, launch_kv_sketch(a, k->stream, small));
     if (k->timing) KV_HIP(k, hipEventRecord(k->ev[2], k->stream));
-    KV_HIP(k, launch_kv_candidates(a, k->stream));
+    KV_HIP(k, launch_kv_candidates(a, k->stream, small));
     if (k->timing) KV_HIP(k, hipEventRecord(k->ev[3], k->stream));
-    KV_HIP(k, launch_kv_merge(a, k->stream));
+    KV_HIP(k, launch_kv_merge(a, k->stream, small));
     if (k->timing) {
         KV_HIP(k, hipEventRecord(k->ev[4], k->stream));
         k->ev_recorded = true;
@@ -420,7 +421,7 @@ zk_status zk_kv_merge_candidates(zk_kv* k, const uint64_t* keys, const uint32_t*
     a.extra_key = keys;
     a.extra_est = est;
     a.extra_lists = lists;
-    KV_HIP(k, launch_kv_merge(a, k->stream));
+    KV_HIP(k, launch_kv_merge(a, k->stream, false));
     return ZK_OK;
     ZK_GUARD_END
 }

@@ -90,9 +90,12 @@ struct KvArgs {
     uint32_t extra_lists;
 };
 
-hipError_t launch_kv_sketch(const KvArgs& a, hipStream_t s);
-hipError_t launch_kv_candidates(const KvArgs& a, hipStream_t s);
-hipError_t launch_kv_merge(const KvArgs& a, hipStream_t s);  // prev cand + unit lists + extra lists
+// small: the counters are read and added in global memory instead of an LDS row block per unit
+// (zk_kv_accumulate picks it for batches of fewer than kKvSmallPerService keys per service)
+constexpr uint64_t kKvSmallPerService = 8192;
+hipError_t launch_kv_sketch(const KvArgs& a, hipStream_t s, bool small);
+hipError_t launch_kv_candidates(const KvArgs& a, hipStream_t s, bool small);
+hipError_t launch_kv_merge(const KvArgs& a, hipStream_t s, bool small);  // prev cand + unit lists + extra lists
 hipError_t launch_kv_estimate(const KvArgs& a, uint32_t svc, const uint64_t* keys, uint64_t n, uint32_t* est,
                               hipStream_t s);
 
