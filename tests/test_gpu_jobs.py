@@ -75,6 +75,13 @@ def test_stored_span_job_streams_ten_million_fragments(gpu):
             for svc in job.top_kv:
                 assert dstore.getTopKeyValueAnnotations(svc) == store.getTopKeyValueAnnotations(svc)
                 assert dstore.getTopAnnotations(svc) == store.getTopAnnotations(svc)
+        # a second run of the same job reuses its device objects (reset, not rebuilt): same result
+        t0 = time.perf_counter()
+        again = djob.run_device(dev, indexer=indexer)
+        adt = time.perf_counter() - t0
+        print(f"  ... run again: {adt * 1e3:.1f} ms, {len(cols) / adt:.3e} fragments/s")
+        assert _by_name(again) == want and djob.stats["records"] == len(cols)
+        djob.close()
 
 
 def test_stored_span_job_on_the_device_decoder(gpu):

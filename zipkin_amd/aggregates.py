@@ -774,59 +774,120 @@ class StoredSpanJob:
                 self.aggregates.storeTopAnnotations(name, values)
         return deps
 
-    def run_device(self, batches, *, indexer: bool = True) -> Optional[Dependencies]:
-        """batches: (buf uint8, offsets int64[n + 1], n) torch tensors already in HBM, in row order.
-        Decoded on the device into a reused column buffer and accumulated on the same stream; with
-        `indexer` the decoder's items feed the two count-min + top-K sketches as in run()."""
-        import contextlib
+    # run_device: decoded batches are gathered in one column buffer of this many records and
+    # accumulated together (row-order batches back to back are one row-order batch, and the
+    # dependency sums do not depend on where batches are cut), so a stream of small batches pays the
+    # accumulate's fixed cost once per buffer instead of once per batch
+    device_accumulate_records = 1 << 22
 
+    def _device_state(self, indexer: bool):
+        """The device objects of run_device, kept between runs (a scheduled job reuses its buffers,
+        as ZipkinAggregateJob keeps its context): stream, decoder (its service dictionary and string
+        map persist: ids stay stable, outputs are by name), context, gathering buffer and the two
+        sketches, reset at the start of every run. close() frees them. The dictionary persisting,
+        max_services bounds the distinct services over the job's lifetime, not per run."""
         import torch
 
         from .context import DepsContext
         from .ingest import DeviceSpanDecoder
         from .kv import KvSketch
 
-        S = self.max_services
+        st = getattr(self, "_dev", None)
+        if st is None:
+            S = self.max_services
+            stream = torch.cuda.Stream(device=self.device)
+            st = {"stream": stream, "pool": None,
+                  "dec": DeviceSpanDecoder(max(4096, S), device=self.device, stream=stream.cuda_stream),
+                  "ctx": DepsContext(S, device=self.device, strict=self.strict, stream=stream.cuda_stream),
+                  "kvs": None, "anns": None}
+            self._dev = st
+        else:
+            st["ctx"].reset()
+        if indexer:
+            for k in ("kvs", "anns"):
+                if st[k] is None:
+                    st[k] = KvSketch(self.max_services, device=self.device, stream=st["stream"].cuda_stream,
+                                     width=self.kv_width or 4096, seed=self.seed)
+                else:
+                    st[k].reset()
+        return st
+
+    def close(self) -> None:
+        st = getattr(self, "_dev", None)
+        if st is not None:
+            for k in ("kvs", "anns", "ctx", "dec"):
+                if st[k] is not None:
+                    st[k].close()
+            self._dev = None
+
+    def run_device(self, batches, *, indexer: bool = True) -> Optional[Dependencies]:
+        """batches: (buf uint8, offsets int64[n + 1], n) torch tensors already in HBM, in row order.
+        Decoded on the device into a reused column buffer and accumulated on the same stream, several
+        small batches at a time (device_accumulate_records); with `indexer` the decoder's items feed
+        the two count-min + top-K sketches batch by batch as in run(). The device objects are kept
+        for the next run (close() frees them)."""
+        import torch
+
+        from .columns import DeviceColumns
+
         self.rejected = 0
-        stream = torch.cuda.Stream(device=self.device)
-        dec = DeviceSpanDecoder(max(4096, S), device=self.device, stream=stream.cuda_stream)
-        width = self.kv_width or 4096
+        st = self._device_state(indexer)
+        stream, dec, ctx, kvs, anns = st["stream"], st["dec"], st["ctx"], st["kvs"], st["anns"]
+        cap = self.device_accumulate_records
+        filled = 0
+        cols = None  # a batch larger than the gathering buffer: its own columns
+
+        def flush():
+            nonlocal filled
+            if filled:
+                ctx.accumulate(st["pool"].slice(0, filled), clustered=True, continues=True, verify=self.verify)
+                filled = 0
+
         try:
-            with DepsContext(S, device=self.device, strict=self.strict, stream=stream.cuda_stream) as ctx, \
-                    (KvSketch(S, device=self.device, stream=stream.cuda_stream, width=width, seed=self.seed) if indexer
-                     else contextlib.nullcontext()) as kvs, \
-                    (KvSketch(S, device=self.device, stream=stream.cuda_stream, width=width, seed=self.seed) if indexer
-                     else contextlib.nullcontext()) as anns:
-                cols = None
-                for buf, off, n in batches:
-                    # the caller's tensors may still be in flight on its current stream (a
-                    # non_blocking copy, a kernel that writes them; a lazy iterator makes each batch
-                    # just before it is read): the job's stream waits for everything queued there, and
-                    # the caller's allocator keeps the batch's memory until the job's stream is done
-                    stream.wait_stream(torch.cuda.current_stream(self.device))
-                    buf.record_stream(stream)
-                    off.record_stream(stream)
-                    if cols is not None and cols.capacity < n:
+            for buf, off, n in batches:
+                # the caller's tensors may still be in flight on its current stream (a non_blocking
+                # copy, a kernel that writes them; a lazy iterator makes each batch just before it is
+                # read): the job's stream waits for everything queued there, and the caller's
+                # allocator keeps the batch's memory until the job's stream is done
+                stream.wait_stream(torch.cuda.current_stream(self.device))
+                buf.record_stream(stream)
+                off.record_stream(stream)
+                if n <= cap:
+                    if st["pool"] is None:
+                        st["pool"] = DeviceColumns(cap, device=f"cuda:{self.device}")
+                    if filled + n > cap:
+                        flush()
+                    out = st["pool"].slice(filled, filled + n)
+                else:
+                    flush()
+                    if cols is None or cols.capacity < n:
                         cols = None
-                    if indexer:
-                        cols, rej, (ks, kh), (as_, ah) = dec.decode_device(
-                            buf, off, n, snappy=self.snappy, strict=self.strict, out=cols, items=True)
-                    else:
-                        cols, rej = dec.decode_device(buf, off, n, snappy=self.snappy, strict=self.strict, out=cols)
-                    self.rejected += rej
-                    ctx.accumulate(cols, clustered=True, continues=True, verify=self.verify)
-                    if indexer:
-                        if len(ks):
-                            kvs.accumulate(ks, kh)
-                        if len(as_):
-                            anns.accumulate(as_, ah)
-                names = dec.service_names()
-                deps = self._finish(ctx, names)
+                    out = cols
                 if indexer:
-                    self.top_kv = self._tops(dec, kvs, len(names))
-                    self.top_annotations = self._tops(dec, anns, len(names))
-        finally:
-            dec.close()
+                    out, rej, (ks, kh), (as_, ah) = dec.decode_device(
+                        buf, off, n, snappy=self.snappy, strict=self.strict, out=out, items=True)
+                else:
+                    out, rej = dec.decode_device(buf, off, n, snappy=self.snappy, strict=self.strict, out=out)
+                self.rejected += rej
+                if n <= cap:
+                    filled += out.n
+                else:
+                    cols = out
+                    ctx.accumulate(cols, clustered=True, continues=True, verify=self.verify)
+                if indexer:
+                    if len(ks):
+                        kvs.accumulate(ks, kh)
+                    if len(as_):
+                        anns.accumulate(as_, ah)
+            flush()
+            names = dec.service_names()
+            deps = self._finish(ctx, names)
+            if indexer:
+                self.top_kv = self._tops(dec, kvs, len(names))
+                self.top_annotations = self._tops(dec, anns, len(names))
+        except BaseException:
+            self.close()  # a failed run leaves no half-used state behind
+            raise
         if self.aggregates is not None:
             if deps is not None:
                 self.aggregates.storeDependencies(deps)

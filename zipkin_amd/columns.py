@@ -94,6 +94,15 @@ class DeviceColumns:
         self.service_id = torch.empty(n, dtype=torch.int32, device=device)
         self.flags = torch.empty(n, dtype=torch.int32, device=device)
 
+    def slice(self, a: int, b: int) -> "DeviceColumns":
+        """Records [a, b) as a view of the same HBM (capacity b - a, n = b - a)."""
+        v = DeviceColumns.__new__(DeviceColumns)
+        for k, _ in COLUMNS:
+            setattr(v, k, getattr(self, k)[a:b])
+        v.n = v.capacity = b - a
+        v._parent = self  # (keeps the storage alive)
+        return v
+
     def abi(self, n: int | None = None) -> _abi.zk_span_cols:
         return _abi.zk_span_cols(
             *[getattr(self, k).data_ptr() for k, _ in COLUMNS], self.n if n is None else n
