@@ -58,7 +58,17 @@ def test_stored_span_job_streams_ten_million_fragments(gpu):
 
     dev = [(torch.from_numpy(b).cuda(), torch.from_numpy(o.view(np.int64)).cuda(), len(o) - 1) for b, o in parts]
     torch.cuda.synchronize()
+    # the oracle's 250k-entry result dict is the test's, not the job's: kept out of the collector's
+    # full passes while the job is timed
+    import gc
+
+    gc.collect()
+    gc.freeze()
     for indexer in (True, False):
+        if not indexer:
+            # the previous iteration's records, released outside the timed region: comparing them
+            # (_by_name) materialised ~250k DependencyLink objects each, whose teardown is the test's
+            del ddeps, again
         dstore = GpuAggregates("cassandra")
         djob = StoredSpanJob(aggregates=dstore, top_k=5, clock=lambda: 10**15, max_services=S)
         djob.run_device(dev[:1], indexer=indexer)  # warm
@@ -79,9 +89,11 @@ def test_stored_span_job_streams_ten_million_fragments(gpu):
         t0 = time.perf_counter()
         again = djob.run_device(dev, indexer=indexer)
         adt = time.perf_counter() - t0
+        print("  phases (ms):", {k: round(v, 2) for k, v in djob.phase_ms.items()})
         print(f"  ... run again: {adt * 1e3:.1f} ms, {len(cols) / adt:.3e} fragments/s")
         assert _by_name(again) == want and djob.stats["records"] == len(cols)
         djob.close()
+    gc.unfreeze()
 
 
 def test_stored_span_job_on_the_device_decoder(gpu):

@@ -37,6 +37,24 @@ def main():
             print(f"run_device(indexer={indexer}): {len(cols)} fragments, {len(dev)} batches: "
                   f"{(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
 
+    # with an Aggregates store (as tests/test_gpu_jobs.py): the run, then the store call alone
+    from zipkin_amd.aggregates import GpuAggregates
+
+    for indexer in (False, True):
+        store = GpuAggregates("cassandra")
+        j2 = StoredSpanJob(aggregates=store, top_k=5, clock=lambda: 10**15, max_services=S)
+        j2.run_device(dev[:1], indexer=indexer)
+        t0 = time.perf_counter()
+        deps = j2.run_device(dev, indexer=indexer)
+        t1 = time.perf_counter()
+        store.storeDependencies(deps)
+        t2 = time.perf_counter()
+        n_links = len(deps.links)
+        t3 = time.perf_counter()
+        print(f"run_device(indexer={indexer}) with a store: {(t1 - t0) * 1e3:.1f} ms; storeDependencies again "
+              f"{(t2 - t1) * 1e3:.1f} ms; len(links) {(t3 - t2) * 1e3:.1f} ms ({n_links} links)", flush=True)
+        j2.close()
+
     # the phases, by hand, on one stream (as run_device)
     stream = torch.cuda.Stream()
     t = {}
@@ -64,18 +82,38 @@ def main():
     t0 = time.perf_counter()
     ctx.finalize()
     tick("finalize", t0)
-    # the same batches again through the warm decoder: per-batch decode times
-    per = []
-    for b, o, n in dev:
-        if out.capacity < n:
-            out = None
-        t0 = time.perf_counter()
-        out, _ = dec.decode_device(b, o, n, out=out)
-        torch.cuda.synchronize()
-        per.append((time.perf_counter() - t0) * 1e3)
-    per = np.array(per)
-    print(f"  warm decoder, per batch: median {np.median(per):.3f} ms, min {per.min():.3f}, max {per.max():.3f}, "
-          f"sum {per.sum():.2f} ms", flush=True)
+    # the same batches again through the warm decoder: per-batch decode times, without and with items,
+    # and the two sketches' accumulates of the items
+    from zipkin_amd.kv import KvSketch
+
+    kvs = KvSketch(S, stream=stream.cuda_stream, width=4096)
+    anns = KvSketch(S, stream=stream.cuda_stream, width=4096)
+    for items in (False, True):
+        per, sk = [], []
+        for b, o, n in dev:
+            if out.capacity < n:
+                out = None
+            t0 = time.perf_counter()
+            if items:
+                out, _, (ks, kh), (as_, ah) = dec.decode_device(b, o, n, out=out, items=True)
+            else:
+                out, _ = dec.decode_device(b, o, n, out=out)
+            torch.cuda.synchronize()
+            per.append((time.perf_counter() - t0) * 1e3)
+            if items:
+                t0 = time.perf_counter()
+                kvs.accumulate(ks, kh)
+                anns.accumulate(as_, ah)
+                torch.cuda.synchronize()
+                sk.append((time.perf_counter() - t0) * 1e3)
+        per = np.array(per)
+        print(f"  warm decoder (items={items}), per batch: median {np.median(per):.3f} ms, min {per.min():.3f}, "
+              f"max {per.max():.3f}, sum {per.sum():.2f} ms", flush=True)
+        if sk:
+            sk = np.array(sk)
+            print(f"  two sketch accumulates per batch: median {np.median(sk):.3f} ms, sum {sk.sum():.2f} ms", flush=True)
+    kvs.close()
+    anns.close()
     ctx.close()
     dec.close()
     for k, v in t.items():

@@ -831,8 +831,10 @@ class StoredSpanJob:
         from .columns import DeviceColumns
 
         self.rejected = 0
+        t0 = time.perf_counter()
         st = self._device_state(indexer)
         stream, dec, ctx, kvs, anns = st["stream"], st["dec"], st["ctx"], st["kvs"], st["anns"]
+        t1 = time.perf_counter()
         cap = self.device_accumulate_records
         filled = 0
         cols = None  # a batch larger than the gathering buffer: its own columns
@@ -880,11 +882,13 @@ class StoredSpanJob:
                     if len(as_):
                         anns.accumulate(as_, ah)
             flush()
+            t2 = time.perf_counter()
             names = dec.service_names()
             deps = self._finish(ctx, names)
             if indexer:
                 self.top_kv = self._tops(dec, kvs, len(names))
                 self.top_annotations = self._tops(dec, anns, len(names))
+            t3 = time.perf_counter()
         except BaseException:
             self.close()  # a failed run leaves no half-used state behind
             raise
@@ -896,4 +900,8 @@ class StoredSpanJob:
                     self.aggregates.storeTopKeyValueAnnotations(name, keys)
                 for name, values in self.top_annotations.items():
                     self.aggregates.storeTopAnnotations(name, values)
+        # where the run's wall time went (ms): device objects ready, the batches decoded and
+        # accumulated, finalize + the record (+ the top lists), the store calls
+        self.phase_ms = {"setup": (t1 - t0) * 1e3, "batches": (t2 - t1) * 1e3, "finish": (t3 - t2) * 1e3,
+                         "store": (time.perf_counter() - t3) * 1e3}
         return deps
