@@ -14,6 +14,8 @@ if [ "${PART:-a}" = a ]; then
   rm -rf gpurun_out/pmc
   BENCH_ARGS="--pipeline 0" timeout -k 10 600 bash tools/pmc.sh FETCH_SIZE WRITE_SIZE > gpurun_out/${T}_pmc.log 2>&1 || { echo "pmc failed"; cat gpurun_out/${T}_pmc.log; exit 1; }
 else
+  timeout -k 10 500 python -u bench.py --workload ingest --ingest-items 1 > gpurun_out/${T}_ingest_items.json 2> gpurun_out/${T}_ingest_items.err || { echo "ingest items failed"; tail gpurun_out/${T}_ingest_items.err; exit 1; }
+  timeout -k 10 300 python -u tools/diag/run_device_timing.py > gpurun_out/${T}_run_device.txt 2>&1 || { echo "run_device timing failed"; exit 1; }
   for w in c3 c4 c5 ingest; do
     timeout -k 10 500 python -u bench.py --workload $w > gpurun_out/${T}_$w.json 2> gpurun_out/${T}_$w.err || { echo "$w failed"; tail gpurun_out/${T}_$w.err; exit 1; }
   done
