@@ -2598,6 +2598,10 @@ zk_status ingest_batch(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* off
     a.max_services = g->max_services;
     a.unknown = g->arena;
     a.icnt = g->counts + 16;
+    // fragments per wave of the LDS decoder: 1024 once a batch gives ~4096 waves (2 per wave slot of
+    // 256 CUs x 8), else the power of two that does, at least 128 (~2 rounds of a wave)
+    uint32_t lds_block = 128;
+    while (lds_block < kLdsBlock && (uint64_t)lds_block * 4096 < n) lds_block <<= 1;
     IngArgs ax{};  // the extra names (items only)
     if (items) {
         a.items = 1;
@@ -2605,12 +2609,7 @@ zk_status ingest_batch(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* off
         a.an_cap = want_ann ? items->ann_cap : 0;
         // staging: the direct items (as many as the caller's buffers take) and the chunks (the
         // caller's capacity in chunks plus one partly filled chunk per LDS-decoder wave)
-        uint64_t waves = 0;
-        {
-            uint32_t lb = 128;
-            while (lb < kLdsBlock && (uint64_t)lb * 4096 < n) lb <<= 1;
-            waves = (n + lb - 1) / lb;
-        }
+        const uint64_t waves = (n + lds_block - 1) / lds_block;  // the LDS decoder's workgroups (one wave each)
         const uint64_t ck_cap = (std::max(a.kv_cap, a.an_cap) + kItemChunk - 1) / kItemChunk + waves + 1;
         if (ck_cap > 0xFFFFFFF0ull) return dfail(g, ZK_ERR_INVALID_ARG, "items: item buffers too large");
         const uint64_t ck_items = ck_cap * kItemChunk;
@@ -2674,10 +2673,7 @@ zk_status ingest_batch(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* off
     a.scratch_used = used;
     if (items) bind_items(g, a, ax);  // (ax copies a: every field of a is set by now)
     // D1 + D2, D3
-    // fragments per wave: 1024 once a batch gives ~4096 waves (2 per wave slot of 256 CUs x 8), else
-    // the power of two that does, at least 128 (~2 rounds of a wave)
-    a.lds_block = 128;
-    while (a.lds_block < kLdsBlock && (uint64_t)a.lds_block * 4096 < n) a.lds_block <<= 1;
+    a.lds_block = lds_block;
     const dim3 dgrid((unsigned)((n + a.lds_block - 1) / a.lds_block));
     if (items) {
         ING_HIP(g, launch_checked("k_ing_decode_lds", k_ing_decode_lds<true>, dgrid, dim3(kLdsWG), 0, s, a));
