@@ -204,13 +204,19 @@ class DeviceSpanDecoder:
         return cols, int(nrej.value), (ks[: it.kv_n], kh[: it.kv_n]), (as_[: it.ann_n], ah[: it.ann_n])
 
     def string(self, h: int) -> str:
-        """The key / value string behind a hash an items batch has seen (zk_ingest_dev_string)."""
-        ln = C.c_uint64()
+        """The key / value string behind a hash an items batch has seen (zk_ingest_dev_string);
+        memoised (a hash keeps the string first captured for it)."""
         h = int(h) & 0xFFFFFFFFFFFFFFFF
+        memo = self.__dict__.setdefault("_strings", {})
+        if h in memo:
+            return memo[h]
+        ln = C.c_uint64()
         self._check(self._L.zk_ingest_dev_string(self._h, h, None, 0, C.byref(ln)))
         buf = C.create_string_buffer(max(1, ln.value))
         self._check(self._L.zk_ingest_dev_string(self._h, h, buf, ln.value, C.byref(ln)))
-        return buf.raw[: ln.value].decode("utf-8", "surrogateescape")
+        v = buf.raw[: ln.value].decode("utf-8", "surrogateescape")
+        memo[h] = v
+        return v
 
     def decode(self, blobs: Sequence[bytes], *, snappy: bool = True, strict: bool = True, items: bool = False):
         import torch
@@ -231,11 +237,17 @@ class DeviceSpanDecoder:
         return int(n.value)
 
     def service_name(self, i: int) -> str:
+        """Memoised: a decoder's service ids never change."""
+        memo = self.__dict__.setdefault("_names", {})
+        if i in memo:
+            return memo[i]
         ln = C.c_uint64()
         self._check(self._L.zk_ingest_dev_service_name(self._h, i, None, 0, C.byref(ln)))
         buf = C.create_string_buffer(max(1, ln.value))
         self._check(self._L.zk_ingest_dev_service_name(self._h, i, buf, ln.value, C.byref(ln)))
-        return buf.raw[: ln.value].decode("utf-8", "surrogateescape")
+        v = buf.raw[: ln.value].decode("utf-8", "surrogateescape")
+        memo[i] = v
+        return v
 
     def service_names(self) -> List[str]:
         return [self.service_name(i) for i in range(self.num_services)]
