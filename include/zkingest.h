@@ -118,6 +118,16 @@ zk_status   zk_ingest_dev_spans(zk_ingest_dev* ing, const uint8_t* buf, const ui
 zk_status   zk_ingest_dev_spans_items(zk_ingest_dev* ing, const uint8_t* buf, const uint64_t* offsets, uint64_t n,
                                       uint32_t codec, uint32_t flags, const zk_span_cols* out, uint64_t* n_out,
                                       uint64_t* n_rejected, zk_ingest_items* items);
+/* Several stored batches in one decode: batch b is bufs[b] + offsets[b][0..ns[b]] (device pointers;
+ * host arrays of nb entries; ns[b] == 0 allowed). Records, rejected count and items (items may be
+ * NULL: none) are those of zk_ingest_dev_spans(_items) over the batches joined in order; fragment
+ * numbers in errors count across the batches. One set of launches and one host round trip for all
+ * of them: a job reading many small stored batches (StorageRecordReader.scala:49-54, one row batch
+ * per read) decodes them at the large-batch rate. */
+zk_status   zk_ingest_dev_spans_multi(zk_ingest_dev* ing, uint32_t nb, const uint8_t* const* bufs,
+                                      const uint64_t* const* offsets, const uint64_t* ns, uint32_t codec,
+                                      uint32_t flags, const zk_span_cols* out, uint64_t* n_out,
+                                      uint64_t* n_rejected, zk_ingest_items* items);
 /* the string behind a key / value hash an items batch of this decoder has seen (two-phase) */
 zk_status   zk_ingest_dev_string(const zk_ingest_dev* ing, uint64_t hash, char* buf, uint64_t cap, uint64_t* len);
 zk_status   zk_ingest_dev_num_services(const zk_ingest_dev* ing, uint32_t* n);

@@ -340,6 +340,8 @@ _SIGNATURES = [
     ("zk_ingest_dev_spans", C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, C.c_uint32, _P, _U64P, _U64P]),
     ("zk_ingest_dev_spans_items", C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, C.c_uint32, _P, _U64P, _U64P,
                                             C.POINTER(zk_ingest_items)]),
+    ("zk_ingest_dev_spans_multi", C.c_int, [_P, C.c_uint32, _P, _P, _P, C.c_uint32, C.c_uint32, _P, _U64P, _U64P,
+                                            C.POINTER(zk_ingest_items)]),
     ("zk_ingest_dev_string", C.c_int, [_P, C.c_uint64, C.c_char_p, C.c_uint64, _U64P]),
     ("zk_ingest_dev_num_services", C.c_int, [_P, C.POINTER(C.c_uint32)]),
     ("zk_ingest_dev_set_scratch", C.c_int, [_P, C.c_uint64]),

@@ -713,7 +713,7 @@ class StoredSpanJob:
         cap = max(16, 8 * n)
         while True:
             try:
-                return dec.decode(blobs, snappy=self.snappy, strict=self.strict, items=True, item_cap=cap)
+                return dec.decode(blobs, snappy=self.snappy, strict=self.strict, items=True, item_cap=cap), n
             except _abi.ZkError as e:
                 if e.status != _abi.ZK_ERR_CAPACITY:
                     raise
@@ -750,17 +750,33 @@ class StoredSpanJob:
             it = iter(batches)
             nxt = next(it, None)
             fut = pool.submit(self._decode, dec, nxt) if nxt is not None else None
+            cap = self.device_accumulate_records
+            pend, gn = [], 0  # the items of a group of batches (run_device's decode groups)
+
+            def items_in():
+                nonlocal pend, gn
+                for k, sk in ((0, kvs), (2, anns)):
+                    svc = np.concatenate([p[k] for p in pend]) if pend else np.zeros(0, np.uint32)
+                    if len(svc):
+                        sk.accumulate(svc, np.concatenate([p[k + 1] for p in pend]))
+                pend, gn = [], 0
+
             while fut is not None:
-                cols, rej, (ks, kh), (as_, ah) = fut.result()
+                (cols, rej, (ks, kh), (as_, ah)), n = fut.result()  # n: the batch's fragments
                 nxt = next(it, None)
                 # the decoder's C call releases the GIL: batch k+1 decodes while batch k is staged and runs
                 fut = pool.submit(self._decode, dec, nxt) if nxt is not None else None
                 self.rejected += rej
                 ctx.accumulate(cols, clustered=True, continues=True, verify=self.verify)
-                if len(ks):
-                    kvs.accumulate(ks, kh)
-                if len(as_):
-                    anns.accumulate(as_, ah)
+                # the sketches take consecutive batches of up to `cap` fragments together, as
+                # run_device's decode groups do, so both drivers store the same top lists
+                if gn + n > cap or n > cap:
+                    items_in()
+                pend.append((ks, kh, as_, ah))
+                gn += n
+                if n > cap:
+                    items_in()
+            items_in()
             names = dec.service_names()
             deps = self._finish(ctx, names)
             self.top_kv = self._tops(dec, kvs, len(names))
@@ -774,11 +790,12 @@ class StoredSpanJob:
                 self.aggregates.storeTopAnnotations(name, values)
         return deps
 
-    # run_device: decoded batches are gathered in one column buffer of this many records and
-    # accumulated together (row-order batches back to back are one row-order batch, and the
-    # dependency sums do not depend on where batches are cut), so a stream of small batches pays the
-    # accumulate's fixed cost once per buffer instead of once per batch
-    device_accumulate_records = 1 << 22
+    # run_device: consecutive batches are decoded together (one zk_ingest_dev_spans_multi call per
+    # group of up to this many fragments) into one column buffer and accumulated together
+    # (row-order batches back to back are one row-order batch, and the dependency sums do not depend
+    # on where batches are cut), so a stream of small batches pays the decoder's and the
+    # accumulate's fixed costs once per buffer instead of once per batch
+    device_accumulate_records = 1 << 23
 
     def _device_state(self, indexer: bool):
         """The device objects of run_device, kept between runs (a scheduled job reuses its buffers,
@@ -838,6 +855,7 @@ class StoredSpanJob:
         cap = self.device_accumulate_records
         filled = 0
         cols = None  # a batch larger than the gathering buffer: its own columns
+        group, gn = [], 0  # consecutive batches decoded together (one decode call)
 
         def flush():
             nonlocal filled
@@ -845,42 +863,62 @@ class StoredSpanJob:
                 ctx.accumulate(st["pool"].slice(0, filled), clustered=True, continues=True, verify=self.verify)
                 filled = 0
 
+        def items_in(ks, kh, as_, ah):
+            if len(ks):
+                kvs.accumulate(ks, kh)
+            if len(as_):
+                anns.accumulate(as_, ah)
+
+        def decode_group():
+            # the group's batches joined in one decode (zk_ingest_dev_spans_multi) straight into the
+            # gathering buffer: one set of launches and one host round trip for all of them
+            nonlocal filled, group, gn
+            if not group:
+                return
+            if st["pool"] is None:
+                st["pool"] = DeviceColumns(cap, device=f"cuda:{self.device}")
+            if filled + gn > cap:
+                flush()
+            out = st["pool"].slice(filled, filled + gn)
+            # the caller's tensors may still be in flight on its current stream (a non_blocking copy,
+            # a kernel that writes them; a lazy iterator makes each batch just before it is read):
+            # the job's stream waits for everything queued there
+            stream.wait_stream(torch.cuda.current_stream(self.device))
+            if indexer:
+                out, rej, (ks, kh), (as_, ah) = dec.decode_device_many(
+                    group, snappy=self.snappy, strict=self.strict, out=out, items=True)
+                items_in(ks, kh, as_, ah)
+            else:
+                out, rej = dec.decode_device_many(group, snappy=self.snappy, strict=self.strict, out=out)
+            self.rejected += rej
+            filled += out.n
+            group, gn = [], 0
+
         try:
             for buf, off, n in batches:
-                # the caller's tensors may still be in flight on its current stream (a non_blocking
-                # copy, a kernel that writes them; a lazy iterator makes each batch just before it is
-                # read): the job's stream waits for everything queued there, and the caller's
-                # allocator keeps the batch's memory until the job's stream is done
-                stream.wait_stream(torch.cuda.current_stream(self.device))
+                # the caller's allocator keeps the batch's memory until the job's stream is done
                 buf.record_stream(stream)
                 off.record_stream(stream)
                 if n <= cap:
-                    if st["pool"] is None:
-                        st["pool"] = DeviceColumns(cap, device=f"cuda:{self.device}")
-                    if filled + n > cap:
-                        flush()
-                    out = st["pool"].slice(filled, filled + n)
-                else:
-                    flush()
-                    if cols is None or cols.capacity < n:
-                        cols = None
-                    out = cols
+                    if gn + n > cap:
+                        decode_group()
+                    group.append((buf, off, n))
+                    gn += n
+                    continue
+                decode_group()
+                flush()
+                stream.wait_stream(torch.cuda.current_stream(self.device))
+                if cols is None or cols.capacity < n:
+                    cols = None
                 if indexer:
-                    out, rej, (ks, kh), (as_, ah) = dec.decode_device(
-                        buf, off, n, snappy=self.snappy, strict=self.strict, out=out, items=True)
+                    cols, rej, (ks, kh), (as_, ah) = dec.decode_device(
+                        buf, off, n, snappy=self.snappy, strict=self.strict, out=cols, items=True)
+                    items_in(ks, kh, as_, ah)
                 else:
-                    out, rej = dec.decode_device(buf, off, n, snappy=self.snappy, strict=self.strict, out=out)
+                    cols, rej = dec.decode_device(buf, off, n, snappy=self.snappy, strict=self.strict, out=cols)
                 self.rejected += rej
-                if n <= cap:
-                    filled += out.n
-                else:
-                    cols = out
-                    ctx.accumulate(cols, clustered=True, continues=True, verify=self.verify)
-                if indexer:
-                    if len(ks):
-                        kvs.accumulate(ks, kh)
-                    if len(as_):
-                        anns.accumulate(as_, ah)
+                ctx.accumulate(cols, clustered=True, continues=True, verify=self.verify)
+            decode_group()
             flush()
             t2 = time.perf_counter()
             names = dec.service_names()

@@ -411,7 +411,8 @@ __device__ __forceinline__ bool snappy_block(const uint8_t* in, uint64_t n, uint
 
 struct IngArgs {
     const uint8_t* buf;
-    const uint64_t* offsets;
+    const uint64_t* offsets;  // fragment i: buf[offsets[i], ends[i])
+    const uint64_t* ends;     // offsets + 1 for one batch; a separate array for several (ingest_multi)
     uint64_t n;
     uint32_t snappy;
     uint8_t* scratch;                   // Snappy: deferred fragments' Spans and copied-out names
@@ -1523,7 +1524,7 @@ __device__ __forceinline__ void ing_decode_one(const IngArgs& a, uint64_t i, uin
     a.status[i] = kStOk;
     a.keep[i] = 0u;
     a.svc_hash[i] = 0ull;
-    const uint64_t b = a.offsets[i], e = a.offsets[i + 1];
+    const uint64_t b = a.offsets[i], e = a.ends[i];
     const uint8_t* src = a.buf + b;
     uint64_t len = e - b;
     if (a.snappy) {
@@ -1865,7 +1866,7 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
     // a round's fragment extents and Snappy headers are loaded during the round before (the first
     // round's here), so no round starts with a dependent global round trip
     bool nh = blk0 + lane < blk1;
-    uint64_t nb = nh ? a.offsets[blk0 + lane] : 0, ne = nh ? a.offsets[blk0 + lane + 1] : 0;
+    uint64_t nb = nh ? a.offsets[blk0 + lane] : 0, ne = nh ? a.ends[blk0 + lane] : 0;
     uint32_t hb[5];
     head_bytes(a, nh, nb, ne, hb);
     ing_u32x4 pre[kPreBlk];
@@ -1924,7 +1925,7 @@ __global__ __launch_bounds__(kLdsWG) void k_ing_decode_lds(IngArgs a) {
         // the next round's extents (its copy-in below waits for them in passing: loads return in order)
         nh = f0 + k + lane < blk1;
         nb = nh ? a.offsets[f0 + k + lane] : 0;
-        ne = nh ? a.offsets[f0 + k + lane + 1] : 0;
+        ne = nh ? a.ends[f0 + k + lane] : 0;
         const bool go = lane < k && have && st == kStOk && fits;
         uint32_t D = 0, mis = 0;
         uint8_t* reg = s_buf + R0;
@@ -2168,6 +2169,33 @@ __global__ void k_ing_gather_names(const uint64_t* __restrict__ src, const uint6
     for (uint32_t q = 0; q < len[k]; ++q) y[q] = x[q];
 }
 
+// Several stored batches as one (zk_ingest_dev_spans_multi): fragment i of the joined batch is
+// fragment i - first[b] of batch b, where first[b] <= i < first[b + 1]; its extents relative to the
+// lowest batch buffer (rel[b] = bufs[b] - base) go to starts / ends, so the decoder reads
+// base + [starts[i], ends[i]) exactly as one batch's buf + [offsets[i], offsets[i + 1]).
+struct IngMultiBatch {
+    uint64_t rel;
+    const uint64_t* offsets;
+    uint64_t first;
+};
+__global__ void k_ing_multi_bounds(const IngMultiBatch* __restrict__ tab, uint32_t nb, uint64_t n,
+                                   uint64_t* __restrict__ starts, uint64_t* __restrict__ ends) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t lo = 0, hi = nb;  // the last batch with first <= i (empty batches share a first)
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (tab[mid].first <= i)
+            lo = mid;
+        else
+            hi = mid;
+    }
+    const IngMultiBatch t = tab[lo];
+    const uint64_t j = i - t.first;
+    starts[i] = t.rel + t.offsets[j];
+    ends[i] = t.rel + t.offsets[j + 1];
+}
+
 __global__ void k_ing_count(const uint8_t* status, uint64_t n, unsigned long long* counts, unsigned int* first_bad) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -2302,6 +2330,8 @@ struct zk_ingest_dev {
     uint64_t x_cap = 0;
     uint8_t* istage = nullptr;  // item staging: the global decoder's direct items, the LDS decoder's chunks
     uint64_t istage_cap = 0;
+    uint8_t* multi = nullptr;   // zk_ingest_dev_spans_multi: the batch table, then starts / ends [n]
+    uint64_t multi_cap = 0;
     std::string err;
 };
 
@@ -2396,6 +2426,7 @@ zk_status zk_ingest_dev_destroy(zk_ingest_dev* g) {
     hipFree(g->ns);
     hipFree(g->xs);
     hipFree(g->istage);
+    hipFree(g->multi);
     if (g->own_stream && g->stream) hipStreamDestroy(g->stream);
     delete g;
     return ZK_OK;
@@ -2527,7 +2558,7 @@ void bind_items(zk_ingest_dev* g, IngArgs& a, IngArgs& x) {
 
 zk_status ingest_batch(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* offsets, uint64_t n, uint32_t codec,
                        uint32_t flags, const zk_span_cols* out, uint64_t* n_out, uint64_t* n_rejected,
-                       zk_ingest_items* items) {
+                       zk_ingest_items* items, const uint64_t* ends = nullptr) {
     if (!g || !n_out || !n_rejected) return ZK_ERR_INVALID_ARG;
     *n_out = *n_rejected = 0;
     if (items) items->kv_n = items->ann_n = 0;
@@ -2559,6 +2590,7 @@ zk_status ingest_batch(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* off
     IngArgs a{};
     a.buf = buf;
     a.offsets = offsets;
+    a.ends = ends ? ends : offsets + 1;
     a.n = n;
     a.snappy = codec == ZK_CODEC_SNAPPY_THRIFT;
     // records are written straight into the caller's columns at their fragment index; when some
@@ -2945,9 +2977,72 @@ zk_status ingest_batch(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* off
     return ZK_OK;
 }
 
+// zk_ingest_dev_spans_multi: the batches' extents joined into starts / ends (one small kernel), then
+// one decode over all of them
+zk_status ingest_multi(zk_ingest_dev* g, uint32_t nb, const uint8_t* const* bufs, const uint64_t* const* offsets,
+                       const uint64_t* ns, uint32_t codec, uint32_t flags, const zk_span_cols* out, uint64_t* n_out,
+                       uint64_t* n_rejected, zk_ingest_items* items) {
+    if (!g || !n_out || !n_rejected) return ZK_ERR_INVALID_ARG;
+    *n_out = *n_rejected = 0;
+    if (items) items->kv_n = items->ann_n = 0;
+    if (nb && (!bufs || !offsets || !ns)) return dfail(g, ZK_ERR_INVALID_ARG, "null batch arrays");
+    uint64_t n = 0;
+    uintptr_t base = UINTPTR_MAX;
+    uint32_t only = nb;  // the one non-empty batch, if there is exactly one
+    for (uint32_t b = 0; b < nb; ++b) {
+        if (!ns[b]) continue;
+        if (!bufs[b] || !offsets[b]) return dfail(g, ZK_ERR_INVALID_ARG, "batch " + std::to_string(b) + ": null buffer");
+        if (ns[b] >= 0x7FFFFFFFull - n) return dfail(g, ZK_ERR_INVALID_ARG, "batches of 2^31 fragments or more");
+        n += ns[b];
+        base = std::min(base, (uintptr_t)bufs[b]);
+        only = only == nb ? b : nb + 1;
+    }
+    if (n == 0) return ZK_OK;
+    if (only < nb)  // one batch: its own extents
+        return ingest_batch(g, bufs[only], offsets[only], ns[only], codec, flags, out, n_out, n_rejected, items);
+    ING_HIP(g, hipSetDevice(g->device));
+    const uint64_t tab_bytes = align256((uint64_t)nb * sizeof(IngMultiBatch));
+    const uint64_t need = tab_bytes + 2 * align256(8 * n);
+    if (need > g->multi_cap) {
+        ING_HIP(g, hipStreamSynchronize(g->stream));  // (a previous call's decode may still read it)
+        hipFree(g->multi);
+        g->multi = nullptr;
+        g->multi_cap = 0;
+        ING_HIP(g, hipMalloc(&g->multi, need));
+        g->multi_cap = need;
+    }
+    std::vector<IngMultiBatch> tab(nb);
+    uint64_t first = 0;
+    for (uint32_t b = 0; b < nb; ++b) {
+        tab[b].rel = ns[b] ? (uint64_t)((uintptr_t)bufs[b] - base) : 0;
+        tab[b].offsets = offsets[b];
+        tab[b].first = first;
+        first += ns[b];
+    }
+    IngMultiBatch* dtab = (IngMultiBatch*)g->multi;
+    uint64_t* starts = (uint64_t*)(g->multi + tab_bytes);
+    uint64_t* ends = (uint64_t*)(g->multi + tab_bytes + align256(8 * n));
+    // the table from pageable memory; the decode below synchronises before this call returns
+    ING_HIP(g, hipMemcpyAsync(dtab, tab.data(), (uint64_t)nb * sizeof(IngMultiBatch), hipMemcpyHostToDevice, g->stream));
+    ING_HIP(g, launch_checked("k_ing_multi_bounds", k_ing_multi_bounds, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                              g->stream, (const IngMultiBatch*)dtab, nb, n, starts, ends));
+    const zk_status st = ingest_batch(g, (const uint8_t*)base, starts, n, codec, flags, out, n_out, n_rejected, items, ends);
+    if (st != ZK_OK) hipStreamSynchronize(g->stream);  // (an early error return: the table copy is done)
+    return st;
+}
+
 }  // namespace
 
 extern "C" {
+
+zk_status zk_ingest_dev_spans_multi(zk_ingest_dev* g, uint32_t nb, const uint8_t* const* bufs,
+                                    const uint64_t* const* offsets, const uint64_t* ns, uint32_t codec, uint32_t flags,
+                                    const zk_span_cols* out, uint64_t* n_out, uint64_t* n_rejected,
+                                    zk_ingest_items* items) {
+    ZK_GUARD_BEGIN
+    return ingest_multi(g, nb, bufs, offsets, ns, codec, flags, out, n_out, n_rejected, items);
+    ZK_GUARD_END
+}
 
 zk_status zk_ingest_dev_spans(zk_ingest_dev* g, const uint8_t* buf, const uint64_t* offsets, uint64_t n,
                               uint32_t codec, uint32_t flags, const zk_span_cols* out, uint64_t* n_out,

@@ -171,6 +171,36 @@ class DeviceSpanDecoder:
         device tensors (int32 service ids of this decoder, int64 hashes = uint64 bit patterns), in no
         particular order within the batch (zk_ingest_dev_spans_items). item_cap: the items per kind
         to allow for (default 2n + 16; a batch with more is decoded again with 4x the room)."""
+        L, h = self._L, self._h
+        bp, op = buf.data_ptr(), offsets.data_ptr()
+
+        def call(codec, flags, ab, nout, nrej, it):
+            if it is None:
+                return L.zk_ingest_dev_spans(h, bp, op, n, codec, flags, C.byref(ab), C.byref(nout), C.byref(nrej))
+            return L.zk_ingest_dev_spans_items(h, bp, op, n, codec, flags, C.byref(ab), C.byref(nout), C.byref(nrej),
+                                               C.byref(it))
+
+        return self._run(call, n, snappy, strict, out, items, item_cap)
+
+    def decode_device_many(self, batches, *, snappy: bool = True, strict: bool = True, out=None,
+                           items: bool = False, item_cap: int | None = None):
+        """Several HBM-resident batches [(buf, offsets, n), ...] in ONE decode
+        (zk_ingest_dev_spans_multi): the results of decode_device over the batches joined in order,
+        for one set of launches and one host round trip."""
+        L, h = self._L, self._h
+        nb = len(batches)
+        n = sum(int(b[2]) for b in batches)
+        bufs = (C.c_void_p * max(1, nb))(*[b[0].data_ptr() if int(b[2]) else None for b in batches])
+        offs = (C.c_void_p * max(1, nb))(*[b[1].data_ptr() if int(b[2]) else None for b in batches])
+        ns = (C.c_uint64 * max(1, nb))(*[int(b[2]) for b in batches])
+
+        def call(codec, flags, ab, nout, nrej, it):
+            return L.zk_ingest_dev_spans_multi(h, nb, bufs, offs, ns, codec, flags, C.byref(ab), C.byref(nout),
+                                               C.byref(nrej), None if it is None else C.byref(it))
+
+        return self._run(call, n, snappy, strict, out, items, item_cap)
+
+    def _run(self, call, n, snappy, strict, out, items, item_cap):
         import torch
 
         from .columns import DeviceColumns
@@ -182,8 +212,7 @@ class DeviceSpanDecoder:
         codec = _abi.ZK_CODEC_SNAPPY_THRIFT if snappy else _abi.ZK_CODEC_THRIFT
         flags = _abi.ZK_INGEST_STRICT if strict else 0
         if not items:
-            self._check(self._L.zk_ingest_dev_spans(self._h, buf.data_ptr(), offsets.data_ptr(), n, codec, flags,
-                                                    C.byref(ab), C.byref(nout), C.byref(nrej)))
+            self._check(call(codec, flags, ab, nout, nrej, None))
             cols.n = int(nout.value)
             return cols, int(nrej.value)
         cap = item_cap if item_cap is not None else 2 * n + 16
@@ -193,8 +222,7 @@ class DeviceSpanDecoder:
             as_ = torch.empty(cap, dtype=torch.int32, device=dev)
             ah = torch.empty(cap, dtype=torch.int64, device=dev)
             it = _abi.zk_ingest_items(ks.data_ptr(), kh.data_ptr(), cap, 0, as_.data_ptr(), ah.data_ptr(), cap, 0)
-            st = self._L.zk_ingest_dev_spans_items(self._h, buf.data_ptr(), offsets.data_ptr(), n, codec, flags,
-                                                   C.byref(ab), C.byref(nout), C.byref(nrej), C.byref(it))
+            st = call(codec, flags, ab, nout, nrej, it)
             if st == _abi.ZK_ERR_CAPACITY and (it.kv_n == cap or it.ann_n == cap):
                 cap *= 4  # more items than guessed: the batch again
                 continue
