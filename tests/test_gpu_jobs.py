@@ -76,8 +76,11 @@ def test_stored_span_job_streams_ten_million_fragments(gpu):
         ddeps = djob.run_device(dev, indexer=indexer)
         ddt = time.perf_counter() - t0
         what = "decode with indexer items + accumulate + 2 sketches" if indexer else "decode + accumulate"
+        job_ms = sum(v for k, v in djob.phase_ms.items() if k != "store")
         print(f"StoredSpanJob.run_device(indexer={indexer}): the same {len(cols)} fragments in HBM, {len(dev)} "
-              f"batches: {ddt * 1e3:.1f} ms, {len(cols) / ddt:.3e} fragments/s ({what} + finalize)")
+              f"batches: {ddt * 1e3:.1f} ms, {len(cols) / ddt:.3e} fragments/s ({what} + finalize + the "
+              f"Aggregates store's puts); the job without the store's puts: {job_ms:.1f} ms, "
+              f"{len(cols) / (job_ms * 1e-3):.3e} fragments/s")
         assert djob.rejected == 0 and djob.stats["records"] == len(cols)
         assert _by_name(ddeps) == want
         if indexer:  # the device decoder's items give run()'s top lists, stored the same way

@@ -450,9 +450,12 @@ class GpuAggregates(Aggregates):
         if isinstance(links, LinkList):  # a job's compact record: remap its ids to this store's names
             raw, names = links.compact()
             remap = np.array([self.services.id(x) for x in names] or [0], np.uint32)
-            arr = raw.copy()
-            arr["parent"] = remap[raw["parent"]]
-            arr["child"] = remap[raw["child"]]
+            if np.array_equal(remap, np.arange(len(remap), dtype=np.uint32)):
+                arr = raw  # the same ids (a store fed by one job): no remapped copy
+            else:
+                arr = raw.copy()
+                arr["parent"] = remap[raw["parent"]]
+                arr["child"] = remap[raw["child"]]
             self._check(self._L.zk_store_put_dependencies(self._h, int(dependencies.start_time),
                                                           int(dependencies.end_time), arr.ctypes.data, n))
             return
@@ -721,8 +724,8 @@ class StoredSpanJob:
 
     def _tops(self, dec, sketch, S) -> Dict[str, List[str]]:
         keys, _, cnt = sketch.topk_all(self.top_k)
-        return {dec.service_name(s_): [dec.string(int(h)) for h in keys[s_][: cnt[s_]]]
-                for s_ in range(S) if cnt[s_]}
+        kl, cl = keys[:S].tolist(), cnt[:S].tolist()  # Python ints: no numpy scalar per lookup
+        return {dec.service_name(s_): [dec.string(h) for h in kl[s_][: cl[s_]]] for s_ in range(S) if cl[s_]}
 
     def _finish(self, ctx, names: List[str]) -> Optional[Dependencies]:
         if len(names) > self.max_services:
@@ -795,7 +798,7 @@ class StoredSpanJob:
     # (row-order batches back to back are one row-order batch, and the dependency sums do not depend
     # on where batches are cut), so a stream of small batches pays the decoder's and the
     # accumulate's fixed costs once per buffer instead of once per batch
-    device_accumulate_records = 1 << 23
+    device_accumulate_records = 1 << 24
 
     def _device_state(self, indexer: bool):
         """The device objects of run_device, kept between runs (a scheduled job reuses its buffers,
@@ -875,11 +878,13 @@ class StoredSpanJob:
             nonlocal filled, group, gn
             if not group:
                 return
-            if st["pool"] is None:
-                st["pool"] = DeviceColumns(cap, device=f"cuda:{self.device}")
-            if filled + gn > cap:
+            pool = st["pool"]
+            if pool is None or filled + gn > pool.capacity:
                 flush()
-            out = st["pool"].slice(filled, filled + gn)
+                if pool is None or gn > pool.capacity:  # grown on demand, up to `cap` records
+                    pool = st["pool"] = None
+                    pool = st["pool"] = DeviceColumns(min(cap, max(gn, 1 << 20)), device=f"cuda:{self.device}")
+            out = pool.slice(filled, filled + gn)
             # the caller's tensors may still be in flight on its current stream (a non_blocking copy,
             # a kernel that writes them; a lazy iterator makes each batch just before it is read):
             # the job's stream waits for everything queued there

@@ -86,7 +86,7 @@ struct TopSet {
     uint64_t sk[kSortCap];
     uint32_t se[kSortCap];
     uint32_t count, gcount;
-    uint32_t pending[2];  // survivors of the current block (candidates kernel), by block parity
+    uint32_t pending[3];  // survivors of the current block (candidates kernel), block k's in pending[k % 3]
     uint32_t has_thr, thr_est;
     uint64_t thr_key;
     uint32_t special, special_est;  // the key whose hash equals the empty sentinel
@@ -357,8 +357,8 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
     // between.
     constexpr int J = 2 * kPrefetch;
     constexpr uint64_t BS = (uint64_t)kKvWG * J;  // keys per block
-    uint32_t parity = 0;
-    if (threadIdx.x == 0) t.pending[0] = t.pending[1] = 0u;
+    uint32_t rot = 0;  // this block's survivor counter
+    if (threadIdx.x == 0) t.pending[0] = t.pending[1] = t.pending[2] = 0u;
     __syncthreads();
     auto load_block = [&](uint64_t (&kq)[J], uint64_t b) {
 #pragma unroll
@@ -430,10 +430,18 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
                 if (((slow_m >> j) & 1u) && !ts_contains(t, kq[j], kq[j] == kEmptyKey ? slot[j] : (slot[j] + 2) & (kSetCap - 1)))
                     need |= 1u << j;
         }
-        if (need) atomicAdd(&t.pending[parity], (uint32_t)__popc(need));
+        // the next block's counter, last read right after the previous block's B1 (three counters: a
+        // block without survivors skips B2, so a fast thread may add to the next block's counter
+        // before a slow one has passed this block's B1)
+        const uint32_t nxt = rot == 2u ? 0u : rot + 1u;
+        if (threadIdx.x == 0) t.pending[nxt] = 0u;
+        if (need) atomicAdd(&t.pending[rot], (uint32_t)__popc(need));
         __syncthreads();  // B1: survivors counted
-        if (threadIdx.x == 0) t.pending[parity ^ 1u] = 0u;  // the previous block's count: read by all before B1
-        const uint32_t pend = t.pending[parity];
+        const uint32_t pend = t.pending[rot];
+        rot = nxt;
+        // no survivors (most blocks once the threshold has risen): the set, its count and the threshold
+        // stay as they are, so the next block may filter at once (no B2)
+        if (pend == 0u) return;
         if (t.count + pend > kSortCap && t.count > a.cand) ts_compact(t, a.cand, a.seeds[0]);
         if (t.count + pend <= kSortCap) {
             if (need) {  // (most threads insert nothing: one branch instead of J)
@@ -450,7 +458,6 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
                 if (t.count > kSortCap - kKvWG) ts_compact(t, a.cand, a.seeds[0]);
             }
         }
-        parity ^= 1u;
     };
     // two key buffers, alternating: the next block's loads are in flight while this one is
     // estimated and inserted (each buffer is loaded and consumed in fixed places, so nothing is
