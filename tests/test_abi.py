@@ -61,6 +61,9 @@ def test_null_ctx_calls_are_errors():
     assert L.zk_deps_reset(None) == _abi.ZK_ERR_INVALID_ARG
     assert L.zk_ctx_destroy(None) == _abi.ZK_ERR_INVALID_ARG
     assert L.zk_deps_accumulate(None, None, 0) == _abi.ZK_ERR_INVALID_ARG
+    n, r = C.c_uint64(), C.c_uint64()
+    assert L.zk_ingest_dev_spans_multi(None, 0, None, None, None, 0, 0, None, C.byref(n), C.byref(r),
+                                       None) == _abi.ZK_ERR_INVALID_ARG
 
 
 def test_jni_sources_bind_only_declared_entry_points():
