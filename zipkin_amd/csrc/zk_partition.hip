@@ -244,8 +244,14 @@ __global__ __launch_bounds__(WG) void k_part_scatter_lines(const uint32_t* __res
 // drained takes chunks of the others: placement changes only speed. Same pattern as the
 // clustering pass (zk_cluster.hip k_cl_xscatter, profiles/r03/ab_cluster_writes.txt).
 constexpr uint32_t kPartParts = 8;
+#ifndef ZK_PX_U
+#define ZK_PX_U 8  // items per thread of a chunk (A/B knob)
+#endif
+#ifndef ZK_PX_PER_CU
+#define ZK_PX_PER_CU 1  // scatter workgroups per CU (A/B knob; 2 needs ZK_PX_U <= 4 for the LDS)
+#endif
 constexpr int kPxWG = 1024;  // XCD scatter workgroup (chunks of 8 items per thread), one per CU
-constexpr int kPxU = 8;
+constexpr int kPxU = ZK_PX_U;
 constexpr uint32_t kPxChunk = kPxWG * kPxU;
 
 struct PartX {
@@ -288,7 +294,7 @@ __global__ void k_part_xprep(const uint32_t* __restrict__ offs, uint32_t S, uint
 // XCD i % 8), so no chunk claim is needed, and the next chunk's services and payloads load while this
 // chunk is placed and stored: per chunk, the claim and the load round trips left the critical path
 // (only the cursor claims' round trip stays on it; 5.41 -> 5.11-5.14 ms against claimed chunks).
-__global__ __launch_bounds__(kPxWG, kPxWG / 256) void k_part_xscatter_static(PartX a) {
+__global__ __launch_bounds__(kPxWG, kPxWG / 256 * ZK_PX_PER_CU) void k_part_xscatter_static(PartX a) {
     constexpr int BPT = (kLineMaxS + kPxWG - 1) / kPxWG;  // services per thread in the scan
     __shared__ uint32_t s_cnt[kLineMaxS];  // items of the chunk per service
     __shared__ uint32_t s_off[kLineMaxS];  // exclusive offsets in the sorted chunk
@@ -482,7 +488,7 @@ hipError_t partition_impl(const PartitionPlan& p, const uint32_t* svc, const uin
         x.hash_seed = hash_seed;
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        gx = (uint32_t)(cus > 0 ? cus : 256);
+        gx = (uint32_t)(cus > 0 ? cus : 256) * ZK_PX_PER_CU;
     }
     const size_t lds = (size_t)p.S * 4;
     e = launch_checked("k_part_hist", k_part_hist, dim3(p.grid), dim3(kPartWG), lds, s, svc, n, p.per_wg, counts, p.S,
