@@ -82,6 +82,10 @@ def parse():
     ap.add_argument("--ingest-items", type=int, default=0,
                     help="ingest: 1 = decode with the span indexer's items (zk_ingest_dev_spans_items), checked "
                          "against the host decoder's items as a multiset per replica")
+    ap.add_argument("--ingest-batches", type=int, default=1,
+                    help="ingest: the step's fragments as this many separate stored batches (separate tensors), "
+                         "decoded by ONE zk_ingest_dev_spans_multi call per step; the line's detail also times "
+                         "one decode call per batch")
     ap.add_argument("--comm", default=None, choices=("zk", "torch"),
                     help="N > 1: the exchange's collective. zk (default with RCCL) = the library's own "
                          "communicator, zk_deps_allreduce / zk_rt_allreduce (include/zkcomm.h), the call the "
@@ -778,17 +782,48 @@ def bench_ingest(a):
     dec = DeviceSpanDecoder(max(4096, a.services), stream=stream.cuda_stream)
     cols = None
     items = None
+    # --ingest-batches K: the same fragments as K stored batches (views of the buffer, offsets rebased
+    # per batch), as a job reading row batches holds them
+    K = max(1, a.ingest_batches)
+    cuts = [n * k // K for k in range(K + 1)]
+    parts = [(buf[int(offs[lo]):int(offs[hi])], torch.from_numpy(offs[lo:hi + 1] - offs[lo]).to(dev), hi - lo)
+             for lo, hi in zip(cuts, cuts[1:])] if K > 1 else None
 
     def step():
         nonlocal cols, items
-        if a.ingest_items:
-            cols, rej, kv, an = dec.decode_device(buf, off, n, out=cols, items=True, item_cap=2 * n)
-            items = (kv, an)
+        if K > 1:
+            r = dec.decode_device_many(parts, out=cols, items=bool(a.ingest_items),
+                                       item_cap=2 * n if a.ingest_items else None)
+        elif a.ingest_items:
+            r = dec.decode_device(buf, off, n, out=cols, items=True, item_cap=2 * n)
         else:
-            cols, rej = dec.decode_device(buf, off, n, out=cols)
+            r = dec.decode_device(buf, off, n, out=cols)
+        cols, rej = r[0], r[1]
+        if a.ingest_items:
+            items = (r[2], r[3])
         assert rej == 0 and cols.n == n
 
     wall, ev_ms = _timed(step, a.steps, a.warmup, stream)
+    per_batch_ms = None
+    if K > 1:  # the same batches one decode call each (what the multi-batch call replaces), warm
+        from zipkin_amd.columns import DeviceColumns as _DC
+
+        pool = _DC(n, device=f"cuda:{dev.index}")
+        ts = []
+        for rep in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            at = 0
+            for pb, po, pn in parts:
+                if a.ingest_items:
+                    dec.decode_device(pb, po, pn, out=pool.slice(at, at + pn), items=True, item_cap=2 * pn)
+                else:
+                    dec.decode_device(pb, po, pn, out=pool.slice(at, at + pn))
+                at += pn
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) * 1e3)
+        per_batch_ms = sorted(ts)[1]
+        del pool
     # CPU baseline: the host decoder (zk_ingest_spans, its own pool of up to 16 threads) on the
     # ~200k-fragment set, warm: one untimed decode starts the pool and fills the dictionary, then the
     # median of 5 timed decodes
@@ -840,8 +875,9 @@ def bench_ingest(a):
         "value": value, "unit": "fragments/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": wall * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u8", "data": "synthetic (tracegen records as thrift Spans, Snappy-compressed, replicated)",
-        "config": {"workload": f"ingest: {n:.3g} fragments per step, {in_bytes / n:.1f} B each compressed",
-                   "fragments": n, "input_bytes": in_bytes},
+        "config": {"workload": f"ingest: {n:.3g} fragments per step, {in_bytes / n:.1f} B each compressed"
+                               + (f", as {K} stored batches decoded by one multi-batch call" if K > 1 else ""),
+                   "fragments": n, "input_bytes": in_bytes, "batches": K},
         "roofline": {"bound": "hbm", "kernel": "whole decode (5 kernels + 2 scans)", "achieved": achieved,
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                      "algorithmic_bytes_per_step": algo},
@@ -850,7 +886,8 @@ def bench_ingest(a):
                          "sample": f"{m} fragments through the host decoder (zk_ingest_spans, {cpu_threads} threads, "
                                    f"warm pool and dictionary), median of 5: {cpu_s * 1e3:.1f} ms"},
         "parity": parity,
-        "detail": {"event_ms_per_step": ev_ms / a.steps, "services": dec.num_services},
+        "detail": {"event_ms_per_step": ev_ms / a.steps, "services": dec.num_services,
+                   **({"one_call_per_batch_ms": per_batch_ms} if per_batch_ms is not None else {})},
     }), flush=True)
 
 
