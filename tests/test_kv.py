@@ -147,6 +147,8 @@ def _assert_same(k, o, kk):
     (1022, 200_000, 0, 2, 32),  # largest S whose line-scatter carry fits the LDS
     (1024, 200_000, 0, 2, 32),  # one past it: item-by-item scatter (the line kernel would not launch)
     (2000, 200_000, 0, 3, 256),
+    (3, 300_000, 0, 4, 256),  # the LDS path at the largest candidate list: blocks of more survivors than
+    (2, 400_000, 256, 4, 200),  # the sort buffer takes are inserted in steps with compactions between
 ])
 def test_gpu_topk_bit_exact_vs_oracle(gpu, S, n, width, depth, cand):
     k, o = _pair(S, width=width, depth=depth, candidates=cand, seed=11)

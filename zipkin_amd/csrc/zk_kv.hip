@@ -23,13 +23,28 @@ namespace zk {
 namespace {
 
 constexpr int kKvWG = 512;  // (256: candidates 1.55 -> 1.41 ms with 512 on C4)
-constexpr uint32_t kSetCap = 2048;  // 2^11: RowHash.set is 11 bits  // LDS hash-set slots (load <= 0.5)
-constexpr uint32_t kSortCap = 1024; // compaction sort buffer
-constexpr uint32_t kRound = 512;  // merge: entries offered between compaction checks (<= kSortCap / 2)
+#ifndef ZK_KV_SET_BITS
+#define ZK_KV_SET_BITS 10  // LDS hash-set slots = 2^bits (11: 2.34 -> 10: 2.03 ms candidates with three workgroups per CU)
+#endif
+constexpr uint32_t kSetBits = ZK_KV_SET_BITS;
+constexpr uint32_t kSetCap = 1u << kSetBits;  // LDS hash-set slots (load <= 0.5); RowHash.set: the top kSetBits bits
+constexpr uint32_t kSortCap = kSetCap / 2;    // compaction sort buffer
+constexpr uint32_t kRound = kSortCap / 2;     // merge: entries offered between compaction checks (<= kSortCap / 2)
+// candidates, a block with more survivors than the sort buffer takes: inserted kInsStep threads at a
+// time, each step after a compaction down to <= kKvMaxCand entries, so the set never holds more than
+// kSortCap keys
+constexpr uint32_t kInsStep = kSortCap - kKvMaxCand < 512u ? kSortCap - kKvMaxCand : 512u;
+static_assert(kSortCap >= 2 * kKvMaxCand && kInsStep >= 64, "sort buffer too small for the candidate lists");
 // candidate rounds of keys in flight per thread (two alternating buffers of 2 x 4 keys: the next
 // block's keys load while this block is estimated and inserted, C4: 3.46 -> 3.22-3.26 ms,
 // profiles/r02/ab_kv_cand_pipe.txt)
-constexpr int kPrefetch = 4;
+#ifndef ZK_KV_PREFETCH
+#define ZK_KV_PREFETCH 2  // (4 with 128 VGPRs and two workgroups per CU before round 6)
+#endif
+#ifndef ZK_KV_CAND_WAVES
+#define ZK_KV_CAND_WAVES 6  // candidate pass: min waves per SIMD, 6 = three 512-thread workgroups per CU (<= 80 VGPRs)
+#endif
+constexpr int kPrefetch = ZK_KV_PREFETCH;
 constexpr uint64_t kEmptyKey = ~0ull;
 
 __device__ __forceinline__ bool beats(uint32_t e1, uint64_t k1, uint32_t e2, uint64_t k2) {
@@ -52,7 +67,7 @@ struct RowHash {
         return r;
     }
     __device__ __forceinline__ void init(uint64_t h, uint32_t wbits) {
-        set = (uint32_t)(h >> 53);  // top 11 bits (kSetCap = 2^11)
+        set = (uint32_t)(h >> (64 - kSetBits));  // top kSetBits bits
         x = (uint32_t)h;
         h2 = (uint32_t)(h >> 32) | 1u;
         sh = 32u - wbits;
@@ -146,7 +161,7 @@ __device__ __forceinline__ bool ts_contains(TopSet& t, uint64_t key, uint32_t sl
 __device__ __forceinline__ void ts_offer(TopSet& t, uint64_t key, uint64_t h, uint32_t est) {
     if (est == 0u) return;
     if (t.has_thr && !beats(est, key, t.thr_est, t.thr_key)) return;
-    ts_insert(t, h, est, (uint32_t)(h >> 53));
+    ts_insert(t, h, est, (uint32_t)(h >> (64 - kSetBits)));
 }
 
 // gather + sort (best first) into sk/se, hashes turned back into keys; returns the number of
@@ -219,7 +234,7 @@ __device__ void ts_compact(TopSet& t, uint32_t keep, uint64_t seed) {
     }
     for (uint32_t x = threadIdx.x; x < m; x += kKvWG) {
         const uint64_t h = kv_hash(t.sk[x], seed);
-        ts_insert(t, h, t.se[x], (uint32_t)(h >> 53));
+        ts_insert(t, h, t.se[x], (uint32_t)(h >> (64 - kSetBits)));
     }
     __syncthreads();
 }
@@ -335,7 +350,11 @@ __device__ void load_cm(uint32_t* cm, const KvArgs& a, uint32_t s) {
 }
 
 template <bool kSmall>
+#if ZK_KV_CAND_WAVES
+__global__ __launch_bounds__(kKvWG, ZK_KV_CAND_WAVES) void k_kv_candidates(KvArgs a) {
+#else
 __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
+#endif
     extern __shared__ uint32_t cm_lds[];
     __shared__ TopSet t;
     const uint32_t u = blockIdx.x;
@@ -453,9 +472,11 @@ __global__ __launch_bounds__(kKvWG) void k_kv_candidates(KvArgs a) {
         } else {
 #pragma unroll
             for (int j = 0; j < J; ++j) {
-                if (need & (1u << j)) ts_insert(t, kq[j], est[j], slot[j]);
-                __syncthreads();
-                if (t.count > kSortCap - kKvWG) ts_compact(t, a.cand, a.seeds[0]);
+                for (uint32_t t0 = 0; t0 < (uint32_t)kKvWG; t0 += kInsStep) {
+                    if (threadIdx.x - t0 < kInsStep && (need & (1u << j))) ts_insert(t, kq[j], est[j], slot[j]);
+                    __syncthreads();
+                    if (t.count > kSortCap - kInsStep) ts_compact(t, a.cand, a.seeds[0]);
+                }
             }
         }
     };
@@ -494,9 +515,9 @@ __global__ __launch_bounds__(kKvWG) void k_kv_merge(KvArgs a, uint32_t use_units
     const uint64_t nsrc = (uint64_t)(1 + (u1 - u0) + a.extra_lists) * C;
     for (uint64_t b = 0; b < nsrc; b += kRound) {
 #pragma unroll
-        for (int e = 0; e < (int)(kRound / kKvWG); ++e) {
+        for (int e = 0; e < (int)((kRound + kKvWG - 1) / kKvWG); ++e) {
             const uint64_t i = b + (uint64_t)e * kKvWG + threadIdx.x;
-            if (i >= nsrc) continue;
+            if (i >= nsrc || (uint64_t)e * kKvWG + threadIdx.x >= kRound) continue;
             const uint64_t list = i / C, x = i % C;
             uint64_t key;
             uint32_t old;

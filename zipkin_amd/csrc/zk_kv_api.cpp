@@ -14,6 +14,10 @@
 
 using namespace zk;
 
+#ifndef ZK_KV_UNITS_PER_CU
+#define ZK_KV_UNITS_PER_CU 2  // sketch / candidate units per CU for large batches (A/B knob)
+#endif
+
 struct zk_kv {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -240,7 +244,7 @@ zk_status zk_kv_accumulate(zk_kv* k, const uint32_t* svc, const uint64_t* keys, 
     // longer units are faster as long as they fill the chip (measured on C4: 64 Ki -> 256 Ki keys
     // per unit, candidates 2.40 -> 1.54 ms).
     {
-        const uint64_t target = 2ull * k->cus;
+        const uint64_t target = (uint64_t)ZK_KV_UNITS_PER_CU * k->cus;
         uint64_t u = (n + target - 1) / target;
         u = (u + 4095) & ~4095ull;
         a.unit_items = u > kKvUnitItems ? u : kKvUnitItems;
