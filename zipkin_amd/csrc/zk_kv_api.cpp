@@ -15,7 +15,10 @@
 using namespace zk;
 
 #ifndef ZK_KV_UNITS_PER_CU
-#define ZK_KV_UNITS_PER_CU 2  // sketch / candidate units per CU for large batches (A/B knob)
+#define ZK_KV_UNITS_PER_CU 2  // sketch units per CU for large batches (A/B knob)
+#endif
+#ifndef ZK_KV_CAND_ROUNDS
+#define ZK_KV_CAND_ROUNDS 2  // candidate-pass units: rounds over its resident workgroups (A/B knob)
 #endif
 
 struct zk_kv {
@@ -30,6 +33,7 @@ struct zk_kv {
     uint64_t sorted_cap = 0;
     uint64_t* seg = nullptr;
     uint32_t* unit_base = nullptr;
+    uint32_t* cand_base = nullptr;  // the candidate and merge passes' own unit plan
     void* part = nullptr;
     uint64_t part_bytes = 0;
     uint64_t* unit_key = nullptr;
@@ -156,6 +160,7 @@ zk_status zk_kv_create(const zk_kv_config* cfg, zk_kv** out) {
     if (e == hipSuccess) e = hipMalloc(&k->dropped, 8);
     if (e == hipSuccess) e = hipMalloc(&k->seg, (uint64_t)(S + 1) * 8);
     if (e == hipSuccess) e = hipMalloc(&k->unit_base, (uint64_t)(S + 1) * 4);
+    if (e == hipSuccess) e = hipMalloc(&k->cand_base, (uint64_t)(S + 1) * 4);
     // the pinned query mirror up front: a first query must not pay for a pinned allocation
     if (e == hipSuccess) e = hipHostMalloc((void**)&k->hq, hq_bytes(a), hipHostMallocDefault);
     zk_status st = e == hipSuccess ? zk_kv_reset(k) : ZK_ERR_HIP;
@@ -174,7 +179,7 @@ zk_status zk_kv_destroy(zk_kv* k) {
     hipSetDevice(k->device);
     if (k->stream) hipStreamSynchronize(k->stream);
     for (void* p : {(void*)k->a.cm, (void*)k->a.totals, (void*)k->a.cand_key, (void*)k->a.cand_est, (void*)k->dropped,
-                    (void*)k->sorted, (void*)k->seg, (void*)k->unit_base, k->part, (void*)k->unit_key,
+                    (void*)k->sorted, (void*)k->seg, (void*)k->unit_base, (void*)k->cand_base, k->part, (void*)k->unit_key,
                     (void*)k->unit_est, k->stage, (void*)k->qkeys, (void*)k->qest, (void*)k->g_key, (void*)k->g_est})
         if (p) hipFree(p);
     if (k->hq) hipHostFree(k->hq);
@@ -264,20 +269,37 @@ zk_status zk_kv_accumulate(zk_kv* k, const uint32_t* svc, const uint64_t* keys, 
         k->sorted_cap = n;
     }
     const uint64_t max_units = (n + a.unit_items - 1) / a.unit_items + a.S;
-    if (max_units > k->unit_cap) {
+    // The candidate pass runs ZK_KV_CAND_ROUNDS rounds of units over its resident workgroups (three per
+    // CU at 32 KB of rows: its LDS is the rows + 18.5 KB), in units of their own (a service cut into
+    // equal parts): two full rounds, where the sketch's units would leave most of a second round idle.
+    uint64_t cand_items = a.unit_items;
+    {
+        const uint64_t rows = (uint64_t)a.depth * a.width * 4;
+        uint64_t per_cu = (160ull * 1024) / (rows + 18944);
+        per_cu = per_cu < 1 ? 1 : per_cu > 3 ? 3 : per_cu;
+        const uint64_t slots = per_cu * k->cus * ZK_KV_CAND_ROUNDS;
+        uint64_t u = (n + slots - 1) / slots;
+        u += u / 16;  // slack: a service just over a multiple of u is not cut into one more part
+        u = (u + 4095) & ~4095ull;
+        cand_items = u > kKvUnitItems ? u : kKvUnitItems;
+    }
+    const uint64_t max_cand = (n + cand_items - 1) / cand_items + a.S;
+    const uint64_t max_lists = max_units > max_cand ? max_units : max_cand;
+    if (max_lists > k->unit_cap) {
         if (k->unit_key) KV_HIP(k, hipFree(k->unit_key));
         if (k->unit_est) KV_HIP(k, hipFree(k->unit_est));
         k->unit_key = nullptr;
         k->unit_est = nullptr;
-        KV_HIP(k, hipMalloc(&k->unit_key, max_units * a.cand * 8));
-        KV_HIP(k, hipMalloc(&k->unit_est, max_units * a.cand * 4));
-        k->unit_cap = (uint32_t)max_units;
+        KV_HIP(k, hipMalloc(&k->unit_key, max_lists * a.cand * 8));
+        KV_HIP(k, hipMalloc(&k->unit_est, max_lists * a.cand * 4));
+        k->unit_cap = (uint32_t)max_lists;
     }
     if (k->timing) KV_HIP(k, hipEventRecord(k->ev[0], k->stream));
     // the partition writes each key's count-min hash sk_mix64(key ^ seeds[0]), not the key itself
     KV_HIP(k, launch_partition(plan, svc, keys, n, k->sorted, k->seg, k->dropped, k->part, k->stream, true,
                                a.seeds[0]));
     KV_HIP(k, launch_unit_plan(k->seg, a.S, a.unit_items, k->unit_base, k->stream));
+    KV_HIP(k, launch_unit_plan(k->seg, a.S, cand_items, k->cand_base, k->stream));
     if (k->timing) KV_HIP(k, hipEventRecord(k->ev[1], k->stream));
     a.keys = k->sorted;
     a.seg = k->seg;
@@ -291,6 +313,8 @@ zk_status zk_kv_accumulate(zk_kv* k, const uint32_t* svc, const uint64_t* keys, 
     const bool small = n < (uint64_t)a.S * kKvSmallPerService;
     KV_HIP(k, launch_kv_sketch(a, k->stream, small));
     if (k->timing) KV_HIP(k, hipEventRecord(k->ev[2], k->stream));
+    a.unit_base = k->cand_base;  // the candidate and merge passes' units
+    a.max_units = (uint32_t)max_cand;
     KV_HIP(k, launch_kv_candidates(a, k->stream, small));
     if (k->timing) KV_HIP(k, hipEventRecord(k->ev[3], k->stream));
     KV_HIP(k, launch_kv_merge(a, k->stream, small));
