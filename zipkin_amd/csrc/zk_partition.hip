@@ -377,7 +377,9 @@ __global__ __launch_bounds__(kPxWG, kPxWG / 256 * ZK_PX_PER_CU) void k_part_xsca
             const uint32_t b = s_svc[i];
             a.out[s_cur[b] + (i - s_off[b])] = s_sorted[i];
         }
-        __syncthreads();  // s_sorted, s_svc, s_cur and s_off are read before the next chunk rewrites them
+        // No barrier here: the next chunk's first LDS writes are its rank atomics on s_cnt (zeroed
+        // before this chunk's second barrier); s_cur / s_off and s_sorted / s_svc are rewritten only
+        // after its first barrier, which every thread reaches after these reads.
     }
 }
 
